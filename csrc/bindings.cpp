@@ -1,0 +1,231 @@
+// torch op registrations for the gfx950 kernels: torch.ops.tsamd.<name>(...).
+// Every op launches on the current HIP stream (so it is capturable into a hipGraph via
+// torch.cuda.graph) and validates shapes/dtypes on the host before launch: a kernel
+// never sees operand shapes other than the ones its grid assumes.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <optional>
+
+#include "launchers.h"
+
+using at::Tensor;
+using OT = std::optional<Tensor>;
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void chk(const Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+template <typename T>
+T* P(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+template <typename T>
+T* PO(const OT& t) { return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr; }
+void numel_eq(const Tensor& t, int64_t n, const char* name) {
+  TORCH_CHECK(t.numel() == n, name, " has ", t.numel(), " elements, expected ", n);
+}
+void chko(const OT& t, at::ScalarType dt, int64_t n, const char* name) {
+  if (t.has_value() && t->defined()) { chk(*t, dt, name); numel_eq(*t, n, name); }
+}
+const auto F32 = at::kFloat;
+const auto BF = at::kBFloat16;
+const auto I32 = at::kInt;
+
+// ---------------------------------------------------------------- encoder LSTM
+void lstm_enc_fwd_step(const Tensor& gx, const Tensor& Wt, const Tensor& hs, const Tensor& cs, const Tensor& acts,
+                       const Tensor& out, const Tensor& lens, int64_t s, int64_t T, int64_t B, int64_t H) {
+  chk(gx, F32, "gx"); chk(Wt, BF, "Wt"); chk(hs, BF, "hs"); chk(cs, F32, "cs"); chk(acts, F32, "acts");
+  chk(out, BF, "out"); chk(lens, I32, "lens");
+  TORCH_CHECK(H % 32 == 0 && s >= 0 && s < T, "bad lstm args");
+  numel_eq(gx, 2 * T * B * 4 * H, "gx"); numel_eq(Wt, 2 * 4 * H * H, "Wt");
+  numel_eq(hs, 2 * (T + 1) * B * H, "hs"); numel_eq(cs, 2 * (T + 1) * B * H, "cs");
+  numel_eq(acts, 2 * T * B * 4 * H, "acts"); numel_eq(out, B * T * 2 * H, "out"); numel_eq(lens, B, "lens");
+  launch_lstm_enc_fwd_step(P<float>(gx), P<bf16>(Wt), P<bf16>(hs), P<float>(cs), P<float>(acts), P<bf16>(out),
+                           P<int>(lens), s, T, B, H, stream());
+}
+
+void lstm_enc_bwd_step(const Tensor& dz, const Tensor& Wn, const Tensor& dout, const Tensor& dh_fin,
+                       const Tensor& dc_carry, const Tensor& acts, const Tensor& cs, const Tensor& lens, int64_t s,
+                       int64_t T, int64_t B, int64_t H) {
+  chk(dz, BF, "dz"); chk(Wn, BF, "Wn"); chk(dout, F32, "dout"); chk(dh_fin, F32, "dh_fin");
+  chk(dc_carry, F32, "dc_carry"); chk(acts, F32, "acts"); chk(cs, F32, "cs"); chk(lens, I32, "lens");
+  TORCH_CHECK(H % 32 == 0 && s >= 0 && s < T, "bad lstm args");
+  numel_eq(dz, 2 * T * B * 4 * H, "dz"); numel_eq(Wn, 2 * 4 * H * H, "Wn"); numel_eq(dout, B * T * 2 * H, "dout");
+  numel_eq(dh_fin, 2 * B * H, "dh_fin"); numel_eq(dc_carry, 2 * B * H, "dc_carry");
+  numel_eq(acts, 2 * T * B * 4 * H, "acts"); numel_eq(cs, 2 * (T + 1) * B * H, "cs");
+  launch_lstm_enc_bwd_step(P<bf16>(dz), P<bf16>(Wn), P<float>(dout), P<float>(dh_fin), P<float>(dc_carry),
+                           P<float>(acts), P<float>(cs), P<int>(lens), s, T, B, H, stream());
+}
+
+// ---------------------------------------------------------------- attention
+void attn_score(const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov, const Tensor& lens,
+                const Tensor& e, int64_t B, int64_t T, int64_t A) {
+  chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens"); chk(e, F32, "e");
+  TORCH_CHECK(A % 64 == 0 && A <= 1024, "attention size must be a multiple of 64 and <= 1024");
+  numel_eq(F, B * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v"); numel_eq(e, B * T, "e");
+  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov");
+  launch_attn_score(P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens), P<float>(e), B,
+                    T, A, stream());
+}
+
+void attn_softmax_ctx(const Tensor& e, const Tensor& E, const Tensor& lens, const OT& cov, const Tensor& a_out,
+                      const OT& cov_out, const OT& covloss, const Tensor& ctx, const OT& ctx_bf, int64_t B, int64_t T,
+                      int64_t A) {
+  chk(e, F32, "e"); chk(E, BF, "E"); chk(lens, I32, "lens"); chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
+  TORCH_CHECK(A % 64 == 0 && T <= 2048, "bad attention shape");
+  numel_eq(e, B * T, "e"); numel_eq(E, B * T * A, "E"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx");
+  chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out"); chko(covloss, F32, B, "covloss");
+  chko(ctx_bf, BF, B * A, "ctx_bf");
+  launch_attn_softmax_ctx(P<float>(e), P<bf16>(E), P<int>(lens), PO<float>(cov), P<float>(a_out), PO<float>(cov_out),
+                          PO<float>(covloss), P<float>(ctx), PO<bf16>(ctx_bf), B, T, A, stream());
+}
+
+void attn_bwd_da(const Tensor& E, const Tensor& dctx, const OT& Ga, const OT& dcov_next, const Tensor& a,
+                 const OT& cov, const OT& gcl, const Tensor& lens, const Tensor& da, int64_t B, int64_t T, int64_t A) {
+  chk(E, BF, "E"); chk(dctx, F32, "dctx"); chk(a, F32, "a"); chk(lens, I32, "lens"); chk(da, F32, "da");
+  TORCH_CHECK(A % 64 == 0 && A <= 1024, "bad A");
+  numel_eq(E, B * T * A, "E"); numel_eq(dctx, B * A, "dctx"); numel_eq(a, B * T, "a"); numel_eq(da, B * T, "da");
+  chko(Ga, F32, B * T, "Ga"); chko(dcov_next, F32, B * T, "dcov_next"); chko(cov, F32, B * T, "cov");
+  chko(gcl, F32, B, "gcl");
+  launch_attn_bwd_da(P<bf16>(E), P<float>(dctx), PO<float>(Ga), PO<float>(dcov_next), P<float>(a), PO<float>(cov),
+                     PO<float>(gcl), P<int>(lens), P<float>(da), B, T, A, stream());
+}
+
+void attn_bwd_tanh(const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov, const Tensor& a,
+                   const Tensor& da, const OT& dcov_next, const OT& gcl, const Tensor& lens, const Tensor& de_out,
+                   const Tensor& dsp, const OT& dcov_out, int64_t B, int64_t T, int64_t A) {
+  chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(da, F32, "da"); chk(lens, I32, "lens");
+  chk(de_out, F32, "de_out"); chk(dsp, F32, "dsp");
+  TORCH_CHECK(A % 64 == 0 && A <= 1024, "bad A");
+  numel_eq(F, B * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(a, B * T, "a"); numel_eq(da, B * T, "da");
+  numel_eq(de_out, B * T, "de_out"); numel_eq(dsp, B * attn_nchunk(T) * A, "dsp");
+  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(dcov_next, F32, B * T, "dcov_next");
+  chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
+  launch_attn_bwd_tanh(P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a), P<float>(da),
+                       PO<float>(dcov_next), PO<float>(gcl), P<int>(lens), P<float>(de_out), P<float>(dsp),
+                       PO<float>(dcov_out), B, T, A, stream());
+}
+
+void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const OT& wc, const OT& cov_all,
+                   const Tensor& de_all, const Tensor& lens, const Tensor& dF, const Tensor& dv, const OT& dwc,
+                   int64_t D, int64_t B, int64_t T, int64_t A) {
+  chk(F, BF, "F"); chk(S_all, F32, "S_all"); chk(v, F32, "v"); chk(de_all, F32, "de_all"); chk(lens, I32, "lens");
+  chk(dF, F32, "dF"); chk(dv, F32, "dv");
+  TORCH_CHECK(A % 64 == 0, "bad A");
+  numel_eq(F, B * T * A, "F"); numel_eq(S_all, D * B * A, "S_all"); numel_eq(de_all, D * B * T, "de_all");
+  numel_eq(dF, B * T * A, "dF"); numel_eq(dv, A, "dv");
+  chko(wc, F32, A, "wc"); chko(cov_all, F32, D * B * T, "cov_all"); chko(dwc, F32, A, "dwc");
+  launch_attn_bwd_feat(P<bf16>(F), P<float>(S_all), P<float>(v), PO<float>(wc), PO<float>(cov_all), P<float>(de_all),
+                       P<int>(lens), P<float>(dF), P<float>(dv), PO<float>(dwc), D, B, T, A, stream());
+}
+
+int64_t attn_chunks(int64_t T) { return attn_nchunk(T); }
+
+// ---------------------------------------------------------------- decoder cell
+void dec_xcell_fwd(const Tensor& xe, const OT& ctxp, const Tensor& WicT, const Tensor& WcT, const Tensor& bc,
+                   const Tensor& hprev, const Tensor& cprev, const Tensor& x_out, const Tensor& xb_out,
+                   const Tensor& c_out, const Tensor& cb_out, const Tensor& hb_out, const Tensor& act, int64_t B,
+                   int64_t E, int64_t H, int64_t A) {
+  chk(xe, F32, "xe"); chk(WicT, BF, "WicT"); chk(WcT, BF, "WcT"); chk(bc, F32, "bc"); chk(hprev, BF, "hprev");
+  chk(cprev, F32, "cprev"); chk(x_out, F32, "x_out"); chk(xb_out, BF, "xb_out"); chk(c_out, F32, "c_out");
+  chk(cb_out, BF, "cb_out"); chk(hb_out, BF, "hb_out"); chk(act, F32, "act");
+  TORCH_CHECK(E % 32 == 0 && H % 32 == 0 && A % 32 == 0, "dims must be multiples of 32");
+  numel_eq(xe, B * E, "xe"); chko(ctxp, BF, B * A, "ctxp"); numel_eq(WicT, E * A, "WicT");
+  numel_eq(WcT, 4 * H * (E + H), "WcT"); numel_eq(bc, 4 * H, "bc"); numel_eq(hprev, B * H, "hprev");
+  numel_eq(cprev, B * H, "cprev"); numel_eq(x_out, B * E, "x_out"); numel_eq(c_out, B * H, "c_out");
+  numel_eq(act, B * 4 * H, "act");
+  launch_dec_xcell_fwd(P<float>(xe), PO<bf16>(ctxp), P<bf16>(WicT), P<bf16>(WcT), P<float>(bc), P<bf16>(hprev),
+                       P<float>(cprev), P<float>(x_out), P<bf16>(xb_out), P<float>(c_out), P<bf16>(cb_out),
+                       P<bf16>(hb_out), P<float>(act), B, E, H, A, stream());
+}
+
+void dec_sproj(const Tensor& cb, const Tensor& hb, const Tensor& WsT, const Tensor& bs, const Tensor& s_out, int64_t B,
+               int64_t H, int64_t A) {
+  chk(cb, BF, "cb"); chk(hb, BF, "hb"); chk(WsT, BF, "WsT"); chk(bs, F32, "bs"); chk(s_out, F32, "s_out");
+  numel_eq(cb, B * H, "cb"); numel_eq(hb, B * H, "hb"); numel_eq(WsT, A * 2 * H, "WsT"); numel_eq(bs, A, "bs");
+  numel_eq(s_out, B * A, "s_out");
+  launch_dec_sproj(P<bf16>(cb), P<bf16>(hb), P<bf16>(WsT), P<float>(bs), P<float>(s_out), B, H, A, stream());
+}
+
+void dec_bwd_cell(const Tensor& dsp, int64_t nchunk, const Tensor& Ws, const OT& dC_dir, const OT& dH_dir,
+                  const Tensor& dh_rec, const Tensor& dc_carry, const Tensor& act, const Tensor& c_now,
+                  const Tensor& c_prev, const Tensor& ds_out, const Tensor& dz, int64_t B, int64_t H, int64_t A) {
+  chk(dsp, F32, "dsp"); chk(Ws, BF, "Ws"); chk(dh_rec, F32, "dh_rec"); chk(dc_carry, F32, "dc_carry");
+  chk(act, F32, "act"); chk(c_now, F32, "c_now"); chk(c_prev, F32, "c_prev"); chk(ds_out, F32, "ds_out");
+  chk(dz, BF, "dz");
+  numel_eq(dsp, B * nchunk * A, "dsp"); numel_eq(Ws, 2 * H * A, "Ws"); chko(dC_dir, F32, B * H, "dC_dir");
+  chko(dH_dir, F32, B * H, "dH_dir"); numel_eq(dh_rec, B * H, "dh_rec"); numel_eq(dc_carry, B * H, "dc_carry");
+  numel_eq(act, B * 4 * H, "act"); numel_eq(c_now, B * H, "c_now"); numel_eq(c_prev, B * H, "c_prev");
+  numel_eq(ds_out, B * A, "ds_out"); numel_eq(dz, B * 4 * H, "dz");
+  launch_dec_bwd_cell(P<float>(dsp), nchunk, P<bf16>(Ws), PO<float>(dC_dir), PO<float>(dH_dir), P<float>(dh_rec),
+                      P<float>(dc_carry), P<float>(act), P<float>(c_now), P<float>(c_prev), P<float>(ds_out),
+                      P<bf16>(dz), B, H, A, stream());
+}
+
+void dec_bwd_dz(const Tensor& dz, const Tensor& Wc, const Tensor& Wic, const OT& dX_dir, const OT& dCTX_dir_prev,
+                const Tensor& dx_out, const OT& dctx_prev_out, const Tensor& dh_rec, int64_t B, int64_t E, int64_t H,
+                int64_t A) {
+  chk(dz, BF, "dz"); chk(Wc, BF, "Wc"); chk(Wic, BF, "Wic"); chk(dx_out, F32, "dx_out"); chk(dh_rec, F32, "dh_rec");
+  numel_eq(dz, B * 4 * H, "dz"); numel_eq(Wc, (E + H) * 4 * H, "Wc"); numel_eq(Wic, A * E, "Wic");
+  chko(dX_dir, F32, B * E, "dX_dir"); chko(dCTX_dir_prev, F32, B * A, "dCTX_dir_prev");
+  numel_eq(dx_out, B * E, "dx_out"); chko(dctx_prev_out, F32, B * A, "dctx_prev_out");
+  numel_eq(dh_rec, B * H, "dh_rec");
+  launch_dec_bwd_dz(P<bf16>(dz), P<bf16>(Wc), P<bf16>(Wic), PO<float>(dX_dir), PO<float>(dCTX_dir_prev),
+                    P<float>(dx_out), PO<float>(dctx_prev_out), P<float>(dh_rec), B, E, H, A, stream());
+}
+
+// ---------------------------------------------------------------- loss / optimizer
+void ptr_loss(const Tensor& logits, const Tensor& bias, const Tensor& target, const Tensor& rowg, const OT& pgen, const OT& attn,
+              const Tensor& ext, const Tensor& lens, const Tensor& loss_row, const OT& dlogits, const OT& dpre,
+              const OT& dA, int64_t N, int64_t B, int64_t T, int64_t V) {
+  chk(logits, F32, "logits"); chk(bias, F32, "bias"); numel_eq(bias, V, "bias"); chk(target, I32, "target"); chk(rowg, F32, "rowg"); chk(ext, I32, "ext");
+  chk(lens, I32, "lens"); chk(loss_row, F32, "loss_row");
+  numel_eq(logits, N * V, "logits"); numel_eq(target, N, "target"); numel_eq(rowg, N, "rowg");
+  numel_eq(ext, B * T, "ext"); numel_eq(lens, B, "lens"); numel_eq(loss_row, N, "loss_row");
+  TORCH_CHECK(N % B == 0, "N must be D*B");
+  chko(pgen, F32, N, "pgen"); chko(attn, F32, N * T, "attn"); chko(dlogits, BF, N * V, "dlogits");
+  chko(dpre, F32, N, "dpre"); chko(dA, F32, N * T, "dA");
+  TORCH_CHECK(!PO<float>(pgen) || (PO<float>(attn) && (!PO<bf16>(dlogits) || (PO<float>(dpre) && PO<float>(dA)))),
+              "pointer mode needs attn, and dpre/dA when computing grads");
+  launch_ptr_loss(P<float>(logits), P<float>(bias), P<int>(target), P<float>(rowg), PO<float>(pgen), PO<float>(attn), P<int>(ext),
+                  P<int>(lens), P<float>(loss_row), PO<bf16>(dlogits), PO<float>(dpre), PO<float>(dA), N, B, T, V,
+                  stream());
+}
+
+void clip_adagrad(const Tensor& w, const Tensor& acc, const Tensor& g, const Tensor& part, double lr, double max_norm,
+                  const Tensor& norm_out, const Tensor& flag) {
+  chk(w, F32, "w"); chk(acc, F32, "acc"); chk(g, F32, "g"); chk(part, F32, "part"); chk(norm_out, F32, "norm_out");
+  chk(flag, I32, "flag");
+  TORCH_CHECK(w.numel() == acc.numel() && w.numel() == g.numel(), "flat buffers differ in size");
+  numel_eq(part, opt_nparts(), "part");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(acc.data_ptr()) % 16 == 0,
+              "flat buffers must be 16-byte aligned");
+  launch_clip_adagrad(P<float>(w), P<float>(acc), P<float>(g), w.numel(), P<float>(part), (float)lr, (float)max_norm,
+                      P<float>(norm_out), P<int>(flag), stream());
+}
+int64_t opt_parts() { return opt_nparts(); }
+
+}  // namespace
+
+TORCH_LIBRARY(tsamd, m) {
+  m.def("lstm_enc_fwd_step", &lstm_enc_fwd_step);
+  m.def("lstm_enc_bwd_step", &lstm_enc_bwd_step);
+  m.def("attn_score", &attn_score);
+  m.def("attn_softmax_ctx", &attn_softmax_ctx);
+  m.def("attn_bwd_da", &attn_bwd_da);
+  m.def("attn_bwd_tanh", &attn_bwd_tanh);
+  m.def("attn_bwd_feat", &attn_bwd_feat);
+  m.def("attn_chunks", &attn_chunks);
+  m.def("dec_xcell_fwd", &dec_xcell_fwd);
+  m.def("dec_sproj", &dec_sproj);
+  m.def("dec_bwd_cell", &dec_bwd_cell);
+  m.def("dec_bwd_dz", &dec_bwd_dz);
+  m.def("ptr_loss", &ptr_loss);
+  m.def("clip_adagrad", &clip_adagrad);
+  m.def("opt_parts", &opt_parts);
+}

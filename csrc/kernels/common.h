@@ -1,0 +1,92 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave = 64 lanes; blocks are multiples of 64 threads.
+//  * GEMM-shaped work uses v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
+//    Operand maps (cdna_hip_programming.md s3): lane l holds
+//      A[row = l&15][k = 8*(l>>4) + j], B[k = 8*(l>>4) + j][col = l&15], j=0..7
+//    and the accumulator holds C[row = (l>>4)*4 + r][col = l&15], r=0..3.
+//  * Weight operands are stored "Bt" = [N][K] with K contiguous, so both A and B
+//    fragments are one 16-byte load per lane straight from L2 (M <= a few hundred,
+//    the operands are L2-resident and re-read every step of a recurrence).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define WAVE 64
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8 a, const bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (bf16)0.0f;
+  return z;
+}
+
+// Fast activations (fp32).  exp via v_exp_f32 (2^x).
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + fexp(-x)); }
+__device__ __forceinline__ float ftanh(float x) {
+  // tanh(x) = 1 - 2/(exp(2x)+1); clamp keeps exp finite, exact to fp32 rounding for |x|>=9.
+  x = fminf(fmaxf(x, -15.0f), 15.0f);
+  float e = fexp(2.0f * x);
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide reductions for blockDim.x == NT (multiple of 64); scratch >= NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += scratch[i];
+  return r;
+}
+template <int NT>
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r = fmaxf(r, scratch[i]);
+  return r;
+}
+
+// One 16x16 output tile, K loop of 32: acc += A[rows][k] * Bt[cols][k].
+// a_row / b_row already point at this lane's row (A row l&15 / Bt row l&15) and k offset 8*(l>>4).
+__device__ __forceinline__ f32x4 mfma_k(const bf16* a_row, const bf16* b_row, int K, f32x4 acc) {
+  for (int k = 0; k < K; k += 32) acc = mfma16(ld8(a_row + k), ld8(b_row + k), acc);
+  return acc;
+}
+
+#define HIP_LAUNCH_CHECK() (void)0

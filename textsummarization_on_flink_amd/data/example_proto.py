@@ -1,0 +1,160 @@
+"""Minimal ``tf.train.Example`` protobuf codec (no TensorFlow dependency).
+
+The reference moves rows as serialized ``tf.Example`` messages: the CNN/DM ``.bin``
+chunks hold ``{article, abstract}`` (``make_datafiles.py:183-189``), the Flink reader
+parses ``{uuid, article, reference}`` (``batcher.py:554-557``) and the writer emits
+``{uuid, article, summary, reference}`` (``flink_writer.py:26-33``).  This module speaks
+the same wire format so those files/records interoperate:
+
+    Example  { Features features = 1; }
+    Features { map<string, Feature> feature = 1; }
+    Feature  { oneof { BytesList bytes_list = 1; FloatList float_list = 2; Int64List int64_list = 3; } }
+
+Values are returned as python lists: bytes for bytes_list, float for float_list and
+int for int64_list (the ``DataTypes`` mapping of ``CodingUtils.java:37-61``).
+"""
+from __future__ import annotations
+
+import struct
+from typing import Dict, List, Tuple, Union
+
+Value = Union[bytes, str, int, float]
+
+
+def _varint(n: int) -> bytes:
+    if n < 0:
+        n += 1 << 64
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        if n:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _read_varint(buf: bytes, pos: int) -> Tuple[int, int]:
+    shift = 0
+    res = 0
+    while True:
+        b = buf[pos]
+        pos += 1
+        res |= (b & 0x7F) << shift
+        if not b & 0x80:
+            return res, pos
+        shift += 7
+
+
+def _ld(field: int, payload: bytes) -> bytes:
+    return _varint((field << 3) | 2) + _varint(len(payload)) + payload
+
+
+def _feature(values) -> bytes:
+    if not isinstance(values, (list, tuple)):
+        values = [values]
+    if all(isinstance(v, (bytes, str)) for v in values):
+        body = b"".join(_ld(1, v.encode("utf-8") if isinstance(v, str) else v) for v in values)
+        return _ld(1, body)
+    if all(isinstance(v, bool) or isinstance(v, int) for v in values):
+        packed = b"".join(_varint(int(v)) for v in values)
+        return _ld(3, _ld(1, packed))
+    packed = struct.pack("<%df" % len(values), *[float(v) for v in values])
+    return _ld(2, _ld(1, packed))
+
+
+def encode_example(features: Dict[str, object]) -> bytes:
+    """Serialize ``{name: value or [values]}`` as a tf.Example (keys sorted, like TF)."""
+    entries = b"".join(_ld(1, _ld(1, k.encode("utf-8")) + _ld(2, _feature(v))) for k, v in sorted(features.items()))
+    return _ld(1, entries)
+
+
+def _skip(buf, pos, wt):
+    if wt == 0:
+        _, pos = _read_varint(buf, pos)
+    elif wt == 1:
+        pos += 8
+    elif wt == 2:
+        n, pos = _read_varint(buf, pos)
+        pos += n
+    elif wt == 5:
+        pos += 4
+    else:
+        raise ValueError(f"unsupported wire type {wt}")
+    return pos
+
+
+def _fields(buf: bytes):
+    pos, end = 0, len(buf)
+    while pos < end:
+        key, pos = _read_varint(buf, pos)
+        f, wt = key >> 3, key & 7
+        if wt == 2:
+            n, pos = _read_varint(buf, pos)
+            yield f, wt, buf[pos:pos + n]
+            pos += n
+        elif wt == 0:
+            v, pos = _read_varint(buf, pos)
+            yield f, wt, v
+        else:
+            start = pos
+            pos = _skip(buf, pos, wt)
+            yield f, wt, buf[start:pos]
+
+
+def _decode_feature(buf: bytes) -> List:
+    for f, wt, payload in _fields(buf):
+        if f == 1:  # BytesList
+            return [p for ff, _, p in _fields(payload) if ff == 1]
+        if f == 2:  # FloatList
+            out = []
+            for ff, w2, p in _fields(payload):
+                if ff != 1:
+                    continue
+                if w2 == 2:
+                    out += list(struct.unpack("<%df" % (len(p) // 4), p))
+                else:
+                    out.append(struct.unpack("<f", p)[0])
+            return out
+        if f == 3:  # Int64List
+            out = []
+            for ff, w2, p in _fields(payload):
+                if ff != 1:
+                    continue
+                if w2 == 2:
+                    q = 0
+                    while q < len(p):
+                        v, q = _read_varint(p, q)
+                        out.append(v - (1 << 64) if v >= 1 << 63 else v)
+                else:
+                    out.append(p - (1 << 64) if p >= 1 << 63 else p)
+            return out
+    return []
+
+
+def decode_example(buf: bytes) -> Dict[str, List]:
+    out: Dict[str, List] = {}
+    for f, wt, features in _fields(buf):
+        if f != 1 or wt != 2:
+            continue
+        for f2, wt2, entry in _fields(features):
+            if f2 != 1 or wt2 != 2:
+                continue
+            key, val = None, b""
+            for f3, _, p in _fields(entry):
+                if f3 == 1:
+                    key = p.decode("utf-8")
+                elif f3 == 2:
+                    val = p
+            if key is not None:
+                out[key] = _decode_feature(val)
+    return out
+
+
+def get_text(ex: Dict[str, List], key: str, default: str = "") -> str:
+    v = ex.get(key)
+    if not v:
+        return default
+    x = v[0]
+    return x.decode("utf-8", errors="replace") if isinstance(x, (bytes, bytearray)) else str(x)

@@ -1,0 +1,471 @@
+"""MI355X production path of the pointer-generator network (train / eval).
+
+The step is written as an explicit forward + hand-derived backward over preallocated
+buffers (no autograd graph, no per-step allocation), so ``train_step`` is a fixed
+sequence of launches on one stream that ``torch.cuda.graph`` captures once and replays
+(hipGraph): per step ~8 kernels x D decoder steps and 2 kernels x T encoder steps, each
+paying only the ~1.5 us dependent-kernel boundary instead of ~10 us of Python dispatch.
+
+Where the work goes:
+  * recurrences (encoder bi-LSTM, decoder cell, attention) -> hand-written gfx950 kernels
+    (``csrc/kernels/{lstm,decoder,attention}.hip``), one launch per time step;
+  * vocab distribution + pointer mixture + NLL -> fused kernel (``loss.hip``) that never
+    materialises the [N, V+O] final distribution;
+  * every hoistable GEMM (input projections for all T, W_h features, p_gen / output
+    projections for all D, vocab projection, all weight gradients) -> one big bf16 GEMM
+    each (hipBLASLt through torch.mm, fp32 accumulate/output);
+  * clip + Adagrad -> fused kernel over the flat parameter buffer (``optim.hip``).
+
+Reference semantics: ``model.py:76-305``, ``attention_decoder.py:27-180``.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+
+from ..ops import ops as _ops
+from .params import DEC, P, FlatParams, enc_prefix
+
+BF = torch.bfloat16
+F32 = torch.float32
+
+EMB = f"{P}/embedding/embedding"
+RC, RH = f"{P}/reduce_final_st/w_reduce_c", f"{P}/reduce_final_st/w_reduce_h"
+BRC, BRH = f"{P}/reduce_final_st/bias_reduce_c", f"{P}/reduce_final_st/bias_reduce_h"
+WH, VATT, WCOV = f"{DEC}/W_h", f"{DEC}/v", f"{DEC}/coverage/w_c"
+LIN_M, LIN_B = f"{DEC}/Linear/Matrix", f"{DEC}/Linear/Bias"
+CELL_K, CELL_B = f"{DEC}/lstm_cell/kernel", f"{DEC}/lstm_cell/bias"
+ATT_M, ATT_B = f"{DEC}/Attention/Linear/Matrix", f"{DEC}/Attention/Linear/Bias"
+PG_M, PG_B = f"{DEC}/calculate_pgen/Linear/Matrix", f"{DEC}/calculate_pgen/Linear/Bias"
+OUT_M, OUT_B = f"{DEC}/AttnOutputProjection/Linear/Matrix", f"{DEC}/AttnOutputProjection/Linear/Bias"
+OW, OV = f"{P}/output_projection/w", f"{P}/output_projection/v"
+
+
+def enc_k(layer, d):
+    return f"{enc_prefix(layer)}/bidirectional_rnn/{d}/lstm_cell/kernel"
+
+
+def enc_b(layer, d):
+    return f"{enc_prefix(layer)}/bidirectional_rnn/{d}/lstm_cell/bias"
+
+
+def mmf(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 x bf16 -> fp32 GEMM (fp32 accumulate), hipBLASLt."""
+    return torch.mm(a, b, out_dtype=F32)
+
+
+class HipPointerGenerator:
+    """Fixed-shape (B rows, T encoder steps, D decoder steps) train/eval engine."""
+
+    def __init__(self, hps, vsize: int, params: FlatParams, B: int, T: int, D: Optional[int] = None):
+        self.hps = hps
+        self.V, self.E, self.H = vsize, hps.emb_dim, hps.hidden_dim
+        self.A = 2 * self.H
+        self.B, self.T, self.D = B, T, D or hps.max_dec_steps
+        self.L = max(1, getattr(hps, "enc_layers", 1))
+        self.p = params
+        self.dev = params.flat.device
+        if self.dev.type != "cuda":
+            raise RuntimeError("HipPointerGenerator runs on the GPU; use ReferencePointerGenerator on CPU")
+        if self.E % 32 or self.H % 32:
+            raise ValueError("emb_dim and hidden_dim must be multiples of 32 for the MFMA kernels")
+        if T > 2048:
+            raise ValueError("max_enc_steps > 2048 not supported by the attention kernels")
+        self.k = _ops()
+        self.nchunk = int(self.k.attn_chunks(T))
+        self._alloc()
+        self.pack()
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self):
+        B, T, D, E, H, A, V, L = self.B, self.T, self.D, self.E, self.H, self.A, self.V, self.L
+        z = lambda *s, dt=F32: torch.zeros(*s, dtype=dt, device=self.dev)
+        w: Dict[str, torch.Tensor] = {}
+        # inputs (static, copied into before every replay)
+        w["enc_batch"] = z(B, T, dt=torch.long)
+        w["enc_lens"] = torch.ones(B, dtype=torch.int32, device=self.dev)
+        w["rev_idx"] = z(B, T, dt=torch.long)
+        w["ext"] = z(B, T, dt=torch.int32)
+        w["dec_batch_t"] = z(D, B, dt=torch.long)
+        w["target_t"] = z(D, B, dt=torch.int32)
+        w["rowg"] = z(D, B)
+        w["gcl"] = z(D, B)
+        # encoder, per layer
+        self.enc = []
+        for layer in range(L):
+            din = E if layer == 0 else A
+            self.enc.append({
+                "din": din,
+                "x_sf": z(2, T, B, din, dt=BF),          # step-frame inputs (bw reversed)
+                "gx": z(2, T, B, 4 * H),
+                "hs": z(2, T + 1, B, H, dt=BF),
+                "cs": z(2, T + 1, B, H),
+                "acts": z(2, T, B, 4 * H),
+                "out": z(B, T, A, dt=BF),
+                "dz": z(2, T, B, 4 * H, dt=BF),
+                "dout": z(B, T, A),
+                "dh_fin": z(2, B, H),
+                "dc_carry": z(2, B, H),
+            })
+        w["F"] = z(B, T, A, dt=BF)
+        # decoder forward state
+        w["xe"] = z(D, B, E)
+        w["X"] = z(D, B, E)
+        w["Xb"] = z(D, B, E, dt=BF)
+        w["Cst"] = z(D + 1, B, H)
+        w["Cb"] = z(D + 1, B, H, dt=BF)
+        w["Hb"] = z(D + 1, B, H, dt=BF)
+        w["ACT"] = z(D, B, 4 * H)
+        w["S"] = z(D, B, A)
+        w["COV"] = z(D + 1, B, T)
+        w["ATT"] = z(D, B, T)
+        w["CTX"] = z(D, B, A)
+        w["CTXb"] = z(D, B, A, dt=BF)
+        w["e"] = z(B, T)
+        w["covloss"] = z(D, B)
+        w["outb"] = z(D * B, H, dt=BF)
+        w["pg"] = z(D, B)
+        w["loss_row"] = z(D, B)
+        w["logits"] = z(D * B, V)
+        # backward
+        w["dlogits"] = z(D * B, V, dt=BF)
+        w["dpre"] = z(D, B)
+        w["dA"] = z(D, B, T)
+        w["DCTX"] = z(D, B, A)
+        w["DX"] = z(D, B, E)
+        w["DZ"] = z(D, B, 4 * H, dt=BF)
+        w["DS"] = z(D, B, A)
+        w["DE"] = z(D, B, T)
+        w["da"] = z(B, T)
+        w["dsp"] = z(B, self.nchunk, A)
+        w["dcov"] = z(2, B, T)
+        w["dh_rec"] = z(B, H)
+        w["dc_carry"] = z(B, H)
+        w["dF"] = z(B, T, A)
+        w["dv"] = z(A)
+        w["dwc"] = z(A)
+        # optimizer
+        w["opt_part"] = z(int(self.k.opt_parts()))
+        w["gnorm"] = z(1)
+        w["nan_flag"] = z(1, dt=torch.int32)
+        self.w = w
+
+    # ------------------------------------------------------------------ weights
+    def pack(self):
+        """fp32 master -> bf16 kernel layouts (recomputed after every optimizer step)."""
+        p, E, H, A = self.p, self.E, self.H, self.A
+        pk = getattr(self, "pk", None) or {}
+
+        def put(name, t):
+            t = t.to(BF)
+            if name in pk and pk[name].shape == t.shape:
+                pk[name].copy_(t)
+            else:
+                pk[name] = t.contiguous()
+
+        put("emb", p[EMB])
+        for layer in range(self.L):
+            din = E if layer == 0 else A
+            for di, d in enumerate(("fw", "bw")):
+                K = p[enc_k(layer, d)]
+                put(f"enc{layer}_Kx{di}", K[:din])
+            Kh = torch.stack([p[enc_k(layer, d)][din:] for d in ("fw", "bw")])  # [2][H][4H]
+            put(f"enc{layer}_Wn", Kh)
+            put(f"enc{layer}_Wt", Kh.transpose(1, 2))
+        put("Wh", p[WH].reshape(A, A))
+        M = p[LIN_M]
+        put("lin_emb", M[:E])
+        put("Wic", M[E:])
+        put("WicT", M[E:].t())
+        put("Wc", p[CELL_K])
+        put("WcT", p[CELL_K].t())
+        put("Ws", p[ATT_M])
+        put("WsT", p[ATT_M].t())
+        put("OUTm", p[OUT_M])
+        put("ow", p[OW])
+        self.pk = pk
+        self.f32 = {
+            "v": p[VATT].reshape(A).contiguous(),
+            "wc": p[WCOV].reshape(A).contiguous() if self.hps.coverage else None,
+        }
+
+    # ------------------------------------------------------------------ inputs
+    def set_batch(self, batch) -> None:
+        """Host batch -> static device buffers (H2D copies; pinned staging)."""
+        import numpy as np
+        hps, w, B, T, D = self.hps, self.w, self.B, self.T, self.D
+        if batch.enc_batch.shape != (B, T):
+            raise ValueError(f"batch enc shape {batch.enc_batch.shape} != engine shape {(B, T)}")
+        lens = batch.enc_lens.astype(np.int64)
+        if lens.min() < 1:
+            raise ValueError("empty article in batch")
+        t = np.arange(T)[None, :]
+        rev = np.where(t < lens[:, None], lens[:, None] - 1 - t, t)
+        valid = batch.valid.astype(np.float64)
+        nvalid = valid.sum()
+        dm = batch.dec_padding_mask.astype(np.float64)
+        dec_lens = dm.sum(1)
+        if hps.pointer_gen:
+            rowg = dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
+        else:  # sequence_loss: sum(mask*CE)/sum(mask)
+            wm = dm * valid[:, None]
+            rowg = wm / wm.sum()
+        gcl = hps.cov_loss_wt * dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
+        host = {
+            "enc_batch": batch.enc_batch.astype(np.int64),
+            "enc_lens": batch.enc_lens.astype(np.int32),
+            "rev_idx": rev.astype(np.int64),
+            "ext": batch.enc_batch_extend_vocab.astype(np.int32),
+            "dec_batch_t": np.ascontiguousarray(batch.dec_batch.T).astype(np.int64),
+            "target_t": np.ascontiguousarray(batch.target_batch.T).astype(np.int32),
+            "rowg": np.ascontiguousarray(rowg.T).astype(np.float32),
+            "gcl": np.ascontiguousarray(gcl.T).astype(np.float32),
+        }
+        for k, v in host.items():
+            w[k].copy_(torch.from_numpy(v).pin_memory() if torch.cuda.is_available() else torch.from_numpy(v),
+                       non_blocking=True)
+
+    # ------------------------------------------------------------------ forward
+    def _encoder_forward(self):
+        k, w, B, T, H, A = self.k, self.w, self.B, self.T, self.H, self.A
+        lens, rev = w["enc_lens"], w["rev_idx"]
+        x = self.pk["emb"][w["enc_batch"]]  # [B,T,E] bf16
+        for layer, st in enumerate(self.enc):
+            din = st["din"]
+            xs = st["x_sf"]
+            xs[0].copy_(x.transpose(0, 1))
+            xs[1].copy_(x.gather(1, rev[..., None].expand(B, T, din)).transpose(0, 1))
+            for di, d in enumerate(("fw", "bw")):
+                g = mmf(xs[di].view(T * B, din), self.pk[f"enc{layer}_Kx{di}"])
+                st["gx"][di].copy_(g.view(T, B, 4 * H)).add_(self.p[enc_b(layer, d)])
+            st["hs"][:, 0].zero_()
+            st["cs"][:, 0].zero_()
+            st["out"].zero_()
+            for s in range(T):
+                k.lstm_enc_fwd_step(st["gx"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"], st["out"],
+                                    lens, s, T, B, H)
+            x = st["out"]
+        top = self.enc[-1]
+        old_c = torch.cat([top["cs"][0, T], top["cs"][1, T]], 1)
+        old_h = torch.cat([top["hs"][0, T], top["hs"][1, T]], 1).float()
+        pc = old_c @ self.p[RC] + self.p[BRC]
+        ph = old_h @ self.p[RH] + self.p[BRH]
+        self._red = (old_c, old_h, pc, ph)
+        c0, h0 = torch.relu(pc), torch.relu(ph)
+        w["Cst"][0].copy_(c0)
+        w["Cb"][0].copy_(c0)
+        w["Hb"][0].copy_(h0)
+        w["F"].view(B * T, A).copy_(torch.mm(top["out"].view(B * T, A), self.pk["Wh"]))
+
+    def _decoder_forward(self):
+        k, w, hps = self.k, self.w, self.hps
+        B, T, D, E, H, A = self.B, self.T, self.D, self.E, self.H, self.A
+        cov = hps.coverage
+        emb_dec = self.pk["emb"][w["dec_batch_t"]].view(D * B, E)
+        w["xe"].view(D * B, E).copy_(mmf(emb_dec, self.pk["lin_emb"])).add_(self.p[LIN_B])
+        self._emb_dec = emb_dec
+        enc_out, lens, F = self.enc[-1]["out"], w["enc_lens"], w["F"]
+        v, wc = self.f32["v"], self.f32["wc"]
+        for t in range(D):
+            k.dec_xcell_fwd(w["xe"][t], w["CTXb"][t - 1] if t > 0 else None, self.pk["WicT"], self.pk["WcT"],
+                            self.p[CELL_B], w["Hb"][t], w["Cst"][t], w["X"][t], w["Xb"][t], w["Cst"][t + 1],
+                            w["Cb"][t + 1], w["Hb"][t + 1], w["ACT"][t], B, E, H, A)
+            k.dec_sproj(w["Cb"][t + 1], w["Hb"][t + 1], self.pk["WsT"], self.p[ATT_B], w["S"][t], B, H, A)
+            cov_in = w["COV"][t] if (cov and t > 0) else None
+            k.attn_score(F, w["S"][t], v, wc, cov_in, lens, w["e"], B, T, A)
+            k.attn_softmax_ctx(w["e"], enc_out, lens, cov_in, w["ATT"][t], w["COV"][t + 1] if cov else None,
+                               w["covloss"][t] if cov else None, w["CTX"][t], w["CTXb"][t], B, T, A)
+
+    def _head_forward(self, need_grad: bool):
+        w, hps, p = self.w, self.hps, self.p
+        B, T, D, E, H, A, V = self.B, self.T, self.D, self.E, self.H, self.A, self.V
+        N = D * B
+        Hn = w["Hb"][1:].reshape(N, H)
+        ctxb = w["CTXb"].view(N, A)
+        out = mmf(Hn, self.pk["OUTm"][:H]) + mmf(ctxb, self.pk["OUTm"][H:]) + p[OUT_B]
+        self._out = out
+        w["outb"].copy_(out)
+        pg = None
+        if hps.pointer_gen:
+            pm = p[PG_M][:, 0]
+            pre = (w["CTX"].view(N, A) @ pm[:A] + w["Cst"][1:].reshape(N, H) @ pm[A:A + H]
+                   + Hn.float() @ pm[A + H:A + 2 * H] + w["X"].view(N, E) @ pm[A + 2 * H:] + p[PG_B])
+            w["pg"].view(N).copy_(torch.sigmoid(pre))
+            pg = w["pg"]
+        torch.mm(w["outb"], self.pk["ow"], out_dtype=F32, out=w["logits"])
+        self.k.ptr_loss(w["logits"], p[OV], w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None,
+                        w["ext"], w["enc_lens"], w["loss_row"], w["dlogits"] if need_grad else None,
+                        w["dpre"] if (need_grad and hps.pointer_gen) else None,
+                        w["dA"] if (need_grad and hps.pointer_gen) else None, N, B, T, V)
+
+    def forward(self, need_grad: bool = False):
+        self._encoder_forward()
+        self._decoder_forward()
+        self._head_forward(need_grad)
+        return self.losses()
+
+    def losses(self):
+        w, hps = self.w, self.hps
+        loss = (w["loss_row"] * w["rowg"]).sum()
+        out = {"loss": loss}
+        if hps.coverage:
+            covl = (w["covloss"] * w["gcl"]).sum() / hps.cov_loss_wt if hps.cov_loss_wt else w["covloss"].sum() * 0
+            out["coverage_loss"] = covl
+            out["total_loss"] = loss + hps.cov_loss_wt * covl
+        else:
+            out["total_loss"] = loss
+        return out
+
+    # ------------------------------------------------------------------ backward
+    def backward(self):
+        k, w, hps, p = self.k, self.w, self.hps, self.p
+        B, T, D, E, H, A, V = self.B, self.T, self.D, self.E, self.H, self.A, self.V
+        N = D * B
+        g = p.g
+        cov = hps.coverage
+        p.grad.zero_()
+        # ---- vocab projection
+        dl = w["dlogits"]
+        g(OW).copy_(torch.mm(w["outb"].t(), dl, out_dtype=F32))
+        g(OV).copy_(dl.sum(0, dtype=F32))
+        dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
+        # ---- output projection [h, ctx]
+        Hn = w["Hb"][1:].reshape(N, H)
+        ctxb = w["CTXb"].view(N, A)
+        doutb = dout.to(BF)
+        g(OUT_M)[:H].copy_(mmf(Hn.t(), doutb))
+        g(OUT_M)[H:].copy_(mmf(ctxb.t(), doutb))
+        g(OUT_B).copy_(dout.sum(0))
+        dH_dir = mmf(doutb, self.pk["OUTm"][:H].t()).view(D, B, H)
+        dCTX_dir = mmf(doutb, self.pk["OUTm"][H:].t()).view(D, B, A)
+        dC_dir = None
+        dX_dir = None
+        if hps.pointer_gen:
+            dpre = w["dpre"].view(N)
+            pm = p[PG_M][:, 0]
+            gp = g(PG_M)[:, 0]
+            gp[:A].copy_(w["CTX"].view(N, A).t() @ dpre)
+            gp[A:A + H].copy_(w["Cst"][1:].reshape(N, H).t() @ dpre)
+            gp[A + H:A + 2 * H].copy_(Hn.float().t() @ dpre)
+            gp[A + 2 * H:].copy_(w["X"].view(N, E).t() @ dpre)
+            g(PG_B).copy_(dpre.sum().view(1))
+            dp = dpre.view(D, B, 1)
+            dCTX_dir.add_(dp * pm[:A])
+            dC_dir = (dp * pm[A:A + H]).contiguous()
+            dH_dir.add_(dp * pm[A + H:A + 2 * H])
+            dX_dir = (dp * pm[A + 2 * H:]).contiguous()
+        # ---- decoder reverse loop
+        enc_out, lens, F = self.enc[-1]["out"], w["enc_lens"], w["F"]
+        v, wc = self.f32["v"], self.f32["wc"]
+        w["DCTX"][D - 1].copy_(dCTX_dir[D - 1])
+        w["dh_rec"].zero_()
+        w["dc_carry"].zero_()
+        dcov = w["dcov"]
+        Ga = w["dA"] if hps.pointer_gen else None
+        for t in reversed(range(D)):
+            dcov_next = dcov[(t + 1) % 2] if (cov and t < D - 1) else None
+            cov_t = w["COV"][t] if (cov and t > 0) else None
+            gcl_t = w["gcl"][t] if cov else None
+            k.attn_bwd_da(enc_out, w["DCTX"][t], Ga[t] if Ga is not None else None, dcov_next, w["ATT"][t], cov_t,
+                          gcl_t, lens, w["da"], B, T, A)
+            k.attn_bwd_tanh(F, w["S"][t], v, wc, cov_t, w["ATT"][t], w["da"], dcov_next, gcl_t, lens, w["DE"][t],
+                            w["dsp"], dcov[t % 2] if cov else None, B, T, A)
+            k.dec_bwd_cell(w["dsp"], self.nchunk, self.pk["Ws"], dC_dir[t] if dC_dir is not None else None,
+                           dH_dir[t], w["dh_rec"], w["dc_carry"], w["ACT"][t], w["Cst"][t + 1], w["Cst"][t],
+                           w["DS"][t], w["DZ"][t], B, H, A)
+            k.dec_bwd_dz(w["DZ"][t], self.pk["Wc"], self.pk["Wic"], dX_dir[t] if dX_dir is not None else None,
+                         dCTX_dir[t - 1] if t > 0 else None, w["DX"][t], w["DCTX"][t - 1] if t > 0 else None,
+                         w["dh_rec"], B, E, H, A)
+        # ---- decoder weight gradients (one GEMM each over all D*B rows)
+        DZ = w["DZ"].view(N, 4 * H)
+        gk = g(CELL_K)
+        gk[:E].copy_(mmf(w["Xb"].view(N, E).t(), DZ))
+        gk[E:].copy_(mmf(w["Hb"][:D].reshape(N, H).t(), DZ))
+        g(CELL_B).copy_(DZ.sum(0, dtype=F32))
+        DX = w["DX"].view(N, E)
+        DXb = DX.to(BF)
+        gl = g(LIN_M)
+        gl[:E].copy_(mmf(self._emb_dec.t(), DXb))
+        gl[E:].zero_()
+        if D > 1:
+            gl[E:].copy_(mmf(w["CTXb"][:D - 1].reshape((D - 1) * B, A).t(), DXb[B:]))
+        g(LIN_B).copy_(DX.sum(0))
+        d_emb_dec = mmf(DXb, self.pk["lin_emb"].t())  # [N,E]
+        DS = w["DS"].view(N, A)
+        DSb = DS.to(BF)
+        gs = g(ATT_M)
+        gs[:H].copy_(mmf(w["Cb"][1:].reshape(N, H).t(), DSb))
+        gs[H:].copy_(mmf(Hn.t(), DSb))
+        g(ATT_B).copy_(DS.sum(0))
+        # ---- attention feature gradients (tanh recomputed once over all steps)
+        w["dF"].zero_()
+        w["dv"].zero_()
+        w["dwc"].zero_()
+        k.attn_bwd_feat(F, w["S"], v, wc, w["COV"][:D] if cov else None, w["DE"], lens, w["dF"], w["dv"],
+                        w["dwc"] if cov else None, D, B, T, A)
+        g(VATT).copy_(w["dv"])
+        if cov:
+            g(WCOV).view(A).copy_(w["dwc"])
+        dFb = w["dF"].view(B * T, A).to(BF)
+        top = self.enc[-1]
+        g(WH).view(A, A).copy_(mmf(top["out"].view(B * T, A).t(), dFb))
+        dE = torch.bmm(w["ATT"].permute(1, 2, 0), w["DCTX"].permute(1, 0, 2))  # [B,T,A]
+        dE.view(B * T, A).add_(mmf(dFb, self.pk["Wh"].t()))
+        # ---- reduce_states
+        old_c, old_h, pc, ph = self._red
+        dpc = w["dc_carry"] * (pc > 0)
+        dph = w["dh_rec"] * (ph > 0)
+        g(RC).copy_(old_c.t() @ dpc)
+        g(BRC).copy_(dpc.sum(0))
+        g(RH).copy_(old_h.t() @ dph)
+        g(BRH).copy_(dph.sum(0))
+        d_old_c = dpc @ self.p[RC].t()
+        d_old_h = dph @ self.p[RH].t()
+        # ---- encoder BPTT, top layer down
+        d_in = dE
+        gemb = g(EMB)
+        for layer in reversed(range(self.L)):
+            st = self.enc[layer]
+            din = st["din"]
+            st["dout"].copy_(d_in)
+            if layer == self.L - 1:
+                st["dh_fin"][0].copy_(d_old_h[:, :H]); st["dh_fin"][1].copy_(d_old_h[:, H:])
+                st["dc_carry"][0].copy_(d_old_c[:, :H]); st["dc_carry"][1].copy_(d_old_c[:, H:])
+            else:
+                st["dh_fin"].zero_()
+                st["dc_carry"].zero_()
+            for s in reversed(range(T)):
+                k.lstm_enc_bwd_step(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"], st["dc_carry"],
+                                    st["acts"], st["cs"], lens, s, T, B, H)
+            dx = torch.zeros(B, T, din, dtype=F32, device=self.dev)
+            for di, d in enumerate(("fw", "bw")):
+                dzd = st["dz"][di].view(T * B, 4 * H)
+                gkd = g(enc_k(layer, d))
+                gkd[:din].copy_(mmf(st["x_sf"][di].view(T * B, din).t(), dzd))
+                gkd[din:].copy_(mmf(st["hs"][di, :T].reshape(T * B, H).t(), dzd))
+                g(enc_b(layer, d)).copy_(dzd.sum(0, dtype=F32))
+                dxs = mmf(dzd, self.pk[f"enc{layer}_Kx{di}"].t()).view(T, B, din).transpose(0, 1)
+                if di == 0:
+                    dx.add_(dxs)
+                else:
+                    dx.scatter_add_(1, w["rev_idx"][..., None].expand(B, T, din), dxs)
+            d_in = dx
+        gemb.index_add_(0, w["enc_batch"].view(-1), d_in.view(B * T, self.E))
+        gemb.index_add_(0, w["dec_batch_t"].view(-1), d_emb_dec)
+
+    # ------------------------------------------------------------------ optimizer
+    def optimizer_step(self):
+        hps, p, w = self.hps, self.p, self.w
+        self.k.clip_adagrad(p.flat, p.accum, p.grad, w["opt_part"], hps.lr, hps.max_grad_norm, w["gnorm"],
+                            w["nan_flag"])
+        self.pack()
+
+    def train_step(self, allreduce=None):
+        """forward + backward (+ optional grad all-reduce hook) + clip/Adagrad + repack."""
+        out = self.forward(need_grad=True)
+        self.backward()
+        if allreduce is not None:
+            allreduce(self.p.grad)
+        self.optimizer_step()
+        return out
