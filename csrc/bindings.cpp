@@ -65,7 +65,7 @@ void lstm_enc_bwd_step(const Tensor& dz, const Tensor& Wn, const Tensor& dout, c
 void attn_score(const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov, const Tensor& lens,
                 const Tensor& e, int64_t B, int64_t T, int64_t A) {
   chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens"); chk(e, F32, "e");
-  TORCH_CHECK(A % 64 == 0 && A <= 1024, "attention size must be a multiple of 64 and <= 1024");
+  TORCH_CHECK(A % 64 == 0 && A <= 1024 && T % 2 == 0, "attention size must be a multiple of 64 (<= 1024), T even");
   numel_eq(F, B * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v"); numel_eq(e, B * T, "e");
   chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov");
   launch_attn_score(P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens), P<float>(e), B,
@@ -86,8 +86,8 @@ void attn_softmax_ctx(const Tensor& e, const Tensor& E, const Tensor& lens, cons
 
 void attn_bwd_da(const Tensor& E, const Tensor& dctx, const OT& Ga, const OT& dcov_next, const Tensor& a,
                  const OT& cov, const OT& gcl, const Tensor& lens, const Tensor& da, int64_t B, int64_t T, int64_t A) {
-  chk(E, BF, "E"); chk(dctx, F32, "dctx"); chk(a, F32, "a"); chk(lens, I32, "lens"); chk(da, F32, "da");
-  TORCH_CHECK(A % 64 == 0 && A <= 1024, "bad A");
+  chk(E, BF, "Et"); chk(dctx, F32, "dctx"); chk(a, F32, "a"); chk(lens, I32, "lens"); chk(da, F32, "da");
+  TORCH_CHECK(A % 64 == 0 && A <= 1024 && T % 2 == 0, "bad A/T");
   numel_eq(E, B * T * A, "E"); numel_eq(dctx, B * A, "dctx"); numel_eq(a, B * T, "a"); numel_eq(da, B * T, "da");
   chko(Ga, F32, B * T, "Ga"); chko(dcov_next, F32, B * T, "dcov_next"); chko(cov, F32, B * T, "cov");
   chko(gcl, F32, B, "gcl");
@@ -97,16 +97,16 @@ void attn_bwd_da(const Tensor& E, const Tensor& dctx, const OT& Ga, const OT& dc
 
 void attn_bwd_tanh(const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov, const Tensor& a,
                    const Tensor& da, const OT& dcov_next, const OT& gcl, const Tensor& lens, const Tensor& de_out,
-                   const Tensor& dsp, const OT& dcov_out, int64_t B, int64_t T, int64_t A) {
+                   const Tensor& ds, const OT& dcov_out, int64_t B, int64_t T, int64_t A) {
   chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(da, F32, "da"); chk(lens, I32, "lens");
-  chk(de_out, F32, "de_out"); chk(dsp, F32, "dsp");
+  chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
   TORCH_CHECK(A % 64 == 0 && A <= 1024, "bad A");
   numel_eq(F, B * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(a, B * T, "a"); numel_eq(da, B * T, "da");
-  numel_eq(de_out, B * T, "de_out"); numel_eq(dsp, B * attn_nchunk(T) * A, "dsp");
+  numel_eq(de_out, B * T, "de_out"); numel_eq(ds, B * A, "ds");
   chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(dcov_next, F32, B * T, "dcov_next");
   chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
   launch_attn_bwd_tanh(P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a), P<float>(da),
-                       PO<float>(dcov_next), PO<float>(gcl), P<int>(lens), P<float>(de_out), P<float>(dsp),
+                       PO<float>(dcov_next), PO<float>(gcl), P<int>(lens), P<float>(de_out), P<float>(ds),
                        PO<float>(dcov_out), B, T, A, stream());
 }
 
@@ -126,56 +126,53 @@ void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const 
 int64_t attn_chunks(int64_t T) { return attn_nchunk(T); }
 
 // ---------------------------------------------------------------- decoder cell
-void dec_xcell_fwd(const Tensor& xe, const OT& ctxp, const Tensor& WicT, const Tensor& WcT, const Tensor& bc,
-                   const Tensor& hprev, const Tensor& cprev, const Tensor& x_out, const Tensor& xb_out,
-                   const Tensor& c_out, const Tensor& cb_out, const Tensor& hb_out, const Tensor& act, int64_t B,
-                   int64_t E, int64_t H, int64_t A) {
-  chk(xe, F32, "xe"); chk(WicT, BF, "WicT"); chk(WcT, BF, "WcT"); chk(bc, F32, "bc"); chk(hprev, BF, "hprev");
-  chk(cprev, F32, "cprev"); chk(x_out, F32, "x_out"); chk(xb_out, BF, "xb_out"); chk(c_out, F32, "c_out");
+void dec_cell_fwd(const Tensor& XG, const OT& ctxp, const Tensor& hprev, const Tensor& cprev, const Tensor& WcT,
+                  const Tensor& c_out, const Tensor& cb_out, const Tensor& hb_out, const Tensor& act, int64_t B,
+                  int64_t H, int64_t A) {
+  chk(XG, F32, "XG"); chk(hprev, BF, "hprev"); chk(cprev, F32, "cprev"); chk(WcT, BF, "WcT"); chk(c_out, F32, "c_out");
   chk(cb_out, BF, "cb_out"); chk(hb_out, BF, "hb_out"); chk(act, F32, "act");
-  TORCH_CHECK(E % 32 == 0 && H % 32 == 0 && A % 32 == 0, "dims must be multiples of 32");
-  numel_eq(xe, B * E, "xe"); chko(ctxp, BF, B * A, "ctxp"); numel_eq(WicT, E * A, "WicT");
-  numel_eq(WcT, 4 * H * (E + H), "WcT"); numel_eq(bc, 4 * H, "bc"); numel_eq(hprev, B * H, "hprev");
-  numel_eq(cprev, B * H, "cprev"); numel_eq(x_out, B * E, "x_out"); numel_eq(c_out, B * H, "c_out");
-  numel_eq(act, B * 4 * H, "act");
-  launch_dec_xcell_fwd(P<float>(xe), PO<bf16>(ctxp), P<bf16>(WicT), P<bf16>(WcT), P<float>(bc), P<bf16>(hprev),
-                       P<float>(cprev), P<float>(x_out), P<bf16>(xb_out), P<float>(c_out), P<bf16>(cb_out),
-                       P<bf16>(hb_out), P<float>(act), B, E, H, A, stream());
+  TORCH_CHECK(H % 32 == 0 && A % 32 == 0, "dims must be multiples of 32");
+  numel_eq(XG, B * 4 * H, "XG"); chko(ctxp, BF, B * A, "ctxp"); numel_eq(hprev, B * H, "hprev");
+  numel_eq(cprev, B * H, "cprev"); numel_eq(WcT, 4 * H * (A + H), "WcT"); numel_eq(c_out, B * H, "c_out");
+  numel_eq(cb_out, B * H, "cb_out"); numel_eq(hb_out, B * H, "hb_out"); numel_eq(act, B * 4 * H, "act");
+  launch_dec_cell_fwd(P<float>(XG), PO<bf16>(ctxp), P<bf16>(hprev), P<float>(cprev), P<bf16>(WcT), P<float>(c_out),
+                      P<bf16>(cb_out), P<bf16>(hb_out), P<float>(act), B, H, A, stream());
 }
 
 void dec_sproj(const Tensor& cb, const Tensor& hb, const Tensor& WsT, const Tensor& bs, const Tensor& s_out, int64_t B,
                int64_t H, int64_t A) {
   chk(cb, BF, "cb"); chk(hb, BF, "hb"); chk(WsT, BF, "WsT"); chk(bs, F32, "bs"); chk(s_out, F32, "s_out");
+  TORCH_CHECK(H % 32 == 0 && A % 16 == 0, "bad dims");
   numel_eq(cb, B * H, "cb"); numel_eq(hb, B * H, "hb"); numel_eq(WsT, A * 2 * H, "WsT"); numel_eq(bs, A, "bs");
   numel_eq(s_out, B * A, "s_out");
   launch_dec_sproj(P<bf16>(cb), P<bf16>(hb), P<bf16>(WsT), P<float>(bs), P<float>(s_out), B, H, A, stream());
 }
 
-void dec_bwd_cell(const Tensor& dsp, int64_t nchunk, const Tensor& Ws, const OT& dC_dir, const OT& dH_dir,
-                  const Tensor& dh_rec, const Tensor& dc_carry, const Tensor& act, const Tensor& c_now,
-                  const Tensor& c_prev, const Tensor& ds_out, const Tensor& dz, int64_t B, int64_t H, int64_t A) {
-  chk(dsp, F32, "dsp"); chk(Ws, BF, "Ws"); chk(dh_rec, F32, "dh_rec"); chk(dc_carry, F32, "dc_carry");
-  chk(act, F32, "act"); chk(c_now, F32, "c_now"); chk(c_prev, F32, "c_prev"); chk(ds_out, F32, "ds_out");
-  chk(dz, BF, "dz");
-  numel_eq(dsp, B * nchunk * A, "dsp"); numel_eq(Ws, 2 * H * A, "Ws"); chko(dC_dir, F32, B * H, "dC_dir");
+void dec_bwd_cell(const Tensor& ds, const Tensor& Ws, const OT& dC_dir, const OT& dH_dir, const Tensor& dh_rec,
+                  const Tensor& dc_carry, const Tensor& act, const Tensor& c_now, const Tensor& c_prev,
+                  const Tensor& dz, int64_t B, int64_t H, int64_t A) {
+  chk(ds, F32, "ds"); chk(Ws, BF, "Ws"); chk(dh_rec, F32, "dh_rec"); chk(dc_carry, F32, "dc_carry");
+  chk(act, F32, "act"); chk(c_now, F32, "c_now"); chk(c_prev, F32, "c_prev"); chk(dz, BF, "dz");
+  TORCH_CHECK(H % 16 == 0 && A % 32 == 0, "bad dims");
+  numel_eq(ds, B * A, "ds"); numel_eq(Ws, 2 * H * A, "Ws"); chko(dC_dir, F32, B * H, "dC_dir");
   chko(dH_dir, F32, B * H, "dH_dir"); numel_eq(dh_rec, B * H, "dh_rec"); numel_eq(dc_carry, B * H, "dc_carry");
   numel_eq(act, B * 4 * H, "act"); numel_eq(c_now, B * H, "c_now"); numel_eq(c_prev, B * H, "c_prev");
-  numel_eq(ds_out, B * A, "ds_out"); numel_eq(dz, B * 4 * H, "dz");
-  launch_dec_bwd_cell(P<float>(dsp), nchunk, P<bf16>(Ws), PO<float>(dC_dir), PO<float>(dH_dir), P<float>(dh_rec),
-                      P<float>(dc_carry), P<float>(act), P<float>(c_now), P<float>(c_prev), P<float>(ds_out),
-                      P<bf16>(dz), B, H, A, stream());
+  numel_eq(dz, B * 4 * H, "dz");
+  launch_dec_bwd_cell(P<float>(ds), P<bf16>(Ws), PO<float>(dC_dir), PO<float>(dH_dir), P<float>(dh_rec),
+                      P<float>(dc_carry), P<float>(act), P<float>(c_now), P<float>(c_prev), P<bf16>(dz), B, H, A,
+                      stream());
 }
 
-void dec_bwd_dz(const Tensor& dz, const Tensor& Wc, const Tensor& Wic, const OT& dX_dir, const OT& dCTX_dir_prev,
-                const Tensor& dx_out, const OT& dctx_prev_out, const Tensor& dh_rec, int64_t B, int64_t E, int64_t H,
-                int64_t A) {
-  chk(dz, BF, "dz"); chk(Wc, BF, "Wc"); chk(Wic, BF, "Wic"); chk(dx_out, F32, "dx_out"); chk(dh_rec, F32, "dh_rec");
-  numel_eq(dz, B * 4 * H, "dz"); numel_eq(Wc, (E + H) * 4 * H, "Wc"); numel_eq(Wic, A * E, "Wic");
+void dec_bwd_dz(const Tensor& dz, const Tensor& Wbig, const OT& dX_dir, const OT& dCTX_dir_prev, const Tensor& dx_out,
+                const OT& dctx_prev_out, const Tensor& dh_rec, int64_t B, int64_t E, int64_t H, int64_t A) {
+  chk(dz, BF, "dz"); chk(Wbig, BF, "Wbig"); chk(dx_out, F32, "dx_out"); chk(dh_rec, F32, "dh_rec");
+  TORCH_CHECK(E % 16 == 0 && H % 32 == 0 && A % 16 == 0, "bad dims");
+  numel_eq(dz, B * 4 * H, "dz"); numel_eq(Wbig, (E + H + A) * 4 * H, "Wbig");
   chko(dX_dir, F32, B * E, "dX_dir"); chko(dCTX_dir_prev, F32, B * A, "dCTX_dir_prev");
   numel_eq(dx_out, B * E, "dx_out"); chko(dctx_prev_out, F32, B * A, "dctx_prev_out");
   numel_eq(dh_rec, B * H, "dh_rec");
-  launch_dec_bwd_dz(P<bf16>(dz), P<bf16>(Wc), P<bf16>(Wic), PO<float>(dX_dir), PO<float>(dCTX_dir_prev),
-                    P<float>(dx_out), PO<float>(dctx_prev_out), P<float>(dh_rec), B, E, H, A, stream());
+  launch_dec_bwd_dz(P<bf16>(dz), P<bf16>(Wbig), PO<float>(dX_dir), PO<float>(dCTX_dir_prev), P<float>(dx_out),
+                    PO<float>(dctx_prev_out), P<float>(dh_rec), B, E, H, A, stream());
 }
 
 // ---------------------------------------------------------------- loss / optimizer
@@ -221,7 +218,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("attn_bwd_tanh", &attn_bwd_tanh);
   m.def("attn_bwd_feat", &attn_bwd_feat);
   m.def("attn_chunks", &attn_chunks);
-  m.def("dec_xcell_fwd", &dec_xcell_fwd);
+  m.def("dec_cell_fwd", &dec_cell_fwd);
   m.def("dec_sproj", &dec_sproj);
   m.def("dec_bwd_cell", &dec_bwd_cell);
   m.def("dec_bwd_dz", &dec_bwd_dz);

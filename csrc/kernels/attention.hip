@@ -6,57 +6,58 @@
 //   cov'  = cov + a           covloss = sum_i min(a_i, cov_i)
 //   ctx   = sum_i a_i E[i,:]
 //
-// Score kernels map lanes to the feature axis (8 contiguous bf16 per lane = one
-// 16-byte load of a [B][T][A] row) and waves to positions, so every F/E byte is read
-// once per step with full-width loads; the per-position dot product is a 6-step DPP
-// reduction.  The weight gradients of v, w_c and the [B,T,A] gradient of F are NOT
-// accumulated per step: the backward step stores de_t and a post-loop kernel
-// (attn_bwd_feat) recomputes tanh once over all steps, so the recurrent critical path
-// only carries what the recurrence needs (ds_t, dcov_t).
+// Two layouts of the [B,T,A] encoder tensors are kept (both fit trivially in HBM):
+//  * row-major F/E [B][T][A] -- lanes on the feature axis (8 bf16 = one 16-B load);
+//  * transposed Ft/Et [B][A][T] -- lanes on the position axis, so the score e_i and
+//    da_i = dctx . E_i reduce over k inside a lane (no cross-lane reduction at all), the
+//    per-k parameters (s_k, v_k, w_c_k, dctx_k) are wave-uniform scalar loads, and the 4
+//    waves of a block split the k axis (summed once in LDS).
+// The v / w_c / F gradients are NOT accumulated per step: the backward step stores
+// de_t, and attn_bwd_feat recomputes tanh once over all steps after the loop.  The
+// recurrent path only carries ds_t (atomically accumulated across position chunks) and
+// dcov_t.
 #include "common.h"
 
-#define POS_PER_WAVE 16
-#define POS_PER_BLOCK 64
+#define SCORE_POS 128  // positions per block in the lanes-over-positions kernels (2 per lane)
 
 // ---------------------------------------------------------------- forward: scores
+// grid (ceil(T/128), B).  Ft: [B][A][T] bf16, T even.
 __global__ __launch_bounds__(256) void attn_score_kernel(
-    const bf16* __restrict__ F, const float* __restrict__ s, const float* __restrict__ v,
+    const bf16* __restrict__ Ft, const float* __restrict__ s, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov, const int* __restrict__ lens,
     float* __restrict__ e, int T, int A) {
+  __shared__ float red[4][SCORE_POS];
   const int b = blockIdx.y;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int len = lens[b];
-  const int p0 = blockIdx.x * POS_PER_BLOCK + wid * POS_PER_WAVE;
-  if (p0 >= len) return;  // masked positions are never read by the softmax
-  const int NK = (A + 511) / 512;  // k-blocks of 512 per lane-slice
-  float sk[2][8], vk[2][8], wk[2][8];
-  for (int kb = 0; kb < NK; ++kb) {
-    const int k0 = kb * 512 + lane * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bool ok = k0 + j < A;
-      sk[kb][j] = ok ? s[(size_t)b * A + k0 + j] : 0.f;
-      vk[kb][j] = ok ? v[k0 + j] : 0.f;
-      wk[kb][j] = (ok && wc) ? wc[k0 + j] : 0.f;
-    }
+  const int pb = blockIdx.x * SCORE_POS;
+  if (pb >= len) return;  // uniform: masked positions are never read by the softmax
+  const int p = pb + 2 * lane;
+  const bool ok = p < T;
+  const int pc = ok ? p : 0;
+  float c0 = 0.f, c1 = 0.f;
+  if (cov && ok) {
+    c0 = cov[(size_t)b * T + pc];
+    c1 = cov[(size_t)b * T + pc + 1];
   }
-  const bf16* Fb = F + (size_t)b * T * A;
-#pragma unroll 4
-  for (int q = 0; q < POS_PER_WAVE; ++q) {
-    const int p = p0 + q;
-    if (p >= len) break;
-    const float c = cov ? cov[(size_t)b * T + p] : 0.f;
-    float acc = 0.f;
-    for (int kb = 0; kb < NK; ++kb) {
-      const int k0 = kb * 512 + lane * 8;
-      if (k0 < A) {
-        bf16x8 f = ld8(Fb + (size_t)p * A + k0);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc += vk[kb][j] * ftanh(bf2f(f[j]) + sk[kb][j] + wk[kb][j] * c);
-      }
-    }
-    acc = wave_sum(acc);
-    if (lane == 0) e[(size_t)b * T + p] = acc;
+  const int ka = wid * (A / 4), kb = ka + A / 4;
+  const bf16* fp = Ft + ((size_t)b * A) * T + pc;
+  const float* sb = s + (size_t)b * A;
+  float e0 = 0.f, e1 = 0.f;
+#pragma unroll 8
+  for (int k = ka; k < kb; ++k) {
+    const uint32_t raw = *reinterpret_cast<const uint32_t*>(fp + (size_t)k * T);
+    const float f0 = __uint_as_float(raw << 16), f1 = __uint_as_float(raw & 0xffff0000u);
+    const float sk = sb[k], vk = v[k], wk = wc ? wc[k] : 0.f;
+    e0 += vk * ftanh(f0 + sk + wk * c0);
+    e1 += vk * ftanh(f1 + sk + wk * c1);
+  }
+  red[wid][2 * lane] = e0;
+  red[wid][2 * lane + 1] = e1;
+  __syncthreads();
+  if (threadIdx.x < SCORE_POS) {
+    const int q = pb + threadIdx.x;
+    if (q < len) e[(size_t)b * T + q] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
   }
 }
 
@@ -109,6 +110,7 @@ __global__ __launch_bounds__(256) void attn_softmax_ctx_kernel(
   const int ps = lane >> 3, fg = lane & 7;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const bf16* Eb = E + (size_t)b * T * A + f0 + fg * 8;
+#pragma unroll 4
   for (int i = wid * 8 + ps; i < len; i += 32) {
     const float a = sa[i];
     bf16x8 x = ld8(Eb + (size_t)i * A);
@@ -136,73 +138,84 @@ __global__ __launch_bounds__(256) void attn_softmax_ctx_kernel(
 }
 
 // ------------------------------------------------------------- backward step: da
-//   da_i = Ga_i + dcov_next_i + g_cl*[a_i <= cov_i] + dctx . E[i,:]
+//   da_i = Ga_i + dcov_next_i + g_cl*[a_i <= cov_i] + dctx . E[i,:]     (Et: [B][A][T])
 __global__ __launch_bounds__(256) void attn_bwd_da_kernel(
-    const bf16* __restrict__ E, const float* __restrict__ dctx, const float* __restrict__ Ga,
+    const bf16* __restrict__ Et, const float* __restrict__ dctx, const float* __restrict__ Ga,
     const float* __restrict__ dcov_next, const float* __restrict__ a, const float* __restrict__ cov,
     const float* __restrict__ gcl, const int* __restrict__ lens, float* __restrict__ da, int T, int A) {
+  __shared__ float red[4][SCORE_POS];
   const int b = blockIdx.y;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int len = lens[b];
-  const int p0 = blockIdx.x * POS_PER_BLOCK + wid * POS_PER_WAVE;
-  if (p0 >= len) return;
-  const int NK = (A + 511) / 512;
-  float dk[2][8];
-  for (int kb = 0; kb < NK; ++kb) {
-    const int k0 = kb * 512 + lane * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dk[kb][j] = k0 + j < A ? dctx[(size_t)b * A + k0 + j] : 0.f;
+  const int pb = blockIdx.x * SCORE_POS;
+  if (pb >= len) return;
+  const int p = pb + 2 * lane;
+  const int pc = p < T ? p : 0;
+  const int ka = wid * (A / 4), kb = ka + A / 4;
+  const bf16* ep = Et + ((size_t)b * A) * T + pc;
+  const float* db = dctx + (size_t)b * A;
+  float d0 = 0.f, d1 = 0.f;
+#pragma unroll 8
+  for (int k = ka; k < kb; ++k) {
+    const uint32_t raw = *reinterpret_cast<const uint32_t*>(ep + (size_t)k * T);
+    const float dk = db[k];
+    d0 += dk * __uint_as_float(raw << 16);
+    d1 += dk * __uint_as_float(raw & 0xffff0000u);
   }
-  const float g = gcl ? gcl[b] : 0.f;
-  const bf16* Eb = E + (size_t)b * T * A;
-#pragma unroll 4
-  for (int q = 0; q < POS_PER_WAVE; ++q) {
-    const int p = p0 + q;
-    if (p >= len) break;
-    float acc = 0.f;
-    for (int kb = 0; kb < NK; ++kb) {
-      const int k0 = kb * 512 + lane * 8;
-      if (k0 < A) {
-        bf16x8 x = ld8(Eb + (size_t)p * A + k0);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc += dk[kb][j] * bf2f(x[j]);
-      }
-    }
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      const size_t ix = (size_t)b * T + p;
-      float r = acc;
+  red[wid][2 * lane] = d0;
+  red[wid][2 * lane + 1] = d1;
+  __syncthreads();
+  if (threadIdx.x < SCORE_POS) {
+    const int q = pb + threadIdx.x;
+    if (q < len) {
+      const size_t ix = (size_t)b * T + q;
+      float r = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
       if (Ga) r += Ga[ix];
       if (dcov_next) r += dcov_next[ix];
-      if (gcl && a[ix] <= (cov ? cov[ix] : 0.f)) r += g;
+      if (gcl && a[ix] <= (cov ? cov[ix] : 0.f)) r += gcl[b];
       da[ix] = r;
     }
   }
 }
 
 // ----------------------------------------------------- backward step: de, ds, dcov
-// de_i = a_i (da_i - sum_j a_j da_j);  ds_k = sum_i de_i v_k sech2(u_ik) (partial per
-// 64-position chunk: dsp[b][chunk][A]);  dcov_i = dcov_next_i + g_cl*[a_i > cov_i]
-//   + de_i sum_k v_k w_c_k sech2(u_ik).
+// de_i = a_i (da_i - sum_j a_j da_j);  ds_k += sum_i de_i v_k sech2(u_ik) (atomic into
+// ds[b][k], pre-zeroed);  dcov_i = dcov_next_i + g_cl*[a_i > cov_i] + de_i sum_k v_k w_c_k sech2(u_ik).
+// Lanes on the feature axis (8 per lane, NK blocks of 512); each wave takes 16 positions
+// in groups of 8 and reduces the 8 per-position dcov partials across the 64 lanes with a
+// butterfly reduce-scatter (10 shuffles per 8 positions instead of 48).
+template <int NK>
 __global__ __launch_bounds__(256) void attn_bwd_tanh_kernel(
     const bf16* __restrict__ F, const float* __restrict__ s, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov, const float* __restrict__ a,
     const float* __restrict__ da, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
-    const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ dsp,
+    const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
     float* __restrict__ dcov_out, int T, int A) {
   __shared__ float red[8];
-  __shared__ float part[4][1024];
+  __shared__ float part[4][512 * NK];
   const int b = blockIdx.y;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = lens[b];
   const size_t rb = (size_t)b * T;
+  const int p0 = blockIdx.x * 64 + wid * 16;
+  if (blockIdx.x * 64 >= len) {  // whole block masked: only pass dcov through
+    if (dcov_out)
+      for (int i = tid; i < 64; i += 256) {
+        const int p = blockIdx.x * 64 + i;
+        if (p < T) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
+      }
+    for (int i = tid; i < 64; i += 256) {
+      const int p = blockIdx.x * 64 + i;
+      if (p < T) de_out[rb + p] = 0.f;
+    }
+    return;
+  }
   float S = 0.f;
   for (int i = tid; i < len; i += 256) S += a[rb + i] * da[rb + i];
   S = block_sum<256>(S, red);
-  const int NK = (A + 511) / 512;
-  const int p0 = blockIdx.x * POS_PER_BLOCK + wid * POS_PER_WAVE;
   const float g = gcl ? gcl[b] : 0.f;
-  float sk[2][8], vk[2][8], wk[2][8], acc[2][8];
+  float sk[NK][8], vk[NK][8], wk[NK][8], acc[NK][8];
+#pragma unroll
   for (int kb = 0; kb < NK; ++kb) {
     const int k0 = kb * 512 + lane * 8;
 #pragma unroll
@@ -215,58 +228,94 @@ __global__ __launch_bounds__(256) void attn_bwd_tanh_kernel(
     }
   }
   const bf16* Fb = F + (size_t)b * T * A;
-  for (int q = 0; q < POS_PER_WAVE; ++q) {
-    const int p = p0 + q;
-    if (p >= T) break;
-    const size_t ix = rb + p;
-    if (p >= len) {
-      if (lane == 0) {
-        de_out[ix] = 0.f;
-        if (dcov_out) dcov_out[ix] = dcov_next ? dcov_next[ix] : 0.f;
-      }
-      continue;
-    }
-    const float ap = a[ix];
-    const float de = ap * (da[ix] - S);
-    const float c = cov ? cov[ix] : 0.f;
-    float dcv = 0.f;
-    for (int kb = 0; kb < NK; ++kb) {
-      const int k0 = kb * 512 + lane * 8;
-      if (k0 < A) {
-        bf16x8 f = ld8(Fb + (size_t)p * A + k0);
+  const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1;
+  for (int grp = 0; grp < 2; ++grp) {
+    const int pg = p0 + grp * 8;
+    float dcv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float th = ftanh(bf2f(f[j]) + sk[kb][j] + wk[kb][j] * c);
-          const float gs = de * vk[kb][j] * (1.0f - th * th);
-          acc[kb][j] += gs;
-          dcv += gs * wk[kb][j];
+    for (int q = 0; q < 8; ++q) {
+      const int p = pg + q;
+      dcv[q] = 0.f;
+      if (p < len) {  // wave-uniform
+        const size_t ix = rb + p;
+        const float de = a[ix] * (da[ix] - S);
+        const float c = cov ? cov[ix] : 0.f;
+#pragma unroll
+        for (int kb = 0; kb < NK; ++kb) {
+          const int k0 = kb * 512 + lane * 8;
+          if (k0 < A) {
+            bf16x8 f = ld8(Fb + (size_t)p * A + k0);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float th = ftanh(bf2f(f[j]) + sk[kb][j] + wk[kb][j] * c);
+              const float gs = de * vk[kb][j] * (1.0f - th * th);
+              acc[kb][j] += gs;
+              dcv[q] += gs * wk[kb][j];
+            }
+          }
         }
       }
     }
-    if (dcov_out) dcv = wave_sum(dcv);
-    if (lane == 0) {
-      de_out[ix] = de;
-      if (dcov_out) {
-        float r = dcv + (dcov_next ? dcov_next[ix] : 0.f);
-        if (gcl && ap > c) r += g;
-        dcov_out[ix] = r;
+    // butterfly reduce-scatter of dcv[0..7] over 64 lanes
+    float h4[4], h2[2], h1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float send = b5 ? dcv[i] : dcv[i + 4];
+      const float keep = b5 ? dcv[i + 4] : dcv[i];
+      h4[i] = keep + __shfl_xor(send, 32, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float send = b4 ? h4[i] : h4[i + 2];
+      const float keep = b4 ? h4[i + 2] : h4[i];
+      h2[i] = keep + __shfl_xor(send, 16, 64);
+    }
+    {
+      const float send = b3 ? h2[0] : h2[1];
+      const float keep = b3 ? h2[1] : h2[0];
+      h1 = keep + __shfl_xor(send, 8, 64);
+    }
+    h1 += __shfl_xor(h1, 4, 64);
+    h1 += __shfl_xor(h1, 2, 64);
+    h1 += __shfl_xor(h1, 1, 64);
+    if ((lane & 7) == 0) {
+      const int q = 4 * b5 + 2 * b4 + b3;
+      const int p = pg + q;
+      if (p < T) {
+        const size_t ix = rb + p;
+        if (p < len) {
+          const float ap = a[ix];
+          de_out[ix] = ap * (da[ix] - S);
+          if (dcov_out) {
+            float r = h1 + (dcov_next ? dcov_next[ix] : 0.f);
+            if (gcl && ap > (cov ? cov[ix] : 0.f)) r += g;
+            dcov_out[ix] = r;
+          }
+        } else {
+          de_out[ix] = 0.f;
+          if (dcov_out) dcov_out[ix] = dcov_next ? dcov_next[ix] : 0.f;
+        }
       }
     }
   }
+#pragma unroll
   for (int kb = 0; kb < NK; ++kb) {
     const int k0 = kb * 512 + lane * 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (k0 + j < A) part[wid][k0 + j] = acc[kb][j];
+    for (int j = 0; j < 8; ++j) part[wid][kb * 512 + lane * 8 + j] = (k0 + j < A) ? acc[kb][j] : 0.f;
   }
   __syncthreads();
-  float* out = dsp + ((size_t)b * gridDim.x + blockIdx.x) * A;
-  for (int k = tid; k < A; k += 256) out[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+  float* out = ds + (size_t)b * A;
+  for (int k = tid; k < A; k += 256) {
+    const float x = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+    atomicAdd(out + k, x);
+  }
 }
 
 // ------------------------------------------------------ post-loop: dF, dv, dw_c
 // dF[b,i,k] = sum_t de[t,b,i] v_k sech2(u_tik); dv_k = sum de tanh(u); dwc_k = sum de v_k sech2 cov.
-// Each wave keeps 8 positions x 8 features of dF in registers across all D steps.
+// Lanes on features (8 per lane), each wave keeps 4 positions x 8 features of dF in
+// registers across all D steps; de / cov are wave-uniform scalar loads.
 __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
     const bf16* __restrict__ F, const float* __restrict__ S_all, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov_all, const float* __restrict__ de_all,
@@ -280,7 +329,7 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
   const int kbase = blockIdx.z * 512;
   const int k0 = kbase + lane * 8;
   const bool kok = k0 < A;
-  const int p0 = blockIdx.x * 32 + wid * 8;
+  const int p0 = blockIdx.x * 16 + wid * 4;
   float vk[8], wk[8], adv[8], adw[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -291,9 +340,10 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
     adw[j] = 0.f;
   }
   if (p0 < len && kok) {
-    const int np = min(8, len - p0);
-    float f[8][8], acc[8][8];
-    for (int q = 0; q < 8; ++q) {
+    const int np = min(4, len - p0);
+    float f[4][8], acc[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
       const int p = min(p0 + q, T - 1);
       bf16x8 x = ld8(F + ((size_t)b * T + p) * A + k0);
 #pragma unroll
@@ -304,12 +354,12 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
     }
     for (int t = 0; t < D; ++t) {
       const float* st = S_all + ((size_t)t * B + b) * A + k0;
-      float sk[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sk[j] = st[j];
+      const float4 s0 = *reinterpret_cast<const float4*>(st);
+      const float4 s1 = *reinterpret_cast<const float4*>(st + 4);
+      const float sk[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
       const size_t rb = ((size_t)t * B + b) * T + p0;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < 4; ++q) {
         if (q < np) {
           const float de = de_all[rb + q];
           const float c = cov_all ? cov_all[rb + q] : 0.f;
@@ -324,11 +374,13 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
         }
       }
     }
-    for (int q = 0; q < np; ++q) {
-      float* o = dF + ((size_t)b * T + p0 + q) * A + k0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (k0 + j < A) o[j] = acc[q][j];
+    for (int q = 0; q < 4; ++q) {
+      if (q < np) {
+        float* o = dF + ((size_t)b * T + p0 + q) * A + k0;
+        *reinterpret_cast<float4*>(o) = make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(acc[q][4], acc[q][5], acc[q][6], acc[q][7]);
+      }
     }
   }
 #pragma unroll
@@ -348,10 +400,10 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
   }
 }
 
-void launch_attn_score(const bf16* F, const float* s, const float* v, const float* wc, const float* cov,
+void launch_attn_score(const bf16* Ft, const float* s, const float* v, const float* wc, const float* cov,
                        const int* lens, float* e, int B, int T, int A, hipStream_t st) {
-  dim3 grid((T + POS_PER_BLOCK - 1) / POS_PER_BLOCK, B);
-  hipLaunchKernelGGL(attn_score_kernel, grid, dim3(256), 0, st, F, s, v, wc, cov, lens, e, T, A);
+  dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B);
+  hipLaunchKernelGGL(attn_score_kernel, grid, dim3(256), 0, st, Ft, s, v, wc, cov, lens, e, T, A);
 }
 void launch_attn_softmax_ctx(const float* e, const bf16* E, const int* lens, const float* cov, float* a_out,
                              float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A,
@@ -360,25 +412,29 @@ void launch_attn_softmax_ctx(const float* e, const bf16* E, const int* lens, con
   hipLaunchKernelGGL(attn_softmax_ctx_kernel, grid, dim3(256), 0, st, e, E, lens, cov, a_out, cov_out, covloss, ctx,
                      ctx_bf, T, A);
 }
-void launch_attn_bwd_da(const bf16* E, const float* dctx, const float* Ga, const float* dcov_next, const float* a,
+void launch_attn_bwd_da(const bf16* Et, const float* dctx, const float* Ga, const float* dcov_next, const float* a,
                         const float* cov, const float* gcl, const int* lens, float* da, int B, int T, int A,
                         hipStream_t st) {
-  dim3 grid((T + POS_PER_BLOCK - 1) / POS_PER_BLOCK, B);
-  hipLaunchKernelGGL(attn_bwd_da_kernel, grid, dim3(256), 0, st, E, dctx, Ga, dcov_next, a, cov, gcl, lens, da, T,
+  dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B);
+  hipLaunchKernelGGL(attn_bwd_da_kernel, grid, dim3(256), 0, st, Et, dctx, Ga, dcov_next, a, cov, gcl, lens, da, T,
                      A);
 }
-int attn_nchunk(int T) { return (T + POS_PER_BLOCK - 1) / POS_PER_BLOCK; }
+int attn_nchunk(int T) { return (T + 63) / 64; }
 void launch_attn_bwd_tanh(const bf16* F, const float* s, const float* v, const float* wc, const float* cov,
                           const float* a, const float* da, const float* dcov_next, const float* gcl, const int* lens,
-                          float* de_out, float* dsp, float* dcov_out, int B, int T, int A, hipStream_t st) {
+                          float* de_out, float* ds, float* dcov_out, int B, int T, int A, hipStream_t st) {
   dim3 grid(attn_nchunk(T), B);
-  hipLaunchKernelGGL(attn_bwd_tanh_kernel, grid, dim3(256), 0, st, F, s, v, wc, cov, a, da, dcov_next, gcl, lens,
-                     de_out, dsp, dcov_out, T, A);
+  if (A <= 512)
+    hipLaunchKernelGGL(attn_bwd_tanh_kernel<1>, grid, dim3(256), 0, st, F, s, v, wc, cov, a, da, dcov_next, gcl, lens,
+                       de_out, ds, dcov_out, T, A);
+  else
+    hipLaunchKernelGGL(attn_bwd_tanh_kernel<2>, grid, dim3(256), 0, st, F, s, v, wc, cov, a, da, dcov_next, gcl, lens,
+                       de_out, ds, dcov_out, T, A);
 }
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, float* dF, float* dv, float* dwc, int D, int B, int T,
                           int A, hipStream_t st) {
-  dim3 grid((T + 31) / 32, B, (A + 511) / 512);
+  dim3 grid((T + 15) / 16, B, (A + 511) / 512);
   hipLaunchKernelGGL(attn_bwd_feat_kernel, grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF, dv,
                      dwc, D, B, T, A);
 }

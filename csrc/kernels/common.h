@@ -9,6 +9,10 @@
 //  * Weight operands are stored "Bt" = [N][K] with K contiguous, so both A and B
 //    fragments are one 16-byte load per lane straight from L2 (M <= a few hundred,
 //    the operands are L2-resident and re-read every step of a recurrence).
+//  * Recurrence GEMMs are latency-bound (a few MFLOP per step): each block's 4 waves
+//    split K, every wave issues ALL of its fragment loads before its first MFMA (one
+//    L2 round trip instead of K/32 dependent ones), and the 4 partial tiles are summed
+//    through LDS.  See kslice_mma / ksplit_reduce.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -27,6 +31,16 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8 a, const bf16x8 b, f32x4 c)
 }
 
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// 8 fp32 -> one bf16x8 fragment (A operand taken from an fp32 activation).
+__device__ __forceinline__ bf16x8 ld8f(const float* p) {
+  const float4 x = *reinterpret_cast<const float4*>(p);
+  const float4 y = *reinterpret_cast<const float4*>(p + 4);
+  bf16x8 r;
+  r[0] = f2bf(x.x); r[1] = f2bf(x.y); r[2] = f2bf(x.z); r[3] = f2bf(x.w);
+  r[4] = f2bf(y.x); r[5] = f2bf(y.y); r[6] = f2bf(y.z); r[7] = f2bf(y.w);
+  return r;
+}
 
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 z;
@@ -87,6 +101,53 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 __device__ __forceinline__ f32x4 mfma_k(const bf16* a_row, const bf16* b_row, int K, f32x4 acc) {
   for (int k = 0; k < K; k += 32) acc = mfma16(ld8(a_row + k), ld8(b_row + k), acc);
   return acc;
+}
+
+// K-slice of NB tiles that share the A fragment: acc[j] += A[:, k0:k1] . Bt_j[:, k0:k1].
+// Loads are issued in batches of 4 k-steps before the MFMAs of the batch; a batch step
+// past k1 loads a valid (clamped) address and is zeroed, so the code is branch-free.
+// a(k) / b(j, k): pointers for this lane at absolute k (must include the 8*(l>>4) offset).
+template <int NB, typename FA, typename FB>
+__device__ __forceinline__ void kslice_mma(FA a, FB b, int k0, int k1, f32x4 (&acc)[NB]) {
+  for (int k = k0; k < k1; k += 128) {
+    bf16x8 af[4];
+    bf16x8 bfr[NB][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = k + 32 * i;
+      const int kc = kk < k1 ? kk : k0;
+      af[i] = a(kc);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) bfr[j][i] = b(j, kc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (k + 32 * i < k1) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = mfma16(af[i], bfr[j][i], acc[j]);
+      }
+    }
+  }
+}
+
+// Sum NB tiles across the 4 waves of a 256-thread block.  red: >= 4*NB*256 floats of LDS.
+// Afterwards wave w owns accumulator register r = w of every tile: lane l holds the
+// full sum for C[row = (l>>4)*4 + w][col = l&15] of tile j in out[j].
+template <int NB>
+__device__ __forceinline__ void ksplit_reduce(const f32x4 (&acc)[NB], float* red, float (&out)[NB]) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[((w * NB + j) * 4 + r) * 64 + l] = acc[j][r];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int src = 0; src < 4; ++src) s += red[((src * NB + j) * 4 + w) * 64 + l];
+    out[j] = s;
+  }
 }
 
 #define HIP_LAUNCH_CHECK() (void)0

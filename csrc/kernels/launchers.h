@@ -20,22 +20,21 @@ void launch_attn_bwd_da(const bf16* E, const float* dctx, const float* Ga, const
 int attn_nchunk(int T);
 void launch_attn_bwd_tanh(const bf16* F, const float* s, const float* v, const float* wc, const float* cov,
                           const float* a, const float* da, const float* dcov_next, const float* gcl, const int* lens,
-                          float* de_out, float* dsp, float* dcov_out, int B, int T, int A, hipStream_t st);
+                          float* de_out, float* ds, float* dcov_out, int B, int T, int A, hipStream_t st);
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, float* dF, float* dv, float* dwc, int D, int B, int T,
                           int A, hipStream_t st);
 
-void launch_dec_xcell_fwd(const float* xe, const bf16* ctxp, const bf16* WicT, const bf16* WcT, const float* bc,
-                          const bf16* hprev, const float* cprev, float* x_out, bf16* xb_out, float* c_out,
-                          bf16* cb_out, bf16* hb_out, float* act, int B, int E, int H, int A, hipStream_t st);
+void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
+                         float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st);
 void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out, int B, int H,
                       int A, hipStream_t st);
-void launch_dec_bwd_cell(const float* dsp, int nchunk, const bf16* Ws, const float* dC_dir, const float* dH_dir,
+void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,
-                         const float* c_prev, float* ds_out, bf16* dz, int B, int H, int A, hipStream_t st);
-void launch_dec_bwd_dz(const bf16* dz, const bf16* Wc, const bf16* Wic, const float* dX_dir,
-                       const float* dCTX_dir_prev, float* dx_out, float* dctx_prev_out, float* dh_rec, int B, int E,
-                       int H, int A, hipStream_t st);
+                         const float* c_prev, bf16* dz, int B, int H, int A, hipStream_t st);
+void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, const float* dCTX_dir_prev,
+                       float* dx_out, float* dctx_prev_out, float* dh_rec, int B, int E, int H, int A,
+                       hipStream_t st);
 
 void launch_ptr_loss(const float* logits, const float* bias, const int* target, const float* rowg, const float* pgen, const float* attn,
                      const int* ext, const int* lens, float* loss_row, bf16* dlogits, float* dpre, float* dA, int N,

@@ -1,10 +1,12 @@
 // Bidirectional LSTM encoder recurrence (reference model.py:76-94, TF LSTMCell).
 //
-// One launch per time step runs BOTH directions (fw on blockIdx.z==0, bw on 1); the
-// launches are captured into one hipGraph by the caller, so the per-step cost is the
-// dependent-kernel boundary (~1.5 us, MI355X_MICROARCH "boundary") plus one small MFMA
-// GEMM: h_{s-1}[B,H] x W_hh[H,4H].  The input projection x.W_x + b for all T steps is
-// hoisted out of the recurrence into one big GEMM (gx), as is every weight gradient.
+// One launch per time step runs BOTH directions (blockIdx.z = direction); the launches
+// are captured into one hipGraph by the caller, so a step costs the dependent-kernel
+// boundary (~1.5 us, MI355X_MICROARCH "boundary") plus one L2 round trip: each block
+// owns a 16-row x 16-unit tile of all four gates, its 4 waves split the K = H reduction
+// (all fragment loads issued up front, kslice_mma), and the partial tiles are summed in
+// LDS.  The input projection x.W_x + b for all T steps is hoisted out of the recurrence
+// into one big GEMM (gx), as is every weight gradient.
 //
 // Layout ("step frame"): the bw direction consumes x reversed within each sequence
 // length (TF ReverseSequence), so step s of direction d reads gx[d][s] for every row,
@@ -15,8 +17,6 @@
 // Gate order i, j, f, o (TF LSTMCell), forget_bias = 1.0 added at runtime.
 #include "common.h"
 
-// Each wave owns a 16-row x 16-unit tile and computes the 4 gate tiles of those units,
-// so the whole cell update stays in registers.  Block = 4 waves = 64 units.
 __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
     const float* __restrict__ gx,     // [2][T][B][4H]  x.W_x + b (step frame)
     const bf16* __restrict__ Wt,      // [2][4H][H]     W_hh^T
@@ -25,55 +25,57 @@ __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
     float* __restrict__ acts,         // [2][T][B][4H]  sig(i) tanh(j) sig(f+1) sig(o)
     bf16* __restrict__ out,           // [B][T][2H]
     const int* __restrict__ lens, int s, int T, int B, int H) {
+  __shared__ float red[4 * 4 * 256];
   const int d = blockIdx.z;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int u0 = (blockIdx.x * 4 + wid) * 16;
-  const int r0 = blockIdx.y * 16;
-  if (u0 >= H) return;
+  const int u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
   const size_t BH = (size_t)B * H, G = 4 * (size_t)H;
+  // ---- prefetch this lane's epilogue operands (independent of the GEMM)
+  const int r = r0 + (lane >> 4) * 4 + wid, u = u0 + (lane & 15);
+  const bool rok = r < B;
+  const int len = rok ? lens[r] : 0;
+  const bool active = s < len;
+  const float* gxs = gx + ((size_t)d * T + s) * B * G + (size_t)(rok ? r : 0) * G;
+  const bf16* hprev = hs + ((size_t)d * (T + 1) + s) * BH;
+  const float* cprev = cs + ((size_t)d * (T + 1) + s) * BH;
+  const size_t ri = (size_t)(rok ? r : 0) * H + u;
+  float gz[4] = {0, 0, 0, 0}, cp = 0.f;
+  if (active) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) gz[g] = gxs[g * H + u];
+  }
+  if (rok) cp = cprev[ri];
+  // ---- h_{s-1} . W_hh, K split over the 4 waves
   const int ar = min(r0 + (lane & 15), B - 1);
   const int kof = 8 * (lane >> 4);
-  const bf16* hprev = hs + ((size_t)d * (T + 1) + s) * BH;
   const bf16* arow = hprev + (size_t)ar * H + kof;
-  const bf16* W = Wt + (size_t)d * G * H;
+  const bf16* W = Wt + (size_t)d * G * H + (size_t)(u0 + (lane & 15)) * H + kof;
+  const int nst = H / 32;
+  const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
   f32x4 acc[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) acc[g] = f32x4{0, 0, 0, 0};
-  for (int k = 0; k < H; k += 32) {
-    bf16x8 a = ld8(arow + k);
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-      acc[g] = mfma16(a, ld8(W + ((size_t)g * H + u0 + (lane & 15)) * H + kof + k), acc[g]);
-  }
-  const int u = u0 + (lane & 15);
-  const float* gxs = gx + ((size_t)d * T + s) * B * G;
-  const float* cprev = cs + ((size_t)d * (T + 1) + s) * BH;
+  kslice_mma<4>([&](int k) { return ld8(arow + k); }, [&](int g, int k) { return ld8(W + (size_t)g * H * H + k); },
+                k0, k1, acc);
+  float z[4];
+  ksplit_reduce<4>(acc, red, z);
+  if (!rok) return;
   float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
   bf16* hnext = hs + ((size_t)d * (T + 1) + s + 1) * BH;
-  float* act = acts + ((size_t)d * T + s) * B * G;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int r = r0 + (lane >> 4) * 4 + j;
-    if (r >= B) continue;
-    const int len = lens[r];
-    const size_t ri = (size_t)r * H + u;
-    if (s < len) {
-      const float* gr = gxs + (size_t)r * G;
-      float zi = acc[0][j] + gr[u], zj = acc[1][j] + gr[H + u];
-      float zf = acc[2][j] + gr[2 * H + u], zo = acc[3][j] + gr[3 * H + u];
-      float ig = fsigmoid(zi), jg = ftanh(zj), fg = fsigmoid(zf + 1.0f), og = fsigmoid(zo);
-      float c = fg * cprev[ri] + ig * jg;
-      float h = og * ftanh(c);
-      cnext[ri] = c;
-      hnext[ri] = f2bf(h);
-      float* ar4 = act + (size_t)r * G;
-      ar4[u] = ig; ar4[H + u] = jg; ar4[2 * H + u] = fg; ar4[3 * H + u] = og;
-      const int t = d == 0 ? s : len - 1 - s;
-      out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(h);
-    } else {
-      cnext[ri] = cprev[ri];
-      hnext[ri] = hprev[ri];
-    }
+  if (active) {
+    const float ig = fsigmoid(z[0] + gz[0]), jg = ftanh(z[1] + gz[1]);
+    const float fg = fsigmoid(z[2] + gz[2] + 1.0f), og = fsigmoid(z[3] + gz[3]);
+    const float c = fg * cp + ig * jg;
+    const float h = og * ftanh(c);
+    cnext[ri] = c;
+    hnext[ri] = f2bf(h);
+    float* a4 = acts + ((size_t)d * T + s) * B * G + (size_t)r * G;
+    a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
+    const int t = d == 0 ? s : len - 1 - s;
+    out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(h);
+  } else {
+    cnext[ri] = cp;
+    hnext[ri] = hprev[ri];
   }
 }
 
@@ -91,64 +93,71 @@ __global__ __launch_bounds__(256) void lstm_enc_bwd_step_kernel(
     float* __restrict__ dc_carry,     // [2][B][H]
     const float* __restrict__ acts, const float* __restrict__ cs,
     const int* __restrict__ lens, int s, int T, int B, int H) {
+  __shared__ float red[4 * 256];
   const int d = blockIdx.z;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int u0 = (blockIdx.x * 4 + wid) * 16;
-  const int r0 = blockIdx.y * 16;
-  if (u0 >= H) return;
+  const int u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
   const size_t BH = (size_t)B * H, G = 4 * (size_t)H;
-  f32x4 acc = {0, 0, 0, 0};
+  // ---- prefetch epilogue operands
+  const int r = r0 + (lane >> 4) * 4 + wid, u = u0 + (lane & 15);
+  const bool rok = r < B;
+  const int len = rok ? lens[r] : 0;
+  const bool active = s < len;
+  const size_t ri = (size_t)(rok ? r : 0) * H + u;
+  float dh = 0.f, dcin = 0.f, a4[4] = {0, 0, 0, 0}, cn = 0.f, cpv = 0.f;
+  if (active) {
+    const int t = d == 0 ? s : len - 1 - s;
+    dh = dout[((size_t)r * T + t) * 2 * H + d * H + u];
+    if (s + 1 >= len) dh += dh_fin[(size_t)d * BH + ri];
+    const float* ap = acts + ((size_t)d * T + s) * B * G + (size_t)r * G;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) a4[g] = ap[g * H + u];
+    cn = cs[((size_t)d * (T + 1) + s + 1) * BH + ri];
+    cpv = cs[((size_t)d * (T + 1) + s) * BH + ri];
+    dcin = dc_carry[(size_t)d * BH + ri];
+  }
+  // ---- dz_{s+1} . W_hh^T, K = 4H split over the 4 waves
+  f32x4 acc[1] = {f32x4{0, 0, 0, 0}};
   if (s + 1 < T) {
     const int ar = min(r0 + (lane & 15), B - 1);
     const int kof = 8 * (lane >> 4);
     const bf16* arow = dz + (((size_t)d * T + s + 1) * B + ar) * G + kof;
     const bf16* brow = Wn + ((size_t)d * H + u0 + (lane & 15)) * G + kof;
-    acc = mfma_k(arow, brow, (int)G, acc);
+    const int nst = (int)(G / 32);
+    const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
+    kslice_mma<1>([&](int k) { return ld8(arow + k); }, [&](int, int k) { return ld8(brow + k); }, k0, k1, acc);
   }
-  const int u = u0 + (lane & 15);
-  const float* act = acts + ((size_t)d * T + s) * B * G;
-  const float* cprev = cs + ((size_t)d * (T + 1) + s) * BH;
-  const float* cnow = cs + ((size_t)d * (T + 1) + s + 1) * BH;
-  bf16* dzs = dz + ((size_t)d * T + s) * B * G;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int r = r0 + (lane >> 4) * 4 + j;
-    if (r >= B) continue;
-    const int len = lens[r];
-    const size_t ri = (size_t)r * H + u;
-    bf16* dzr = dzs + (size_t)r * G;
-    if (s < len) {
-      const int t = d == 0 ? s : len - 1 - s;
-      float dh = acc[j] + dout[((size_t)r * T + t) * 2 * H + d * H + u];
-      if (s + 1 >= len) dh += dh_fin[(size_t)d * BH + ri];
-      const float* a4 = act + (size_t)r * G;
-      const float ig = a4[u], jg = a4[H + u], fg = a4[2 * H + u], og = a4[3 * H + u];
-      const float c = cnow[ri];
-      const float tc = ftanh(c);
-      float dc = dc_carry[(size_t)d * BH + ri] + dh * og * (1.0f - tc * tc);
-      const float dzo = dh * tc * og * (1.0f - og);
-      const float dzi = dc * jg * ig * (1.0f - ig);
-      const float dzj = dc * ig * (1.0f - jg * jg);
-      const float dzf = dc * cprev[ri] * fg * (1.0f - fg);
-      dc_carry[(size_t)d * BH + ri] = dc * fg;
-      dzr[u] = f2bf(dzi); dzr[H + u] = f2bf(dzj); dzr[2 * H + u] = f2bf(dzf); dzr[3 * H + u] = f2bf(dzo);
-    } else {
-      const bf16 z = f2bf(0.f);
-      dzr[u] = z; dzr[H + u] = z; dzr[2 * H + u] = z; dzr[3 * H + u] = z;
-    }
+  float rec[1];
+  ksplit_reduce<1>(acc, red, rec);
+  if (!rok) return;
+  bf16* dzr = dz + (((size_t)d * T + s) * B + r) * G;
+  if (active) {
+    dh += rec[0];
+    const float ig = a4[0], jg = a4[1], fg = a4[2], og = a4[3];
+    const float tc = ftanh(cn);
+    const float dc = dcin + dh * og * (1.0f - tc * tc);
+    const float dzo = dh * tc * og * (1.0f - og);
+    const float dzi = dc * jg * ig * (1.0f - ig);
+    const float dzj = dc * ig * (1.0f - jg * jg);
+    const float dzf = dc * cpv * fg * (1.0f - fg);
+    dc_carry[(size_t)d * BH + ri] = dc * fg;
+    dzr[u] = f2bf(dzi); dzr[H + u] = f2bf(dzj); dzr[2 * H + u] = f2bf(dzf); dzr[3 * H + u] = f2bf(dzo);
+  } else {
+    const bf16 zz = f2bf(0.f);
+    dzr[u] = zz; dzr[H + u] = zz; dzr[2 * H + u] = zz; dzr[3 * H + u] = zz;
   }
 }
 
 void launch_lstm_enc_fwd_step(const float* gx, const bf16* Wt, bf16* hs, float* cs, float* acts, bf16* out,
                               const int* lens, int s, int T, int B, int H, hipStream_t st) {
-  dim3 grid((H + 63) / 64, (B + 15) / 16, 2);
+  dim3 grid(H / 16, (B + 15) / 16, 2);
   hipLaunchKernelGGL(lstm_enc_fwd_step_kernel, grid, dim3(256), 0, st, gx, Wt, hs, cs, acts, out, lens, s, T, B, H);
 }
 
 void launch_lstm_enc_bwd_step(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                               const float* acts, const float* cs, const int* lens, int s, int T, int B, int H,
                               hipStream_t st) {
-  dim3 grid((H + 63) / 64, (B + 15) / 16, 2);
+  dim3 grid(H / 16, (B + 15) / 16, 2);
   hipLaunchKernelGGL(lstm_enc_bwd_step_kernel, grid, dim3(256), 0, st, dz, Wn, dout, dh_fin, dc_carry, acts, cs,
                      lens, s, T, B, H);
 }

@@ -109,6 +109,9 @@ class HipPointerGenerator:
                 "dc_carry": z(2, B, H),
             })
         w["F"] = z(B, T, A, dt=BF)
+        w["Ft"] = z(B, A, T, dt=BF)   # transposed copies for the lanes-over-positions kernels
+        w["Et"] = z(B, A, T, dt=BF)
+        w["XG"] = z(D, B, 4 * H)
         # decoder forward state
         w["xe"] = z(D, B, E)
         w["X"] = z(D, B, E)
@@ -138,7 +141,6 @@ class HipPointerGenerator:
         w["DS"] = z(D, B, A)
         w["DE"] = z(D, B, T)
         w["da"] = z(B, T)
-        w["dsp"] = z(B, self.nchunk, A)
         w["dcov"] = z(2, B, T)
         w["dh_rec"] = z(B, H)
         w["dc_carry"] = z(B, H)
@@ -178,8 +180,11 @@ class HipPointerGenerator:
         put("lin_emb", M[:E])
         put("Wic", M[E:])
         put("WicT", M[E:].t())
-        put("Wc", p[CELL_K])
-        put("WcT", p[CELL_K].t())
+        K = p[CELL_K]
+        Wcomb = M[E:] @ K[:E]                      # [A][4H]: ctx_{t-1} -> z through x_t
+        put("cell_x", K[:E])
+        put("WcT2", torch.cat([Wcomb, K[E:]], 0).t())  # [4H][A+H]
+        put("Wbig", torch.cat([K, Wcomb], 0))          # [E+H+A][4H]
         put("Ws", p[ATT_M])
         put("WsT", p[ATT_M].t())
         put("OUTm", p[OUT_M])
@@ -257,25 +262,33 @@ class HipPointerGenerator:
         w["Cb"][0].copy_(c0)
         w["Hb"][0].copy_(h0)
         w["F"].view(B * T, A).copy_(torch.mm(top["out"].view(B * T, A), self.pk["Wh"]))
+        w["Ft"].copy_(w["F"].transpose(1, 2))
+        w["Et"].copy_(top["out"].transpose(1, 2))
 
     def _decoder_forward(self):
         k, w, hps = self.k, self.w, self.hps
         B, T, D, E, H, A = self.B, self.T, self.D, self.E, self.H, self.A
         cov = hps.coverage
         emb_dec = self.pk["emb"][w["dec_batch_t"]].view(D * B, E)
-        w["xe"].view(D * B, E).copy_(mmf(emb_dec, self.pk["lin_emb"])).add_(self.p[LIN_B])
+        xe = w["xe"].view(D * B, E)
+        xe.copy_(mmf(emb_dec, self.pk["lin_emb"])).add_(self.p[LIN_B])
+        w["XG"].view(D * B, 4 * H).copy_(mmf(xe.to(BF), self.pk["cell_x"])).add_(self.p[CELL_B])
         self._emb_dec = emb_dec
-        enc_out, lens, F = self.enc[-1]["out"], w["enc_lens"], w["F"]
+        enc_out, lens, Ft = self.enc[-1]["out"], w["enc_lens"], w["Ft"]
         v, wc = self.f32["v"], self.f32["wc"]
         for t in range(D):
-            k.dec_xcell_fwd(w["xe"][t], w["CTXb"][t - 1] if t > 0 else None, self.pk["WicT"], self.pk["WcT"],
-                            self.p[CELL_B], w["Hb"][t], w["Cst"][t], w["X"][t], w["Xb"][t], w["Cst"][t + 1],
-                            w["Cb"][t + 1], w["Hb"][t + 1], w["ACT"][t], B, E, H, A)
+            k.dec_cell_fwd(w["XG"][t], w["CTXb"][t - 1] if t > 0 else None, w["Hb"][t], w["Cst"][t], self.pk["WcT2"],
+                           w["Cst"][t + 1], w["Cb"][t + 1], w["Hb"][t + 1], w["ACT"][t], B, H, A)
             k.dec_sproj(w["Cb"][t + 1], w["Hb"][t + 1], self.pk["WsT"], self.p[ATT_B], w["S"][t], B, H, A)
             cov_in = w["COV"][t] if (cov and t > 0) else None
-            k.attn_score(F, w["S"][t], v, wc, cov_in, lens, w["e"], B, T, A)
+            k.attn_score(Ft, w["S"][t], v, wc, cov_in, lens, w["e"], B, T, A)
             k.attn_softmax_ctx(w["e"], enc_out, lens, cov_in, w["ATT"][t], w["COV"][t + 1] if cov else None,
                                w["covloss"][t] if cov else None, w["CTX"][t], w["CTXb"][t], B, T, A)
+        # x_t = xe_t + ctx_{t-1} . W_in[E:]  (rebuilt after the loop, one GEMM)
+        w["X"].copy_(w["xe"])
+        if D > 1:
+            w["X"][1:].view((D - 1) * B, E).add_(mmf(w["CTXb"][:D - 1].reshape((D - 1) * B, A), self.pk["Wic"]))
+        w["Xb"].copy_(w["X"])
 
     def _head_forward(self, need_grad: bool):
         w, hps, p = self.w, self.hps, self.p
@@ -355,26 +368,29 @@ class HipPointerGenerator:
             dC_dir = (dp * pm[A:A + H]).contiguous()
             dH_dir.add_(dp * pm[A + H:A + 2 * H])
             dX_dir = (dp * pm[A + 2 * H:]).contiguous()
+        if dX_dir is not None and D > 1:  # p_gen path into ctx_{t-1} through x_t (hoisted out of the loop)
+            dCTX_dir[:D - 1].view((D - 1) * B, A).add_(dX_dir[1:].view((D - 1) * B, E) @ p[LIN_M][E:].t())
         # ---- decoder reverse loop
-        enc_out, lens, F = self.enc[-1]["out"], w["enc_lens"], w["F"]
+        enc_out, lens, F, Et = self.enc[-1]["out"], w["enc_lens"], w["F"], w["Et"]
         v, wc = self.f32["v"], self.f32["wc"]
         w["DCTX"][D - 1].copy_(dCTX_dir[D - 1])
         w["dh_rec"].zero_()
         w["dc_carry"].zero_()
         dcov = w["dcov"]
+        w["DS"].zero_()
         Ga = w["dA"] if hps.pointer_gen else None
         for t in reversed(range(D)):
             dcov_next = dcov[(t + 1) % 2] if (cov and t < D - 1) else None
             cov_t = w["COV"][t] if (cov and t > 0) else None
             gcl_t = w["gcl"][t] if cov else None
-            k.attn_bwd_da(enc_out, w["DCTX"][t], Ga[t] if Ga is not None else None, dcov_next, w["ATT"][t], cov_t,
+            k.attn_bwd_da(Et, w["DCTX"][t], Ga[t] if Ga is not None else None, dcov_next, w["ATT"][t], cov_t,
                           gcl_t, lens, w["da"], B, T, A)
             k.attn_bwd_tanh(F, w["S"][t], v, wc, cov_t, w["ATT"][t], w["da"], dcov_next, gcl_t, lens, w["DE"][t],
-                            w["dsp"], dcov[t % 2] if cov else None, B, T, A)
-            k.dec_bwd_cell(w["dsp"], self.nchunk, self.pk["Ws"], dC_dir[t] if dC_dir is not None else None,
+                            w["DS"][t], dcov[t % 2] if cov else None, B, T, A)
+            k.dec_bwd_cell(w["DS"][t], self.pk["Ws"], dC_dir[t] if dC_dir is not None else None,
                            dH_dir[t], w["dh_rec"], w["dc_carry"], w["ACT"][t], w["Cst"][t + 1], w["Cst"][t],
-                           w["DS"][t], w["DZ"][t], B, H, A)
-            k.dec_bwd_dz(w["DZ"][t], self.pk["Wc"], self.pk["Wic"], dX_dir[t] if dX_dir is not None else None,
+                           w["DZ"][t], B, H, A)
+            k.dec_bwd_dz(w["DZ"][t], self.pk["Wbig"], dX_dir[t] if dX_dir is not None else None,
                          dCTX_dir[t - 1] if t > 0 else None, w["DX"][t], w["DCTX"][t - 1] if t > 0 else None,
                          w["dh_rec"], B, E, H, A)
         # ---- decoder weight gradients (one GEMM each over all D*B rows)
