@@ -10,7 +10,7 @@
 //  * row-major F/E [B][T][A] -- lanes on the feature axis (8 bf16 = one 16-B load);
 //  * transposed Ft/Et [B][A][T] -- lanes on the position axis, so the score e_i and
 //    da_i = dctx . E_i reduce over k inside a lane (no cross-lane reduction at all), the
-//    per-k parameters (s_k, v_k, w_c_k, dctx_k) are wave-uniform scalar loads, and the 4
+//    per-k parameters (s_k, v_k, w_c_k, dctx_k) are wave-uniform scalar loads, and the 8
 //    waves of a block split the k axis (summed once in LDS).
 // The v / w_c / F gradients are NOT accumulated per step: the backward step stores
 // de_t, and attn_bwd_feat recomputes tanh once over all steps after the loop.  The
@@ -19,45 +19,70 @@
 #include "common.h"
 
 #define SCORE_POS 128  // positions per block in the lanes-over-positions kernels (2 per lane)
+#define SCORE_WAVES 8  // waves per block; each takes A/8 of the feature axis
+
+__device__ __forceinline__ float lo_bf(uint32_t r) { return __uint_as_float(r << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t r) { return __uint_as_float(r & 0xffff0000u); }
+__device__ __forceinline__ float rdlane(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
 
 // ---------------------------------------------------------------- forward: scores
-// grid (ceil(T/128), B).  Ft: [B][A][T] bf16, T even.
-__global__ __launch_bounds__(256) void attn_score_kernel(
+// grid (ceil(T/128), B), 512 threads.  Ft: [B][A][T] bf16, T even.  Each lane owns 2
+// positions; the 8 waves split the feature axis; per 8-feature batch all 8 Ft loads
+// are issued before the tanh work and s/v/w_c come in as scalar (s_load) vectors.
+__global__ __launch_bounds__(512) void attn_score_kernel(
     const bf16* __restrict__ Ft, const float* __restrict__ s, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov, const int* __restrict__ lens,
     float* __restrict__ e, int T, int A) {
-  __shared__ float red[4][SCORE_POS];
+  __shared__ float red[SCORE_WAVES][SCORE_POS];
   const int b = blockIdx.y;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int len = lens[b];
   const int pb = blockIdx.x * SCORE_POS;
   if (pb >= len) return;  // uniform: masked positions are never read by the softmax
   const int p = pb + 2 * lane;
-  const bool ok = p < T;
-  const int pc = ok ? p : 0;
+  const int pc = p < T ? p : 0;
   float c0 = 0.f, c1 = 0.f;
-  if (cov && ok) {
-    c0 = cov[(size_t)b * T + pc];
-    c1 = cov[(size_t)b * T + pc + 1];
+  if (cov) {
+    const float2 cc = *reinterpret_cast<const float2*>(cov + (size_t)b * T + pc);
+    c0 = cc.x; c1 = cc.y;
   }
-  const int ka = wid * (A / 4), kb = ka + A / 4;
+  const int ka = wid * (A / SCORE_WAVES), kb = ka + A / SCORE_WAVES;
   const bf16* fp = Ft + ((size_t)b * A) * T + pc;
   const float* sb = s + (size_t)b * A;
   float e0 = 0.f, e1 = 0.f;
-#pragma unroll 8
-  for (int k = ka; k < kb; ++k) {
-    const uint32_t raw = *reinterpret_cast<const uint32_t*>(fp + (size_t)k * T);
-    const float f0 = __uint_as_float(raw << 16), f1 = __uint_as_float(raw & 0xffff0000u);
-    const float sk = sb[k], vk = v[k], wk = wc ? wc[k] : 0.f;
-    e0 += vk * ftanh(f0 + sk + wk * c0);
-    e1 += vk * ftanh(f1 + sk + wk * c1);
+  for (int k = ka; k < kb; k += 8) {
+    uint32_t raw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) raw[i] = *reinterpret_cast<const uint32_t*>(fp + (size_t)(k + i) * T);
+    float sk[8], vk[8], wk[8];
+    *reinterpret_cast<float4*>(sk) = *reinterpret_cast<const float4*>(sb + k);
+    *reinterpret_cast<float4*>(sk + 4) = *reinterpret_cast<const float4*>(sb + k + 4);
+    *reinterpret_cast<float4*>(vk) = *reinterpret_cast<const float4*>(v + k);
+    *reinterpret_cast<float4*>(vk + 4) = *reinterpret_cast<const float4*>(v + k + 4);
+    if (wc) {
+      *reinterpret_cast<float4*>(wk) = *reinterpret_cast<const float4*>(wc + k);
+      *reinterpret_cast<float4*>(wk + 4) = *reinterpret_cast<const float4*>(wc + k + 4);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) wk[i] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      e0 += vk[i] * ftanh(lo_bf(raw[i]) + sk[i] + wk[i] * c0);
+      e1 += vk[i] * ftanh(hi_bf(raw[i]) + sk[i] + wk[i] * c1);
+    }
   }
   red[wid][2 * lane] = e0;
   red[wid][2 * lane + 1] = e1;
   __syncthreads();
   if (threadIdx.x < SCORE_POS) {
     const int q = pb + threadIdx.x;
-    if (q < len) e[(size_t)b * T + q] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    float r = 0.f;
+#pragma unroll
+    for (int w = 0; w < SCORE_WAVES; ++w) r += red[w][threadIdx.x];
+    if (q < len) e[(size_t)b * T + q] = r;
   }
 }
 
@@ -139,28 +164,34 @@ __global__ __launch_bounds__(256) void attn_softmax_ctx_kernel(
 
 // ------------------------------------------------------------- backward step: da
 //   da_i = Ga_i + dcov_next_i + g_cl*[a_i <= cov_i] + dctx . E[i,:]     (Et: [B][A][T])
-__global__ __launch_bounds__(256) void attn_bwd_da_kernel(
+__global__ __launch_bounds__(512) void attn_bwd_da_kernel(
     const bf16* __restrict__ Et, const float* __restrict__ dctx, const float* __restrict__ Ga,
     const float* __restrict__ dcov_next, const float* __restrict__ a, const float* __restrict__ cov,
     const float* __restrict__ gcl, const int* __restrict__ lens, float* __restrict__ da, int T, int A) {
-  __shared__ float red[4][SCORE_POS];
+  __shared__ float red[SCORE_WAVES][SCORE_POS];
   const int b = blockIdx.y;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int len = lens[b];
   const int pb = blockIdx.x * SCORE_POS;
   if (pb >= len) return;
   const int p = pb + 2 * lane;
   const int pc = p < T ? p : 0;
-  const int ka = wid * (A / 4), kb = ka + A / 4;
+  const int ka = wid * (A / SCORE_WAVES), kb = ka + A / SCORE_WAVES;
   const bf16* ep = Et + ((size_t)b * A) * T + pc;
   const float* db = dctx + (size_t)b * A;
   float d0 = 0.f, d1 = 0.f;
-#pragma unroll 8
-  for (int k = ka; k < kb; ++k) {
-    const uint32_t raw = *reinterpret_cast<const uint32_t*>(ep + (size_t)k * T);
-    const float dk = db[k];
-    d0 += dk * __uint_as_float(raw << 16);
-    d1 += dk * __uint_as_float(raw & 0xffff0000u);
+  for (int k = ka; k < kb; k += 8) {
+    uint32_t raw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) raw[i] = *reinterpret_cast<const uint32_t*>(ep + (size_t)(k + i) * T);
+    float dk[8];
+    *reinterpret_cast<float4*>(dk) = *reinterpret_cast<const float4*>(db + k);
+    *reinterpret_cast<float4*>(dk + 4) = *reinterpret_cast<const float4*>(db + k + 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      d0 += dk[i] * lo_bf(raw[i]);
+      d1 += dk[i] * hi_bf(raw[i]);
+    }
   }
   red[wid][2 * lane] = d0;
   red[wid][2 * lane + 1] = d1;
@@ -169,7 +200,9 @@ __global__ __launch_bounds__(256) void attn_bwd_da_kernel(
     const int q = pb + threadIdx.x;
     if (q < len) {
       const size_t ix = (size_t)b * T + q;
-      float r = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+      float r = 0.f;
+#pragma unroll
+      for (int w = 0; w < SCORE_WAVES; ++w) r += red[w][threadIdx.x];
       if (Ga) r += Ga[ix];
       if (dcov_next) r += dcov_next[ix];
       if (gcl && a[ix] <= (cov ? cov[ix] : 0.f)) r += gcl[b];
@@ -229,30 +262,45 @@ __global__ __launch_bounds__(256) void attn_bwd_tanh_kernel(
   }
   const bf16* Fb = F + (size_t)b * T * A;
   const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1;
+  // per-position scalars of this wave's 16 positions, one per lane (lanes 0..15), all
+  // loaded at once and later broadcast with v_readlane (no dependent loads per position)
+  float de_l = 0.f, c_l = 0.f, a_l = 0.f, dn_l = 0.f;
+  {
+    const int p = p0 + (lane & 15);
+    if (p < len) {
+      const size_t ix = rb + p;
+      a_l = a[ix];
+      de_l = a_l * (da[ix] - S);
+      c_l = cov ? cov[ix] : 0.f;
+    }
+    if (p < T && dcov_next) dn_l = dcov_next[rb + p];
+  }
   for (int grp = 0; grp < 2; ++grp) {
     const int pg = p0 + grp * 8;
+    bf16x8 f[NK][8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int pq = min(pg + q, len - 1);
+#pragma unroll
+      for (int kb = 0; kb < NK; ++kb) {
+        const int k0 = min(kb * 512 + lane * 8, A - 8);
+        f[kb][q] = ld8(Fb + (size_t)pq * A + k0);
+      }
+    }
     float dcv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int p = pg + q;
+      const float de = rdlane(de_l, grp * 8 + q);
+      const float c = rdlane(c_l, grp * 8 + q);
       dcv[q] = 0.f;
-      if (p < len) {  // wave-uniform
-        const size_t ix = rb + p;
-        const float de = a[ix] * (da[ix] - S);
-        const float c = cov ? cov[ix] : 0.f;
 #pragma unroll
-        for (int kb = 0; kb < NK; ++kb) {
-          const int k0 = kb * 512 + lane * 8;
-          if (k0 < A) {
-            bf16x8 f = ld8(Fb + (size_t)p * A + k0);
+      for (int kb = 0; kb < NK; ++kb) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float th = ftanh(bf2f(f[j]) + sk[kb][j] + wk[kb][j] * c);
-              const float gs = de * vk[kb][j] * (1.0f - th * th);
-              acc[kb][j] += gs;
-              dcv[q] += gs * wk[kb][j];
-            }
-          }
+        for (int j = 0; j < 8; ++j) {
+          const float th = ftanh(bf2f(f[kb][q][j]) + sk[kb][j] + wk[kb][j] * c);
+          const float gs = de * vk[kb][j] * (1.0f - th * th);
+          acc[kb][j] += gs;
+          dcv[q] += gs * wk[kb][j];
         }
       }
     }
@@ -278,22 +326,24 @@ __global__ __launch_bounds__(256) void attn_bwd_tanh_kernel(
     h1 += __shfl_xor(h1, 4, 64);
     h1 += __shfl_xor(h1, 2, 64);
     h1 += __shfl_xor(h1, 1, 64);
+    // position q's total sits in lanes 8q' .. 8q'+7 with q = 4*b5 + 2*b4 + b3; fetch the
+    // per-position scalars of q from lane (grp*8 + q) and let lane 8*(...) write.
+    const int q = 4 * b5 + 2 * b4 + b3;
+    const int src = grp * 8 + q;
+    const float de_q = __shfl(de_l, src, 64), a_q = __shfl(a_l, src, 64);
+    const float c_q = __shfl(c_l, src, 64), dn_q = __shfl(dn_l, src, 64);
     if ((lane & 7) == 0) {
-      const int q = 4 * b5 + 2 * b4 + b3;
       const int p = pg + q;
       if (p < T) {
         const size_t ix = rb + p;
-        if (p < len) {
-          const float ap = a[ix];
-          de_out[ix] = ap * (da[ix] - S);
-          if (dcov_out) {
-            float r = h1 + (dcov_next ? dcov_next[ix] : 0.f);
-            if (gcl && ap > (cov ? cov[ix] : 0.f)) r += g;
-            dcov_out[ix] = r;
+        de_out[ix] = p < len ? de_q : 0.f;
+        if (dcov_out) {
+          float r = dn_q;
+          if (p < len) {
+            r += h1;
+            if (gcl && a_q > c_q) r += g;
           }
-        } else {
-          de_out[ix] = 0.f;
-          if (dcov_out) dcov_out[ix] = dcov_next ? dcov_next[ix] : 0.f;
+          dcov_out[ix] = r;
         }
       }
     }
@@ -403,7 +453,7 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
 void launch_attn_score(const bf16* Ft, const float* s, const float* v, const float* wc, const float* cov,
                        const int* lens, float* e, int B, int T, int A, hipStream_t st) {
   dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B);
-  hipLaunchKernelGGL(attn_score_kernel, grid, dim3(256), 0, st, Ft, s, v, wc, cov, lens, e, T, A);
+  hipLaunchKernelGGL(attn_score_kernel, grid, dim3(512), 0, st, Ft, s, v, wc, cov, lens, e, T, A);
 }
 void launch_attn_softmax_ctx(const float* e, const bf16* E, const int* lens, const float* cov, float* a_out,
                              float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A,
@@ -416,7 +466,7 @@ void launch_attn_bwd_da(const bf16* Et, const float* dctx, const float* Ga, cons
                         const float* cov, const float* gcl, const int* lens, float* da, int B, int T, int A,
                         hipStream_t st) {
   dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B);
-  hipLaunchKernelGGL(attn_bwd_da_kernel, grid, dim3(256), 0, st, Et, dctx, Ga, dcov_next, a, cov, gcl, lens, da, T,
+  hipLaunchKernelGGL(attn_bwd_da_kernel, grid, dim3(512), 0, st, Et, dctx, Ga, dcov_next, a, cov, gcl, lens, da, T,
                      A);
 }
 int attn_nchunk(int T) { return (T + 63) / 64; }

@@ -39,12 +39,10 @@ __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
   const bf16* hprev = hs + ((size_t)d * (T + 1) + s) * BH;
   const float* cprev = cs + ((size_t)d * (T + 1) + s) * BH;
   const size_t ri = (size_t)(rok ? r : 0) * H + u;
-  float gz[4] = {0, 0, 0, 0}, cp = 0.f;
-  if (active) {
+  float gz[4], cp;  // unconditional: no lens -> address dependence on the critical path
 #pragma unroll
-    for (int g = 0; g < 4; ++g) gz[g] = gxs[g * H + u];
-  }
-  if (rok) cp = cprev[ri];
+  for (int g = 0; g < 4; ++g) gz[g] = gxs[g * H + u];
+  cp = cprev[ri];
   // ---- h_{s-1} . W_hh, K split over the 4 waves
   const int ar = min(r0 + (lane & 15), B - 1);
   const int kof = 8 * (lane >> 4);
@@ -80,7 +78,7 @@ __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
 }
 
 // BPTT step s (launched for s = T-1 ... 0).  dh entering the cell at step s is
-//   dz_{s+1} . W_hh^T  (recurrent, all gate columns of step s+1)  + dOut[r][t]
+//   dz_{s+1} . W_hh^T  (recurrent, all gate columns of step s+1)  + dOut (step frame)
 //   + dh_fin for the last active step (s+1 == len_r; frozen steps pass it through).
 // dc is carried per unit in dc_carry (initialised to dc_fin by the caller).
 // dz is written in bf16 for the step-frame weight-gradient GEMMs done after the loop;
@@ -88,7 +86,7 @@ __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
 __global__ __launch_bounds__(256) void lstm_enc_bwd_step_kernel(
     bf16* __restrict__ dz,            // [2][T][B][4H]
     const bf16* __restrict__ Wn,      // [2][H][4H]  W_hh (rows = input unit)
-    const float* __restrict__ dout,   // [B][T][2H]
+    const float* __restrict__ dout,   // [2][T][B][H]  dL/dh_out in step frame
     const float* __restrict__ dh_fin, // [2][B][H]
     float* __restrict__ dc_carry,     // [2][B][H]
     const float* __restrict__ acts, const float* __restrict__ cs,
@@ -104,18 +102,16 @@ __global__ __launch_bounds__(256) void lstm_enc_bwd_step_kernel(
   const int len = rok ? lens[r] : 0;
   const bool active = s < len;
   const size_t ri = (size_t)(rok ? r : 0) * H + u;
-  float dh = 0.f, dcin = 0.f, a4[4] = {0, 0, 0, 0}, cn = 0.f, cpv = 0.f;
-  if (active) {
-    const int t = d == 0 ? s : len - 1 - s;
-    dh = dout[((size_t)r * T + t) * 2 * H + d * H + u];
-    if (s + 1 >= len) dh += dh_fin[(size_t)d * BH + ri];
-    const float* ap = acts + ((size_t)d * T + s) * B * G + (size_t)r * G;
+  // all epilogue operands loaded unconditionally (addresses independent of len)
+  float a4[4];
+  const float dho = dout[((size_t)d * T + s) * BH + ri];
+  const float dhf = dh_fin[(size_t)d * BH + ri];
+  const float* ap = acts + ((size_t)d * T + s) * B * G + (size_t)(rok ? r : 0) * G;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) a4[g] = ap[g * H + u];
-    cn = cs[((size_t)d * (T + 1) + s + 1) * BH + ri];
-    cpv = cs[((size_t)d * (T + 1) + s) * BH + ri];
-    dcin = dc_carry[(size_t)d * BH + ri];
-  }
+  for (int g = 0; g < 4; ++g) a4[g] = ap[g * H + u];
+  const float cn = cs[((size_t)d * (T + 1) + s + 1) * BH + ri];
+  const float cpv = cs[((size_t)d * (T + 1) + s) * BH + ri];
+  const float dcin = dc_carry[(size_t)d * BH + ri];
   // ---- dz_{s+1} . W_hh^T, K = 4H split over the 4 waves
   f32x4 acc[1] = {f32x4{0, 0, 0, 0}};
   if (s + 1 < T) {
@@ -132,7 +128,7 @@ __global__ __launch_bounds__(256) void lstm_enc_bwd_step_kernel(
   if (!rok) return;
   bf16* dzr = dz + (((size_t)d * T + s) * B + r) * G;
   if (active) {
-    dh += rec[0];
+    const float dh = rec[0] + dho + (s + 1 >= len ? dhf : 0.f);
     const float ig = a4[0], jg = a4[1], fg = a4[2], og = a4[3];
     const float tc = ftanh(cn);
     const float dc = dcin + dh * og * (1.0f - tc * tc);

@@ -444,7 +444,10 @@ class HipPointerGenerator:
         for layer in reversed(range(self.L)):
             st = self.enc[layer]
             din = st["din"]
-            st["dout"].copy_(d_in)
+            # dL/dh_out in step frame: fw as is, bw reversed within each length
+            dsf = st["dout"].view(2, T, B, H)
+            dsf[0].copy_(d_in[:, :, :H].transpose(0, 1))
+            dsf[1].copy_(d_in[:, :, H:].gather(1, w["rev_idx"][..., None].expand(B, T, H)).transpose(0, 1))
             if layer == self.L - 1:
                 st["dh_fin"][0].copy_(d_old_h[:, :H]); st["dh_fin"][1].copy_(d_old_h[:, H:])
                 st["dc_carry"][0].copy_(d_old_c[:, :H]); st["dc_carry"][1].copy_(d_old_c[:, H:])
