@@ -32,7 +32,7 @@ def save_bundle(prefix: str, tensors: Dict[str, object]) -> None:
         for name, t in tensors.items():
             if hasattr(t, "detach"):
                 t = t.detach().cpu().numpy()
-            a = np.ascontiguousarray(np.asarray(t))
+            a = np.require(np.asarray(t), requirements="C")  # keeps 0-d scalars 0-d
             if a.dtype not in DT:
                 raise TypeError(f"unsupported dtype {a.dtype} for {name}")
             dims = (C.c_int64 * max(1, a.ndim))(*a.shape)
