@@ -207,6 +207,42 @@ void clip_adagrad(const Tensor& w, const Tensor& acc, const Tensor& g, const Ten
 }
 int64_t opt_parts() { return opt_nparts(); }
 
+// ---------------------------------------------------------------- beam search
+void final_topk(const Tensor& logits, const Tensor& bias, const OT& pgen, const OT& attn, const Tensor& ext,
+                const Tensor& lens, const Tensor& out_ids, const Tensor& out_lp, int64_t R, int64_t V, int64_t T,
+                int64_t K, int64_t beam) {
+  chk(logits, F32, "logits"); chk(bias, F32, "bias"); chk(ext, I32, "ext"); chk(lens, I32, "lens");
+  chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp");
+  TORCH_CHECK(K >= 1 && K <= 16 && beam >= 1 && R % beam == 0 && T <= 2048, "bad topk args");
+  numel_eq(logits, R * V, "logits"); numel_eq(bias, V, "bias"); numel_eq(ext, (R / beam) * T, "ext");
+  numel_eq(lens, R / beam, "lens"); numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
+  chko(pgen, F32, R, "pgen"); chko(attn, F32, R * T, "attn");
+  TORCH_CHECK(!PO<float>(pgen) || PO<float>(attn), "pointer mode needs attn");
+  launch_final_topk(P<float>(logits), P<float>(bias), PO<float>(pgen), PO<float>(attn), P<int>(ext), P<int>(lens),
+                    P<int>(out_ids), P<float>(out_lp), R, V, T, K, beam, stream());
+}
+
+void beam_step(const Tensor& top_ids, const Tensor& top_lp, const Tensor& lp_sum, const Tensor& latest,
+               const Tensor& gidx, const Tensor& tok_hist, const Tensor& par_hist, const Tensor& done,
+               const Tensor& res_count, const Tensor& res_score, const Tensor& res_len, const Tensor& res_step,
+               const Tensor& res_par, const Tensor& step, int64_t Na, int64_t beam, int64_t K, int64_t stop_id,
+               int64_t min_dec, int64_t max_dec) {
+  chk(top_ids, I32, "top_ids"); chk(top_lp, F32, "top_lp"); chk(lp_sum, F32, "lp_sum"); chk(latest, I32, "latest");
+  chk(gidx, I32, "gidx"); chk(tok_hist, I32, "tok_hist"); chk(par_hist, I32, "par_hist"); chk(done, I32, "done");
+  chk(res_count, I32, "res_count"); chk(res_score, F32, "res_score"); chk(res_len, I32, "res_len");
+  chk(res_step, I32, "res_step"); chk(res_par, I32, "res_par"); chk(step, I32, "step");
+  const int64_t R = Na * beam;
+  TORCH_CHECK(beam >= 1 && beam <= 16 && K >= 1 && K <= 16 && beam * K <= 64, "bad beam args");
+  numel_eq(top_ids, R * K, "top_ids"); numel_eq(top_lp, R * K, "top_lp"); numel_eq(lp_sum, R, "lp_sum");
+  numel_eq(latest, R, "latest"); numel_eq(gidx, R, "gidx"); numel_eq(tok_hist, max_dec * R, "tok_hist");
+  numel_eq(par_hist, max_dec * R, "par_hist"); numel_eq(done, Na, "done"); numel_eq(res_count, Na, "res_count");
+  numel_eq(res_score, R, "res_score"); numel_eq(res_len, R, "res_len"); numel_eq(res_step, R, "res_step");
+  numel_eq(res_par, R, "res_par"); numel_eq(step, 1, "step");
+  launch_beam_step(P<int>(top_ids), P<float>(top_lp), P<float>(lp_sum), P<int>(latest), P<int>(gidx), P<int>(tok_hist),
+                   P<int>(par_hist), P<int>(done), P<int>(res_count), P<float>(res_score), P<int>(res_len),
+                   P<int>(res_step), P<int>(res_par), P<int>(step), Na, beam, K, stop_id, min_dec, max_dec, stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tsamd, m) {
@@ -225,4 +261,6 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("ptr_loss", &ptr_loss);
   m.def("clip_adagrad", &clip_adagrad);
   m.def("opt_parts", &opt_parts);
+  m.def("final_topk", &final_topk);
+  m.def("beam_step", &beam_step);
 }

@@ -43,3 +43,11 @@ void launch_ptr_loss(const float* logits, const float* bias, const int* target, 
 void launch_clip_adagrad(float* w, float* acc, const float* g, long n, float* part, float lr, float max_norm,
                          float* norm_out, int* flag, hipStream_t st);
 int opt_nparts();
+
+void launch_final_topk(const float* logits, const float* bias, const float* pgen, const float* attn, const int* ext,
+                       const int* lens, int* out_ids, float* out_lp, int R, int V, int T, int K, int beam,
+                       hipStream_t st);
+void launch_beam_step(const int* top_ids, const float* top_lp, float* lp_sum, int* latest, int* gidx, int* tok_hist,
+                      int* par_hist, int* done, int* res_count, float* res_score, int* res_len, int* res_step,
+                      int* res_par, const int* step, int Na, int beam, int K, int stop_id, int min_dec, int max_dec,
+                      hipStream_t st);

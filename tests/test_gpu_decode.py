@@ -1,0 +1,154 @@
+"""Device beam search: final_topk / beam_step kernels vs references, graph == eager, and
+end-to-end agreement with the host beam search over the PyTorch oracle."""
+import numpy as np
+import pytest
+import torch
+
+from textsummarization_on_flink_amd.config import HParams
+from textsummarization_on_flink_amd.data.synthetic import SyntheticCorpus, make_batches
+from textsummarization_on_flink_amd.models.params import build_params
+from textsummarization_on_flink_amd.models.reference import ReferencePointerGenerator
+
+pytestmark = pytest.mark.gpu
+
+
+def test_final_topk_matches_materialised_distribution():
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    torch.manual_seed(0)
+    Na, beam, V, T, K = 5, 4, 3000, 96, 8
+    R = Na * beam
+    logits = torch.randn(R, V, device="cuda") * 3
+    bias = torch.randn(V, device="cuda")
+    pg = torch.rand(R, device="cuda")
+    lens = torch.randint(20, T + 1, (Na,), device="cuda", dtype=torch.int32)
+    ext = torch.randint(0, V + 20, (Na, T), device="cuda", dtype=torch.int32)
+    ext[:, :10] = ext[:, 10:20]  # duplicates
+    attn = torch.rand(R, T, device="cuda")
+    mask = (torch.arange(T, device="cuda")[None] < lens.repeat_interleave(beam)[:, None]).float()
+    attn = attn * mask
+    attn = attn / attn.sum(1, keepdim=True)
+    ids = torch.zeros(R, K, dtype=torch.int32, device="cuda")
+    lp = torch.zeros(R, K, device="cuda")
+    k.final_topk(logits, bias, pg, attn, ext, lens, ids, lp, R, V, T, K, beam)
+    # reference: materialise [R, V + 20]
+    vd = torch.softmax(logits + bias, 1)
+    fd = torch.cat([pg[:, None] * vd, torch.zeros(R, 20, device="cuda")], 1)
+    fd = fd.scatter_add(1, ext.repeat_interleave(beam, 0).long(), (1 - pg[:, None]) * attn)
+    rp, ri = torch.topk(fd, K, 1)
+    assert torch.equal(ids.long(), ri)
+    torch.testing.assert_close(lp, torch.log(rp), rtol=1e-4, atol=1e-5)
+    # baseline mode
+    k.final_topk(logits, bias, None, None, ext, lens, ids, lp, R, V, T, K, beam)
+    rp, ri = torch.topk(vd, K, 1)
+    assert torch.equal(ids.long(), ri)
+
+
+def _py_beam_step(state, ids, lps, t, beam, K, stop, min_dec):
+    """numpy mirror of beam_search.py:126-154 for Na articles."""
+    Na = len(state["done"])
+    for a in range(Na):
+        base = a * beam
+        if state["done"][a]:
+            state["gidx"][base:base + beam] = np.arange(base, base + beam)
+            continue
+        norig = 1 if t == 0 else beam
+        cands = []
+        for i in range(norig):
+            for j in range(K):
+                cands.append((state["lp"][base + i] + lps[base + i, j], i, int(ids[base + i, j])))
+        order = sorted(range(len(cands)), key=lambda c: cands[c][0], reverse=True)
+        nh, new = 0, []
+        for c in order:
+            v, i, tok = cands[c]
+            if tok == stop:
+                if t >= min_dec:
+                    state["res"][a].append((v / (t + 2), t, i))
+            else:
+                new.append((v, tok, i))
+            if len(new) == beam or len(state["res"][a]) == beam:
+                break
+        if len(state["res"][a]) >= beam:
+            state["done"][a] = 1
+        for kk in range(beam):
+            v, tok, i = new[min(kk, len(new) - 1)]
+            state["lp"][base + kk] = v
+            state["latest"][base + kk] = tok
+            state["gidx"][base + kk] = base + i
+
+
+def test_beam_step_kernel_matches_python():
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    rng = np.random.default_rng(1)
+    Na, beam, K, stop, min_dec, maxD = 6, 4, 8, 3, 2, 12
+    R = Na * beam
+    dev = {n: torch.zeros(s, dtype=d, device="cuda") for n, s, d in [
+        ("lp", (R,), torch.float32), ("latest", (R,), torch.int32), ("gidx", (R,), torch.int32),
+        ("th", (maxD, R), torch.int32), ("ph", (maxD, R), torch.int32), ("done", (Na,), torch.int32),
+        ("rc", (Na,), torch.int32), ("rs", (R,), torch.float32), ("rl", (R,), torch.int32),
+        ("rst", (R,), torch.int32), ("rp", (R,), torch.int32), ("step", (1,), torch.int32)]}
+    st = {"lp": np.zeros(R, np.float32), "latest": np.zeros(R, np.int64), "gidx": np.arange(R),
+          "done": np.zeros(Na, np.int64), "res": [[] for _ in range(Na)]}
+    for t in range(maxD):
+        ids = rng.integers(0, 40, (R, K)).astype(np.int32)
+        ids[rng.random((R, K)) < 0.15] = stop
+        for r in range(R):  # distinct ids per row like top_k
+            ids[r] = rng.permutation(40)[:K]
+            if rng.random() < 0.3:
+                ids[r, rng.integers(0, K)] = stop
+        lps = np.sort(np.log(rng.random((R, K)).astype(np.float32)), 1)[:, ::-1].copy()
+        k.beam_step(torch.from_numpy(ids).cuda(), torch.from_numpy(lps).cuda(), dev["lp"], dev["latest"], dev["gidx"],
+                    dev["th"], dev["ph"], dev["done"], dev["rc"], dev["rs"], dev["rl"], dev["rst"], dev["rp"],
+                    dev["step"], Na, beam, K, stop, min_dec, maxD)
+        dev["step"].add_(1)
+        _py_beam_step(st, ids, lps, t, beam, K, stop, min_dec)
+        np.testing.assert_array_equal(dev["done"].cpu().numpy(), st["done"])
+        live = np.repeat(st["done"] == 0, beam)
+        np.testing.assert_allclose(dev["lp"].cpu().numpy()[live], st["lp"][live], rtol=1e-6)
+        np.testing.assert_array_equal(dev["latest"].cpu().numpy()[live], st["latest"][live])
+        np.testing.assert_array_equal(dev["gidx"].cpu().numpy(), st["gidx"])
+        rc = dev["rc"].cpu().numpy()
+        for a in range(Na):
+            assert rc[a] == len(st["res"][a])
+            got = dev["rs"].cpu().numpy()[a * beam:a * beam + rc[a]]
+            np.testing.assert_allclose(got, [x[0] for x in st["res"][a]], rtol=1e-6)
+
+
+def _peaked_setup(coverage, Na=8, T=48, V=600, pointer_gen=True):
+    hps = HParams(batch_size=Na, max_enc_steps=T, max_dec_steps=20, min_dec_steps=3, beam_size=4, vocab_size=V,
+                  emb_dim=64, hidden_dim=64, coverage=coverage, pointer_gen=pointer_gen, trunc_norm_init_std=0.5,
+                  rand_unif_init_mag=0.3)
+    corpus = SyntheticCorpus(vocab_size=V, raw_vocab=3 * V, seed=2, art_mean=40, art_sd=10, sent_mean=4)
+    vocab = corpus.vocab(V)
+    batch = make_batches(hps, vocab, corpus, 1, pad_enc_to=T)[0]
+    params = build_params(hps, vocab.size(), device="cuda", seed=3)
+    return hps, vocab, batch, params
+
+
+@pytest.mark.parametrize("coverage,pointer_gen", [(True, True), (False, True), (False, False)])
+def test_device_beam_graph_equals_eager_and_tracks_oracle(coverage, pointer_gen):
+    from textsummarization_on_flink_amd.data.batch import Batch, Example
+    from textsummarization_on_flink_amd.decode.beam_search import OracleStepModel, run_beam_search
+    from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
+    hps, vocab, batch, params = _peaked_setup(coverage, pointer_gen=pointer_gen)
+    dg = DeviceBeamDecoder(hps, vocab, params, n_articles=hps.batch_size, T=hps.max_enc_steps, use_graph=True)
+    hg = dg.decode(batch)
+    de = DeviceBeamDecoder(hps, vocab, params, n_articles=hps.batch_size, T=hps.max_enc_steps, use_graph=False)
+    he = de.decode(batch)
+    assert [h.tokens for h in hg] == [h.tokens for h in he]
+    # host beam search over the fp32 oracle, one article at a time (reference decode path)
+    flat = params.flat
+    W = {n: flat[o:o + c].view(params.view(n).shape) for n, (o, c) in params.offsets.items()}
+    model = OracleStepModel(ReferencePointerGenerator(hps, vocab.size()), W, hps, device="cuda")
+    hps1 = hps.replace(batch_size=hps.beam_size)
+    agree = 0
+    for a in range(hps.batch_size):
+        ex = Example(batch.original_articles[a], batch.original_abstracts_sents[a], vocab, hps1)
+        b1 = Batch([ex] * hps.beam_size, hps1, vocab, pad_enc_to=hps.max_enc_steps)
+        best = run_beam_search(model, vocab, b1, hps)
+        n = min(len(best.tokens), len(hg[a].tokens), 6)
+        agree += best.tokens[:n] == hg[a].tokens[:n]
+    assert agree >= hps.batch_size - 2, agree
+    if dg.keep_attn:
+        assert len(hg[0].attn_dists) == len(hg[0].tokens) - 1

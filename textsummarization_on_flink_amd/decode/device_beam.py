@@ -1,0 +1,246 @@
+"""Batched, device-resident beam search on MI355X (SURVEY PAR3, K17/K20/K25/K26, 7.5-3).
+
+The reference decodes ONE article at a time with beam_size rows and a host round trip per
+step (``beam_search.py:82-168``, one ``sess.run`` + numpy state packing per step).  Here
+``n_articles x beam`` rows decode together and the whole step stays on the GPU:
+
+  gather-by-parent (c, h, ctx*, a*, cov)  ->  cov' = cov + a*  ->  XG / x from per-token
+  tables  ->  dec_cell_fwd  ->  dec_sproj  ->  attn_score / attn_softmax_ctx  ->  p_gen,
+  output projection, vocab GEMM  ->  final_topk (pointer mixture + top-2k)  ->  beam_step
+
+The step reads its index t from a device counter, so ONE captured hipGraph of one step
+is replayed up to max_dec_steps times (host checks the all-done flag every ``chunk``
+replays, the only host sync).
+
+The reference's decode-mode attention runs twice per step (initial_state_attention):
+the first attention of step t recomputes attention(state_{t-1}, cov'_{t-1}), which is
+exactly the parent's post-cell attention of step t-1 -- same inputs -- so it is gathered
+instead of recomputed (only step 0 runs it, in the prologue).  Coverage semantics are
+unchanged: cov'_t = cov'_{t-1}[parent] + a_{t-1}[parent].
+"""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+import torch
+
+from ..data.vocab import START_DECODING, STOP_DECODING, UNKNOWN_TOKEN
+from ..models.pointer_generator import (ATT_B, CELL_B, CELL_K, EMB, LIN_B, LIN_M, OUT_B, OV, PG_B, PG_M,
+                                        HipPointerGenerator, mmf)
+from .beam_search import Hypothesis
+
+BF = torch.bfloat16
+F32 = torch.float32
+
+
+class DeviceBeamDecoder:
+    def __init__(self, hps, vocab, params, n_articles: int, T: int, use_graph: bool = True, chunk: int = 10,
+                 keep_attn: bool = True):
+        self.hps, self.vocab, self.p = hps, vocab, params
+        self.Na, self.beam = n_articles, hps.beam_size
+        self.R = self.Na * self.beam
+        self.K = 2 * self.beam
+        self.T = T
+        self.V = vocab.size()
+        self.maxD = hps.max_dec_steps
+        self.use_graph, self.chunk, self.keep_attn = use_graph, chunk, keep_attn
+        self.eng = HipPointerGenerator(hps, self.V, params, B=self.Na, T=T, D=1)
+        self.k = self.eng.k
+        self.dev = self.eng.dev
+        self._alloc()
+        self.refresh_weights()
+        self.graph = None
+
+    # ------------------------------------------------------------------ setup
+    def _alloc(self):
+        R, T, H, A, E, V, K, Na, D = self.R, self.T, self.eng.H, self.eng.A, self.eng.E, self.V, self.K, self.Na, \
+            self.maxD
+        z = lambda *s, dt=F32: torch.zeros(*s, dtype=dt, device=self.dev)
+        b = {}
+        for name, shape, dt in [
+            ("Ft", (R, A, T), BF), ("E", (R, T, A), BF), ("lens_rep", (R,), torch.int32),
+            ("Cn", (R, H), F32), ("Hn", (R, H), BF), ("CTXn", (R, A), F32), ("ATTn", (R, T), F32), ("COVp", (R, T), F32),
+            ("c", (R, H), F32), ("h", (R, H), BF), ("ctxs", (R, A), F32), ("astar", (R, T), F32), ("cov", (R, T), F32),
+            ("Cb2", (R, H), BF), ("XG", (R, 4 * H), F32), ("act", (R, 4 * H), F32), ("s", (R, A), F32), ("e", (R, T), F32),
+            ("ctx_bf", (R, A), BF), ("PG", (R,), F32), ("outb", (R, H), BF), ("logits", (R, V), F32),
+            ("top_ids", (R, K), torch.int32), ("top_lp", (R, K), F32), ("lp_sum", (R,), F32),
+            ("latest", (R,), torch.int32), ("gidx", (R,), torch.int32), ("tok_hist", (D, R), torch.int32),
+            ("par_hist", (D, R), torch.int32), ("done", (Na,), torch.int32), ("res_count", (Na,), torch.int32),
+            ("res_score", (R,), F32), ("res_len", (R,), torch.int32), ("res_step", (R,), torch.int32),
+            ("res_par", (R,), torch.int32), ("step", (1,), torch.int32), ("ext", (Na, T), torch.int32),
+            ("lens", (Na,), torch.int32),
+        ]:
+            b[name] = z(*shape, dt=dt)
+        if self.keep_attn:
+            b["ATT_hist"] = z(D, R, T)
+            b["PG_hist"] = z(D, R)
+        self.b = b
+
+    def refresh_weights(self):
+        """Per-token tables for the current weights (call after loading a checkpoint):
+        Xtab = emb . W_in[:E] + b_in  and  XGtab = Xtab . W_cell[:E] + b_cell."""
+        self.eng.pack()
+        p, E = self.p, self.eng.E
+        emb = p[EMB]
+        self.Xtab = (emb @ p[LIN_M][:E] + p[LIN_B]).contiguous()
+        self.XGtab = (self.Xtab @ p[CELL_K][:E] + p[CELL_B]).contiguous()
+        self.graph = None
+
+    # ------------------------------------------------------------------ per-chunk phases
+    def _encode(self, batch):
+        eng, b, beam = self.eng, self.b, self.beam
+        eng.set_batch(batch)
+        eng._encoder_forward()
+        w = eng.w
+        b["E"].copy_(eng.enc[-1]["out"].repeat_interleave(beam, 0))
+        b["Ft"].copy_(w["Ft"].repeat_interleave(beam, 0))
+        b["lens_rep"].copy_(w["enc_lens"].repeat_interleave(beam, 0))
+        b["lens"].copy_(w["enc_lens"])
+        b["ext"].copy_(w["ext"])
+        b["Cn"].copy_(w["Cst"][0].repeat_interleave(beam, 0))
+        b["Hn"].copy_(w["Hb"][0].repeat_interleave(beam, 0))
+
+    def _prologue(self):
+        """Step-0 initial-state attention, beam state reset."""
+        k, b, hps, eng = self.k, self.b, self.hps, self.eng
+        R, T, H, A = self.R, self.T, eng.H, eng.A
+        b["Cb2"].copy_(b["Cn"])
+        k.dec_sproj(b["Cb2"], b["Hn"], eng.pk["WsT"], self.p[ATT_B], b["s"], R, H, A)
+        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], None, b["lens_rep"], b["e"], R, T, A)
+        k.attn_softmax_ctx(b["e"], b["E"], b["lens_rep"], None, b["ATTn"], None, None, b["CTXn"], None, R, T, A)
+        b["COVp"].zero_()
+        b["gidx"].copy_(torch.arange(R, dtype=torch.int32, device=self.dev))
+        b["latest"].fill_(self.vocab.word2id(START_DECODING))
+        b["lp_sum"].zero_()
+        for n in ("done", "res_count", "step", "tok_hist", "par_hist", "res_len", "res_step", "res_par"):
+            b[n].zero_()
+        b["res_score"].fill_(-float("inf"))
+
+    def _step(self):
+        k, b, hps, eng, p = self.k, self.b, self.hps, self.eng, self.p
+        R, T, H, A, E, V, K = self.R, self.T, eng.H, eng.A, eng.E, self.V, self.K
+        idx = b["gidx"].long()
+        torch.index_select(b["Cn"], 0, idx, out=b["c"])
+        torch.index_select(b["Hn"], 0, idx, out=b["h"])
+        torch.index_select(b["CTXn"], 0, idx, out=b["ctxs"])
+        torch.index_select(b["ATTn"], 0, idx, out=b["astar"])
+        torch.index_select(b["COVp"], 0, idx, out=b["cov"])
+        if hps.coverage:
+            torch.add(b["cov"], b["astar"], out=b["COVp"])
+        unk = self.vocab.word2id(UNKNOWN_TOKEN)
+        tok = torch.where(b["latest"] >= V, torch.full_like(b["latest"], unk), b["latest"]).long()
+        torch.index_select(self.XGtab, 0, tok, out=b["XG"])
+        ctxs_bf = b["ctxs"].to(BF)
+        x = self.Xtab.index_select(0, tok) + mmf(ctxs_bf, eng.pk["Wic"])
+        k.dec_cell_fwd(b["XG"], ctxs_bf, b["h"], b["c"], eng.pk["WcT2"], b["Cn"], b["Cb2"], b["Hn"], b["act"], R, H, A)
+        k.dec_sproj(b["Cb2"], b["Hn"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
+        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], b["COVp"] if hps.coverage else None, b["lens_rep"],
+                     b["e"], R, T, A)
+        k.attn_softmax_ctx(b["e"], b["E"], b["lens_rep"], None, b["ATTn"], None, None, b["CTXn"], b["ctx_bf"], R, T, A)
+        pg = None
+        if hps.pointer_gen:
+            pm = p[PG_M][:, 0]
+            pre = (b["CTXn"] @ pm[:A] + b["Cn"] @ pm[A:A + H] + b["Hn"].float() @ pm[A + H:A + 2 * H]
+                   + x @ pm[A + 2 * H:] + p[PG_B])
+            torch.sigmoid(pre, out=b["PG"])
+            pg = b["PG"]
+        out = mmf(b["Hn"], eng.pk["OUTm"][:H]) + mmf(b["ctx_bf"], eng.pk["OUTm"][H:]) + p[OUT_B]
+        b["outb"].copy_(out)
+        torch.mm(b["outb"], eng.pk["ow"], out_dtype=F32, out=b["logits"])
+        k.final_topk(b["logits"], p[OV], pg, b["ATTn"] if hps.pointer_gen else None, b["ext"], b["lens"], b["top_ids"],
+                     b["top_lp"], R, V, T, K, self.beam)
+        if self.keep_attn:
+            si = b["step"].long().clamp_(max=self.maxD - 1)
+            b["ATT_hist"].index_copy_(0, si, b["ATTn"][None])
+            if pg is not None:
+                b["PG_hist"].index_copy_(0, si, b["PG"][None])
+        k.beam_step(b["top_ids"], b["top_lp"], b["lp_sum"], b["latest"], b["gidx"], b["tok_hist"], b["par_hist"],
+                    b["done"], b["res_count"], b["res_score"], b["res_len"], b["res_step"], b["res_par"], b["step"],
+                    self.Na, self.beam, K, self.vocab.word2id(STOP_DECODING), hps.min_dec_steps, self.maxD)
+        b["step"].add_(1)
+
+    def _capture(self):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._step()  # warm-up (results discarded: prologue re-runs before decoding)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._step()
+        torch.cuda.synchronize()
+
+    # ------------------------------------------------------------------ driver
+    def run(self, batch) -> None:
+        """Decode one engine batch (n_articles rows) fully on the device."""
+        if self.use_graph and self.graph is None:
+            self._encode(batch)
+            self._prologue()
+            self._capture()
+        self._encode(batch)
+        self._prologue()
+        t = 0
+        while t < self.maxD:
+            n = min(self.chunk, self.maxD - t)
+            for _ in range(n):
+                if self.use_graph:
+                    self.graph.replay()
+                else:
+                    self._step()
+            t += n
+            if int(self.b["done"].min().item()) == 1:
+                break
+        self.steps_run = t
+
+    def results(self, n_valid: int = None) -> List[Hypothesis]:
+        """Backtrack the best hypothesis per article (host)."""
+        b = {k: v.cpu().numpy() for k, v in self.b.items() if k in (
+            "res_count", "res_score", "res_len", "res_step", "res_par", "lp_sum", "tok_hist", "par_hist", "step",
+            "ATT_hist", "PG_hist", "done")}
+        beam, start, stop = self.beam, self.vocab.word2id(START_DECODING), self.vocab.word2id(STOP_DECODING)
+        nsteps = int(min(b["step"][0], self.maxD))
+        out = []
+        for a in range(n_valid if n_valid is not None else self.Na):
+            base = a * beam
+
+            def path(tl, slot):
+                toks, atts, pgs = [], [], []
+                while tl >= 0:
+                    toks.append(int(b["tok_hist"][tl, base + slot]))
+                    par = int(b["par_hist"][tl, base + slot])
+                    if self.keep_attn:
+                        atts.append(b["ATT_hist"][tl, base + par])
+                        pgs.append(float(b["PG_hist"][tl, base + par]) if self.hps.pointer_gen else None)
+                    slot = par
+                    tl -= 1
+                return toks[::-1], atts[::-1], pgs[::-1]
+
+            cands = []
+            nres = int(b["res_count"][a])
+            if nres > 0:
+                for q in range(nres):
+                    t, par = int(b["res_step"][base + q]), int(b["res_par"][base + q])
+                    toks, atts, pgs = path(t - 1, par)
+                    if self.keep_attn:
+                        atts = atts + [b["ATT_hist"][t, base + par]]
+                        pgs = pgs + [float(b["PG_hist"][t, base + par]) if self.hps.pointer_gen else None]
+                    cands.append((float(b["res_score"][base + q]), [start] + toks + [stop], atts, pgs))
+            else:
+                tl = nsteps - 1
+                for slot in range(beam):
+                    toks, atts, pgs = path(tl, slot)
+                    cands.append((float(b["lp_sum"][base + slot]) / (tl + 2), [start] + toks, atts, pgs))
+            best = sorted(cands, key=lambda c: c[0], reverse=True)[0]  # stable, like sort_hyps
+            h = Hypothesis(best[1], [best[0] * len(best[1])] + [0.0] * (len(best[1]) - 1), None,
+                           list(best[2]), list(best[3]), None)
+            out.append(h)
+        return out
+
+    def decode(self, batch) -> List[Hypothesis]:
+        """Decode a Batch of up to n_articles examples; best hypothesis per valid row."""
+        if batch.enc_batch.shape[0] != self.Na:
+            raise ValueError(f"batch has {batch.enc_batch.shape[0]} rows, engine expects {self.Na}")
+        self.run(batch)
+        return self.results(int(batch.valid.sum()))

@@ -209,7 +209,9 @@ class HipPointerGenerator:
         rev = np.where(t < lens[:, None], lens[:, None] - 1 - t, t)
         valid = batch.valid.astype(np.float64)
         nvalid = valid.sum()
-        dm = batch.dec_padding_mask.astype(np.float64)
+        if batch.dec_batch.shape[1] < D:
+            raise ValueError(f"batch has {batch.dec_batch.shape[1]} decoder steps, engine needs {D}")
+        dm = batch.dec_padding_mask[:, :D].astype(np.float64)
         dec_lens = dm.sum(1)
         if hps.pointer_gen:
             rowg = dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
@@ -222,8 +224,8 @@ class HipPointerGenerator:
             "enc_lens": batch.enc_lens.astype(np.int32),
             "rev_idx": rev.astype(np.int64),
             "ext": batch.enc_batch_extend_vocab.astype(np.int32),
-            "dec_batch_t": np.ascontiguousarray(batch.dec_batch.T).astype(np.int64),
-            "target_t": np.ascontiguousarray(batch.target_batch.T).astype(np.int32),
+            "dec_batch_t": np.ascontiguousarray(batch.dec_batch[:, :D].T).astype(np.int64),
+            "target_t": np.ascontiguousarray(batch.target_batch[:, :D].T).astype(np.int32),
             "rowg": np.ascontiguousarray(rowg.T).astype(np.float32),
             "gcl": np.ascontiguousarray(gcl.T).astype(np.float32),
         }
