@@ -209,18 +209,24 @@ int64_t opt_parts() { return opt_nparts(); }
 
 // ---------------------------------------------------------------- beam search
 void final_topk(const Tensor& logits, const Tensor& bias, const OT& pgen, const OT& attn, const Tensor& ext,
-                const Tensor& lens, const Tensor& out_ids, const Tensor& out_lp, int64_t R, int64_t V, int64_t T,
-                int64_t K, int64_t beam) {
+                const Tensor& lens, const Tensor& out_ids, const Tensor& out_lp, const Tensor& part_ms,
+                const Tensor& part_v, const Tensor& part_i, int64_t R, int64_t V, int64_t T, int64_t K, int64_t beam) {
   chk(logits, F32, "logits"); chk(bias, F32, "bias"); chk(ext, I32, "ext"); chk(lens, I32, "lens");
-  chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp");
+  chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp"); chk(part_ms, F32, "part_ms"); chk(part_v, F32, "part_v");
+  chk(part_i, I32, "part_i");
   TORCH_CHECK(K >= 1 && K <= 16 && beam >= 1 && R % beam == 0 && T <= 2048, "bad topk args");
   numel_eq(logits, R * V, "logits"); numel_eq(bias, V, "bias"); numel_eq(ext, (R / beam) * T, "ext");
   numel_eq(lens, R / beam, "lens"); numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
+  TORCH_CHECK(topk_split(V) <= 64, "vocab too large for final_topk");
+  numel_eq(part_ms, R * topk_split(V) * 2, "part_ms"); numel_eq(part_v, R * topk_split(V) * K, "part_v");
+  numel_eq(part_i, R * topk_split(V) * K, "part_i");
   chko(pgen, F32, R, "pgen"); chko(attn, F32, R * T, "attn");
   TORCH_CHECK(!PO<float>(pgen) || PO<float>(attn), "pointer mode needs attn");
   launch_final_topk(P<float>(logits), P<float>(bias), PO<float>(pgen), PO<float>(attn), P<int>(ext), P<int>(lens),
-                    P<int>(out_ids), P<float>(out_lp), R, V, T, K, beam, stream());
+                    P<int>(out_ids), P<float>(out_lp), P<float>(part_ms), P<float>(part_v), P<int>(part_i), R, V, T, K,
+                    beam, stream());
 }
+int64_t topk_parts(int64_t V) { return topk_split(V); }
 
 void beam_step(const Tensor& top_ids, const Tensor& top_lp, const Tensor& lp_sum, const Tensor& latest,
                const Tensor& gidx, const Tensor& tok_hist, const Tensor& par_hist, const Tensor& done,
@@ -243,6 +249,50 @@ void beam_step(const Tensor& top_ids, const Tensor& top_lp, const Tensor& lp_sum
                    P<int>(res_step), P<int>(res_par), P<int>(step), Na, beam, K, stop_id, min_dec, max_dec, stream());
 }
 
+void beam_gather(const Tensor& gidx, const Tensor& latest, const Tensor& c_src, const Tensor& h_src,
+                 const Tensor& ctx_src, const Tensor& a_src, const OT& cov_src, const Tensor& XGtab, const Tensor& Xtab,
+                 const Tensor& c_out, const Tensor& h_out, const Tensor& ctx_out, const Tensor& ctxb_out,
+                 const OT& cov_out, const Tensor& XG_out, const Tensor& x_out, int64_t R, int64_t H, int64_t A,
+                 int64_t T, int64_t E, int64_t V, int64_t unk) {
+  chk(gidx, I32, "gidx"); chk(latest, I32, "latest"); chk(c_src, F32, "c_src"); chk(h_src, BF, "h_src");
+  chk(ctx_src, F32, "ctx_src"); chk(a_src, F32, "a_src"); chk(XGtab, F32, "XGtab"); chk(Xtab, F32, "Xtab");
+  chk(c_out, F32, "c_out"); chk(h_out, BF, "h_out"); chk(ctx_out, F32, "ctx_out"); chk(ctxb_out, BF, "ctxb_out");
+  chk(XG_out, F32, "XG_out"); chk(x_out, F32, "x_out");
+  numel_eq(gidx, R, "gidx"); numel_eq(latest, R, "latest"); numel_eq(c_src, R * H, "c_src"); numel_eq(h_src, R * H, "h_src");
+  numel_eq(ctx_src, R * A, "ctx_src"); numel_eq(a_src, R * T, "a_src"); numel_eq(XGtab, V * 4 * H, "XGtab");
+  numel_eq(Xtab, V * E, "Xtab"); numel_eq(c_out, R * H, "c_out"); numel_eq(h_out, R * H, "h_out");
+  numel_eq(ctx_out, R * A, "ctx_out"); numel_eq(ctxb_out, R * A, "ctxb_out"); numel_eq(XG_out, R * 4 * H, "XG_out");
+  numel_eq(x_out, R * E, "x_out"); chko(cov_src, F32, R * T, "cov_src"); chko(cov_out, F32, R * T, "cov_out");
+  TORCH_CHECK(unk >= 0 && unk < V, "bad unk id");
+  TORCH_CHECK(!PO<float>(cov_out) || PO<float>(cov_src), "coverage gather needs cov_src");
+  launch_beam_gather(P<int>(gidx), P<int>(latest), P<float>(c_src), P<bf16>(h_src), P<float>(ctx_src), P<float>(a_src),
+                     PO<float>(cov_src), P<float>(XGtab), P<float>(Xtab), P<float>(c_out), P<bf16>(h_out),
+                     P<float>(ctx_out), P<bf16>(ctxb_out), PO<float>(cov_out), P<float>(XG_out), P<float>(x_out), R, H,
+                     A, T, E, V, unk, stream());
+}
+
+void linear2(const Tensor& a1, int64_t K1, const OT& a2, int64_t K2, const Tensor& Wt, const OT& bias, const OT& add,
+             const OT& out, const OT& outb, int64_t B, int64_t N) {
+  chk(a1, BF, "a1"); chk(Wt, BF, "Wt");
+  TORCH_CHECK(K1 % 32 == 0 && K2 % 32 == 0 && N % 16 == 0 && K1 > 0, "linear2: K multiples of 32, N of 16");
+  TORCH_CHECK((K2 == 0) == !(a2.has_value() && a2->defined()), "linear2: a2 given iff K2 > 0");
+  numel_eq(a1, B * K1, "a1"); chko(a2, BF, B * K2, "a2"); numel_eq(Wt, N * (K1 + K2), "Wt");
+  chko(bias, F32, N, "bias"); chko(add, F32, B * N, "add"); chko(out, F32, B * N, "out"); chko(outb, BF, B * N, "outb");
+  TORCH_CHECK(PO<float>(out) || PO<bf16>(outb), "linear2 needs an output");
+  launch_linear2(P<bf16>(a1), K1, PO<bf16>(a2), K2, P<bf16>(Wt), PO<float>(bias), PO<float>(add), PO<float>(out),
+                 PO<bf16>(outb), B, N, stream());
+}
+
+void pgen(const Tensor& ctx, const Tensor& c, const Tensor& h, const Tensor& x, const Tensor& w, const Tensor& b,
+          const Tensor& pg, int64_t R, int64_t A, int64_t H, int64_t E) {
+  chk(ctx, F32, "ctx"); chk(c, F32, "c"); chk(h, BF, "h"); chk(x, F32, "x"); chk(w, F32, "w"); chk(b, F32, "b");
+  chk(pg, F32, "pg");
+  numel_eq(ctx, R * A, "ctx"); numel_eq(c, R * H, "c"); numel_eq(h, R * H, "h"); numel_eq(x, R * E, "x");
+  numel_eq(w, A + 2 * H + E, "w"); numel_eq(b, 1, "b"); numel_eq(pg, R, "pg");
+  launch_pgen(P<float>(ctx), P<float>(c), P<bf16>(h), P<float>(x), P<float>(w), P<float>(b), P<float>(pg), R, A, H, E,
+              stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tsamd, m) {
@@ -262,5 +312,9 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("clip_adagrad", &clip_adagrad);
   m.def("opt_parts", &opt_parts);
   m.def("final_topk", &final_topk);
+  m.def("topk_parts", &topk_parts);
   m.def("beam_step", &beam_step);
+  m.def("beam_gather", &beam_gather);
+  m.def("linear2", &linear2);
+  m.def("pgen", &pgen);
 }

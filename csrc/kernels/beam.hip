@@ -42,134 +42,223 @@ __device__ __forceinline__ void cand_insert(Cand (&c)[TOPK_MAX], float v, int id
   }
 }
 
-__global__ __launch_bounds__(TOPK_THREADS) void final_topk_kernel(
-    const float* __restrict__ logits, const float* __restrict__ bias, const float* __restrict__ pgen,
-    const float* __restrict__ attn, const int* __restrict__ ext, const int* __restrict__ lens,
-    int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam) {
-  __shared__ float red[8];
-  __shared__ float sv[TOPK_THREADS * TOPK_MAX];
-  __shared__ int si[TOPK_THREADS * TOPK_MAX];
-  __shared__ float sa[2048];
-  __shared__ int se[2048];
-  __shared__ float cv[2 * TOPK_MAX];
-  __shared__ int ci[2 * TOPK_MAX];
-  __shared__ int ncopy;
-  const int r = blockIdx.x, tid = threadIdx.x;
-  const int art = r / beam;
-  const float* z = logits + (size_t)r * V;
-  // ---- pass 1: LSE and per-thread plain top-K
-  Cand c[TOPK_MAX];
-#pragma unroll
-  for (int k = 0; k < TOPK_MAX; ++k) c[k] = Cand{-INFINITY, 0x7fffffff};
-  float m = -INFINITY, s = 0.f;
-  for (int k = tid; k < V; k += TOPK_THREADS) {
-    const float x = z[k] + bias[k];
-    if (x > m) { s *= fexp(m - x); m = x; }
-    s += fexp(x - m);
-    cand_insert(c, x, k);
-  }
-  const float M = block_max<TOPK_THREADS>(m, red);
-  const float S = block_sum<TOPK_THREADS>(m == -INFINITY ? 0.f : s * fexp(m - M), red);
-  const float lse = M + __logf(S);
-#pragma unroll
-  for (int k = 0; k < TOPK_MAX; ++k) {
-    if (k < K) {
-      sv[tid * K + k] = c[k].v;
-      si[tid * K + k] = c[k].id;
+#define MAX_SPLIT 64  // blocks per row in the vocab pass: ceil(V / (256*32)), V <= 524288
+#define HASH_SIZE 2048
+
+// Block-wide selection of the best K (value, id) pairs from n LDS entries by wave 0:
+// K rounds of wave arg-max, selected entries knocked out.  Writes out_v / out_i.
+__device__ __forceinline__ void wave_select(float* v, int* id, int n, int K, float* out_v, int* out_i) {
+  const int lane = threadIdx.x & 63;
+  for (int round = 0; round < K; ++round) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff, bs = -1;
+    for (int q = lane; q < n; q += 64) {
+      const float x = v[q];
+      const int xi = id[q];
+      if (better(x, xi, bv, bi)) { bv = x; bi = xi; bs = q; }
     }
-  }
-  const float pg = pgen ? pgen[r] : 1.0f;
-  const int len = pgen ? lens[art] : 0;
-  for (int i = tid; i < len; i += TOPK_THREADS) {
-    sa[i] = attn[(size_t)r * T + i];
-    se[i] = ext[(size_t)art * T + i];
-  }
-  if (tid == 0) ncopy = 0;
-  __syncthreads();
-  // ---- block merge of the plain candidates: K rounds of arg-max by wave 0
-  if (tid < 64) {
-    for (int round = 0; round < K; ++round) {
-      float bv = -INFINITY;
-      int bi = 0x7fffffff, bs = -1;
-      for (int q = tid; q < TOPK_THREADS * K; q += 64) {
-        if (better(sv[q], si[q], bv, bi)) { bv = sv[q]; bi = si[q]; bs = q; }
-      }
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64), os = __shfl_xor(bs, o, 64);
-        if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; bs = os; }
-      }
-      if (tid == 0) {
-        // plain value -> final-dist probability
-        cv[round] = pg * fexp(bv - lse);
-        ci[round] = bi;
-        if (bs >= 0) sv[bs] = -INFINITY;
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64), os = __shfl_xor(bs, o, 64);
+      if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; bs = os; }
     }
-  }
-  __syncthreads();
-  // ---- copy distribution: representatives (first occurrence of each id) with combined value
-  // candidates from the copy set are appended after the K plain ones (dedup below)
-  for (int i = tid; i < len; i += TOPK_THREADS) {
-    const int w = se[i];
-    bool rep = true;
-    float mass = 0.f;
-    for (int j = 0; j < len; ++j) {
-      if (se[j] == w) {
-        if (j < i) { rep = false; break; }
-        mass += sa[j];
-      }
-    }
-    if (!rep) continue;
-    const float pv = w < V ? fexp(z[w] + bias[w] - lse) : 0.f;
-    const float val = pg * pv + (1.0f - pg) * mass;
-    // keep the K best copy candidates in a small LDS list guarded by an atomic counter
-    // (len <= T distinct ids; we only need the best K, so store all reps in sv/si scratch)
-    const int slot = atomicAdd(&ncopy, 1);
-    sv[slot] = val;
-    si[slot] = w;
-  }
-  __syncthreads();
-  if (tid < 64) {
-    const int nc = ncopy;
-    // drop plain candidates whose id is in the copy set (the copy entry carries the true value)
-    for (int k = tid; k < K; k += 64) {
-      const int w = ci[k];
-      bool incopy = false;
-      for (int q = 0; q < nc; ++q)
-        if (si[q] == w) { incopy = true; break; }
-      if (incopy) cv[k] = -INFINITY;
+    if (lane == 0) {
+      out_v[round] = bv;
+      out_i[round] = bi;
+      if (bs >= 0) v[bs] = -INFINITY;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    // final K rounds over plain (K) + copy (nc) candidates
-    for (int round = 0; round < K; ++round) {
-      float bv = -INFINITY;
-      int bi = 0x7fffffff, bs = -1;
-      for (int q = tid; q < K + nc; q += 64) {
-        const float v = q < K ? cv[q] : sv[q - K];
-        const int id = q < K ? ci[q] : si[q - K];
-        if (better(v, id, bv, bi)) { bv = v; bi = id; bs = q; }
-      }
+  }
+}
+
+// Pass 1, grid (nsplit, R): each block owns <= 256*32 logits of one row, held in
+// registers (32 per thread, 4 vector batches issued together).  One read gives the online
+// (max, sumexp) and the per-thread maximum; tau = K-th largest per-thread maximum is a
+// lower bound of the true K-th largest value (the top-K thread maxima are K distinct
+// elements), so every top-K element satisfies x >= tau.  Survivors are appended to LDS
+// and the block's top-K selected from them.  Pathological ties (> FILTER_CAP survivors,
+// e.g. all-equal logits) fall back to a register bubble-insert top-K.
+#define PER_THREAD 32
+#define FILTER_CAP 2048
+__global__ __launch_bounds__(TOPK_THREADS) void final_topk_partial_kernel(
+    const float* __restrict__ logits, const float* __restrict__ bias, float* __restrict__ part_ms,
+    float* __restrict__ part_v, int* __restrict__ part_i, int V, int K, int per) {
+  __shared__ float red[8];
+  __shared__ float sv[FILTER_CAP];
+  __shared__ int si[FILTER_CAP];
+  __shared__ float tmax_v[TOPK_THREADS];
+  __shared__ int tmax_i[TOPK_THREADS];
+  __shared__ float selv[TOPK_MAX];
+  __shared__ int seli[TOPK_MAX];
+  __shared__ int cnt;
+  const int r = blockIdx.y, sp = blockIdx.x, tid = threadIdx.x;
+  const int lo = sp * per, hi = min(V, lo + per);
+  const float* z = logits + (size_t)r * V;
+  float x[PER_THREAD];
+  const bool vec = (V % 8 == 0) && (per % 8 == 0);
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(bv, o, 64);
-        const int oi = __shfl_xor(bi, o, 64), os = __shfl_xor(bs, o, 64);
-        if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; bs = os; }
+  for (int bt = 0; bt < PER_THREAD / 8; ++bt) {
+    const int k0 = lo + (bt * TOPK_THREADS + tid) * 8;
+    if (vec && k0 + 8 <= hi) {
+      const float4 a0 = *reinterpret_cast<const float4*>(z + k0), a1 = *reinterpret_cast<const float4*>(z + k0 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + k0), b1 = *reinterpret_cast<const float4*>(bias + k0 + 4);
+      x[bt * 8 + 0] = a0.x + b0.x; x[bt * 8 + 1] = a0.y + b0.y; x[bt * 8 + 2] = a0.z + b0.z; x[bt * 8 + 3] = a0.w + b0.w;
+      x[bt * 8 + 4] = a1.x + b1.x; x[bt * 8 + 5] = a1.y + b1.y; x[bt * 8 + 6] = a1.z + b1.z; x[bt * 8 + 7] = a1.w + b1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[bt * 8 + j] = (k0 + j < hi) ? z[k0 + j] + bias[k0 + j] : -INFINITY;
+    }
+  }
+  float m = -INFINITY;
+  int mi = 0x7fffffff;
+#pragma unroll
+  for (int q = 0; q < PER_THREAD; ++q) {
+    const int id = lo + ((q >> 3) * TOPK_THREADS + tid) * 8 + (q & 7);
+    if (better(x[q], id, m, mi)) { m = x[q]; mi = id; }
+  }
+  float s = 0.f;
+  if (m > -INFINITY) {
+#pragma unroll
+    for (int q = 0; q < PER_THREAD; ++q) s += fexp(x[q] - m);
+  }
+  const float M = block_max<TOPK_THREADS>(m, red);
+  const float S = block_sum<TOPK_THREADS>(m == -INFINITY ? 0.f : s * fexp(m - M), red);
+  tmax_v[tid] = m;
+  tmax_i[tid] = mi;
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  if (tid < 64) wave_select(tmax_v, tmax_i, TOPK_THREADS, K, selv, seli);
+  __syncthreads();
+  const float tau = selv[K - 1];
+#pragma unroll
+  for (int q = 0; q < PER_THREAD; ++q) {
+    if (x[q] >= tau && x[q] > -INFINITY) {
+      const int slot = atomicAdd(&cnt, 1);
+      if (slot < FILTER_CAP) {
+        sv[slot] = x[q];
+        si[slot] = lo + ((q >> 3) * TOPK_THREADS + tid) * 8 + (q & 7);
       }
-      if (tid == 0) {
-        out_ids[(size_t)r * K + round] = bi;
-        out_lp[(size_t)r * K + round] = __logf(bv);
-        if (bs >= 0) {
-          if (bs < K) cv[bs] = -INFINITY;
-          else sv[bs - K] = -INFINITY;
-        }
+    }
+  }
+  __syncthreads();
+  const int n = cnt;
+  const size_t o = ((size_t)r * gridDim.x + sp) * K;
+  if (n <= FILTER_CAP) {
+    if (tid < 64) wave_select(sv, si, n, K, part_v + o, part_i + o);
+  } else {  // tie-heavy fallback: exact per-thread insertion then block selection
+    Cand c[TOPK_MAX];
+#pragma unroll
+    for (int k = 0; k < TOPK_MAX; ++k) c[k] = Cand{-INFINITY, 0x7fffffff};
+#pragma unroll
+    for (int q = 0; q < PER_THREAD; ++q) cand_insert(c, x[q], lo + ((q >> 3) * TOPK_THREADS + tid) * 8 + (q & 7));
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TOPK_MAX; ++k) {
+      if (k < K && tid * K + k < FILTER_CAP) {
+        sv[tid * K + k] = c[k].v;
+        si[tid * K + k] = c[k].id;
       }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+    __syncthreads();
+    if (tid < 64) wave_select(sv, si, min(TOPK_THREADS * K, FILTER_CAP), K, part_v + o, part_i + o);
+  }
+  if (tid == 0) {
+    part_ms[((size_t)r * gridDim.x + sp) * 2] = M;
+    part_ms[((size_t)r * gridDim.x + sp) * 2 + 1] = S;
+  }
+}
+
+__device__ __forceinline__ int hslot(int w) { return (int)(((unsigned)w * 2654435761u) >> 21) & (HASH_SIZE - 1); }
+
+// Pass 2, grid R: merge the TOPK_SPLIT partials (LSE + plain top-K), build the copy
+// distribution with an LDS hash table (one atomicCAS/atomicAdd per source position),
+// replace copied ids' plain values by their combined value, take the final top-K.
+__global__ __launch_bounds__(TOPK_THREADS) void final_topk_merge_kernel(
+    const float* __restrict__ part_ms, const float* __restrict__ part_v, const int* __restrict__ part_i,
+    const float* __restrict__ logits, const float* __restrict__ bias, const float* __restrict__ pgen,
+    const float* __restrict__ attn, const int* __restrict__ ext, const int* __restrict__ lens,
+    int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam, int nsplit) {
+  __shared__ int hkey[HASH_SIZE];
+  __shared__ float hmass[HASH_SIZE];
+  __shared__ float cvv[MAX_SPLIT * TOPK_MAX + HASH_SIZE];
+  __shared__ int cii[MAX_SPLIT * TOPK_MAX + HASH_SIZE];
+  __shared__ float plain_v[TOPK_MAX];
+  __shared__ int plain_i[TOPK_MAX];
+  __shared__ int ncopy;
+  __shared__ float s_lse;
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const int art = r / beam;
+  for (int i = tid; i < HASH_SIZE; i += TOPK_THREADS) { hkey[i] = -1; hmass[i] = 0.f; }
+  if (tid == 0) {
+    float M = -INFINITY;
+    for (int q = 0; q < nsplit; ++q) M = fmaxf(M, part_ms[((size_t)r * nsplit + q) * 2]);
+    float S = 0.f;
+    for (int q = 0; q < nsplit; ++q) {
+      const float mq = part_ms[((size_t)r * nsplit + q) * 2];
+      if (mq > -INFINITY) S += part_ms[((size_t)r * nsplit + q) * 2 + 1] * fexp(mq - M);
+    }
+    s_lse = M + __logf(S);
+    ncopy = 0;
+  }
+  for (int q = tid; q < nsplit * K; q += TOPK_THREADS) {
+    cvv[q] = part_v[(size_t)r * nsplit * K + q];
+    cii[q] = part_i[(size_t)r * nsplit * K + q];
+  }
+  __syncthreads();
+  const float lse = s_lse;
+  const float pg = pgen ? pgen[r] : 1.0f;
+  const int len = pgen ? lens[art] : 0;
+  // copy mass per distinct id
+  for (int i = tid; i < len; i += TOPK_THREADS) {
+    const int w = ext[(size_t)art * T + i];
+    const float a = attn[(size_t)r * T + i];
+    int h = hslot(w);
+    for (int probe = 0; probe < HASH_SIZE; ++probe) {
+      const int prev = atomicCAS(&hkey[h], -1, w);
+      if (prev == -1 || prev == w) {
+        atomicAdd(&hmass[h], a);
+        break;
+      }
+      h = (h + 1) & (HASH_SIZE - 1);
+    }
+  }
+  __syncthreads();
+  // plain top-K over the split winners (logit values)
+  if (tid < 64) wave_select(cvv, cii, nsplit * K, K, plain_v, plain_i);
+  __syncthreads();
+  // candidates: plain ids not in the copy set (value p_gen*pv) + every copied id (combined)
+  if (tid < K) {
+    const int w = plain_i[tid];
+    bool incopy = false;
+    if (len > 0) {
+      int h = hslot(w);
+      for (int probe = 0; probe < HASH_SIZE; ++probe) {
+        const int kk = hkey[h];
+        if (kk == -1) break;
+        if (kk == w) { incopy = true; break; }
+        h = (h + 1) & (HASH_SIZE - 1);
+      }
+    }
+    cvv[tid] = incopy ? -INFINITY : pg * fexp(plain_v[tid] - lse);
+    cii[tid] = w;
+  }
+  __syncthreads();
+  for (int hsl = tid; hsl < HASH_SIZE; hsl += TOPK_THREADS) {
+    const int w = hkey[hsl];
+    if (w < 0) continue;
+    const float pv = w < V ? fexp(logits[(size_t)r * V + w] + bias[w] - lse) : 0.f;
+    const int slot = atomicAdd(&ncopy, 1);
+    cvv[K + slot] = pg * pv + (1.0f - pg) * hmass[hsl];
+    cii[K + slot] = w;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    wave_select(cvv, cii, K + ncopy, K, plain_v, plain_i);
+    if (tid < K) {
+      out_ids[(size_t)r * K + tid] = plain_i[tid];
+      out_lp[(size_t)r * K + tid] = __logf(plain_v[tid]);
     }
   }
 }
@@ -250,11 +339,61 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
   }
 }
 
+// ------------------------------------------------------------------ state gather
+// One block per hypothesis row r with parent g = gidx[r]: copies the parent's decoder
+// state (c fp32, h bf16, post-cell ctx fp32 -> fp32 + bf16), advances coverage
+// cov'[r] = cov_src[g] + a[g] (coverage on), and gathers the per-token input tables
+// (XG = (emb.W_in + b).W_cell[:E] + b_cell, x0 = emb.W_in + b) for the hypothesis's
+// latest token (in-article OOV ids -> [UNK]).  Replaces ~10 tiny gather / elementwise
+// launches per decode step.
+__global__ __launch_bounds__(256) void beam_gather_kernel(
+    const int* __restrict__ gidx, const int* __restrict__ latest,
+    const float* __restrict__ c_src, const bf16* __restrict__ h_src, const float* __restrict__ ctx_src,
+    const float* __restrict__ a_src, const float* __restrict__ cov_src,
+    const float* __restrict__ XGtab, const float* __restrict__ Xtab,
+    float* __restrict__ c_out, bf16* __restrict__ h_out, float* __restrict__ ctx_out, bf16* __restrict__ ctxb_out,
+    float* __restrict__ cov_out, float* __restrict__ XG_out, float* __restrict__ x_out,
+    int H, int A, int T, int E, int V, int unk) {
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const int g = gidx[r];
+  int tok = latest[r];
+  tok = tok < V ? tok : unk;
+  for (int i = tid; i < H; i += 256) {
+    c_out[(size_t)r * H + i] = c_src[(size_t)g * H + i];
+    h_out[(size_t)r * H + i] = h_src[(size_t)g * H + i];
+  }
+  for (int i = tid; i < A; i += 256) {
+    const float v = ctx_src[(size_t)g * A + i];
+    ctx_out[(size_t)r * A + i] = v;
+    ctxb_out[(size_t)r * A + i] = f2bf(v);
+  }
+  if (cov_out)
+    for (int i = tid; i < T; i += 256) cov_out[(size_t)r * T + i] = cov_src[(size_t)g * T + i] + a_src[(size_t)g * T + i];
+  for (int i = tid; i < 4 * H; i += 256) XG_out[(size_t)r * 4 * H + i] = XGtab[(size_t)tok * 4 * H + i];
+  for (int i = tid; i < E; i += 256) x_out[(size_t)r * E + i] = Xtab[(size_t)tok * E + i];
+}
+
+void launch_beam_gather(const int* gidx, const int* latest, const float* c_src, const bf16* h_src,
+                        const float* ctx_src, const float* a_src, const float* cov_src, const float* XGtab,
+                        const float* Xtab, float* c_out, bf16* h_out, float* ctx_out, bf16* ctxb_out, float* cov_out,
+                        float* XG_out, float* x_out, int R, int H, int A, int T, int E, int V, int unk,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(beam_gather_kernel, dim3(R), dim3(256), 0, st, gidx, latest, c_src, h_src, ctx_src, a_src,
+                     cov_src, XGtab, Xtab, c_out, h_out, ctx_out, ctxb_out, cov_out, XG_out, x_out, H, A, T, E, V,
+                     unk);
+}
+
+int topk_split(int V) { return (V + TOPK_THREADS * PER_THREAD - 1) / (TOPK_THREADS * PER_THREAD); }
+
 void launch_final_topk(const float* logits, const float* bias, const float* pgen, const float* attn, const int* ext,
-                       const int* lens, int* out_ids, float* out_lp, int R, int V, int T, int K, int beam,
-                       hipStream_t st) {
-  hipLaunchKernelGGL(final_topk_kernel, dim3(R), dim3(TOPK_THREADS), 0, st, logits, bias, pgen, attn, ext, lens,
-                     out_ids, out_lp, V, T, K, beam);
+                       const int* lens, int* out_ids, float* out_lp, float* part_ms, float* part_v, int* part_i, int R,
+                       int V, int T, int K, int beam, hipStream_t st) {
+  const int ns = topk_split(V);
+  const int per = ((V + ns - 1) / ns + 7) / 8 * 8;
+  hipLaunchKernelGGL(final_topk_partial_kernel, dim3(ns, R), dim3(TOPK_THREADS), 0, st, logits, bias, part_ms, part_v,
+                     part_i, V, K, per);
+  hipLaunchKernelGGL(final_topk_merge_kernel, dim3(R), dim3(TOPK_THREADS), 0, st, part_ms, part_v, part_i, logits, bias,
+                     pgen, attn, ext, lens, out_ids, out_lp, V, T, K, beam, ns);
 }
 
 void launch_beam_step(const int* top_ids, const float* top_lp, float* lp_sum, int* latest, int* gidx, int* tok_hist,

@@ -69,27 +69,51 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
   a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
 }
 
-// s = [c, h] . W_s + b_s  -> [B][A] fp32.  WsT: [A][2H].  grid (A/16, ceil(B/16)).
-__global__ __launch_bounds__(256) void dec_sproj_kernel(
-    const bf16* __restrict__ cb, const bf16* __restrict__ hb, const bf16* __restrict__ WsT,
-    const float* __restrict__ bs, float* __restrict__ s_out, int B, int H, int A) {
+// Generic small-M linear on two concatenated bf16 inputs (the shape of every per-step
+// projection of the decoder: s = [c,h].W_s + b, out = [h,ctx].W_o + b, x = x0 + ctx.W_in[E:]):
+//   out[r][n] = sum_{k<K1} a1[r][k] Wt[n][k] + sum_{k<K2} a2[r][k] Wt[n][K1+k] + bias[n] + add[r][n]
+// Wt: [N][K1+K2] bf16 ("Bt" layout).  fp32 and/or bf16 outputs.  grid (N/16, ceil(B/16)),
+// 4 waves split K (kslice_mma) and reduce in LDS.  add may alias out (same element, same lane).
+__global__ __launch_bounds__(256) void linear2_kernel(
+    const bf16* __restrict__ a1, int K1, const bf16* __restrict__ a2, int K2, const bf16* __restrict__ Wt,
+    const float* __restrict__ bias, const float* add, float* out, bf16* __restrict__ outb, int B, int N) {
   __shared__ float red[4 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
   const int ar = min(r0 + (lane & 15), B - 1);
   const int kof = 8 * (lane >> 4);
-  const bf16* crow = cb + (size_t)ar * H + kof;
-  const bf16* hrow = hb + (size_t)ar * H + kof - H;
-  const bf16* brow = WsT + (size_t)(n0 + (lane & 15)) * 2 * H + kof;
-  const int nst = 2 * H / 32;
+  const int K = K1 + K2;
+  const bf16* r1 = a1 + (size_t)ar * K1 + kof;
+  const bf16* r2 = a2 ? a2 + (size_t)ar * K2 + kof - K1 : nullptr;
+  const bf16* brow = Wt + (size_t)(n0 + (lane & 15)) * K + kof;
+  const int nst = K / 32;
   const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
   f32x4 acc[1] = {f32x4{0, 0, 0, 0}};
-  kslice_mma<1>([&](int k) { return k < H ? ld8(crow + k) : ld8(hrow + k); },
+  kslice_mma<1>([&](int k) { return k < K1 ? ld8(r1 + k) : ld8(r2 + k); },
                 [&](int, int k) { return ld8(brow + k); }, k0, k1, acc);
   float o[1];
   ksplit_reduce<1>(acc, red, o);
   const int r = r0 + (lane >> 4) * 4 + wid, n = n0 + (lane & 15);
-  if (r < B) s_out[(size_t)r * A + n] = o[0] + bs[n];
+  if (r >= B) return;
+  const size_t ix = (size_t)r * N + n;
+  float v = o[0] + (bias ? bias[n] : 0.f) + (add ? add[ix] : 0.f);
+  if (out) out[ix] = v;
+  if (outb) outb[ix] = f2bf(v);
+}
+
+// p_gen = sigmoid([ctx, c, h, x] . w + b), one wave per row (reference attention_decoder.py:164-168).
+__global__ __launch_bounds__(256) void pgen_kernel(const float* __restrict__ ctx, const float* __restrict__ c,
+                                                   const bf16* __restrict__ h, const float* __restrict__ x,
+                                                   const float* __restrict__ w, const float* __restrict__ b,
+                                                   float* __restrict__ pg, int R, int A, int H, int E) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= R) return;
+  float s = 0.f;
+  for (int k = lane; k < A; k += 64) s += ctx[(size_t)r * A + k] * w[k];
+  for (int k = lane; k < H; k += 64) s += c[(size_t)r * H + k] * w[A + k] + bf2f(h[(size_t)r * H + k]) * w[A + H + k];
+  for (int k = lane; k < E; k += 64) s += x[(size_t)r * E + k] * w[A + 2 * H + k];
+  s = wave_sum(s);
+  if (lane == 0) pg[r] = fsigmoid(s + b[0]);
 }
 
 // Backward of s-projection + LSTM cell for step t.  grid (H/16, ceil(B/16)).
@@ -187,10 +211,18 @@ void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, c
   hipLaunchKernelGGL(dec_cell_fwd_kernel, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out, hb_out,
                      act, B, H, A);
 }
+void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
+                    const float* add, float* out, bf16* outb, int B, int N, hipStream_t st) {
+  dim3 grid(N / 16, (B + 15) / 16);
+  hipLaunchKernelGGL(linear2_kernel, grid, dim3(256), 0, st, a1, K1, a2, K2, Wt, bias, add, out, outb, B, N);
+}
 void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out, int B, int H,
                       int A, hipStream_t st) {
-  dim3 grid(A / 16, (B + 15) / 16);
-  hipLaunchKernelGGL(dec_sproj_kernel, grid, dim3(256), 0, st, cb, hb, WsT, bs, s_out, B, H, A);
+  launch_linear2(cb, H, hb, H, WsT, bs, nullptr, s_out, nullptr, B, A, st);
+}
+void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x, const float* w, const float* b,
+                 float* pg, int R, int A, int H, int E, hipStream_t st) {
+  hipLaunchKernelGGL(pgen_kernel, dim3((R + 3) / 4), dim3(256), 0, st, ctx, c, h, x, w, b, pg, R, A, H, E);
 }
 void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,

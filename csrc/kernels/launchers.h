@@ -45,9 +45,19 @@ void launch_clip_adagrad(float* w, float* acc, const float* g, long n, float* pa
 int opt_nparts();
 
 void launch_final_topk(const float* logits, const float* bias, const float* pgen, const float* attn, const int* ext,
-                       const int* lens, int* out_ids, float* out_lp, int R, int V, int T, int K, int beam,
-                       hipStream_t st);
+                       const int* lens, int* out_ids, float* out_lp, float* part_ms, float* part_v, int* part_i, int R,
+                       int V, int T, int K, int beam, hipStream_t st);
+int topk_split(int V);
 void launch_beam_step(const int* top_ids, const float* top_lp, float* lp_sum, int* latest, int* gidx, int* tok_hist,
                       int* par_hist, int* done, int* res_count, float* res_score, int* res_len, int* res_step,
                       int* res_par, const int* step, int Na, int beam, int K, int stop_id, int min_dec, int max_dec,
                       hipStream_t st);
+void launch_beam_gather(const int* gidx, const int* latest, const float* c_src, const bf16* h_src,
+                        const float* ctx_src, const float* a_src, const float* cov_src, const float* XGtab,
+                        const float* Xtab, float* c_out, bf16* h_out, float* ctx_out, bf16* ctxb_out, float* cov_out,
+                        float* XG_out, float* x_out, int R, int H, int A, int T, int E, int V, int unk,
+                        hipStream_t st);
+void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
+                    const float* add, float* out, bf16* outb, int B, int N, hipStream_t st);
+void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x, const float* w, const float* b,
+                 float* pg, int R, int A, int H, int E, hipStream_t st);

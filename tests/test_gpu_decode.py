@@ -30,7 +30,11 @@ def test_final_topk_matches_materialised_distribution():
     attn = attn / attn.sum(1, keepdim=True)
     ids = torch.zeros(R, K, dtype=torch.int32, device="cuda")
     lp = torch.zeros(R, K, device="cuda")
-    k.final_topk(logits, bias, pg, attn, ext, lens, ids, lp, R, V, T, K, beam)
+    S = int(k.topk_parts(V))
+    pms = torch.zeros(R, S, 2, device="cuda")
+    pv = torch.zeros(R, S, K, device="cuda")
+    pi = torch.zeros(R, S, K, dtype=torch.int32, device="cuda")
+    k.final_topk(logits, bias, pg, attn, ext, lens, ids, lp, pms, pv, pi, R, V, T, K, beam)
     # reference: materialise [R, V + 20]
     vd = torch.softmax(logits + bias, 1)
     fd = torch.cat([pg[:, None] * vd, torch.zeros(R, 20, device="cuda")], 1)
@@ -39,7 +43,7 @@ def test_final_topk_matches_materialised_distribution():
     assert torch.equal(ids.long(), ri)
     torch.testing.assert_close(lp, torch.log(rp), rtol=1e-4, atol=1e-5)
     # baseline mode
-    k.final_topk(logits, bias, None, None, ext, lens, ids, lp, R, V, T, K, beam)
+    k.final_topk(logits, bias, None, None, ext, lens, ids, lp, pms, pv, pi, R, V, T, K, beam)
     rp, ri = torch.topk(vd, K, 1)
     assert torch.equal(ids.long(), ri)
 
@@ -152,3 +156,40 @@ def test_device_beam_graph_equals_eager_and_tracks_oracle(coverage, pointer_gen)
     assert agree >= hps.batch_size - 2, agree
     if dg.keep_attn:
         assert len(hg[0].attn_dists) == len(hg[0].tokens) - 1
+
+
+@pytest.mark.parametrize("B,K1,K2,N,use_add", [(20, 256, 512, 256, False), (37, 512, 0, 128, True),
+                                               (64, 256, 256, 512, False)])
+def test_linear2_matches_fp32(B, K1, K2, N, use_add):
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    torch.manual_seed(1)
+    a1 = torch.randn(B, K1, device="cuda").bfloat16()
+    a2 = torch.randn(B, K2, device="cuda").bfloat16() if K2 else None
+    Wt = (torch.randn(N, K1 + K2, device="cuda") * 0.05).bfloat16()
+    bias = torch.randn(N, device="cuda")
+    add = torch.randn(B, N, device="cuda") if use_add else None
+    A = a1.float() if a2 is None else torch.cat([a1.float(), a2.float()], 1)
+    ref = A @ Wt.float().t() + bias + (add if add is not None else 0)
+    out = add.clone() if use_add else torch.zeros(B, N, device="cuda")
+    outb = torch.zeros(B, N, device="cuda", dtype=torch.bfloat16)
+    k.linear2(a1, K1, a2, K2, Wt, bias, out if use_add else None, out, outb, B, N)
+    torch.cuda.synchronize()
+    assert (out - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-4
+    assert (outb.float() - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+
+
+def test_pgen_matches_fp32():
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    torch.manual_seed(2)
+    R, A, H, E = 30, 512, 256, 128
+    ctx, c, x = torch.randn(R, A, device="cuda"), torch.randn(R, H, device="cuda"), torch.randn(R, E, device="cuda")
+    h = torch.randn(R, H, device="cuda").bfloat16()
+    w = torch.randn(A + 2 * H + E, device="cuda") * 0.05
+    b = torch.randn(1, device="cuda")
+    pg = torch.zeros(R, device="cuda")
+    k.pgen(ctx, c, h, x, w, b, pg, R, A, H, E)
+    ref = torch.sigmoid(torch.cat([ctx, c, h.float(), x], 1) @ w + b)
+    torch.cuda.synchronize()
+    assert (pg - ref).abs().max().item() < 1e-4

@@ -8,7 +8,8 @@ step (``beam_search.py:82-168``, one ``sess.run`` + numpy state packing per step
   tables  ->  dec_cell_fwd  ->  dec_sproj  ->  attn_score / attn_softmax_ctx  ->  p_gen,
   output projection, vocab GEMM  ->  final_topk (pointer mixture + top-2k)  ->  beam_step
 
-The step reads its index t from a device counter, so ONE captured hipGraph of one step
+The step reads its index t from a device counter and the decoder state ping-pongs between
+two buffer sets, so ONE captured hipGraph of two steps
 is replayed up to max_dec_steps times (host checks the all-done flag every ``chunk``
 replays, the only host sync).
 
@@ -60,9 +61,9 @@ class DeviceBeamDecoder:
         b = {}
         for name, shape, dt in [
             ("Ft", (R, A, T), BF), ("E", (R, T, A), BF), ("lens_rep", (R,), torch.int32),
-            ("Cn", (R, H), F32), ("Hn", (R, H), BF), ("CTXn", (R, A), F32), ("ATTn", (R, T), F32), ("COVp", (R, T), F32),
-            ("c", (R, H), F32), ("h", (R, H), BF), ("ctxs", (R, A), F32), ("astar", (R, T), F32), ("cov", (R, T), F32),
-            ("Cb2", (R, H), BF), ("XG", (R, 4 * H), F32), ("act", (R, 4 * H), F32), ("s", (R, A), F32), ("e", (R, T), F32),
+            ("c", (R, H), F32), ("h", (R, H), BF), ("ctxs", (R, A), F32), ("ctxs_bf", (R, A), BF),
+            ("x", (R, E), F32), ("Cb2", (R, H), BF), ("XG", (R, 4 * H), F32), ("act", (R, 4 * H), F32),
+            ("s", (R, A), F32), ("e", (R, T), F32),
             ("ctx_bf", (R, A), BF), ("PG", (R,), F32), ("outb", (R, H), BF), ("logits", (R, V), F32),
             ("top_ids", (R, K), torch.int32), ("top_lp", (R, K), F32), ("lp_sum", (R,), F32),
             ("latest", (R,), torch.int32), ("gidx", (R,), torch.int32), ("tok_hist", (D, R), torch.int32),
@@ -70,8 +71,14 @@ class DeviceBeamDecoder:
             ("res_score", (R,), F32), ("res_len", (R,), torch.int32), ("res_step", (R,), torch.int32),
             ("res_par", (R,), torch.int32), ("step", (1,), torch.int32), ("ext", (Na, T), torch.int32),
             ("lens", (Na,), torch.int32),
+            ("part_ms", (R, int(self.k.topk_parts(V)), 2), F32), ("part_v", (R, int(self.k.topk_parts(V)), K), F32),
+            ("part_i", (R, int(self.k.topk_parts(V)), K), torch.int32),
         ]:
             b[name] = z(*shape, dt=dt)
+        # ping-pong decoder state: step t reads set t%2 and writes set (t+1)%2, so a
+        # captured 2-step graph needs no copies between steps
+        self.st = [{"C": z(R, H), "H": z(R, H, dt=BF), "CTX": z(R, A), "ATT": z(R, T), "COV": z(R, T)}
+                   for _ in range(2)]
         if self.keep_attn:
             b["ATT_hist"] = z(D, R, T)
             b["PG_hist"] = z(D, R)
@@ -85,6 +92,7 @@ class DeviceBeamDecoder:
         emb = p[EMB]
         self.Xtab = (emb @ p[LIN_M][:E] + p[LIN_B]).contiguous()
         self.XGtab = (self.Xtab @ p[CELL_K][:E] + p[CELL_B]).contiguous()
+        self.pg_w = p[PG_M][:, 0].contiguous() if self.hps.pointer_gen else None
         self.graph = None
 
     # ------------------------------------------------------------------ per-chunk phases
@@ -98,18 +106,20 @@ class DeviceBeamDecoder:
         b["lens_rep"].copy_(w["enc_lens"].repeat_interleave(beam, 0))
         b["lens"].copy_(w["enc_lens"])
         b["ext"].copy_(w["ext"])
-        b["Cn"].copy_(w["Cst"][0].repeat_interleave(beam, 0))
-        b["Hn"].copy_(w["Hb"][0].repeat_interleave(beam, 0))
+        X = self.st[0]
+        X["C"].copy_(w["Cst"][0].repeat_interleave(beam, 0))
+        X["H"].copy_(w["Hb"][0].repeat_interleave(beam, 0))
 
     def _prologue(self):
-        """Step-0 initial-state attention, beam state reset."""
+        """Step-0 initial-state attention into state set 0, beam state reset."""
         k, b, hps, eng = self.k, self.b, self.hps, self.eng
         R, T, H, A = self.R, self.T, eng.H, eng.A
-        b["Cb2"].copy_(b["Cn"])
-        k.dec_sproj(b["Cb2"], b["Hn"], eng.pk["WsT"], self.p[ATT_B], b["s"], R, H, A)
+        X = self.st[0]
+        b["Cb2"].copy_(X["C"])
+        k.dec_sproj(b["Cb2"], X["H"], eng.pk["WsT"], self.p[ATT_B], b["s"], R, H, A)
         k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], None, b["lens_rep"], b["e"], R, T, A)
-        k.attn_softmax_ctx(b["e"], b["E"], b["lens_rep"], None, b["ATTn"], None, None, b["CTXn"], None, R, T, A)
-        b["COVp"].zero_()
+        k.attn_softmax_ctx(b["e"], b["E"], b["lens_rep"], None, X["ATT"], None, None, X["CTX"], None, R, T, A)
+        X["COV"].zero_()
         b["gidx"].copy_(torch.arange(R, dtype=torch.int32, device=self.dev))
         b["latest"].fill_(self.vocab.word2id(START_DECODING))
         b["lp_sum"].zero_()
@@ -117,42 +127,33 @@ class DeviceBeamDecoder:
             b[n].zero_()
         b["res_score"].fill_(-float("inf"))
 
-    def _step(self):
+    def _step(self, parity: int):
         k, b, hps, eng, p = self.k, self.b, self.hps, self.eng, self.p
         R, T, H, A, E, V, K = self.R, self.T, eng.H, eng.A, eng.E, self.V, self.K
-        idx = b["gidx"].long()
-        torch.index_select(b["Cn"], 0, idx, out=b["c"])
-        torch.index_select(b["Hn"], 0, idx, out=b["h"])
-        torch.index_select(b["CTXn"], 0, idx, out=b["ctxs"])
-        torch.index_select(b["ATTn"], 0, idx, out=b["astar"])
-        torch.index_select(b["COVp"], 0, idx, out=b["cov"])
-        if hps.coverage:
-            torch.add(b["cov"], b["astar"], out=b["COVp"])
-        unk = self.vocab.word2id(UNKNOWN_TOKEN)
-        tok = torch.where(b["latest"] >= V, torch.full_like(b["latest"], unk), b["latest"]).long()
-        torch.index_select(self.XGtab, 0, tok, out=b["XG"])
-        ctxs_bf = b["ctxs"].to(BF)
-        x = self.Xtab.index_select(0, tok) + mmf(ctxs_bf, eng.pk["Wic"])
-        k.dec_cell_fwd(b["XG"], ctxs_bf, b["h"], b["c"], eng.pk["WcT2"], b["Cn"], b["Cb2"], b["Hn"], b["act"], R, H, A)
-        k.dec_sproj(b["Cb2"], b["Hn"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
-        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], b["COVp"] if hps.coverage else None, b["lens_rep"],
+        X, Y = self.st[parity], self.st[1 - parity]
+        cov = hps.coverage
+        k.beam_gather(b["gidx"], b["latest"], X["C"], X["H"], X["CTX"], X["ATT"], X["COV"] if cov else None,
+                      self.XGtab, self.Xtab, b["c"], b["h"], b["ctxs"], b["ctxs_bf"], Y["COV"] if cov else None,
+                      b["XG"], b["x"], R, H, A, T, E, V, self.vocab.word2id(UNKNOWN_TOKEN))
+        k.dec_cell_fwd(b["XG"], b["ctxs_bf"], b["h"], b["c"], eng.pk["WcT2"], Y["C"], b["Cb2"], Y["H"], b["act"],
+                       R, H, A)
+        k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
+        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], Y["COV"] if cov else None, b["lens_rep"],
                      b["e"], R, T, A)
-        k.attn_softmax_ctx(b["e"], b["E"], b["lens_rep"], None, b["ATTn"], None, None, b["CTXn"], b["ctx_bf"], R, T, A)
+        k.attn_softmax_ctx(b["e"], b["E"], b["lens_rep"], None, Y["ATT"], None, None, Y["CTX"], b["ctx_bf"], R, T, A)
         pg = None
         if hps.pointer_gen:
-            pm = p[PG_M][:, 0]
-            pre = (b["CTXn"] @ pm[:A] + b["Cn"] @ pm[A:A + H] + b["Hn"].float() @ pm[A + H:A + 2 * H]
-                   + x @ pm[A + 2 * H:] + p[PG_B])
-            torch.sigmoid(pre, out=b["PG"])
+            # x = x0 + ctx* . W_in[E:]  (x0 = emb . W_in[:E] + b_in gathered per token)
+            k.linear2(b["ctxs_bf"], A, None, 0, eng.pk["WicT"], None, b["x"], b["x"], None, R, E)
+            k.pgen(Y["CTX"], Y["C"], Y["H"], b["x"], self.pg_w, p[PG_B], b["PG"], R, A, H, E)
             pg = b["PG"]
-        out = mmf(b["Hn"], eng.pk["OUTm"][:H]) + mmf(b["ctx_bf"], eng.pk["OUTm"][H:]) + p[OUT_B]
-        b["outb"].copy_(out)
+        k.linear2(Y["H"], H, b["ctx_bf"], A, eng.pk["OUTmT"], p[OUT_B], None, None, b["outb"], R, H)
         torch.mm(b["outb"], eng.pk["ow"], out_dtype=F32, out=b["logits"])
-        k.final_topk(b["logits"], p[OV], pg, b["ATTn"] if hps.pointer_gen else None, b["ext"], b["lens"], b["top_ids"],
-                     b["top_lp"], R, V, T, K, self.beam)
+        k.final_topk(b["logits"], p[OV], pg, Y["ATT"] if hps.pointer_gen else None, b["ext"], b["lens"],
+                     b["top_ids"], b["top_lp"], b["part_ms"], b["part_v"], b["part_i"], R, V, T, K, self.beam)
         if self.keep_attn:
             si = b["step"].long().clamp_(max=self.maxD - 1)
-            b["ATT_hist"].index_copy_(0, si, b["ATTn"][None])
+            b["ATT_hist"].index_copy_(0, si, Y["ATT"][None])
             if pg is not None:
                 b["PG_hist"].index_copy_(0, si, b["PG"][None])
         k.beam_step(b["top_ids"], b["top_lp"], b["lp_sum"], b["latest"], b["gidx"], b["tok_hist"], b["par_hist"],
@@ -160,16 +161,20 @@ class DeviceBeamDecoder:
                     self.Na, self.beam, K, self.vocab.word2id(STOP_DECODING), hps.min_dec_steps, self.maxD)
         b["step"].add_(1)
 
+    def _two_steps(self):
+        self._step(0)
+        self._step(1)
+
     def _capture(self):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            self._step()  # warm-up (results discarded: prologue re-runs before decoding)
+            self._two_steps()  # warm-up (state discarded: the prologue re-runs before decoding)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self._step()
+            self._two_steps()
         torch.cuda.synchronize()
 
     # ------------------------------------------------------------------ driver
@@ -184,11 +189,14 @@ class DeviceBeamDecoder:
         t = 0
         while t < self.maxD:
             n = min(self.chunk, self.maxD - t)
-            for _ in range(n):
-                if self.use_graph:
-                    self.graph.replay()
+            i = 0
+            while i < n:
+                if self.use_graph and n - i >= 2:
+                    self.graph.replay()  # steps t+i, t+i+1 (parity 0 then 1)
+                    i += 2
                 else:
-                    self._step()
+                    self._step((t + i) % 2)
+                    i += 1
             t += n
             if int(self.b["done"].min().item()) == 1:
                 break

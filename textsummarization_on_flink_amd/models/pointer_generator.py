@@ -188,6 +188,7 @@ class HipPointerGenerator:
         put("Ws", p[ATT_M])
         put("WsT", p[ATT_M].t())
         put("OUTm", p[OUT_M])
+        put("OUTmT", p[OUT_M].t())  # [H][H+A] for the per-step linear2 kernel (decode)
         put("ow", p[OW])
         self.pk = pk
         self.f32 = {
