@@ -1,0 +1,26 @@
+"""Shared fixtures: a tiny CNN/DM-shaped dataset on disk and tiny model flags."""
+import os
+
+from textsummarization_on_flink_amd.data import binfmt
+from textsummarization_on_flink_amd.data.synthetic import SyntheticCorpus
+
+TINY_FLAGS = ["--hidden_dim=16", "--emb_dim=8", "--vocab_size=200", "--max_enc_steps=30", "--max_dec_steps=8",
+              "--min_dec_steps=2", "--batch_size=4", "--beam_size=2", "--save_model_secs=0"]
+
+
+def tiny_corpus(seed=0):
+    return SyntheticCorpus(vocab_size=200, raw_vocab=400, seed=seed, art_mean=30, art_sd=8, sent_mean=5)
+
+
+def make_dataset(root, n_files=2, per_file=12, seed=0):
+    """Writes <root>/data/{train,val,test}_00k.bin + <root>/vocab; returns (data_dir, vocab_path, corpus)."""
+    c = tiny_corpus(seed)
+    d = os.path.join(root, "data")
+    os.makedirs(d, exist_ok=True)
+    for split in ("train", "val", "test"):
+        for k in range(n_files):
+            exs = [{"article": a, "abstract": s} for a, s in c.examples(per_file)]
+            binfmt.write_bin(os.path.join(d, f"{split}_{k:03d}.bin"), exs)
+    vp = os.path.join(root, "vocab")
+    c.vocab().save(vp)
+    return d, vp, c

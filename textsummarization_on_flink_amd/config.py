@@ -72,6 +72,12 @@ class HParams:
     max_to_keep: int = 3           # Saver(max_to_keep=3)
     log_every: int = 1
     drop_last: bool = False        # Issue-5 fix: pad (False) or drop (True) a short final batch
+    metrics_path: str = ""         # JSONL metrics file ("" = <log_root>/metrics_<mode>.jsonl)
+    html_escape: bool = False      # fix quirk: make_html_safe discards its result in the reference
+    load_retries: int = 6          # bounded checkpoint-load retries (util.py:29-41 retried forever)
+    fault_nan_step: int = -1       # fault injection: NaN gradient at this (relative) step
+    fault_kill_step: int = -1      # fault injection: hard-exit rank fault_kill_rank at this step
+    fault_kill_rank: int = 0
 
     # ------------------------------------------------------------------ helpers
     def replace(self, **kw) -> "HParams":

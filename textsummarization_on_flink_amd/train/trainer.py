@@ -55,6 +55,7 @@ class GraphTrainer:
         self.g_opt = None
         self.out = None
         self.global_step = 0
+        self.poison_next = False  # fault injection: NaN gradient on the next step (exercises the NaN guard)
 
     # ------------------------------------------------------------------ capture
     def _fb(self):
@@ -96,15 +97,22 @@ class GraphTrainer:
             if self.g_fb is None:
                 self.capture()
             self.g_fb.replay()
+            self._maybe_poison()
             self.reducer()
             self.g_opt.replay()
             out = self.out
         else:
             out = self._fb()
+            self._maybe_poison()
             self.reducer()
             self._opt()
         self.global_step += 1
         return out
+
+    def _maybe_poison(self):
+        if self.poison_next:
+            self.params.grad[0] = float("nan")
+            self.poison_next = False
 
     def check_finite(self, out) -> Dict[str, float]:
         """Host sync: raise on non-finite loss / skipped update (NaN guard)."""
