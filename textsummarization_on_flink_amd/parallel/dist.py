@@ -116,6 +116,8 @@ class GradAllReducer:
 def all_reduce_scalar(x: float, info: DistInfo, op="sum", device=None) -> float:
     if not info.enabled:
         return x
+    if device is None:
+        device = f"cuda:{info.local_rank}" if info.backend == "nccl" else "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
     return float(t.item())
