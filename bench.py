@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--enc", type=int, default=400)
     ap.add_argument("--dec", type=int, default=100)
     ap.add_argument("--vocab", type=int, default=50000)
+    ap.add_argument("--layers", type=int, default=1, help="stacked bi-LSTM encoder layers (config #5: 2)")
+    ap.add_argument("--backend", default=None, help="process-group backend override (default nccl = RCCL; gloo "
+                                                    "lets several ranks share one GPU for a plumbing check)")
     args = ap.parse_args()
 
     import torch
@@ -49,16 +52,18 @@ def main():
     from textsummarization_on_flink_amd.parallel import dist as D
     from textsummarization_on_flink_amd.train.trainer import GraphTrainer
 
-    info = D.init_from_env()
+    info = D.init_from_env(backend=args.backend)
     if info.world != args.gpus and not (info.world == 1 and args.gpus == 1):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world}", file=sys.stderr)
-    torch.cuda.set_device(info.local_rank)
+    dev_id = info.local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_id)
     hps = HParams(batch_size=args.batch, max_enc_steps=args.enc, max_dec_steps=args.dec, vocab_size=args.vocab,
-                  hidden_dim=args.hidden, emb_dim=args.emb, coverage=not args.no_coverage, pointer_gen=True)
+                  hidden_dim=args.hidden, emb_dim=args.emb, coverage=not args.no_coverage, pointer_gen=True,
+                  enc_layers=args.layers)
     corpus = SyntheticCorpus(vocab_size=args.vocab, seed=1000 + info.rank)
     vocab = corpus.vocab(args.vocab)
     batches = make_batches(hps, vocab, corpus, args.pool, pad_enc_to=args.enc)
-    tr = GraphTrainer(hps, vocab.size(), B=args.batch, T=args.enc, device=f"cuda:{info.local_rank}", info=info,
+    tr = GraphTrainer(hps, vocab.size(), B=args.batch, T=args.enc, device=f"cuda:{dev_id}", info=info,
                       use_graph=not args.no_graph)
 
     for i in range(args.warmup):
@@ -101,7 +106,8 @@ def main():
             "data": "synthetic (CNN/DM-shaped, random-init weights)",
             "config": {
                 "model": f"pointer-generator{'+coverage' if hps.coverage else ''} hidden={hps.hidden_dim} "
-                         f"emb={hps.emb_dim} enc={hps.max_enc_steps} dec={hps.max_dec_steps} vocab={hps.vocab_size}",
+                         f"emb={hps.emb_dim} enc={hps.max_enc_steps} dec={hps.max_dec_steps} vocab={hps.vocab_size}"
+                         + (f" enc_layers={hps.enc_layers}" if hps.enc_layers > 1 else ""),
                 "global_batch": args.batch * info.world,
                 "per_gpu_batch": args.batch,
                 "seq_len": f"{hps.max_enc_steps}->{hps.max_dec_steps}",

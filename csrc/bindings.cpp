@@ -293,6 +293,16 @@ void pgen(const Tensor& ctx, const Tensor& c, const Tensor& h, const Tensor& x, 
               stream());
 }
 
+void pgen_bwd(const Tensor& ctx, const Tensor& c, const Tensor& h, const Tensor& x, const Tensor& dpre,
+              const Tensor& gw, int64_t N, int64_t A, int64_t H, int64_t E) {
+  chk(ctx, F32, "ctx"); chk(c, F32, "c"); chk(h, BF, "h"); chk(x, F32, "x"); chk(dpre, F32, "dpre");
+  chk(gw, F32, "gw");
+  numel_eq(ctx, N * A, "ctx"); numel_eq(c, N * H, "c"); numel_eq(h, N * H, "h"); numel_eq(x, N * E, "x");
+  numel_eq(dpre, N, "dpre"); numel_eq(gw, A + 2 * H + E, "gw");
+  launch_pgen_bwd(P<float>(ctx), P<float>(c), P<bf16>(h), P<float>(x), P<float>(dpre), P<float>(gw), N, A, H, E,
+                  stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tsamd, m) {
@@ -317,4 +327,5 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("beam_gather", &beam_gather);
   m.def("linear2", &linear2);
   m.def("pgen", &pgen);
+  m.def("pgen_bwd", &pgen_bwd);
 }

@@ -116,6 +116,34 @@ __global__ __launch_bounds__(256) void pgen_kernel(const float* __restrict__ ctx
   if (lane == 0) pg[r] = fsigmoid(s + b[0]);
 }
 
+// p_gen weight gradient: gw[k] = sum_n dpre[n] * [ctx, c, h, x][n][k]  (k < A+2H+E).
+// grid (ceil(Ktot/256), nsplit): each thread owns one column (coalesced row reads),
+// loops its row chunk, then one atomicAdd.  Replaces four fp32 GEMVs (transposed
+// large-N GEMV is a slow path in the BLAS library).  gw must be zeroed by the caller.
+__global__ __launch_bounds__(256) void pgen_bwd_kernel(const float* __restrict__ ctx, const float* __restrict__ c,
+                                                       const bf16* __restrict__ h, const float* __restrict__ x,
+                                                       const float* __restrict__ dpre, float* __restrict__ gw,
+                                                       int N, int A, int H, int E, int rows_per) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  const int Kt = A + 2 * H + E;
+  if (k >= Kt) return;
+  const int n0 = blockIdx.y * rows_per, n1 = min(N, n0 + rows_per);
+  float acc = 0.f;
+  if (k < A) {
+    for (int n = n0; n < n1; ++n) acc += dpre[n] * ctx[(size_t)n * A + k];
+  } else if (k < A + H) {
+    const int kk = k - A;
+    for (int n = n0; n < n1; ++n) acc += dpre[n] * c[(size_t)n * H + kk];
+  } else if (k < A + 2 * H) {
+    const int kk = k - A - H;
+    for (int n = n0; n < n1; ++n) acc += dpre[n] * bf2f(h[(size_t)n * H + kk]);
+  } else {
+    const int kk = k - A - 2 * H;
+    for (int n = n0; n < n1; ++n) acc += dpre[n] * x[(size_t)n * E + kk];
+  }
+  atomicAdd(gw + k, acc);
+}
+
 // Backward of s-projection + LSTM cell for step t.  grid (H/16, ceil(B/16)).
 //   dc_t = ds . W_s[0:H]^T + dC_dir + dc_carry ;  dh_t = ds . W_s[H:2H]^T + dH_dir + dh_rec
 //   cell backward -> dz_t (bf16), dc_carry <- dc_total * f
@@ -219,6 +247,15 @@ void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* 
 void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out, int B, int H,
                       int A, hipStream_t st) {
   launch_linear2(cb, H, hb, H, WsT, bs, nullptr, s_out, nullptr, B, A, st);
+}
+void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
+                     int N, int A, int H, int E, hipStream_t st) {
+  const int Kt = A + 2 * H + E;
+  const int cols = (Kt + 255) / 256;
+  const int nsplit = max(1, min((N + 63) / 64, 2048 / cols));
+  const int rows_per = (N + nsplit - 1) / nsplit;
+  hipLaunchKernelGGL(pgen_bwd_kernel, dim3(cols, nsplit), dim3(256), 0, st, ctx, c, h, x, dpre, gw, N, A, H, E,
+                     rows_per);
 }
 void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x, const float* w, const float* b,
                  float* pg, int R, int A, int H, int E, hipStream_t st) {

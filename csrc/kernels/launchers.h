@@ -61,3 +61,5 @@ void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* 
                     const float* add, float* out, bf16* outb, int B, int N, hipStream_t st);
 void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x, const float* w, const float* b,
                  float* pg, int R, int A, int H, int E, hipStream_t st);
+void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
+                     int N, int A, int H, int E, hipStream_t st);

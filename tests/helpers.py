@@ -12,9 +12,17 @@ def tiny_corpus(seed=0):
     return SyntheticCorpus(vocab_size=200, raw_vocab=400, seed=seed, art_mean=30, art_sd=8, sent_mean=5)
 
 
-def make_dataset(root, n_files=2, per_file=12, seed=0):
+GPU_FLAGS = ["--hidden_dim=64", "--emb_dim=64", "--vocab_size=600", "--max_enc_steps=48", "--max_dec_steps=12",
+             "--min_dec_steps=3", "--batch_size=8", "--beam_size=4", "--decode_batch=8", "--save_model_secs=0"]
+
+
+def gpu_corpus(seed=0):
+    return SyntheticCorpus(vocab_size=600, raw_vocab=1800, seed=seed, art_mean=40, art_sd=10, sent_mean=4)
+
+
+def make_dataset(root, n_files=2, per_file=12, seed=0, corpus=None):
     """Writes <root>/data/{train,val,test}_00k.bin + <root>/vocab; returns (data_dir, vocab_path, corpus)."""
-    c = tiny_corpus(seed)
+    c = corpus or tiny_corpus(seed)
     d = os.path.join(root, "data")
     os.makedirs(d, exist_ok=True)
     for split in ("train", "val", "test"):

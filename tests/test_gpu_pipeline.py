@@ -1,0 +1,51 @@
+"""The user-facing paths on the MI355X backends: CLI train/resume (hipGraph HIP-kernel
+trainer) and single-pass decode (batched device beam search), and the streaming API
+(fit -> execute -> transform) with GPU worker processes."""
+import glob
+
+import pytest
+
+from textsummarization_on_flink_amd import cli
+from textsummarization_on_flink_amd.api import Row, app
+from textsummarization_on_flink_amd.api.io import CollectionSource, CollectSink
+from textsummarization_on_flink_amd.api.message import FIELDS
+from textsummarization_on_flink_amd.train import checkpoint as ckpt
+
+from helpers import GPU_FLAGS, gpu_corpus, make_dataset
+
+pytestmark = pytest.mark.gpu
+
+
+def _flags(tmp, d, vp, *extra, split="train"):
+    return [f"--data_path={d}/{split}_*", f"--vocab_path={vp}", f"--log_root={tmp}/log", "--exp_name=exp",
+            *GPU_FLAGS, *extra]
+
+
+def test_cli_train_resume_decode_on_gpu(tmp_path):
+    d, vp, _ = make_dataset(str(tmp_path), per_file=12, corpus=gpu_corpus())
+    assert cli.main(_flags(tmp_path, d, vp, "--mode=train", "--num_steps=3")) == 0
+    assert cli.main(_flags(tmp_path, d, vp, "--mode=train", "--num_steps=2")) == 0
+    assert ckpt.latest_checkpoint(f"{tmp_path}/log/exp/train").endswith("model.ckpt-5")
+    import json
+    recs = [json.loads(x) for x in open(f"{tmp_path}/log/exp/metrics_train.jsonl")]
+    assert [r["step"] for r in recs] == [1, 2, 3, 4, 5] and all(r["loss"] > 0 for r in recs)
+    assert cli.main(_flags(tmp_path, d, vp, "--mode=decode", "--single_pass=1", split="test")) == 0
+    dec = glob.glob(f"{tmp_path}/log/exp/decode_*")
+    assert len(dec) == 1
+    assert len(glob.glob(f"{dec[0]}/decoded/*_decoded.txt")) == 24
+    assert "ROUGE-1" in open(f"{dec[0]}/ROUGE_results.txt").read()
+
+
+def test_streaming_fit_then_transform_on_gpu(tmp_path):
+    import os
+    c = gpu_corpus(1)
+    make_dataset(str(tmp_path), corpus=c)
+    os.replace(f"{tmp_path}/vocab", f"{tmp_path}/vocab")
+    extra = list(GPU_FLAGS)
+    rows = [Row(*[r[k] for k in FIELDS]) for r in c.rows(16)]
+    js = app.start_training(CollectionSource(rows), str(tmp_path), extra + ["--num_steps=2"], extra, echo=False)
+    assert ckpt.latest_checkpoint(f"{tmp_path}/log/pretrained_model/train").endswith("model.ckpt-2")
+    sink = CollectSink()
+    q = [Row(*[r[k] for k in FIELDS]) for r in c.rows(10, "q")]
+    app.start_inference(js, CollectionSource(q), [sink], str(tmp_path), extra, echo=False)
+    assert sorted(r[0] for r in sink.rows) == sorted(f"q-{i}" for i in range(10))

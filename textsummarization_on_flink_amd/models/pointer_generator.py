@@ -334,18 +334,37 @@ class HipPointerGenerator:
         return out
 
     # ------------------------------------------------------------------ backward
+    # The backward runs in three phases so a data-parallel trainer can all-reduce each
+    # phase's gradient bucket while the next phase computes (the flat gradient is laid out
+    # in this order: output_projection | decoder + attention | reduce_states + encoder + emb).
+    PHASE_FIRST_PARAM = (f"{DEC}/AttnOutputProjection/Linear/Matrix", f"{P}/reduce_final_st/w_reduce_c")
+
+    def phase_bounds(self):
+        return [self.p.offsets[n][0] for n in self.PHASE_FIRST_PARAM]
+
     def backward(self):
+        self.backward_head()
+        self.backward_mid()
+        self.backward_tail()
+
+    def backward_head(self):
+        """Vocab projection gradients (the 51 MB output_projection bucket)."""
+        w, p = self.w, self.p
+        g = p.g
+        p.grad.zero_()
+        dl = w["dlogits"]
+        g(OW).copy_(torch.mm(w["outb"].t(), dl, out_dtype=F32))
+        g(OV).copy_(dl.sum(0, dtype=F32))
+        self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
+
+    def backward_mid(self):
+        """Output projection, p_gen, decoder reverse loop, decoder/attention weight grads."""
         k, w, hps, p = self.k, self.w, self.hps, self.p
         B, T, D, E, H, A, V = self.B, self.T, self.D, self.E, self.H, self.A, self.V
         N = D * B
         g = p.g
         cov = hps.coverage
-        p.grad.zero_()
-        # ---- vocab projection
-        dl = w["dlogits"]
-        g(OW).copy_(torch.mm(w["outb"].t(), dl, out_dtype=F32))
-        g(OV).copy_(dl.sum(0, dtype=F32))
-        dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
+        dout = self._dout
         # ---- output projection [h, ctx]
         Hn = w["Hb"][1:].reshape(N, H)
         ctxb = w["CTXb"].view(N, A)
@@ -360,11 +379,9 @@ class HipPointerGenerator:
         if hps.pointer_gen:
             dpre = w["dpre"].view(N)
             pm = p[PG_M][:, 0]
-            gp = g(PG_M)[:, 0]
-            gp[:A].copy_(w["CTX"].view(N, A).t() @ dpre)
-            gp[A:A + H].copy_(w["Cst"][1:].reshape(N, H).t() @ dpre)
-            gp[A + H:A + 2 * H].copy_(Hn.float().t() @ dpre)
-            gp[A + 2 * H:].copy_(w["X"].view(N, E).t() @ dpre)
+            # one fused column-reduction kernel for the four p_gen weight slices (gw zeroed above)
+            k.pgen_bwd(w["CTX"].view(N, A), w["Cst"][1:].reshape(N, H), Hn, w["X"].view(N, E), dpre,
+                       g(PG_M).view(-1), N, A, H, E)
             g(PG_B).copy_(dpre.sum().view(1))
             dp = dpre.view(D, B, 1)
             dCTX_dir.add_(dp * pm[:A])
@@ -431,6 +448,15 @@ class HipPointerGenerator:
         g(WH).view(A, A).copy_(mmf(top["out"].view(B * T, A).t(), dFb))
         dE = torch.bmm(w["ATT"].permute(1, 2, 0), w["DCTX"].permute(1, 0, 2))  # [B,T,A]
         dE.view(B * T, A).add_(mmf(dFb, self.pk["Wh"].t()))
+        self._dE, self._d_emb_dec = dE, d_emb_dec
+
+    def backward_tail(self):
+        """reduce_states, encoder BPTT, embedding (the last bucket)."""
+        k, w, p = self.k, self.w, self.p
+        B, T, H = self.B, self.T, self.H
+        g = p.g
+        dE, d_emb_dec = self._dE, self._d_emb_dec
+        lens = w["enc_lens"]
         # ---- reduce_states
         old_c, old_h, pc, ph = self._red
         dpc = w["dc_carry"] * (pc > 0)

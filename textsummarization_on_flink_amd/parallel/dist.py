@@ -74,42 +74,48 @@ def broadcast_params(flat: torch.Tensor, info: DistInfo) -> None:
 
 
 class GradAllReducer:
-    """Bucketed average of a flat gradient buffer."""
+    """Bucketed average of a flat gradient buffer.
 
-    def __init__(self, grad: torch.Tensor, info: DistInfo, bucket_mb: float = 32.0, overlap: bool = False):
+    ``bounds`` (element offsets) defines the buckets explicitly -- the trainer aligns them
+    with the phases of its backward so bucket i can be all-reduced while the next phase
+    computes; otherwise the buffer is cut into ``bucket_mb`` pieces.  ``bucket_ready(i)``
+    issues bucket i's all-reduce asynchronously (RCCL runs it on its own stream after the
+    work already queued on the current stream), ``__call__`` issues the rest, waits, and
+    averages."""
+
+    def __init__(self, grad: torch.Tensor, info: DistInfo, bucket_mb: float = 32.0, overlap: bool = False,
+                 bounds: Optional[List[int]] = None):
         self.info = info
         self.grad = grad
         n = grad.numel()
-        per = max(1, int(bucket_mb * 1024 * 1024 // grad.element_size()))
-        self.buckets: List[torch.Tensor] = [grad[i:min(n, i + per)] for i in range(0, n, per)]
-        self.overlap = overlap and grad.is_cuda
-        self.stream = torch.cuda.Stream() if self.overlap else None
+        if bounds:
+            edges = sorted(set([0] + [int(b) for b in bounds if 0 < int(b) < n] + [n]))
+            self.buckets: List[torch.Tensor] = [grad[a:b] for a, b in zip(edges[:-1], edges[1:])]
+        else:
+            per = max(1, int(bucket_mb * 1024 * 1024 // grad.element_size()))
+            self.buckets = [grad[i:min(n, i + per)] for i in range(0, n, per)]
+        self.overlap = overlap
         self._pending = []
+        self._issued = 0
 
     def bucket_ready(self, idx: int):
-        """Issue bucket ``idx``'s all-reduce now (comm stream) -- called from backward."""
+        """Issue bucket ``idx``'s all-reduce now (async) -- called between backward phases."""
         if not self.info.enabled:
             return
         b = self.buckets[idx]
-        if self.overlap:
-            self.stream.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self.stream):
-                self._pending.append(dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True))
-        else:
-            dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        self._pending.append(dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True))
+        self._issued = max(self._issued, idx + 1)
 
     def __call__(self, grad: Optional[torch.Tensor] = None):
         """All-reduce every bucket not yet issued, wait, and average."""
         if not self.info.enabled:
             return
-        issued = len(self._pending) if self.overlap else 0
-        for i in range(issued, len(self.buckets)):
+        for i in range(self._issued, len(self.buckets)):
             self.bucket_ready(i)
         for w in self._pending:
             w.wait()
         self._pending = []
-        if self.overlap:
-            torch.cuda.current_stream().wait_stream(self.stream)
+        self._issued = 0
         self.grad.mul_(1.0 / self.info.world)
 
 

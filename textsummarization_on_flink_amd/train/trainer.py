@@ -49,7 +49,10 @@ class GraphTrainer:
         if self.info.enabled:
             broadcast_params(params.accum, self.info)
         self.engine = HipPointerGenerator(hps, vsize, params, B=B, T=T)
-        self.reducer = GradAllReducer(params.grad, self.info, bucket_mb=bucket_mb)
+        # buckets = backward phases: output_projection | decoder+attention | encoder+embedding;
+        # each is all-reduced while the following phase computes (RCCL over xGMI)
+        self.reducer = GradAllReducer(params.grad, self.info, bucket_mb=bucket_mb,
+                                      bounds=self.engine.phase_bounds())
         self.use_graph = use_graph
         self.g_fb = None
         self.g_opt = None
@@ -59,8 +62,14 @@ class GraphTrainer:
 
     # ------------------------------------------------------------------ capture
     def _fb(self):
+        out = self._fwd_head()
+        self.engine.backward_mid()
+        self.engine.backward_tail()
+        return out
+
+    def _fwd_head(self):
         out = self.engine.forward(need_grad=True)
-        self.engine.backward()
+        self.engine.backward_head()
         return out
 
     def _opt(self):
@@ -82,9 +91,15 @@ class GraphTrainer:
         self.engine.pack()
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb, pool=pool):
-            self.out = self._fb()
+        # three graphs (forward + vocab backward | decoder backward | encoder backward) so
+        # each gradient bucket's all-reduce overlaps the next phase
+        self.g_fb = [torch.cuda.CUDAGraph() for _ in range(3)]
+        with torch.cuda.graph(self.g_fb[0], pool=pool):
+            self.out = self._fwd_head()
+        with torch.cuda.graph(self.g_fb[1], pool=pool):
+            self.engine.backward_mid()
+        with torch.cuda.graph(self.g_fb[2], pool=pool):
+            self.engine.backward_tail()
         self.g_opt = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_opt, pool=pool):
             self._opt()
@@ -96,7 +111,10 @@ class GraphTrainer:
         if self.use_graph:
             if self.g_fb is None:
                 self.capture()
-            self.g_fb.replay()
+            for i, g in enumerate(self.g_fb):
+                g.replay()
+                if i < 2:
+                    self.reducer.bucket_ready(i)
             self._maybe_poison()
             self.reducer()
             self.g_opt.replay()
@@ -110,8 +128,8 @@ class GraphTrainer:
         return out
 
     def _maybe_poison(self):
-        if self.poison_next:
-            self.params.grad[0] = float("nan")
+        if self.poison_next:  # last element: its bucket's all-reduce has not been issued yet
+            self.params.grad[-1] = float("nan")
             self.poison_next = False
 
     def check_finite(self, out) -> Dict[str, float]:
