@@ -61,6 +61,48 @@ void lstm_enc_bwd_step(const Tensor& dz, const Tensor& Wn, const Tensor& dout, c
                            P<float>(acts), P<float>(cs), P<int>(lens), s, T, B, H, stream());
 }
 
+// persistent (one launch for all T steps) variants; see lstm_persistent.hip
+int64_t lstm_persistent_grid_op(int64_t H, int64_t B) { return lstm_persistent_grid((int)H, (int)B); }
+int64_t lstm_persistent_xbuf_op(int64_t H, int64_t B, bool bwd) {
+  return (int64_t)lstm_persistent_xbuf_elems((int)H, (int)B, bwd);
+}
+
+void lstm_fwd_persistent(const Tensor& gx, const Tensor& Wt, const Tensor& hs, const Tensor& cs, const Tensor& acts,
+                         const Tensor& out, const Tensor& lens, const Tensor& xbuf, const Tensor& err, int64_t T,
+                         int64_t B, int64_t H) {
+  chk(gx, F32, "gx"); chk(Wt, BF, "Wt"); chk(hs, BF, "hs"); chk(cs, F32, "cs"); chk(acts, F32, "acts");
+  chk(out, BF, "out"); chk(lens, I32, "lens"); chk(xbuf, at::kLong, "xbuf"); chk(err, I32, "err");
+  TORCH_CHECK(lstm_persistent_grid((int)H, (int)B) > 0, "persistent LSTM: unsupported H/B (H in {64,128,256}, "
+              "grid <= 256 workgroups)");
+  TORCH_CHECK(T >= 1 && T < (1 << 30), "bad T");
+  numel_eq(gx, 2 * T * B * 4 * H, "gx"); numel_eq(Wt, 2 * 4 * H * H, "Wt");
+  numel_eq(hs, 2 * (T + 1) * B * H, "hs"); numel_eq(cs, 2 * (T + 1) * B * H, "cs");
+  numel_eq(acts, 2 * T * B * 4 * H, "acts"); numel_eq(out, B * T * 2 * H, "out"); numel_eq(lens, B, "lens");
+  TORCH_CHECK(xbuf.numel() >= (int64_t)lstm_persistent_xbuf_elems((int)H, (int)B, false), "xbuf too small");
+  numel_eq(err, 1, "err");
+  launch_lstm_fwd_persistent(P<float>(gx), P<bf16>(Wt), P<bf16>(hs), P<float>(cs), P<float>(acts), P<bf16>(out),
+                             P<int>(lens), (unsigned long long*)xbuf.data_ptr(), (unsigned*)err.data_ptr(), T, B, H,
+                             stream());
+}
+
+void lstm_bwd_persistent(const Tensor& dz, const Tensor& Wn, const Tensor& dout, const Tensor& dh_fin,
+                         const Tensor& dc_carry, const Tensor& acts, const Tensor& cs, const Tensor& lens,
+                         const Tensor& xbuf, const Tensor& err, int64_t T, int64_t B, int64_t H) {
+  chk(dz, BF, "dz"); chk(Wn, BF, "Wn"); chk(dout, F32, "dout"); chk(dh_fin, F32, "dh_fin");
+  chk(dc_carry, F32, "dc_carry"); chk(acts, F32, "acts"); chk(cs, F32, "cs"); chk(lens, I32, "lens");
+  chk(xbuf, at::kLong, "xbuf"); chk(err, I32, "err");
+  TORCH_CHECK(lstm_persistent_grid((int)H, (int)B) > 0, "persistent LSTM: unsupported H/B");
+  TORCH_CHECK(T >= 1 && T < (1 << 30), "bad T");
+  numel_eq(dz, 2 * T * B * 4 * H, "dz"); numel_eq(Wn, 2 * 4 * H * H, "Wn"); numel_eq(dout, B * T * 2 * H, "dout");
+  numel_eq(dh_fin, 2 * B * H, "dh_fin"); numel_eq(dc_carry, 2 * B * H, "dc_carry");
+  numel_eq(acts, 2 * T * B * 4 * H, "acts"); numel_eq(cs, 2 * (T + 1) * B * H, "cs"); numel_eq(lens, B, "lens");
+  TORCH_CHECK(xbuf.numel() >= (int64_t)lstm_persistent_xbuf_elems((int)H, (int)B, true), "xbuf too small");
+  numel_eq(err, 1, "err");
+  launch_lstm_bwd_persistent(P<bf16>(dz), P<bf16>(Wn), P<float>(dout), P<float>(dh_fin), P<float>(dc_carry),
+                             P<float>(acts), P<float>(cs), P<int>(lens), (unsigned long long*)xbuf.data_ptr(),
+                             (unsigned*)err.data_ptr(), T, B, H, stream());
+}
+
 // ---------------------------------------------------------------- attention
 void attn_score(const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov, const Tensor& lens,
                 const Tensor& e, int64_t B, int64_t T, int64_t A) {
@@ -308,6 +350,10 @@ void pgen_bwd(const Tensor& ctx, const Tensor& c, const Tensor& h, const Tensor&
 TORCH_LIBRARY(tsamd, m) {
   m.def("lstm_enc_fwd_step", &lstm_enc_fwd_step);
   m.def("lstm_enc_bwd_step", &lstm_enc_bwd_step);
+  m.def("lstm_persistent_grid", &lstm_persistent_grid_op);
+  m.def("lstm_persistent_xbuf", &lstm_persistent_xbuf_op);
+  m.def("lstm_fwd_persistent", &lstm_fwd_persistent);
+  m.def("lstm_bwd_persistent", &lstm_bwd_persistent);
   m.def("attn_score", &attn_score);
   m.def("attn_softmax_ctx", &attn_softmax_ctx);
   m.def("attn_bwd_da", &attn_bwd_da);

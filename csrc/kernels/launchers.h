@@ -63,3 +63,11 @@ void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x
                  float* pg, int R, int A, int H, int E, hipStream_t st);
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
                      int N, int A, int H, int E, hipStream_t st);
+int lstm_persistent_grid(int H, int B);
+size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd);
+void launch_lstm_fwd_persistent(const float* gx, const bf16* Wt, bf16* hs, float* cs, float* acts, bf16* out,
+                                const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B, int H,
+                                hipStream_t st);
+void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
+                                const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
+                                unsigned* err, int T, int B, int H, hipStream_t st);

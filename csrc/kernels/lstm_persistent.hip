@@ -1,0 +1,408 @@
+// Persistent, weight-resident bidirectional LSTM recurrence (hard part 7.5-1;
+// reference model.py:76-94 / TF LSTMCell semantics exactly as lstm.hip).
+//
+// Why: the per-step kernels of lstm.hip pay a dependent-kernel boundary (~1.5 us) plus an
+// L2 round trip for W_hh every step, 2 x T = 800 times per training step.  Here ONE launch
+// runs all T steps.  Work split:
+//   * a TEAM = NC = H/64 workgroups owns one (direction, 16-row batch tile);
+//   * workgroup c of a team owns hidden units [64c, 64c+64); its wave w owns 16 units and
+//     computes all four gates for them, so the cell update needs no cross-wave reduction;
+//   * W_hh for those gate columns lives in REGISTERS for the whole launch (H/2 VGPRs per
+//     lane: 128 at H = 256) -- the B operand of every MFMA is already in place;
+//   * the only per-step traffic between workgroups is h (forward) / dz (backward) of the
+//     16-row tile, handed over as 8-byte {value, tag} granules written with ONE agent-scope
+//     (sc1) store each and polled with sc1 loads until the tag matches (recipe R2 of the HIP
+//     guide, Guideline 16; tags = step index + 1, the granule buffer is zeroed before every
+//     launch).  Team members are placed on one XCD (blocks b, b+8, ...), so the hand-off stays
+//     in that XCD's L2;
+//   * the hand-off buffer is double-buffered by step parity; a member can only overwrite a
+//     slot after every member has consumed it (it needed their next-step granules first);
+//   * cell state c (forward) / dc (backward) never leaves registers.
+// Every spin is bounded: on timeout the workgroup records a code in *err and stops waiting
+// (results are then garbage, but the grid always drains).
+//
+// Layouts are those of lstm.hip (step frame; hs/cs [2][T+1][B][H], acts [2][T][B][4H],
+// out [B][T][2H], dz [2][T][B][4H]), so the two implementations are interchangeable.
+#include "common.h"
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+namespace {
+
+constexpr unsigned kSpinLimit = 1u << 21;  // x s_sleep(1): ~0.1-1 s before giving up
+
+__device__ __forceinline__ unsigned pack_bf2(float lo, float hi) {
+  const unsigned a = __builtin_bit_cast(unsigned short, f2bf(lo));
+  const unsigned b = __builtin_bit_cast(unsigned short, f2bf(hi));
+  return a | (b << 16);
+}
+
+__device__ __forceinline__ void store_granule(gu64* g, unsigned tag, unsigned v) {
+  __hip_atomic_store(g, ((unsigned long long)tag << 32) | v, RLX_AGENT);
+}
+
+// One wave reads NPL granules per lane (indices first + j*64 + lane) until every tag
+// matches; a pass re-reads only the granules that were not ready yet.
+template <int NPL>
+__device__ __forceinline__ void sweep(const gu64* g, int first, unsigned tag, unsigned (&v)[NPL], bool& dead,
+                                      gu32* err, unsigned code, int lane) {
+  static_assert(NPL <= 32, "ready mask is 32 bits");
+  constexpr unsigned all = NPL == 32 ? 0xffffffffu : ((1u << NPL) - 1);
+  unsigned ready = 0;
+  unsigned long long x[NPL];
+  for (unsigned spins = 0;;) {
+    // issue every outstanding load first (one round trip per pass), then check them
+#pragma unroll
+    for (int j = 0; j < NPL; ++j)
+      if (!((ready >> j) & 1)) x[j] = __hip_atomic_load(g + first + j * 64 + lane, RLX_AGENT);
+#pragma unroll
+    for (int j = 0; j < NPL; ++j)
+      if (!((ready >> j) & 1) && (unsigned)(x[j] >> 32) == tag) {
+        v[j] = (unsigned)x[j];
+        ready |= 1u << j;
+      }
+    if (__all(ready == all) || dead) return;
+    if (++spins > kSpinLimit) {
+      if (lane == 0) __hip_atomic_store(err, code, RLX_AGENT);
+      dead = true;
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// LDS tile [16 rows][RS] bf16 with the 16-byte chunk index XOR-swizzled by row (no padding:
+// the backward tile is exactly 2 x 32 KB at H = 256).
+template <int RS>
+__device__ __forceinline__ int swz(int row, int col) {
+  return row * RS + ((((col >> 3) ^ (row & 7))) << 3) + (col & 7);
+}
+
+// block -> (team, slice): team members share blockIdx % 8 (same XCD under round-robin dealing)
+__device__ __forceinline__ bool team_of(int NC, int nteams, int& team, int& c) {
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+  team = (q / NC) * 8 + xcd;
+  c = q % NC;
+  return team < nteams;
+}
+
+}  // namespace
+
+template <int H>
+__global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
+    const float* __restrict__ gx, const bf16* __restrict__ Wt, bf16* __restrict__ hs, float* __restrict__ cs,
+    float* __restrict__ acts, bf16* __restrict__ out, const int* __restrict__ lens, gu64* xbuf, gu32* err, int T,
+    int B, int ntile) {
+  constexpr int KS = H / 32, NC = H / 64, HP = H / 2, G = 16 * HP, NPL = G / 256;
+  __shared__ __attribute__((aligned(16))) bf16 Ash[2][16 * H];
+  int team, c;
+  if (!team_of(NC, 2 * ntile, team, c)) return;
+  const int d = team / ntile, r0 = (team % ntile) * 16;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int u = c * 64 + wid * 16 + (lane & 15);
+  const size_t G4 = 4 * (size_t)H, BH = (size_t)B * H;
+  bf16x8 Wf[4][KS];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) Wf[g][kk] = ld8(Wt + ((size_t)d * G4 + g * H + u) * H + kk * 32 + 8 * (lane >> 4));
+  int rc[4], ln[4];
+  bool rok[4];
+  float creg[4], hreg[4];
+  const bf16* hs0 = hs + (size_t)d * (T + 1) * BH;
+  const float* cs0 = cs + (size_t)d * (T + 1) * BH;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + (lane >> 4) * 4 + i;
+    rok[i] = r < B;
+    rc[i] = rok[i] ? r : B - 1;
+    ln[i] = rok[i] ? lens[r] : 0;
+    creg[i] = cs0[(size_t)rc[i] * H + u];
+    hreg[i] = bf2f(hs0[(size_t)rc[i] * H + u]);
+  }
+  gu64* xb = xbuf + (size_t)team * 2 * G;
+  bool dead = false;
+  for (int s = 0; s < T; ++s) {
+    const int buf = s & 1;
+    // gate pre-activations x.W_x + b of this step: independent of the hand-off, issued first
+    float gz[4][4];
+    const float* gxs = gx + ((size_t)d * T + s) * B * G4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gz[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u];
+    // ---- h_s of the whole 16-row tile -> LDS
+    if (s == 0) {
+      for (int idx = threadIdx.x; idx < G; idx += 256) {
+        const int row = idx / HP, p = idx % HP;
+        const int rr = min(r0 + row, B - 1);
+        *reinterpret_cast<unsigned*>(&Ash[0][swz<H>(row, 2 * p)]) =
+            *reinterpret_cast<const unsigned*>(hs0 + (size_t)rr * H + 2 * p);
+      }
+    } else {
+      unsigned v[NPL];
+      sweep<NPL>(xb + (size_t)(s & 1) * G, wid * (G / 4), (unsigned)s, v, dead, err, 1u, lane);
+#pragma unroll
+      for (int j = 0; j < NPL; ++j) {
+        const int idx = wid * (G / 4) + j * 64 + lane;
+        *reinterpret_cast<unsigned*>(&Ash[buf][swz<H>(idx / HP, 2 * (idx % HP))]) = v[j];
+      }
+    }
+    __syncthreads();
+    // ---- z = h_s . W_hh for this wave's 16 units x 4 gates (B operands in registers)
+    f32x4 acc[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ash[buf][swz<H>(lane & 15, kk * 32 + 8 * (lane >> 4))]);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = mfma16(a, Wf[g][kk], acc[g]);
+    }
+    // ---- cell update, 4 rows x 1 unit per lane
+    float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
+    bf16* hnext = hs + ((size_t)d * (T + 1) + s + 1) * BH;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rc[i];
+      if (s < ln[i]) {
+        const float ig = fsigmoid(acc[0][i] + gz[i][0]), jg = ftanh(acc[1][i] + gz[i][1]);
+        const float fg = fsigmoid(acc[2][i] + gz[i][2] + 1.0f), og = fsigmoid(acc[3][i] + gz[i][3]);
+        const float cc = fg * creg[i] + ig * jg;
+        const float h = bf2f(f2bf(og * ftanh(cc)));
+        creg[i] = cc;
+        hreg[i] = h;
+        float* a4 = acts + (((size_t)d * T + s) * B + r) * G4;
+        a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
+        const int t = d == 0 ? s : ln[i] - 1 - s;
+        out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(h);
+      }
+      if (rok[i]) {
+        cnext[(size_t)r * H + u] = creg[i];
+        hnext[(size_t)r * H + u] = f2bf(hreg[i]);
+      }
+    }
+    // ---- publish h_{s+1}: unit pairs (u, u+1) of adjacent lanes -> one granule
+    if (s + 1 < T) {
+      gu64* dst = xb + (size_t)((s + 1) & 1) * G;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float hn = __shfl_xor(hreg[i], 1, 64);
+        if (!(lane & 1)) store_granule(dst + ((lane >> 4) * 4 + i) * HP + u / 2, (unsigned)(s + 1),
+                                       pack_bf2(hreg[i], hn));
+      }
+    }
+  }
+}
+
+// Backward.  Exchanging dz (4H gate columns) would cost 4x the forward's traffic, so the
+// recurrent GEMM is split by K instead: workgroup c multiplies ITS dz slice (the 4 gates of
+// its 64 units, 256 columns, written to LDS) by the matching W_hh rows and produces a
+// PARTIAL dh for all H units; wave w's 64 output units are exactly slice w's, and go to
+// workgroup (team, w) as fp32 granules.  Each workgroup sums NC partials for its own units
+// (its own partial stays in LDS): per step a lane reads 4 x (NC-1) granules instead of 32.
+template <int H>
+__global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
+    bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
+    const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
+    const float* __restrict__ cs, const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile) {
+  constexpr int G4 = 4 * H, NC = H / 64, KS = 256 / 32, SLOT = 16 * 64, TEAMX = 2 * NC * NC * SLOT;
+  __shared__ __attribute__((aligned(16))) bf16 Ash[16 * 256];   // dz slice [16 rows][4 gates x 64 units]
+  __shared__ float Pown[16 * 64];                                // own partial dh [16 rows][64 units]
+  int team, c;
+  if (!team_of(NC, 2 * ntile, team, c)) return;
+  const int d = team / ntile, r0 = (team % ntile) * 16;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ul = wid * 16 + (lane & 15);  // this lane's unit within the slice (cell update)
+  const int u = c * 64 + ul;
+  const size_t BH = (size_t)B * H;
+  // B operand of the partial GEMM: B[k][n] = W_hh[v][gate col(k)], k = g*64 + unit-in-slice,
+  // n = output unit v = 64*wid + 16*t + (lane&15)
+  bf16x8 Wp[4][KS];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int k0 = kk * 32 + 8 * (lane >> 4), g = k0 / 64, ul0 = k0 % 64;
+      const int v = min(64 * wid + 16 * t + (lane & 15), H - 1);  // waves >= NC own no output units
+      Wp[t][kk] = ld8(Wn + ((size_t)d * H + v) * G4 + g * H + 64 * c + ul0);
+    }
+  int rc[4], ln[4];
+  bool rok[4];
+  float dcreg[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + (lane >> 4) * 4 + i;
+    rok[i] = r < B;
+    rc[i] = rok[i] ? r : B - 1;
+    ln[i] = rok[i] ? lens[r] : 0;
+    dcreg[i] = dc_carry[(size_t)d * BH + (size_t)rc[i] * H + u];
+  }
+  gu64* xb = xbuf + (size_t)team * TEAMX;  // [parity][dest][src][16][64]
+  bool dead = false;
+  for (int s = T - 1; s >= 0; --s) {
+    float dho[4], dhf[4], a4[4][4], cn[4], cpv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t ri = (size_t)rc[i] * H + u;
+      dho[i] = dout[((size_t)d * T + s) * BH + ri];
+      dhf[i] = dh_fin[(size_t)d * BH + ri];
+      const float* ap = acts + (((size_t)d * T + s) * B + rc[i]) * G4;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) a4[i][g] = ap[g * H + u];
+      cn[i] = cs[((size_t)d * (T + 1) + s + 1) * BH + ri];
+      cpv[i] = cs[((size_t)d * (T + 1) + s) * BH + ri];
+    }
+    // ---- recurrent dh for this lane's 4 rows: own partial (LDS) + the peers' (granules)
+    float rec[4] = {0.f, 0.f, 0.f, 0.f};
+    if (s + 1 < T) {
+      const int row0 = (lane >> 4) * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rec[i] = Pown[(row0 + i) * 64 + ul];
+      if constexpr (NC > 1) {
+        const gu64* src = xb + (size_t)((s + 1) & 1) * NC * NC * SLOT + (size_t)c * NC * SLOT;
+        const unsigned tag = (unsigned)(T - 1 - s);
+        unsigned ready = 0;
+        float got[NC][4];
+        unsigned long long x[NC][4];
+        for (unsigned spins = 0;;) {
+#pragma unroll
+          for (int p = 0; p < NC; ++p)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (p != c && !((ready >> (p * 4 + i)) & 1))
+                x[p][i] = __hip_atomic_load(src + (size_t)p * SLOT + (row0 + i) * 64 + ul, RLX_AGENT);
+#pragma unroll
+          for (int p = 0; p < NC; ++p)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int bit = p * 4 + i;
+              if (p != c && !((ready >> bit) & 1) && (unsigned)(x[p][i] >> 32) == tag) {
+                got[p][i] = __uint_as_float((unsigned)x[p][i]);
+                ready |= 1u << bit;
+              }
+            }
+          const unsigned need = ((1u << (4 * NC)) - 1) & ~(0xFu << (4 * c));
+          if (__all((ready & need) == need) || dead) break;
+          if (++spins > kSpinLimit) {
+            if (lane == 0) __hip_atomic_store(err, 2u, RLX_AGENT);
+            dead = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int p = 0; p < NC; ++p)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (p != c) rec[i] += ((ready >> (p * 4 + i)) & 1) ? got[p][i] : 0.f;
+      }
+    }
+    // ---- cell backward -> dz (4 gates) for (4 rows, unit u)
+    float dzv[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (s < ln[i]) {
+        const float dh = rec[i] + dho[i] + (s + 1 >= ln[i] ? dhf[i] : 0.f);
+        const float ig = a4[i][0], jg = a4[i][1], fg = a4[i][2], og = a4[i][3];
+        const float tc = ftanh(cn[i]);
+        const float dc = dcreg[i] + dh * og * (1.0f - tc * tc);
+        dzv[i][0] = dc * jg * ig * (1.0f - ig);
+        dzv[i][1] = dc * ig * (1.0f - jg * jg);
+        dzv[i][2] = dc * cpv[i] * fg * (1.0f - fg);
+        dzv[i][3] = dh * tc * og * (1.0f - og);
+        dcreg[i] = dc * fg;
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dzv[i][g] = 0.f;
+      }
+      const int row = (lane >> 4) * 4 + i;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) Ash[swz<256>(row, g * 64 + ul)] = f2bf(dzv[i][g]);
+      if (rok[i]) {
+        bf16* dzr = dz + (((size_t)d * T + s) * B + rc[i]) * G4;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dzr[g * H + u] = f2bf(dzv[i][g]);
+      }
+    }
+    if (s == 0) break;
+    __syncthreads();  // dz slice complete in LDS (and every lane has read Pown)
+    // ---- partial dh over this slice's gate columns, for units 64*wid .. +63
+    if (wid < NC) {
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ash[swz<256>(lane & 15, kk * 32 + 8 * (lane >> 4))]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = mfma16(a, Wp[t][kk], acc[t]);
+    }
+    // ---- publish: wave wid's units belong to slice wid
+    if (wid == c) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Pown[((lane >> 4) * 4 + r) * 64 + 16 * t + (lane & 15)] = acc[t][r];
+    } else {
+      gu64* dst = xb + (size_t)(s & 1) * NC * NC * SLOT + ((size_t)wid * NC + c) * SLOT;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          store_granule(dst + ((lane >> 4) * 4 + r) * 64 + 16 * t + (lane & 15), (unsigned)(T - s),
+                        __float_as_uint(acc[t][r]));
+    }
+    }
+    __syncthreads();  // Pown visible before the next step reads it; Ash free for rewriting
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (rok[i]) dc_carry[(size_t)d * BH + (size_t)rc[i] * H + u] = dcreg[i];
+}
+
+// ---------------------------------------------------------------------- launchers
+int lstm_persistent_grid(int H, int B) {
+  if (H != 64 && H != 128 && H != 256) return 0;
+  const int NC = H / 64, ntile = (B + 15) / 16;
+  const int grid = 8 * NC * ((2 * ntile + 7) / 8);
+  return grid <= 256 ? grid : 0;  // every workgroup must be co-resident (1 per CU)
+}
+
+size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {
+  const int ntile = (B + 15) / 16, NC = H / 64;
+  // fwd: [team][parity][16 rows][H/2 unit pairs]; bwd: [team][parity][dest][src][16][64]
+  return (size_t)2 * ntile * 2 * (bwd ? (size_t)NC * NC * 16 * 64 : (size_t)16 * (H / 2));
+}
+
+void launch_lstm_fwd_persistent(const float* gx, const bf16* Wt, bf16* hs, float* cs, float* acts, bf16* out,
+                                const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B, int H,
+                                hipStream_t st) {
+  const int grid = lstm_persistent_grid(H, B), ntile = (B + 15) / 16;
+  gu64* xb = (gu64*)xbuf;
+  gu32* e = (gu32*)err;
+#define LAUNCH_F(HH)                                                                                       \
+  hipLaunchKernelGGL(lstm_fwd_persistent_kernel<HH>, dim3(grid), dim3(256), 0, st, gx, Wt, hs, cs, acts, out, \
+                     lens, xb, e, T, B, ntile)
+  if (H == 64) LAUNCH_F(64);
+  else if (H == 128) LAUNCH_F(128);
+  else LAUNCH_F(256);
+#undef LAUNCH_F
+}
+
+void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
+                                const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
+                                unsigned* err, int T, int B, int H, hipStream_t st) {
+  const int grid = lstm_persistent_grid(H, B), ntile = (B + 15) / 16;
+  gu64* xb = (gu64*)xbuf;
+  gu32* e = (gu32*)err;
+#define LAUNCH_B(HH)                                                                                          \
+  hipLaunchKernelGGL(lstm_bwd_persistent_kernel<HH>, dim3(grid), dim3(256), 0, st, dz, Wn, dout, dh_fin, dc_carry, \
+                     acts, cs, lens, xb, e, T, B, ntile)
+  if (H == 64) LAUNCH_B(64);
+  else if (H == 128) LAUNCH_B(128);
+  else LAUNCH_B(256);
+#undef LAUNCH_B
+}

@@ -1,0 +1,89 @@
+"""Persistent weight-resident LSTM (one launch, granule hand-offs) vs the per-step kernels:
+same layouts, same TF LSTMCell semantics (variable lengths, frozen rows, step frame)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(H, B, T, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    r = lambda *s, sc=1.0: (torch.randn(*s, device="cuda", generator=g) * sc)
+    lens = torch.randint(1, T + 1, (B,), device="cuda", generator=g, dtype=torch.int32)
+    lens[0] = T
+    lens[-1] = 1
+    gx = r(2, T, B, 4 * H, sc=0.5)
+    W = r(2, 4 * H, H, sc=1.0 / H ** 0.5).bfloat16()          # Wt [2][4H][H]
+    Wn = W.transpose(1, 2).contiguous()                        # [2][H][4H]
+    hs = torch.zeros(2, T + 1, B, H, device="cuda", dtype=torch.bfloat16)
+    cs = torch.zeros(2, T + 1, B, H, device="cuda")
+    hs[:, 0] = r(2, B, H, sc=0.3).bfloat16()
+    cs[:, 0] = r(2, B, H, sc=0.3)
+    return g, r, lens, gx, W.contiguous(), Wn, hs, cs
+
+
+@pytest.mark.parametrize("H,B,T", [(64, 16, 9), (128, 37, 20), (256, 64, 33), (256, 200, 12)])
+def test_persistent_matches_step_kernels(H, B, T):
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    assert int(k.lstm_persistent_grid(H, B)) > 0
+    g, r, lens, gx, Wt, Wn, hs0, cs0 = _setup(H, B, T, 7 + H + B)
+    res = {}
+    for mode in ("step", "persistent"):
+        hs, cs = hs0.clone(), cs0.clone()
+        acts = torch.zeros(2, T, B, 4 * H, device="cuda")
+        out = torch.zeros(B, T, 2 * H, device="cuda", dtype=torch.bfloat16)
+        err = torch.zeros(1, device="cuda", dtype=torch.int32)
+        if mode == "step":
+            for s in range(T):
+                k.lstm_enc_fwd_step(gx, Wt, hs, cs, acts, out, lens, s, T, B, H)
+        else:
+            xf = torch.zeros(int(k.lstm_persistent_xbuf(H, B, False)), device="cuda", dtype=torch.long)
+            k.lstm_fwd_persistent(gx, Wt, hs, cs, acts, out, lens, xf, err, T, B, H)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        # backward on the forward's own activations
+        gb = torch.Generator(device="cuda").manual_seed(99)
+        dout = torch.randn(2, T, B, H, device="cuda", generator=gb) * 0.1
+        dh_fin = torch.randn(2, B, H, device="cuda", generator=gb) * 0.1
+        dcc = torch.randn(2, B, H, device="cuda", generator=gb) * 0.1
+        dz = torch.zeros(2, T, B, 4 * H, device="cuda", dtype=torch.bfloat16)
+        if mode == "step":
+            for s in reversed(range(T)):
+                k.lstm_enc_bwd_step(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, s, T, B, H)
+        else:
+            xb = torch.zeros(int(k.lstm_persistent_xbuf(H, B, True)), device="cuda", dtype=torch.long)
+            k.lstm_bwd_persistent(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, xb, err, T, B, H)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        res[mode] = dict(hs=hs.float(), cs=cs, acts=acts, out=out.float(), dz=dz.float(), dc=dcc)
+    a, b = res["step"], res["persistent"]
+    for name, tol in [("hs", 3e-2), ("cs", 3e-2), ("acts", 2e-2), ("out", 3e-2), ("dz", 3e-2), ("dc", 3e-2)]:
+        diff = (a[name] - b[name]).abs()
+        assert diff.max().item() < tol, (name, diff.max().item())
+        assert diff.mean().item() < 2e-3, (name, diff.mean().item())
+    # frozen rows: final state equals the state at their length
+    L = int(lens[-1])
+    assert torch.equal(res["persistent"]["hs"][:, T, -1], res["persistent"]["hs"][:, L, -1])
+
+
+def test_persistent_repeated_launches_reset_tags():
+    """Graph-style replays: the hand-off buffer is zeroed before every launch, so a second
+    launch on the same buffers gives identical results."""
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    H, B, T = 256, 48, 17
+    g, r, lens, gx, Wt, Wn, hs0, cs0 = _setup(H, B, T, 3)
+    xf = torch.zeros(int(k.lstm_persistent_xbuf(H, B, False)), device="cuda", dtype=torch.long)
+    err = torch.zeros(1, device="cuda", dtype=torch.int32)
+    outs = []
+    for _ in range(3):
+        hs, cs = hs0.clone(), cs0.clone()
+        acts = torch.zeros(2, T, B, 4 * H, device="cuda")
+        out = torch.zeros(B, T, 2 * H, device="cuda", dtype=torch.bfloat16)
+        xf.zero_()
+        k.lstm_fwd_persistent(gx, Wt, hs, cs, acts, out, lens, xf, err, T, B, H)
+        outs.append(out.clone())
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])

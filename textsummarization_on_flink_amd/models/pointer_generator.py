@@ -20,6 +20,8 @@ Reference semantics: ``model.py:76-305``, ``attention_decoder.py:27-180``.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, List, Optional
 
 import torch
@@ -108,6 +110,14 @@ class HipPointerGenerator:
                 "dh_fin": z(2, B, H),
                 "dc_carry": z(2, B, H),
             })
+        # persistent weight-resident recurrence (lstm_persistent.hip) when the shape allows
+        # it; TSAMD_LSTM_PERSISTENT=0 forces the per-step kernels
+        self.persistent_lstm = (os.environ.get("TSAMD_LSTM_PERSISTENT", "1") != "0"
+                                and int(self.k.lstm_persistent_grid(H, B)) > 0)
+        if self.persistent_lstm:
+            w["lstm_xf"] = z(int(self.k.lstm_persistent_xbuf(H, B, False)), dt=torch.long)
+            w["lstm_xb"] = z(int(self.k.lstm_persistent_xbuf(H, B, True)), dt=torch.long)
+        w["lstm_err"] = z(1, dt=torch.int32)
         w["F"] = z(B, T, A, dt=BF)
         w["Ft"] = z(B, A, T, dt=BF)   # transposed copies for the lanes-over-positions kernels
         w["Et"] = z(B, A, T, dt=BF)
@@ -250,9 +260,14 @@ class HipPointerGenerator:
             st["hs"][:, 0].zero_()
             st["cs"][:, 0].zero_()
             st["out"].zero_()
-            for s in range(T):
-                k.lstm_enc_fwd_step(st["gx"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"], st["out"],
-                                    lens, s, T, B, H)
+            if self.persistent_lstm:
+                w["lstm_xf"].zero_()  # hand-off tags must start at 0 every launch
+                k.lstm_fwd_persistent(st["gx"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"], st["out"],
+                                      lens, w["lstm_xf"], w["lstm_err"], T, B, H)
+            else:
+                for s in range(T):
+                    k.lstm_enc_fwd_step(st["gx"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"],
+                                        st["out"], lens, s, T, B, H)
             x = st["out"]
         top = self.enc[-1]
         old_c = torch.cat([top["cs"][0, T], top["cs"][1, T]], 1)
@@ -483,9 +498,14 @@ class HipPointerGenerator:
             else:
                 st["dh_fin"].zero_()
                 st["dc_carry"].zero_()
-            for s in reversed(range(T)):
-                k.lstm_enc_bwd_step(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"], st["dc_carry"],
-                                    st["acts"], st["cs"], lens, s, T, B, H)
+            if self.persistent_lstm:
+                w["lstm_xb"].zero_()
+                k.lstm_bwd_persistent(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"], st["dc_carry"],
+                                      st["acts"], st["cs"], lens, w["lstm_xb"], w["lstm_err"], T, B, H)
+            else:
+                for s in reversed(range(T)):
+                    k.lstm_enc_bwd_step(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"],
+                                        st["dc_carry"], st["acts"], st["cs"], lens, s, T, B, H)
             dx = torch.zeros(B, T, din, dtype=F32, device=self.dev)
             for di, d in enumerate(("fw", "bw")):
                 dzd = st["dz"][di].view(T * B, 4 * H)

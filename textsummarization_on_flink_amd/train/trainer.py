@@ -135,6 +135,9 @@ class GraphTrainer:
     def check_finite(self, out) -> Dict[str, float]:
         """Host sync: raise on non-finite loss / skipped update (NaN guard)."""
         vals = {k: float(v) for k, v in out.items()}
+        if int(self.engine.w["lstm_err"].item()):
+            raise RuntimeError("persistent LSTM hand-off timed out (a workgroup was not co-resident); "
+                               "set TSAMD_LSTM_PERSISTENT=0")
         if not all(math.isfinite(v) for v in vals.values()) or int(self.engine.w["nan_flag"].item()):
             raise NonFiniteLossError("Loss is not finite. Stopping.")
         vals["global_norm"] = float(self.engine.w["gnorm"].item())
