@@ -104,7 +104,7 @@ def load_params_into(hps, params):
 
 def main(argv: Optional[Sequence[str]] = None) -> int:
     hps = parse_flags(sys.argv[1:] if argv is None else argv, known_only=True)
-    info = init_from_env() if hps.mode == "train" else DistInfo()
+    info = init_from_env(timeout_s=hps.dist_timeout_s) if hps.mode == "train" else DistInfo()
     vocab, hps = default_setup(hps, info)
     metrics = metrics_for(hps, info)
     try:

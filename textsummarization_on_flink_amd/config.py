@@ -78,6 +78,9 @@ class HParams:
     fault_nan_step: int = -1       # fault injection: NaN gradient at this (relative) step
     fault_kill_step: int = -1      # fault injection: hard-exit rank fault_kill_rank at this step
     fault_kill_rank: int = 0
+    dist_timeout_s: int = 600      # collective timeout: a dead rank surfaces as an error, not a hang
+    profile_phases: bool = False   # per-phase step timing (HIP events) into the metrics JSONL
+    flink_tokenize_article: bool = False  # quirk 4: the Flink path whitespace-splits the raw article
 
     # ------------------------------------------------------------------ helpers
     def replace(self, **kw) -> "HParams":

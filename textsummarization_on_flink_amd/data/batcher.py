@@ -264,6 +264,8 @@ class _StreamBatcher:
     def _example(self, row) -> Example:
         uuid = _ex_text(row.get("uuid"))
         article = _ex_text(row.get("article"))
+        if getattr(self._hps, "flink_tokenize_article", False):
+            article = " ".join(word_tokenize(article))
         reference = _ex_text(row.get("reference"))
         return Example(article, reference_to_sentences(reference), self._vocab, self._hps, uuid=uuid)
 

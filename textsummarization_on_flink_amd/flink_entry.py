@@ -86,9 +86,43 @@ def main_on_flink(context):
     if context.get_role_name() == "ps":
         raise ValueError("ps role is not supported (ps_num must be 0): gradients are all-reduced across workers")
     if hps.mode == "train":
-        info = init_from_env()
+        info = init_from_env(timeout_s=hps.dist_timeout_s)
         training_on_flink(context, hps, info)
     elif hps.mode == "decode":
         inference_on_flink(context, hps)
     else:
         raise ValueError("The 'mode' flag must be one of train/eval/decode")
+
+
+class AbstractFlinkWriter:
+    """Generic result-writer template (``flink_writer.py:40-89``): subclasses name the output
+    fields in ``_fields()``; ``write_result(*values)`` sends one row to the stream."""
+
+    def __init__(self, context):
+        self._w = context.output_writer()
+
+    def _fields(self):
+        raise NotImplementedError
+
+    def write_result(self, *values):
+        self._w.write(dict(zip(self._fields(), values)))
+
+    def close(self):
+        self._w.close()
+
+
+def test_trainer_on_flink(context):
+    """``FlinkTestTrainer`` (``train.py:12-55``): a plumbing stub that only pulls batches from
+    the stream (select it with ``train_map_func="test_trainer_on_flink"``)."""
+    from textsummarization_on_flink_amd import cli
+    from textsummarization_on_flink_amd.data.batcher import FlinkTrainBatcher
+    vocab, hps = cli.default_setup(_hps(context))
+    batcher = FlinkTrainBatcher(context.reader(), vocab, hps)
+    n = 0
+    while True:
+        b = batcher.next_batch()
+        if b is None:
+            break
+        n += 1
+        log.info("pulled batch %d: %s", n, b.uuids)
+    return n

@@ -106,7 +106,9 @@ def run_training(trainer, batcher, hps, info: Optional[DistInfo] = None, saver: 
                 log.info("step %d: seconds for training step: %.3f loss: %f%s", trainer.global_step, dt,
                          vals["loss"], f" coverage_loss: {vals['coverage_loss']:f}" if "coverage_loss" in vals else "")
             if metrics:
-                metrics.log(step=trainer.global_step, step_ms=dt * 1e3, tokens_per_sec=toks / max(dt, 1e-9), **vals)
+                extra = trainer.phase_ms() if getattr(trainer, "timing", False) else {}
+                metrics.log(step=trainer.global_step, step_ms=dt * 1e3, tokens_per_sec=toks / max(dt, 1e-9),
+                            **extra, **vals)
             if saver and info.is_chief and save_model_secs and time.time() - last_save >= save_model_secs:
                 saver.save(trainer.params, trainer.global_step)
                 last_save = time.time()
@@ -142,7 +144,21 @@ def setup_training(hps, vocab, batcher, info: Optional[DistInfo] = None, metrics
             trainer.engine.pack()
         log.info("Restored %s at step %d", latest, trainer.global_step)
     saver = ckpt.Saver(train_dir, max_to_keep=hps.max_to_keep) if info.is_chief else None
+    if info.is_chief:
+        write_embedding_projector(train_dir, vocab)
+    if getattr(hps, "profile_phases", False) and hasattr(trainer, "timing"):
+        trainer.timing = True
     return trainer, run_training(trainer, batcher, hps, info=info, saver=saver, metrics=metrics)
+
+
+def write_embedding_projector(train_dir: str, vocab) -> str:
+    """vocab_metadata.tsv + projector_config.pbtxt for the embedding projector
+    (``model.py:185-197``, ``data.py:93-105``)."""
+    meta = os.path.join(train_dir, "vocab_metadata.tsv")
+    vocab.write_metadata(meta)
+    with open(os.path.join(train_dir, "projector_config.pbtxt"), "w") as f:
+        f.write('embeddings {\n  tensor_name: "seq2seq/embedding/embedding"\n  metadata_path: "%s"\n}\n' % meta)
+    return meta
 
 
 def run_eval(hps, vocab, batcher, max_iters: Optional[int] = None, device: Optional[str] = None,

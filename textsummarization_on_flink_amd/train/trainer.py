@@ -59,6 +59,8 @@ class GraphTrainer:
         self.out = None
         self.global_step = 0
         self.poison_next = False  # fault injection: NaN gradient on the next step (exercises the NaN guard)
+        self.timing = False       # per-phase HIP-event timing (phase_ms)
+        self._ev = None
 
     # ------------------------------------------------------------------ capture
     def _fb(self):
@@ -111,13 +113,22 @@ class GraphTrainer:
         if self.use_graph:
             if self.g_fb is None:
                 self.capture()
+            ev = self._events() if self.timing else None
+            if ev:
+                ev[0].record()
             for i, g in enumerate(self.g_fb):
                 g.replay()
+                if ev:
+                    ev[i + 1].record()
                 if i < 2:
                     self.reducer.bucket_ready(i)
             self._maybe_poison()
             self.reducer()
+            if ev:
+                ev[4].record()
             self.g_opt.replay()
+            if ev:
+                ev[5].record()
             out = self.out
         else:
             out = self._fb()
@@ -126,6 +137,20 @@ class GraphTrainer:
             self._opt()
         self.global_step += 1
         return out
+
+    def _events(self):
+        if self._ev is None:
+            self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        return self._ev
+
+    def phase_ms(self) -> Dict[str, float]:
+        """Time of each phase of the last step (host-synchronising): forward + vocab backward,
+        decoder backward, encoder backward, exposed all-reduce wait, optimizer."""
+        if not self._ev:
+            return {}
+        self._ev[5].synchronize()
+        names = ("ms_fwd_head", "ms_bwd_dec", "ms_bwd_enc", "ms_allreduce", "ms_optimizer")
+        return {n: self._ev[i].elapsed_time(self._ev[i + 1]) for i, n in enumerate(names)}
 
     def _maybe_poison(self):
         if self.poison_next:  # last element: its bucket's all-reduce has not been issued yet
