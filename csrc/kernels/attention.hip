@@ -17,12 +17,27 @@
 // recurrent path only carries ds_t (atomically accumulated across position chunks) and
 // dcov_t.
 #include "common.h"
+#include <stdlib.h>
 
 #define SCORE_POS 128  // positions per block in the lanes-over-positions kernels (2 per lane)
-#define SCORE_WAVES 8  // waves per block; each takes A/8 of the feature axis
+// waves per block (template SW): each takes A/SW of the feature axis.  16 waves (A % 128 == 0)
+// keep 4 waves per SIMD resident at B = 64 -- these kernels are latency-bound there.
 
 __device__ __forceinline__ float lo_bf(uint32_t r) { return __uint_as_float(r << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t r) { return __uint_as_float(r & 0xffff0000u); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// tanh through r = 1 / (1 + 2^(y)), y = 2u*log2(e):  tanh(u) = 1 - 2r,  sech^2(u) = 4 r (1 - r).
+// Scores become  e = sum_k v_k - 2 sum_k v_k r_k  (no clamp needed: 2^y -> inf gives r = 0,
+// 2^y -> 0 gives r = 1), i.e. per element 2 packed FMAs + exp + add + rcp + packed FMA.
+#define K2LOG2E 2.8853900817779268f
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 splat2(float x) { return f32x2{x, x}; }
+__device__ __forceinline__ f32x2 rsig2(f32x2 y) {
+  const f32x2 ex = f32x2{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)} + 1.0f;
+  return f32x2{__builtin_amdgcn_rcpf(ex.x), __builtin_amdgcn_rcpf(ex.y)};
+}
+__device__ __forceinline__ f32x2 bf2pair(uint32_t r) { return f32x2{__uint_as_float(r << 16), __uint_as_float(r & 0xffff0000u)}; }
+
 __device__ __forceinline__ float rdlane(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
@@ -31,11 +46,12 @@ __device__ __forceinline__ float rdlane(float x, int l) {
 // grid (ceil(T/128), B), 512 threads.  Ft: [B][A][T] bf16, T even.  Each lane owns 2
 // positions; the 8 waves split the feature axis; per 8-feature batch all 8 Ft loads
 // are issued before the tanh work and s/v/w_c come in as scalar (s_load) vectors.
-__global__ __launch_bounds__(512) void attn_score_kernel(
+template <int SW>
+__global__ __launch_bounds__(SW * 64) void attn_score_kernel(
     const bf16* __restrict__ Ft, const float* __restrict__ s, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov, const int* __restrict__ lens,
     float* __restrict__ e, int T, int A) {
-  __shared__ float red[SCORE_WAVES][SCORE_POS];
+  __shared__ float red[SW][SCORE_POS];
   const int b = blockIdx.y;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int len = lens[b];
@@ -48,10 +64,12 @@ __global__ __launch_bounds__(512) void attn_score_kernel(
     const float2 cc = *reinterpret_cast<const float2*>(cov + (size_t)b * T + pc);
     c0 = cc.x; c1 = cc.y;
   }
-  const int ka = wid * (A / SCORE_WAVES), kb = ka + A / SCORE_WAVES;
+  const int ka = wid * (A / SW), kb = ka + A / SW;
   const bf16* fp = Ft + ((size_t)b * A) * T + pc;
   const float* sb = s + (size_t)b * A;
-  float e0 = 0.f, e1 = 0.f;
+  f32x2 acc = f32x2{0.f, 0.f};
+  float vsum = 0.f;
+  const f32x2 cc = f32x2{c0, c1};
   for (int k = ka; k < kb; k += 8) {
     uint32_t raw[8];
 #pragma unroll
@@ -70,10 +88,14 @@ __global__ __launch_bounds__(512) void attn_score_kernel(
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      e0 += vk[i] * ftanh(lo_bf(raw[i]) + sk[i] + wk[i] * c0);
-      e1 += vk[i] * ftanh(hi_bf(raw[i]) + sk[i] + wk[i] * c1);
+      // y = 2 log2(e) (F + s_k + w_k cov) for both positions at once
+      const f32x2 base = fma2(splat2(wk[i] * K2LOG2E), cc, splat2(sk[i] * K2LOG2E));
+      const f32x2 y = fma2(bf2pair(raw[i]), splat2(K2LOG2E), base);
+      acc = fma2(splat2(vk[i]), rsig2(y), acc);
+      vsum += vk[i];
     }
   }
+  const float e0 = vsum - 2.0f * acc.x, e1 = vsum - 2.0f * acc.y;
   red[wid][2 * lane] = e0;
   red[wid][2 * lane + 1] = e1;
   __syncthreads();
@@ -81,7 +103,7 @@ __global__ __launch_bounds__(512) void attn_score_kernel(
     const int q = pb + threadIdx.x;
     float r = 0.f;
 #pragma unroll
-    for (int w = 0; w < SCORE_WAVES; ++w) r += red[w][threadIdx.x];
+    for (int w = 0; w < SW; ++w) r += red[w][threadIdx.x];
     if (q < len) e[(size_t)b * T + q] = r;
   }
 }
@@ -164,11 +186,12 @@ __global__ __launch_bounds__(256) void attn_softmax_ctx_kernel(
 
 // ------------------------------------------------------------- backward step: da
 //   da_i = Ga_i + dcov_next_i + g_cl*[a_i <= cov_i] + dctx . E[i,:]     (Et: [B][A][T])
-__global__ __launch_bounds__(512) void attn_bwd_da_kernel(
+template <int SW>
+__global__ __launch_bounds__(SW * 64) void attn_bwd_da_kernel(
     const bf16* __restrict__ Et, const float* __restrict__ dctx, const float* __restrict__ Ga,
     const float* __restrict__ dcov_next, const float* __restrict__ a, const float* __restrict__ cov,
     const float* __restrict__ gcl, const int* __restrict__ lens, float* __restrict__ da, int T, int A) {
-  __shared__ float red[SCORE_WAVES][SCORE_POS];
+  __shared__ float red[SW][SCORE_POS];
   const int b = blockIdx.y;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int len = lens[b];
@@ -176,7 +199,7 @@ __global__ __launch_bounds__(512) void attn_bwd_da_kernel(
   if (pb >= len) return;
   const int p = pb + 2 * lane;
   const int pc = p < T ? p : 0;
-  const int ka = wid * (A / SCORE_WAVES), kb = ka + A / SCORE_WAVES;
+  const int ka = wid * (A / SW), kb = ka + A / SW;
   const bf16* ep = Et + ((size_t)b * A) * T + pc;
   const float* db = dctx + (size_t)b * A;
   float d0 = 0.f, d1 = 0.f;
@@ -202,7 +225,7 @@ __global__ __launch_bounds__(512) void attn_bwd_da_kernel(
       const size_t ix = (size_t)b * T + q;
       float r = 0.f;
 #pragma unroll
-      for (int w = 0; w < SCORE_WAVES; ++w) r += red[w][threadIdx.x];
+      for (int w = 0; w < SW; ++w) r += red[w][threadIdx.x];
       if (Ga) r += Ga[ix];
       if (dcov_next) r += dcov_next[ix];
       if (gcl && a[ix] <= (cov ? cov[ix] : 0.f)) r += gcl[b];
@@ -380,46 +403,61 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
   const int k0 = kbase + lane * 8;
   const bool kok = k0 < A;
   const int p0 = blockIdx.x * 16 + wid * 4;
-  float vk[8], wk[8], adv[8], adw[8];
+  // r-form (see rsig2): with r = 1/(1 + 2^y),
+  //   dF  = 4 v sum_t de r(1-r),  dv = sum_t de - 2 sum_t de r,  dwc = 4 v sum_t de cov r(1-r)
+  f32x2 w2[4], accv[4], accw[4];
+  float vk[8], sum_de = 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool ok = kok && k0 + j < A;
-    vk[j] = ok ? v[k0 + j] : 0.f;
-    wk[j] = (ok && wc) ? wc[k0 + j] : 0.f;
-    adv[j] = 0.f;
-    adw[j] = 0.f;
+  for (int jp = 0; jp < 4; ++jp) {
+    float wv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = 2 * jp + h;
+      const bool ok = kok && k0 + j < A;
+      vk[j] = ok ? v[k0 + j] : 0.f;
+      wv[h] = (ok && wc) ? wc[k0 + j] : 0.f;
+    }
+    w2[jp] = f32x2{wv[0], wv[1]} * K2LOG2E;
+    accv[jp] = f32x2{0.f, 0.f};
+    accw[jp] = f32x2{0.f, 0.f};
   }
+  float adv[8], adw[8];
   if (p0 < len && kok) {
     const int np = min(4, len - p0);
-    float f[4][8], acc[4][8];
+    f32x2 fs[4][4], acc[4][4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int p = min(p0 + q, T - 1);
-      bf16x8 x = ld8(F + ((size_t)b * T + p) * A + k0);
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 fw = __builtin_bit_cast(u32x4, ld8(F + ((size_t)b * T + p) * A + k0));
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        f[q][j] = bf2f(x[j]);
-        acc[q][j] = 0.f;
+      for (int jp = 0; jp < 4; ++jp) {
+        fs[q][jp] = bf2pair(fw[jp]) * K2LOG2E;  // pre-scaled features
+        acc[q][jp] = f32x2{0.f, 0.f};
       }
     }
     for (int t = 0; t < D; ++t) {
       const float* st = S_all + ((size_t)t * B + b) * A + k0;
       const float4 s0 = *reinterpret_cast<const float4*>(st);
       const float4 s1 = *reinterpret_cast<const float4*>(st + 4);
-      const float sk[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const f32x2 s2[4] = {f32x2{s0.x, s0.y} * K2LOG2E, f32x2{s0.z, s0.w} * K2LOG2E,
+                           f32x2{s1.x, s1.y} * K2LOG2E, f32x2{s1.z, s1.w} * K2LOG2E};
       const size_t rb = ((size_t)t * B + b) * T + p0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (q < np) {
           const float de = de_all[rb + q];
           const float c = cov_all ? cov_all[rb + q] : 0.f;
+          const float dec = de * c;
+          sum_de += de;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float th = ftanh(f[q][j] + sk[j] + wk[j] * c);
-            const float g = de * (1.0f - th * th);
-            acc[q][j] += g * vk[j];
-            adv[j] += de * th;
-            adw[j] += g * vk[j] * c;
+          for (int jp = 0; jp < 4; ++jp) {
+            const f32x2 y = fma2(w2[jp], splat2(c), s2[jp]) + fs[q][jp];
+            const f32x2 r = rsig2(y);
+            const f32x2 qv = fma2(-r, r, r);
+            acc[q][jp] = fma2(qv, splat2(de), acc[q][jp]);
+            accv[jp] = fma2(r, splat2(de), accv[jp]);
+            accw[jp] = fma2(qv, splat2(dec), accw[jp]);
           }
         }
       }
@@ -428,10 +466,18 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
     for (int q = 0; q < 4; ++q) {
       if (q < np) {
         float* o = dF + ((size_t)b * T + p0 + q) * A + k0;
-        *reinterpret_cast<float4*>(o) = make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
-        *reinterpret_cast<float4*>(o + 4) = make_float4(acc[q][4], acc[q][5], acc[q][6], acc[q][7]);
+        float r8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r8[j] = 4.0f * vk[j] * acc[q][j >> 1][j & 1];
+        *reinterpret_cast<float4*>(o) = make_float4(r8[0], r8[1], r8[2], r8[3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(r8[4], r8[5], r8[6], r8[7]);
       }
     }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    adv[j] = sum_de - 2.0f * accv[j >> 1][j & 1];
+    adw[j] = 4.0f * vk[j] * accw[j >> 1][j & 1];
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -450,10 +496,20 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
   }
 }
 
+// A/B switch for tuning runs: TSAMD_ATTN_SW=8 forces the 8-wave variants.
+static int attn_sw(int A) {
+  static const int forced = [] { const char* e = getenv("TSAMD_ATTN_SW"); return e ? atoi(e) : 0; }();
+  if (forced == 8) return 8;
+  return A % 128 == 0 ? 16 : 8;
+}
+
 void launch_attn_score(const bf16* Ft, const float* s, const float* v, const float* wc, const float* cov,
                        const int* lens, float* e, int B, int T, int A, hipStream_t st) {
   dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B);
-  hipLaunchKernelGGL(attn_score_kernel, grid, dim3(512), 0, st, Ft, s, v, wc, cov, lens, e, T, A);
+  if (attn_sw(A) == 16)
+    hipLaunchKernelGGL(attn_score_kernel<16>, grid, dim3(1024), 0, st, Ft, s, v, wc, cov, lens, e, T, A);
+  else
+    hipLaunchKernelGGL(attn_score_kernel<8>, grid, dim3(512), 0, st, Ft, s, v, wc, cov, lens, e, T, A);
 }
 void launch_attn_softmax_ctx(const float* e, const bf16* E, const int* lens, const float* cov, float* a_out,
                              float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A,
@@ -466,8 +522,12 @@ void launch_attn_bwd_da(const bf16* Et, const float* dctx, const float* Ga, cons
                         const float* cov, const float* gcl, const int* lens, float* da, int B, int T, int A,
                         hipStream_t st) {
   dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B);
-  hipLaunchKernelGGL(attn_bwd_da_kernel, grid, dim3(512), 0, st, Et, dctx, Ga, dcov_next, a, cov, gcl, lens, da, T,
-                     A);
+  if (attn_sw(A) == 16)
+    hipLaunchKernelGGL(attn_bwd_da_kernel<16>, grid, dim3(1024), 0, st, Et, dctx, Ga, dcov_next, a, cov, gcl, lens, da,
+                       T, A);
+  else
+    hipLaunchKernelGGL(attn_bwd_da_kernel<8>, grid, dim3(512), 0, st, Et, dctx, Ga, dcov_next, a, cov, gcl, lens, da,
+                       T, A);
 }
 int attn_nchunk(int T) { return (T + 63) / 64; }
 void launch_attn_bwd_tanh(const bf16* F, const float* s, const float* v, const float* wc, const float* cov,
