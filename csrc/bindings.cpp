@@ -270,6 +270,29 @@ void final_topk(const Tensor& logits, const Tensor& bias, const OT& pgen, const 
 }
 int64_t topk_parts(int64_t V) { return topk_split(V); }
 
+// fused decode vocab head (vocab_topk.hip): logits never materialised
+void vocab_topk(const Tensor& X, const Tensor& WT, const Tensor& bias, const OT& pgen, const OT& attn,
+                const Tensor& ext, const Tensor& lens, const Tensor& out_ids, const Tensor& out_lp,
+                const Tensor& logits, const Tensor& part_ms, int64_t R, int64_t V, int64_t H, int64_t T, int64_t K,
+                int64_t beam) {
+  chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(ext, I32, "ext"); chk(lens, I32, "lens");
+  chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp"); chk(logits, F32, "logits"); chk(part_ms, F32, "part_ms");
+  const int64_t nt = vocab_topk_tiles((int)V);
+  TORCH_CHECK(K >= 1 && K <= 8 && beam >= 1 && R % beam == 0 && T <= 2048, "bad vocab_topk args (K <= 8)");
+  TORCH_CHECK(H % 32 == 0 && H <= 256 && nt <= 4096, "vocab_topk: H % 32 == 0, H <= 256, V <= 1M");
+  numel_eq(X, R * H, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias");
+  numel_eq(ext, (R / beam) * T, "ext"); numel_eq(lens, R / beam, "lens");
+  numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
+  numel_eq(logits, R * V, "logits"); numel_eq(part_ms, R * nt * 2, "part_ms");
+  chko(pgen, F32, R, "pgen"); chko(attn, F32, R * T, "attn");
+  TORCH_CHECK(!PO<float>(pgen) || PO<float>(attn), "pointer mode needs attn");
+  launch_vocab_topk(P<bf16>(X), P<bf16>(WT), P<float>(bias), PO<float>(pgen), PO<float>(attn), P<int>(ext),
+                    P<int>(lens), P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), R, V, H, T,
+                    K, beam, stream());
+}
+int64_t vocab_topk_parts(int64_t V) { return vocab_topk_tiles((int)V); }
+
+
 void beam_step(const Tensor& top_ids, const Tensor& top_lp, const Tensor& lp_sum, const Tensor& latest,
                const Tensor& gidx, const Tensor& tok_hist, const Tensor& par_hist, const Tensor& done,
                const Tensor& res_count, const Tensor& res_score, const Tensor& res_len, const Tensor& res_step,
@@ -373,5 +396,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("beam_gather", &beam_gather);
   m.def("linear2", &linear2);
   m.def("pgen", &pgen);
+  m.def("vocab_topk", &vocab_topk);
+  m.def("vocab_topk_parts", &vocab_topk_parts);
   m.def("pgen_bwd", &pgen_bwd);
 }

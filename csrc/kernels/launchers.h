@@ -71,3 +71,7 @@ void launch_lstm_fwd_persistent(const float* gx, const bf16* Wt, bf16* hs, float
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, int T, int B, int H, hipStream_t st);
+int vocab_topk_tiles(int V);
+void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
+                       const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
+                       int R, int V, int H, int T, int K, int beam, hipStream_t st);

@@ -193,3 +193,44 @@ def test_pgen_matches_fp32():
     ref = torch.sigmoid(torch.cat([ctx, c, h.float(), x], 1) @ w + b)
     torch.cuda.synchronize()
     assert (pg - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("pointer", [True, False])
+def test_fused_vocab_topk_matches_materialised_path(pointer):
+    """vocab_topk (GEMM + per-tile LSE/top-K epilogue + merge, no logits in HBM) == the
+    materialised-logits GEMM + final_topk path."""
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    torch.manual_seed(5)
+    Na, beam, V, T, K, H = 5, 4, 3000, 96, 8, 128
+    R = Na * beam
+    X = (torch.randn(R, H, device="cuda")).bfloat16()
+    W = (torch.randn(H, V, device="cuda") * 0.3).bfloat16()
+    bias = torch.randn(V, device="cuda")
+    lens = torch.randint(20, T + 1, (Na,), device="cuda", dtype=torch.int32)
+    ext = torch.randint(0, V + 20, (Na, T), device="cuda", dtype=torch.int32)
+    ext[:, :10] = ext[:, 10:20]
+    pg = torch.rand(R, device="cuda") if pointer else None
+    attn = None
+    if pointer:
+        attn = torch.rand(R, T, device="cuda")
+        mask = (torch.arange(T, device="cuda")[None] < lens.repeat_interleave(beam)[:, None]).float()
+        attn = attn * mask
+        attn = attn / attn.sum(1, keepdim=True)
+    logits = torch.mm(X, W, out_dtype=torch.float32)
+    S = int(k.topk_parts(V))
+    ids0 = torch.zeros(R, K, dtype=torch.int32, device="cuda")
+    lp0 = torch.zeros(R, K, device="cuda")
+    k.final_topk(logits, bias, pg, attn, ext, lens, ids0, lp0, torch.zeros(R, S, 2, device="cuda"),
+                 torch.zeros(R, S, K, device="cuda"), torch.zeros(R, S, K, dtype=torch.int32, device="cuda"),
+                 R, V, T, K, beam)
+    nt = int(k.vocab_topk_parts(V))
+    ids1 = torch.zeros(R, K, dtype=torch.int32, device="cuda")
+    lp1 = torch.zeros(R, K, device="cuda")
+    lg = torch.zeros(R, V, device="cuda")
+    k.vocab_topk(X, W.t().contiguous(), bias, pg, attn, ext, lens, ids1, lp1, lg, torch.zeros(R, nt, 2, device="cuda"),
+                 R, V, H, T, K, beam)
+    torch.cuda.synchronize()
+    assert (lg - (logits + bias)).abs().max().item() < 1e-3
+    assert torch.equal(ids0, ids1)
+    assert (lp0 - lp1).abs().max().item() < 1e-3

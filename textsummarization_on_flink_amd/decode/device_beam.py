@@ -21,6 +21,8 @@ unchanged: cov'_t = cov'_{t-1}[parent] + a_{t-1}[parent].
 """
 from __future__ import annotations
 
+import os
+
 from typing import List
 
 import numpy as np
@@ -75,6 +77,12 @@ class DeviceBeamDecoder:
             ("part_i", (R, int(self.k.topk_parts(V)), K), torch.int32),
         ]:
             b[name] = z(*shape, dt=dt)
+        # fused vocab head (vocab_topk.hip) partials; TSAMD_FUSED_VOCAB=0 selects the
+        # materialised-logits path (GEMM + final_topk) instead
+        self.fused_vocab = (os.environ.get("TSAMD_FUSED_VOCAB", "1") != "0" and self.K <= 8
+                            and self.eng.H <= 256)
+        if self.fused_vocab:
+            b["vpart_ms"] = z(R, int(self.k.vocab_topk_parts(V)), 2)
         # ping-pong decoder state: step t reads set t%2 and writes set (t+1)%2, so a
         # captured 2-step graph needs no copies between steps
         self.st = [{"C": z(R, H), "H": z(R, H, dt=BF), "CTX": z(R, A), "ATT": z(R, T), "COV": z(R, T)}
@@ -93,6 +101,7 @@ class DeviceBeamDecoder:
         self.Xtab = (emb @ p[LIN_M][:E] + p[LIN_B]).contiguous()
         self.XGtab = (self.Xtab @ p[CELL_K][:E] + p[CELL_B]).contiguous()
         self.pg_w = p[PG_M][:, 0].contiguous() if self.hps.pointer_gen else None
+        self.owT = self.eng.pk["ow"].t().contiguous() if self.fused_vocab else None  # [V][H] for the fused head
         self.graph = None
 
     # ------------------------------------------------------------------ per-chunk phases
@@ -148,9 +157,13 @@ class DeviceBeamDecoder:
             k.pgen(Y["CTX"], Y["C"], Y["H"], b["x"], self.pg_w, p[PG_B], b["PG"], R, A, H, E)
             pg = b["PG"]
         k.linear2(Y["H"], H, b["ctx_bf"], A, eng.pk["OUTmT"], p[OUT_B], None, None, b["outb"], R, H)
-        torch.mm(b["outb"], eng.pk["ow"], out_dtype=F32, out=b["logits"])
-        k.final_topk(b["logits"], p[OV], pg, Y["ATT"] if hps.pointer_gen else None, b["ext"], b["lens"],
-                     b["top_ids"], b["top_lp"], b["part_ms"], b["part_v"], b["part_i"], R, V, T, K, self.beam)
+        if self.fused_vocab:
+            k.vocab_topk(b["outb"], self.owT, p[OV], pg, Y["ATT"] if hps.pointer_gen else None, b["ext"], b["lens"],
+                         b["top_ids"], b["top_lp"], b["logits"], b["vpart_ms"], R, V, H, T, K, self.beam)
+        else:
+            torch.mm(b["outb"], eng.pk["ow"], out_dtype=F32, out=b["logits"])
+            k.final_topk(b["logits"], p[OV], pg, Y["ATT"] if hps.pointer_gen else None, b["ext"], b["lens"],
+                         b["top_ids"], b["top_lp"], b["part_ms"], b["part_v"], b["part_i"], R, V, T, K, self.beam)
         if self.keep_attn:
             si = b["step"].long().clamp_(max=self.maxD - 1)
             b["ATT_hist"].index_copy_(0, si, Y["ATT"][None])
