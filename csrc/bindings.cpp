@@ -104,26 +104,31 @@ void lstm_bwd_persistent(const Tensor& dz, const Tensor& Wn, const Tensor& dout,
 }
 
 // ---------------------------------------------------------------- attention
+// rep: rows per F/E row (decode: the beam hypotheses of one article share its encoder
+// features).  F/E hold B/rep rows, s/cov/e/a/ctx hold B rows, lens has B/rep entries.
 void attn_score(const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov, const Tensor& lens,
-                const Tensor& e, int64_t B, int64_t T, int64_t A) {
+                const Tensor& e, int64_t B, int64_t T, int64_t A, int64_t rep) {
   chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens"); chk(e, F32, "e");
   TORCH_CHECK(A % 64 == 0 && A <= 1024 && T % 2 == 0, "attention size must be a multiple of 64 (<= 1024), T even");
-  numel_eq(F, B * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v"); numel_eq(e, B * T, "e");
-  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov");
+  TORCH_CHECK((rep == 1 || rep == 2 || rep == 4) && B % rep == 0, "rep must be 1, 2 or 4 and divide B");
+  numel_eq(F, B / rep * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v"); numel_eq(e, B * T, "e");
+  numel_eq(lens, B / rep, "lens"); chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov");
   launch_attn_score(P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens), P<float>(e), B,
-                    T, A, stream());
+                    T, A, rep, stream());
 }
 
 void attn_softmax_ctx(const Tensor& e, const Tensor& E, const Tensor& lens, const OT& cov, const Tensor& a_out,
                       const OT& cov_out, const OT& covloss, const Tensor& ctx, const OT& ctx_bf, int64_t B, int64_t T,
-                      int64_t A) {
+                      int64_t A, int64_t rep) {
   chk(e, F32, "e"); chk(E, BF, "E"); chk(lens, I32, "lens"); chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
-  TORCH_CHECK(A % 64 == 0 && T <= 2048, "bad attention shape");
-  numel_eq(e, B * T, "e"); numel_eq(E, B * T * A, "E"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx");
+  TORCH_CHECK((rep == 1 || rep == 2 || rep == 4) && B % rep == 0, "rep must be 1, 2 or 4 and divide B");
+  TORCH_CHECK(A % 64 == 0 && T <= (rep == 1 ? 2048 : 1024), "bad attention shape");
+  numel_eq(e, B * T, "e"); numel_eq(E, B / rep * T * A, "E"); numel_eq(a_out, B * T, "a_out");
+  numel_eq(ctx, B * A, "ctx"); numel_eq(lens, B / rep, "lens");
   chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out"); chko(covloss, F32, B, "covloss");
   chko(ctx_bf, BF, B * A, "ctx_bf");
   launch_attn_softmax_ctx(P<float>(e), P<bf16>(E), P<int>(lens), PO<float>(cov), P<float>(a_out), PO<float>(cov_out),
-                          PO<float>(covloss), P<float>(ctx), PO<bf16>(ctx_bf), B, T, A, stream());
+                          PO<float>(covloss), P<float>(ctx), PO<bf16>(ctx_bf), B, T, A, rep, stream());
 }
 
 void attn_bwd_da(const Tensor& E, const Tensor& dctx, const OT& Ga, const OT& dcov_next, const Tensor& a,
@@ -270,7 +275,7 @@ void final_topk(const Tensor& logits, const Tensor& bias, const OT& pgen, const 
 }
 int64_t topk_parts(int64_t V) { return topk_split(V); }
 
-// fused decode vocab head (vocab_topk.hip): logits never materialised
+// fused decode vocab head (vocab_topk.hip): MFMA logits + tile partials, select reads K tiles per row
 void vocab_topk(const Tensor& X, const Tensor& WT, const Tensor& bias, const OT& pgen, const OT& attn,
                 const Tensor& ext, const Tensor& lens, const Tensor& out_ids, const Tensor& out_lp,
                 const Tensor& logits, const Tensor& part_ms, int64_t R, int64_t V, int64_t H, int64_t T, int64_t K,
@@ -293,25 +298,35 @@ void vocab_topk(const Tensor& X, const Tensor& WT, const Tensor& bias, const OT&
 int64_t vocab_topk_parts(int64_t V) { return vocab_topk_tiles((int)V); }
 
 
+// Advances step[0] by one (the last block to finish); ctr: one zeroed uint32 scratch word.
+// att/att_hist/pg/pg_hist (optional): this step's attention rows and p_gen copied into row
+// min(step, max_dec - 1) of the histories.
 void beam_step(const Tensor& top_ids, const Tensor& top_lp, const Tensor& lp_sum, const Tensor& latest,
                const Tensor& gidx, const Tensor& tok_hist, const Tensor& par_hist, const Tensor& done,
                const Tensor& res_count, const Tensor& res_score, const Tensor& res_len, const Tensor& res_step,
-               const Tensor& res_par, const Tensor& step, int64_t Na, int64_t beam, int64_t K, int64_t stop_id,
+               const Tensor& res_par, const Tensor& step, const Tensor& ctr, const OT& att, const OT& att_hist,
+               const OT& pg, const OT& pg_hist, int64_t T, int64_t Na, int64_t beam, int64_t K, int64_t stop_id,
                int64_t min_dec, int64_t max_dec) {
   chk(top_ids, I32, "top_ids"); chk(top_lp, F32, "top_lp"); chk(lp_sum, F32, "lp_sum"); chk(latest, I32, "latest");
   chk(gidx, I32, "gidx"); chk(tok_hist, I32, "tok_hist"); chk(par_hist, I32, "par_hist"); chk(done, I32, "done");
   chk(res_count, I32, "res_count"); chk(res_score, F32, "res_score"); chk(res_len, I32, "res_len");
-  chk(res_step, I32, "res_step"); chk(res_par, I32, "res_par"); chk(step, I32, "step");
+  chk(res_step, I32, "res_step"); chk(res_par, I32, "res_par"); chk(step, I32, "step"); chk(ctr, I32, "ctr");
   const int64_t R = Na * beam;
   TORCH_CHECK(beam >= 1 && beam <= 16 && K >= 1 && K <= 16 && beam * K <= 64, "bad beam args");
   numel_eq(top_ids, R * K, "top_ids"); numel_eq(top_lp, R * K, "top_lp"); numel_eq(lp_sum, R, "lp_sum");
   numel_eq(latest, R, "latest"); numel_eq(gidx, R, "gidx"); numel_eq(tok_hist, max_dec * R, "tok_hist");
   numel_eq(par_hist, max_dec * R, "par_hist"); numel_eq(done, Na, "done"); numel_eq(res_count, Na, "res_count");
   numel_eq(res_score, R, "res_score"); numel_eq(res_len, R, "res_len"); numel_eq(res_step, R, "res_step");
-  numel_eq(res_par, R, "res_par"); numel_eq(step, 1, "step");
+  numel_eq(res_par, R, "res_par"); numel_eq(step, 1, "step"); numel_eq(ctr, 1, "ctr");
+  TORCH_CHECK(att.has_value() == att_hist.has_value() && pg.has_value() == pg_hist.has_value() &&
+              (!pg.has_value() || att.has_value()), "att/att_hist and pg/pg_hist come in pairs (pg needs att)");
+  chko(att, F32, R * T, "att"); chko(att_hist, F32, max_dec * R * T, "att_hist");
+  chko(pg, F32, R, "pg"); chko(pg_hist, F32, max_dec * R, "pg_hist");
   launch_beam_step(P<int>(top_ids), P<float>(top_lp), P<float>(lp_sum), P<int>(latest), P<int>(gidx), P<int>(tok_hist),
                    P<int>(par_hist), P<int>(done), P<int>(res_count), P<float>(res_score), P<int>(res_len),
-                   P<int>(res_step), P<int>(res_par), P<int>(step), Na, beam, K, stop_id, min_dec, max_dec, stream());
+                   P<int>(res_step), P<int>(res_par), P<int>(step), (unsigned*)ctr.data_ptr(), PO<float>(att),
+                   PO<float>(att_hist), PO<float>(pg), PO<float>(pg_hist), (int)T, Na, beam, K, stop_id, min_dec,
+                   max_dec, stream());
 }
 
 void beam_gather(const Tensor& gidx, const Tensor& latest, const Tensor& c_src, const Tensor& h_src,

@@ -43,40 +43,44 @@ __device__ __forceinline__ float rdlane(float x, int l) {
 }
 
 // ---------------------------------------------------------------- forward: scores
-// grid (ceil(T/128), B), 512 threads.  Ft: [B][A][T] bf16, T even.  Each lane owns 2
-// positions; the 8 waves split the feature axis; per 8-feature batch all 8 Ft loads
-// are issued before the tanh work and s/v/w_c come in as scalar (s_load) vectors.
-template <int SW>
+// grid (ceil(T/128), B / REP), SW*64 threads.  Ft: [B/REP][A][T] bf16, T even.  Each lane owns
+// 2 positions; the SW waves split the feature axis; per 8-feature batch all 8 Ft loads are
+// issued before the tanh work and s/v/w_c come in as wave-uniform vectors.  REP rows share
+// one Ft row (beam search: the beam hypotheses of an article attend over the same encoder
+// features), so Ft is read once per article instead of once per hypothesis.
+template <int SW, int REP>
 __global__ __launch_bounds__(SW * 64) void attn_score_kernel(
     const bf16* __restrict__ Ft, const float* __restrict__ s, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov, const int* __restrict__ lens,
     float* __restrict__ e, int T, int A) {
-  __shared__ float red[SW][SCORE_POS];
-  const int b = blockIdx.y;
+  __shared__ float red[SW][REP][SCORE_POS];
+  const int b = blockIdx.y;  // Ft row (article)
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int len = lens[b];
   const int pb = blockIdx.x * SCORE_POS;
   if (pb >= len) return;  // uniform: masked positions are never read by the softmax
   const int p = pb + 2 * lane;
   const int pc = p < T ? p : 0;
-  float c0 = 0.f, c1 = 0.f;
-  if (cov) {
-    const float2 cc = *reinterpret_cast<const float2*>(cov + (size_t)b * T + pc);
-    c0 = cc.x; c1 = cc.y;
+  f32x2 cc[REP];
+#pragma unroll
+  for (int q = 0; q < REP; ++q) {
+    cc[q] = f32x2{0.f, 0.f};
+    if (cov) {
+      const float2 c2 = *reinterpret_cast<const float2*>(cov + ((size_t)b * REP + q) * T + pc);
+      cc[q] = f32x2{c2.x, c2.y};
+    }
   }
   const int ka = wid * (A / SW), kb = ka + A / SW;
   const bf16* fp = Ft + ((size_t)b * A) * T + pc;
-  const float* sb = s + (size_t)b * A;
-  f32x2 acc = f32x2{0.f, 0.f};
+  f32x2 acc[REP];
+#pragma unroll
+  for (int q = 0; q < REP; ++q) acc[q] = f32x2{0.f, 0.f};
   float vsum = 0.f;
-  const f32x2 cc = f32x2{c0, c1};
   for (int k = ka; k < kb; k += 8) {
     uint32_t raw[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) raw[i] = *reinterpret_cast<const uint32_t*>(fp + (size_t)(k + i) * T);
-    float sk[8], vk[8], wk[8];
-    *reinterpret_cast<float4*>(sk) = *reinterpret_cast<const float4*>(sb + k);
-    *reinterpret_cast<float4*>(sk + 4) = *reinterpret_cast<const float4*>(sb + k + 4);
+    float vk[8], wk[8];
     *reinterpret_cast<float4*>(vk) = *reinterpret_cast<const float4*>(v + k);
     *reinterpret_cast<float4*>(vk + 4) = *reinterpret_cast<const float4*>(v + k + 4);
     if (wc) {
@@ -87,100 +91,133 @@ __global__ __launch_bounds__(SW * 64) void attn_score_kernel(
       for (int i = 0; i < 8; ++i) wk[i] = 0.f;
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      // y = 2 log2(e) (F + s_k + w_k cov) for both positions at once
-      const f32x2 base = fma2(splat2(wk[i] * K2LOG2E), cc, splat2(sk[i] * K2LOG2E));
-      const f32x2 y = fma2(bf2pair(raw[i]), splat2(K2LOG2E), base);
-      acc = fma2(splat2(vk[i]), rsig2(y), acc);
-      vsum += vk[i];
+    for (int i = 0; i < 8; ++i) vsum += vk[i];
+#pragma unroll
+    for (int q = 0; q < REP; ++q) {
+      const float* sb = s + ((size_t)b * REP + q) * A;
+      float sk[8];
+      *reinterpret_cast<float4*>(sk) = *reinterpret_cast<const float4*>(sb + k);
+      *reinterpret_cast<float4*>(sk + 4) = *reinterpret_cast<const float4*>(sb + k + 4);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        // y = 2 log2(e) (F + s_k + w_k cov) for both positions at once
+        const f32x2 base = fma2(splat2(wk[i] * K2LOG2E), cc[q], splat2(sk[i] * K2LOG2E));
+        const f32x2 y = fma2(bf2pair(raw[i]), splat2(K2LOG2E), base);
+        acc[q] = fma2(splat2(vk[i]), rsig2(y), acc[q]);
+      }
     }
   }
-  const float e0 = vsum - 2.0f * acc.x, e1 = vsum - 2.0f * acc.y;
-  red[wid][2 * lane] = e0;
-  red[wid][2 * lane + 1] = e1;
+#pragma unroll
+  for (int q = 0; q < REP; ++q) {
+    red[wid][q][2 * lane] = vsum - 2.0f * acc[q].x;
+    red[wid][q][2 * lane + 1] = vsum - 2.0f * acc[q].y;
+  }
   __syncthreads();
-  if (threadIdx.x < SCORE_POS) {
-    const int q = pb + threadIdx.x;
+  for (int t = threadIdx.x; t < REP * SCORE_POS; t += SW * 64) {
+    const int q = t / SCORE_POS, pp = t % SCORE_POS, pos = pb + pp;
     float r = 0.f;
 #pragma unroll
-    for (int w = 0; w < SW; ++w) r += red[w][threadIdx.x];
-    if (q < len) e[(size_t)b * T + q] = r;
+    for (int w = 0; w < SW; ++w) r += red[w][q][pp];
+    if (pos < len) e[((size_t)b * REP + q) * T + pos] = r;
   }
 }
 
 // ------------------------------------------------- forward: softmax, coverage, context
-// grid (A/64 feature chunks, B).  Every block recomputes the row softmax (T floats);
-// block x==0 also publishes a_t, cov_{t+1} and the coverage loss of this step.
+// grid (A/64 feature chunks, B / REP).  Every block recomputes the softmax of its REP rows
+// (T floats each); block x==0 also publishes a_t, cov_{t+1} and the coverage loss.  The REP
+// rows share one E row, read once for all of them.
 #define MAXT 2048
+template <int REP>
 __global__ __launch_bounds__(256) void attn_softmax_ctx_kernel(
     const float* __restrict__ e, const bf16* __restrict__ E, const int* __restrict__ lens,
     const float* __restrict__ cov, float* __restrict__ a_out, float* __restrict__ cov_out,
     float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T, int A) {
-  __shared__ float sa[MAXT];
+  __shared__ float sa[REP][MAXT / (REP > 1 ? 2 : 1)];
   __shared__ float red[8];
-  __shared__ float part[4][64];
-  const int b = blockIdx.y;
+  __shared__ float part[4][REP][64];
+  const int b = blockIdx.y;  // E row (article)
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = lens[b];
-  const float* er = e + (size_t)b * T;
-  float m = -INFINITY;
-  for (int i = tid; i < len; i += 256) m = fmaxf(m, er[i]);
-  m = block_max<256>(m, red);
-  float sum = 0.f;
-  for (int i = tid; i < len; i += 256) {
-    float x = fexp(er[i] - m);
-    sa[i] = x;
-    sum += x;
+#pragma unroll
+  for (int q = 0; q < REP; ++q) {
+    const size_t row = (size_t)b * REP + q;
+    const float* er = e + row * T;
+    float m = -INFINITY;
+    for (int i = tid; i < len; i += 256) m = fmaxf(m, er[i]);
+    m = block_max<256>(m, red);
+    float sum = 0.f;
+    for (int i = tid; i < len; i += 256) {
+      float x = fexp(er[i] - m);
+      sa[q][i] = x;
+      sum += x;
+    }
+    sum = block_sum<256>(sum, red);
+    const float inv = 1.0f / sum;
+    for (int i = tid; i < len; i += 256) sa[q][i] *= inv;
   }
-  sum = block_sum<256>(sum, red);
-  const float inv = 1.0f / sum;
-  for (int i = tid; i < len; i += 256) sa[i] *= inv;
   __syncthreads();
   if (blockIdx.x == 0) {
-    float cl = 0.f;
-    for (int i = tid; i < T; i += 256) {
-      const float a = i < len ? sa[i] : 0.f;
-      a_out[(size_t)b * T + i] = a;
-      if (cov_out) {
-        const float c = cov ? cov[(size_t)b * T + i] : 0.f;
-        cov_out[(size_t)b * T + i] = c + a;
-        cl += fminf(a, c);
+#pragma unroll
+    for (int q = 0; q < REP; ++q) {
+      const size_t row = (size_t)b * REP + q;
+      float cl = 0.f;
+      for (int i = tid; i < T; i += 256) {
+        const float a = i < len ? sa[q][i] : 0.f;
+        a_out[row * T + i] = a;
+        if (cov_out) {
+          const float c = cov ? cov[row * T + i] : 0.f;
+          cov_out[row * T + i] = c + a;
+          cl += fminf(a, c);
+        }
       }
-    }
-    if (covloss) {
-      cl = block_sum<256>(cl, red);
-      if (tid == 0) covloss[b] = cl;
+      if (covloss) {
+        cl = block_sum<256>(cl, red);
+        if (tid == 0) covloss[row] = cl;
+      }
     }
   }
   // context: 64 features per block; lane = (pos sub-index 0..7, feature group 0..7)
   const int f0 = blockIdx.x * 64;
   const int ps = lane >> 3, fg = lane & 7;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float acc[REP][8];
+#pragma unroll
+  for (int q = 0; q < REP; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
   const bf16* Eb = E + (size_t)b * T * A + f0 + fg * 8;
 #pragma unroll 4
   for (int i = wid * 8 + ps; i < len; i += 32) {
-    const float a = sa[i];
     bf16x8 x = ld8(Eb + (size_t)i * A);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += a * bf2f(x[j]);
+    for (int q = 0; q < REP; ++q) {
+      const float a = sa[q][i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[q][j] += a * bf2f(x[j]);
+    }
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float x = acc[j];
-    x += __shfl_xor(x, 8, 64);
-    x += __shfl_xor(x, 16, 64);
-    x += __shfl_xor(x, 32, 64);
-    acc[j] = x;
-  }
+  for (int q = 0; q < REP; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = acc[q][j];
+      x += __shfl_xor(x, 8, 64);
+      x += __shfl_xor(x, 16, 64);
+      x += __shfl_xor(x, 32, 64);
+      acc[q][j] = x;
+    }
   if (ps == 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) part[wid][fg * 8 + j] = acc[j];
+    for (int q = 0; q < REP; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part[wid][q][fg * 8 + j] = acc[q][j];
   }
   __syncthreads();
-  if (tid < 64) {
-    const float c = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
-    ctx[(size_t)b * A + f0 + tid] = c;
-    if (ctx_bf) ctx_bf[(size_t)b * A + f0 + tid] = f2bf(c);
+  if (tid < 64 * REP) {
+    const int q = tid >> 6, f = tid & 63;
+    const size_t row = (size_t)b * REP + q;
+    const float c = part[0][q][f] + part[1][q][f] + part[2][q][f] + part[3][q][f];
+    ctx[row * A + f0 + f] = c;
+    if (ctx_bf) ctx_bf[row * A + f0 + f] = f2bf(c);
   }
 }
 
@@ -504,19 +541,25 @@ static int attn_sw(int A) {
 }
 
 void launch_attn_score(const bf16* Ft, const float* s, const float* v, const float* wc, const float* cov,
-                       const int* lens, float* e, int B, int T, int A, hipStream_t st) {
-  dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B);
-  if (attn_sw(A) == 16)
-    hipLaunchKernelGGL(attn_score_kernel<16>, grid, dim3(1024), 0, st, Ft, s, v, wc, cov, lens, e, T, A);
-  else
-    hipLaunchKernelGGL(attn_score_kernel<8>, grid, dim3(512), 0, st, Ft, s, v, wc, cov, lens, e, T, A);
+                       const int* lens, float* e, int B, int T, int A, int rep, hipStream_t st) {
+  dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B / rep);
+  const bool w16 = attn_sw(A) == 16;
+#define LS(SW, RP) hipLaunchKernelGGL((attn_score_kernel<SW, RP>), grid, dim3(SW * 64), 0, st, Ft, s, v, wc, cov, lens, e, T, A)
+  if (rep == 4) { if (w16) LS(16, 4); else LS(8, 4); }
+  else if (rep == 2) { if (w16) LS(16, 2); else LS(8, 2); }
+  else { if (w16) LS(16, 1); else LS(8, 1); }
+#undef LS
 }
 void launch_attn_softmax_ctx(const float* e, const bf16* E, const int* lens, const float* cov, float* a_out,
-                             float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A,
+                             float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A, int rep,
                              hipStream_t st) {
-  dim3 grid(A / 64, B);
-  hipLaunchKernelGGL(attn_softmax_ctx_kernel, grid, dim3(256), 0, st, e, E, lens, cov, a_out, cov_out, covloss, ctx,
-                     ctx_bf, T, A);
+  dim3 grid(A / 64, B / rep);
+#define LC(RP) hipLaunchKernelGGL(attn_softmax_ctx_kernel<RP>, grid, dim3(256), 0, st, e, E, lens, cov, a_out, cov_out, \
+                                  covloss, ctx, ctx_bf, T, A)
+  if (rep == 4) LC(4);
+  else if (rep == 2) LC(2);
+  else LC(1);
+#undef LC
 }
 void launch_attn_bwd_da(const bf16* Et, const float* dctx, const float* Ga, const float* dcov_next, const float* a,
                         const float* cov, const float* gcl, const int* lens, float* da, int B, int T, int A,

@@ -264,26 +264,12 @@ __global__ __launch_bounds__(TOPK_THREADS) void final_topk_merge_kernel(
 }
 
 // ------------------------------------------------------------------ beam bookkeeping
-__global__ __launch_bounds__(64) void beam_step_kernel(
-    const int* __restrict__ top_ids, const float* __restrict__ top_lp,  // [R][K]
-    float* __restrict__ lp_sum,        // [R] in: per live hyp; out: per new hyp
-    int* __restrict__ latest,          // [R] out: token of each new hyp
-    int* __restrict__ gidx,            // [R] out: global row of each new hyp's parent
-    int* __restrict__ tok_hist, int* __restrict__ par_hist,  // [maxD][R]
-    int* __restrict__ done, int* __restrict__ res_count,    // [Na]
-    float* __restrict__ res_score, int* __restrict__ res_len, int* __restrict__ res_step,
-    int* __restrict__ res_par,         // [Na][beam]
-    const int* __restrict__ step, int beam, int K, int stop_id, int min_dec, int max_dec) {
-  __shared__ float cval[64];
-  __shared__ int cid[64];
-  __shared__ int srt[64];
-  const int a = blockIdx.x, lane = threadIdx.x;
-  const int t = *step;
-  const int base = a * beam;
-  if (done[a] || t >= max_dec) {
-    if (lane < beam) gidx[base + lane] = base + lane;
-    return;
-  }
+__device__ __forceinline__ void beam_step_body(
+    const int* __restrict__ top_ids, const float* __restrict__ top_lp, float* __restrict__ lp_sum,
+    int* __restrict__ latest, int* __restrict__ gidx, int* __restrict__ tok_hist, int* __restrict__ par_hist,
+    int* __restrict__ done, int* __restrict__ res_count, float* __restrict__ res_score, int* __restrict__ res_len,
+    int* __restrict__ res_step, int* __restrict__ res_par, float* cval, int* cid, int* srt, int a, int lane, int t,
+    int base, int beam, int K, int stop_id, int min_dec) {
   const int norig = t == 0 ? 1 : beam;
   const int ncand = norig * K;
   float tot = -INFINITY;
@@ -335,6 +321,47 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
       gidx[base + k] = base + par;
       tok_hist[(size_t)t * gridDim.x * beam + base + k] = nh > 0 ? new_tok[kk] : stop_id;
       par_hist[(size_t)t * gridDim.x * beam + base + k] = par;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void beam_step_kernel(
+    const int* __restrict__ top_ids, const float* __restrict__ top_lp,  // [R][K]
+    float* __restrict__ lp_sum,        // [R] in: per live hyp; out: per new hyp
+    int* __restrict__ latest,          // [R] out: token of each new hyp
+    int* __restrict__ gidx,            // [R] out: global row of each new hyp's parent
+    int* __restrict__ tok_hist, int* __restrict__ par_hist,  // [maxD][R]
+    int* __restrict__ done, int* __restrict__ res_count,    // [Na]
+    float* __restrict__ res_score, int* __restrict__ res_len, int* __restrict__ res_step,
+    int* __restrict__ res_par,         // [Na][beam]
+    int* __restrict__ step, unsigned* __restrict__ ctr,  // step advanced by the last block to finish
+    const float* __restrict__ att, float* __restrict__ att_hist,  // optional: [R][T] -> [maxD][R][T]
+    const float* __restrict__ pg, float* __restrict__ pg_hist,    // optional: [R] -> [maxD][R]
+    int T, int beam, int K, int stop_id, int min_dec, int max_dec) {
+  __shared__ float cval[64];
+  __shared__ int cid[64];
+  __shared__ int srt[64];
+  const int a = blockIdx.x, lane = threadIdx.x;
+  const int t = *step;
+  const int base = a * beam;
+  const size_t R = (size_t)gridDim.x * beam;
+  if (att_hist) {  // attention / p_gen history for the visualiser, row t (clamped)
+    const size_t th = (size_t)min(t, max_dec - 1);
+    for (int i = lane; i < beam * T; i += 64) att_hist[(th * R + base) * T + i] = att[(size_t)base * T + i];
+    if (pg_hist && lane < beam) pg_hist[th * R + base + lane] = pg[base + lane];
+  }
+  if (done[a] || t >= max_dec) {
+    if (lane < beam) gidx[base + lane] = base + lane;
+  } else {
+    beam_step_body(top_ids, top_lp, lp_sum, latest, gidx, tok_hist, par_hist, done, res_count, res_score, res_len,
+                   res_step, res_par, cval, cid, srt, a, lane, t, base, beam, K, stop_id, min_dec);
+  }
+  // grid-wide step advance: every block read *step above; the last one to arrive bumps it
+  if (lane == 0) {
+    __threadfence();
+    if (atomicAdd(ctr, 1u) == gridDim.x - 1) {
+      *step = t + 1;
+      *ctr = 0u;
     }
   }
 }
@@ -398,9 +425,10 @@ void launch_final_topk(const float* logits, const float* bias, const float* pgen
 
 void launch_beam_step(const int* top_ids, const float* top_lp, float* lp_sum, int* latest, int* gidx, int* tok_hist,
                       int* par_hist, int* done, int* res_count, float* res_score, int* res_len, int* res_step,
-                      int* res_par, const int* step, int Na, int beam, int K, int stop_id, int min_dec, int max_dec,
+                      int* res_par, int* step, unsigned* ctr, const float* att, float* att_hist, const float* pg,
+                      float* pg_hist, int T, int Na, int beam, int K, int stop_id, int min_dec, int max_dec,
                       hipStream_t st) {
   hipLaunchKernelGGL(beam_step_kernel, dim3(Na), dim3(64), 0, st, top_ids, top_lp, lp_sum, latest, gidx, tok_hist,
-                     par_hist, done, res_count, res_score, res_len, res_step, res_par, step, beam, K, stop_id, min_dec,
-                     max_dec);
+                     par_hist, done, res_count, res_score, res_len, res_step, res_par, step, ctr, att, att_hist, pg,
+                     pg_hist, T, beam, K, stop_id, min_dec, max_dec);
 }

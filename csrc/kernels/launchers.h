@@ -10,9 +10,9 @@ void launch_lstm_enc_bwd_step(bf16* dz, const bf16* Wn, const float* dout, const
                               hipStream_t st);
 
 void launch_attn_score(const bf16* F, const float* s, const float* v, const float* wc, const float* cov,
-                       const int* lens, float* e, int B, int T, int A, hipStream_t st);
+                       const int* lens, float* e, int B, int T, int A, int rep, hipStream_t st);
 void launch_attn_softmax_ctx(const float* e, const bf16* E, const int* lens, const float* cov, float* a_out,
-                             float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A,
+                             float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A, int rep,
                              hipStream_t st);
 void launch_attn_bwd_da(const bf16* E, const float* dctx, const float* Ga, const float* dcov_next, const float* a,
                         const float* cov, const float* gcl, const int* lens, float* da, int B, int T, int A,
@@ -50,7 +50,8 @@ void launch_final_topk(const float* logits, const float* bias, const float* pgen
 int topk_split(int V);
 void launch_beam_step(const int* top_ids, const float* top_lp, float* lp_sum, int* latest, int* gidx, int* tok_hist,
                       int* par_hist, int* done, int* res_count, float* res_score, int* res_len, int* res_step,
-                      int* res_par, const int* step, int Na, int beam, int K, int stop_id, int min_dec, int max_dec,
+                      int* res_par, int* step, unsigned* ctr, const float* att, float* att_hist, const float* pg,
+                      float* pg_hist, int T, int Na, int beam, int K, int stop_id, int min_dec, int max_dec,
                       hipStream_t st);
 void launch_beam_gather(const int* gidx, const int* latest, const float* c_src, const bf16* h_src,
                         const float* ctx_src, const float* a_src, const float* cov_src, const float* XGtab,

@@ -4,19 +4,19 @@
 //   vocab_logits_kernel grid (ceil(R/64), ceil(V/256)), 4 waves: a 64-row x 256-column tile of
 //                       logits = X . W_out + b by MFMA (K = H), stored fp32 straight from the
 //                       accumulators, plus the tile's per-row (max, sum exp) partials;
-//   vocab_select_kernel grid R: log-sum-exp from the partials; tau = K-th largest TILE max is a
-//                       lower bound of the row's K-th largest logit (tile maxima are distinct
-//                       elements), so one scan keeps only x >= tau (a handful) for the plain
-//                       top-K; then the pointer copy mass (LDS hash) and the exact top-K of the
-//                       extended-vocab final distribution (same argument as final_topk in
-//                       beam.hip: plain top-K union copied ids).
+//   vocab_select_kernel grid R: log-sum-exp from the partials; the K tiles with the largest
+//                       maxima hold the row's plain top-K, so only those K x 256 logits are
+//                       read (x >= tau = K-th largest tile max); then the pointer copy mass
+//                       (LDS hash) and the exact top-K of the extended-vocab final
+//                       distribution (same argument as final_topk in beam.hip: plain top-K
+//                       union copied ids).
 // Replaces a library GEMM + a separate per-element top-k pass over the logits.
 #include "common.h"
 
 #define VT_COLS 256   // vocab columns per workgroup
 #define VT_ROWS 64    // rows per workgroup
 #define VT_K 8        // max K (= 2 * beam, beam <= 4)
-#define VM_CAND 4096  // max nt * K candidates in the merge
+#define VM_CAND 4096  // tile maxima (nt <= 4096), then <= K * VT_COLS survivors + copied ids
 #define VM_HASH 2048
 #define VT_HMAX 256   // hidden size limit of the logits kernel (X tile staged in LDS)
 
@@ -35,7 +35,10 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void vocab_logits_kernel(
+// 36 KB of LDS and <= 128 VGPRs (AGPRs included): 4 workgroups per CU, so the R/64 x V/256
+// tiles of a decode step (784 at R = 256, V = 50k) run in one round instead of 3-per-CU
+// rounds with a 2% tail.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void vocab_logits_kernel(
     const bf16* __restrict__ X,     // [R][H]  output-projection activations (bf16)
     const bf16* __restrict__ WT,    // [V][H]  output_projection/w transposed ("Bt")
     const float* __restrict__ bias, // [V]
@@ -43,8 +46,10 @@ __global__ __launch_bounds__(256) void vocab_logits_kernel(
     float* __restrict__ part_ms,    // [R][nt][2]  per tile (max, sum exp)
     int R, int V, int H) {
   __shared__ float Pm[4][VT_ROWS], Ps[4][VT_ROWS];
-  __shared__ float St[4][16][68];  // per wave: one 16 x 64 row tile, staged for full-line stores
+  // X tile during the MFMA loop; afterwards reused as the per-wave 16 x 64 store staging
   __shared__ __attribute__((aligned(16))) bf16 Xs[VT_ROWS * (VT_HMAX + 8)];
+  static_assert(sizeof(float) * 4 * 16 * 68 <= sizeof(bf16) * VT_ROWS * (VT_HMAX + 8), "staging alias");
+  float (*St)[16][68] = reinterpret_cast<float (*)[16][68]>(Xs);
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // XCD-aware order: the RB row blocks of one vocab tile get block ids equal mod 8 (one XCD
   // under round-robin dealing), so the tile's W^T columns come from HBM once and are then
@@ -87,6 +92,7 @@ __global__ __launch_bounds__(256) void vocab_logits_kernel(
       }
     }
   }
+  __syncthreads();  // every wave is done reading Xs before it becomes the store staging
   // ---- epilogue: + bias, store fp32, per-row (max, sum exp) over this wave's 64 columns.
   // Accumulator (i, j, r) holds row 16i + 4(lane>>4) + r, column 16j + (lane&15).
   float bj[4];
@@ -162,144 +168,189 @@ __global__ __launch_bounds__(256) void vocab_logits_kernel(
 namespace {
 __device__ __forceinline__ int vhslot(int w) { return (int)(((unsigned)w * 2654435761u) >> 21) & (VM_HASH - 1); }
 
-// K rounds of wave arg-max over n LDS entries (selected entries knocked out)
-__device__ __forceinline__ void vselect(float* v, int* id, int n, int K, float* out_v, int* out_i) {
-  const int lane = threadIdx.x & 63;
-  for (int round = 0; round < K; ++round) {
-    float bv = -INFINITY;
-    int bi = 0x7fffffff, bs = -1;
-    for (int q = lane; q < n; q += 64) {
-      const float x = v[q];
-      const int xi = id[q];
-      if (vbetter(x, xi, bv, bi)) { bv = x; bi = xi; bs = q; }
+}  // namespace
+
+#define VS_THREADS 1024
+#define VS_NONE 0x7fffffff  // sentinel id: (-inf, VS_NONE) never beats anything
+
+namespace {
+// Top-K of n4 (multiple of 4, padded with sentinels) LDS entries by rank counting: every
+// entry counts the entries that beat it (value desc, id asc -- a strict order for distinct
+// pairs) with broadcast float4/int4 LDS reads; entries of rank < K land in ov/oi[rank].
+// Used on small, pre-pruned sets (typically K to a few K entries).  ov/oi
+// must be pre-filled with (-inf, VS_NONE).
+// vbetter without short-circuit branches (the rank loop stays straight-line)
+__device__ __forceinline__ int beats(float a, int ai, float x, int xi) {
+  return (int)(a > x) | ((int)(a == x) & (int)(ai < xi));
+}
+
+// order-preserving float -> int key (for LDS atomicMax)
+__device__ __forceinline__ int okey(float f) {
+  const int b = __float_as_int(f);
+  return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float okey_inv(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff); }
+
+__device__ __forceinline__ void rank_select(const float* v, const int* id, int n4, int K, float* ov, int* oi) {
+  for (int i = threadIdx.x; i < n4; i += VS_THREADS) {
+    const float x = v[i];
+    const int xi = id[i];
+    if (xi == VS_NONE) continue;
+    int rank = 0;
+#pragma unroll 4
+    for (int j = 0; j < n4; j += 4) {  // no early exit: the loads stay independent and pipelined
+      const float4 a = *reinterpret_cast<const float4*>(v + j);
+      const int4 b = *reinterpret_cast<const int4*>(id + j);
+      rank += beats(a.x, b.x, x, xi) + beats(a.y, b.y, x, xi) + beats(a.z, b.z, x, xi) + beats(a.w, b.w, x, xi);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64), os = __shfl_xor(bs, o, 64);
-      if (vbetter(ov, oi, bv, bi)) { bv = ov; bi = oi; bs = os; }
+    if (rank < K) {
+      ov[rank] = x;
+      oi[rank] = xi;
     }
-    if (lane == 0) {
-      out_v[round] = bv;
-      out_i[round] = bi;
-      if (bs >= 0) v[bs] = -INFINITY;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  }
+}
+
+__device__ __forceinline__ void pad4(float* v, int* id, int n) {
+  if (threadIdx.x < 4) {
+    v[n + threadIdx.x] = -INFINITY;
+    id[n + threadIdx.x] = VS_NONE;
   }
 }
 }  // namespace
 
-#define VS_THREADS 1024
+// grid R, 1024 threads.  Two global round trips: (partials, copy ids, attention) issued
+// together, then (the K best tiles' logits, the copied words' logits) issued together.
 __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     const float* __restrict__ logits, const float* __restrict__ part_ms, const float* __restrict__ pgen,
     const float* __restrict__ attn, const int* __restrict__ ext, const int* __restrict__ lens,
     int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam, int nt) {
   __shared__ int hkey[VM_HASH];
   __shared__ float hmass[VM_HASH];
-  __shared__ float cv[VM_CAND];
-  __shared__ int ci[VM_CAND];
+  __shared__ __attribute__((aligned(16))) float cv[VM_CAND + 8];
+  __shared__ __attribute__((aligned(16))) int ci[VM_CAND + 8];
   __shared__ float red[16];
-  __shared__ float pv_s[VT_K];
-  __shared__ int pi_s[VT_K];
+  __shared__ float pv_s[3][VT_K];
+  __shared__ int pi_s[3][VT_K];
+  __shared__ int gkey[VT_K], gkey2[VT_K];
   __shared__ int ncand, ncopy;
   const int r = blockIdx.x, tid = threadIdx.x;
   const int art = r / beam;
   const float* z = logits + (size_t)r * V;
-  for (int i = tid; i < VM_HASH; i += VS_THREADS) { hkey[i] = -1; hmass[i] = 0.f; }
-  // tile maxima -> LDS (for tau) and the log-sum-exp
-  float m = -INFINITY;
-  for (int q = tid; q < nt; q += VS_THREADS) {
-    const float mq = part_ms[((size_t)r * nt + q) * 2];
-    cv[q] = mq;
-    ci[q] = q;
-    m = fmaxf(m, mq);
-  }
-  const float M = block_max<VS_THREADS>(m, red);
-  float s = 0.f;
-  for (int q = tid; q < nt; q += VS_THREADS) {
-    const float mq = part_ms[((size_t)r * nt + q) * 2];
-    if (mq > -INFINITY) s += part_ms[((size_t)r * nt + q) * 2 + 1] * fexp(mq - M);
-  }
-  const float lse = M + __logf(block_sum<VS_THREADS>(s, red));
-  if (tid < 64) vselect(cv, ci, nt, K, pv_s, pi_s);  // K-th largest tile max
-  if (tid == 0) { ncand = 0; ncopy = 0; }
-  __syncthreads();
-  const float tau = pv_s[K - 1];
-  __syncthreads();
-  // survivors x >= tau of the row (a handful); vectorised scan
-  const int V4 = V & ~3;
-  constexpr int UNR = 16;  // 16 independent 16-B loads in flight per thread (V <= 64k: one pass)
-  for (int c0 = tid * 4; c0 < V4; c0 += VS_THREADS * 4 * UNR) {
-    float4 x[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int c = c0 + u * VS_THREADS * 4;
-      x[u] = c < V4 ? *reinterpret_cast<const float4*>(z + c) : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-    }
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const float xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (xs[j] >= tau) {
-          const int slot = atomicAdd(&ncand, 1);
-          if (slot < VM_CAND) { cv[slot] = xs[j]; ci[slot] = c0 + u * VS_THREADS * 4 + j; }
-        }
-    }
-  }
-  for (int c = V4 + tid; c < V; c += VS_THREADS)
-    if (z[c] >= tau) {
-      const int slot = atomicAdd(&ncand, 1);
-      if (slot < VM_CAND) { cv[slot] = z[c]; ci[slot] = c; }
-    }
+  constexpr int PPT = VM_CAND / VS_THREADS;  // tile partials per thread (nt <= 4096)
+  constexpr int TPT = 2048 / VS_THREADS;     // source positions per thread (T <= 2048)
+  constexpr int SPT = VM_HASH / VS_THREADS;  // hash slots per thread
+  // ---- round trip 1: tile partials, copy ids and attention, all in flight together
   const float pg = pgen ? pgen[r] : 1.0f;
   const int len = pgen ? lens[art] : 0;
-  for (int i = tid; i < len; i += VS_THREADS) {
-    const int w = ext[(size_t)art * T + i];
-    const float a = attn[(size_t)r * T + i];
+  float2 pm[PPT];
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) {
+    const int q = tid + u * VS_THREADS;
+    pm[u] = q < nt ? *reinterpret_cast<const float2*>(part_ms + ((size_t)r * nt + q) * 2) : make_float2(-INFINITY, 0.f);
+  }
+  int ew[TPT];
+  float ea[TPT];
+#pragma unroll
+  for (int u = 0; u < TPT; ++u) {
+    const int i = tid + u * VS_THREADS;
+    ew[u] = i < len ? ext[(size_t)art * T + i] : -1;
+    ea[u] = i < len ? attn[(size_t)r * T + i] : 0.f;
+  }
+  for (int i = tid; i < VM_HASH; i += VS_THREADS) { hkey[i] = -1; hmass[i] = 0.f; }
+  if (tid < 3 * VT_K) { (&pv_s[0][0])[tid] = -INFINITY; (&pi_s[0][0])[tid] = VS_NONE; }
+  if (tid == 0) { ncand = 0; ncopy = 0; }
+  if (tid < VT_K) { gkey[tid] = okey(-INFINITY); gkey2[tid] = okey(-INFINITY); }
+  float m = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) m = fmaxf(m, pm[u].x);
+  __syncthreads();  // hash cleared before the inserts below
+  // pointer copy mass per extended-vocab word (LDS hash)
+#pragma unroll
+  for (int u = 0; u < TPT; ++u) {
+    const int w = ew[u];
+    if (w < 0) continue;
     int h = vhslot(w);
     for (int probe = 0; probe < VM_HASH; ++probe) {
       const int prev = atomicCAS(&hkey[h], -1, w);
       if (prev == -1 || prev == w) {
-        atomicAdd(&hmass[h], a);
+        atomicAdd(&hmass[h], ea[u]);
         break;
       }
       h = (h + 1) & (VM_HASH - 1);
     }
   }
-  __syncthreads();
-  const int nc = ncand;
-  if (nc > VM_CAND) {  // pathological ties: exact fallback by K-round full scans (wave 0)
-    if (tid < 64) {
-      for (int round = 0; round < K; ++round) {
-        float bv = -INFINITY;
-        int bi = 0x7fffffff;
-        for (int c = tid; c < V; c += 64) {
-          const float x = z[c];
-          bool taken = false;
-          for (int p = 0; p < round; ++p) taken |= (pi_s[p] == c);
-          if (!taken && vbetter(x, c, bv, bi)) { bv = x; bi = c; }
-        }
+  // log-sum-exp of the row from the partials
+  const float M = block_max<VS_THREADS>(m, red);
+  float s = 0.f;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const float ov = __shfl_xor(bv, o, 64);
-          const int oi = __shfl_xor(bi, o, 64);
-          if (vbetter(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-        }
-        if (tid == 0) { pv_s[round] = bv; pi_s[round] = bi; }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      }
+  for (int u = 0; u < PPT; ++u)
+    if (pm[u].x > -INFINITY) s += pm[u].y * fexp(pm[u].x - M);
+  // prune the tiles: the maxima of K disjoint tile groups (q mod K) are K distinct tile maxima,
+  // so their minimum is <= the K-th largest tile max; only tiles at or above it can matter
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) {
+    const int q = tid + u * VS_THREADS;
+    if (q < nt) atomicMax(&gkey[q % K], okey(pm[u].x));
+  }
+  const float lse = M + __logf(block_sum<VS_THREADS>(s, red));  // (its syncs also close the hash inserts)
+  float gmin = INFINITY;
+  for (int g = 0; g < K; ++g) gmin = fminf(gmin, okey_inv(gkey[g]));
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) {
+    const int q = tid + u * VS_THREADS;
+    if (q < nt && pm[u].x >= gmin) {
+      const int slot = atomicAdd(&ncand, 1);
+      cv[slot] = pm[u].x;
+      ci[slot] = q;
     }
-  } else if (tid < 64) {
-    vselect(cv, ci, nc, K, pv_s, pi_s);
   }
   __syncthreads();
+  const int ntile = ncand;
+  pad4(cv, ci, ntile);
+  __syncthreads();
+  // the K tiles with the largest maxima hold the plain top-K (value desc, index asc): an
+  // element of any other tile is <= its tile max <= tau, and each selected tile max beats it
+  rank_select(cv, ci, (ntile + 3) & ~3, K, pv_s[0], pi_s[0]);
+  __syncthreads();
+  if (tid == 0) ncand = 0;
+  const float tau = pv_s[0][K - 1];
+  // ---- round trip 2: the K selected tiles' logits and the copied words' logits
+  constexpr int EPT = VT_K * VT_COLS / VS_THREADS;
+  float zs[EPT];
+  int cs[EPT];
+#pragma unroll
+  for (int u = 0; u < EPT; ++u) {
+    const int e = tid + u * VS_THREADS;
+    const int tq = e < K * VT_COLS ? pi_s[0][e / VT_COLS] : VS_NONE;
+    cs[u] = tq < nt ? tq * VT_COLS + (e % VT_COLS) : V;
+    zs[u] = cs[u] < V ? z[cs[u]] : -INFINITY;
+  }
+  int wk[SPT];
+  float zk[SPT];
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) {
+    wk[u] = hkey[tid + VS_THREADS * u];
+    zk[u] = (wk[u] >= 0 && wk[u] < V) ? z[wk[u]] : -INFINITY;
+  }
+  __syncthreads();  // ncand reset and the tile list read by everyone before the appends
+#pragma unroll
+  for (int u = 0; u < EPT; ++u)
+    if (cs[u] < V && zs[u] >= tau) {
+      const int slot = atomicAdd(&ncand, 1);
+      cv[slot] = zs[u];
+      ci[slot] = cs[u];
+    }
+  __syncthreads();
+  const int nc = ncand;
+  pad4(cv, ci, nc);
+  __syncthreads();
+  rank_select(cv, ci, (nc + 3) & ~3, K, pv_s[1], pi_s[1]);  // plain top-K
+  __syncthreads();
+  // final candidates: plain top-K (copied words masked: their entry below is exact) U copied words
   if (tid < K) {
-    const int w = pi_s[tid];
+    const int w = pi_s[1][tid];
     bool incopy = false;
-    if (len > 0) {
+    if (len > 0 && w != VS_NONE) {
       int h = vhslot(w);
       for (int probe = 0; probe < VM_HASH; ++probe) {
         const int kk = hkey[h];
@@ -308,36 +359,44 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
         h = (h + 1) & (VM_HASH - 1);
       }
     }
-    cv[tid] = incopy ? -INFINITY : pg * fexp(pv_s[tid] - lse);
+    cv[tid] = (incopy || w == VS_NONE) ? -INFINITY : pg * fexp(pv_s[1][tid] - lse);
     ci[tid] = w;
   }
+  // every plain top-K word has a final probability >= theta (the smallest plain term
+  // pg * p_vocab among them), so a copied word below theta cannot make the top-K; and the
+  // maxima of K disjoint groups of copied words are K distinct entries, so nothing below
+  // their minimum can either
+  float theta = INFINITY;
+  for (int k = 0; k < K; ++k)
+    theta = fminf(theta, pi_s[1][k] == VS_NONE ? -INFINITY : pg * fexp(pv_s[1][k] - lse));
+  float fin[SPT];
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) {
+    const float pv = (wk[u] >= 0 && wk[u] < V) ? fexp(zk[u] - lse) : 0.f;
+    fin[u] = wk[u] < 0 ? -INFINITY : pg * pv + (1.0f - pg) * hmass[tid + VS_THREADS * u];
+    if (fin[u] >= theta) atomicMax(&gkey2[(tid + VS_THREADS * u) % K], okey(fin[u]));
+  }
   __syncthreads();
-  {
-    // all of this thread's hash slots' logit loads in flight at once (one round trip)
-    constexpr int SPT = VM_HASH / VS_THREADS;
-    int wk[SPT];
-    float zk[SPT];
+  float thr = INFINITY;
+  for (int g = 0; g < K; ++g) thr = fminf(thr, okey_inv(gkey2[g]));
+  thr = fmaxf(thr, theta);
 #pragma unroll
-    for (int u = 0; u < SPT; ++u) {
-      wk[u] = hkey[tid + VS_THREADS * u];
-      zk[u] = (wk[u] >= 0 && wk[u] < V) ? z[wk[u]] : -INFINITY;
-    }
-#pragma unroll
-    for (int u = 0; u < SPT; ++u) {
-      if (wk[u] < 0) continue;
-      const float pv = wk[u] < V ? fexp(zk[u] - lse) : 0.f;
+  for (int u = 0; u < SPT; ++u) {
+    if (wk[u] >= 0 && fin[u] >= thr) {
       const int slot = atomicAdd(&ncopy, 1);
-      cv[K + slot] = pg * pv + (1.0f - pg) * hmass[tid + VS_THREADS * u];
+      cv[K + slot] = fin[u];
       ci[K + slot] = wk[u];
     }
   }
   __syncthreads();
-  if (tid < 64) {
-    vselect(cv, ci, K + ncopy, K, pv_s, pi_s);
-    if (tid < K) {
-      out_ids[(size_t)r * K + tid] = pi_s[tid];
-      out_lp[(size_t)r * K + tid] = __logf(pv_s[tid]);
-    }
+  const int nf = K + ncopy;
+  pad4(cv, ci, nf);
+  __syncthreads();
+  rank_select(cv, ci, (nf + 3) & ~3, K, pv_s[2], pi_s[2]);
+  __syncthreads();
+  if (tid < K) {
+    out_ids[(size_t)r * K + tid] = pi_s[2][tid];
+    out_lp[(size_t)r * K + tid] = __logf(pv_s[2][tid]);
   }
 }
 

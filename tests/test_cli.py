@@ -107,3 +107,23 @@ def test_non_train_mode_requires_logdir(ds):
         cli.main(_flags(tmp, d, vp, "--mode=decode"))
     with pytest.raises(ValueError, match="single_pass"):
         cli.main(_flags(tmp, d, vp, "--mode=train", "--single_pass=1"))
+
+
+def test_debug_watch_names_nonfinite_tensors(ds, monkeypatch, caplog):
+    """--debug (tfdbg has_inf_or_nan): the step whose gradients carry NaN stops training and
+    the report names the offending tensors."""
+    monkeypatch.setattr("torch.cuda.is_available", lambda: False)
+    tmp, d, vp = ds
+    with pytest.raises(NonFiniteLossError, match="has_inf_or_nan"):
+        cli.main(_flags(tmp, d, vp, "--mode=train", "--num_steps=5", "--fault_nan_step=1", "--debug=1"))
+    msgs = [r.getMessage() for r in caplog.records if "has_inf_or_nan" in r.getMessage()]
+    assert msgs and "grad/" in msgs[0]
+
+
+def test_log_file_rotating_handler(ds, monkeypatch):
+    monkeypatch.setattr("torch.cuda.is_available", lambda: False)
+    tmp, d, vp = ds
+    log_file = f"{tmp}/logs/run.log"
+    cli.main(_flags(tmp, d, vp, "--mode=train", "--num_steps=1", f"--log_file={log_file}"))
+    text = open(log_file).read()
+    assert "Starting seq2seq_attention in train mode" in text

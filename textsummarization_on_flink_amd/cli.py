@@ -30,13 +30,15 @@ from .config import HParams, check_hps, parse_flags
 from .data.batcher import Batcher, RawTextBatcher
 from .data.vocab import Vocab
 from .parallel.dist import DistInfo, init_from_env
+from .utils.logs import setup_logging
 
 log = logging.getLogger("textsummarization_on_flink_amd")
 
 
 def default_setup(hps: HParams, info: Optional[DistInfo] = None):
     """run_summarization.py:295-330 -> (vocab, hps)."""
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    setup_logging(logging.INFO, log_file=hps.log_file or None,
+                  rank=info.rank if (info is not None and info.enabled) else None)
     log.info("Starting seq2seq_attention in %s mode...", hps.mode)
     log_root = os.path.join(hps.log_root, hps.exp_name) if hps.exp_name else hps.log_root
     if not os.path.exists(log_root):

@@ -81,6 +81,7 @@ class HParams:
     dist_timeout_s: int = 600      # collective timeout: a dead rank surfaces as an error, not a hang
     profile_phases: bool = False   # per-phase step timing (HIP events) into the metrics JSONL
     flink_tokenize_article: bool = False  # quirk 4: the Flink path whitespace-splits the raw article
+    log_file: str = ""             # rotating log file, 100 MB x 20 (log4j2.xml); one file per rank
 
     # ------------------------------------------------------------------ helpers
     def replace(self, **kw) -> "HParams":

@@ -43,6 +43,9 @@ class DeviceBeamDecoder:
         self.hps, self.vocab, self.p = hps, vocab, params
         self.Na, self.beam = n_articles, hps.beam_size
         self.R = self.Na * self.beam
+        # rows per encoder-feature row in the attention kernels (1, 2 or 4); other beam
+        # sizes fall back to replicating E/F per hypothesis
+        self.rep = self.beam if self.beam in (1, 2, 4) else 1
         self.K = 2 * self.beam
         self.T = T
         self.V = vocab.size()
@@ -62,7 +65,8 @@ class DeviceBeamDecoder:
         z = lambda *s, dt=F32: torch.zeros(*s, dtype=dt, device=self.dev)
         b = {}
         for name, shape, dt in [
-            ("Ft", (R, A, T), BF), ("E", (R, T, A), BF), ("lens_rep", (R,), torch.int32),
+            ("Ft", (R // self.rep, A, T), BF), ("E", (R // self.rep, T, A), BF),
+            ("lens_att", (R // self.rep,), torch.int32),
             ("c", (R, H), F32), ("h", (R, H), BF), ("ctxs", (R, A), F32), ("ctxs_bf", (R, A), BF),
             ("x", (R, E), F32), ("Cb2", (R, H), BF), ("XG", (R, 4 * H), F32), ("act", (R, 4 * H), F32),
             ("s", (R, A), F32), ("e", (R, T), F32),
@@ -71,7 +75,8 @@ class DeviceBeamDecoder:
             ("latest", (R,), torch.int32), ("gidx", (R,), torch.int32), ("tok_hist", (D, R), torch.int32),
             ("par_hist", (D, R), torch.int32), ("done", (Na,), torch.int32), ("res_count", (Na,), torch.int32),
             ("res_score", (R,), F32), ("res_len", (R,), torch.int32), ("res_step", (R,), torch.int32),
-            ("res_par", (R,), torch.int32), ("step", (1,), torch.int32), ("ext", (Na, T), torch.int32),
+            ("res_par", (R,), torch.int32), ("step", (1,), torch.int32), ("step_ctr", (1,), torch.int32),
+            ("ext", (Na, T), torch.int32),
             ("lens", (Na,), torch.int32),
             ("part_ms", (R, int(self.k.topk_parts(V)), 2), F32), ("part_v", (R, int(self.k.topk_parts(V)), K), F32),
             ("part_i", (R, int(self.k.topk_parts(V)), K), torch.int32),
@@ -110,9 +115,12 @@ class DeviceBeamDecoder:
         eng.set_batch(batch)
         eng._encoder_forward()
         w = eng.w
-        b["E"].copy_(eng.enc[-1]["out"].repeat_interleave(beam, 0))
-        b["Ft"].copy_(w["Ft"].repeat_interleave(beam, 0))
-        b["lens_rep"].copy_(w["enc_lens"].repeat_interleave(beam, 0))
+        # encoder features stay one row per article: the attention kernels read them once for
+        # all ``beam`` hypotheses of the article (rep = beam)
+        r = beam // self.rep
+        b["E"].copy_(eng.enc[-1]["out"].repeat_interleave(r, 0) if r > 1 else eng.enc[-1]["out"])
+        b["Ft"].copy_(w["Ft"].repeat_interleave(r, 0) if r > 1 else w["Ft"])
+        b["lens_att"].copy_(w["enc_lens"].repeat_interleave(r, 0) if r > 1 else w["enc_lens"])
         b["lens"].copy_(w["enc_lens"])
         b["ext"].copy_(w["ext"])
         X = self.st[0]
@@ -126,13 +134,13 @@ class DeviceBeamDecoder:
         X = self.st[0]
         b["Cb2"].copy_(X["C"])
         k.dec_sproj(b["Cb2"], X["H"], eng.pk["WsT"], self.p[ATT_B], b["s"], R, H, A)
-        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], None, b["lens_rep"], b["e"], R, T, A)
-        k.attn_softmax_ctx(b["e"], b["E"], b["lens_rep"], None, X["ATT"], None, None, X["CTX"], None, R, T, A)
+        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], None, b["lens_att"], b["e"], R, T, A, self.rep)
+        k.attn_softmax_ctx(b["e"], b["E"], b["lens_att"], None, X["ATT"], None, None, X["CTX"], None, R, T, A, self.rep)
         X["COV"].zero_()
         b["gidx"].copy_(torch.arange(R, dtype=torch.int32, device=self.dev))
         b["latest"].fill_(self.vocab.word2id(START_DECODING))
         b["lp_sum"].zero_()
-        for n in ("done", "res_count", "step", "tok_hist", "par_hist", "res_len", "res_step", "res_par"):
+        for n in ("done", "res_count", "step", "step_ctr", "tok_hist", "par_hist", "res_len", "res_step", "res_par"):
             b[n].zero_()
         b["res_score"].fill_(-float("inf"))
 
@@ -147,9 +155,10 @@ class DeviceBeamDecoder:
         k.dec_cell_fwd(b["XG"], b["ctxs_bf"], b["h"], b["c"], eng.pk["WcT2"], Y["C"], b["Cb2"], Y["H"], b["act"],
                        R, H, A)
         k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
-        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], Y["COV"] if cov else None, b["lens_rep"],
-                     b["e"], R, T, A)
-        k.attn_softmax_ctx(b["e"], b["E"], b["lens_rep"], None, Y["ATT"], None, None, Y["CTX"], b["ctx_bf"], R, T, A)
+        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], Y["COV"] if cov else None, b["lens_att"],
+                     b["e"], R, T, A, self.rep)
+        k.attn_softmax_ctx(b["e"], b["E"], b["lens_att"], None, Y["ATT"], None, None, Y["CTX"], b["ctx_bf"], R, T, A,
+                           self.rep)
         pg = None
         if hps.pointer_gen:
             # x = x0 + ctx* . W_in[E:]  (x0 = emb . W_in[:E] + b_in gathered per token)
@@ -164,15 +173,13 @@ class DeviceBeamDecoder:
             torch.mm(b["outb"], eng.pk["ow"], out_dtype=F32, out=b["logits"])
             k.final_topk(b["logits"], p[OV], pg, Y["ATT"] if hps.pointer_gen else None, b["ext"], b["lens"],
                          b["top_ids"], b["top_lp"], b["part_ms"], b["part_v"], b["part_i"], R, V, T, K, self.beam)
-        if self.keep_attn:
-            si = b["step"].long().clamp_(max=self.maxD - 1)
-            b["ATT_hist"].index_copy_(0, si, Y["ATT"][None])
-            if pg is not None:
-                b["PG_hist"].index_copy_(0, si, b["PG"][None])
+        # beam bookkeeping; also appends a_t / p_gen to the histories and advances b["step"]
+        hist = self.keep_attn
         k.beam_step(b["top_ids"], b["top_lp"], b["lp_sum"], b["latest"], b["gidx"], b["tok_hist"], b["par_hist"],
                     b["done"], b["res_count"], b["res_score"], b["res_len"], b["res_step"], b["res_par"], b["step"],
-                    self.Na, self.beam, K, self.vocab.word2id(STOP_DECODING), hps.min_dec_steps, self.maxD)
-        b["step"].add_(1)
+                    b["step_ctr"], Y["ATT"] if hist else None, b["ATT_hist"] if hist else None,
+                    pg if (hist and pg is not None) else None, b["PG_hist"] if (hist and pg is not None) else None,
+                    T, self.Na, self.beam, K, self.vocab.word2id(STOP_DECODING), hps.min_dec_steps, self.maxD)
 
     def _two_steps(self):
         self._step(0)

@@ -299,9 +299,9 @@ class HipPointerGenerator:
                            w["Cst"][t + 1], w["Cb"][t + 1], w["Hb"][t + 1], w["ACT"][t], B, H, A)
             k.dec_sproj(w["Cb"][t + 1], w["Hb"][t + 1], self.pk["WsT"], self.p[ATT_B], w["S"][t], B, H, A)
             cov_in = w["COV"][t] if (cov and t > 0) else None
-            k.attn_score(Ft, w["S"][t], v, wc, cov_in, lens, w["e"], B, T, A)
+            k.attn_score(Ft, w["S"][t], v, wc, cov_in, lens, w["e"], B, T, A, 1)
             k.attn_softmax_ctx(w["e"], enc_out, lens, cov_in, w["ATT"][t], w["COV"][t + 1] if cov else None,
-                               w["covloss"][t] if cov else None, w["CTX"][t], w["CTXb"][t], B, T, A)
+                               w["covloss"][t] if cov else None, w["CTX"][t], w["CTXb"][t], B, T, A, 1)
         # x_t = xe_t + ctx_{t-1} . W_in[E:]  (rebuilt after the loop, one GEMM)
         w["X"].copy_(w["xe"])
         if D > 1:

@@ -95,6 +95,13 @@ class CpuTrainer:
         vals["global_norm"] = self.last_norm
         return vals
 
+    def named_debug_tensors(self):
+        """(name, tensor) of parameters and gradients (``--debug``)."""
+        p = self.params
+        for n in p.names:
+            yield "param/" + n, p.view(n)
+            yield "grad/" + n, p.view(n, p.grad)
+
     @torch.no_grad()
     def eval_step(self, batch) -> Dict[str, float]:
         _, out = self._forward(batch, False)

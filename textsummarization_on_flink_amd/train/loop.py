@@ -12,6 +12,9 @@
   ``checkpoint_best`` state file.
 * ``MetricsLogger``: structured JSONL (step, loss, coverage_loss, global_norm, tokens/s,
   step_ms) -- replaces TensorBoard summaries (``model.py:270-300``).
+* ``--debug``: ``NonFiniteWatch`` scans parameters, gradients and activations after every
+  step and stops with a report of the non-finite tensors (tfdbg ``has_inf_or_nan``,
+  ``run_summarization.py:216-218``).
 * fault injection (``hps.fault_nan_step`` / ``hps.fault_kill_step`` + ``fault_kill_rank``):
   a NaN gradient at step k (exercises the device NaN guard and the "Loss is not finite"
   stop) or a hard exit of one rank (exercises restart-from-latest).
@@ -27,6 +30,7 @@ from typing import Dict, Optional
 import torch
 
 from ..parallel.dist import DistInfo, all_reduce_scalar, barrier
+from ..utils.debug import NonFiniteWatch
 from . import checkpoint as ckpt
 from .trainer import NonFiniteLossError
 
@@ -90,6 +94,8 @@ def run_training(trainer, batcher, hps, info: Optional[DistInfo] = None, saver: 
     save_model_secs = hps.save_model_secs if save_model_secs is None else save_model_secs
     start = trainer.global_step
     last_save = time.time()
+    watch = NonFiniteWatch(trainer) if getattr(hps, "debug", False) and hasattr(trainer, "named_debug_tensors") \
+        else None
     vals: Dict[str, float] = {}
     try:
         while not num_steps or trainer.global_step - start < num_steps:
@@ -99,6 +105,8 @@ def run_training(trainer, batcher, hps, info: Optional[DistInfo] = None, saver: 
             _fault(hps, trainer, trainer.global_step - start, info)
             t0 = time.time()
             out = trainer.step(batch)
+            if watch is not None and watch.check(trainer.global_step):
+                raise NonFiniteLossError("Loss is not finite. Stopping. (--debug: has_inf_or_nan tripped)")
             vals = trainer.check_finite(out)  # host sync; raises "Loss is not finite. Stopping."
             dt = time.time() - t0
             toks = all_reduce_scalar(float(batch.num_tokens()), info)

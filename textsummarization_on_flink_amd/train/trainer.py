@@ -168,6 +168,17 @@ class GraphTrainer:
         vals["global_norm"] = float(self.engine.w["gnorm"].item())
         return vals
 
+    def named_debug_tensors(self):
+        """(name, tensor) of parameters, gradients and every activation buffer (``--debug``)."""
+        p = self.params
+        for n in p.names:
+            yield "param/" + n, p.view(n)
+            if p.grad is not None:
+                yield "grad/" + n, p.view(n, p.grad)
+        for n, t in self.engine.w.items():
+            if isinstance(t, torch.Tensor):
+                yield "act/" + n, t
+
     def eval_step(self, batch) -> Dict[str, float]:
         self.engine.set_batch(batch)
         out = self.engine.forward(need_grad=False)
