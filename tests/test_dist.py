@@ -43,7 +43,7 @@ def _train_worker(rank, world, port, q, batches_state):
     tr = CpuTrainer(hps, vsize, info=info)
     for b in batches[rank]:
         vals = tr.check_finite(tr.step(b))
-    q.put((rank, tr.params.flat.clone(), vals))
+    q.put((rank, tr.params.flat.clone().numpy(), vals))  # by value: the sender may exit before the read
     torch.distributed.destroy_process_group()
 
 
@@ -85,8 +85,8 @@ def test_dp2_matches_dp1_on_concatenated_batch():
     tr = CpuTrainer(hps8, vocab.size())
     for k in range(2):
         tr.step(Batch(exs[8 * k: 8 * k + 8], hps8, vocab, pad_enc_to=30))
-    assert torch.allclose(res[0][0], res[1][0])  # ranks stay identical
-    assert torch.allclose(res[0][0], tr.params.flat, atol=1e-5, rtol=1e-4)
+    assert (res[0][0] == res[1][0]).all()  # ranks stay identical
+    assert torch.allclose(torch.from_numpy(res[0][0]), tr.params.flat, atol=1e-5, rtol=1e-4)
 
 
 def _cli_rank(rank, world, port, q, flags):

@@ -201,6 +201,7 @@ class WorkerJob:
         self.in_rings: List[RecordRing] = []
         self.out_rings: List[RecordRing] = []
         self.drainers: List[RingDrainer] = []
+        self._emit_lock = threading.Lock()
         self._rr = 0
         self._tmp = None
         self.has_input = CodingUtils.input_coding(config.properties) is not None
@@ -237,8 +238,11 @@ class WorkerJob:
                 self.drainers.append(d)
 
     def _emit(self, rec: bytes):
+        # one drainer thread per worker: serialise the hand-off, downstream nodes and sinks
+        # are single-threaded
         if self.on_output:
-            self.on_output(rec)
+            with self._emit_lock:
+                self.on_output(rec)
 
     def push(self, rec: bytes) -> None:
         """Round-robin a record to the workers' input rings."""
