@@ -223,11 +223,16 @@ void dec_bwd_dz(const Tensor& dz, const Tensor& Wbig, const OT& dX_dir, const OT
 }
 
 // ---------------------------------------------------------------- loss / optimizer
-void ptr_loss(const Tensor& logits, const Tensor& bias, const Tensor& target, const Tensor& rowg, const OT& pgen, const OT& attn,
-              const Tensor& ext, const Tensor& lens, const Tensor& loss_row, const OT& dlogits, const OT& dpre,
-              const OT& dA, int64_t N, int64_t B, int64_t T, int64_t V) {
-  chk(logits, F32, "logits"); chk(bias, F32, "bias"); numel_eq(bias, V, "bias"); chk(target, I32, "target"); chk(rowg, F32, "rowg"); chk(ext, I32, "ext");
+// logits fp32 + bias (two-pass kernel), or bf16 with the bias already added (bias = None,
+// one-pass kernel; dlogits may be the logits tensor itself: dz is written in place)
+void ptr_loss(const Tensor& logits, const OT& bias, const Tensor& target, const Tensor& rowg, const OT& pgen,
+              const OT& attn, const Tensor& ext, const Tensor& lens, const Tensor& loss_row, const OT& dlogits,
+              const OT& dpre, const OT& dA, int64_t N, int64_t B, int64_t T, int64_t V) {
+  const bool lbf = logits.scalar_type() == at::kBFloat16;
+  chk(logits, lbf ? BF : F32, "logits"); chk(target, I32, "target"); chk(rowg, F32, "rowg"); chk(ext, I32, "ext");
   chk(lens, I32, "lens"); chk(loss_row, F32, "loss_row");
+  TORCH_CHECK(lbf != bias.has_value(), "bf16 logits carry their bias (pass None); fp32 logits need the bias");
+  chko(bias, F32, V, "bias");
   numel_eq(logits, N * V, "logits"); numel_eq(target, N, "target"); numel_eq(rowg, N, "rowg");
   numel_eq(ext, B * T, "ext"); numel_eq(lens, B, "lens"); numel_eq(loss_row, N, "loss_row");
   TORCH_CHECK(N % B == 0, "N must be D*B");
@@ -235,9 +240,16 @@ void ptr_loss(const Tensor& logits, const Tensor& bias, const Tensor& target, co
   chko(dpre, F32, N, "dpre"); chko(dA, F32, N * T, "dA");
   TORCH_CHECK(!PO<float>(pgen) || (PO<float>(attn) && (!PO<bf16>(dlogits) || (PO<float>(dpre) && PO<float>(dA)))),
               "pointer mode needs attn, and dpre/dA when computing grads");
-  launch_ptr_loss(P<float>(logits), P<float>(bias), P<int>(target), P<float>(rowg), PO<float>(pgen), PO<float>(attn), P<int>(ext),
-                  P<int>(lens), P<float>(loss_row), PO<bf16>(dlogits), PO<float>(dpre), PO<float>(dA), N, B, T, V,
-                  stream());
+  if (lbf) {
+    TORCH_CHECK(V <= ptr_loss_bf16_max_vocab(), "bf16 ptr_loss: V <= 65536");
+    launch_ptr_loss_bf16(P<bf16>(logits), P<int>(target), P<float>(rowg), PO<float>(pgen), PO<float>(attn),
+                         P<int>(ext), P<int>(lens), P<float>(loss_row), PO<bf16>(dlogits), PO<float>(dpre),
+                         PO<float>(dA), N, B, T, V, stream());
+    return;
+  }
+  launch_ptr_loss(P<float>(logits), P<float>(*bias), P<int>(target), P<float>(rowg), PO<float>(pgen), PO<float>(attn),
+                  P<int>(ext), P<int>(lens), P<float>(loss_row), PO<bf16>(dlogits), PO<float>(dpre), PO<float>(dA), N,
+                  B, T, V, stream());
 }
 
 void clip_adagrad(const Tensor& w, const Tensor& acc, const Tensor& g, const Tensor& part, double lr, double max_norm,

@@ -36,6 +36,10 @@ void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, co
                        float* dx_out, float* dctx_prev_out, float* dh_rec, int B, int E, int H, int A,
                        hipStream_t st);
 
+void launch_ptr_loss_bf16(const bf16* logits, const int* target, const float* rowg, const float* pgen,
+                          const float* attn, const int* ext, const int* lens, float* loss_row, bf16* dlogits,
+                          float* dpre, float* dA, int N, int B, int T, int V, hipStream_t st);
+int ptr_loss_bf16_max_vocab();
 void launch_ptr_loss(const float* logits, const float* bias, const int* target, const float* rowg, const float* pgen, const float* attn,
                      const int* ext, const int* lens, float* loss_row, bf16* dlogits, float* dpre, float* dA, int N,
                      int B, int T, int V, hipStream_t st);

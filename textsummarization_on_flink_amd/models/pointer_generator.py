@@ -52,6 +52,33 @@ def enc_b(layer, d):
     return f"{enc_prefix(layer)}/bidirectional_rnn/{d}/lstm_cell/bias"
 
 
+def mm_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None):
+    """out = a . b (+ bias), fp32 accumulate, written straight into ``out`` (fp32 or bf16)
+    -- no temporary, no separate bias pass (hipBLASLt bias epilogue)."""
+    if out.dtype == F32 and a.dtype == BF:
+        if bias is None:
+            return torch.mm(a, b, out_dtype=F32, out=out)
+        return torch.addmm(bias, a, b, out_dtype=F32, out=out)
+    if bias is None:
+        return torch.mm(a, b, out=out)
+    return torch.addmm(bias.to(out.dtype), a, b, out=out)
+
+
+def wgrad_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
+    """out[M,N] = a[K,M]^T . b[K,N] for weight gradients: K (= rows: tokens or decoder steps
+    x batch) is long and M x N is a handful of output tiles, which a plain GEMM runs on a
+    few CUs.  Split K into S chunks as one batched GEMM (S x the tiles, fp32 partials) and
+    sum the partials: 3-5x faster on MI355X for K = 25.6k-102k (tools/wgrad_micro.py)."""
+    K = a.shape[0]
+    if a.is_cuda:
+        for S in ((32, 16, 8) if K >= 65536 else (16, 8)):
+            if K % S == 0 and K // S >= 256:
+                parts = torch.bmm(a.reshape(S, K // S, a.shape[1]).transpose(1, 2), b.reshape(S, K // S, b.shape[1]),
+                                  out_dtype=F32)
+                return torch.sum(parts, 0, out=out)
+    return out.copy_(mmf(a.t(), b))
+
+
 def mmf(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """bf16 x bf16 -> fp32 GEMM (fp32 accumulate), hipBLASLt."""
     return torch.mm(a, b, out_dtype=F32)
@@ -137,12 +164,18 @@ class HipPointerGenerator:
         w["CTXb"] = z(D, B, A, dt=BF)
         w["e"] = z(B, T)
         w["covloss"] = z(D, B)
-        w["outb"] = z(D * B, H, dt=BF)
+        # [outb | 1 | 0...]: the ones column makes the output-projection weight-gradient GEMM
+        # also produce the bias gradient (one read of dlogits instead of two)
+        w["outb_ext"] = z(D * B, H + 8, dt=BF)
+        w["outb_ext"][:, H] = 1.0
+        w["outb"] = w["outb_ext"][:, :H]
         w["pg"] = z(D, B)
         w["loss_row"] = z(D, B)
-        w["logits"] = z(D * B, V)
+        # bf16 logits (bias added in the GEMM epilogue); ptr_loss overwrites them in place
+        # with dlogits
+        w["logits"] = z(D * B, V, dt=BF)
         # backward
-        w["dlogits"] = z(D * B, V, dt=BF)
+        w["dlogits"] = w["logits"]
         w["dpre"] = z(D, B)
         w["dA"] = z(D, B, T)
         w["DCTX"] = z(D, B, A)
@@ -155,6 +188,7 @@ class HipPointerGenerator:
         w["dh_rec"] = z(B, H)
         w["dc_carry"] = z(B, H)
         w["dF"] = z(B, T, A)
+        self._dE = z(B, T, A)
         w["dv"] = z(A)
         w["dwc"] = z(A)
         # optimizer
@@ -200,6 +234,7 @@ class HipPointerGenerator:
         put("OUTm", p[OUT_M])
         put("OUTmT", p[OUT_M].t())  # [H][H+A] for the per-step linear2 kernel (decode)
         put("ow", p[OW])
+        put("ovb", p[OV])  # bias of the bf16 logits GEMM epilogue
         self.pk = pk
         self.f32 = {
             "v": p[VATT].reshape(A).contiguous(),
@@ -255,8 +290,8 @@ class HipPointerGenerator:
             xs[0].copy_(x.transpose(0, 1))
             xs[1].copy_(x.gather(1, rev[..., None].expand(B, T, din)).transpose(0, 1))
             for di, d in enumerate(("fw", "bw")):
-                g = mmf(xs[di].view(T * B, din), self.pk[f"enc{layer}_Kx{di}"])
-                st["gx"][di].copy_(g.view(T, B, 4 * H)).add_(self.p[enc_b(layer, d)])
+                mm_into(st["gx"][di].view(T * B, 4 * H), xs[di].view(T * B, din), self.pk[f"enc{layer}_Kx{di}"],
+                        self.p[enc_b(layer, d)])
             st["hs"][:, 0].zero_()
             st["cs"][:, 0].zero_()
             st["out"].zero_()
@@ -279,7 +314,7 @@ class HipPointerGenerator:
         w["Cst"][0].copy_(c0)
         w["Cb"][0].copy_(c0)
         w["Hb"][0].copy_(h0)
-        w["F"].view(B * T, A).copy_(torch.mm(top["out"].view(B * T, A), self.pk["Wh"]))
+        mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["Wh"])
         w["Ft"].copy_(w["F"].transpose(1, 2))
         w["Et"].copy_(top["out"].transpose(1, 2))
 
@@ -289,8 +324,8 @@ class HipPointerGenerator:
         cov = hps.coverage
         emb_dec = self.pk["emb"][w["dec_batch_t"]].view(D * B, E)
         xe = w["xe"].view(D * B, E)
-        xe.copy_(mmf(emb_dec, self.pk["lin_emb"])).add_(self.p[LIN_B])
-        w["XG"].view(D * B, 4 * H).copy_(mmf(xe.to(BF), self.pk["cell_x"])).add_(self.p[CELL_B])
+        mm_into(xe, emb_dec, self.pk["lin_emb"], self.p[LIN_B])
+        mm_into(w["XG"].view(D * B, 4 * H), xe.to(BF), self.pk["cell_x"], self.p[CELL_B])
         self._emb_dec = emb_dec
         enc_out, lens, Ft = self.enc[-1]["out"], w["enc_lens"], w["Ft"]
         v, wc = self.f32["v"], self.f32["wc"]
@@ -324,8 +359,8 @@ class HipPointerGenerator:
                    + Hn.float() @ pm[A + H:A + 2 * H] + w["X"].view(N, E) @ pm[A + 2 * H:] + p[PG_B])
             w["pg"].view(N).copy_(torch.sigmoid(pre))
             pg = w["pg"]
-        torch.mm(w["outb"], self.pk["ow"], out_dtype=F32, out=w["logits"])
-        self.k.ptr_loss(w["logits"], p[OV], w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None,
+        torch.addmm(self.pk["ovb"], w["outb"], self.pk["ow"], out=w["logits"])
+        self.k.ptr_loss(w["logits"], None, w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None,
                         w["ext"], w["enc_lens"], w["loss_row"], w["dlogits"] if need_grad else None,
                         w["dpre"] if (need_grad and hps.pointer_gen) else None,
                         w["dA"] if (need_grad and hps.pointer_gen) else None, N, B, T, V)
@@ -368,8 +403,12 @@ class HipPointerGenerator:
         g = p.g
         p.grad.zero_()
         dl = w["dlogits"]
-        g(OW).copy_(torch.mm(w["outb"].t(), dl, out_dtype=F32))
-        g(OV).copy_(dl.sum(0, dtype=F32))
+        # [W | b] gradient in one GEMM: output_projection/w and /v are adjacent in the flat
+        # buffer, and row H of outb_ext is all ones
+        H, V = self.H, self.V
+        assert p.offsets[OV][0] == p.offsets[OW][0] + H * V
+        o = p.offsets[OW][0]
+        torch.mm(w["outb_ext"][:, :H + 1].t(), dl, out_dtype=F32, out=p.grad[o:o + (H + 1) * V].view(H + 1, V))
         self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
 
     def backward_mid(self):
@@ -384,8 +423,8 @@ class HipPointerGenerator:
         Hn = w["Hb"][1:].reshape(N, H)
         ctxb = w["CTXb"].view(N, A)
         doutb = dout.to(BF)
-        g(OUT_M)[:H].copy_(mmf(Hn.t(), doutb))
-        g(OUT_M)[H:].copy_(mmf(ctxb.t(), doutb))
+        wgrad_into(g(OUT_M)[:H], Hn, doutb)
+        wgrad_into(g(OUT_M)[H:], ctxb, doutb)
         g(OUT_B).copy_(dout.sum(0))
         dH_dir = mmf(doutb, self.pk["OUTm"][:H].t()).view(D, B, H)
         dCTX_dir = mmf(doutb, self.pk["OUTm"][H:].t()).view(D, B, A)
@@ -431,23 +470,23 @@ class HipPointerGenerator:
         # ---- decoder weight gradients (one GEMM each over all D*B rows)
         DZ = w["DZ"].view(N, 4 * H)
         gk = g(CELL_K)
-        gk[:E].copy_(mmf(w["Xb"].view(N, E).t(), DZ))
-        gk[E:].copy_(mmf(w["Hb"][:D].reshape(N, H).t(), DZ))
+        wgrad_into(gk[:E], w["Xb"].view(N, E), DZ)
+        wgrad_into(gk[E:], w["Hb"][:D].reshape(N, H), DZ)
         g(CELL_B).copy_(DZ.sum(0, dtype=F32))
         DX = w["DX"].view(N, E)
         DXb = DX.to(BF)
         gl = g(LIN_M)
-        gl[:E].copy_(mmf(self._emb_dec.t(), DXb))
+        wgrad_into(gl[:E], self._emb_dec, DXb)
         gl[E:].zero_()
         if D > 1:
-            gl[E:].copy_(mmf(w["CTXb"][:D - 1].reshape((D - 1) * B, A).t(), DXb[B:]))
+            wgrad_into(gl[E:], w["CTXb"][:D - 1].reshape((D - 1) * B, A), DXb[B:])
         g(LIN_B).copy_(DX.sum(0))
         d_emb_dec = mmf(DXb, self.pk["lin_emb"].t())  # [N,E]
         DS = w["DS"].view(N, A)
         DSb = DS.to(BF)
         gs = g(ATT_M)
-        gs[:H].copy_(mmf(w["Cb"][1:].reshape(N, H).t(), DSb))
-        gs[H:].copy_(mmf(Hn.t(), DSb))
+        wgrad_into(gs[:H], w["Cb"][1:].reshape(N, H), DSb)
+        wgrad_into(gs[H:], Hn, DSb)
         g(ATT_B).copy_(DS.sum(0))
         # ---- attention feature gradients (tanh recomputed once over all steps)
         w["dF"].zero_()
@@ -460,9 +499,10 @@ class HipPointerGenerator:
             g(WCOV).view(A).copy_(w["dwc"])
         dFb = w["dF"].view(B * T, A).to(BF)
         top = self.enc[-1]
-        g(WH).view(A, A).copy_(mmf(top["out"].view(B * T, A).t(), dFb))
-        dE = torch.bmm(w["ATT"].permute(1, 2, 0), w["DCTX"].permute(1, 0, 2))  # [B,T,A]
-        dE.view(B * T, A).add_(mmf(dFb, self.pk["Wh"].t()))
+        wgrad_into(g(WH).view(A, A), top["out"].view(B * T, A), dFb)
+        dE = self._dE
+        mm_into(dE.view(B * T, A), dFb, self.pk["Wh"].t())
+        dE.baddbmm_(w["ATT"].permute(1, 2, 0), w["DCTX"].permute(1, 0, 2))  # += a^T . dctx  [B,T,A]
         self._dE, self._d_emb_dec = dE, d_emb_dec
 
     def backward_tail(self):
@@ -510,8 +550,8 @@ class HipPointerGenerator:
             for di, d in enumerate(("fw", "bw")):
                 dzd = st["dz"][di].view(T * B, 4 * H)
                 gkd = g(enc_k(layer, d))
-                gkd[:din].copy_(mmf(st["x_sf"][di].view(T * B, din).t(), dzd))
-                gkd[din:].copy_(mmf(st["hs"][di, :T].reshape(T * B, H).t(), dzd))
+                wgrad_into(gkd[:din], st["x_sf"][di].view(T * B, din), dzd)
+                wgrad_into(gkd[din:], st["hs"][di, :T].reshape(T * B, H), dzd)
                 g(enc_b(layer, d)).copy_(dzd.sum(0, dtype=F32))
                 dxs = mmf(dzd, self.pk[f"enc{layer}_Kx{di}"].t()).view(T, B, din).transpose(0, 1)
                 if di == 0:
