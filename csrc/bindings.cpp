@@ -157,6 +157,23 @@ void attn_bwd_tanh(const Tensor& F, const Tensor& s, const Tensor& v, const OT& 
                        PO<float>(dcov_out), B, T, A, stream());
 }
 
+void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
+                   const Tensor& a, const Tensor& dctx, const Tensor& ctx, const OT& Ga, const OT& dcov_next,
+                   const OT& gcl, const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out,
+                   int64_t B, int64_t T, int64_t A) {
+  chk(E, BF, "E"); chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(dctx, F32, "dctx");
+  chk(ctx, F32, "ctx"); chk(lens, I32, "lens"); chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
+  TORCH_CHECK(A % 64 == 0 && A <= 1024 && T >= 1, "bad A/T");
+  numel_eq(E, B * T * A, "E"); numel_eq(F, B * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v");
+  numel_eq(a, B * T, "a"); numel_eq(dctx, B * A, "dctx"); numel_eq(ctx, B * A, "ctx"); numel_eq(lens, B, "lens");
+  numel_eq(de_out, B * T, "de_out"); numel_eq(ds, B * A, "ds");
+  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(Ga, F32, B * T, "Ga");
+  chko(dcov_next, F32, B * T, "dcov_next"); chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
+  launch_attn_bwd_step(P<bf16>(E), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
+                       P<float>(dctx), P<float>(ctx), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl),
+                       P<int>(lens), P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, stream());
+}
+
 void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const OT& wc, const OT& cov_all,
                    const Tensor& de_all, const Tensor& lens, const Tensor& dF, const Tensor& dv, const OT& dwc,
                    int64_t D, int64_t B, int64_t T, int64_t A) {
@@ -408,6 +425,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("attn_softmax_ctx", &attn_softmax_ctx);
   m.def("attn_bwd_da", &attn_bwd_da);
   m.def("attn_bwd_tanh", &attn_bwd_tanh);
+  m.def("attn_bwd_step", &attn_bwd_step);
   m.def("attn_bwd_feat", &attn_bwd_feat);
   m.def("attn_chunks", &attn_chunks);
   m.def("dec_cell_fwd", &dec_cell_fwd);

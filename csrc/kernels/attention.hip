@@ -422,6 +422,243 @@ __global__ __launch_bounds__(256) void attn_bwd_tanh_kernel(
   }
 }
 
+// ------------------------------------------ backward step, fused: da, de, ds, dcov
+// One pass over the rows E_i (encoder outputs) and F_i (W_h features) of a block's positions:
+//   da_i   = r_i + dctx . E_i,        r_i = Ga_i + dcov_next_i + g_cl [a_i <= cov_i]
+//   S      = sum_j a_j da_j = sum_j a_j r_j + dctx . ctx     (ctx = sum_j a_j E_j, forward)
+//   de_i   = a_i (da_i - S)
+//   ds_k  += sum_i de_i v_k sech2(u_ik)                        (atomic, ds pre-zeroed)
+//   dcov_i = dcov_next_i + g_cl [a_i > cov_i] + de_i sum_k v_k w_c_k sech2(u_ik)
+// S needs no pass over da (its dctx.E half is dctx.ctx), so the da kernel over the
+// transposed Et and the tanh kernel over F collapse into ONE launch per decoder step and
+// every block is independent.  Lanes on the feature axis (8 per lane, NK blocks of 512);
+// each wave takes NG groups of 8 positions.  Per group: the 8 partial dctx.E_i
+// dots are reduced with the butterfly reduce-scatter (the lanes of position q end up
+// holding its total), de_q is broadcast with v_readlane, then the r-form tanh pass
+// (packed fp32, see rsig2) accumulates ds and the 8 dcov partials, reduced the same way.
+//   v_k sech2(u) = 4 v_k r (1 - r)  ->  ds_k = 4 v_k sum_i de_i q_ik,  q = r - r^2.
+__device__ __forceinline__ float bfly8(const float (&x)[8], int b5, int b4, int b3) {
+  float h4[4], h2[2], h1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float send = b5 ? x[i] : x[i + 4];
+    const float keep = b5 ? x[i + 4] : x[i];
+    h4[i] = keep + __shfl_xor(send, 32, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float send = b4 ? h4[i] : h4[i + 2];
+    const float keep = b4 ? h4[i + 2] : h4[i];
+    h2[i] = keep + __shfl_xor(send, 16, 64);
+  }
+  {
+    const float send = b3 ? h2[0] : h2[1];
+    const float keep = b3 ? h2[1] : h2[0];
+    h1 = keep + __shfl_xor(send, 8, 64);
+  }
+  h1 += __shfl_xor(h1, 4, 64);
+  h1 += __shfl_xor(h1, 2, 64);
+  h1 += __shfl_xor(h1, 1, 64);
+  return h1;  // total of element q = 4*b5 + 2*b4 + b3, in all 8 lanes of that group
+}
+
+// NG groups of 8 positions per wave (a block = 4 waves = 32*NG positions).  The loads are
+// software-pipelined: group 0's E/F rows are issued before the S reduction (whose global
+// loads and block barriers then overlap them); group g+1's E rows are issued right after
+// group g's dots, its F rows right after group g's tanh pass.
+template <int NK, int NG>
+__global__ __launch_bounds__(256) void attn_bwd_step_kernel(
+    const bf16* __restrict__ E, const bf16* __restrict__ F, const float* __restrict__ s,
+    const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
+    const float* __restrict__ a, const float* __restrict__ dctx, const float* __restrict__ ctx,
+    const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
+    const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
+    float* __restrict__ dcov_out, int T, int A) {
+  constexpr int PB = 32 * NG;  // positions per block
+  static_assert(NG >= 1 && 8 * NG <= 64, "one lane per position of a wave");
+  __shared__ float red[8];
+  __shared__ float part[4][512 * NK];
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int len = lens[b];
+  const size_t rb = (size_t)b * T;
+  const int p0 = blockIdx.x * PB + wid * 8 * NG;
+  if (blockIdx.x * PB >= len) {  // whole block masked: only pass dcov through
+    for (int i = tid; i < PB; i += 256) {
+      const int p = blockIdx.x * PB + i;
+      if (p < T) {
+        if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
+        de_out[rb + p] = 0.f;
+      }
+    }
+    return;
+  }
+  const float g = gcl ? gcl[b] : 0.f;
+  const bf16* Eb = E + (size_t)b * T * A;
+  const bf16* Fb = F + (size_t)b * T * A;
+  int k0c[NK];
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) k0c[kb] = min(kb * 512 + lane * 8, A - 8);
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 fr[NK][8], er[NK][8];
+  auto load_e = [&](int pg) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int pq = min(pg + q, len - 1);
+#pragma unroll
+      for (int kb = 0; kb < NK; ++kb) er[kb][q] = __builtin_bit_cast(u32x4, ld8(Eb + (size_t)pq * A + k0c[kb]));
+    }
+  };
+  auto load_f = [&](int pg) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int pq = min(pg + q, len - 1);
+#pragma unroll
+      for (int kb = 0; kb < NK; ++kb) fr[kb][q] = __builtin_bit_cast(u32x4, ld8(Fb + (size_t)pq * A + k0c[kb]));
+    }
+  };
+  // group 0 rows first: nothing below depends on them until the first dot
+  if (p0 < len) {
+    load_e(p0);
+    load_f(p0);
+  }
+  // per-lane feature parameters (pre-scaled for the r-form)
+  float dk[NK][8];
+  f32x2 s2[NK][4], w2[NK][4], v4w[NK][4], acc[NK][4];
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) {
+    const int k0 = kb * 512 + lane * 8;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      float sv[2], wv[2], vv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = k0 + 2 * jp + h;
+        const bool ok = k < A;
+        sv[h] = ok ? s[(size_t)b * A + k] : 0.f;
+        vv[h] = ok ? v[k] : 0.f;
+        wv[h] = (ok && wc) ? wc[k] : 0.f;
+        dk[kb][2 * jp + h] = ok ? dctx[(size_t)b * A + k] : 0.f;
+      }
+      s2[kb][jp] = f32x2{sv[0], sv[1]} * K2LOG2E;
+      w2[kb][jp] = f32x2{wv[0], wv[1]} * K2LOG2E;
+      v4w[kb][jp] = f32x2{4.f * vv[0] * wv[0], 4.f * vv[1] * wv[1]};
+      acc[kb][jp] = f32x2{0.f, 0.f};
+    }
+  }
+  // per-position scalars of this wave's 8*NG positions, one per lane
+  float a_l = 0.f, r_l = 0.f, c_l = 0.f, dn_l = 0.f;
+  {
+    const int p = p0 + (lane & (8 * NG - 1));
+    if (p < len) {
+      const size_t ix = rb + p;
+      a_l = a[ix];
+      c_l = cov ? cov[ix] : 0.f;
+      r_l = (Ga ? Ga[ix] : 0.f) + (dcov_next ? dcov_next[ix] : 0.f);
+      if (gcl && a_l <= c_l) r_l += g;
+    }
+    if (p < T && dcov_next) dn_l = dcov_next[rb + p];
+  }
+  // S = sum_j a_j r_j + dctx . ctx
+  float S = 0.f;
+  for (int i = tid; i < len; i += 256) {
+    const size_t ix = rb + i;
+    const float ai = a[ix];
+    float r = (Ga ? Ga[ix] : 0.f) + (dcov_next ? dcov_next[ix] : 0.f);
+    if (gcl && ai <= (cov ? cov[ix] : 0.f)) r += g;
+    S += ai * r;
+  }
+  for (int k = tid; k < A; k += 256) S += dctx[(size_t)b * A + k] * ctx[(size_t)b * A + k];
+  S = block_sum<256>(S, red);
+  const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1;
+  const int qm = 4 * b5 + 2 * b4 + b3;  // the position whose totals this lane's group holds
+#pragma unroll
+  for (int grp = 0; grp < NG; ++grp) {
+    const int pg = p0 + grp * 8;
+    if (pg >= len) {  // wave-uniform: this and every later group lie past len -> pass dcov through
+      for (int i = lane; i < 8 * (NG - grp); i += 64) {
+        const int p = pg + i;
+        if (p < T) {
+          de_out[rb + p] = 0.f;
+          if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
+        }
+      }
+      break;
+    }
+    const bool more = grp + 1 < NG && pg + 8 < len;
+    // da: partial dctx . E_q, reduced
+    float pd[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      f32x2 d2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp)
+          d2 = fma2(bf2pair(er[kb][q][jp]), f32x2{dk[kb][2 * jp], dk[kb][2 * jp + 1]}, d2);
+      pd[q] = d2.x + d2.y;
+    }
+    if (more) load_e(pg + 8);
+    const float dot = bfly8(pd, b5, b4, b3);
+    const int src = grp * 8 + qm;
+    const float a_q = __shfl(a_l, src, 64), r_q = __shfl(r_l, src, 64);
+    const float c_q = __shfl(c_l, src, 64), dn_q = __shfl(dn_l, src, 64);
+    const float de_q = (pg + qm < len) ? a_q * (r_q + dot - S) : 0.f;
+    // tanh pass: ds accumulation and dcov partials
+    float dcv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      // the lanes holding position q's totals start at 32*b5 + 16*b4 + 8*b3
+      const float de = rdlane(de_q, ((q >> 2) << 5) | (((q >> 1) & 1) << 4) | ((q & 1) << 3));
+      const float c = rdlane(c_l, grp * 8 + q);
+      f32x2 dc2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          const f32x2 y = fma2(bf2pair(fr[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          const f32x2 r = rsig2(y);
+          const f32x2 qv = fma2(-r, r, r);
+          acc[kb][jp] = fma2(qv, splat2(de), acc[kb][jp]);
+          dc2 = fma2(qv, v4w[kb][jp], dc2);
+        }
+      dcv[q] = dc2.x + dc2.y;
+    }
+    if (more) load_f(pg + 8);
+    const float hc = bfly8(dcv, b5, b4, b3);
+    if ((lane & 7) == 0) {
+      const int p = pg + qm;
+      if (p < T) {
+        const size_t ix = rb + p;
+        de_out[ix] = de_q;
+        if (dcov_out) {
+          float r = dn_q;
+          if (p < len) {
+            r += de_q * hc;
+            if (gcl && a_q > c_q) r += g;
+          }
+          dcov_out[ix] = r;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) {
+    const int k0 = kb * 512 + lane * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = k0 + j < A;
+      part[wid][kb * 512 + lane * 8 + j] = ok ? 4.f * v[ok ? k0 + j : 0] * acc[kb][j >> 1][j & 1] : 0.f;
+    }
+  }
+  __syncthreads();
+  float* out = ds + (size_t)b * A;
+  for (int k = tid; k < A; k += 256) {
+    const float x = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+    atomicAdd(out + k, x);
+  }
+}
+
 // ------------------------------------------------------ post-loop: dF, dv, dw_c
 // dF[b,i,k] = sum_t de[t,b,i] v_k sech2(u_tik); dv_k = sum de tanh(u); dwc_k = sum de v_k sech2 cov.
 // Lanes on features (8 per lane), each wave keeps 4 positions x 8 features of dF in
@@ -583,6 +820,19 @@ void launch_attn_bwd_tanh(const bf16* F, const float* s, const float* v, const f
   else
     hipLaunchKernelGGL(attn_bwd_tanh_kernel<2>, grid, dim3(256), 0, st, F, s, v, wc, cov, a, da, dcov_next, gcl, lens,
                        de_out, ds, dcov_out, T, A);
+}
+void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
+                          const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
+                          const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
+                          float* dcov_out, int B, int T, int A, hipStream_t st) {
+  // groups of 8 positions per wave; TSAMD_ATTN_NG=2 selects 64-position blocks (A/B runs)
+  static const int ng = [] { const char* e = getenv("TSAMD_ATTN_NG"); return e && atoi(e) == 2 ? 2 : 4; }();
+  dim3 grid((T + 32 * ng - 1) / (32 * ng), B);
+#define LB(NK, NG) hipLaunchKernelGGL((attn_bwd_step_kernel<NK, NG>), grid, dim3(256), 0, st, E, F, s, v, wc, cov, a, \
+                                      dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A)
+  if (A <= 512) { if (ng == 2) LB(1, 2); else LB(1, 4); }
+  else { if (ng == 2) LB(2, 2); else LB(2, 4); }
+#undef LB
 }
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, float* dF, float* dv, float* dwc, int D, int B, int T,

@@ -21,6 +21,10 @@ int attn_nchunk(int T);
 void launch_attn_bwd_tanh(const bf16* F, const float* s, const float* v, const float* wc, const float* cov,
                           const float* a, const float* da, const float* dcov_next, const float* gcl, const int* lens,
                           float* de_out, float* ds, float* dcov_out, int B, int T, int A, hipStream_t st);
+void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
+                          const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
+                          const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
+                          float* dcov_out, int B, int T, int A, hipStream_t st);
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, float* dF, float* dv, float* dwc, int D, int B, int T,
                           int A, hipStream_t st);

@@ -45,3 +45,33 @@ def test_nonfinite_report_and_watch():
             yield "param/y", a
 
     assert [r[0] for r in NonFiniteWatch(T()).check(7)] == ["grad/x"]
+
+
+def test_tensorboard_event_roundtrip(tmp_path):
+    from textsummarization_on_flink_amd.utils.tensorboard import EventWriter, read_events
+    w = EventWriter(str(tmp_path / "train"))
+    w.add_scalars(1, {"loss": 7.5, "coverage_loss": 0.25})
+    w.add_scalars(2, {"loss": 7.25, "global_norm": 1.5})
+    w.close()
+    evs = read_events(w.path)
+    assert evs[0]["file_version"] == "brain.Event:2"
+    assert [e["step"] for e in evs[1:]] == [1, 2]
+    assert evs[1]["scalars"] == {"loss": 7.5, "coverage_loss": 0.25}
+    assert evs[2]["scalars"]["global_norm"] == 1.5
+    raw = bytearray(open(w.path, "rb").read())
+    raw[-6] ^= 0xFF  # corrupt the last payload: the masked crc32c must catch it
+    open(w.path, "wb").write(bytes(raw))
+    import pytest
+    with pytest.raises(ValueError):
+        read_events(w.path)
+
+
+def test_metrics_logger_writes_reference_summary_tags(tmp_path):
+    from textsummarization_on_flink_amd.train.loop import MetricsLogger
+    from textsummarization_on_flink_amd.utils.tensorboard import read_events
+    m = MetricsLogger(str(tmp_path / "m.jsonl"), tb_dir=str(tmp_path / "eval"))
+    m.log(step=3, eval_loss=6.0, running_avg_loss=6.5)
+    m.close()
+    (f,) = [p for p in os.listdir(tmp_path / "eval") if p.startswith("events.out.tfevents.")]
+    sc = read_events(str(tmp_path / "eval" / f))[1]["scalars"]
+    assert sc == {"loss": 6.0, "running_avg_loss/decay=0.990000": 6.5}

@@ -59,7 +59,10 @@ def metrics_for(hps, info: Optional[DistInfo] = None):
     from .train.loop import MetricsLogger
     chief = info is None or info.is_chief
     path = hps.metrics_path or (os.path.join(hps.log_root, f"metrics_{hps.mode}.jsonl") if hps.log_root else "")
-    return MetricsLogger(path or None, enabled=chief)
+    tb_dir = None
+    if hps.tensorboard and hps.log_root and hps.mode in ("train", "eval") and not hps.inference:
+        tb_dir = os.path.join(hps.log_root, hps.mode)  # Supervisor(logdir=train) / eval summary_writer
+    return MetricsLogger(path or None, enabled=chief, tb_dir=tb_dir)
 
 
 def load_params_for_decode(hps, vocab, device, retries: Optional[int] = None):

@@ -73,6 +73,7 @@ class HParams:
     log_every: int = 1
     drop_last: bool = False        # Issue-5 fix: pad (False) or drop (True) a short final batch
     metrics_path: str = ""         # JSONL metrics file ("" = <log_root>/metrics_<mode>.jsonl)
+    tensorboard: bool = True       # also write TensorBoard scalar event files (train/ and eval/)
     html_escape: bool = False      # fix quirk: make_html_safe discards its result in the reference
     load_retries: int = 6          # bounded checkpoint-load retries (util.py:29-41 retried forever)
     fault_nan_step: int = -1       # fault injection: NaN gradient at this (relative) step

@@ -145,9 +145,12 @@ class HipPointerGenerator:
             w["lstm_xf"] = z(int(self.k.lstm_persistent_xbuf(H, B, False)), dt=torch.long)
             w["lstm_xb"] = z(int(self.k.lstm_persistent_xbuf(H, B, True)), dt=torch.long)
         w["lstm_err"] = z(1, dt=torch.int32)
+        # one fused attention-backward kernel per decoder step (attn_bwd_step);
+        # TSAMD_ATTN_BWD_FUSED=0 selects the two-kernel path (attn_bwd_da over Et + attn_bwd_tanh)
+        self.fused_attn_bwd = os.environ.get("TSAMD_ATTN_BWD_FUSED", "1") != "0"
         w["F"] = z(B, T, A, dt=BF)
-        w["Ft"] = z(B, A, T, dt=BF)   # transposed copies for the lanes-over-positions kernels
-        w["Et"] = z(B, A, T, dt=BF)
+        w["Ft"] = z(B, A, T, dt=BF)   # transposed copy for the lanes-over-positions score kernel
+        w["Et"] = None if self.fused_attn_bwd else z(B, A, T, dt=BF)
         w["XG"] = z(D, B, 4 * H)
         # decoder forward state
         w["xe"] = z(D, B, E)
@@ -183,7 +186,7 @@ class HipPointerGenerator:
         w["DZ"] = z(D, B, 4 * H, dt=BF)
         w["DS"] = z(D, B, A)
         w["DE"] = z(D, B, T)
-        w["da"] = z(B, T)
+        w["da"] = None if self.fused_attn_bwd else z(B, T)
         w["dcov"] = z(2, B, T)
         w["dh_rec"] = z(B, H)
         w["dc_carry"] = z(B, H)
@@ -316,7 +319,8 @@ class HipPointerGenerator:
         w["Hb"][0].copy_(h0)
         mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["Wh"])
         w["Ft"].copy_(w["F"].transpose(1, 2))
-        w["Et"].copy_(top["out"].transpose(1, 2))
+        if w["Et"] is not None:
+            w["Et"].copy_(top["out"].transpose(1, 2))
 
     def _decoder_forward(self):
         k, w, hps = self.k, self.w, self.hps
@@ -457,10 +461,15 @@ class HipPointerGenerator:
             dcov_next = dcov[(t + 1) % 2] if (cov and t < D - 1) else None
             cov_t = w["COV"][t] if (cov and t > 0) else None
             gcl_t = w["gcl"][t] if cov else None
-            k.attn_bwd_da(Et, w["DCTX"][t], Ga[t] if Ga is not None else None, dcov_next, w["ATT"][t], cov_t,
-                          gcl_t, lens, w["da"], B, T, A)
-            k.attn_bwd_tanh(F, w["S"][t], v, wc, cov_t, w["ATT"][t], w["da"], dcov_next, gcl_t, lens, w["DE"][t],
-                            w["DS"][t], dcov[t % 2] if cov else None, B, T, A)
+            if self.fused_attn_bwd:
+                k.attn_bwd_step(enc_out, F, w["S"][t], v, wc, cov_t, w["ATT"][t], w["DCTX"][t], w["CTX"][t],
+                                Ga[t] if Ga is not None else None, dcov_next, gcl_t, lens, w["DE"][t], w["DS"][t],
+                                dcov[t % 2] if cov else None, B, T, A)
+            else:
+                k.attn_bwd_da(Et, w["DCTX"][t], Ga[t] if Ga is not None else None, dcov_next, w["ATT"][t], cov_t,
+                              gcl_t, lens, w["da"], B, T, A)
+                k.attn_bwd_tanh(F, w["S"][t], v, wc, cov_t, w["ATT"][t], w["da"], dcov_next, gcl_t, lens,
+                                w["DE"][t], w["DS"][t], dcov[t % 2] if cov else None, B, T, A)
             k.dec_bwd_cell(w["DS"][t], self.pk["Ws"], dC_dir[t] if dC_dir is not None else None,
                            dH_dir[t], w["dh_rec"], w["dc_carry"], w["ACT"][t], w["Cst"][t + 1], w["Cst"][t],
                            w["DZ"][t], B, H, A)

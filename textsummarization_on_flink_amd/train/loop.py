@@ -38,22 +38,44 @@ log = logging.getLogger(__name__)
 
 
 class MetricsLogger:
-    def __init__(self, path: Optional[str], enabled: bool = True):
+    """JSONL metrics plus (optionally) TensorBoard scalars in ``tb_dir`` -- the reference's
+    summary tags: ``loss``, ``coverage_loss``, ``total_loss``, ``global_norm`` (train,
+    ``model.py:270-300``) and ``running_avg_loss/decay=0.990000`` (eval,
+    ``run_summarization.py:124-127``); flushed every 100 records (``:243-244``)."""
+
+    TB_RENAME = {"eval_loss": "loss", "running_avg_loss": "running_avg_loss/decay=0.990000"}
+
+    def __init__(self, path: Optional[str], enabled: bool = True, tb_dir: Optional[str] = None):
         self.path = path if enabled else None
         self._f = None
         if self.path:
             os.makedirs(os.path.dirname(os.path.abspath(self.path)), exist_ok=True)
             self._f = open(self.path, "a", buffering=1)
+        self._tb = None
+        self._n = 0
+        if tb_dir and enabled:
+            from ..utils.tensorboard import EventWriter
+            self._tb = EventWriter(tb_dir)
 
     def log(self, **kv):
         if self._f:
             kv.setdefault("time", time.time())
             self._f.write(json.dumps(kv, sort_keys=True) + "\n")
+        if self._tb is not None and "step" in kv:
+            sc = {self.TB_RENAME.get(k, k): float(v) for k, v in kv.items()
+                  if k not in ("step", "time") and isinstance(v, (int, float)) and not isinstance(v, bool)}
+            self._tb.add_scalars(int(kv["step"]), sc)
+            self._n += 1
+            if self._n % 100 == 0:
+                self._tb.flush()
 
     def close(self):
         if self._f:
             self._f.close()
             self._f = None
+        if self._tb is not None:
+            self._tb.close()
+            self._tb = None
 
 
 def make_trainer(hps, vsize: int, info: Optional[DistInfo] = None, device: Optional[str] = None, params=None):
