@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch (rows)")
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (rows); 256 keeps the persistent LSTM grid at 128 of 256 CUs so the overlapped RCCL all-reduce always finds free CUs")
     ap.add_argument("--no-coverage", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled per rank")

@@ -269,6 +269,52 @@ void ptr_loss(const Tensor& logits, const OT& bias, const Tensor& target, const 
                   B, T, V, stream());
 }
 
+// fused training vocab head (vocab_train.hip): logits never materialised
+int64_t vocab_train_tiles_op(int64_t V) { return vocab_train_tiles((int)V); }
+
+// X: [N][ldx] bf16 (the first H columns are the activations; ldx >= H, ldx % 8 == 0)
+void vocab_train_fwd(const Tensor& X, const Tensor& WT, const Tensor& bias, const Tensor& target, const Tensor& part,
+                     const Tensor& zg, const Tensor& lse, const Tensor& pv, int64_t N, int64_t V, int64_t H,
+                     int64_t ldx) {
+  chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(target, I32, "target"); chk(part, F32, "part");
+  chk(zg, F32, "zg"); chk(lse, F32, "lse"); chk(pv, F32, "pv");
+  TORCH_CHECK(H == 128 || H == 256, "fused training vocab head: hidden size 128 or 256");
+  TORCH_CHECK(N >= 1 && V >= 1 && ldx >= H && ldx % 8 == 0, "bad N/V/ldx");
+  numel_eq(X, N * ldx, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias"); numel_eq(target, N, "target");
+  numel_eq(part, (int64_t)vocab_train_tiles((int)V) * N * 2, "part"); numel_eq(zg, N, "zg"); numel_eq(lse, N, "lse");
+  numel_eq(pv, N, "pv");
+  launch_vocab_train_fwd(P<bf16>(X), (int)ldx, P<bf16>(WT), P<float>(bias), P<int>(target), P<float>(part), P<float>(zg),
+                         P<float>(lse), P<float>(pv), N, V, H, stream());
+}
+
+void vocab_train_bwd(const Tensor& X, const Tensor& WT, const Tensor& bias, const Tensor& target, const Tensor& lse,
+                     const Tensor& alpha, const Tensor& dl, int64_t N, int64_t V, int64_t H, int64_t ldx) {
+  chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(target, I32, "target"); chk(lse, F32, "lse");
+  chk(alpha, F32, "alpha"); chk(dl, BF, "dl");
+  TORCH_CHECK(H == 128 || H == 256, "fused training vocab head: hidden size 128 or 256");
+  TORCH_CHECK(N >= 1 && V >= 1 && ldx >= H && ldx % 8 == 0, "bad N/V/ldx");
+  numel_eq(X, N * ldx, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias"); numel_eq(target, N, "target");
+  numel_eq(lse, N, "lse"); numel_eq(alpha, N, "alpha"); numel_eq(dl, N * V, "dl");
+  launch_vocab_train_bwd(P<bf16>(X), (int)ldx, P<bf16>(WT), P<float>(bias), P<int>(target), P<float>(lse), P<float>(alpha),
+                         P<bf16>(dl), N, V, H, stream());
+}
+
+void ptr_rowfin(const Tensor& pv, const Tensor& target, const Tensor& rowg, const OT& pgen, const OT& attn,
+                const Tensor& ext, const Tensor& lens, const Tensor& loss_row, const OT& alpha, const OT& dpre,
+                const OT& dA, int64_t N, int64_t B, int64_t T) {
+  chk(pv, F32, "pv"); chk(target, I32, "target"); chk(rowg, F32, "rowg"); chk(ext, I32, "ext"); chk(lens, I32, "lens");
+  chk(loss_row, F32, "loss_row");
+  TORCH_CHECK(B >= 1 && N % B == 0, "N must be D*B");
+  numel_eq(pv, N, "pv"); numel_eq(target, N, "target"); numel_eq(rowg, N, "rowg"); numel_eq(ext, B * T, "ext");
+  numel_eq(lens, B, "lens"); numel_eq(loss_row, N, "loss_row");
+  chko(pgen, F32, N, "pgen"); chko(attn, F32, N * T, "attn"); chko(alpha, F32, N, "alpha"); chko(dpre, F32, N, "dpre");
+  chko(dA, F32, N * T, "dA");
+  TORCH_CHECK(!PO<float>(pgen) || PO<float>(attn), "pointer mode needs attn");
+  launch_ptr_rowfin(P<float>(pv), P<int>(target), P<float>(rowg), PO<float>(pgen), PO<float>(attn), P<int>(ext),
+                    P<int>(lens), P<float>(loss_row), PO<float>(alpha), PO<float>(dpre), PO<float>(dA), N, B, T,
+                    stream());
+}
+
 void clip_adagrad(const Tensor& w, const Tensor& acc, const Tensor& g, const Tensor& part, double lr, double max_norm,
                   const Tensor& norm_out, const Tensor& flag) {
   chk(w, F32, "w"); chk(acc, F32, "acc"); chk(g, F32, "g"); chk(part, F32, "part"); chk(norm_out, F32, "norm_out");
@@ -433,6 +479,10 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("dec_bwd_cell", &dec_bwd_cell);
   m.def("dec_bwd_dz", &dec_bwd_dz);
   m.def("ptr_loss", &ptr_loss);
+  m.def("vocab_train_tiles", &vocab_train_tiles_op);
+  m.def("vocab_train_fwd", &vocab_train_fwd);
+  m.def("vocab_train_bwd", &vocab_train_bwd);
+  m.def("ptr_rowfin", &ptr_rowfin);
   m.def("clip_adagrad", &clip_adagrad);
   m.def("opt_parts", &opt_parts);
   m.def("final_topk", &final_topk);

@@ -84,3 +84,11 @@ int vocab_topk_tiles(int V);
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
                        int R, int V, int H, int T, int K, int beam, hipStream_t st);
+int vocab_train_tiles(int V);
+void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
+                            float* zg, float* lse, float* pv, int N, int V, int H, hipStream_t st);
+void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
+                            const float* lse, const float* alpha, bf16* dl, int N, int V, int H, hipStream_t st);
+void launch_ptr_rowfin(const float* pv, const int* target, const float* rowg, const float* pgen, const float* attn,
+                       const int* ext, const int* lens, float* loss_row, float* alpha, float* dpre, float* dA, int N,
+                       int B, int T, hipStream_t st);

@@ -1,0 +1,328 @@
+// Training vocab head without materialised logits (hard part 7.5-2;
+// reference model.py:229-268, 146-183, 446-460).
+//
+// The library path writes the [N, V] bf16 logits (N = D*B rows: 2.56 GB at B = 256) from a
+// K = 256 GEMM that is store-bound, then a loss kernel reads them back and overwrites them
+// with dlogits.  Here the logits only ever exist in MFMA accumulators:
+//
+//   pass 1  vocab_train_kernel<false>: logits tile (32 rows x 256 columns, K = H) ->
+//           per-row (max, sum exp) partial of the tile -> part[vt][row]; the tile holding a
+//           row's gold id also records its logit z_w.  No [N, V] traffic at all.
+//   rows    vocab_rowstats_kernel: lse = combine(partials), p_vocab(w) = exp(z_w - lse).
+//           ptr_rowfin_kernel: copy mass of w, P = p_gen p_vocab + (1 - p_gen) copy,
+//           loss, alpha = g p_gen p_vocab / P, dpre, dA (one wave per row).
+//   pass 2  vocab_train_kernel<true>: recompute the tile, dz = alpha (exp(z - lse) - [k == w])
+//           -> bf16 dlogits (the only [N, V] traffic: one write, read by the two weight /
+//           input gradient GEMMs).
+//
+// Both passes run a persistent grid: the (vocab tile, row block) units are laid out vocab-
+// tile-major and every workgroup takes one contiguous range, so a workgroup keeps one W^T
+// tile's fragments in registers (128 VGPRs at H = 256) across many row blocks and reloads
+// them only at a tile boundary; the 32 x H row block of X is staged in LDS per unit (shared
+// by the 4 waves, each of which owns 64 of the 256 columns).
+#include "common.h"
+
+#define VR_ROWS 32   // rows per unit (2 MFMA row tiles)
+#define VR_COLS 256
+#define LOG2E_F 1.4426950408889634f
+#define LN2_F 0.6931471805599453f
+
+namespace {
+
+__device__ __forceinline__ void ms_merge(float& m, float& s, float m2, float s2) {
+  const float M = fmaxf(m, m2);
+  if (M == -INFINITY) return;
+  s = (m == -INFINITY ? 0.f : s * fexp(m - M)) + (m2 == -INFINITY ? 0.f : s2 * fexp(m2 - M));
+  m = M;
+}
+
+// max / sum over the 16 lanes of one accumulator column group (lanes l, l^1, .., l^8)
+__device__ __forceinline__ float max16(float x) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+__device__ __forceinline__ float sum16(float x) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+}  // namespace
+
+// Operands are swapped relative to a plain logits GEMM: A = W^T fragments (16 vocab
+// columns x 32 k, held in registers), B = X fragments (32 k x 16 rows, from LDS), so
+// accumulator (i, j, r) holds logit[row = rb + 16j + (lane & 15)][col = cw + 16i + 4(lane>>4) + r]:
+// every lane owns 16 columns of each of its rows, so a row's softmax partial is 15 in-lane
+// ops + 2 cross-lane steps (the 4 lanes l, l^16, l^32, l^48), and each lane's 4 consecutive
+// columns are one 8-byte bf16 store in pass 2.
+//
+// Per unit ONE barrier: the X rows of unit u+1 are loaded into registers before unit u's
+// MFMAs and written to the other LDS buffer after its epilogue; the cross-wave (max, sum)
+// merge of unit u is done by wave 0 after the barrier (double-buffered Pm/Ps).
+template <int H, bool GRAD>
+__global__ __launch_bounds__(256, 2) void vocab_train_kernel(
+    const bf16* __restrict__ X,       // [N][ldx] output-projection activations (first H columns)
+    const bf16* __restrict__ WT,      // [V][H]   output_projection/w transposed
+    const float* __restrict__ bias,   // [V]
+    const int* __restrict__ target,   // [N]      gold extended-vocab id
+    float* __restrict__ part,         // [nt][N][2]  pass 1: per-tile (max, sum exp)
+    float* __restrict__ zg,           // [N]      pass 1: gold logit (rows with w < V)
+    const float* __restrict__ lse,    // [N]      pass 2
+    const float* __restrict__ alpha,  // [N]      pass 2
+    bf16* __restrict__ dl,            // [N][V]   pass 2: dlogits
+    int N, int V, int ldx) {
+  constexpr int KS = H / 32;          // k-steps of 32
+  constexpr int XS = H + 8;           // padded LDS row (bank spread)
+  constexpr int RJ = VR_ROWS / 16;    // 16-row MFMA tiles per unit
+  constexpr int CH = VR_ROWS * H / 8 / 256;  // 16-byte X chunks per thread per unit
+  static_assert(CH >= 1 && VR_ROWS * H / 8 % 256 == 0, "X staging");
+  __shared__ __attribute__((aligned(16))) bf16 Xs[2][VR_ROWS * XS];
+  __shared__ float Pm[2][4][VR_ROWS], Ps[2][4][VR_ROWS];
+  __shared__ int Tg[2][VR_ROWS];
+  __shared__ float Ls[2][VR_ROWS], Al[2][VR_ROWS];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int RB = (N + VR_ROWS - 1) / VR_ROWS, nt = (V + VR_COLS - 1) / VR_COLS;
+  const long units = (long)RB * nt;
+  const int u0 = (int)(units * blockIdx.x / gridDim.x), u1 = (int)(units * (blockIdx.x + 1) / gridDim.x);
+  if (u0 >= u1) return;
+  const int kof = 8 * (lane >> 4), c16 = lane & 15, q4 = 4 * (lane >> 4);
+  bf16x8 wa[KS][4];   // A fragments: W^T rows (vocab columns) of this wave's 4 column tiles
+  float bcol[4][4];   // log2(e) x bias of the lane's columns cw + 16i + q4 + r (-inf past V in pass 1)
+  int cur_vt = -1;
+  bf16x8 xr[CH];      // prefetched X chunks of the next unit
+  int tg_r = 0;
+  float ls_r = 0.f, al_r = 0.f;
+  auto fetch = [&](int u) {  // global -> registers (unit u's X rows, targets, row scalars)
+    const int rb = (u % RB) * VR_ROWS;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = c * 256 + threadIdx.x, rr = idx / (H / 8), k8 = (idx % (H / 8)) * 8;
+      xr[c] = ld8(X + (size_t)min(rb + rr, N - 1) * ldx + k8);
+    }
+    if (threadIdx.x < VR_ROWS) {
+      const int row = min(rb + threadIdx.x, N - 1);
+      tg_r = target[row];
+      if (GRAD) {
+        ls_r = lse[row];
+        al_r = alpha[row];
+      }
+    }
+  };
+  auto stash = [&](int buf) {  // registers -> LDS buffer
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = c * 256 + threadIdx.x, rr = idx / (H / 8), k8 = (idx % (H / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&Xs[buf][rr * XS + k8]) = xr[c];
+    }
+    if (threadIdx.x < VR_ROWS) {
+      Tg[buf][threadIdx.x] = tg_r;
+      if (GRAD) {
+        Ls[buf][threadIdx.x] = ls_r;
+        Al[buf][threadIdx.x] = al_r;
+      }
+    }
+  };
+  auto merge_store = [&](int buf, int u) {  // pass 1: cross-wave (max, sum) of unit u -> part
+    const int vt = u / RB, rb = (u % RB) * VR_ROWS;
+    if (wid == 0 && lane < VR_ROWS && rb + lane < N) {
+      float m = Pm[buf][0][lane], sm = Ps[buf][0][lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) ms_merge(m, sm, Pm[buf][w][lane], Ps[buf][w][lane]);
+      *reinterpret_cast<float2*>(part + ((size_t)vt * N + rb + lane) * 2) = make_float2(m, sm);
+    }
+  };
+  fetch(u0);
+  stash(0);
+  __syncthreads();
+  for (int u = u0; u < u1; ++u) {
+    const int buf = (u - u0) & 1;
+    const int vt = u / RB, rb = (u % RB) * VR_ROWS;
+    const int cw = vt * VR_COLS + 64 * wid;  // this wave's first column
+    if (vt != cur_vt) {  // new vocab tile: its A fragments and bias into registers
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16* arow = WT + (size_t)min(cw + 16 * i + c16, V - 1) * H + kof;
+#pragma unroll
+        for (int h = 0; h < KS; ++h) wa[h][i] = ld8(arow + 32 * h);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int col = cw + 16 * i + q4 + r;
+          bcol[i][r] = col < V ? bias[col] * LOG2E_F : (GRAD ? 0.f : -INFINITY);
+        }
+      }
+      cur_vt = vt;
+    }
+    if (u + 1 < u1) fetch(u + 1);
+    f32x4 acc[4][RJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int h = 0; h < KS; ++h)
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&Xs[buf][(16 * j + c16) * XS + 32 * h + kof]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(wa[h][i], xb, acc[i][j]);
+      }
+    if constexpr (!GRAD) {
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        const int rr = 16 * j + c16, row = rb + rr;
+        const int wo = Tg[buf][rr] - cw - q4;  // gold column relative to the lane's first one
+        // y = log2(e) x logit (base-2 domain: one FMA per element, exp2 without a multiply)
+        float y[4][4], m = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            y[i][r] = fmaf(acc[i][j][r], LOG2E_F, bcol[i][r]);  // -inf for columns >= V
+            m = fmaxf(m, y[i][r]);
+          }
+          const int o = wo - 16 * i;
+          if ((unsigned)o < 4u && row < N)
+            zg[row] = (o == 0 ? y[i][0] : o == 1 ? y[i][1] : o == 2 ? y[i][2] : y[i][3]) * LN2_F;
+        }
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        float sm = 0.f;
+        if (m > -INFINITY) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sm += __builtin_amdgcn_exp2f(y[i][r] - m);
+        }
+        sm += __shfl_xor(sm, 16, 64);
+        sm += __shfl_xor(sm, 32, 64);
+        if (lane < 16) {
+          Pm[buf][wid][rr] = m * LN2_F;  // natural-log domain for the partial
+          Ps[buf][wid][rr] = sm;
+        }
+      }
+    } else {
+      const bool vec = (V % 4 == 0);
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        const int rr = 16 * j + c16, row = rb + rr;
+        const int wo = Tg[buf][rr] - cw - q4;
+        const float al = Al[buf][rr];
+        // alpha exp(z - lse) = exp2(log2(e) z + log2(alpha) - log2(e) lse)   (alpha >= 0)
+        const float c = al > 0.f ? __log2f(al) - Ls[buf][rr] * LOG2E_F : -INFINITY;
+        if (row < N) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int col = cw + 16 * i + q4;
+            const int o = wo - 16 * i;
+            float d[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              d[r] = __builtin_amdgcn_exp2f(fmaf(acc[i][j][r], LOG2E_F, bcol[i][r] + c)) - (o == r ? al : 0.f);
+            bf16* dst = dl + (size_t)row * V + col;
+            if (vec && col + 4 <= V) {
+              typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+              *reinterpret_cast<bf16x4*>(dst) = bf16x4{f2bf(d[0]), f2bf(d[1]), f2bf(d[2]), f2bf(d[3])};
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (col + r < V) dst[r] = f2bf(d[r]);
+            }
+          }
+        }
+      }
+    }
+    if (u + 1 < u1) stash(buf ^ 1);
+    __syncthreads();
+    if constexpr (!GRAD) merge_store(buf, u);
+  }
+}
+
+// lse and p_vocab(gold) per row; one thread per row, partials read coalesced across rows.
+__global__ __launch_bounds__(256) void vocab_rowstats_kernel(const float* __restrict__ part, const float* __restrict__ zg,
+                                                             const int* __restrict__ target, float* __restrict__ lse,
+                                                             float* __restrict__ pv, int N, int V, int nt) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float m = -INFINITY, s = 0.f;
+  for (int vt = 0; vt < nt; ++vt) {
+    const float2 p = *reinterpret_cast<const float2*>(part + ((size_t)vt * N + n) * 2);
+    ms_merge(m, s, p.x, p.y);
+  }
+  const float L = m + __logf(s);
+  lse[n] = L;
+  const int w = target[n];
+  pv[n] = w < V ? fexp(zg[n] - L) : 0.f;
+}
+
+// Pointer mixture per row (one wave per row): copy mass of the gold id, P, loss, the
+// dlogits scale alpha, dpre (p_gen pre-sigmoid) and dA (attention), as ptr_loss.
+__global__ __launch_bounds__(256) void ptr_rowfin_kernel(
+    const float* __restrict__ pv_in, const int* __restrict__ target, const float* __restrict__ rowg,
+    const float* __restrict__ pgen, const float* __restrict__ attn, const int* __restrict__ ext,
+    const int* __restrict__ lens, float* __restrict__ loss_row, float* __restrict__ alpha, float* __restrict__ dpre,
+    float* __restrict__ dA, int N, int B, int T) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
+  const int b = n % B, w = target[n], len = lens[b];
+  const float g = rowg[n], pv = pv_in[n];
+  const float pg = pgen ? pgen[n] : 1.0f;
+  const int* er = ext + (size_t)b * T;
+  float cm = 0.f;
+  if (pgen) {
+    const float* ar = attn + (size_t)n * T;
+    for (int i = lane; i < len; i += 64) cm += er[i] == w ? ar[i] : 0.f;
+    cm = wave_sum(cm);
+  }
+  const float P = pg * pv + (1.0f - pg) * cm;
+  const float invP = 1.0f / P;
+  if (lane == 0) {
+    loss_row[n] = g != 0.f ? -__logf(P) : 0.f;
+    if (alpha) alpha[n] = g != 0.f ? g * pg * pv * invP : 0.f;
+    if (pgen && dpre) dpre[n] = g != 0.f ? -g * (pv - cm) * invP * pg * (1.0f - pg) : 0.f;
+  }
+  if (pgen && dA) {
+    const float coef = g != 0.f ? -g * (1.0f - pg) * invP : 0.f;
+    float* dar = dA + (size_t)n * T;
+    for (int i = lane; i < T; i += 64) dar[i] = (i < len && er[i] == w) ? coef : 0.f;
+  }
+}
+
+int vocab_train_tiles(int V) { return (V + VR_COLS - 1) / VR_COLS; }
+
+// 2 workgroups per CU (<= 256 VGPRs, ~36 KB LDS each): 512 persistent workgroups
+static int vocab_train_grid(int N, int V) {
+  const long units = (long)((N + VR_ROWS - 1) / VR_ROWS) * vocab_train_tiles(V);
+  return (int)(units < 512 ? units : 512);
+}
+
+void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
+                            float* zg, float* lse, float* pv, int N, int V, int H, hipStream_t st) {
+  const int grid = vocab_train_grid(N, V);
+  if (H == 256)
+    hipLaunchKernelGGL((vocab_train_kernel<256, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, part, zg,
+                       nullptr, nullptr, nullptr, N, V, ldx);
+  else
+    hipLaunchKernelGGL((vocab_train_kernel<128, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, part, zg,
+                       nullptr, nullptr, nullptr, N, V, ldx);
+  hipLaunchKernelGGL(vocab_rowstats_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part, zg, target, lse, pv, N, V,
+                     vocab_train_tiles(V));
+}
+
+void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
+                            const float* lse, const float* alpha, bf16* dl, int N, int V, int H, hipStream_t st) {
+  const int grid = vocab_train_grid(N, V);
+  if (H == 256)
+    hipLaunchKernelGGL((vocab_train_kernel<256, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, nullptr,
+                       nullptr, lse, alpha, dl, N, V, ldx);
+  else
+    hipLaunchKernelGGL((vocab_train_kernel<128, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, nullptr,
+                       nullptr, lse, alpha, dl, N, V, ldx);
+}
+
+void launch_ptr_rowfin(const float* pv, const int* target, const float* rowg, const float* pgen, const float* attn,
+                       const int* ext, const int* lens, float* loss_row, float* alpha, float* dpre, float* dA, int N,
+                       int B, int T, hipStream_t st) {
+  hipLaunchKernelGGL(ptr_rowfin_kernel, dim3((N + 3) / 4), dim3(256), 0, st, pv, target, rowg, pgen, attn, ext, lens,
+                     loss_row, alpha, dpre, dA, N, B, T);
+}

@@ -101,6 +101,31 @@ def test_fused_attention_backward_matches_two_kernel_path(monkeypatch, coverage,
         assert _rel(a, b) < tol, _rel(a, b)
 
 
+@pytest.mark.parametrize("coverage,pointer_gen,H", [(True, True, 256), (False, False, 128)])
+def test_fused_vocab_head_matches_library_path(monkeypatch, coverage, pointer_gen, H):
+    """vocab_train (MFMA logits in registers, per-tile LSE partials, recomputed dlogits) ==
+    library GEMM + ptr_loss.  V = 2000 leaves a partial 256-column tile, N = 150 a partial
+    32-row block."""
+    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
+    hps, vocab, batch, params = _setup(coverage, pointer_gen, B=15, T=64, D=10, H=H)
+    got = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TSAMD_FUSED_VOCAB_TRAIN", flag)
+        params.enable_grad()
+        eng = HipPointerGenerator(hps, vocab.size(), params, B=hps.batch_size, T=hps.max_enc_steps)
+        assert eng.fused_vocab == (flag == "1")
+        eng.set_batch(batch)
+        out = eng.forward(need_grad=True)
+        eng.backward()
+        torch.cuda.synchronize()
+        got.append((out["loss"].clone(), eng.w["loss_row"].clone(), params.grad.clone()))
+        if pointer_gen:
+            got[-1] += (eng.w["dpre"].clone(), eng.w["dA"].clone())
+    # fp32 bias and fp32 accumulators vs bf16 logits: agreement at the bf16 rounding level
+    for a, b in zip(got[0], got[1]):
+        assert _rel(a, b) < 1e-2, _rel(a, b)
+
+
 def test_train_step_decreases_loss():
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
     hps, vocab, batch, params = _setup(True, B=16, T=64, D=10, V=2000, E=64, H=64)

@@ -103,6 +103,11 @@ class HipPointerGenerator:
             raise ValueError("max_enc_steps > 2048 not supported by the attention kernels")
         self.k = _ops()
         self.nchunk = int(self.k.attn_chunks(T))
+        # the output-projection weight gradient runs on a side stream, overlapped with the
+        # decoder backward loop (joined at the end of backward_mid) when TSAMD_OVERLAP_DW=1.
+        # Off by default: the graph-captured B=256 bench with the fork/join stalled on MI355X
+        # (no progress for 180 s) and the GEMM is ~0.7 ms of a ~27 ms step.
+        self._side = torch.cuda.Stream(self.dev) if os.environ.get("TSAMD_OVERLAP_DW", "0") == "1" else None
         self._alloc()
         self.pack()
 
@@ -174,8 +179,15 @@ class HipPointerGenerator:
         w["outb"] = w["outb_ext"][:, :H]
         w["pg"] = z(D, B)
         w["loss_row"] = z(D, B)
-        # bf16 logits (bias added in the GEMM epilogue); ptr_loss overwrites them in place
-        # with dlogits
+        # fused vocab head (vocab_train.hip): logits live only in MFMA accumulators, the
+        # [N, V] buffer receives dlogits; TSAMD_FUSED_VOCAB_TRAIN=0 selects the library GEMM
+        # (bf16 logits, bias in the epilogue) + ptr_loss, which rewrites them in place
+        self.fused_vocab = (os.environ.get("TSAMD_FUSED_VOCAB_TRAIN", "1") != "0" and H in (128, 256))
+        if self.fused_vocab:
+            N = D * B
+            w["vpart"] = z(int(self.k.vocab_train_tiles(V)) * N * 2)
+            for n in ("zg", "lse", "pv", "alpha"):
+                w[n] = z(N)
         w["logits"] = z(D * B, V, dt=BF)
         # backward
         w["dlogits"] = w["logits"]
@@ -238,6 +250,8 @@ class HipPointerGenerator:
         put("OUTmT", p[OUT_M].t())  # [H][H+A] for the per-step linear2 kernel (decode)
         put("ow", p[OW])
         put("ovb", p[OV])  # bias of the bf16 logits GEMM epilogue
+        if getattr(self, "fused_vocab", False):
+            put("owT", p[OW].t())  # [V][H] B operand of the fused vocab head
         self.pk = pk
         self.f32 = {
             "v": p[VATT].reshape(A).contiguous(),
@@ -363,6 +377,18 @@ class HipPointerGenerator:
                    + Hn.float() @ pm[A + H:A + 2 * H] + w["X"].view(N, E) @ pm[A + 2 * H:] + p[PG_B])
             w["pg"].view(N).copy_(torch.sigmoid(pre))
             pg = w["pg"]
+        if self.fused_vocab:
+            k, ldx = self.k, H + 8  # outb is the first H columns of outb_ext
+            k.vocab_train_fwd(w["outb_ext"], self.pk["owT"], p[OV], w["target_t"], w["vpart"], w["zg"], w["lse"],
+                              w["pv"], N, V, H, ldx)
+            k.ptr_rowfin(w["pv"], w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None, w["ext"],
+                         w["enc_lens"], w["loss_row"], w["alpha"] if need_grad else None,
+                         w["dpre"] if (need_grad and hps.pointer_gen) else None,
+                         w["dA"] if (need_grad and hps.pointer_gen) else None, N, B, T)
+            if need_grad:
+                k.vocab_train_bwd(w["outb_ext"], self.pk["owT"], p[OV], w["target_t"], w["lse"], w["alpha"],
+                                  w["dlogits"], N, V, H, ldx)
+            return
         torch.addmm(self.pk["ovb"], w["outb"], self.pk["ow"], out=w["logits"])
         self.k.ptr_loss(w["logits"], None, w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None,
                         w["ext"], w["enc_lens"], w["loss_row"], w["dlogits"] if need_grad else None,
@@ -412,7 +438,13 @@ class HipPointerGenerator:
         H, V = self.H, self.V
         assert p.offsets[OV][0] == p.offsets[OW][0] + H * V
         o = p.offsets[OW][0]
-        torch.mm(w["outb_ext"][:, :H + 1].t(), dl, out_dtype=F32, out=p.grad[o:o + (H + 1) * V].view(H + 1, V))
+        dst = p.grad[o:o + (H + 1) * V].view(H + 1, V)
+        if self._side is not None:  # off the critical path: only the all-reduce bucket needs it
+            self._side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._side):
+                torch.mm(w["outb_ext"][:, :H + 1].t(), dl, out_dtype=F32, out=dst)
+        else:
+            torch.mm(w["outb_ext"][:, :H + 1].t(), dl, out_dtype=F32, out=dst)
         self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
 
     def backward_mid(self):
@@ -513,6 +545,8 @@ class HipPointerGenerator:
         mm_into(dE.view(B * T, A), dFb, self.pk["Wh"].t())
         dE.baddbmm_(w["ATT"].permute(1, 2, 0), w["DCTX"].permute(1, 0, 2))  # += a^T . dctx  [B,T,A]
         self._dE, self._d_emb_dec = dE, d_emb_dec
+        if self._side is not None:  # join the output-projection weight gradient
+            torch.cuda.current_stream().wait_stream(self._side)
 
     def backward_tail(self):
         """reduce_states, encoder BPTT, embedding (the last bucket)."""

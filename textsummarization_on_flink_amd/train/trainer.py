@@ -93,14 +93,23 @@ class GraphTrainer:
         self.engine.pack()
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        # three graphs (forward + vocab backward | decoder backward | encoder backward) so
-        # each gradient bucket's all-reduce overlaps the next phase
-        self.g_fb = [torch.cuda.CUDAGraph() for _ in range(3)]
-        with torch.cuda.graph(self.g_fb[0], pool=pool):
-            self.out = self._fwd_head()
-        with torch.cuda.graph(self.g_fb[1], pool=pool):
-            self.engine.backward_mid()
-        with torch.cuda.graph(self.g_fb[2], pool=pool):
+        if self.engine._side is None:
+            # three graphs (forward + vocab backward | decoder backward | encoder backward) so
+            # each gradient bucket's all-reduce overlaps the next phase
+            self.g_fb = [torch.cuda.CUDAGraph() for _ in range(3)]
+            with torch.cuda.graph(self.g_fb[0], pool=pool):
+                self.out = self._fwd_head()
+            with torch.cuda.graph(self.g_fb[1], pool=pool):
+                self.engine.backward_mid()
+        else:
+            # TSAMD_OVERLAP_DW=1: two graphs (forward + vocab backward + decoder backward, with
+            # the output-projection weight gradient forked onto a side stream and joined inside
+            # the graph) | encoder backward
+            self.g_fb = [torch.cuda.CUDAGraph() for _ in range(2)]
+            with torch.cuda.graph(self.g_fb[0], pool=pool):
+                self.out = self._fwd_head()
+                self.engine.backward_mid()
+        with torch.cuda.graph(self.g_fb[-1], pool=pool):
             self.engine.backward_tail()
         self.g_opt = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_opt, pool=pool):
@@ -116,19 +125,23 @@ class GraphTrainer:
             ev = self._events() if self.timing else None
             if ev:
                 ev[0].record()
+            ng = len(self.g_fb)
             for i, g in enumerate(self.g_fb):
                 g.replay()
                 if ev:
                     ev[i + 1].record()
-                if i < 2:
+                if ng == 3 and i < 2:
                     self.reducer.bucket_ready(i)
+                elif ng == 2 and i == 0:  # the merged graph finalises both buckets
+                    self.reducer.bucket_ready(0)
+                    self.reducer.bucket_ready(1)
             self._maybe_poison()
             self.reducer()
             if ev:
-                ev[4].record()
+                ev[ng + 1].record()
             self.g_opt.replay()
             if ev:
-                ev[5].record()
+                ev[ng + 2].record()
             out = self.out
         else:
             out = self._fb()
@@ -140,16 +153,20 @@ class GraphTrainer:
 
     def _events(self):
         if self._ev is None:
-            self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+            self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(self.g_fb) + 3)]
         return self._ev
 
     def phase_ms(self) -> Dict[str, float]:
         """Time of each phase of the last step (host-synchronising): forward + vocab backward,
-        decoder backward, encoder backward, exposed all-reduce wait, optimizer."""
+        decoder backward, encoder backward, exposed all-reduce wait, optimizer (the first two
+        are one phase, ``ms_fwd_bwd_dec``, under TSAMD_OVERLAP_DW=1)."""
         if not self._ev:
             return {}
-        self._ev[5].synchronize()
-        names = ("ms_fwd_head", "ms_bwd_dec", "ms_bwd_enc", "ms_allreduce", "ms_optimizer")
+        self._ev[-1].synchronize()
+        if len(self._ev) == 6:
+            names = ("ms_fwd_head", "ms_bwd_dec", "ms_bwd_enc", "ms_allreduce", "ms_optimizer")
+        else:
+            names = ("ms_fwd_bwd_dec", "ms_bwd_enc", "ms_allreduce", "ms_optimizer")
         return {n: self._ev[i].elapsed_time(self._ev[i + 1]) for i, n in enumerate(names)}
 
     def _maybe_poison(self):
