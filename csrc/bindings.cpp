@@ -178,16 +178,29 @@ void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const 
                    const Tensor& de_all, const Tensor& lens, const Tensor& dF, const Tensor& dv, const OT& dwc,
                    int64_t D, int64_t B, int64_t T, int64_t A) {
   chk(F, BF, "F"); chk(S_all, F32, "S_all"); chk(v, F32, "v"); chk(de_all, F32, "de_all"); chk(lens, I32, "lens");
-  chk(dF, F32, "dF"); chk(dv, F32, "dv");
+  chk(dF, BF, "dF"); chk(dv, F32, "dv");
   TORCH_CHECK(A % 64 == 0, "bad A");
   numel_eq(F, B * T * A, "F"); numel_eq(S_all, D * B * A, "S_all"); numel_eq(de_all, D * B * T, "de_all");
   numel_eq(dF, B * T * A, "dF"); numel_eq(dv, A, "dv");
   chko(wc, F32, A, "wc"); chko(cov_all, F32, D * B * T, "cov_all"); chko(dwc, F32, A, "dwc");
   launch_attn_bwd_feat(P<bf16>(F), P<float>(S_all), P<float>(v), PO<float>(wc), PO<float>(cov_all), P<float>(de_all),
-                       P<int>(lens), P<float>(dF), P<float>(dv), PO<float>(dwc), D, B, T, A, stream());
+                       P<int>(lens), P<bf16>(dF), P<float>(dv), PO<float>(dwc), D, B, T, A, stream());
 }
 
 int64_t attn_chunks(int64_t T) { return attn_nchunk(T); }
+
+// ---------------------------------------------------------------- embedding gradient
+void emb_grad(const Tensor& gemb, const Tensor& ids0, const Tensor& src0, const Tensor& ids1, const Tensor& src1) {
+  chk(gemb, F32, "gemb"); chk(src0, F32, "src0"); chk(src1, F32, "src1");
+  TORCH_CHECK(ids0.scalar_type() == at::kLong && ids1.scalar_type() == at::kLong && ids0.is_contiguous() &&
+              ids1.is_contiguous(), "ids must be contiguous int64");
+  TORCH_CHECK(gemb.dim() == 2, "gemb must be [V][E]");
+  const int64_t E = gemb.size(1), V = gemb.size(0);
+  numel_eq(src0, ids0.numel() * E, "src0"); numel_eq(src1, ids1.numel() * E, "src1");
+  launch_emb_grad(P<float>(gemb), P<int64_t>(ids0), P<float>(src0), (int)ids0.numel(), P<int64_t>(ids1), P<float>(src1),
+                  (int)ids1.numel(), (int)E, (int)V, stream());
+}
+
 
 // ---------------------------------------------------------------- decoder cell
 void dec_cell_fwd(const Tensor& XG, const OT& ctxp, const Tensor& hprev, const Tensor& cprev, const Tensor& WcT,
@@ -288,15 +301,16 @@ void vocab_train_fwd(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
 }
 
 void vocab_train_bwd(const Tensor& X, const Tensor& WT, const Tensor& bias, const Tensor& target, const Tensor& lse,
-                     const Tensor& alpha, const Tensor& dl, int64_t N, int64_t V, int64_t H, int64_t ldx) {
+                     const Tensor& alpha, const Tensor& dl, const OT& dbias, int64_t N, int64_t V, int64_t H,
+                     int64_t ldx) {
   chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(target, I32, "target"); chk(lse, F32, "lse");
   chk(alpha, F32, "alpha"); chk(dl, BF, "dl");
   TORCH_CHECK(H == 128 || H == 256, "fused training vocab head: hidden size 128 or 256");
   TORCH_CHECK(N >= 1 && V >= 1 && ldx >= H && ldx % 8 == 0, "bad N/V/ldx");
   numel_eq(X, N * ldx, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias"); numel_eq(target, N, "target");
-  numel_eq(lse, N, "lse"); numel_eq(alpha, N, "alpha"); numel_eq(dl, N * V, "dl");
+  numel_eq(lse, N, "lse"); numel_eq(alpha, N, "alpha"); numel_eq(dl, N * V, "dl"); chko(dbias, F32, V, "dbias");
   launch_vocab_train_bwd(P<bf16>(X), (int)ldx, P<bf16>(WT), P<float>(bias), P<int>(target), P<float>(lse), P<float>(alpha),
-                         P<bf16>(dl), N, V, H, stream());
+                         P<bf16>(dl), PO<float>(dbias), N, V, H, stream());
 }
 
 void ptr_rowfin(const Tensor& pv, const Tensor& target, const Tensor& rowg, const OT& pgen, const OT& attn,
@@ -482,6 +496,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("vocab_train_tiles", &vocab_train_tiles_op);
   m.def("vocab_train_fwd", &vocab_train_fwd);
   m.def("vocab_train_bwd", &vocab_train_bwd);
+  m.def("emb_grad", &emb_grad);
   m.def("ptr_rowfin", &ptr_rowfin);
   m.def("clip_adagrad", &clip_adagrad);
   m.def("opt_parts", &opt_parts);

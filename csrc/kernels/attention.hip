@@ -466,8 +466,8 @@ __device__ __forceinline__ float bfly8(const float (&x)[8], int b5, int b4, int 
 // software-pipelined: group 0's E/F rows are issued before the S reduction (whose global
 // loads and block barriers then overlap them); group g+1's E rows are issued right after
 // group g's dots, its F rows right after group g's tanh pass.
-template <int NK, int NG>
-__global__ __launch_bounds__(256) void attn_bwd_step_kernel(
+template <int NK, int NG, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_step_kernel(
     const bf16* __restrict__ E, const bf16* __restrict__ F, const float* __restrict__ s,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
     const float* __restrict__ a, const float* __restrict__ dctx, const float* __restrict__ ctx,
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(256) void attn_bwd_step_kernel(
 __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
     const bf16* __restrict__ F, const float* __restrict__ S_all, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov_all, const float* __restrict__ de_all,
-    const int* __restrict__ lens, float* __restrict__ dF, float* __restrict__ dv, float* __restrict__ dwc,
+    const int* __restrict__ lens, bf16* __restrict__ dF, float* __restrict__ dv, float* __restrict__ dwc,
     int D, int B, int T, int A) {
   __shared__ float pv[4][512];
   __shared__ float pw[4][512];
@@ -738,15 +738,17 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (q < np) {
-        float* o = dF + ((size_t)b * T + p0 + q) * A + k0;
-        float r8[8];
+      if (p0 + q < T) {  // bf16 straight into the GEMM operand; zeros past len
+        bf16x8 o8;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r8[j] = 4.0f * vk[j] * acc[q][j >> 1][j & 1];
-        *reinterpret_cast<float4*>(o) = make_float4(r8[0], r8[1], r8[2], r8[3]);
-        *reinterpret_cast<float4*>(o + 4) = make_float4(r8[4], r8[5], r8[6], r8[7]);
+        for (int j = 0; j < 8; ++j) o8[j] = f2bf(q < np ? 4.0f * vk[j] * acc[q][j >> 1][j & 1] : 0.f);
+        *reinterpret_cast<bf16x8*>(dF + ((size_t)b * T + p0 + q) * A + k0) = o8;
       }
     }
+  } else if (kok) {  // fully masked positions of this wave: dF = 0 (no separate memset)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (p0 + q < T) *reinterpret_cast<bf16x8*>(dF + ((size_t)b * T + p0 + q) * A + k0) = zero8();
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -825,17 +827,25 @@ void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const fl
                           const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
                           float* dcov_out, int B, int T, int A, hipStream_t st) {
-  // groups of 8 positions per wave; TSAMD_ATTN_NG=2 selects 64-position blocks (A/B runs)
+  // groups of 8 positions per wave; TSAMD_ATTN_NG=2 selects 64-position blocks (A/B runs).
+  // TSAMD_ATTN_OCC=3|4 caps the registers for 3|4 waves per SIMD (tuning runs).
   static const int ng = [] { const char* e = getenv("TSAMD_ATTN_NG"); return e && atoi(e) == 2 ? 2 : 4; }();
+  static const int occ = [] { const char* e = getenv("TSAMD_ATTN_OCC"); return e ? atoi(e) : 0; }();
   dim3 grid((T + 32 * ng - 1) / (32 * ng), B);
-#define LB(NK, NG) hipLaunchKernelGGL((attn_bwd_step_kernel<NK, NG>), grid, dim3(256), 0, st, E, F, s, v, wc, cov, a, \
-                                      dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A)
-  if (A <= 512) { if (ng == 2) LB(1, 2); else LB(1, 4); }
-  else { if (ng == 2) LB(2, 2); else LB(2, 4); }
+#define LB(NK, NG, OC) hipLaunchKernelGGL((attn_bwd_step_kernel<NK, NG, OC>), grid, dim3(256), 0, st, E, F, s, v, wc, \
+                                          cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A)
+  if (A <= 512) {
+    if (ng == 2) LB(1, 2, 1);
+    else if (occ == 3) LB(1, 4, 3);
+    else if (occ == 4) LB(1, 4, 4);
+    else LB(1, 4, 1);
+  } else {
+    if (ng == 2) LB(2, 2, 1); else LB(2, 4, 1);
+  }
 #undef LB
 }
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
-                          const float* de_all, const int* lens, float* dF, float* dv, float* dwc, int D, int B, int T,
+                          const float* de_all, const int* lens, bf16* dF, float* dv, float* dwc, int D, int B, int T,
                           int A, hipStream_t st) {
   dim3 grid((T + 15) / 16, B, (A + 511) / 512);
   hipLaunchKernelGGL(attn_bwd_feat_kernel, grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF, dv,

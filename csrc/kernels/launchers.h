@@ -26,7 +26,7 @@ void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const fl
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
                           float* dcov_out, int B, int T, int A, hipStream_t st);
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
-                          const float* de_all, const int* lens, float* dF, float* dv, float* dwc, int D, int B, int T,
+                          const float* de_all, const int* lens, bf16* dF, float* dv, float* dwc, int D, int B, int T,
                           int A, hipStream_t st);
 
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
@@ -88,7 +88,12 @@ int vocab_train_tiles(int V);
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
                             float* zg, float* lse, float* pv, int N, int V, int H, hipStream_t st);
 void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
-                            const float* lse, const float* alpha, bf16* dl, int N, int V, int H, hipStream_t st);
+                            const float* lse, const float* alpha, bf16* dl, float* dbias, int N, int V, int H,
+                            hipStream_t st);
 void launch_ptr_rowfin(const float* pv, const int* target, const float* rowg, const float* pgen, const float* attn,
                        const int* ext, const int* lens, float* loss_row, float* alpha, float* dpre, float* dA, int N,
                        int B, int T, hipStream_t st);
+
+// embedding.hip
+void launch_emb_grad(float* gemb, const int64_t* ids0, const float* src0, int n0, const int64_t* ids1,
+                     const float* src1, int n1, int E, int V, hipStream_t st);

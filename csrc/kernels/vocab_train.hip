@@ -48,6 +48,38 @@ __device__ __forceinline__ float sum16(float x) {
   return x;
 }
 
+// x <- x + x(partner) where partner is given by a DPP lane pattern inside a 16-lane row
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+#define DPP_MIRROR 0x140       // l <-> 15 - l  (flips bit 3 of the row lane)
+#define DPP_HALF_MIRROR 0x141  // l <-> 7 - l within each half (flips bit 2)
+#define DPP_XOR2 0x4e          // quad_perm [2,3,0,1]
+#define DPP_XOR1 0xb1          // quad_perm [1,0,3,2]
+// 16 values per lane (index q = 4i + r) summed over the 16 lanes of a DPP row; lane l returns
+// the total of value q = l & 15.  Each step sends the half of the values the partner keeps.
+__device__ __forceinline__ float row_transpose_sum(float (&v)[16], int c16) {
+  const bool b3 = c16 & 8, b2 = c16 & 4, b1 = c16 & 2, b0 = c16 & 1;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    const float keep = b3 ? v[a + 8] : v[a], send = b3 ? v[a] : v[a + 8];
+    v[a] = keep + dpp_f<DPP_MIRROR>(send);
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const float keep = b2 ? v[a + 4] : v[a], send = b2 ? v[a] : v[a + 4];
+    v[a] = keep + dpp_f<DPP_HALF_MIRROR>(send);
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const float keep = b1 ? v[a + 2] : v[a], send = b1 ? v[a] : v[a + 2];
+    v[a] = keep + dpp_f<DPP_XOR2>(send);
+  }
+  const float keep = b0 ? v[1] : v[0], send = b0 ? v[0] : v[1];
+  return keep + dpp_f<DPP_XOR1>(send);
+}
+
 }  // namespace
 
 // Operands are swapped relative to a plain logits GEMM: A = W^T fragments (16 vocab
@@ -71,6 +103,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     const float* __restrict__ lse,    // [N]      pass 2
     const float* __restrict__ alpha,  // [N]      pass 2
     bf16* __restrict__ dl,            // [N][V]   pass 2: dlogits
+    float* __restrict__ dbias,        // [V]      pass 2 (nullable): += column sums of dlogits
     int N, int V, int ldx) {
   constexpr int KS = H / 32;          // k-steps of 32
   constexpr int XS = H + 8;           // padded LDS row (bank spread)
@@ -90,6 +123,18 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
   bf16x8 wa[KS][4];   // A fragments: W^T rows (vocab columns) of this wave's 4 column tiles
   float bcol[4][4];   // log2(e) x bias of the lane's columns cw + 16i + q4 + r (-inf past V in pass 1)
   int cur_vt = -1;
+  // pass 2: the output-projection bias gradient db = sum_rows dlogits.  Per unit the lane's
+  // 16 column partials (its 2 rows) are folded across the 16 lanes that share those columns by
+  // a halving butterfly (8 + 4 + 2 + 1 DPP exchanges), which leaves lane l with the full
+  // column sum for column index c16 = l & 15 -- ONE accumulator register per lane, carried
+  // over the workgroup's units of a vocab tile and flushed with one atomic per column when
+  // the tile changes (a 16-register accumulator spilled at 256 VGPRs).
+  float cacc = 0.f;
+  auto flush_bias = [&](int vt_old) {
+    const int col = vt_old * VR_COLS + 64 * wid + 16 * (c16 >> 2) + q4 + (c16 & 3);
+    if (col < V) atomicAdd(dbias + col, cacc);
+    cacc = 0.f;
+  };
   bf16x8 xr[CH];      // prefetched X chunks of the next unit
   int tg_r = 0;
   float ls_r = 0.f, al_r = 0.f;
@@ -140,6 +185,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     const int vt = u / RB, rb = (u % RB) * VR_ROWS;
     const int cw = vt * VR_COLS + 64 * wid;  // this wave's first column
     if (vt != cur_vt) {  // new vocab tile: its A fragments and bias into registers
+      if (GRAD && dbias && cur_vt >= 0) flush_bias(cur_vt);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const bf16* arow = WT + (size_t)min(cw + 16 * i + c16, V - 1) * H + kof;
@@ -203,6 +249,9 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
       }
     } else {
       const bool vec = (V % 4 == 0);
+      float cs[16];  // this unit's column partials, index 4i + r
+#pragma unroll
+      for (int q = 0; q < 16; ++q) cs[q] = 0.f;
 #pragma unroll
       for (int j = 0; j < RJ; ++j) {
         const int rr = 16 * j + c16, row = rb + rr;
@@ -217,8 +266,10 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
             const int o = wo - 16 * i;
             float d[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r) {
               d[r] = __builtin_amdgcn_exp2f(fmaf(acc[i][j][r], LOG2E_F, bcol[i][r] + c)) - (o == r ? al : 0.f);
+              cs[4 * i + r] += d[r];
+            }
             bf16* dst = dl + (size_t)row * V + col;
             if (vec && col + 4 <= V) {
               typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -231,11 +282,13 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
           }
         }
       }
+      if (dbias) cacc += row_transpose_sum(cs, c16);
     }
     if (u + 1 < u1) stash(buf ^ 1);
     __syncthreads();
     if constexpr (!GRAD) merge_store(buf, u);
   }
+  if (GRAD && dbias) flush_bias(cur_vt);
 }
 
 // lse and p_vocab(gold) per row; one thread per row, partials read coalesced across rows.
@@ -301,23 +354,24 @@ void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float*
   const int grid = vocab_train_grid(N, V);
   if (H == 256)
     hipLaunchKernelGGL((vocab_train_kernel<256, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, part, zg,
-                       nullptr, nullptr, nullptr, N, V, ldx);
+                       nullptr, nullptr, nullptr, nullptr, N, V, ldx);
   else
     hipLaunchKernelGGL((vocab_train_kernel<128, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, part, zg,
-                       nullptr, nullptr, nullptr, N, V, ldx);
+                       nullptr, nullptr, nullptr, nullptr, N, V, ldx);
   hipLaunchKernelGGL(vocab_rowstats_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part, zg, target, lse, pv, N, V,
                      vocab_train_tiles(V));
 }
 
 void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
-                            const float* lse, const float* alpha, bf16* dl, int N, int V, int H, hipStream_t st) {
+                            const float* lse, const float* alpha, bf16* dl, float* dbias, int N, int V, int H,
+                            hipStream_t st) {
   const int grid = vocab_train_grid(N, V);
   if (H == 256)
     hipLaunchKernelGGL((vocab_train_kernel<256, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, nullptr,
-                       nullptr, lse, alpha, dl, N, V, ldx);
+                       nullptr, lse, alpha, dl, dbias, N, V, ldx);
   else
     hipLaunchKernelGGL((vocab_train_kernel<128, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, nullptr,
-                       nullptr, lse, alpha, dl, N, V, ldx);
+                       nullptr, lse, alpha, dl, dbias, N, V, ldx);
 }
 
 void launch_ptr_rowfin(const float* pv, const int* target, const float* rowg, const float* pgen, const float* attn,

@@ -188,6 +188,7 @@ class HipPointerGenerator:
             w["vpart"] = z(int(self.k.vocab_train_tiles(V)) * N * 2)
             for n in ("zg", "lse", "pv", "alpha"):
                 w[n] = z(N)
+            w["dbias"] = z(V)  # output_projection/v gradient, column sums taken inside pass 2
         w["logits"] = z(D * B, V, dt=BF)
         # backward
         w["dlogits"] = w["logits"]
@@ -202,7 +203,9 @@ class HipPointerGenerator:
         w["dcov"] = z(2, B, T)
         w["dh_rec"] = z(B, H)
         w["dc_carry"] = z(B, H)
-        w["dF"] = z(B, T, A)
+        w["dF"] = z(B, T, A, dt=BF)  # written whole (zeros past len) by attn_bwd_feat, in bf16
+        w["ATTb"] = z(D, B, T, dt=BF)
+        w["DCTXb"] = z(D, B, A, dt=BF)
         self._dE = z(B, T, A)
         w["dv"] = z(A)
         w["dwc"] = z(A)
@@ -386,8 +389,9 @@ class HipPointerGenerator:
                          w["dpre"] if (need_grad and hps.pointer_gen) else None,
                          w["dA"] if (need_grad and hps.pointer_gen) else None, N, B, T)
             if need_grad:
+                w["dbias"].zero_()
                 k.vocab_train_bwd(w["outb_ext"], self.pk["owT"], p[OV], w["target_t"], w["lse"], w["alpha"],
-                                  w["dlogits"], N, V, H, ldx)
+                                  w["dlogits"], w["dbias"], N, V, H, ldx)
             return
         torch.addmm(self.pk["ovb"], w["outb"], self.pk["ow"], out=w["logits"])
         self.k.ptr_loss(w["logits"], None, w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None,
@@ -433,18 +437,34 @@ class HipPointerGenerator:
         g = p.g
         p.grad.zero_()
         dl = w["dlogits"]
-        # [W | b] gradient in one GEMM: output_projection/w and /v are adjacent in the flat
-        # buffer, and row H of outb_ext is all ones
         H, V = self.H, self.V
-        assert p.offsets[OV][0] == p.offsets[OW][0] + H * V
-        o = p.offsets[OW][0]
-        dst = p.grad[o:o + (H + 1) * V].view(H + 1, V)
+        if self.fused_vocab:
+            # the bias gradient came out of the fused kernel; the weight GEMM keeps M = H (an
+            # M = H + 1 problem runs twice the output tiles on hipBLASLt's 256-row tiles)
+            m, dst = H, g(OW)
+            g(OV).copy_(w["dbias"])
+        else:
+            # [W | b] gradient in one GEMM: output_projection/w and /v are adjacent in the flat
+            # buffer, and row H of outb_ext is all ones
+            assert p.offsets[OV][0] == p.offsets[OW][0] + H * V
+            o = p.offsets[OW][0]
+            m, dst = H + 1, p.grad[o:o + (H + 1) * V].view(H + 1, V)
+        N = self.D * self.B
+
+        def dw():
+            if m == H and N % 4 == 0:
+                # split K = N in 4 (one batched GEMM + a sum): 0.82 -> 0.74 ms at B = 256
+                xe = w["outb_ext"].view(4, N // 4, H + 8)[:, :, :H]
+                parts = torch.bmm(xe.transpose(1, 2), dl.view(4, N // 4, V), out_dtype=F32)
+                torch.sum(parts, 0, out=dst)
+            else:
+                torch.mm(w["outb_ext"][:, :m].t(), dl, out_dtype=F32, out=dst)
         if self._side is not None:  # off the critical path: only the all-reduce bucket needs it
             self._side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self._side):
-                torch.mm(w["outb_ext"][:, :H + 1].t(), dl, out_dtype=F32, out=dst)
+                dw()
         else:
-            torch.mm(w["outb_ext"][:, :H + 1].t(), dl, out_dtype=F32, out=dst)
+            dw()
         self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
 
     def backward_mid(self):
@@ -530,7 +550,6 @@ class HipPointerGenerator:
         wgrad_into(gs[H:], Hn, DSb)
         g(ATT_B).copy_(DS.sum(0))
         # ---- attention feature gradients (tanh recomputed once over all steps)
-        w["dF"].zero_()
         w["dv"].zero_()
         w["dwc"].zero_()
         k.attn_bwd_feat(F, w["S"], v, wc, w["COV"][:D] if cov else None, w["DE"], lens, w["dF"], w["dv"],
@@ -538,12 +557,16 @@ class HipPointerGenerator:
         g(VATT).copy_(w["dv"])
         if cov:
             g(WCOV).view(A).copy_(w["dwc"])
-        dFb = w["dF"].view(B * T, A).to(BF)
+        dFb = w["dF"].view(B * T, A)
         top = self.enc[-1]
         wgrad_into(g(WH).view(A, A), top["out"].view(B * T, A), dFb)
         dE = self._dE
-        mm_into(dE.view(B * T, A), dFb, self.pk["Wh"].t())
-        dE.baddbmm_(w["ATT"].permute(1, 2, 0), w["DCTX"].permute(1, 0, 2))  # += a^T . dctx  [B,T,A]
+        # dE = a^T . dctx (bf16 batched GEMM, fp32 out) + dF . W_h^T (accumulated in place)
+        w["ATTb"].copy_(w["ATT"])
+        w["DCTXb"].copy_(w["DCTX"])
+        torch.bmm(w["ATTb"].permute(1, 2, 0), w["DCTXb"].permute(1, 0, 2), out_dtype=F32, out=dE)
+        dE2 = dE.view(B * T, A)
+        torch.addmm(dE2, dFb, self.pk["Wh"].t(), out_dtype=F32, out=dE2)
         self._dE, self._d_emb_dec = dE, d_emb_dec
         if self._side is not None:  # join the output-projection weight gradient
             torch.cuda.current_stream().wait_stream(self._side)
@@ -602,8 +625,9 @@ class HipPointerGenerator:
                 else:
                     dx.scatter_add_(1, w["rev_idx"][..., None].expand(B, T, din), dxs)
             d_in = dx
-        gemb.index_add_(0, w["enc_batch"].view(-1), d_in.view(B * T, self.E))
-        gemb.index_add_(0, w["dec_batch_t"].view(-1), d_emb_dec)
+        # encoder + decoder token rows in one atomic scatter-add launch (embedding.hip)
+        k.emb_grad(gemb, w["enc_batch"].view(-1), d_in.reshape(B * T, self.E), w["dec_batch_t"].view(-1),
+                   d_emb_dec.contiguous())
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_step(self):
