@@ -36,15 +36,16 @@ const auto BF = at::kBFloat16;
 const auto I32 = at::kInt;
 
 // ---------------------------------------------------------------- encoder LSTM
-void lstm_enc_fwd_step(const Tensor& gx, const Tensor& Wt, const Tensor& hs, const Tensor& cs, const Tensor& acts,
-                       const Tensor& out, const Tensor& lens, int64_t s, int64_t T, int64_t B, int64_t H) {
-  chk(gx, F32, "gx"); chk(Wt, BF, "Wt"); chk(hs, BF, "hs"); chk(cs, F32, "cs"); chk(acts, F32, "acts");
+void lstm_enc_fwd_step(const Tensor& gx, const Tensor& bias, const Tensor& Wt, const Tensor& hs, const Tensor& cs,
+                       const Tensor& acts, const Tensor& out, const Tensor& lens, int64_t s, int64_t T, int64_t B,
+                       int64_t H) {
+  chk(gx, F32, "gx"); chk(bias, F32, "bias"); numel_eq(bias, 2 * 4 * H, "bias"); chk(Wt, BF, "Wt"); chk(hs, BF, "hs"); chk(cs, F32, "cs"); chk(acts, F32, "acts");
   chk(out, BF, "out"); chk(lens, I32, "lens");
   TORCH_CHECK(H % 32 == 0 && s >= 0 && s < T, "bad lstm args");
   numel_eq(gx, 2 * T * B * 4 * H, "gx"); numel_eq(Wt, 2 * 4 * H * H, "Wt");
   numel_eq(hs, 2 * (T + 1) * B * H, "hs"); numel_eq(cs, 2 * (T + 1) * B * H, "cs");
   numel_eq(acts, 2 * T * B * 4 * H, "acts"); numel_eq(out, B * T * 2 * H, "out"); numel_eq(lens, B, "lens");
-  launch_lstm_enc_fwd_step(P<float>(gx), P<bf16>(Wt), P<bf16>(hs), P<float>(cs), P<float>(acts), P<bf16>(out),
+  launch_lstm_enc_fwd_step(P<float>(gx), P<float>(bias), P<bf16>(Wt), P<bf16>(hs), P<float>(cs), P<float>(acts), P<bf16>(out),
                            P<int>(lens), s, T, B, H, stream());
 }
 
@@ -67,10 +68,10 @@ int64_t lstm_persistent_xbuf_op(int64_t H, int64_t B, bool bwd) {
   return (int64_t)lstm_persistent_xbuf_elems((int)H, (int)B, bwd);
 }
 
-void lstm_fwd_persistent(const Tensor& gx, const Tensor& Wt, const Tensor& hs, const Tensor& cs, const Tensor& acts,
-                         const Tensor& out, const Tensor& lens, const Tensor& xbuf, const Tensor& err, int64_t T,
-                         int64_t B, int64_t H) {
-  chk(gx, F32, "gx"); chk(Wt, BF, "Wt"); chk(hs, BF, "hs"); chk(cs, F32, "cs"); chk(acts, F32, "acts");
+void lstm_fwd_persistent(const Tensor& gx, const Tensor& bias, const Tensor& Wt, const Tensor& hs, const Tensor& cs,
+                         const Tensor& acts, const Tensor& out, const Tensor& lens, const Tensor& xbuf,
+                         const Tensor& err, int64_t T, int64_t B, int64_t H) {
+  chk(gx, F32, "gx"); chk(bias, F32, "bias"); numel_eq(bias, 2 * 4 * H, "bias"); chk(Wt, BF, "Wt"); chk(hs, BF, "hs"); chk(cs, F32, "cs"); chk(acts, F32, "acts");
   chk(out, BF, "out"); chk(lens, I32, "lens"); chk(xbuf, at::kLong, "xbuf"); chk(err, I32, "err");
   TORCH_CHECK(lstm_persistent_grid((int)H, (int)B) > 0, "persistent LSTM: unsupported H/B (H in {64,128,256}, "
               "grid <= 256 workgroups)");
@@ -80,7 +81,7 @@ void lstm_fwd_persistent(const Tensor& gx, const Tensor& Wt, const Tensor& hs, c
   numel_eq(acts, 2 * T * B * 4 * H, "acts"); numel_eq(out, B * T * 2 * H, "out"); numel_eq(lens, B, "lens");
   TORCH_CHECK(xbuf.numel() >= (int64_t)lstm_persistent_xbuf_elems((int)H, (int)B, false), "xbuf too small");
   numel_eq(err, 1, "err");
-  launch_lstm_fwd_persistent(P<float>(gx), P<bf16>(Wt), P<bf16>(hs), P<float>(cs), P<float>(acts), P<bf16>(out),
+  launch_lstm_fwd_persistent(P<float>(gx), P<float>(bias), P<bf16>(Wt), P<bf16>(hs), P<float>(cs), P<float>(acts), P<bf16>(out),
                              P<int>(lens), (unsigned long long*)xbuf.data_ptr(), (unsigned*)err.data_ptr(), T, B, H,
                              stream());
 }
@@ -188,6 +189,41 @@ void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const 
 }
 
 int64_t attn_chunks(int64_t T) { return attn_nchunk(T); }
+
+// ---------------------------------------------------------------- frames (frames.hip)
+// out[2][T][B][W] from src rows: (ids? ids[b,tt] : b*T+tt), tt = t | rev[b,t]; columns d*doff..
+void to_step_frame(const Tensor& src, const OT& ids, const Tensor& rev, const Tensor& out, int64_t B, int64_t T,
+                   int64_t W, int64_t doff) {
+  TORCH_CHECK(src.is_cuda() && src.is_contiguous() && out.is_contiguous() && src.scalar_type() == out.scalar_type(),
+              "src/out: contiguous GPU tensors of one dtype");
+  TORCH_CHECK(src.scalar_type() == BF || src.scalar_type() == F32, "bf16 or fp32");
+  TORCH_CHECK(rev.scalar_type() == at::kLong && rev.is_contiguous() && rev.numel() == B * T, "rev [B,T] int64");
+  const int es = (int)src.element_size();
+  TORCH_CHECK((W * es) % 16 == 0 && (doff * es) % 16 == 0, "rows must be 16-byte multiples");
+  const int64_t S = src.size(-1);
+  TORCH_CHECK(doff + W <= S && (S * es) % 16 == 0, "bad row width");
+  if (ids.has_value()) {
+    TORCH_CHECK(ids->scalar_type() == at::kLong && ids->is_contiguous() && ids->numel() == B * T, "ids [B,T] int64");
+  } else {
+    TORCH_CHECK(src.numel() == B * T * S, "src must be [B,T,S] without ids");
+  }
+  numel_eq(out, 2 * T * B * W, "out");
+  launch_to_step_frame(src.data_ptr(), es, PO<int64_t>(ids), P<int64_t>(rev), out.data_ptr(), (int)B, (int)T, (int)W,
+                       (int)S, (int)doff, stream());
+}
+void from_step_frame(const Tensor& in, const Tensor& rev, const Tensor& out, int64_t B, int64_t T, int64_t W) {
+  chk(in, F32, "in"); chk(out, F32, "out");
+  TORCH_CHECK(rev.scalar_type() == at::kLong && rev.is_contiguous() && rev.numel() == B * T, "rev [B,T] int64");
+  TORCH_CHECK(W % 4 == 0, "W % 4");
+  numel_eq(in, 2 * T * B * W, "in"); numel_eq(out, B * T * W, "out");
+  launch_from_step_frame(P<float>(in), P<int64_t>(rev), P<float>(out), (int)B, (int)T, (int)W, stream());
+}
+void transpose_bta(const Tensor& in, const Tensor& out, int64_t B, int64_t T, int64_t A) {
+  chk(in, BF, "in"); chk(out, BF, "out");
+  TORCH_CHECK(A % 64 == 0, "A % 64");
+  numel_eq(in, B * T * A, "in"); numel_eq(out, B * T * A, "out");
+  launch_transpose_bta(P<bf16>(in), P<bf16>(out), (int)B, (int)T, (int)A, stream());
+}
 
 // ---------------------------------------------------------------- embedding gradient
 void emb_grad(const Tensor& gemb, const Tensor& ids0, const Tensor& src0, const Tensor& ids1, const Tensor& src1) {
@@ -497,6 +533,9 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("vocab_train_fwd", &vocab_train_fwd);
   m.def("vocab_train_bwd", &vocab_train_bwd);
   m.def("emb_grad", &emb_grad);
+  m.def("to_step_frame", &to_step_frame);
+  m.def("from_step_frame", &from_step_frame);
+  m.def("transpose_bta", &transpose_bta);
   m.def("ptr_rowfin", &ptr_rowfin);
   m.def("clip_adagrad", &clip_adagrad);
   m.def("opt_parts", &opt_parts);

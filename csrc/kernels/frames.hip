@@ -1,0 +1,105 @@
+// Layout kernels of the encoder: batch frame [B][T][*] <-> step frame [2][T][B][*] (the bw
+// direction reversed within each sequence length), and the W_h feature transpose.
+//
+// The reference runs tf.nn.bidirectional_dynamic_rnn (model.py:89-93), whose bw pass is
+// ReverseSequence -> LSTM -> ReverseSequence.  Here both directions run in one persistent
+// kernel over step-frame inputs, so the frames are rebuilt around it; each of these replaces
+// a chain of torch gather / transpose / copy / scatter_add launches (one 16-byte chunk per
+// thread, ~2x the bytes moved, no temporaries).
+#include "common.h"
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// out[d][t][b][0:W] = src[row(b, tt)][off_d + 0:W], tt = t (d = 0) or rev[b][t] (d = 1),
+// row(b, tt) = ids ? ids[b*T + tt] : b*T + tt; off_d = d * doff.  ES = element bytes.
+template <int ES>
+__global__ __launch_bounds__(256) void to_step_frame_kernel(const char* __restrict__ src, const int64_t* __restrict__ ids,
+                                                            const int64_t* __restrict__ rev, char* __restrict__ out,
+                                                            int B, int T, int W, int S, int doff) {
+  const int cpr = W * ES / 16;  // 16-byte chunks per row
+  const long n = 2L * T * B * cpr;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % cpr);
+    const long rowo = i / cpr;  // (d, t, b)
+    const int b = (int)(rowo % B);
+    const int t = (int)((rowo / B) % T);
+    const int d = (int)(rowo / ((long)B * T));
+    const int tt = d == 0 ? t : (int)rev[(size_t)b * T + t];
+    const long srow = ids ? ids[(size_t)b * T + tt] : (long)b * T + tt;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(src + ((size_t)srow * S + (size_t)d * doff) * ES + (size_t)c * 16);
+    *reinterpret_cast<u32x4*>(out + (size_t)rowo * W * ES + (size_t)c * 16) = v;
+  }
+}
+
+// fp32: out[b][t][0:W] = in[0][t][b][:] + in[1][rev[b][t]][b][:]   (rev is an involution)
+__global__ __launch_bounds__(256) void from_step_frame_kernel(const float* __restrict__ in, const int64_t* __restrict__ rev,
+                                                              float* __restrict__ out, int B, int T, int W) {
+  const int cpr = W / 4;
+  const long n = (long)B * T * cpr;
+  const size_t plane = (size_t)T * B * W;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % cpr);
+    const long bt = i / cpr;
+    const int t = (int)(bt % T), b = (int)(bt / T);
+    const int rt = (int)rev[(size_t)b * T + t];
+    const float4 x = *reinterpret_cast<const float4*>(in + ((size_t)t * B + b) * W + 4 * c);
+    const float4 y = *reinterpret_cast<const float4*>(in + plane + ((size_t)rt * B + b) * W + 4 * c);
+    *reinterpret_cast<float4*>(out + (size_t)bt * W + 4 * c) = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+  }
+}
+
+// bf16 [B][T][A] -> [B][A][T] through a 64 x 64 LDS tile (8-byte loads and stores)
+__global__ __launch_bounds__(256) void transpose_bta_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int T,
+                                                            int A) {
+  __shared__ bf16 tile[64][64 + 4];
+  const int b = blockIdx.z, t0 = blockIdx.y * 64, a0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, q = (tid & 15) * 4;
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  for (int r = tid >> 4; r < 64; r += 16) {
+    const int t = t0 + r;
+    bf16x4 v = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+    if (t < T) v = *reinterpret_cast<const bf16x4*>(in + ((size_t)b * T + t) * A + a0 + q);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tile[r][q + j] = v[j];
+  }
+  __syncthreads();
+  for (int r = tid >> 4; r < 64; r += 16) {  // r: feature within the tile, q: 4 positions
+    const int t = t0 + q;
+    bf16x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = tile[q + j][r];
+    bf16* dst = out + ((size_t)b * A + a0 + r) * T + t;
+    if (t + 4 <= T && (T & 3) == 0) {
+      *reinterpret_cast<bf16x4*>(dst) = v;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (t + j < T) dst[j] = v[j];
+    }
+  }
+}
+
+static int grid_for(long n) {
+  const long g = (n + 255) / 256;
+  return (int)(g < 8192 ? g : 8192);
+}
+
+void launch_to_step_frame(const void* src, int es, const int64_t* ids, const int64_t* rev, void* out, int B, int T,
+                          int W, int S, int doff, hipStream_t st) {
+  const long n = 2L * T * B * (W * es / 16);
+  if (es == 2)
+    hipLaunchKernelGGL(to_step_frame_kernel<2>, dim3(grid_for(n)), dim3(256), 0, st, (const char*)src, ids, rev,
+                       (char*)out, B, T, W, S, doff);
+  else
+    hipLaunchKernelGGL(to_step_frame_kernel<4>, dim3(grid_for(n)), dim3(256), 0, st, (const char*)src, ids, rev,
+                       (char*)out, B, T, W, S, doff);
+}
+
+void launch_from_step_frame(const float* in, const int64_t* rev, float* out, int B, int T, int W, hipStream_t st) {
+  const long n = (long)B * T * (W / 4);
+  hipLaunchKernelGGL(from_step_frame_kernel, dim3(grid_for(n)), dim3(256), 0, st, in, rev, out, B, T, W);
+}
+
+void launch_transpose_bta(const bf16* in, bf16* out, int B, int T, int A, hipStream_t st) {
+  hipLaunchKernelGGL(transpose_bta_kernel, dim3(A / 64, (T + 63) / 64, B), dim3(256), 0, st, in, out, T, A);
+}

@@ -3,7 +3,7 @@
 #include <hip/hip_runtime.h>
 typedef __bf16 bf16;
 
-void launch_lstm_enc_fwd_step(const float* gx, const bf16* Wt, bf16* hs, float* cs, float* acts, bf16* out,
+void launch_lstm_enc_fwd_step(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts, bf16* out,
                               const int* lens, int s, int T, int B, int H, hipStream_t st);
 void launch_lstm_enc_bwd_step(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                               const float* acts, const float* cs, const int* lens, int s, int T, int B, int H,
@@ -74,9 +74,9 @@ void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const floa
                      int N, int A, int H, int E, hipStream_t st);
 int lstm_persistent_grid(int H, int B);
 size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd);
-void launch_lstm_fwd_persistent(const float* gx, const bf16* Wt, bf16* hs, float* cs, float* acts, bf16* out,
-                                const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B, int H,
-                                hipStream_t st);
+void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
+                                bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
+                                int H, hipStream_t st);
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, int T, int B, int H, hipStream_t st);
@@ -97,3 +97,9 @@ void launch_ptr_rowfin(const float* pv, const int* target, const float* rowg, co
 // embedding.hip
 void launch_emb_grad(float* gemb, const int64_t* ids0, const float* src0, int n0, const int64_t* ids1,
                      const float* src1, int n1, int E, int V, hipStream_t st);
+
+// frames.hip
+void launch_to_step_frame(const void* src, int es, const int64_t* ids, const int64_t* rev, void* out, int B, int T,
+                          int W, int S, int doff, hipStream_t st);
+void launch_from_step_frame(const float* in, const int64_t* rev, float* out, int B, int T, int W, hipStream_t st);
+void launch_transpose_bta(const bf16* in, bf16* out, int B, int T, int A, hipStream_t st);

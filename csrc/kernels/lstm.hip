@@ -18,7 +18,8 @@
 #include "common.h"
 
 __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
-    const float* __restrict__ gx,     // [2][T][B][4H]  x.W_x + b (step frame)
+    const float* __restrict__ gx,     // [2][T][B][4H]  x.W_x (step frame, bias-free GEMM)
+    const float* __restrict__ bias,   // [2][4H]        gate biases b
     const bf16* __restrict__ Wt,      // [2][4H][H]     W_hh^T
     bf16* __restrict__ hs,            // [2][T+1][B][H] h entering step s (bf16)
     float* __restrict__ cs,           // [2][T+1][B][H] c entering step s
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
   const size_t ri = (size_t)(rok ? r : 0) * H + u;
   float gz[4], cp;  // unconditional: no lens -> address dependence on the critical path
 #pragma unroll
-  for (int g = 0; g < 4; ++g) gz[g] = gxs[g * H + u];
+  for (int g = 0; g < 4; ++g) gz[g] = gxs[g * H + u] + bias[(size_t)d * G + g * H + u];
   cp = cprev[ri];
   // ---- h_{s-1} . W_hh, K split over the 4 waves
   const int ar = min(r0 + (lane & 15), B - 1);
@@ -144,10 +145,11 @@ __global__ __launch_bounds__(256) void lstm_enc_bwd_step_kernel(
   }
 }
 
-void launch_lstm_enc_fwd_step(const float* gx, const bf16* Wt, bf16* hs, float* cs, float* acts, bf16* out,
+void launch_lstm_enc_fwd_step(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts, bf16* out,
                               const int* lens, int s, int T, int B, int H, hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16, 2);
-  hipLaunchKernelGGL(lstm_enc_fwd_step_kernel, grid, dim3(256), 0, st, gx, Wt, hs, cs, acts, out, lens, s, T, B, H);
+  hipLaunchKernelGGL(lstm_enc_fwd_step_kernel, grid, dim3(256), 0, st, gx, bias, Wt, hs, cs, acts, out, lens, s, T, B,
+                     H);
 }
 
 void launch_lstm_enc_bwd_step(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,

@@ -92,9 +92,9 @@ __device__ __forceinline__ bool team_of(int NC, int nteams, int& team, int& c) {
 
 template <int H>
 __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
-    const float* __restrict__ gx, const bf16* __restrict__ Wt, bf16* __restrict__ hs, float* __restrict__ cs,
-    float* __restrict__ acts, bf16* __restrict__ out, const int* __restrict__ lens, gu64* xbuf, gu32* err, int T,
-    int B, int ntile) {
+    const float* __restrict__ gx, const float* __restrict__ bias, const bf16* __restrict__ Wt,
+    bf16* __restrict__ hs, float* __restrict__ cs, float* __restrict__ acts, bf16* __restrict__ out,
+    const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile) {
   constexpr int KS = H / 32, NC = H / 64, HP = H / 2, G = 16 * HP, NPL = G / 256;
   __shared__ __attribute__((aligned(16))) bf16 Ash[2][16 * H];
   int team, c;
@@ -108,6 +108,10 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) Wf[g][kk] = ld8(Wt + ((size_t)d * G4 + g * H + u) * H + kk * 32 + 8 * (lane >> 4));
+  // gate biases of this lane's unit (gx = x.W_x comes from a bias-free GEMM)
+  float gb[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) gb[g] = bias[(size_t)d * G4 + g * H + u];
   int rc[4], ln[4];
   bool rok[4];
   float creg[4], hreg[4];
@@ -132,7 +136,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) gz[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u];
+      for (int g = 0; g < 4; ++g) gz[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u] + gb[g];
     // ---- h_s of the whole 16-row tile -> LDS
     if (s == 0) {
       for (int idx = threadIdx.x; idx < G; idx += 256) {
@@ -377,15 +381,15 @@ size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {
   return (size_t)2 * ntile * 2 * (bwd ? (size_t)NC * NC * 16 * 64 : (size_t)16 * (H / 2));
 }
 
-void launch_lstm_fwd_persistent(const float* gx, const bf16* Wt, bf16* hs, float* cs, float* acts, bf16* out,
-                                const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B, int H,
-                                hipStream_t st) {
+void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
+                                bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
+                                int H, hipStream_t st) {
   const int grid = lstm_persistent_grid(H, B), ntile = (B + 15) / 16;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
 #define LAUNCH_F(HH)                                                                                       \
-  hipLaunchKernelGGL(lstm_fwd_persistent_kernel<HH>, dim3(grid), dim3(256), 0, st, gx, Wt, hs, cs, acts, out, \
-                     lens, xb, e, T, B, ntile)
+  hipLaunchKernelGGL(lstm_fwd_persistent_kernel<HH>, dim3(grid), dim3(256), 0, st, gx, bias, Wt, hs, cs, acts, \
+                     out, lens, xb, e, T, B, ntile)
   if (H == 64) LAUNCH_F(64);
   else if (H == 128) LAUNCH_F(128);
   else LAUNCH_F(256);

@@ -28,6 +28,7 @@ def test_persistent_matches_step_kernels(H, B, T):
     k = ops()
     assert int(k.lstm_persistent_grid(H, B)) > 0
     g, r, lens, gx, Wt, Wn, hs0, cs0 = _setup(H, B, T, 7 + H + B)
+    bias = torch.randn(2, 4 * H, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5)) * 0.2
     res = {}
     for mode in ("step", "persistent"):
         hs, cs = hs0.clone(), cs0.clone()
@@ -36,10 +37,10 @@ def test_persistent_matches_step_kernels(H, B, T):
         err = torch.zeros(1, device="cuda", dtype=torch.int32)
         if mode == "step":
             for s in range(T):
-                k.lstm_enc_fwd_step(gx, Wt, hs, cs, acts, out, lens, s, T, B, H)
+                k.lstm_enc_fwd_step(gx, bias, Wt, hs, cs, acts, out, lens, s, T, B, H)
         else:
             xf = torch.zeros(int(k.lstm_persistent_xbuf(H, B, False)), device="cuda", dtype=torch.long)
-            k.lstm_fwd_persistent(gx, Wt, hs, cs, acts, out, lens, xf, err, T, B, H)
+            k.lstm_fwd_persistent(gx, bias, Wt, hs, cs, acts, out, lens, xf, err, T, B, H)
         torch.cuda.synchronize()
         assert int(err.item()) == 0
         # backward on the forward's own activations
@@ -76,13 +77,14 @@ def test_persistent_repeated_launches_reset_tags():
     g, r, lens, gx, Wt, Wn, hs0, cs0 = _setup(H, B, T, 3)
     xf = torch.zeros(int(k.lstm_persistent_xbuf(H, B, False)), device="cuda", dtype=torch.long)
     err = torch.zeros(1, device="cuda", dtype=torch.int32)
+    bias = torch.zeros(2, 4 * H, device="cuda")
     outs = []
     for _ in range(3):
         hs, cs = hs0.clone(), cs0.clone()
         acts = torch.zeros(2, T, B, 4 * H, device="cuda")
         out = torch.zeros(B, T, 2 * H, device="cuda", dtype=torch.bfloat16)
         xf.zero_()
-        k.lstm_fwd_persistent(gx, Wt, hs, cs, acts, out, lens, xf, err, T, B, H)
+        k.lstm_fwd_persistent(gx, bias, Wt, hs, cs, acts, out, lens, xf, err, T, B, H)
         outs.append(out.clone())
     torch.cuda.synchronize()
     assert int(err.item()) == 0

@@ -141,6 +141,8 @@ class HipPointerGenerator:
                 "dout": z(B, T, A),
                 "dh_fin": z(2, B, H),
                 "dc_carry": z(2, B, H),
+                "dxs": z(2, T * B, din),
+                "dx": z(B, T, din),
             })
         # persistent weight-resident recurrence (lstm_persistent.hip) when the shape allows
         # it; TSAMD_LSTM_PERSISTENT=0 forces the per-step kernels
@@ -238,6 +240,8 @@ class HipPointerGenerator:
             put(f"enc{layer}_Wn", Kh)
             put(f"enc{layer}_Wt", Kh.transpose(1, 2))
         put("Wh", p[WH].reshape(A, A))
+        put("RC", p[RC])
+        put("RH", p[RH])
         M = p[LIN_M]
         put("lin_emb", M[:E])
         put("Wic", M[E:])
@@ -256,10 +260,19 @@ class HipPointerGenerator:
         if getattr(self, "fused_vocab", False):
             put("owT", p[OW].t())  # [V][H] B operand of the fused vocab head
         self.pk = pk
-        self.f32 = {
-            "v": p[VATT].reshape(A).contiguous(),
-            "wc": p[WCOV].reshape(A).contiguous() if self.hps.coverage else None,
-        }
+        f32 = getattr(self, "f32", None) or {}
+        f32["v"] = p[VATT].reshape(A).contiguous()
+        f32["wc"] = p[WCOV].reshape(A).contiguous() if self.hps.coverage else None
+        # encoder gate biases [fw; bw] (added inside the LSTM kernels; the x.W_x GEMM is
+        # bias-free): persistent buffers refreshed in place, captured graphs keep their address
+        for layer in range(self.L):
+            bb = torch.stack([p[enc_b(layer, d)] for d in ("fw", "bw")])
+            key = f"enc{layer}_b"
+            if key in f32:
+                f32[key].copy_(bb)
+            else:
+                f32[key] = bb
+        self.f32 = f32
 
     # ------------------------------------------------------------------ inputs
     def set_batch(self, batch) -> None:
@@ -303,41 +316,45 @@ class HipPointerGenerator:
     def _encoder_forward(self):
         k, w, B, T, H, A = self.k, self.w, self.B, self.T, self.H, self.A
         lens, rev = w["enc_lens"], w["rev_idx"]
-        x = self.pk["emb"][w["enc_batch"]]  # [B,T,E] bf16
+        x = None
         for layer, st in enumerate(self.enc):
             din = st["din"]
             xs = st["x_sf"]
-            xs[0].copy_(x.transpose(0, 1))
-            xs[1].copy_(x.gather(1, rev[..., None].expand(B, T, din)).transpose(0, 1))
-            for di, d in enumerate(("fw", "bw")):
-                mm_into(st["gx"][di].view(T * B, 4 * H), xs[di].view(T * B, din), self.pk[f"enc{layer}_Kx{di}"],
-                        self.p[enc_b(layer, d)])
+            # step-frame inputs [2][T][B][din] (bw reversed within each length) in one gather
+            # launch: layer 0 straight from the embedding table by token id (frames.hip)
+            if x is None:
+                k.to_step_frame(self.pk["emb"], w["enc_batch"], rev, xs, B, T, din, 0)
+            else:
+                k.to_step_frame(x, None, rev, xs, B, T, din, 0)
+            for di in range(2):  # x.W_x, bias added in the recurrence kernel
+                mm_into(st["gx"][di].view(T * B, 4 * H), xs[di].view(T * B, din), self.pk[f"enc{layer}_Kx{di}"])
             st["hs"][:, 0].zero_()
             st["cs"][:, 0].zero_()
             st["out"].zero_()
             if self.persistent_lstm:
                 w["lstm_xf"].zero_()  # hand-off tags must start at 0 every launch
-                k.lstm_fwd_persistent(st["gx"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"], st["out"],
+                k.lstm_fwd_persistent(st["gx"], self.f32[f"enc{layer}_b"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"], st["out"],
                                       lens, w["lstm_xf"], w["lstm_err"], T, B, H)
             else:
                 for s in range(T):
-                    k.lstm_enc_fwd_step(st["gx"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"],
+                    k.lstm_enc_fwd_step(st["gx"], self.f32[f"enc{layer}_b"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"],
                                         st["out"], lens, s, T, B, H)
             x = st["out"]
         top = self.enc[-1]
         old_c = torch.cat([top["cs"][0, T], top["cs"][1, T]], 1)
         old_h = torch.cat([top["hs"][0, T], top["hs"][1, T]], 1).float()
-        pc = old_c @ self.p[RC] + self.p[BRC]
-        ph = old_h @ self.p[RH] + self.p[BRH]
+        # bf16 operands: the fp32 [256 x 512] x [512 x 256] GEMM ran as ONE 256x256 tile (~120 us)
+        pc = mmf(old_c.to(BF), self.pk["RC"]) + self.p[BRC]
+        ph = mmf(old_h.to(BF), self.pk["RH"]) + self.p[BRH]
         self._red = (old_c, old_h, pc, ph)
         c0, h0 = torch.relu(pc), torch.relu(ph)
         w["Cst"][0].copy_(c0)
         w["Cb"][0].copy_(c0)
         w["Hb"][0].copy_(h0)
         mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["Wh"])
-        w["Ft"].copy_(w["F"].transpose(1, 2))
+        k.transpose_bta(w["F"], w["Ft"], B, T, A)
         if w["Et"] is not None:
-            w["Et"].copy_(top["out"].transpose(1, 2))
+            k.transpose_bta(top["out"], w["Et"], B, T, A)
 
     def _decoder_forward(self):
         k, w, hps = self.k, self.w, self.hps
@@ -595,9 +612,7 @@ class HipPointerGenerator:
             st = self.enc[layer]
             din = st["din"]
             # dL/dh_out in step frame: fw as is, bw reversed within each length
-            dsf = st["dout"].view(2, T, B, H)
-            dsf[0].copy_(d_in[:, :, :H].transpose(0, 1))
-            dsf[1].copy_(d_in[:, :, H:].gather(1, w["rev_idx"][..., None].expand(B, T, H)).transpose(0, 1))
+            k.to_step_frame(d_in, None, w["rev_idx"], st["dout"], B, T, H, H)
             if layer == self.L - 1:
                 st["dh_fin"][0].copy_(d_old_h[:, :H]); st["dh_fin"][1].copy_(d_old_h[:, H:])
                 st["dc_carry"][0].copy_(d_old_c[:, :H]); st["dc_carry"][1].copy_(d_old_c[:, H:])
@@ -612,18 +627,16 @@ class HipPointerGenerator:
                 for s in reversed(range(T)):
                     k.lstm_enc_bwd_step(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"],
                                         st["dc_carry"], st["acts"], st["cs"], lens, s, T, B, H)
-            dx = torch.zeros(B, T, din, dtype=F32, device=self.dev)
+            dxs = st["dxs"]  # [2][T*B][din]: both directions' input gradients, step frame
             for di, d in enumerate(("fw", "bw")):
                 dzd = st["dz"][di].view(T * B, 4 * H)
                 gkd = g(enc_k(layer, d))
                 wgrad_into(gkd[:din], st["x_sf"][di].view(T * B, din), dzd)
                 wgrad_into(gkd[din:], st["hs"][di, :T].reshape(T * B, H), dzd)
                 g(enc_b(layer, d)).copy_(dzd.sum(0, dtype=F32))
-                dxs = mmf(dzd, self.pk[f"enc{layer}_Kx{di}"].t()).view(T, B, din).transpose(0, 1)
-                if di == 0:
-                    dx.add_(dxs)
-                else:
-                    dx.scatter_add_(1, w["rev_idx"][..., None].expand(B, T, din), dxs)
+                torch.mm(dzd, self.pk[f"enc{layer}_Kx{di}"].t(), out_dtype=F32, out=dxs[di])
+            dx = st["dx"]
+            k.from_step_frame(dxs, w["rev_idx"], dx, B, T, din)  # fw + reversed bw, batch frame
             d_in = dx
         # encoder + decoder token rows in one atomic scatter-add launch (embedding.hip)
         k.emb_grad(gemb, w["enc_batch"].view(-1), d_in.reshape(B * T, self.E), w["dec_batch_t"].view(-1),
