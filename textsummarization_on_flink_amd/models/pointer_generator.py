@@ -638,9 +638,11 @@ class HipPointerGenerator:
             dx = st["dx"]
             k.from_step_frame(dxs, w["rev_idx"], dx, B, T, din)  # fw + reversed bw, batch frame
             d_in = dx
-        # encoder + decoder token rows in one atomic scatter-add launch (embedding.hip)
-        k.emb_grad(gemb, w["enc_batch"].view(-1), d_in.reshape(B * T, self.E), w["dec_batch_t"].view(-1),
-                   d_emb_dec.contiguous())
+        # encoder + decoder token rows in id order (one radix sort + one launch, embedding.hip):
+        # atomics only where the id changes, so Zipf-hot tokens do not serialise
+        ids = torch.cat([w["enc_batch"].view(-1), w["dec_batch_t"].view(-1)]).to(torch.int32)
+        sid, perm = torch.sort(ids)
+        k.emb_grad_sorted(gemb, sid, perm, d_in.reshape(B * T, self.E), d_emb_dec.contiguous())
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_step(self):
