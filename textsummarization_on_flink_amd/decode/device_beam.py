@@ -223,7 +223,60 @@ class DeviceBeamDecoder:
         self.steps_run = t
 
     def results(self, n_valid: int = None) -> List[Hypothesis]:
-        """Backtrack the best hypothesis per article (host)."""
+        """Best hypothesis per article (host).  The winner is picked from the device scores
+        first and only the winners are backtracked, vectorised over articles (one numpy
+        gather per step instead of a Python walk per candidate)."""
+        names = ["res_count", "res_score", "res_step", "res_par", "lp_sum", "tok_hist", "par_hist", "step"]
+        if self.keep_attn:
+            names += ["ATT_hist", "PG_hist"]
+        b = {k: self.b[k].cpu().numpy() for k in names}
+        beam, start, stop = self.beam, self.vocab.word2id(START_DECODING), self.vocab.word2id(STOP_DECODING)
+        nsteps = int(min(b["step"][0], self.maxD))
+        na = n_valid if n_valid is not None else self.Na
+        ar = np.arange(na)
+        base = ar * beam
+        nres = b["res_count"][:na].astype(np.int64)
+        fin = nres > 0
+        # winners: the finished hypotheses by final score, else the live beams by average
+        # log-prob including [START]; argmax keeps the first of equal maxima, as the stable
+        # sort of sort_hyps does
+        rs = b["res_score"][:na * beam].reshape(na, beam).astype(np.float64)
+        rs = np.where(np.arange(beam)[None, :] < nres[:, None], rs, -np.inf)
+        q_fin = rs.argmax(1) if na else np.zeros(0, np.int64)
+        live = b["lp_sum"][:na * beam].reshape(na, beam).astype(np.float64) / (nsteps + 1)
+        q_live = live.argmax(1) if na else np.zeros(0, np.int64)
+        score = np.where(fin, rs[ar, q_fin], live[ar, q_live])
+        t_fin = b["res_step"][base + q_fin].astype(np.int64)
+        tl0 = np.where(fin, t_fin - 1, nsteps - 1)
+        slot = np.where(fin, b["res_par"][base + q_fin], q_live).astype(np.int64)
+        L = int(tl0.max()) + 1 if na else 0
+        toks = np.zeros((na, max(L, 1)), dtype=np.int64)
+        arow = np.zeros((na, max(L, 1)), dtype=np.int64)  # attention / p_gen history rows (base + parent)
+        for tl in range(L - 1, -1, -1):
+            act = tl <= tl0
+            rows = base + slot
+            par = b["par_hist"][tl, rows].astype(np.int64)
+            toks[act, tl] = b["tok_hist"][tl, rows][act]
+            arow[act, tl] = (base + par)[act]
+            slot = np.where(act, par, slot)
+        out = []
+        for a in range(na):
+            n = int(tl0[a]) + 1
+            tokens = [start] + toks[a, :n].tolist() + ([stop] if fin[a] else [])
+            atts, pgs = [], []
+            if self.keep_attn:
+                atts = [b["ATT_hist"][tl, arow[a, tl]] for tl in range(n)]
+                pgs = [float(b["PG_hist"][tl, arow[a, tl]]) if self.hps.pointer_gen else None for tl in range(n)]
+                if fin[a]:
+                    t, par = int(t_fin[a]), int(b["res_par"][base[a] + q_fin[a]])
+                    atts.append(b["ATT_hist"][t, base[a] + par])
+                    pgs.append(float(b["PG_hist"][t, base[a] + par]) if self.hps.pointer_gen else None)
+            sc = float(score[a])
+            out.append(Hypothesis(tokens, [sc * len(tokens)] + [0.0] * (len(tokens) - 1), None, atts, pgs, None))
+        return out
+
+    def _results_walk(self, n_valid: int = None) -> List[Hypothesis]:
+        """Per-candidate Python walk (the original form of ``results``; kept as the test oracle)."""
         b = {k: v.cpu().numpy() for k, v in self.b.items() if k in (
             "res_count", "res_score", "res_len", "res_step", "res_par", "lp_sum", "tok_hist", "par_hist", "step",
             "ATT_hist", "PG_hist", "done")}
