@@ -659,6 +659,198 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step_kernel(
   }
 }
 
+// Same math with 4 positions per group (NG4 groups per wave): the E/F rows in flight per
+// lane halve (32 instead of 64 VGPRs), which buys a third wave per SIMD at the 168-VGPR cap.
+__device__ __forceinline__ float bfly4(const float (&x)[4], int b5, int b4) {
+  float h2[2], h1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float send = b5 ? x[i] : x[i + 2];
+    const float keep = b5 ? x[i + 2] : x[i];
+    h2[i] = keep + __shfl_xor(send, 32, 64);
+  }
+  {
+    const float send = b4 ? h2[0] : h2[1];
+    const float keep = b4 ? h2[1] : h2[0];
+    h1 = keep + __shfl_xor(send, 16, 64);
+  }
+  h1 += __shfl_xor(h1, 8, 64);
+  h1 += __shfl_xor(h1, 4, 64);
+  h1 += __shfl_xor(h1, 2, 64);
+  h1 += __shfl_xor(h1, 1, 64);
+  return h1;  // total of element q = 2*b5 + b4, in all 16 lanes of that group
+}
+
+template <int NG4, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
+    const bf16* __restrict__ E, const bf16* __restrict__ F, const float* __restrict__ s,
+    const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
+    const float* __restrict__ a, const float* __restrict__ dctx, const float* __restrict__ ctx,
+    const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
+    const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
+    float* __restrict__ dcov_out, int T, int A) {
+  constexpr int PW = 4 * NG4;  // positions per wave
+  constexpr int PB = 4 * PW;   // positions per block
+  static_assert(PW == 32 || PW == 16 || PW == 64, "lane -> position map needs a power of two <= 64");
+  __shared__ float red[8];
+  __shared__ float part[4][512];
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int len = lens[b];
+  const size_t rb = (size_t)b * T;
+  const int p0 = blockIdx.x * PB + wid * PW;
+  if (blockIdx.x * PB >= len) {  // whole block masked: only pass dcov through
+    for (int i = tid; i < PB; i += 256) {
+      const int p = blockIdx.x * PB + i;
+      if (p < T) {
+        if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
+        de_out[rb + p] = 0.f;
+      }
+    }
+    return;
+  }
+  const float g = gcl ? gcl[b] : 0.f;
+  const bf16* Eb = E + (size_t)b * T * A;
+  const bf16* Fb = F + (size_t)b * T * A;
+  const int k0c = min(lane * 8, A - 8);
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 fr[4], er[4];
+#define LOAD4(dst, base, pg)                                                             \
+  {                                                                                      \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                      \
+      const int pq = min((pg) + q, len - 1);                                             \
+      dst[q] = __builtin_bit_cast(u32x4, ld8(base + (size_t)pq * A + k0c));              \
+    }                                                                                    \
+  }
+  if (p0 < len) {
+    LOAD4(er, Eb, p0);
+    LOAD4(fr, Fb, p0);
+  }
+  float dk[8];
+  f32x2 s2[4], w2[4], v4w[4], acc[4];
+  {
+    const int k0 = lane * 8;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      float sv[2], wv[2], vv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = k0 + 2 * jp + h;
+        const bool ok = k < A;
+        sv[h] = ok ? s[(size_t)b * A + k] : 0.f;
+        vv[h] = ok ? v[k] : 0.f;
+        wv[h] = (ok && wc) ? wc[k] : 0.f;
+        dk[2 * jp + h] = ok ? dctx[(size_t)b * A + k] : 0.f;
+      }
+      s2[jp] = f32x2{sv[0], sv[1]} * K2LOG2E;
+      w2[jp] = f32x2{wv[0], wv[1]} * K2LOG2E;
+      v4w[jp] = f32x2{4.f * vv[0] * wv[0], 4.f * vv[1] * wv[1]};
+      acc[jp] = f32x2{0.f, 0.f};
+    }
+  }
+  float a_l = 0.f, r_l = 0.f, c_l = 0.f, dn_l = 0.f;
+  {
+    const int p = p0 + (lane & (PW - 1));
+    if (p < len) {
+      const size_t ix = rb + p;
+      a_l = a[ix];
+      c_l = cov ? cov[ix] : 0.f;
+      r_l = (Ga ? Ga[ix] : 0.f) + (dcov_next ? dcov_next[ix] : 0.f);
+      if (gcl && a_l <= c_l) r_l += g;
+    }
+    if (p < T && dcov_next) dn_l = dcov_next[rb + p];
+  }
+  float S = 0.f;
+  for (int i = tid; i < len; i += 256) {
+    const size_t ix = rb + i;
+    const float ai = a[ix];
+    float r = (Ga ? Ga[ix] : 0.f) + (dcov_next ? dcov_next[ix] : 0.f);
+    if (gcl && ai <= (cov ? cov[ix] : 0.f)) r += g;
+    S += ai * r;
+  }
+  for (int k = tid; k < A; k += 256) S += dctx[(size_t)b * A + k] * ctx[(size_t)b * A + k];
+  S = block_sum<256>(S, red);
+  const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
+  const int qm = 2 * b5 + b4;
+#pragma unroll
+  for (int grp = 0; grp < NG4; ++grp) {
+    const int pg = p0 + grp * 4;
+    if (pg >= len) {
+      for (int i = lane; i < 4 * (NG4 - grp); i += 64) {
+        const int p = pg + i;
+        if (p < T) {
+          de_out[rb + p] = 0.f;
+          if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
+        }
+      }
+      break;
+    }
+    const bool more = grp + 1 < NG4 && pg + 4 < len;
+    float pd[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x2 d2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) d2 = fma2(bf2pair(er[q][jp]), f32x2{dk[2 * jp], dk[2 * jp + 1]}, d2);
+      pd[q] = d2.x + d2.y;
+    }
+    if (more) LOAD4(er, Eb, pg + 4);
+    const float dot = bfly4(pd, b5, b4);
+    const int src = grp * 4 + qm;
+    const float a_q = __shfl(a_l, src, 64), r_q = __shfl(r_l, src, 64);
+    const float c_q = __shfl(c_l, src, 64), dn_q = __shfl(dn_l, src, 64);
+    const float de_q = (pg + qm < len) ? a_q * (r_q + dot - S) : 0.f;
+    float dcv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float de = rdlane(de_q, ((q >> 1) << 5) | ((q & 1) << 4));
+      const float c = rdlane(c_l, grp * 4 + q);
+      f32x2 dc2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        const f32x2 y = fma2(bf2pair(fr[q][jp]), splat2(K2LOG2E), fma2(w2[jp], splat2(c), s2[jp]));
+        const f32x2 r = rsig2(y);
+        const f32x2 qv = fma2(-r, r, r);
+        acc[jp] = fma2(qv, splat2(de), acc[jp]);
+        dc2 = fma2(qv, v4w[jp], dc2);
+      }
+      dcv[q] = dc2.x + dc2.y;
+    }
+    if (more) LOAD4(fr, Fb, pg + 4);
+    const float hc = bfly4(dcv, b5, b4);
+    if ((lane & 15) == 0) {
+      const int p = pg + qm;
+      if (p < T) {
+        const size_t ix = rb + p;
+        de_out[ix] = de_q;
+        if (dcov_out) {
+          float r = dn_q;
+          if (p < len) {
+            r += de_q * hc;
+            if (gcl && a_q > c_q) r += g;
+          }
+          dcov_out[ix] = r;
+        }
+      }
+    }
+  }
+#undef LOAD4
+  {
+    const int k0 = lane * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = k0 + j < A;
+      part[wid][lane * 8 + j] = ok ? 4.f * v[ok ? k0 + j : 0] * acc[j >> 1][j & 1] : 0.f;
+    }
+  }
+  __syncthreads();
+  float* out = ds + (size_t)b * A;
+  for (int k = tid; k < A; k += 256) {
+    const float x = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+    atomicAdd(out + k, x);
+  }
+}
+
 // ------------------------------------------------------ post-loop: dF, dv, dw_c
 // dF[b,i,k] = sum_t de[t,b,i] v_k sech2(u_tik); dv_k = sum de tanh(u); dwc_k = sum de v_k sech2 cov.
 // Lanes on features (8 per lane), each wave keeps 4 positions x 8 features of dF in
@@ -834,6 +1026,19 @@ void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const fl
   dim3 grid((T + 32 * ng - 1) / (32 * ng), B);
 #define LB(NK, NG, OC) hipLaunchKernelGGL((attn_bwd_step_kernel<NK, NG, OC>), grid, dim3(256), 0, st, E, F, s, v, wc, \
                                           cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A)
+  // Default: the 4-positions-per-group kernel capped at 126 VGPRs (4 waves per SIMD): 54 us vs
+  // 61 us for the 8-position kernel at B = 256, T = 400 (tools/attn_micro.py).  TSAMD_ATTN_P4=0
+  // selects the 8-position kernel; 1 / 3 the 4-position one uncapped / at 3 waves per SIMD.
+  static const int p4 = [] { const char* e = getenv("TSAMD_ATTN_P4"); return e ? atoi(e) : 2; }();
+  if (A <= 512 && p4 > 0) {
+#define L4(OC) hipLaunchKernelGGL((attn_bwd_step4_kernel<8, OC>), dim3((T + 127) / 128, B), dim3(256), 0, st, E, F, s, v, \
+                                  wc, cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A)
+    if (p4 == 3) L4(3);
+    else if (p4 == 2) L4(2);
+    else L4(1);
+#undef L4
+    return;
+  }
   if (A <= 512) {
     if (ng == 2) LB(1, 2, 1);
     else if (occ == 3) LB(1, 4, 3);
