@@ -855,7 +855,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
 // dF[b,i,k] = sum_t de[t,b,i] v_k sech2(u_tik); dv_k = sum de tanh(u); dwc_k = sum de v_k sech2 cov.
 // Lanes on features (8 per lane), each wave keeps 4 positions x 8 features of dF in
 // registers across all D steps; de / cov are wave-uniform scalar loads.
-__global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
+template <int NPW, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
     const bf16* __restrict__ F, const float* __restrict__ S_all, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov_all, const float* __restrict__ de_all,
     const int* __restrict__ lens, bf16* __restrict__ dF, float* __restrict__ dv, float* __restrict__ dwc,
@@ -868,7 +869,7 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
   const int kbase = blockIdx.z * 512;
   const int k0 = kbase + lane * 8;
   const bool kok = k0 < A;
-  const int p0 = blockIdx.x * 16 + wid * 4;
+  const int p0 = blockIdx.x * (4 * NPW) + wid * NPW;  // NPW positions per wave
   // r-form (see rsig2): with r = 1/(1 + 2^y),
   //   dF  = 4 v sum_t de r(1-r),  dv = sum_t de - 2 sum_t de r,  dwc = 4 v sum_t de cov r(1-r)
   f32x2 w2[4], accv[4], accw[4];
@@ -889,10 +890,10 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
   }
   float adv[8], adw[8];
   if (p0 < len && kok) {
-    const int np = min(4, len - p0);
-    f32x2 fs[4][4], acc[4][4];
+    const int np = min(NPW, len - p0);
+    f32x2 fs[NPW][4], acc[NPW][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NPW; ++q) {
       const int p = min(p0 + q, T - 1);
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       const u32x4 fw = __builtin_bit_cast(u32x4, ld8(F + ((size_t)b * T + p) * A + k0));
@@ -910,7 +911,7 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
                            f32x2{s1.x, s1.y} * K2LOG2E, f32x2{s1.z, s1.w} * K2LOG2E};
       const size_t rb = ((size_t)t * B + b) * T + p0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NPW; ++q) {
         if (q < np) {
           const float de = de_all[rb + q];
           const float c = cov_all ? cov_all[rb + q] : 0.f;
@@ -929,7 +930,7 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
       }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NPW; ++q) {
       if (p0 + q < T) {  // bf16 straight into the GEMM operand; zeros past len
         bf16x8 o8;
 #pragma unroll
@@ -939,7 +940,7 @@ __global__ __launch_bounds__(256) void attn_bwd_feat_kernel(
     }
   } else if (kok) {  // fully masked positions of this wave: dF = 0 (no separate memset)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < NPW; ++q)
       if (p0 + q < T) *reinterpret_cast<bf16x8*>(dF + ((size_t)b * T + p0 + q) * A + k0) = zero8();
   }
 #pragma unroll
@@ -1052,7 +1053,21 @@ void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const fl
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, bf16* dF, float* dv, float* dwc, int D, int B, int T,
                           int A, hipStream_t st) {
-  dim3 grid((T + 15) / 16, B, (A + 511) / 512);
-  hipLaunchKernelGGL(attn_bwd_feat_kernel, grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF, dv,
-                     dwc, D, B, T, A);
+  // Default (2): 4 positions per wave capped at 128 VGPRs = 4 waves/SIMD (a few prologue
+  // spills): 1.51 ms vs 1.64 ms uncapped at 3 waves/SIMD (B = 256, T = 400, D = 100).
+  // TSAMD_FEAT_V=0: uncapped; 1: 2 positions per wave (1.65 ms).
+  static const int fv = [] { const char* e = getenv("TSAMD_FEAT_V"); return e ? atoi(e) : 2; }();
+  if (fv == 1) {
+    dim3 grid((T + 7) / 8, B, (A + 511) / 512);
+    hipLaunchKernelGGL((attn_bwd_feat_kernel<2, 1>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
+                       dv, dwc, D, B, T, A);
+  } else if (fv == 2) {
+    dim3 grid((T + 15) / 16, B, (A + 511) / 512);
+    hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 4>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
+                       dv, dwc, D, B, T, A);
+  } else {
+    dim3 grid((T + 15) / 16, B, (A + 511) / 512);
+    hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 1>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
+                       dv, dwc, D, B, T, A);
+  }
 }
