@@ -200,9 +200,8 @@ __global__ __launch_bounds__(256) void attn_softmax_ctx_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float x = acc[q][j];
-      x += __shfl_xor(x, 8, 64);
-      x += __shfl_xor(x, 16, 64);
-      x += __shfl_xor(x, 32, 64);
+      x += dpp_f<DPP_ROR8>(x);
+      x = sum_x32(sum_x16(x));
       acc[q][j] = x;
     }
   if (ps == 0) {
@@ -370,22 +369,20 @@ __global__ __launch_bounds__(256) void attn_bwd_tanh_kernel(
     for (int i = 0; i < 4; ++i) {
       const float send = b5 ? dcv[i] : dcv[i + 4];
       const float keep = b5 ? dcv[i + 4] : dcv[i];
-      h4[i] = keep + __shfl_xor(send, 32, 64);
+      h4[i] = keep + xor32_f(send);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const float send = b4 ? h4[i] : h4[i + 2];
       const float keep = b4 ? h4[i + 2] : h4[i];
-      h2[i] = keep + __shfl_xor(send, 16, 64);
+      h2[i] = keep + xor16_f(send);
     }
     {
       const float send = b3 ? h2[0] : h2[1];
       const float keep = b3 ? h2[1] : h2[0];
-      h1 = keep + __shfl_xor(send, 8, 64);
+      h1 = keep + dpp_f<DPP_ROR8>(send);
     }
-    h1 += __shfl_xor(h1, 4, 64);
-    h1 += __shfl_xor(h1, 2, 64);
-    h1 += __shfl_xor(h1, 1, 64);
+    h1 = dpp_sum8(h1);
     // position q's total sits in lanes 8q' .. 8q'+7 with q = 4*b5 + 2*b4 + b3; fetch the
     // per-position scalars of q from lane (grp*8 + q) and let lane 8*(...) write.
     const int q = 4 * b5 + 2 * b4 + b3;
@@ -443,22 +440,20 @@ __device__ __forceinline__ float bfly8(const float (&x)[8], int b5, int b4, int 
   for (int i = 0; i < 4; ++i) {
     const float send = b5 ? x[i] : x[i + 4];
     const float keep = b5 ? x[i + 4] : x[i];
-    h4[i] = keep + __shfl_xor(send, 32, 64);
+    h4[i] = keep + xor32_f(send);
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const float send = b4 ? h4[i] : h4[i + 2];
     const float keep = b4 ? h4[i + 2] : h4[i];
-    h2[i] = keep + __shfl_xor(send, 16, 64);
+    h2[i] = keep + xor16_f(send);
   }
   {
     const float send = b3 ? h2[0] : h2[1];
     const float keep = b3 ? h2[1] : h2[0];
-    h1 = keep + __shfl_xor(send, 8, 64);
+    h1 = keep + dpp_f<DPP_ROR8>(send);
   }
-  h1 += __shfl_xor(h1, 4, 64);
-  h1 += __shfl_xor(h1, 2, 64);
-  h1 += __shfl_xor(h1, 1, 64);
+  h1 = dpp_sum8(h1);
   return h1;  // total of element q = 4*b5 + 2*b4 + b3, in all 8 lanes of that group
 }
 
@@ -667,17 +662,14 @@ __device__ __forceinline__ float bfly4(const float (&x)[4], int b5, int b4) {
   for (int i = 0; i < 2; ++i) {
     const float send = b5 ? x[i] : x[i + 2];
     const float keep = b5 ? x[i + 2] : x[i];
-    h2[i] = keep + __shfl_xor(send, 32, 64);
+    h2[i] = keep + xor32_f(send);
   }
   {
     const float send = b4 ? h2[0] : h2[1];
     const float keep = b4 ? h2[1] : h2[0];
-    h1 = keep + __shfl_xor(send, 16, 64);
+    h1 = keep + xor16_f(send);
   }
-  h1 += __shfl_xor(h1, 8, 64);
-  h1 += __shfl_xor(h1, 4, 64);
-  h1 += __shfl_xor(h1, 2, 64);
-  h1 += __shfl_xor(h1, 1, 64);
+  h1 = dpp_sum16(h1);
   return h1;  // total of element q = 2*b5 + b4, in all 16 lanes of that group
 }
 

@@ -150,4 +150,62 @@ __device__ __forceinline__ void ksplit_reduce(const f32x4 (&acc)[NB], float* red
   }
 }
 
+// Cross-lane moves inside a 16-lane DPP row: a VALU operand modifier, no LDS round trip
+// (a __shfl_xor is a ds_bpermute: ~100+ cycles of latency per dependent step).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+#define DPP_MIRROR 0x140       // l <-> 15 - l  (flips bits 0-3 of the row lane)
+#define DPP_HALF_MIRROR 0x141  // l <-> 7 - l within each half (flips bits 0-2)
+#define DPP_XOR2 0x4e          // quad_perm [2,3,0,1]
+#define DPP_XOR1 0xb1          // quad_perm [1,0,3,2]
+// all-reduce over the 8 lanes l, l^1, .., l^7 / the 16 lanes of the DPP row (partners xor 1,
+// xor 2, then the mirrors: lanes of a quad already agree, so 7 - l acts as l ^ 4)
+__device__ __forceinline__ float dpp_sum8(float x) {
+  x += dpp_f<DPP_XOR1>(x);
+  x += dpp_f<DPP_XOR2>(x);
+  return x + dpp_f<DPP_HALF_MIRROR>(x);
+}
+__device__ __forceinline__ float dpp_sum16(float x) {
+  x = dpp_sum8(x);
+  return x + dpp_f<DPP_MIRROR>(x);
+}
+__device__ __forceinline__ float dpp_max16(float x) {
+  x = fmaxf(x, dpp_f<DPP_XOR1>(x));
+  x = fmaxf(x, dpp_f<DPP_XOR2>(x));
+  x = fmaxf(x, dpp_f<DPP_HALF_MIRROR>(x));
+  return fmaxf(x, dpp_f<DPP_MIRROR>(x));
+}
+
+#define DPP_ROR8 0x128         // row_ror:8 -- within a 16-lane row this is l ^ 8
+// Value of lane l ^ 32 / l ^ 16 through the gfx950 v_permlane{32,16}_swap (VALU, no LDS).
+// With both operands = v the swap returns {lower half, upper half} (rows {0,2} / {1,3}).
+__device__ __forceinline__ float xor32_f(float v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? p[0] : p[1]);
+}
+__device__ __forceinline__ float xor16_f(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 16) ? p[0] : p[1]);
+}
+// v + v(l ^ 32), v + v(l ^ 16), max likewise (the two halves are summed in the same order on
+// both sides, so every lane gets the bit-identical result)
+__device__ __forceinline__ float sum_x32(float v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float sum_x16(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float max_x32(float v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+}
+__device__ __forceinline__ float max_x16(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+}
+
 #define HIP_LAUNCH_CHECK() (void)0

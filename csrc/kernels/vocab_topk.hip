@@ -35,10 +35,14 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 
 }  // namespace
 
-// 36 KB of LDS and <= 128 VGPRs (AGPRs included): 4 workgroups per CU, so the R/64 x V/256
-// tiles of a decode step (784 at R = 256, V = 50k) run in one round instead of 3-per-CU
-// rounds with a 2% tail.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void vocab_logits_kernel(
+// 36 KB of LDS.  OCC = 2 (206 VGPRs): all 32 W^T fragments of a wave in flight at once, two
+// rounds of workgroups at R = 256, V = 50k (784 tiles).  OCC = 4 (128 VGPRs) fits every tile in
+// one round but the compiler then issues the fragments 4 at a time (8 dependent round trips).
+// Both measure 47.5 us with the select kernel (tools/vocab_micro.py); PMC: the epilogue's
+// ~1500 VALU instructions per wave (bias, row max / sum exp, staging) are the larger cost.
+// TSAMD_VL_OCC=4 selects the other variant.
+template <int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void vocab_logits_kernel(
     const bf16* __restrict__ X,     // [R][H]  output-projection activations (bf16)
     const bf16* __restrict__ WT,    // [V][H]  output_projection/w transposed ("Bt")
     const float* __restrict__ bias, // [V]
@@ -59,34 +63,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   if (vt >= nt) return;
   const int rb = (slot % RB) * VT_ROWS;
   const int cw = vt * VT_COLS + 64 * wid;  // this wave's first column
-  // X rows of this block -> LDS once (shared by the 4 waves); every B fragment of the wave
-  // (4 column tiles x H/32 k-steps) is issued before the first MFMA: one memory round trip.
+  // X rows of this block -> LDS once (shared by the 4 waves)
   const int kof = 8 * (lane >> 4);
-  for (int c = threadIdx.x; c < VT_ROWS * (H / 8); c += 256) {
-    const int rr = c / (H / 8), k8 = (c % (H / 8)) * 8;
-    *reinterpret_cast<bf16x8*>(&Xs[rr * (H + 8) + k8]) = ld8(X + (size_t)min(rb + rr, R - 1) * H + k8);
+  constexpr int XPT = VT_ROWS * VT_HMAX / 8 / 256;  // 16-byte X chunks per thread (H <= 256)
+  bf16x8 xr[XPT];
+#pragma unroll
+  for (int u = 0; u < XPT; ++u) {
+    const int c = threadIdx.x + 256 * u, rr = c / (H / 8), k8 = (c % (H / 8)) * 8;
+    if (c < VT_ROWS * (H / 8)) xr[u] = ld8(X + (size_t)min(rb + rr, R - 1) * H + k8);
+  }
+  // every B fragment of the wave (4 column tiles x H/32 k-steps, H <= 256: 128 VGPRs) is
+  // issued right behind the X loads, before their LDS stores: one memory round trip for both
+  const bf16* brow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) brow[j] = WT + (size_t)min(cw + 16 * j + (lane & 15), V - 1) * H + kof;
+  bf16x8 b[8][4];
+#pragma unroll
+  for (int h = 0; h < 8; ++h)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[h][j] = ld8(brow[j] + min(32 * h, H - 32));
+#pragma unroll
+  for (int u = 0; u < XPT; ++u) {
+    const int c = threadIdx.x + 256 * u, rr = c / (H / 8), k8 = (c % (H / 8)) * 8;
+    if (c < VT_ROWS * (H / 8)) *reinterpret_cast<bf16x8*>(&Xs[rr * (H + 8) + k8]) = xr[u];
   }
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-  const bf16* brow[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) brow[j] = WT + (size_t)min(cw + 16 * j + (lane & 15), V - 1) * H + kof;
   __syncthreads();
-  for (int k0 = 0; k0 < H; k0 += 256) {  // H <= 256 in one pass (128 VGPRs of B fragments)
-    bf16x8 b[8][4];
 #pragma unroll
-    for (int h = 0; h < 8; ++h)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[h][j] = ld8(brow[j] + min(k0 + 32 * h, H - 32));
-#pragma unroll
-    for (int h = 0; h < 8; ++h) {
-      if (k0 + 32 * h >= H) break;
+  for (int h = 0; h < 8; ++h) {
+    if (32 * h < H) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Xs[(16 * i + (lane & 15)) * (H + 8) + k0 + 32 * h + kof]);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Xs[(16 * i + (lane & 15)) * (H + 8) + 32 * h + kof]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a, b[h][j], acc[i][j]);
       }
@@ -115,15 +127,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         m = fmaxf(m, x[j]);
         St[wid][4 * (lane >> 4) + r][16 * j + (lane & 15)] = x[j];
       }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      m = dpp_max16(m);
       float sm = 0.f;
       if (m > -INFINITY) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) sm += fexp(x[j] - m);  // exp(-inf) = 0 for padded columns
       }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) sm += __shfl_xor(sm, o, 64);
+      sm = dpp_sum16(sm);
       if ((lane & 15) == 0) {
         Pm[wid][16 * i + 4 * (lane >> 4) + r] = m;
         Ps[wid][16 * i + 4 * (lane >> 4) + r] = sm;
@@ -407,8 +417,13 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
                        int R, int V, int H, int T, int K, int beam, hipStream_t st) {
   const int nt = vocab_topk_tiles(V);
   const int RB = (R + VT_ROWS - 1) / VT_ROWS;
-  hipLaunchKernelGGL(vocab_logits_kernel, dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
-                     part_ms, R, V, H);
+  static const int occ = getenv("TSAMD_VL_OCC") ? atoi(getenv("TSAMD_VL_OCC")) : 2;
+  if (occ == 4)
+    hipLaunchKernelGGL(vocab_logits_kernel<4>, dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
+                       part_ms, R, V, H);
+  else
+    hipLaunchKernelGGL(vocab_logits_kernel<2>, dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
+                       part_ms, R, V, H);
   hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
                      out_lp, V, T, K, beam, nt);
 }

@@ -36,27 +36,10 @@ __device__ __forceinline__ void ms_merge(float& m, float& s, float m2, float s2)
   m = M;
 }
 
-// max / sum over the 16 lanes of one accumulator column group (lanes l, l^1, .., l^8)
-__device__ __forceinline__ float max16(float x) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
-  return x;
-}
-__device__ __forceinline__ float sum16(float x) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) x += __shfl_xor(x, o, 64);
-  return x;
-}
+// max / sum over the 16 lanes of one accumulator column group (one DPP row)
+__device__ __forceinline__ float max16(float x) { return dpp_max16(x); }
+__device__ __forceinline__ float sum16(float x) { return dpp_sum16(x); }
 
-// x <- x + x(partner) where partner is given by a DPP lane pattern inside a 16-lane row
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float x) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, false));
-}
-#define DPP_MIRROR 0x140       // l <-> 15 - l  (flips bit 3 of the row lane)
-#define DPP_HALF_MIRROR 0x141  // l <-> 7 - l within each half (flips bit 2)
-#define DPP_XOR2 0x4e          // quad_perm [2,3,0,1]
-#define DPP_XOR1 0xb1          // quad_perm [1,0,3,2]
 // 16 values per lane (index q = 4i + r) summed over the 16 lanes of a DPP row; lane l returns
 // the total of value q = l & 15.  Each step sends the half of the values the partner keeps.
 __device__ __forceinline__ float row_transpose_sum(float (&v)[16], int c16) {
@@ -231,8 +214,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
           if ((unsigned)o < 4u && row < N)
             zg[row] = (o == 0 ? y[i][0] : o == 1 ? y[i][1] : o == 2 ? y[i][2] : y[i][3]) * LN2_F;
         }
-        m = fmaxf(m, __shfl_xor(m, 16, 64));
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        m = max_x32(max_x16(m));
         float sm = 0.f;
         if (m > -INFINITY) {
 #pragma unroll
@@ -240,8 +222,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
 #pragma unroll
             for (int r = 0; r < 4; ++r) sm += __builtin_amdgcn_exp2f(y[i][r] - m);
         }
-        sm += __shfl_xor(sm, 16, 64);
-        sm += __shfl_xor(sm, 32, 64);
+        sm = sum_x32(sum_x16(sm));
         if (lane < 16) {
           Pm[buf][wid][rr] = m * LN2_F;  // natural-log domain for the partial
           Ps[buf][wid][rr] = sm;
