@@ -52,12 +52,27 @@ template <int SW, int REP>
 __global__ __launch_bounds__(SW * 64) void attn_score_kernel(
     const bf16* __restrict__ Ft, const float* __restrict__ s, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov, const int* __restrict__ lens,
-    float* __restrict__ e, int T, int A) {
+    float* __restrict__ e, int T, int A, int xcd) {
   __shared__ float red[SW][REP][SCORE_POS];
-  const int b = blockIdx.y;  // Ft row (article)
+  // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs, so consecutive
+  // ids would put the position chunks of one Ft row on different XCDs.  A row is T*2 bytes
+  // (800 at T = 400, not a multiple of the 128-byte line): the lines two chunks share were
+  // then fetched from HBM once per XCD (FETCH_SIZE 1.45x the Ft bytes).  Giving each XCD a
+  // contiguous range of (row, chunk) keeps the shared lines in one L2.
+  int bx = blockIdx.x, by = blockIdx.y;
+  {
+    const int nx = gridDim.x, ntot = nx * gridDim.y;
+    if (xcd && (ntot & 7) == 0) {
+      const int id = blockIdx.y * nx + blockIdx.x;
+      const int L = (id & 7) * (ntot >> 3) + (id >> 3);
+      by = L / nx;
+      bx = L - by * nx;
+    }
+  }
+  const int b = by;  // Ft row (article)
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int len = lens[b];
-  const int pb = blockIdx.x * SCORE_POS;
+  const int pb = bx * SCORE_POS;
   if (pb >= len) return;  // uniform: masked positions are never read by the softmax
   const int p = pb + 2 * lane;
   const int pc = p < T ? p : 0;
@@ -968,7 +983,8 @@ void launch_attn_score(const bf16* Ft, const float* s, const float* v, const flo
                        const int* lens, float* e, int B, int T, int A, int rep, hipStream_t st) {
   dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B / rep);
   const bool w16 = attn_sw(A) == 16;
-#define LS(SW, RP) hipLaunchKernelGGL((attn_score_kernel<SW, RP>), grid, dim3(SW * 64), 0, st, Ft, s, v, wc, cov, lens, e, T, A)
+  static const int xcd = getenv("TSAMD_SCORE_XCD") ? atoi(getenv("TSAMD_SCORE_XCD")) : 1;
+#define LS(SW, RP) hipLaunchKernelGGL((attn_score_kernel<SW, RP>), grid, dim3(SW * 64), 0, st, Ft, s, v, wc, cov, lens, e, T, A, xcd)
   if (rep == 4) { if (w16) LS(16, 4); else LS(8, 4); }
   else if (rep == 2) { if (w16) LS(16, 2); else LS(8, 2); }
   else { if (w16) LS(16, 1); else LS(8, 1); }
