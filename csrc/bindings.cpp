@@ -237,6 +237,12 @@ void transpose_bta(const Tensor& in, const Tensor& out, int64_t B, int64_t T, in
   numel_eq(in, B * T * A, "in"); numel_eq(out, B * T * A, "out");
   launch_transpose_bta(P<bf16>(in), P<bf16>(out), (int)B, (int)T, (int)A, stream());
 }
+void cast_colsum(const Tensor& x, const Tensor& xb, const Tensor& colsum, int64_t N, int64_t C) {
+  chk(x, F32, "x"); chk(xb, BF, "xb"); chk(colsum, F32, "colsum");
+  TORCH_CHECK(C % 4 == 0 && C / 4 <= 256 && 256 % (C / 4) == 0, "cast_colsum: C % 4 == 0 and C / 4 divides 256");
+  numel_eq(x, N * C, "x"); numel_eq(xb, N * C, "xb"); numel_eq(colsum, C, "colsum");
+  launch_cast_colsum(P<float>(x), P<bf16>(xb), P<float>(colsum), (int)N, (int)C, stream());
+}
 
 // ---------------------------------------------------------------- embedding gradient
 void emb_grad(const Tensor& gemb, const Tensor& ids0, const Tensor& src0, const Tensor& ids1, const Tensor& src1) {
@@ -550,6 +556,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("to_step_frame", &to_step_frame);
   m.def("from_step_frame", &from_step_frame);
   m.def("transpose_bta", &transpose_bta);
+  m.def("cast_colsum", &cast_colsum);
   m.def("ptr_rowfin", &ptr_rowfin);
   m.def("clip_adagrad", &clip_adagrad);
   m.def("opt_parts", &opt_parts);

@@ -1,0 +1,66 @@
+"""Layout / reduction helper kernels of csrc/kernels/frames.hip against plain PyTorch:
+to_step_frame (embedding gather into the [2][T][B][W] step frame, bw direction reversed per
+length), from_step_frame (fw + reversed bw input gradients), transpose_bta (W_h feature
+transpose) and cast_colsum (bf16 copy + bias-gradient column sums)."""
+import pytest
+import torch
+
+from textsummarization_on_flink_amd.ops import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rev(lens, T):
+    t = torch.arange(T).view(1, T).expand(len(lens), T)
+    L = lens.view(-1, 1)
+    return torch.where(t < L, L - 1 - t, t).contiguous()
+
+
+@pytest.mark.parametrize("B,T,W", [(5, 7, 16), (16, 33, 128)])
+def test_to_and_from_step_frame(B, T, W):
+    k = ops()
+    g = torch.Generator().manual_seed(B + T)
+    lens = torch.randint(1, T + 1, (B,), generator=g)
+    lens[0] = T
+    rev = _rev(lens, T)
+    V = 50
+    emb = torch.randn(V, W, generator=g).to(torch.bfloat16)
+    ids = torch.randint(0, V, (B, T), generator=g)
+    out = torch.empty(2, T, B, W, dtype=torch.bfloat16, device="cuda")
+    k.to_step_frame(emb.cuda(), ids.cuda(), rev.cuda(), out, B, T, W, 0)
+    fw = emb[ids].permute(1, 0, 2)                                  # [T][B][W]
+    bw = emb[torch.gather(ids, 1, rev)].permute(1, 0, 2)
+    torch.testing.assert_close(out.cpu(), torch.stack([fw, bw]), rtol=0, atol=0)
+    # doff: the bw direction reads columns doff.. of a [B, T, 2W] source
+    src = torch.randn(B, T, 2 * W, generator=g)
+    out2 = torch.empty(2, T, B, W, device="cuda")
+    k.to_step_frame(src.cuda(), None, rev.cuda(), out2, B, T, W, W)
+    ref_bw = torch.gather(src[:, :, W:], 1, rev.unsqueeze(-1).expand(B, T, W)).permute(1, 0, 2)
+    torch.testing.assert_close(out2.cpu(), torch.stack([src[:, :, :W].permute(1, 0, 2), ref_bw]), rtol=0, atol=0)
+    # from_step_frame: out[b][t] = in[0][t][b] + in[1][rev[b][t]][b]
+    x = torch.randn(2, T, B, W, generator=g)
+    o = torch.empty(B, T, W, device="cuda")
+    k.from_step_frame(x.cuda(), rev.cuda(), o, B, T, W)
+    ref = x[0].permute(1, 0, 2) + torch.gather(x[1].permute(1, 0, 2), 1, rev.unsqueeze(-1).expand(B, T, W))
+    torch.testing.assert_close(o.cpu(), ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,T,A", [(2, 64, 64), (3, 101, 128)])
+def test_transpose_bta(B, T, A):
+    k = ops()
+    x = torch.randn(B, T, A, generator=torch.Generator().manual_seed(T)).to(torch.bfloat16).cuda()
+    y = torch.empty(B, A, T, dtype=torch.bfloat16, device="cuda")
+    k.transpose_bta(x, y, B, T, A)
+    torch.testing.assert_close(y, x.transpose(1, 2), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("N,C", [(1, 4), (37, 128), (25600, 256), (999, 512), (100, 1024)])
+def test_cast_colsum(N, C):
+    k = ops()
+    x = torch.randn(N, C, generator=torch.Generator().manual_seed(N + C)).cuda()
+    xb = torch.empty(N, C, dtype=torch.bfloat16, device="cuda")
+    cs = torch.full((C,), 0.5, device="cuda")  # accumulates onto what is there
+    k.cast_colsum(x, xb, cs, N, C)
+    torch.testing.assert_close(xb, x.to(torch.bfloat16), rtol=0, atol=0)
+    ref = x.double().sum(0) + 0.5
+    torch.testing.assert_close(cs.double(), ref, rtol=1e-5, atol=1e-4 * (N ** 0.5))

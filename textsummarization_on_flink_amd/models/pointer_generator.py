@@ -484,6 +484,18 @@ class HipPointerGenerator:
             dw()
         self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
 
+    def _cast_colsum(self, x, bias_grad):
+        """bf16 copy of x [N, C] plus bias_grad += its column sums in one read of x (the
+        cast_colsum kernel; bias_grad lies in the gradient buffer, zeroed by backward_head)."""
+        N, C = x.shape
+        xb = torch.empty(N, C, dtype=BF, device=x.device)
+        if C % 4 == 0 and C // 4 <= 256 and 256 % (C // 4) == 0:
+            self.k.cast_colsum(x, xb, bias_grad, N, C)
+        else:
+            xb.copy_(x)
+            bias_grad.copy_(x.sum(0))
+        return xb
+
     def backward_mid(self):
         """Output projection, p_gen, decoder reverse loop, decoder/attention weight grads."""
         k, w, hps, p = self.k, self.w, self.hps, self.p
@@ -495,10 +507,9 @@ class HipPointerGenerator:
         # ---- output projection [h, ctx]
         Hn = w["Hb"][1:].reshape(N, H)
         ctxb = w["CTXb"].view(N, A)
-        doutb = dout.to(BF)
+        doutb = self._cast_colsum(dout, g(OUT_B))
         wgrad_into(g(OUT_M)[:H], Hn, doutb)
         wgrad_into(g(OUT_M)[H:], ctxb, doutb)
-        g(OUT_B).copy_(dout.sum(0))
         dH_dir = mmf(doutb, self.pk["OUTm"][:H].t()).view(D, B, H)
         dCTX_dir = mmf(doutb, self.pk["OUTm"][H:].t()).view(D, B, A)
         dC_dir = None
@@ -552,20 +563,18 @@ class HipPointerGenerator:
         wgrad_into(gk[E:], w["Hb"][:D].reshape(N, H), DZ)
         g(CELL_B).copy_(DZ.sum(0, dtype=F32))
         DX = w["DX"].view(N, E)
-        DXb = DX.to(BF)
+        DXb = self._cast_colsum(DX, g(LIN_B))
         gl = g(LIN_M)
         wgrad_into(gl[:E], self._emb_dec, DXb)
         gl[E:].zero_()
         if D > 1:
             wgrad_into(gl[E:], w["CTXb"][:D - 1].reshape((D - 1) * B, A), DXb[B:])
-        g(LIN_B).copy_(DX.sum(0))
         d_emb_dec = mmf(DXb, self.pk["lin_emb"].t())  # [N,E]
         DS = w["DS"].view(N, A)
-        DSb = DS.to(BF)
+        DSb = self._cast_colsum(DS, g(ATT_B))
         gs = g(ATT_M)
         wgrad_into(gs[:H], w["Cb"][1:].reshape(N, H), DSb)
         wgrad_into(gs[H:], Hn, DSb)
-        g(ATT_B).copy_(DS.sum(0))
         # ---- attention feature gradients (tanh recomputed once over all steps)
         w["dv"].zero_()
         w["dwc"].zero_()
