@@ -182,10 +182,6 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
         const int t = d == 0 ? s : ln[i] - 1 - s;
         out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(h);
-      } else if (rok[i]) {
-        // padded position t = s >= len: zero output (TF dynamic_rnn), written here so the
-        // caller needs no 105 MB memset of out before the launch
-        out[((size_t)r * T + s) * 2 * H + d * H + u] = f2bf(0.f);
       }
       if (rok[i]) {
         cnext[(size_t)r * H + u] = creg[i];

@@ -330,12 +330,12 @@ class HipPointerGenerator:
                 mm_into(st["gx"][di].view(T * B, 4 * H), xs[di].view(T * B, din), self.pk[f"enc{layer}_Kx{di}"])
             st["hs"][:, 0].zero_()
             st["cs"][:, 0].zero_()
-            if self.persistent_lstm:  # (the persistent kernel writes the padded outputs' zeros)
+            st["out"].zero_()
+            if self.persistent_lstm:
                 w["lstm_xf"].zero_()  # hand-off tags must start at 0 every launch
                 k.lstm_fwd_persistent(st["gx"], self.f32[f"enc{layer}_b"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"], st["out"],
                                       lens, w["lstm_xf"], w["lstm_err"], T, B, H)
             else:
-                st["out"].zero_()
                 for s in range(T):
                     k.lstm_enc_fwd_step(st["gx"], self.f32[f"enc{layer}_b"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"],
                                         st["out"], lens, s, T, B, H)
