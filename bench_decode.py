@@ -45,8 +45,11 @@ def main():
     t0 = time.perf_counter()
     n = 0
     steps = 0
+    per = []
     for b in batches[args.warmup:]:
-        hyps = dec.decode(b)
+        tb = time.perf_counter()
+        hyps = dec.decode(b)  # synchronous: results() reads the device buffers
+        per.append(time.perf_counter() - tb)
         n += len(hyps)
         steps += dec.steps_run
     torch.cuda.synchronize()
@@ -55,6 +58,8 @@ def main():
                       "n_gpus": 1, "higher_is_better": True, "dtype": "bf16",
                       "data": "synthetic (CNN/DM-shaped, random-init weights)",
                       "ms_per_batch": round(1000 * el / args.batches, 2), "decode_steps_per_batch": steps / args.batches,
+                      "ms_per_batch_min": round(1000 * min(per), 2),
+                      "ms_per_batch_median": round(1000 * sorted(per)[len(per) // 2], 2),
                       "config": {"model": "pointer-generator+coverage hidden=256 emb=128 enc=400 dec<=100 vocab=50000",
                                  "beam": args.beam, "articles_per_batch": args.articles,
                                  "rows": args.articles * args.beam, "graph": not args.no_graph}}))

@@ -63,6 +63,8 @@ class DeviceBeamDecoder:
         R, T, H, A, E, V, K, Na, D = self.R, self.T, self.eng.H, self.eng.A, self.eng.E, self.V, self.K, self.Na, \
             self.maxD
         z = lambda *s, dt=F32: torch.zeros(*s, dtype=dt, device=self.dev)
+        self._done_dev = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._done_flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
         b = {}
         for name, shape, dt in [
             ("Ft", (R // self.rep, A, T), BF), ("E", (R // self.rep, T, A), BF),
@@ -206,7 +208,12 @@ class DeviceBeamDecoder:
             self._capture()
         self._encode(batch)
         self._prologue()
+        # early exit when every article is done, checked one chunk late: the all-done flag of
+        # chunk c is copied to pinned memory behind an event and read once chunk c+1 is queued,
+        # so the GPU never idles on the host round trip (steps after done are no-ops per article)
         t = 0
+        pend = []
+        chunk = 0
         while t < self.maxD:
             n = min(self.chunk, self.maxD - t)
             i = 0
@@ -218,9 +225,34 @@ class DeviceBeamDecoder:
                     self._step((t + i) % 2)
                     i += 1
             t += n
-            if int(self.b["done"].min().item()) == 1:
-                break
+            flag = self._done_flags[chunk % 2]  # reused by chunk + 2, queued after this one is read
+            chunk += 1
+            torch.amin(self.b["done"], 0, keepdim=True, out=self._done_dev)
+            flag.copy_(self._done_dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            pend.append((ev, flag))
+            if len(pend) == 2:
+                ev0, f0 = pend.pop(0)
+                ev0.synchronize()
+                if int(f0[0]) == 1:
+                    break
         self.steps_run = t
+
+    def _fetch(self, names):
+        """Device buffers -> numpy: every copy queued into pinned memory, one synchronisation."""
+        if not self.b[names[0]].is_cuda:
+            return {k: self.b[k].numpy() for k in names}
+        if not hasattr(self, "_pinned"):
+            self._pinned = {}
+        for k in names:
+            src = self.b[k]
+            h = self._pinned.get(k)
+            if h is None or h.shape != src.shape or h.dtype != src.dtype:
+                h = self._pinned[k] = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+            h.copy_(src, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return {k: self._pinned[k].numpy() for k in names}
 
     def results(self, n_valid: int = None) -> List[Hypothesis]:
         """Best hypothesis per article (host).  The winner is picked from the device scores
@@ -229,7 +261,7 @@ class DeviceBeamDecoder:
         names = ["res_count", "res_score", "res_step", "res_par", "lp_sum", "tok_hist", "par_hist", "step"]
         if self.keep_attn:
             names += ["ATT_hist", "PG_hist"]
-        b = {k: self.b[k].cpu().numpy() for k in names}
+        b = self._fetch(names)
         beam, start, stop = self.beam, self.vocab.word2id(START_DECODING), self.vocab.word2id(STOP_DECODING)
         nsteps = int(min(b["step"][0], self.maxD))
         na = n_valid if n_valid is not None else self.Na
@@ -265,11 +297,12 @@ class DeviceBeamDecoder:
             tokens = [start] + toks[a, :n].tolist() + ([stop] if fin[a] else [])
             atts, pgs = [], []
             if self.keep_attn:
-                atts = [b["ATT_hist"][tl, arow[a, tl]] for tl in range(n)]
+                # copies: b's arrays are views of pinned buffers that the next batch reuses
+                atts = [b["ATT_hist"][tl, arow[a, tl]].copy() for tl in range(n)]
                 pgs = [float(b["PG_hist"][tl, arow[a, tl]]) if self.hps.pointer_gen else None for tl in range(n)]
                 if fin[a]:
                     t, par = int(t_fin[a]), int(b["res_par"][base[a] + q_fin[a]])
-                    atts.append(b["ATT_hist"][t, base[a] + par])
+                    atts.append(b["ATT_hist"][t, base[a] + par].copy())
                     pgs.append(float(b["PG_hist"][t, base[a] + par]) if self.hps.pointer_gen else None)
             sc = float(score[a])
             out.append(Hypothesis(tokens, [sc * len(tokens)] + [0.0] * (len(tokens) - 1), None, atts, pgs, None))

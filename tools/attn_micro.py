@@ -79,6 +79,8 @@ def main():
         f()
         res[f"dout_split{S}"] = timeit(f, it=10)
         res[f"dout_split{S}_err"] = float((out - ref).abs().max() / ref.abs().max())
+    # transposed problem: dout^T = W . dlogits^T (M = H, N = rows)
+    res["dout_T"] = timeit(lambda: torch.mm(ow, dl.t(), out_dtype=F32), it=10)
     p, OV = eng.p, "seq2seq/output_projection/v"
     if eng.fused_vocab:
         ldx = H + 8
@@ -93,6 +95,10 @@ def main():
     dst = torch.empty(H + 1, V, device="cuda")
     res["dw_mm257"] = timeit(lambda: torch.mm(xe[:, :H + 1].t(), dl, out_dtype=F32, out=dst), it=10)
     res["dw_mm256"] = timeit(lambda: torch.mm(xe[:, :H].t(), dl, out_dtype=F32, out=dst[:H]), it=10)
+    # transposed problem: dW^T = dlogits^T . X (M = V, N = H), then without / with the transpose back
+    dstT = torch.empty(V, H, device="cuda")
+    res["dw_T"] = timeit(lambda: torch.mm(dl.t(), xe[:, :H], out_dtype=F32, out=dstT), it=10)
+    res["dw_T_transpose"] = timeit(lambda: dst[:H].copy_(dstT.t()), it=10)
     for S in (2, 4, 8):
         def g(S=S):
             p = torch.bmm(xe.view(S, N // S, H + 8)[:, :, :H].transpose(1, 2), dl.view(S, N // S, V),
