@@ -35,6 +35,79 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 
 }  // namespace
 
+// vocab_logits epilogue for one wave: + bias, per-row (max, sum exp) over the wave's 64
+// columns (DPP row reductions), and the fp32 logits stored through the LDS staging St as
+// 4 rows x 256 B per instruction.  Accumulator (i, j, r) holds row 16i + 4(lane>>4) + r,
+// column 16j + (lane&15).
+template <bool FULL>
+__device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[4][4], const float* __restrict__ bias,
+                                            float* __restrict__ logits, float (*St)[68], float* Pm, float* Ps,
+                                            int rb, int cw, int lane, int R, int V) {
+  constexpr float L2E = 1.4426950408889634f;
+  float bj[4];
+  bool cok[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = cw + 16 * j + (lane & 15);
+    cok[j] = FULL || col < V;
+    bj[j] = cok[j] ? bias[col] : 0.f;
+  }
+  const int c4 = 4 * (lane & 15);
+  // FULL: one base pointer, the per-store offsets (16i + 4q) * V are wave-uniform
+  float* const base = logits + (size_t)(rb + (lane >> 4)) * V + cw + c4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x[4], m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[j] = cok[j] ? acc[i][j][r] + bj[j] : -INFINITY;
+        m = fmaxf(m, x[j]);
+        St[4 * (lane >> 4) + r][16 * j + (lane & 15)] = x[j];
+      }
+      m = dpp_max16(m);
+      float sm = 0.f;
+      if (FULL || m > -INFINITY) {
+        const float mb = m * L2E;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm += __builtin_amdgcn_exp2f(fmaf(x[j], L2E, -mb));  // exp(-inf) = 0
+      }
+      sm = dpp_sum16(sm);
+      if ((lane & 15) == 0) {
+        Pm[16 * i + 4 * (lane >> 4) + r] = m;
+        Ps[16 * i + 4 * (lane >> 4) + r] = sm;
+      }
+      if (r == 3) {
+        // the 16-row tile i is staged: store it as 4 rows x 256 B per instruction
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int tr = 4 * q + (lane >> 4);
+          if (FULL) {
+            *reinterpret_cast<float4*>(base + (size_t)(16 * i + 4 * q) * V) =
+                *reinterpret_cast<const float4*>(&St[tr][c4]);
+          } else {
+            const int row2 = rb + 16 * i + tr, col = cw + c4;
+            if (row2 < R) {
+              float* dst = logits + (size_t)row2 * V + col;
+              if ((V & 3) == 0 && col + 4 <= V) {
+                *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(&St[tr][c4]);
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                  if (col + e < V) dst[e] = St[tr][c4 + e];
+              }
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      }
+    }
+}
+
 // 36 KB of LDS.  OCC = 2 (206 VGPRs): all 32 W^T fragments of a wave in flight at once, two
 // rounds of workgroups at R = 256, V = 50k (784 tiles).  OCC = 4 (128 VGPRs) fits every tile in
 // one round but the compiler then issues the fragments 4 at a time (8 dependent round trips).
@@ -106,62 +179,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   }
   __syncthreads();  // every wave is done reading Xs before it becomes the store staging
   // ---- epilogue: + bias, store fp32, per-row (max, sum exp) over this wave's 64 columns.
-  // Accumulator (i, j, r) holds row 16i + 4(lane>>4) + r, column 16j + (lane&15).
-  float bj[4];
-  bool cok[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = cw + 16 * j + (lane & 15);
-    cok[j] = col < V;
-    bj[j] = cok[j] ? bias[col] : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = rb + 16 * i + 4 * (lane >> 4) + r;
-      float x[4], m = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        x[j] = cok[j] ? acc[i][j][r] + bj[j] : -INFINITY;
-        m = fmaxf(m, x[j]);
-        St[wid][4 * (lane >> 4) + r][16 * j + (lane & 15)] = x[j];
-      }
-      m = dpp_max16(m);
-      float sm = 0.f;
-      if (m > -INFINITY) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) sm += fexp(x[j] - m);  // exp(-inf) = 0 for padded columns
-      }
-      sm = dpp_sum16(sm);
-      if ((lane & 15) == 0) {
-        Pm[wid][16 * i + 4 * (lane >> 4) + r] = m;
-        Ps[wid][16 * i + 4 * (lane >> 4) + r] = sm;
-      }
-      if (r == 3) {
-        // the 16-row tile i is staged: store it as 4 rows x 256 B per instruction
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        const bool vec = (V % 4 == 0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int tr = 4 * q + (lane >> 4), row2 = rb + 16 * i + tr, c4 = 4 * (lane & 15);
-          const int col = cw + c4;
-          if (row2 < R) {
-            float* dst = logits + (size_t)row2 * V + col;
-            if (vec && col + 4 <= V) {
-              *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(&St[wid][tr][c4]);
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                if (col + e < V) dst[e] = St[wid][tr][c4 + e];
-            }
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      }
-    }
+  // FULL (every tile but the last vocab tile / row block): no column or row guards.
+  if ((vt + 1) * VT_COLS <= V && rb + VT_ROWS <= R && (V & 3) == 0)
+    vl_epilogue<true>(acc, bias, logits, St[wid], Pm[wid], Ps[wid], rb, cw, lane, R, V);
+  else
+    vl_epilogue<false>(acc, bias, logits, St[wid], Pm[wid], Ps[wid], rb, cw, lane, R, V);
   __syncthreads();
   if (wid == 0) {
     const int rr = lane, row = rb + rr;
