@@ -202,7 +202,7 @@ __device__ __forceinline__ int vhslot(int w) { return (int)(((unsigned)w * 26544
 
 }  // namespace
 
-#define VS_THREADS 1024
+#define VS_THREADS 1024  // 256 threads measured 16.6 us vs 14.0 at R = 256 (fewer loads in flight)
 #define VS_NONE 0x7fffffff  // sentinel id: (-inf, VS_NONE) never beats anything
 
 namespace {
