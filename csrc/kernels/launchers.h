@@ -79,7 +79,7 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
                                 int H, hipStream_t st);
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
-                                unsigned* err, int T, int B, int H, hipStream_t st);
+                                unsigned* err, float* dbias, int T, int B, int H, hipStream_t st);
 int vocab_topk_tiles(int V);
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,

@@ -211,7 +211,9 @@ template <int H>
 __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
-    const float* __restrict__ cs, const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile) {
+    const float* __restrict__ cs, const int* __restrict__ lens, gu64* xbuf, gu32* err,
+    float* __restrict__ dbias,  // [2][4H] nullable: += sum over rows and steps of dz (gate-bias gradient)
+    int T, int B, int ntile) {
   constexpr int G4 = 4 * H, NC = H / 64, KS = 256 / 32, SLOT = 16 * 64, TEAMX = 2 * NC * NC * SLOT;
   __shared__ __attribute__((aligned(16))) bf16 Ash[16 * 256];   // dz slice [16 rows][4 gates x 64 units]
   __shared__ float Pown[16 * 64];                                // own partial dh [16 rows][64 units]
@@ -246,6 +248,10 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   }
   gu64* xb = xbuf + (size_t)team * TEAMX;  // [parity][dest][src][16][64]
   bool dead = false;
+  // gate-bias gradient of (unit u, gate g): the lane's 4 rows summed over all steps in
+  // registers (fp32, off the recurrence's critical path), reduced over the wave's 4 row
+  // groups and added once per team at the end -- replaces a 2 x 210 MB column reduction
+  float bacc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int s = T - 1; s >= 0; --s) {
     float dho[4], dhf[4], a4[4][4], cn[4], cpv[4];
 #pragma unroll
@@ -324,6 +330,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       }
       const int row = (lane >> 4) * 4 + i;
 #pragma unroll
+      for (int g = 0; g < 4; ++g) bacc[g] += dzv[i][g];
+#pragma unroll
       for (int g = 0; g < 4; ++g) Ash[swz<256>(row, g * 64 + ul)] = f2bf(dzv[i][g]);
       if (rok[i]) {
         bf16* dzr = dz + (((size_t)d * T + s) * B + rc[i]) * G4;
@@ -365,6 +373,13 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     if (rok[i]) dc_carry[(size_t)d * BH + (size_t)rc[i] * H + u] = dcreg[i];
+  if (dbias) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float t = sum_x32(sum_x16(bacc[g]));  // lanes l, l^16, l^32, l^48: the 4 row groups
+      if ((lane >> 4) == 0) atomicAdd(dbias + (size_t)d * G4 + g * H + u, t);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------- launchers
@@ -398,13 +413,13 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
 
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
-                                unsigned* err, int T, int B, int H, hipStream_t st) {
+                                unsigned* err, float* dbias, int T, int B, int H, hipStream_t st) {
   const int grid = lstm_persistent_grid(H, B), ntile = (B + 15) / 16;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
 #define LAUNCH_B(HH)                                                                                          \
   hipLaunchKernelGGL(lstm_bwd_persistent_kernel<HH>, dim3(grid), dim3(256), 0, st, dz, Wn, dout, dh_fin, dc_carry, \
-                     acts, cs, lens, xb, e, T, B, ntile)
+                     acts, cs, lens, xb, e, dbias, T, B, ntile)
   if (H == 64) LAUNCH_B(64);
   else if (H == 128) LAUNCH_B(128);
   else LAUNCH_B(256);

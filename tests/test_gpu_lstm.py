@@ -54,9 +54,15 @@ def test_persistent_matches_step_kernels(H, B, T):
                 k.lstm_enc_bwd_step(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, s, T, B, H)
         else:
             xb = torch.zeros(int(k.lstm_persistent_xbuf(H, B, True)), device="cuda", dtype=torch.long)
-            k.lstm_bwd_persistent(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, xb, err, T, B, H)
+            db = torch.full((2, 4 * H), 0.25, device="cuda")  # accumulates onto what is there
+            k.lstm_bwd_persistent(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, xb, err, db, T, B, H)
         torch.cuda.synchronize()
         assert int(err.item()) == 0
+        if mode != "step":
+            # gate-bias gradient from the kernel's fp32 register sums vs the column sum of the
+            # bf16 dz it wrote (each term rounded to bf16: ~1e-3 relative)
+            ref = dz.float().sum(dim=(1, 2)) + 0.25
+            torch.testing.assert_close(db, ref, rtol=2e-2, atol=1e-2 * float(ref.abs().max()))
         res[mode] = dict(hs=hs.float(), cs=cs, acts=acts, out=out.float(), dz=dz.float(), dc=dcc)
     a, b = res["step"], res["persistent"]
     for name, tol in [("hs", 3e-2), ("cs", 3e-2), ("acts", 2e-2), ("out", 3e-2), ("dz", 3e-2), ("dc", 3e-2)]:

@@ -151,6 +151,7 @@ class HipPointerGenerator:
         if self.persistent_lstm:
             w["lstm_xf"] = z(int(self.k.lstm_persistent_xbuf(H, B, False)), dt=torch.long)
             w["lstm_xb"] = z(int(self.k.lstm_persistent_xbuf(H, B, True)), dt=torch.long)
+            w["lstm_db"] = z(2, 4 * H)  # gate-bias gradients [fw; bw] accumulated by the BPTT kernel
         w["lstm_err"] = z(1, dt=torch.int32)
         # one fused attention-backward kernel per decoder step (attn_bwd_step);
         # TSAMD_ATTN_BWD_FUSED=0 selects the two-kernel path (attn_bwd_da over Et + attn_bwd_tanh)
@@ -630,8 +631,9 @@ class HipPointerGenerator:
                 st["dc_carry"].zero_()
             if self.persistent_lstm:
                 w["lstm_xb"].zero_()
+                w["lstm_db"].zero_()
                 k.lstm_bwd_persistent(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"], st["dc_carry"],
-                                      st["acts"], st["cs"], lens, w["lstm_xb"], w["lstm_err"], T, B, H)
+                                      st["acts"], st["cs"], lens, w["lstm_xb"], w["lstm_err"], w["lstm_db"], T, B, H)
             else:
                 for s in reversed(range(T)):
                     k.lstm_enc_bwd_step(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"],
@@ -642,7 +644,10 @@ class HipPointerGenerator:
                 gkd = g(enc_k(layer, d))
                 wgrad_into(gkd[:din], st["x_sf"][di].view(T * B, din), dzd)
                 wgrad_into(gkd[din:], st["hs"][di, :T].reshape(T * B, H), dzd)
-                g(enc_b(layer, d)).copy_(dzd.sum(0, dtype=F32))
+                if self.persistent_lstm:
+                    g(enc_b(layer, d)).copy_(w["lstm_db"][di])
+                else:
+                    g(enc_b(layer, d)).copy_(dzd.sum(0, dtype=F32))
                 torch.mm(dzd, self.pk[f"enc{layer}_Kx{di}"].t(), out_dtype=F32, out=dxs[di])
             dx = st["dx"]
             k.from_step_frame(dxs, w["rev_idx"], dx, B, T, din)  # fw + reversed bw, batch frame
