@@ -242,7 +242,8 @@ void cast_colsum(const Tensor& x, const Tensor& xb, const Tensor& colsum, int64_
   chk(x, F32, "x"); chk(xb, BF, "xb"); chk(colsum, F32, "colsum");
   TORCH_CHECK(C % 4 == 0 && C / 4 <= 256 && 256 % (C / 4) == 0, "cast_colsum: C % 4 == 0 and C / 4 divides 256");
   numel_eq(x, N * C, "x"); numel_eq(xb, N * C, "xb"); numel_eq(colsum, C, "colsum");
-  launch_cast_colsum(P<float>(x), P<bf16>(xb), P<float>(colsum), (int)N, (int)C, stream());
+  auto part = at::empty({(int64_t)cast_colsum_blocks((int)N, (int)C), C}, x.options());
+  launch_cast_colsum(P<float>(x), P<bf16>(xb), P<float>(part), P<float>(colsum), (int)N, (int)C, stream());
 }
 
 // ---------------------------------------------------------------- embedding gradient
