@@ -183,10 +183,14 @@ void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const 
   chk(dF, BF, "dF"); chk(dv, F32, "dv");
   TORCH_CHECK(A % 64 == 0, "bad A");
   numel_eq(F, B * T * A, "F"); numel_eq(S_all, D * B * A, "S_all"); numel_eq(de_all, D * B * T, "de_all");
-  numel_eq(dF, B * T * A, "dF"); numel_eq(dv, A, "dv");
-  chko(wc, F32, A, "wc"); chko(cov_all, F32, D * B * T, "cov_all"); chko(dwc, F32, A, "dwc");
+  // dv / dwc: [nslot][A] partial rows (nslot a power of two <= 1024; the caller sums them)
+  const int64_t nslot = dv.numel() / A;
+  TORCH_CHECK(nslot >= 1 && nslot <= 1024 && (nslot & (nslot - 1)) == 0 && dv.numel() == nslot * A,
+              "dv: [nslot, A] with nslot a power of two");
+  numel_eq(dF, B * T * A, "dF");
+  chko(wc, F32, A, "wc"); chko(cov_all, F32, D * B * T, "cov_all"); chko(dwc, F32, nslot * A, "dwc");
   launch_attn_bwd_feat(P<bf16>(F), P<float>(S_all), P<float>(v), PO<float>(wc), PO<float>(cov_all), P<float>(de_all),
-                       P<int>(lens), P<bf16>(dF), P<float>(dv), PO<float>(dwc), D, B, T, A, stream());
+                       P<int>(lens), P<bf16>(dF), P<float>(dv), PO<float>(dwc), D, B, T, A, (int)nslot, stream());
 }
 
 int64_t attn_chunks(int64_t T) { return attn_nchunk(T); }

@@ -867,7 +867,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
     const bf16* __restrict__ F, const float* __restrict__ S_all, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov_all, const float* __restrict__ de_all,
     const int* __restrict__ lens, bf16* __restrict__ dF, float* __restrict__ dv, float* __restrict__ dwc,
-    int D, int B, int T, int A) {
+    int D, int B, int T, int A, int nslot) {
   __shared__ float pv[4][512];
   __shared__ float pw[4][512];
   const int b = blockIdx.y;
@@ -966,8 +966,11 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
     if (kk < A) {
       const float x = pv[0][k] + pv[1][k] + pv[2][k] + pv[3][k];
       const float y = pw[0][k] + pw[1][k] + pw[2][k] + pw[3][k];
-      if (x != 0.f) atomicAdd(dv + kk, x);
-      if (dwc && y != 0.f) atomicAdd(dwc + kk, y);
+      // nslot (power of two) partial rows: the B x T/16 workgroups would otherwise all add
+      // into the same A addresses, and same-address atomics serialise at L2
+      const size_t so = (size_t)((blockIdx.x + blockIdx.y * gridDim.x) & (nslot - 1)) * A;
+      if (x != 0.f) atomicAdd(dv + so + kk, x);
+      if (dwc && y != 0.f) atomicAdd(dwc + so + kk, y);
     }
   }
 }
@@ -1060,7 +1063,7 @@ void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const fl
 }
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, bf16* dF, float* dv, float* dwc, int D, int B, int T,
-                          int A, hipStream_t st) {
+                          int A, int nslot, hipStream_t st) {
   // Default (2): 4 positions per wave capped at 128 VGPRs = 4 waves/SIMD (a few prologue
   // spills): 1.51 ms vs 1.64 ms uncapped at 3 waves/SIMD (B = 256, T = 400, D = 100).
   // TSAMD_FEAT_V=0: uncapped; 1: 2 positions per wave (1.65 ms).
@@ -1068,14 +1071,14 @@ void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, con
   if (fv == 1) {
     dim3 grid((T + 7) / 8, B, (A + 511) / 512);
     hipLaunchKernelGGL((attn_bwd_feat_kernel<2, 1>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
-                       dv, dwc, D, B, T, A);
+                       dv, dwc, D, B, T, A, nslot);
   } else if (fv == 2) {
     dim3 grid((T + 15) / 16, B, (A + 511) / 512);
     hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 4>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
-                       dv, dwc, D, B, T, A);
+                       dv, dwc, D, B, T, A, nslot);
   } else {
     dim3 grid((T + 15) / 16, B, (A + 511) / 512);
     hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 1>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
-                       dv, dwc, D, B, T, A);
+                       dv, dwc, D, B, T, A, nslot);
   }
 }

@@ -27,7 +27,7 @@ void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const fl
                           float* dcov_out, int B, int T, int A, hipStream_t st);
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, bf16* dF, float* dv, float* dwc, int D, int B, int T,
-                          int A, hipStream_t st);
+                          int A, int nslot, hipStream_t st);
 
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st);

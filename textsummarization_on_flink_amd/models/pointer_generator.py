@@ -210,8 +210,8 @@ class HipPointerGenerator:
         w["ATTb"] = z(D, B, T, dt=BF)
         w["DCTXb"] = z(D, B, A, dt=BF)
         self._dE = z(B, T, A)
-        w["dv"] = z(A)
-        w["dwc"] = z(A)
+        w["dv"] = z(32, A)   # attn_bwd_feat partial rows (spread the atomics), summed after
+        w["dwc"] = z(32, A)
         # optimizer
         w["opt_part"] = z(int(self.k.opt_parts()))
         w["gnorm"] = z(1)
@@ -581,9 +581,9 @@ class HipPointerGenerator:
         w["dwc"].zero_()
         k.attn_bwd_feat(F, w["S"], v, wc, w["COV"][:D] if cov else None, w["DE"], lens, w["dF"], w["dv"],
                         w["dwc"] if cov else None, D, B, T, A)
-        g(VATT).copy_(w["dv"])
+        g(VATT).copy_(w["dv"].sum(0).view_as(g(VATT)))
         if cov:
-            g(WCOV).view(A).copy_(w["dwc"])
+            g(WCOV).view(A).copy_(w["dwc"].sum(0))
         dFb = w["dF"].view(B * T, A)
         top = self.enc[-1]
         wgrad_into(g(WH).view(A, A), top["out"].view(B * T, A), dFb)
