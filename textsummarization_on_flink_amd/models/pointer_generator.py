@@ -24,6 +24,7 @@ import os
 
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 
 from ..ops import ops as _ops
@@ -116,15 +117,28 @@ class HipPointerGenerator:
         B, T, D, E, H, A, V, L = self.B, self.T, self.D, self.E, self.H, self.A, self.V, self.L
         z = lambda *s, dt=F32: torch.zeros(*s, dtype=dt, device=self.dev)
         w: Dict[str, torch.Tensor] = {}
-        # inputs (static, copied into before every replay)
-        w["enc_batch"] = z(B, T, dt=torch.long)
-        w["enc_lens"] = torch.ones(B, dtype=torch.int32, device=self.dev)
-        w["rev_idx"] = z(B, T, dt=torch.long)
-        w["ext"] = z(B, T, dt=torch.int32)
-        w["dec_batch_t"] = z(D, B, dt=torch.long)
-        w["target_t"] = z(D, B, dt=torch.int32)
-        w["rowg"] = z(D, B)
-        w["gcl"] = z(D, B)
+        # inputs (static, copied into before every replay): views of ONE device buffer, so a
+        # batch arrives with one H2D copy from a pinned host pack instead of eight (each
+        # in-stream copy costs ~15 us of DMA latency ahead of the step)
+        shapes = {"BT": (B, T), "B": (B,), "DB": (D, B)}
+        layout, off = [], 0
+        for name, sk, dt in (("enc_batch", "BT", torch.long), ("enc_lens", "B", torch.int32),
+                             ("rev_idx", "BT", torch.long), ("ext", "BT", torch.int32),
+                             ("dec_batch_t", "DB", torch.long), ("target_t", "DB", torch.int32),
+                             ("rowg", "DB", F32), ("gcl", "DB", F32)):
+            shp = shapes[sk]
+            nb = int(np.prod(shp)) * torch.empty(0, dtype=dt).element_size()
+            layout.append((name, off, shp, dt, nb))
+            off += (nb + 255) // 256 * 256
+        self._in_layout = layout
+        self._in_pack = torch.zeros(off, dtype=torch.uint8, device=self.dev)
+        for name, o, shp, dt, nb in layout:
+            w[name] = self._in_pack[o:o + nb].view(dt).view(shp)
+        w["enc_lens"].fill_(1)
+        # double-buffered pinned host packs; an event per pack guards its reuse
+        self._in_host = [torch.zeros(off, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self._in_ev = [None, None]
+        self._in_i = 0
         # encoder, per layer
         self.enc = []
         for layer in range(L):
@@ -309,9 +323,17 @@ class HipPointerGenerator:
             "rowg": np.ascontiguousarray(rowg.T).astype(np.float32),
             "gcl": np.ascontiguousarray(gcl.T).astype(np.float32),
         }
-        for k, v in host.items():
-            w[k].copy_(torch.from_numpy(v).pin_memory() if torch.cuda.is_available() else torch.from_numpy(v),
-                       non_blocking=True)
+        i = self._in_i
+        if self._in_ev[i] is not None:
+            self._in_ev[i].synchronize()  # the copy out of this pack (two batches ago) is done
+        hn = self._in_host[i].numpy()
+        for name, o, shp, dt, nb in self._in_layout:
+            hn[o:o + nb] = np.ascontiguousarray(host[name]).reshape(-1).view(np.uint8)
+        self._in_pack.copy_(self._in_host[i], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._in_ev[i] = ev
+        self._in_i = i ^ 1
 
     # ------------------------------------------------------------------ forward
     def _encoder_forward(self):
