@@ -513,6 +513,27 @@ void linear2(const Tensor& a1, int64_t K1, const OT& a2, int64_t K2, const Tenso
                  PO<bf16>(outb), B, N, stream());
 }
 
+static void linear2_check(const Tensor& a1, int64_t K1, const OT& a2, int64_t K2, const Tensor& Wt, const OT& bias,
+                          const OT& add, const OT& out, const OT& outb, int64_t B, int64_t N) {
+  chk(a1, BF, "a1"); chk(Wt, BF, "Wt");
+  TORCH_CHECK(K1 % 32 == 0 && K2 % 32 == 0 && N % 16 == 0 && K1 > 0, "linear2: K multiples of 32, N of 16");
+  TORCH_CHECK((K2 == 0) == !(a2.has_value() && a2->defined()), "linear2: a2 given iff K2 > 0");
+  numel_eq(a1, B * K1, "a1"); chko(a2, BF, B * K2, "a2"); numel_eq(Wt, N * (K1 + K2), "Wt");
+  chko(bias, F32, N, "bias"); chko(add, F32, B * N, "add"); chko(out, F32, B * N, "out"); chko(outb, BF, B * N, "outb");
+  TORCH_CHECK(PO<float>(out) || PO<bf16>(outb), "linear2 needs an output");
+}
+// two independent linear2 problems over the same B rows in one launch
+void linear2_pair(const Tensor& a1, int64_t K1, const OT& a2, int64_t K2, const Tensor& Wt, const OT& bias,
+                  const OT& add, const OT& out, const OT& outb, int64_t N, const Tensor& c1, int64_t L1, const OT& c2,
+                  int64_t L2, const Tensor& Vt, const OT& vbias, const OT& vadd, const OT& vout, const OT& voutb,
+                  int64_t M, int64_t B) {
+  linear2_check(a1, K1, a2, K2, Wt, bias, add, out, outb, B, N);
+  linear2_check(c1, L1, c2, L2, Vt, vbias, vadd, vout, voutb, B, M);
+  launch_linear2_pair(P<bf16>(a1), K1, PO<bf16>(a2), K2, P<bf16>(Wt), PO<float>(bias), PO<float>(add), PO<float>(out),
+                      PO<bf16>(outb), N, P<bf16>(c1), L1, PO<bf16>(c2), L2, P<bf16>(Vt), PO<float>(vbias),
+                      PO<float>(vadd), PO<float>(vout), PO<bf16>(voutb), M, B, stream());
+}
+
 void pgen(const Tensor& ctx, const Tensor& c, const Tensor& h, const Tensor& x, const Tensor& w, const Tensor& b,
           const Tensor& pg, int64_t R, int64_t A, int64_t H, int64_t E) {
   chk(ctx, F32, "ctx"); chk(c, F32, "c"); chk(h, BF, "h"); chk(x, F32, "x"); chk(w, F32, "w"); chk(b, F32, "b");
@@ -562,6 +583,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("to_step_frame", &to_step_frame);
   m.def("from_step_frame", &from_step_frame);
   m.def("transpose_bta", &transpose_bta);
+  m.def("linear2_pair", &linear2_pair);
   m.def("cast_colsum", &cast_colsum);
   m.def("ptr_rowfin", &ptr_rowfin);
   m.def("clip_adagrad", &clip_adagrad);

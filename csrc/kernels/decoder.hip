@@ -74,18 +74,19 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
 //   out[r][n] = sum_{k<K1} a1[r][k] Wt[n][k] + sum_{k<K2} a2[r][k] Wt[n][K1+k] + bias[n] + add[r][n]
 // Wt: [N][K1+K2] bf16 ("Bt" layout).  fp32 and/or bf16 outputs.  grid (N/16, ceil(B/16)),
 // 4 waves split K (kslice_mma) and reduce in LDS.  add may alias out (same element, same lane).
-__global__ __launch_bounds__(256) void linear2_kernel(
-    const bf16* __restrict__ a1, int K1, const bf16* __restrict__ a2, int K2, const bf16* __restrict__ Wt,
-    const float* __restrict__ bias, const float* add, float* out, bf16* __restrict__ outb, int B, int N) {
-  __shared__ float red[4 * 256];
+struct L2Args {
+  const bf16* a1; int K1; const bf16* a2; int K2; const bf16* Wt;
+  const float* bias; const float* add; float* out; bf16* outb; int N;
+};
+
+__device__ __forceinline__ void linear2_body(const L2Args& p, int B, int n0, int r0, float* red) {
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
   const int ar = min(r0 + (lane & 15), B - 1);
   const int kof = 8 * (lane >> 4);
-  const int K = K1 + K2;
-  const bf16* r1 = a1 + (size_t)ar * K1 + kof;
-  const bf16* r2 = a2 ? a2 + (size_t)ar * K2 + kof - K1 : nullptr;
-  const bf16* brow = Wt + (size_t)(n0 + (lane & 15)) * K + kof;
+  const int K1 = p.K1, K = p.K1 + p.K2, N = p.N;
+  const bf16* r1 = p.a1 + (size_t)ar * K1 + kof;
+  const bf16* r2 = p.a2 ? p.a2 + (size_t)ar * p.K2 + kof - K1 : nullptr;
+  const bf16* brow = p.Wt + (size_t)(n0 + (lane & 15)) * K + kof;
   const int nst = K / 32;
   const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
   f32x4 acc[1] = {f32x4{0, 0, 0, 0}};
@@ -96,9 +97,25 @@ __global__ __launch_bounds__(256) void linear2_kernel(
   const int r = r0 + (lane >> 4) * 4 + wid, n = n0 + (lane & 15);
   if (r >= B) return;
   const size_t ix = (size_t)r * N + n;
-  float v = o[0] + (bias ? bias[n] : 0.f) + (add ? add[ix] : 0.f);
-  if (out) out[ix] = v;
-  if (outb) outb[ix] = f2bf(v);
+  const float v = o[0] + (p.bias ? p.bias[n] : 0.f) + (p.add ? p.add[ix] : 0.f);
+  if (p.out) p.out[ix] = v;
+  if (p.outb) p.outb[ix] = f2bf(v);
+}
+
+__global__ __launch_bounds__(256) void linear2_kernel(L2Args p, int B) {
+  __shared__ float red[4 * 256];
+  linear2_body(p, B, blockIdx.x * 16, blockIdx.y * 16, red);
+}
+
+// Two independent linear2 problems on the same rows in one launch (blockIdx.z picks the
+// problem; column tiles past a problem's N exit): the beam-decode step pairs the attention
+// query projection with the x-merge of the previous context, saving a kernel boundary.
+__global__ __launch_bounds__(256) void linear2_pair_kernel(L2Args p0, L2Args p1, int B) {
+  __shared__ float red[4 * 256];
+  const L2Args& p = blockIdx.z ? p1 : p0;
+  const int n0 = blockIdx.x * 16;
+  if (n0 >= p.N) return;  // uniform per block, before any barrier
+  linear2_body(p, B, n0, blockIdx.y * 16, red);
 }
 
 // p_gen = sigmoid([ctx, c, h, x] . w + b), one wave per row (reference attention_decoder.py:164-168).
@@ -242,7 +259,17 @@ void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, c
 void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
                     const float* add, float* out, bf16* outb, int B, int N, hipStream_t st) {
   dim3 grid(N / 16, (B + 15) / 16);
-  hipLaunchKernelGGL(linear2_kernel, grid, dim3(256), 0, st, a1, K1, a2, K2, Wt, bias, add, out, outb, B, N);
+  const L2Args p{a1, K1, a2, K2, Wt, bias, add, out, outb, N};
+  hipLaunchKernelGGL(linear2_kernel, grid, dim3(256), 0, st, p, B);
+}
+void launch_linear2_pair(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
+                         const float* add, float* out, bf16* outb, int N, const bf16* c1, int L1, const bf16* c2,
+                         int L2, const bf16* Vt, const float* vbias, const float* vadd, float* vout, bf16* voutb,
+                         int M, int B, hipStream_t st) {
+  dim3 grid((N > M ? N : M) / 16, (B + 15) / 16, 2);
+  const L2Args p0{a1, K1, a2, K2, Wt, bias, add, out, outb, N};
+  const L2Args p1{c1, L1, c2, L2, Vt, vbias, vadd, vout, voutb, M};
+  hipLaunchKernelGGL(linear2_pair_kernel, grid, dim3(256), 0, st, p0, p1, B);
 }
 void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out, int B, int H,
                       int A, hipStream_t st) {

@@ -68,6 +68,10 @@ void launch_beam_gather(const int* gidx, const int* latest, const float* c_src, 
                         hipStream_t st);
 void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
                     const float* add, float* out, bf16* outb, int B, int N, hipStream_t st);
+void launch_linear2_pair(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
+                         const float* add, float* out, bf16* outb, int N, const bf16* c1, int L1, const bf16* c2,
+                         int L2, const bf16* Vt, const float* vbias, const float* vadd, float* vout, bf16* voutb,
+                         int M, int B, hipStream_t st);
 void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x, const float* w, const float* b,
                  float* pg, int R, int A, int H, int E, hipStream_t st);
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,

@@ -156,15 +156,19 @@ class DeviceBeamDecoder:
                       b["XG"], b["x"], R, H, A, T, E, V, self.vocab.word2id(UNKNOWN_TOKEN))
         k.dec_cell_fwd(b["XG"], b["ctxs_bf"], b["h"], b["c"], eng.pk["WcT2"], Y["C"], b["Cb2"], Y["H"], b["act"],
                        R, H, A)
-        k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
+        if hps.pointer_gen:
+            # one launch: attention query s = [c, h] . W_s + b, and the x-merge for p_gen,
+            # x = x0 + ctx*_{t-1} . W_in[E:] (x0 = emb . W_in[:E] + b_in gathered per token)
+            k.linear2_pair(b["Cb2"], H, Y["H"], H, eng.pk["WsT"], p[ATT_B], None, b["s"], None, A,
+                           b["ctxs_bf"], A, None, 0, eng.pk["WicT"], None, b["x"], b["x"], None, E, R)
+        else:
+            k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
         k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], Y["COV"] if cov else None, b["lens_att"],
                      b["e"], R, T, A, self.rep)
         k.attn_softmax_ctx(b["e"], b["E"], b["lens_att"], None, Y["ATT"], None, None, Y["CTX"], b["ctx_bf"], R, T, A,
                            self.rep)
         pg = None
         if hps.pointer_gen:
-            # x = x0 + ctx* . W_in[E:]  (x0 = emb . W_in[:E] + b_in gathered per token)
-            k.linear2(b["ctxs_bf"], A, None, 0, eng.pk["WicT"], None, b["x"], b["x"], None, R, E)
             k.pgen(Y["CTX"], Y["C"], Y["H"], b["x"], self.pg_w, p[PG_B], b["PG"], R, A, H, E)
             pg = b["PG"]
         k.linear2(Y["H"], H, b["ctx_bf"], A, eng.pk["OUTmT"], p[OUT_B], None, None, b["outb"], R, H)
