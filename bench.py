@@ -1,4 +1,5 @@
-"""Headline benchmark: pointer-generator (+coverage) training throughput on MI355X.
+"""Headline benchmark: pointer-generator (+coverage) training throughput on MI355X, plus the
+beam-4 decode throughput as a secondary field of the same JSON line.
 
 Metric (BASELINE.json / BASELINE.md): train tokens/sec for the whole job = sum over
 ranks of non-pad encoder tokens (enc_lens) + non-pad decoder tokens (dec_padding_mask)
@@ -8,16 +9,31 @@ weights + Adagrad accumulators), synthetic CNN/DM-shaped data, random-init weigh
 Weak scaling: the per-GPU batch is fixed, global batch = batch x N.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-       (N > 1 is launched by torch.distributed.run; one rank per GPU, RCCL all-reduce.)
 
-Timed region per step: H2D copy of the batch, forward + backward (one hipGraph replay),
-gradient all-reduce (RCCL), clip + Adagrad + weight repack (second hipGraph) -- i.e. the
-complete optimizer step; only synthetic text generation/tokenisation is done ahead of
-time (like a prefetching loader).
+Multi-GPU: one process per GPU, torch.distributed over RCCL (backend "nccl"), gradients
+all-reduced in three buckets overlapped with the backward.  Either launch it with
+``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` (RANK /
+WORLD_SIZE / MASTER_* come from the environment), or run ``python bench.py --gpus N``
+directly: without WORLD_SIZE in the environment this process starts the N rank processes
+itself (torchrun-style env, rendezvous on 127.0.0.1) before anything touches the GPU,
+relays their output and exits with the worst exit code.  ``n_gpus`` in the JSON is the
+world size the process group reports.
+
+Timed region per step: H2D copy of the batch, forward + backward (three hipGraph
+replays), gradient all-reduce (RCCL), clip + Adagrad + weight repack (a fourth hipGraph)
+-- the complete optimizer step; only synthetic text generation/tokenisation is done ahead
+of time (like a prefetching loader).  The W warmup steps include the graph captures.
+
+Secondary (BASELINE config #4, ``beam4_summaries_per_sec``): after the training timing,
+every rank decodes ``--decode-batches`` batches of 64 articles x beam 4 (hipGraph-captured
+device beam search, fresh random-init weights, encoder included, host backtracking
+included, tokenisation excluded); the value is the sum over ranks of completed summaries
+divided by the slowest rank's wall time.  ``--decode-batches 0`` skips it.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -27,12 +43,12 @@ sys.path.insert(0, REPO)
 BASELINE_TOKENS_PER_S = 6700.0  # See et al. 2017 on a K40m, <=6.7k tokens/s
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (rows); 256 keeps the persistent LSTM grid at 128 of 256 CUs so the overlapped RCCL all-reduce always finds free CUs")
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (rows)")
     ap.add_argument("--no-coverage", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled per rank")
@@ -44,7 +60,66 @@ def main():
     ap.add_argument("--layers", type=int, default=1, help="stacked bi-LSTM encoder layers (config #5: 2)")
     ap.add_argument("--backend", default=None, help="process-group backend override (default nccl = RCCL; gloo "
                                                     "lets several ranks share one GPU for a plumbing check)")
-    args = ap.parse_args()
+    ap.add_argument("--grad-compress", default="none", choices=("none", "bf16"),
+                    help="gradient all-reduce wire format (fp32 master weights either way)")
+    ap.add_argument("--decode-batches", type=int, default=10, help="timed beam-4 decode batches (0 = skip)")
+    ap.add_argument("--decode-articles", type=int, default=64)
+    ap.add_argument("--port", type=int, default=0, help="rendezvous port when launching ranks (0 = free port)")
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, port: int = 0) -> int:
+    """Start ``n`` rank processes of this script (one per GPU) and wait for them.  Runs
+    before anything initialises the GPU in this process (torch is not even imported)."""
+    port = port or _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in procs:  # one rank failed: the others would block in a collective
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def _timed(fn, info, D, torch):
+    torch.cuda.synchronize()
+    D.barrier(info)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = fn()
+    torch.cuda.synchronize()
+    D.barrier(info)
+    torch.cuda.synchronize()
+    return res, time.perf_counter() - t0
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv), args.port)
 
     import torch
     from textsummarization_on_flink_amd.config import HParams
@@ -53,13 +128,15 @@ def main():
     from textsummarization_on_flink_amd.train.trainer import GraphTrainer
 
     info = D.init_from_env(backend=args.backend)
-    if info.world != args.gpus and not (info.world == 1 and args.gpus == 1):
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world}", file=sys.stderr)
+    if info.enabled:
+        assert torch.distributed.get_world_size() == info.world
+    if info.world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but the process group has {info.world} ranks", file=sys.stderr)
     dev_id = info.local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_id)
     hps = HParams(batch_size=args.batch, max_enc_steps=args.enc, max_dec_steps=args.dec, vocab_size=args.vocab,
                   hidden_dim=args.hidden, emb_dim=args.emb, coverage=not args.no_coverage, pointer_gen=True,
-                  enc_layers=args.layers)
+                  enc_layers=args.layers, grad_compress=args.grad_compress)
     corpus = SyntheticCorpus(vocab_size=args.vocab, seed=1000 + info.rank)
     vocab = corpus.vocab(args.vocab)
     batches = make_batches(hps, vocab, corpus, args.pool, pad_enc_to=args.enc)
@@ -70,26 +147,28 @@ def main():
         out = tr.step(batches[i % len(batches)])
     if args.warmup:
         tr.check_finite(out)
-    torch.cuda.synchronize()
-    D.barrier(info)
-    torch.cuda.synchronize()
-    tokens = 0
-    padded = 0
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        b = batches[i % len(batches)]
-        out = tr.step(b)
-        tokens += b.num_tokens()
-        padded += b.padded_tokens()
-    torch.cuda.synchronize()
-    D.barrier(info)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+
+    def train_loop():
+        tokens = padded = 0
+        o = None
+        for i in range(args.steps):
+            b = batches[i % len(batches)]
+            o = tr.step(b)
+            tokens += b.num_tokens()
+            padded += b.padded_tokens()
+        return o, tokens, padded
+
+    (out, tokens, padded), elapsed = _timed(train_loop, info, D, torch)
     vals = tr.check_finite(out)
     elapsed_max = D.all_reduce_scalar(elapsed, info, op="max", device=tr.device)
     tok_all = D.all_reduce_scalar(float(tokens), info, op="sum", device=tr.device)
     pad_all = D.all_reduce_scalar(float(padded), info, op="sum", device=tr.device)
     value = tok_all / elapsed_max
+
+    dec = None
+    if args.decode_batches > 0:
+        dec = bench_decode(args, info, D, torch, dev_id)
+
     if info.is_chief:
         rec = {
             "metric": "train_tokens_per_sec",
@@ -112,15 +191,57 @@ def main():
                 "per_gpu_batch": args.batch,
                 "seq_len": f"{hps.max_enc_steps}->{hps.max_dec_steps}",
                 "parallelism": f"dp{info.world}",
+                "backend": info.backend if info.enabled else "none",
+                "grad_allreduce": ("bf16" if args.grad_compress == "bf16" else "fp32") if info.enabled else "none",
                 "padded_tokens_per_sec": round(pad_all / elapsed_max, 1),
                 "loss": round(vals.get("total_loss", float("nan")), 4),
                 "graph": not args.no_graph,
+                "persistent_lstm": bool(tr.engine.persistent_lstm),
             },
         }
+        if dec is not None:
+            rec.update(dec)
         print(json.dumps(rec), flush=True)
     if info.enabled:
         torch.distributed.destroy_process_group()
+    return 0
+
+
+def bench_decode(args, info, D, torch, dev_id):
+    """Beam-4 decode, config #4 (64 articles x beam 4 per batch), on every rank."""
+    from textsummarization_on_flink_amd.config import HParams
+    from textsummarization_on_flink_amd.data.synthetic import SyntheticCorpus, make_batches
+    from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
+    from textsummarization_on_flink_amd.models.params import build_params
+
+    hps = HParams(mode="decode", batch_size=args.decode_articles, beam_size=4, coverage=not args.no_coverage,
+                  vocab_size=args.vocab, hidden_dim=args.hidden, emb_dim=args.emb, max_enc_steps=args.enc,
+                  max_dec_steps=args.dec, enc_layers=args.layers)
+    corpus = SyntheticCorpus(vocab_size=args.vocab, seed=7 + info.rank)
+    vocab = corpus.vocab(args.vocab)
+    pool = make_batches(hps, vocab, corpus, 3, pad_enc_to=hps.max_enc_steps)
+    params = build_params(hps, vocab.size(), device=f"cuda:{dev_id}")
+    dec = DeviceBeamDecoder(hps, vocab, params, n_articles=args.decode_articles, T=hps.max_enc_steps,
+                            use_graph=not args.no_graph, keep_attn=False)
+    dec.decode(pool[0])  # warm-up: graph capture
+
+    def loop():
+        n = steps = 0
+        for i in range(args.decode_batches):
+            hyps = dec.decode(pool[1 + i % 2])  # synchronous: results() reads the device buffers
+            n += len(hyps)
+            steps += dec.steps_run
+        return n, steps
+
+    (n, steps), el = _timed(loop, info, D, torch)
+    el_max = D.all_reduce_scalar(el, info, op="max", device=f"cuda:{dev_id}")
+    n_all = D.all_reduce_scalar(float(n), info, op="sum", device=f"cuda:{dev_id}")
+    return {"beam4_summaries_per_sec": round(n_all / el_max, 1),
+            "beam4_ms_per_batch": round(1000.0 * el_max / args.decode_batches, 3),
+            "beam4_config": {"articles_per_batch": args.decode_articles, "beam": 4, "batches": args.decode_batches,
+                             "decode_steps_per_batch": steps / args.decode_batches, "min_dec_steps": hps.min_dec_steps,
+                             "max_dec_steps": hps.max_dec_steps, "graph": not args.no_graph}}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

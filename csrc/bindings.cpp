@@ -64,6 +64,7 @@ void lstm_enc_bwd_step(const Tensor& dz, const Tensor& Wn, const Tensor& dout, c
 
 // persistent (one launch for all T steps) variants; see lstm_persistent.hip
 int64_t lstm_persistent_grid_op(int64_t H, int64_t B) { return lstm_persistent_grid((int)H, (int)B); }
+int64_t lstm_persistent_capacity_op(int64_t H) { return lstm_persistent_capacity((int)H); }
 int64_t lstm_persistent_xbuf_op(int64_t H, int64_t B, bool bwd) {
   return (int64_t)lstm_persistent_xbuf_elems((int)H, (int)B, bwd);
 }
@@ -74,7 +75,7 @@ void lstm_fwd_persistent(const Tensor& gx, const Tensor& bias, const Tensor& Wt,
   chk(gx, F32, "gx"); chk(bias, F32, "bias"); numel_eq(bias, 2 * 4 * H, "bias"); chk(Wt, BF, "Wt"); chk(hs, BF, "hs"); chk(cs, F32, "cs"); chk(acts, F32, "acts");
   chk(out, BF, "out"); chk(lens, I32, "lens"); chk(xbuf, at::kLong, "xbuf"); chk(err, I32, "err");
   TORCH_CHECK(lstm_persistent_grid((int)H, (int)B) > 0, "persistent LSTM: unsupported H/B (H in {64,128,256}, "
-              "grid <= 256 workgroups)");
+              "grid <= resident capacity, one workgroup per CU)");
   TORCH_CHECK(T >= 1 && T < (1 << 30), "bad T");
   numel_eq(gx, 2 * T * B * 4 * H, "gx"); numel_eq(Wt, 2 * 4 * H * H, "Wt");
   numel_eq(hs, 2 * (T + 1) * B * H, "hs"); numel_eq(cs, 2 * (T + 1) * B * H, "cs");
@@ -391,16 +392,16 @@ void ptr_rowfin(const Tensor& pv, const Tensor& target, const Tensor& rowg, cons
 }
 
 void clip_adagrad(const Tensor& w, const Tensor& acc, const Tensor& g, const Tensor& part, double lr, double max_norm,
-                  const Tensor& norm_out, const Tensor& flag) {
+                  double gscale, const Tensor& norm_out, const Tensor& flag, const OT& skip) {
   chk(w, F32, "w"); chk(acc, F32, "acc"); chk(g, F32, "g"); chk(part, F32, "part"); chk(norm_out, F32, "norm_out");
-  chk(flag, I32, "flag");
+  chk(flag, I32, "flag"); chko(skip, I32, 1, "skip");
   TORCH_CHECK(w.numel() == acc.numel() && w.numel() == g.numel(), "flat buffers differ in size");
   numel_eq(part, opt_nparts(), "part");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(acc.data_ptr()) % 16 == 0,
               "flat buffers must be 16-byte aligned");
   launch_clip_adagrad(P<float>(w), P<float>(acc), P<float>(g), w.numel(), P<float>(part), (float)lr, (float)max_norm,
-                      P<float>(norm_out), P<int>(flag), stream());
+                      (float)gscale, P<float>(norm_out), P<int>(flag), PO<int>(skip), stream());
 }
 int64_t opt_parts() { return opt_nparts(); }
 
@@ -560,6 +561,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("lstm_enc_fwd_step", &lstm_enc_fwd_step);
   m.def("lstm_enc_bwd_step", &lstm_enc_bwd_step);
   m.def("lstm_persistent_grid", &lstm_persistent_grid_op);
+  m.def("lstm_persistent_capacity", &lstm_persistent_capacity_op);
   m.def("lstm_persistent_xbuf", &lstm_persistent_xbuf_op);
   m.def("lstm_fwd_persistent", &lstm_fwd_persistent);
   m.def("lstm_bwd_persistent", &lstm_bwd_persistent);

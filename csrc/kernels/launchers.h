@@ -49,7 +49,7 @@ void launch_ptr_loss(const float* logits, const float* bias, const int* target, 
                      int B, int T, int V, hipStream_t st);
 
 void launch_clip_adagrad(float* w, float* acc, const float* g, long n, float* part, float lr, float max_norm,
-                         float* norm_out, int* flag, hipStream_t st);
+                         float gscale, float* norm_out, int* flag, const int* skip, hipStream_t st);
 int opt_nparts();
 
 void launch_final_topk(const float* logits, const float* bias, const float* pgen, const float* attn, const int* ext,
@@ -77,6 +77,7 @@ void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
                      int N, int A, int H, int E, hipStream_t st);
 int lstm_persistent_grid(int H, int B);
+int lstm_persistent_capacity(int H);
 size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd);
 void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,

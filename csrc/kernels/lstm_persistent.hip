@@ -383,11 +383,38 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
 }
 
 // ---------------------------------------------------------------------- launchers
+// Workgroups of the persistent kernels the current device keeps resident at once: one per
+// CU (launch bounds (256, 1); the occupancy query must admit at least that), times the CU
+// count the runtime reports -- not an assumed 256, so a partitioned or smaller device
+// shrinks the admissible grid instead of spinning into the hand-off timeout.
+int lstm_persistent_capacity(int H) {
+  static int cache[64][3] = {};  // [device][H/64 - 1 of {64,128,256}] -> capacity + 1
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  const int hi = H == 64 ? 0 : H == 128 ? 1 : H == 256 ? 2 : -1;
+  if (hi < 0) return 0;
+  if (cache[dev][hi]) return cache[dev][hi] - 1;
+  int cus = 0, occ = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+  hipError_t e = hipErrorInvalidValue;
+  if (H == 64) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lstm_bwd_persistent_kernel<64>, 256, 0);
+  else if (H == 128) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lstm_bwd_persistent_kernel<128>, 256, 0);
+  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lstm_bwd_persistent_kernel<256>, 256, 0);
+  int occ_f = 0;
+  hipError_t e2 = hipErrorInvalidValue;
+  if (H == 64) e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, lstm_fwd_persistent_kernel<64>, 256, 0);
+  else if (H == 128) e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, lstm_fwd_persistent_kernel<128>, 256, 0);
+  else e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, lstm_fwd_persistent_kernel<256>, 256, 0);
+  const int cap = (e == hipSuccess && e2 == hipSuccess && occ >= 1 && occ_f >= 1) ? cus : 0;
+  cache[dev][hi] = cap + 1;
+  return cap;
+}
+
 int lstm_persistent_grid(int H, int B) {
   if (H != 64 && H != 128 && H != 256) return 0;
   const int NC = H / 64, ntile = (B + 15) / 16;
   const int grid = 8 * NC * ((2 * ntile + 7) / 8);
-  return grid <= 256 ? grid : 0;  // every workgroup must be co-resident (1 per CU)
+  return grid <= lstm_persistent_capacity(H) ? grid : 0;  // every workgroup co-resident (1 per CU)
 }
 
 size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {

@@ -6,10 +6,14 @@
 // one contiguous grad buffer, which is also the DP all-reduce bucket storage), so the
 // whole optimizer is two launches with no host sync:
 //   1. sumsq:   per-block partial sums of g^2 (deterministic two-level reduction)
-//   2. adagrad: norm = sqrt(sum partials) (every block recomputes it from 1024 floats),
-//               scale = max_norm / max(norm, max_norm); g' = g*scale;
+//   2. adagrad: norm = gscale * sqrt(sum partials) (every block recomputes it from 1024
+//               floats), scale = gscale * max_norm / max(norm, max_norm); g' = g*scale;
 //               acc += g'^2; w -= lr * g' / sqrt(acc)
-// A non-finite norm skips the update (NaN guard) and sets *flag = 1.
+// gscale folds the data-parallel 1/world average of the summed gradient into the update
+// (no separate pass over the 86 MB buffer after the all-reduce).
+// A non-finite norm skips the update (NaN guard) and sets *flag = 1.  A
+// non-zero *skip word (the persistent-LSTM hand-off error, sticky) also skips it and sets
+// *flag |= 2: garbage gradients from a timed-out recurrence are never applied.
 #include "common.h"
 
 #define OPT_BLOCKS 1024
@@ -31,19 +35,21 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 __global__ __launch_bounds__(256) void adagrad_kernel(float* __restrict__ w, float* __restrict__ acc,
                                                       const float* __restrict__ g, long n,
                                                       const float* __restrict__ part, int nparts, float lr,
-                                                      float max_norm, float* __restrict__ norm_out,
-                                                      int* __restrict__ flag) {
+                                                      float max_norm, float gscale, float* __restrict__ norm_out,
+                                                      int* __restrict__ flag, const int* __restrict__ skip) {
   __shared__ float red[8];
   float s = 0.f;
   for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
   s = block_sum<256>(s, red);
-  const float norm = sqrtf(s);
+  const float norm = gscale * sqrtf(s);
+  const bool skipped = skip != nullptr && *skip != 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     norm_out[0] = norm;
-    if (!isfinite(norm)) flag[0] = 1;
+    if (!isfinite(norm)) flag[0] |= 1;
+    if (skipped) flag[0] |= 2;
   }
-  if (!isfinite(norm)) return;
-  const float scale = max_norm > 0.f ? max_norm / fmaxf(norm, max_norm) : 1.0f;
+  if (!isfinite(norm) || skipped) return;
+  const float scale = gscale * (max_norm > 0.f ? max_norm / fmaxf(norm, max_norm) : 1.0f);
   const long n4 = n / 4;
   float4* w4 = reinterpret_cast<float4*>(w);
   float4* a4 = reinterpret_cast<float4*>(acc);
@@ -65,9 +71,9 @@ __global__ __launch_bounds__(256) void adagrad_kernel(float* __restrict__ w, flo
 }
 
 void launch_clip_adagrad(float* w, float* acc, const float* g, long n, float* part, float lr, float max_norm,
-                         float* norm_out, int* flag, hipStream_t st) {
+                         float gscale, float* norm_out, int* flag, const int* skip, hipStream_t st) {
   hipLaunchKernelGGL(sumsq_kernel, dim3(OPT_BLOCKS), dim3(256), 0, st, g, n, part);
   hipLaunchKernelGGL(adagrad_kernel, dim3(OPT_BLOCKS), dim3(256), 0, st, w, acc, g, n, part, OPT_BLOCKS, lr, max_norm,
-                     norm_out, flag);
+                     gscale, norm_out, flag, skip);
 }
 int opt_nparts() { return OPT_BLOCKS; }

@@ -36,6 +36,18 @@ def _reducer_worker(rank, world, port, q):
     torch.distributed.destroy_process_group()
 
 
+def _reducer_bf16_worker(rank, world, port, q):
+    info = _init(rank, world, port)
+    from textsummarization_on_flink_amd.parallel.dist import GradAllReducer
+    g = torch.arange(100, dtype=torch.float32) * (rank + 1)
+    red = GradAllReducer(g, info, bounds=[30, 70], compress="bf16", average=False)
+    red.bucket_ready(0)
+    red.wait_issued()  # bucket 0 complete; its fp32 copy-back happens in __call__
+    red()
+    q.put((rank, g.tolist()))
+    torch.distributed.destroy_process_group()
+
+
 def _train_worker(rank, world, port, q, batches_state):
     info = _init(rank, world, port)
     from textsummarization_on_flink_amd.train.cpu_trainer import CpuTrainer
@@ -65,6 +77,14 @@ def test_bucketed_async_allreduce_averages():
     res = _spawn(_reducer_worker, 2)
     want = [float(i) * 1.5 for i in range(100)]
     assert res[0][0] == pytest.approx(want) and res[1][0] == pytest.approx(want)
+
+
+def test_bf16_compressed_allreduce_sums():
+    """bf16 wire format: the fp32 buffer receives the (bf16-rounded) SUM; averaging is left
+    to the optimizer (average=False, as the GPU trainer uses it)."""
+    res = _spawn(_reducer_bf16_worker, 2)
+    want = [float(torch.tensor(3.0 * i).bfloat16()) for i in range(100)]
+    assert res[0][0] == pytest.approx(want, rel=1e-2) and res[1][0] == res[0][0]
 
 
 def test_dp2_matches_dp1_on_concatenated_batch():

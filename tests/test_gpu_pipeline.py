@@ -23,12 +23,14 @@ def _flags(tmp, d, vp, *extra, split="train"):
 
 def test_cli_train_resume_decode_on_gpu(tmp_path):
     d, vp, _ = make_dataset(str(tmp_path), per_file=12, corpus=gpu_corpus())
-    assert cli.main(_flags(tmp_path, d, vp, "--mode=train", "--num_steps=3")) == 0
+    assert cli.main(_flags(tmp_path, d, vp, "--mode=train", "--num_steps=3", "--check_every=1")) == 0
+    # default cadence: the host reads the flags / loss every check_every=10 steps and after the last
     assert cli.main(_flags(tmp_path, d, vp, "--mode=train", "--num_steps=2")) == 0
     assert ckpt.latest_checkpoint(f"{tmp_path}/log/exp/train").endswith("model.ckpt-5")
     import json
     recs = [json.loads(x) for x in open(f"{tmp_path}/log/exp/metrics_train.jsonl")]
-    assert [r["step"] for r in recs] == [1, 2, 3, 4, 5] and all(r["loss"] > 0 for r in recs)
+    assert [r["step"] for r in recs] == [1, 2, 3, 5] and all(r["loss"] > 0 for r in recs)
+    assert [r["steps"] for r in recs] == [1, 1, 1, 2]
     assert cli.main(_flags(tmp_path, d, vp, "--mode=decode", "--single_pass=1", split="test")) == 0
     dec = glob.glob(f"{tmp_path}/log/exp/decode_*")
     assert len(dec) == 1

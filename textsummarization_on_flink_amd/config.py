@@ -83,6 +83,9 @@ class HParams:
     profile_phases: bool = False   # per-phase step timing (HIP events) into the metrics JSONL
     flink_tokenize_article: bool = False  # quirk 4: the Flink path whitespace-splits the raw article
     log_file: str = ""             # rotating log file, 100 MB x 20 (log4j2.xml); one file per rank
+    check_every: int = 10          # host reads loss / NaN / LSTM-error flags every N steps (1 = every step)
+    grad_compress: str = "none"    # DP gradient all-reduce wire format: none (fp32) | bf16
+    loader_workers: int = 0        # >0: Example/Batch construction in N worker processes (pinned packs)
 
     # ------------------------------------------------------------------ helpers
     def replace(self, **kw) -> "HParams":

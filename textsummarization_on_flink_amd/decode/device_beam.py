@@ -361,4 +361,6 @@ class DeviceBeamDecoder:
         if batch.enc_batch.shape[0] != self.Na:
             raise ValueError(f"batch has {batch.enc_batch.shape[0]} rows, engine expects {self.Na}")
         self.run(batch)
-        return self.results(int(batch.valid.sum()))
+        hyps = self.results(int(batch.valid.sum()))  # synchronises
+        self.eng.check_lstm_err()  # the encoder ran the persistent LSTM: never emit garbage summaries
+        return hyps

@@ -45,6 +45,10 @@ OUT_M, OUT_B = f"{DEC}/AttnOutputProjection/Linear/Matrix", f"{DEC}/AttnOutputPr
 OW, OV = f"{P}/output_projection/w", f"{P}/output_projection/v"
 
 
+class LstmHandoffError(RuntimeError):
+    """A persistent-LSTM launch timed out in a hand-off (a workgroup was not co-resident)."""
+
+
 def enc_k(layer, d):
     return f"{enc_prefix(layer)}/bidirectional_rnn/{d}/lstm_cell/kernel"
 
@@ -103,6 +107,7 @@ class HipPointerGenerator:
         if T > 2048:
             raise ValueError("max_enc_steps > 2048 not supported by the attention kernels")
         self.k = _ops()
+        self.grad_scale = 1.0  # set to 1/world by a data-parallel trainer (see optimizer_step)
         self.nchunk = int(self.k.attn_chunks(T))
         # the output-projection weight gradient runs on a side stream, overlapped with the
         # decoder backward loop (joined at the end of backward_mid) when TSAMD_OVERLAP_DW=1.
@@ -231,6 +236,14 @@ class HipPointerGenerator:
         w["gnorm"] = z(1)
         w["nan_flag"] = z(1, dt=torch.int32)
         self.w = w
+
+    def check_lstm_err(self) -> None:
+        """Host sync: raise if a persistent-LSTM hand-off timed out in any launch since the
+        engine was built.  The word is sticky: those results were garbage, the optimizer
+        kernel skipped the update, and eval / decode must not report them."""
+        if int(self.w["lstm_err"].item()):
+            raise LstmHandoffError("persistent LSTM hand-off timed out (a workgroup was not co-resident); "
+                                   "results of that launch were discarded -- set TSAMD_LSTM_PERSISTENT=0")
 
     # ------------------------------------------------------------------ weights
     def pack(self):
@@ -682,9 +695,12 @@ class HipPointerGenerator:
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_step(self):
+        """Fused clip + Adagrad over the flat buffers, then the bf16 repack.  ``grad_scale``
+        (1/world under data parallelism) averages the all-reduced gradient sum inside the
+        optimizer kernel; a set ``lstm_err`` word (sticky) skips the update on device."""
         hps, p, w = self.hps, self.p, self.w
-        self.k.clip_adagrad(p.flat, p.accum, p.grad, w["opt_part"], hps.lr, hps.max_grad_norm, w["gnorm"],
-                            w["nan_flag"])
+        self.k.clip_adagrad(p.flat, p.accum, p.grad, w["opt_part"], hps.lr, hps.max_grad_norm, self.grad_scale,
+                            w["gnorm"], w["nan_flag"], w["lstm_err"])
         self.pack()
 
     def train_step(self, allreduce=None):

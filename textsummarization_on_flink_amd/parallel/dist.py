@@ -74,17 +74,26 @@ def broadcast_params(flat: torch.Tensor, info: DistInfo) -> None:
 
 
 class GradAllReducer:
-    """Bucketed average of a flat gradient buffer.
+    """Bucketed sum (or average) of a flat gradient buffer.
 
     ``bounds`` (element offsets) defines the buckets explicitly -- the trainer aligns them
     with the phases of its backward so bucket i can be all-reduced while the next phase
     computes; otherwise the buffer is cut into ``bucket_mb`` pieces.  ``bucket_ready(i)``
     issues bucket i's all-reduce asynchronously (RCCL runs it on its own stream after the
-    work already queued on the current stream), ``__call__`` issues the rest, waits, and
-    averages."""
+    work already queued on the current stream), ``__call__`` issues the rest and waits.
+
+    * ``average=True`` scales the sum by 1/world here; the GPU trainer passes False and
+      folds the 1/world into its optimizer kernel instead (one pass over the buffer less).
+    * ``compress="bf16"`` all-reduces a bf16 copy of each bucket (half the xGMI bytes; the
+      fp32 gradient buffer and fp32 master weights are kept, only the wire format and the
+      ring's partial sums are bf16).  Opt-in: summing 8 ranks in bf16 costs ~3 significant
+      bits on each element of the averaged gradient.
+    * ``wait_issued()`` makes the current stream wait for every all-reduce issued so far
+      (a device-side wait for RCCL, no host block): the trainer calls it before a launch
+      that must not share the GPU with RCCL kernels (the persistent LSTM at full grid)."""
 
     def __init__(self, grad: torch.Tensor, info: DistInfo, bucket_mb: float = 32.0, overlap: bool = False,
-                 bounds: Optional[List[int]] = None):
+                 bounds: Optional[List[int]] = None, average: bool = True, compress: Optional[str] = None):
         self.info = info
         self.grad = grad
         n = grad.numel()
@@ -94,7 +103,13 @@ class GradAllReducer:
         else:
             per = max(1, int(bucket_mb * 1024 * 1024 // grad.element_size()))
             self.buckets = [grad[i:min(n, i + per)] for i in range(0, n, per)]
+        if compress not in (None, "none", "bf16"):
+            raise ValueError(f"unknown gradient compression {compress!r} (none | bf16)")
+        self.compress = compress if compress == "bf16" else None
+        self._wire = ([torch.empty(b.numel(), dtype=torch.bfloat16, device=grad.device) for b in self.buckets]
+                      if (self.compress and info.enabled) else None)
         self.overlap = overlap
+        self.average = average
         self._pending = []
         self._issued = 0
 
@@ -103,20 +118,30 @@ class GradAllReducer:
         if not self.info.enabled:
             return
         b = self.buckets[idx]
-        self._pending.append(dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True))
+        if self._wire is not None:
+            self._wire[idx].copy_(b)  # on the producing stream, so the collective sees final values
+            b = self._wire[idx]
+        self._pending.append((idx, dist.all_reduce(b, op=dist.ReduceOp.SUM, async_op=True)))
         self._issued = max(self._issued, idx + 1)
 
+    def wait_issued(self):
+        for _, w in self._pending:
+            w.wait()
+
     def __call__(self, grad: Optional[torch.Tensor] = None):
-        """All-reduce every bucket not yet issued, wait, and average."""
+        """All-reduce every bucket not yet issued, wait, and (``average``) divide by world."""
         if not self.info.enabled:
             return
         for i in range(self._issued, len(self.buckets)):
             self.bucket_ready(i)
-        for w in self._pending:
+        for idx, w in self._pending:
             w.wait()
+            if self._wire is not None:
+                self.buckets[idx].copy_(self._wire[idx])
         self._pending = []
         self._issued = 0
-        self.grad.mul_(1.0 / self.info.world)
+        if self.average:
+            self.grad.mul_(1.0 / self.info.world)
 
 
 def all_reduce_scalar(x: float, info: DistInfo, op="sum", device=None) -> float:

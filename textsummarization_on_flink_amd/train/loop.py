@@ -109,39 +109,62 @@ def _fault(hps, trainer, step: int, info: DistInfo):
 
 def run_training(trainer, batcher, hps, info: Optional[DistInfo] = None, saver: Optional[ckpt.Saver] = None,
                  metrics: Optional[MetricsLogger] = None, num_steps: Optional[int] = None,
-                 save_model_secs: Optional[float] = None, log_every: int = 1) -> Dict[str, float]:
-    """Train until ``num_steps`` more steps (0/None = until the batcher ends)."""
+                 save_model_secs: Optional[float] = None, log_every: Optional[int] = None) -> Dict[str, float]:
+    """Train until ``num_steps`` more steps (0/None = until the batcher ends).
+
+    The host never waits on the GPU between checks: a GPU trainer (``trainer.host_sync_free``)
+    reads the loss, the NaN-guard flag and the persistent-LSTM error word only every
+    ``hps.check_every`` steps (and after the last step).  The flags are sticky, so a
+    non-finite step anywhere in the window stops training at the check ("Loss is not
+    finite. Stopping.", ``train.py:107-108``); the device NaN guard has already skipped that
+    step's update.  The CPU oracle trainer is synchronous anyway and checks every step.
+    Loss lines and metrics are emitted at checks (``log_every`` > 0 enables them); tokens/s
+    is measured over the whole window, and the token count is all-reduced once per check."""
     info = info or DistInfo()
     num_steps = hps.num_steps if num_steps is None else num_steps
     save_model_secs = hps.save_model_secs if save_model_secs is None else save_model_secs
+    log_every = getattr(hps, "log_every", 1) if log_every is None else log_every
+    check_every = max(1, int(getattr(hps, "check_every", 1))) if getattr(trainer, "host_sync_free", False) else 1
     start = trainer.global_step
     last_save = time.time()
     watch = NonFiniteWatch(trainer) if getattr(hps, "debug", False) and hasattr(trainer, "named_debug_tensors") \
         else None
     vals: Dict[str, float] = {}
+    win_t0, win_tokens, win_steps = time.time(), 0.0, 0
+    out = None
+
+    def check():
+        nonlocal vals, win_t0, win_tokens, win_steps
+        vals = trainer.check_finite(out)  # host sync; raises "Loss is not finite. Stopping."
+        dt = time.time() - win_t0
+        toks = all_reduce_scalar(win_tokens, info)
+        if log_every:
+            log.info("step %d: seconds for training step: %.3f loss: %f%s", trainer.global_step, dt / win_steps,
+                     vals["loss"], f" coverage_loss: {vals['coverage_loss']:f}" if "coverage_loss" in vals else "")
+            if metrics:
+                extra = trainer.phase_ms() if getattr(trainer, "timing", False) else {}
+                metrics.log(step=trainer.global_step, step_ms=dt * 1e3 / win_steps, steps=win_steps,
+                            tokens_per_sec=toks / max(dt, 1e-9), **extra, **vals)
+        win_t0, win_tokens, win_steps = time.time(), 0.0, 0
+
     try:
         while not num_steps or trainer.global_step - start < num_steps:
             batch = batcher.next_batch()
             if batch is None:
                 break
             _fault(hps, trainer, trainer.global_step - start, info)
-            t0 = time.time()
             out = trainer.step(batch)
+            win_tokens += float(batch.num_tokens())
+            win_steps += 1
             if watch is not None and watch.check(trainer.global_step):
                 raise NonFiniteLossError("Loss is not finite. Stopping. (--debug: has_inf_or_nan tripped)")
-            vals = trainer.check_finite(out)  # host sync; raises "Loss is not finite. Stopping."
-            dt = time.time() - t0
-            toks = all_reduce_scalar(float(batch.num_tokens()), info)
-            if log_every and (trainer.global_step % log_every == 0):
-                log.info("step %d: seconds for training step: %.3f loss: %f%s", trainer.global_step, dt,
-                         vals["loss"], f" coverage_loss: {vals['coverage_loss']:f}" if "coverage_loss" in vals else "")
-            if metrics:
-                extra = trainer.phase_ms() if getattr(trainer, "timing", False) else {}
-                metrics.log(step=trainer.global_step, step_ms=dt * 1e3, tokens_per_sec=toks / max(dt, 1e-9),
-                            **extra, **vals)
+            if trainer.global_step % check_every == 0:
+                check()
             if saver and info.is_chief and save_model_secs and time.time() - last_save >= save_model_secs:
                 saver.save(trainer.params, trainer.global_step)
                 last_save = time.time()
+        if win_steps:
+            check()
     except KeyboardInterrupt:
         log.info("Caught keyboard interrupt on worker. Stopping supervisor...")
     finally:

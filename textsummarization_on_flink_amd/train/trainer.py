@@ -8,8 +8,15 @@ Replaces ``FlinkTrainer`` / ``run_training`` (``train.py:57-125``,
   * the flat gradient is all-reduced over RCCL between the two graphs (bucketed), then
     the optimizer graph (grad average, fused clip+Adagrad, bf16 repack) replays;
   * ``nan_guard``: a non-finite gradient norm skips the update on device (flag word);
-    the host checks the flag and the loss every ``check_every`` steps and raises like the
-    reference ("Loss is not finite. Stopping.", ``train.py:107-108``);
+    the training loop reads the flag and the loss every ``hps.check_every`` steps
+    (``check_finite``) and raises like the reference ("Loss is not finite. Stopping.",
+    ``train.py:107-108``); between checks the host never waits on the GPU;
+  * persistent-LSTM safety under DP: the hand-off kernels need all their workgroups
+    resident.  When the launch grid leaves fewer than ``LSTM_RCCL_RESERVE_CUS`` CUs free
+    and gradients are all-reduced, the encoder-backward graph is ordered behind the
+    in-flight bucket all-reduces (a device-side stream wait), so no RCCL kernel shares the
+    GPU with the persistent launch; a hand-off timeout anyway sets the sticky ``lstm_err``
+    word, which makes the optimizer kernel skip the update and ``check_finite`` raise;
   * eval mode is the same engine with forward only.
 """
 from __future__ import annotations
@@ -22,7 +29,7 @@ from typing import Callable, Dict, Optional
 import torch
 
 from ..models.params import FlatParams, build_params
-from ..models.pointer_generator import HipPointerGenerator
+from ..models.pointer_generator import HipPointerGenerator, LstmHandoffError  # noqa: F401
 from ..parallel.dist import DistInfo, GradAllReducer, broadcast_params
 
 log = logging.getLogger(__name__)
@@ -30,6 +37,14 @@ log = logging.getLogger(__name__)
 
 class NonFiniteLossError(RuntimeError):
     pass
+
+
+# CUs kept free of persistent-LSTM workgroups before RCCL kernels may overlap the launch
+LSTM_RCCL_RESERVE_CUS = 64
+
+
+def check_lstm_err(engine) -> None:
+    engine.check_lstm_err()
 
 
 class GraphTrainer:
@@ -50,14 +65,24 @@ class GraphTrainer:
             broadcast_params(params.accum, self.info)
         self.engine = HipPointerGenerator(hps, vsize, params, B=B, T=T)
         # buckets = backward phases: output_projection | decoder+attention | encoder+embedding;
-        # each is all-reduced while the following phase computes (RCCL over xGMI)
+        # each is all-reduced while the following phase computes (RCCL over xGMI); the
+        # 1/world average happens inside the optimizer kernel
         self.reducer = GradAllReducer(params.grad, self.info, bucket_mb=bucket_mb,
-                                      bounds=self.engine.phase_bounds())
+                                      bounds=self.engine.phase_bounds(), average=False,
+                                      compress=getattr(hps, "grad_compress", "none"))
+        self.engine.grad_scale = 1.0 / self.info.world
+        eng = self.engine
+        self.lstm_exclusive = False
+        if self.info.enabled and eng.persistent_lstm:
+            grid = int(eng.k.lstm_persistent_grid(eng.H, eng.B))
+            cap = int(eng.k.lstm_persistent_capacity(eng.H))
+            self.lstm_exclusive = grid > cap - LSTM_RCCL_RESERVE_CUS
         self.use_graph = use_graph
         self.g_fb = None
         self.g_opt = None
         self.out = None
         self.global_step = 0
+        self.host_sync_free = True  # step() never waits on the GPU; loops check every hps.check_every steps
         self.poison_next = False  # fault injection: NaN gradient on the next step (exercises the NaN guard)
         self.timing = False       # per-phase HIP-event timing (phase_ms)
         self._ev = None
@@ -127,6 +152,8 @@ class GraphTrainer:
                 ev[0].record()
             ng = len(self.g_fb)
             for i, g in enumerate(self.g_fb):
+                if i == ng - 1 and self.lstm_exclusive:
+                    self.reducer.wait_issued()  # no RCCL kernel beside the full-grid persistent BPTT
                 g.replay()
                 if ev:
                     ev[i + 1].record()
@@ -175,12 +202,12 @@ class GraphTrainer:
             self.poison_next = False
 
     def check_finite(self, out) -> Dict[str, float]:
-        """Host sync: raise on non-finite loss / skipped update (NaN guard)."""
+        """Host sync: raise on a persistent-LSTM hand-off error, a non-finite loss or an
+        update skipped by the NaN guard (the flags are sticky, so a check every
+        ``check_every`` steps sees every earlier step)."""
         vals = {k: float(v) for k, v in out.items()}
-        if int(self.engine.w["lstm_err"].item()):
-            raise RuntimeError("persistent LSTM hand-off timed out (a workgroup was not co-resident); "
-                               "set TSAMD_LSTM_PERSISTENT=0")
-        if not all(math.isfinite(v) for v in vals.values()) or int(self.engine.w["nan_flag"].item()):
+        check_lstm_err(self.engine)
+        if not all(math.isfinite(v) for v in vals.values()) or (int(self.engine.w["nan_flag"].item()) & 1):
             raise NonFiniteLossError("Loss is not finite. Stopping.")
         vals["global_norm"] = float(self.engine.w["gnorm"].item())
         return vals
@@ -199,4 +226,6 @@ class GraphTrainer:
     def eval_step(self, batch) -> Dict[str, float]:
         self.engine.set_batch(batch)
         out = self.engine.forward(need_grad=False)
-        return {k: float(v) for k, v in out.items()}
+        vals = {k: float(v) for k, v in out.items()}
+        check_lstm_err(self.engine)  # never report (or save as bestmodel) a loss from a failed launch
+        return vals
