@@ -160,6 +160,40 @@ void attn_bwd_tanh(const Tensor& F, const Tensor& s, const Tensor& v, const OT& 
                        PO<float>(dcov_out), B, T, A, stream());
 }
 
+// one workgroup per row (attention_row.hip): forward score + softmax + coverage + context in
+// one launch, backward step without atomics (ds stored, not accumulated)
+bool attn_row_ok(int64_t A, int64_t T) { return attn_row_supported((int)A, (int)T); }
+void attn_fwd_row(const Tensor& F, const Tensor& E, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
+                  const Tensor& lens, const Tensor& a_out, const OT& cov_out, const OT& covloss, const Tensor& ctx,
+                  const OT& ctx_bf, int64_t B, int64_t T, int64_t A) {
+  chk(F, BF, "F"); chk(E, BF, "E"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens");
+  chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
+  TORCH_CHECK(attn_row_supported((int)A, (int)T), "row attention needs A in {512, 1024} and T <= 2048");
+  numel_eq(F, B * T * A, "F"); numel_eq(E, B * T * A, "E"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v");
+  numel_eq(lens, B, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx");
+  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out");
+  chko(covloss, F32, B, "covloss"); chko(ctx_bf, BF, B * A, "ctx_bf");
+  launch_attn_fwd_row(P<bf16>(F), P<bf16>(E), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens),
+                      P<float>(a_out), PO<float>(cov_out), PO<float>(covloss), P<float>(ctx), PO<bf16>(ctx_bf), B, T, A,
+                      stream());
+}
+void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
+                  const Tensor& a, const Tensor& dctx, const Tensor& ctx, const OT& Ga, const OT& dcov_next,
+                  const OT& gcl, const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out,
+                  int64_t B, int64_t T, int64_t A) {
+  chk(E, BF, "E"); chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(dctx, F32, "dctx");
+  chk(ctx, F32, "ctx"); chk(lens, I32, "lens"); chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
+  TORCH_CHECK(attn_row_supported((int)A, (int)T), "row attention needs A in {512, 1024} and T <= 2048");
+  numel_eq(E, B * T * A, "E"); numel_eq(F, B * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v");
+  numel_eq(a, B * T, "a"); numel_eq(dctx, B * A, "dctx"); numel_eq(ctx, B * A, "ctx"); numel_eq(lens, B, "lens");
+  numel_eq(de_out, B * T, "de_out"); numel_eq(ds, B * A, "ds");
+  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(Ga, F32, B * T, "Ga");
+  chko(dcov_next, F32, B * T, "dcov_next"); chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
+  launch_attn_bwd_row(P<bf16>(E), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
+                      P<float>(dctx), P<float>(ctx), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl),
+                      P<int>(lens), P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, stream());
+}
+
 void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                    const Tensor& a, const Tensor& dctx, const Tensor& ctx, const OT& Ga, const OT& dcov_next,
                    const OT& gcl, const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out,
@@ -570,6 +604,9 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("attn_bwd_da", &attn_bwd_da);
   m.def("attn_bwd_tanh", &attn_bwd_tanh);
   m.def("attn_bwd_step", &attn_bwd_step);
+  m.def("attn_row_ok", &attn_row_ok);
+  m.def("attn_fwd_row", &attn_fwd_row);
+  m.def("attn_bwd_row", &attn_bwd_row);
   m.def("attn_bwd_feat", &attn_bwd_feat);
   m.def("attn_chunks", &attn_chunks);
   m.def("dec_cell_fwd", &dec_cell_fwd);

@@ -1,0 +1,372 @@
+// Row-resident Bahdanau attention with coverage: ONE workgroup per batch row (article) per
+// decoder step (reference attention_decoder.py:79-129,
+// model.py:463-480).  Same math as attention.hip, different decomposition:
+//
+//   * a workgroup of 8-16 waves (one workgroup per CU, row_waves()) owns row b
+//     and streams its encoder rows F_i = (W_h enc_out)_i and E_i = enc_out_i (1 KB each at
+//     A = 512) exactly once; at B = 256 the 256 rows are the 256 CUs, each pulling ~24 GB/s,
+//     which is the HBM rate of the chip;
+//   * the waves take groups of 4 positions round-robin (wave w: groups w, w + NW, ...); the
+//     next group's rows are loaded before the current group is computed (double-buffered
+//     registers), so 96-128 KB are in flight per CU;
+//   * every row-level reduction (softmax statistics, S = sum_j a_j da_j, the 512-wide ds
+//     and ctx vectors) stays inside the workgroup: no atomics, no partial buffers, no
+//     pre-zeroed outputs, and one launch per step instead of two (score + softmax/context)
+//     in the forward;
+//   * lanes hold 8 features each (A = 512 * NK; NK = 1 at hidden 256, 2 at hidden 512), the
+//     per-position dot products over the feature axis are reduced with the 4-position
+//     butterfly (bfly4: the lanes of position q end up holding its total).
+//
+// forward (attn_fwd_row):  one pass with an online softmax per wave (running max m_w, sum
+//   l_w and the rescaled context partial over the wave's positions, as in flash
+//   attention): e_i = sum_k v_k tanh(F_ik + s_k + w_k cov_i) from F_i, then
+//   ctx += exp(e_i - m) E_i from E_i in the same pass; the waves' partials are merged in LDS,
+//   then a = softmax(e) (scores kept in LDS), cov' = cov + a, covloss = sum min(a, cov).
+// backward (attn_bwd_row): da_i = r_i + dctx . E_i, de_i = a_i (da_i - S),
+//   ds_k = sum_i de_i v_k sech2(u_ik), dcov_i = dcov_next_i + g [a_i > cov_i] +
+//   de_i sum_k v_k w_k sech2(u_ik)  (S = sum_j a_j r_j + dctx . ctx, see attention.hip).
+#include "attn_common.h"
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kRowMaxT = 2048;
+// waves per workgroup: as many as the double-buffered rows leave registers for --
+// forward at hidden 256: 16 (<= 128 VGPRs); backward at hidden 256: 12 (<= 168 VGPRs, the
+// extra dctx / per-feature state); hidden 512 (16 features per lane): 8 (<= 256 VGPRs)
+template <int NK, bool BWD>
+constexpr int row_waves() { return NK == 1 ? (BWD ? 12 : 16) : 8; }
+
+template <int NK>
+struct Rows {
+  u32x4 x[NK][4];  // 4 positions x NK 16-byte feature chunks of one tensor
+};
+
+template <int NK>
+__device__ __forceinline__ void load_rows(Rows<NK>& r, const bf16* base, int p0, int len, int lane) {
+  constexpr int A = 512 * NK;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int p = min(p0 + q, len - 1);
+#pragma unroll
+    for (int kb = 0; kb < NK; ++kb)
+      r.x[kb][q] = __builtin_bit_cast(u32x4, ld8(base + (size_t)p * A + kb * 512 + lane * 8));
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ forward
+template <int NK, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
+    const bf16* __restrict__ F, const bf16* __restrict__ E, const float* __restrict__ s,
+    const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
+    const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
+    float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T) {
+  constexpr int A = 512 * NK, NT = NW * 64;
+  __shared__ float es[kRowMaxT];
+  __shared__ float part[NW][A];
+  __shared__ float wm[NW], wl[NW], red[NW];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int len = lens[b];
+  const size_t rb = (size_t)b * T;
+  const bf16* Fb = F + (size_t)b * T * A;
+  const bf16* Eb = E + (size_t)b * T * A;
+  const int ngrp = (len + 3) >> 2;
+  const int qm = lane >> 4;  // the position (within a group) whose total this lane's 16-lane group holds
+  const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
+  Rows<NK> fA, eA, fB, eB;
+  float cA = 0.f, cB = 0.f;
+  auto load = [&](int grp, Rows<NK>& f, Rows<NK>& e, float& c) {
+    load_rows<NK>(f, Fb, 4 * grp, len, lane);
+    load_rows<NK>(e, Eb, 4 * grp, len, lane);
+    const int p = min(4 * grp + qm, len - 1);
+    c = cov ? cov[rb + p] : 0.f;
+  };
+  if (wid < ngrp) load(wid, fA, eA, cA);
+  // per-lane feature parameters, pre-scaled for the r-form (attn_common.h)
+  f32x2 s2[NK][4], w2[NK][4], v2[NK][4], acc[NK][4];
+  float vsum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) {
+    const int k0 = kb * 512 + lane * 8;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      const float2 sv = *reinterpret_cast<const float2*>(s + (size_t)b * A + k0 + 2 * jp);
+      const float2 vv = *reinterpret_cast<const float2*>(v + k0 + 2 * jp);
+      const float2 wv = wc ? *reinterpret_cast<const float2*>(wc + k0 + 2 * jp) : make_float2(0.f, 0.f);
+      s2[kb][jp] = f32x2{sv.x, sv.y} * K2LOG2E;
+      w2[kb][jp] = f32x2{wv.x, wv.y} * K2LOG2E;
+      v2[kb][jp] = f32x2{vv.x, vv.y};
+      acc[kb][jp] = f32x2{0.f, 0.f};
+      vsum += vv.x + vv.y;
+    }
+  }
+  float m_w = -INFINITY, l_w = 0.f;
+  auto compute = [&](int grp, const Rows<NK>& f, const Rows<NK>& e, float c_l) {
+    // scores of the group's 4 positions: e = sum_k v_k - 2 sum_k v_k r_k
+    float pd[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float c = rdlane(c_l, 16 * q);
+      f32x2 d2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          d2 = fma2(v2[kb][jp], rsig2(y), d2);
+        }
+      pd[q] = vsum - 2.0f * (d2.x + d2.y);
+    }
+    float eq = bfly4(pd, b5, b4);
+    const int p = 4 * grp + qm;
+    if (p >= len) eq = -INFINITY;
+    if ((lane & 15) == 0 && p < len) es[p] = eq;
+    const float e0 = rdlane(eq, 0), e1 = rdlane(eq, 16), e2 = rdlane(eq, 32), e3 = rdlane(eq, 48);
+    const float mn = fmaxf(m_w, fmaxf(fmaxf(e0, e1), fmaxf(e2, e3)));  // e0 is always valid (p0 < len)
+    const float sc = m_w == -INFINITY ? 0.f : fexp(m_w - mn);
+    const float p0 = fexp(e0 - mn), p1 = fexp(e1 - mn), p2 = fexp(e2 - mn), p3 = fexp(e3 - mn);
+    l_w = l_w * sc + ((p0 + p1) + (p2 + p3));
+#pragma unroll
+    for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        f32x2 a2 = acc[kb][jp] * sc;
+        a2 = fma2(bf2pair(e.x[kb][0][jp]), splat2(p0), a2);
+        a2 = fma2(bf2pair(e.x[kb][1][jp]), splat2(p1), a2);
+        a2 = fma2(bf2pair(e.x[kb][2][jp]), splat2(p2), a2);
+        acc[kb][jp] = fma2(bf2pair(e.x[kb][3][jp]), splat2(p3), a2);
+      }
+    m_w = mn;
+  };
+  // double-buffered sweep: group g + NW's rows are in flight while group g is computed
+  for (int g = wid; g < ngrp;) {
+    const int g1 = g + NW;
+    if (g1 < ngrp) load(g1, fB, eB, cB);
+    compute(g, fA, eA, cA);
+    if (g1 >= ngrp) break;
+    const int g2 = g1 + NW;
+    if (g2 < ngrp) load(g2, fA, eA, cA);
+    compute(g1, fB, eB, cB);
+    g = g2;
+  }
+  // merge the waves' online-softmax partials
+  if (lane == 0) {
+    wm[wid] = m_w;
+    wl[wid] = l_w;
+  }
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp)
+      *reinterpret_cast<float2*>(&part[wid][kb * 512 + lane * 8 + 2 * jp]) =
+          make_float2(acc[kb][jp].x, acc[kb][jp].y);
+  __syncthreads();
+  float m = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) m = fmaxf(m, wm[w]);
+  float L = 0.f, wsc[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    wsc[w] = wm[w] == -INFINITY ? 0.f : fexp(wm[w] - m);
+    L += wl[w] * wsc[w];
+  }
+  const float invL = 1.0f / L;
+  for (int k = tid; k < A; k += NT) {
+    float c = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) c += part[w][k] * wsc[w];
+    c *= invL;
+    ctx[(size_t)b * A + k] = c;
+    if (ctx_bf) ctx_bf[(size_t)b * A + k] = f2bf(c);
+  }
+  float cl = 0.f;
+  for (int i = tid; i < T; i += NT) {
+    const float a = i < len ? fexp(es[i] - m) * invL : 0.f;
+    a_out[rb + i] = a;
+    if (cov_out) {
+      const float c = cov ? cov[rb + i] : 0.f;
+      cov_out[rb + i] = c + a;
+      cl += fminf(a, c);
+    }
+  }
+  if (covloss) {
+    cl = block_sum<NT>(cl, red);
+    if (tid == 0) covloss[b] = cl;
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+template <int NK, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
+    const bf16* __restrict__ E, const bf16* __restrict__ F, const float* __restrict__ s,
+    const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
+    const float* __restrict__ a, const float* __restrict__ dctx, const float* __restrict__ ctx,
+    const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
+    const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
+    float* __restrict__ dcov_out, int T) {
+  constexpr int A = 512 * NK, NT = NW * 64;
+  __shared__ float part[NW][A];
+  __shared__ float red[NW];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int len = lens[b];
+  const size_t rb = (size_t)b * T;
+  const float g = gcl ? gcl[b] : 0.f;
+  const bf16* Eb = E + (size_t)b * T * A;
+  const bf16* Fb = F + (size_t)b * T * A;
+  const int ngrp = (len + 3) >> 2;
+  const int qm = lane >> 4;
+  const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
+  struct Scal {
+    float a, r, c, dn;
+  };
+  Rows<NK> eA, fA, eB, fB;
+  Scal xA{}, xB{};
+  auto load = [&](int grp, Rows<NK>& e, Rows<NK>& f, Scal& x) {
+    load_rows<NK>(e, Eb, 4 * grp, len, lane);
+    load_rows<NK>(f, Fb, 4 * grp, len, lane);
+    const int p = 4 * grp + qm;
+    const size_t ix = rb + min(p, len - 1);
+    x.a = a[ix];
+    x.c = cov ? cov[ix] : 0.f;
+    x.dn = dcov_next ? dcov_next[ix] : 0.f;
+    x.r = (Ga ? Ga[ix] : 0.f) + x.dn + ((gcl && x.a <= x.c) ? g : 0.f);
+  };
+  if (wid < ngrp) load(wid, eA, fA, xA);
+  float dk[NK][8];
+  f32x2 s2[NK][4], w2[NK][4], v4w[NK][4], acc[NK][4];
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) {
+    const int k0 = kb * 512 + lane * 8;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      const float2 sv = *reinterpret_cast<const float2*>(s + (size_t)b * A + k0 + 2 * jp);
+      const float2 vv = *reinterpret_cast<const float2*>(v + k0 + 2 * jp);
+      const float2 wv = wc ? *reinterpret_cast<const float2*>(wc + k0 + 2 * jp) : make_float2(0.f, 0.f);
+      const float2 dv = *reinterpret_cast<const float2*>(dctx + (size_t)b * A + k0 + 2 * jp);
+      s2[kb][jp] = f32x2{sv.x, sv.y} * K2LOG2E;
+      w2[kb][jp] = f32x2{wv.x, wv.y} * K2LOG2E;
+      v4w[kb][jp] = f32x2{4.f * vv.x * wv.x, 4.f * vv.y * wv.y};
+      dk[kb][2 * jp] = dv.x;
+      dk[kb][2 * jp + 1] = dv.y;
+      acc[kb][jp] = f32x2{0.f, 0.f};
+    }
+  }
+  // S = sum_j a_j r_j + dctx . ctx  (the row's group-0 loads are already in flight)
+  float S = 0.f;
+  for (int i = tid; i < len; i += NT) {
+    const size_t ix = rb + i;
+    const float ai = a[ix];
+    float r = (Ga ? Ga[ix] : 0.f) + (dcov_next ? dcov_next[ix] : 0.f);
+    if (gcl && ai <= (cov ? cov[ix] : 0.f)) r += g;
+    S += ai * r;
+  }
+  for (int k = tid; k < A; k += NT) S += dctx[(size_t)b * A + k] * ctx[(size_t)b * A + k];
+  S = block_sum<NT>(S, red);
+  auto compute = [&](int grp, const Rows<NK>& e, const Rows<NK>& f, const Scal& x) {
+    float pd[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x2 d2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp)
+          d2 = fma2(bf2pair(e.x[kb][q][jp]), f32x2{dk[kb][2 * jp], dk[kb][2 * jp + 1]}, d2);
+      pd[q] = d2.x + d2.y;
+    }
+    const float dot = bfly4(pd, b5, b4);
+    const int p = 4 * grp + qm;
+    const float de_q = p < len ? x.a * (x.r + dot - S) : 0.f;
+    float dcv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float de = rdlane(de_q, 16 * q);
+      const float c = rdlane(x.c, 16 * q);
+      f32x2 dc2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          const f32x2 r = rsig2(y);
+          const f32x2 qv = fma2(-r, r, r);
+          acc[kb][jp] = fma2(qv, splat2(de), acc[kb][jp]);
+          dc2 = fma2(qv, v4w[kb][jp], dc2);
+        }
+      dcv[q] = dc2.x + dc2.y;
+    }
+    const float hc = bfly4(dcv, b5, b4);
+    if ((lane & 15) == 0 && p < T) {
+      de_out[rb + p] = de_q;
+      if (dcov_out) {
+        float r = x.dn;
+        if (p < len) {
+          r += de_q * hc;
+          if (gcl && x.a > x.c) r += g;
+        } else {
+          r = dcov_next ? dcov_next[rb + p] : 0.f;
+        }
+        dcov_out[rb + p] = r;
+      }
+    }
+  };
+  for (int gi = wid; gi < ngrp;) {
+    const int g1 = gi + NW;
+    if (g1 < ngrp) load(g1, eB, fB, xB);
+    compute(gi, eA, fA, xA);
+    if (g1 >= ngrp) break;
+    const int g2 = g1 + NW;
+    if (g2 < ngrp) load(g2, eA, fA, xA);
+    compute(g1, eB, fB, xB);
+    gi = g2;
+  }
+  // positions past the last group: de = 0, dcov passes through
+  for (int p = 4 * ngrp + tid; p < T; p += NT) {
+    de_out[rb + p] = 0.f;
+    if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
+  }
+  // ds_k = 4 v_k sum_i de_i q_ik, summed over the waves in LDS: one plain store per feature
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp)
+      *reinterpret_cast<float2*>(&part[wid][kb * 512 + lane * 8 + 2 * jp]) =
+          make_float2(acc[kb][jp].x, acc[kb][jp].y);
+  __syncthreads();
+  for (int k = tid; k < A; k += NT) {
+    float x = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) x += part[w][k];
+    ds[(size_t)b * A + k] = 4.f * v[k] * x;
+  }
+}
+
+// ------------------------------------------------------------------------------ launchers
+bool attn_row_supported(int A, int T) { return (A == 512 || A == 1024) && T >= 1 && T <= kRowMaxT; }
+
+void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
+                         const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
+                         bf16* ctx_bf, int B, int T, int A, hipStream_t st) {
+#define LF(NK)                                                                                                 \
+  hipLaunchKernelGGL((attn_fwd_row_kernel<NK, row_waves<NK, false>()>), dim3(B), dim3(row_waves<NK, false>() * 64), \
+                     0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T)
+  if (A == 512) LF(1);
+  else LF(2);
+#undef LF
+}
+
+void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
+                         const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
+                         const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
+                         float* dcov_out, int B, int T, int A, hipStream_t st) {
+#define LB(NK)                                                                                                \
+  hipLaunchKernelGGL((attn_bwd_row_kernel<NK, row_waves<NK, true>()>), dim3(B), dim3(row_waves<NK, true>() * 64), \
+                     0, st, E, F, s, v, wc, cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T)
+  if (A == 512) LB(1);
+  else LB(2);
+#undef LB
+}

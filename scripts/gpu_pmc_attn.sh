@@ -1,11 +1,19 @@
 #!/bin/bash
-# PMC counters of the attention kernels at the B=256 bench shape (tools/attn_micro.py).
+# PMC counters of the attention kernels at the B=256 bench shape (tools/attn_micro.py):
+# pass 1 wave/issue counters, pass 2 VALU + transcendental instruction mix, pass 3 bytes.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/pmc_attn; mkdir -p $OUT
 export TMPDIR=/tmp
-R="attn_score|attn_bwd_step|attn_softmax"
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-include-regex "$R" -d $OUT/p1 -o run --output-format csv -- python3 tools/attn_micro.py > $OUT/p1.log 2>&1 || { tail -5 $OUT/p1.log; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TCC_HIT_sum --kernel-include-regex "$R" -d $OUT/p2 -o run --output-format csv -- python3 tools/attn_micro.py > $OUT/p2.log 2>&1 || { tail -5 $OUT/p2.log; exit 1; }
-python scripts/pmc_sum.py $(find $OUT/p1 -name "*counter_collection.csv")
-python scripts/pmc_sum.py $(find $OUT/p2 -name "*counter_collection.csv")
+R="${PMC_REGEX:-attn_score|attn_bwd_step|attn_softmax|attn_bwd_feat}"
+timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
+p() {  # name counters...
+  local n=$1; shift
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$R" -d $OUT/$n -o run --output-format csv -- python3 tools/attn_micro.py > $OUT/$n.log 2>&1 || { tail -5 $OUT/$n.log; return 1; }
+  python scripts/pmc_sum.py $(find $OUT/$n -name "*counter_collection.csv") | tee $OUT/$n.txt
+}
+p p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD &&
+p p2 SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 &&
+p p3 FETCH_SIZE TCC_HIT_sum &&
+p p4 GRBM_GUI_ACTIVE GRBM_COUNT TCC_EA0_RDREQ_sum
+echo pmc done

@@ -52,6 +52,7 @@ class DeviceBeamDecoder:
         self.maxD = hps.max_dec_steps
         self.use_graph, self.chunk, self.keep_attn = use_graph, chunk, keep_attn
         self.eng = HipPointerGenerator(hps, self.V, params, B=self.Na, T=T, D=1)
+        self.eng.keep_ft = True  # the decode-step attention kernels read the transposed features
         self.k = self.eng.k
         self.dev = self.eng.dev
         self._alloc()

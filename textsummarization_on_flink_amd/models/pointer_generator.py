@@ -114,6 +114,17 @@ class HipPointerGenerator:
         # Off by default: the graph-captured B=256 bench with the fork/join stalled on MI355X
         # (no progress for 180 s) and the GEMM is ~0.7 ms of a ~27 ms step.
         self._side = torch.cuda.Stream(self.dev) if os.environ.get("TSAMD_OVERLAP_DW", "0") == "1" else None
+        # The decoder recurrences (forward: cell -> s-projection -> score -> softmax/context;
+        # backward: attention step -> cell backward -> dz backward) are independent across
+        # batch rows.  With ``split`` > 1 the rows are cut into that many groups, each group's
+        # chain of per-step launches runs on its own stream (forked from and joined to the
+        # current stream, so a captured hipGraph holds parallel branches): one group's small
+        # latency-bound cell kernels run beside another group's bandwidth-bound attention
+        # kernels instead of serialising behind them.  TSAMD_SPLIT overrides (1 = one chain).
+        sp = int(os.environ.get("TSAMD_SPLIT", "0")) or (2 if B >= 128 and B % 32 == 0 else 1)
+        self.split = sp if (sp > 1 and B % (16 * sp) == 0) else 1
+        self._rows = [(B * g // self.split, B * (g + 1) // self.split) for g in range(self.split)]
+        self._streams = [torch.cuda.Stream(self.dev) for _ in range(self.split)] if self.split > 1 else []
         self._alloc()
         self.pack()
 
@@ -175,8 +186,16 @@ class HipPointerGenerator:
         # one fused attention-backward kernel per decoder step (attn_bwd_step);
         # TSAMD_ATTN_BWD_FUSED=0 selects the two-kernel path (attn_bwd_da over Et + attn_bwd_tanh)
         self.fused_attn_bwd = os.environ.get("TSAMD_ATTN_BWD_FUSED", "1") != "0"
+        # row-resident attention (attention_row.hip: one workgroup per row and step, forward
+        # score + softmax + context in one launch) when the batch fills the CUs; else the
+        # multi-block-per-row kernels of attention.hip.  TSAMD_ROW_ATTN=0/1 overrides.
+        ra = os.environ.get("TSAMD_ROW_ATTN", "")
+        self.row_attn = bool(self.k.attn_row_ok(A, T)) and (ra == "1" or (ra != "0" and B >= 128))
         w["F"] = z(B, T, A, dt=BF)
-        w["Ft"] = z(B, A, T, dt=BF)   # transposed copy for the lanes-over-positions score kernel
+        # transposed copy for the lanes-over-positions score kernel (not needed by the row
+        # kernels; the beam decoder sets keep_ft to get it from _encoder_forward)
+        self.keep_ft = not self.row_attn
+        w["Ft"] = z(B, A, T, dt=BF) if self.keep_ft else None
         w["Et"] = None if self.fused_attn_bwd else z(B, A, T, dt=BF)
         w["XG"] = z(D, B, 4 * H)
         # decoder forward state
@@ -388,7 +407,10 @@ class HipPointerGenerator:
         w["Cb"][0].copy_(c0)
         w["Hb"][0].copy_(h0)
         mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["Wh"])
-        k.transpose_bta(w["F"], w["Ft"], B, T, A)
+        if self.keep_ft:
+            if w["Ft"] is None:
+                w["Ft"] = torch.empty(B, A, T, dtype=BF, device=self.dev)
+            k.transpose_bta(w["F"], w["Ft"], B, T, A)
         if w["Et"] is not None:
             k.transpose_bta(top["out"], w["Et"], B, T, A)
 
@@ -401,16 +423,29 @@ class HipPointerGenerator:
         mm_into(xe, emb_dec, self.pk["lin_emb"], self.p[LIN_B])
         mm_into(w["XG"].view(D * B, 4 * H), xe.to(BF), self.pk["cell_x"], self.p[CELL_B])
         self._emb_dec = emb_dec
-        enc_out, lens, Ft = self.enc[-1]["out"], w["enc_lens"], w["Ft"]
+        enc_out, lens, Ft, F = self.enc[-1]["out"], w["enc_lens"], w["Ft"], w["F"]
         v, wc = self.f32["v"], self.f32["wc"]
-        for t in range(D):
-            k.dec_cell_fwd(w["XG"][t], w["CTXb"][t - 1] if t > 0 else None, w["Hb"][t], w["Cst"][t], self.pk["WcT2"],
-                           w["Cst"][t + 1], w["Cb"][t + 1], w["Hb"][t + 1], w["ACT"][t], B, H, A)
-            k.dec_sproj(w["Cb"][t + 1], w["Hb"][t + 1], self.pk["WsT"], self.p[ATT_B], w["S"][t], B, H, A)
-            cov_in = w["COV"][t] if (cov and t > 0) else None
-            k.attn_score(Ft, w["S"][t], v, wc, cov_in, lens, w["e"], B, T, A, 1)
-            k.attn_softmax_ctx(w["e"], enc_out, lens, cov_in, w["ATT"][t], w["COV"][t + 1] if cov else None,
-                               w["covloss"][t] if cov else None, w["CTX"][t], w["CTXb"][t], B, T, A, 1)
+
+        def chain(r0, r1):
+            Bg, rs = r1 - r0, slice(r0, r1)
+            for t in range(D):
+                k.dec_cell_fwd(w["XG"][t][rs], w["CTXb"][t - 1][rs] if t > 0 else None, w["Hb"][t][rs],
+                               w["Cst"][t][rs], self.pk["WcT2"], w["Cst"][t + 1][rs], w["Cb"][t + 1][rs],
+                               w["Hb"][t + 1][rs], w["ACT"][t][rs], Bg, H, A)
+                k.dec_sproj(w["Cb"][t + 1][rs], w["Hb"][t + 1][rs], self.pk["WsT"], self.p[ATT_B], w["S"][t][rs], Bg,
+                            H, A)
+                cov_in = w["COV"][t][rs] if (cov and t > 0) else None
+                if self.row_attn:
+                    k.attn_fwd_row(F[rs], enc_out[rs], w["S"][t][rs], v, wc, cov_in, lens[rs], w["ATT"][t][rs],
+                                   w["COV"][t + 1][rs] if cov else None, w["covloss"][t][rs] if cov else None,
+                                   w["CTX"][t][rs], w["CTXb"][t][rs], Bg, T, A)
+                    continue
+                k.attn_score(Ft[rs], w["S"][t][rs], v, wc, cov_in, lens[rs], w["e"][rs], Bg, T, A, 1)
+                k.attn_softmax_ctx(w["e"][rs], enc_out[rs], lens[rs], cov_in, w["ATT"][t][rs],
+                                   w["COV"][t + 1][rs] if cov else None, w["covloss"][t][rs] if cov else None,
+                                   w["CTX"][t][rs], w["CTXb"][t][rs], Bg, T, A, 1)
+
+        self._row_groups(chain)
         # x_t = xe_t + ctx_{t-1} . W_in[E:]  (rebuilt after the loop, one GEMM)
         w["X"].copy_(w["xe"])
         if D > 1:
@@ -451,6 +486,19 @@ class HipPointerGenerator:
                         w["ext"], w["enc_lens"], w["loss_row"], w["dlogits"] if need_grad else None,
                         w["dpre"] if (need_grad and hps.pointer_gen) else None,
                         w["dA"] if (need_grad and hps.pointer_gen) else None, N, B, T, V)
+
+    def _row_groups(self, chain):
+        """Run ``chain(r0, r1)`` for every row group: inline when split == 1, else each group
+        on its own stream, forked from and joined back to the current stream."""
+        if self.split == 1:
+            return chain(0, self.B)
+        cur = torch.cuda.current_stream()
+        for st, (r0, r1) in zip(self._streams, self._rows):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                chain(r0, r1)
+        for st in self._streams:
+            cur.wait_stream(st)
 
     def forward(self, need_grad: bool = False):
         self._encoder_forward()
@@ -571,27 +619,38 @@ class HipPointerGenerator:
         w["dh_rec"].zero_()
         w["dc_carry"].zero_()
         dcov = w["dcov"]
-        w["DS"].zero_()
+        if not self.row_attn:
+            w["DS"].zero_()  # accumulated with atomics by the multi-block kernels (the row kernel stores)
         Ga = w["dA"] if hps.pointer_gen else None
-        for t in reversed(range(D)):
-            dcov_next = dcov[(t + 1) % 2] if (cov and t < D - 1) else None
-            cov_t = w["COV"][t] if (cov and t > 0) else None
-            gcl_t = w["gcl"][t] if cov else None
-            if self.fused_attn_bwd:
-                k.attn_bwd_step(enc_out, F, w["S"][t], v, wc, cov_t, w["ATT"][t], w["DCTX"][t], w["CTX"][t],
-                                Ga[t] if Ga is not None else None, dcov_next, gcl_t, lens, w["DE"][t], w["DS"][t],
-                                dcov[t % 2] if cov else None, B, T, A)
-            else:
-                k.attn_bwd_da(Et, w["DCTX"][t], Ga[t] if Ga is not None else None, dcov_next, w["ATT"][t], cov_t,
-                              gcl_t, lens, w["da"], B, T, A)
-                k.attn_bwd_tanh(F, w["S"][t], v, wc, cov_t, w["ATT"][t], w["da"], dcov_next, gcl_t, lens,
-                                w["DE"][t], w["DS"][t], dcov[t % 2] if cov else None, B, T, A)
-            k.dec_bwd_cell(w["DS"][t], self.pk["Ws"], dC_dir[t] if dC_dir is not None else None,
-                           dH_dir[t], w["dh_rec"], w["dc_carry"], w["ACT"][t], w["Cst"][t + 1], w["Cst"][t],
-                           w["DZ"][t], B, H, A)
-            k.dec_bwd_dz(w["DZ"][t], self.pk["Wbig"], dX_dir[t] if dX_dir is not None else None,
-                         dCTX_dir[t - 1] if t > 0 else None, w["DX"][t], w["DCTX"][t - 1] if t > 0 else None,
-                         w["dh_rec"], B, E, H, A)
+        def chain(r0, r1):
+            Bg, rs = r1 - r0, slice(r0, r1)
+            for t in reversed(range(D)):
+                dcov_next = dcov[(t + 1) % 2][rs] if (cov and t < D - 1) else None
+                cov_t = w["COV"][t][rs] if (cov and t > 0) else None
+                gcl_t = w["gcl"][t][rs] if cov else None
+                ga_t = Ga[t][rs] if Ga is not None else None
+                if self.row_attn:
+                    k.attn_bwd_row(enc_out[rs], F[rs], w["S"][t][rs], v, wc, cov_t, w["ATT"][t][rs], w["DCTX"][t][rs],
+                                   w["CTX"][t][rs], ga_t, dcov_next, gcl_t, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
+                                   dcov[t % 2][rs] if cov else None, Bg, T, A)
+                elif self.fused_attn_bwd:
+                    k.attn_bwd_step(enc_out[rs], F[rs], w["S"][t][rs], v, wc, cov_t, w["ATT"][t][rs], w["DCTX"][t][rs],
+                                    w["CTX"][t][rs], ga_t, dcov_next, gcl_t, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
+                                    dcov[t % 2][rs] if cov else None, Bg, T, A)
+                else:
+                    k.attn_bwd_da(Et[rs], w["DCTX"][t][rs], ga_t, dcov_next, w["ATT"][t][rs], cov_t, gcl_t, lens[rs],
+                                  w["da"][rs], Bg, T, A)
+                    k.attn_bwd_tanh(F[rs], w["S"][t][rs], v, wc, cov_t, w["ATT"][t][rs], w["da"][rs], dcov_next, gcl_t,
+                                    lens[rs], w["DE"][t][rs], w["DS"][t][rs], dcov[t % 2][rs] if cov else None, Bg, T,
+                                    A)
+                k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
+                               dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A)
+                k.dec_bwd_dz(w["DZ"][t][rs], self.pk["Wbig"], dX_dir[t][rs] if dX_dir is not None else None,
+                             dCTX_dir[t - 1][rs] if t > 0 else None, w["DX"][t][rs],
+                             w["DCTX"][t - 1][rs] if t > 0 else None, w["dh_rec"][rs], Bg, E, H, A)
+
+        self._row_groups(chain)
         # ---- decoder weight gradients (one GEMM each over all D*B rows)
         DZ = w["DZ"].view(N, 4 * H)
         gk = g(CELL_K)

@@ -50,9 +50,20 @@ def main():
     torch.cuda.synchronize()
     k, w, A, H = eng.k, eng.w, eng.A, eng.H
     enc_out, lens, F, Ft = eng.enc[-1]["out"], w["enc_lens"], w["F"], w["Ft"]
+    if Ft is None:  # row-attention engine: build the transposed copy for the multi-block kernels
+        Ft = torch.empty(B, eng.A, T, dtype=BF, device="cuda")
+        eng.k.transpose_bta(F, Ft, B, T, eng.A)
     v, wc = eng.f32["v"], eng.f32["wc"]
     t = 50
     res = {"B": B, "env": {x: os.environ[x] for x in os.environ if x.startswith("TSAMD_")}}
+    if eng.k.attn_row_ok(eng.A, T):
+        res["attn_fwd_row"] = timeit(lambda: eng.k.attn_fwd_row(F, enc_out, w["S"][t], v, wc, w["COV"][t], lens,
+                                                                 w["ATT"][t], w["COV"][t + 1], w["covloss"][t],
+                                                                 w["CTX"][t], w["CTXb"][t], B, T, eng.A))
+        res["attn_bwd_row"] = timeit(lambda: eng.k.attn_bwd_row(enc_out, F, w["S"][t], v, wc, w["COV"][t],
+                                                                 w["ATT"][t], w["DCTX"][t], w["CTX"][t], w["dA"][t],
+                                                                 w["dcov"][1], w["gcl"][t], lens, w["DE"][t],
+                                                                 w["DS"][t], w["dcov"][0], B, T, eng.A))
     res["attn_score"] = timeit(lambda: k.attn_score(Ft, w["S"][t], v, wc, w["COV"][t], lens, w["e"], B, T, A, 1))
     res["attn_softmax_ctx"] = timeit(lambda: k.attn_softmax_ctx(w["e"], enc_out, lens, w["COV"][t], w["ATT"][t],
                                                                 w["COV"][t + 1], w["covloss"][t], w["CTX"][t],
