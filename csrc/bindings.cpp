@@ -65,6 +65,7 @@ void lstm_enc_bwd_step(const Tensor& dz, const Tensor& Wn, const Tensor& dout, c
 // persistent (one launch for all T steps) variants; see lstm_persistent.hip
 int64_t lstm_persistent_grid_op(int64_t H, int64_t B) { return lstm_persistent_grid((int)H, (int)B); }
 int64_t lstm_persistent_capacity_op(int64_t H) { return lstm_persistent_capacity((int)H); }
+int64_t lstm_persistent_launches_op(int64_t H, int64_t B) { return lstm_persistent_launches((int)H, (int)B); }
 int64_t lstm_persistent_xbuf_op(int64_t H, int64_t B, bool bwd) {
   return (int64_t)lstm_persistent_xbuf_elems((int)H, (int)B, bwd);
 }
@@ -74,8 +75,8 @@ void lstm_fwd_persistent(const Tensor& gx, const Tensor& bias, const Tensor& Wt,
                          const Tensor& err, int64_t T, int64_t B, int64_t H) {
   chk(gx, F32, "gx"); chk(bias, F32, "bias"); numel_eq(bias, 2 * 4 * H, "bias"); chk(Wt, BF, "Wt"); chk(hs, BF, "hs"); chk(cs, F32, "cs"); chk(acts, F32, "acts");
   chk(out, BF, "out"); chk(lens, I32, "lens"); chk(xbuf, at::kLong, "xbuf"); chk(err, I32, "err");
-  TORCH_CHECK(lstm_persistent_grid((int)H, (int)B) > 0, "persistent LSTM: unsupported H/B (H in {64,128,256}, "
-              "grid <= resident capacity, one workgroup per CU)");
+  TORCH_CHECK(lstm_persistent_grid((int)H, (int)B) > 0, "persistent LSTM: unsupported H/B (H in {64,128,256,512}; "
+              "a launch's grid must fit the resident capacity, one workgroup per CU)");
   TORCH_CHECK(T >= 1 && T < (1 << 30), "bad T");
   numel_eq(gx, 2 * T * B * 4 * H, "gx"); numel_eq(Wt, 2 * 4 * H * H, "Wt");
   numel_eq(hs, 2 * (T + 1) * B * H, "hs"); numel_eq(cs, 2 * (T + 1) * B * H, "cs");
@@ -596,6 +597,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("lstm_enc_bwd_step", &lstm_enc_bwd_step);
   m.def("lstm_persistent_grid", &lstm_persistent_grid_op);
   m.def("lstm_persistent_capacity", &lstm_persistent_capacity_op);
+  m.def("lstm_persistent_launches", &lstm_persistent_launches_op);
   m.def("lstm_persistent_xbuf", &lstm_persistent_xbuf_op);
   m.def("lstm_fwd_persistent", &lstm_fwd_persistent);
   m.def("lstm_bwd_persistent", &lstm_bwd_persistent);

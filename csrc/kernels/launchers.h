@@ -87,6 +87,7 @@ void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const floa
                      int N, int A, int H, int E, hipStream_t st);
 int lstm_persistent_grid(int H, int B);
 int lstm_persistent_capacity(int H);
+int lstm_persistent_launches(int H, int B);
 size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd);
 void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,

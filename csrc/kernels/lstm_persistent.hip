@@ -24,6 +24,7 @@
 // Layouts are those of lstm.hip (step frame; hs/cs [2][T+1][B][H], acts [2][T][B][4H],
 // out [B][T][2H], dz [2][T][B][4H]), so the two implementations are interchangeable.
 #include "common.h"
+#include <stdlib.h>
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned int gu32;
@@ -94,12 +95,12 @@ template <int H>
 __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     const float* __restrict__ gx, const float* __restrict__ bias, const bf16* __restrict__ Wt,
     bf16* __restrict__ hs, float* __restrict__ cs, float* __restrict__ acts, bf16* __restrict__ out,
-    const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile) {
+    const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile, int tile0, int ntile_l) {
   constexpr int KS = H / 32, NC = H / 64, HP = H / 2, G = 16 * HP, NPL = G / 256;
   __shared__ __attribute__((aligned(16))) bf16 Ash[2][16 * H];
-  int team, c;
-  if (!team_of(NC, 2 * ntile, team, c)) return;
-  const int d = team / ntile, r0 = (team % ntile) * 16;
+  int lt, c;
+  if (!team_of(NC, 2 * ntile_l, lt, c)) return;
+  const int d = lt / ntile_l, tile = tile0 + lt % ntile_l, r0 = tile * 16, team = d * ntile + tile;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int u = c * 64 + wid * 16 + (lane & 15);
   const size_t G4 = 4 * (size_t)H, BH = (size_t)B * H;
@@ -201,27 +202,157 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   }
 }
 
+// Forward with 8 waves per workgroup (H = 512; any H % 64 == 0).  Four waves x 16 units x 4
+// gates would need H = 512 k-rows of W_hh per gate column: 256 VGPRs of B fragments per lane.
+// Here wave w owns 8 units (c*64 + 8w .. +7) and two 16-column MFMA tiles: tile t, column n
+// holds gate 2t + (n >> 3) of unit n & 7, so W_hh stays register-resident at H = 512 with
+// 2 x KS x 4 = 128 VGPRs.  After the MFMAs lane n (< 8) has gates i, f and lane n ^ 8 has
+// j, o of the same unit for the same 4 rows; four row_ror:8 DPP moves swap half of them, and
+// each lane then updates the cell for 2 of the 4 rows (lanes n < 8: rows 0-1, n >= 8: 2-3).
+// Hand-off, layouts and tags are the 4-wave kernel's.
+template <int H>
+__global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
+    const float* __restrict__ gx, const float* __restrict__ bias, const bf16* __restrict__ Wt,
+    bf16* __restrict__ hs, float* __restrict__ cs, float* __restrict__ acts, bf16* __restrict__ out,
+    const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile, int tile0, int ntile_l) {
+  constexpr int KS = H / 32, NC = H / 64, HP = H / 2, G = 16 * HP, NPL = G / 512;
+  static_assert(H % 64 == 0 && G % 512 == 0, "8-wave LSTM layout");
+  __shared__ __attribute__((aligned(16))) bf16 Ash[2][16 * H];
+  int lt, c;
+  if (!team_of(NC, 2 * ntile_l, lt, c)) return;
+  const int d = lt / ntile_l, tile = tile0 + lt % ntile_l, r0 = tile * 16, team = d * ntile + tile;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = lane & 15, half = n >> 3;
+  const int u = c * 64 + wid * 8 + (n & 7);
+  const size_t G4 = 4 * (size_t)H, BH = (size_t)B * H;
+  bf16x8 Wf[2][KS];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+      Wf[t][kk] = ld8(Wt + ((size_t)d * G4 + (2 * t + half) * H + u) * H + kk * 32 + 8 * (lane >> 4));
+  float gb[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) gb[g] = bias[(size_t)d * G4 + g * H + u];
+  // this lane's rows within the tile: 4 (lane >> 4) + 2 half + i
+  int rc[2], ln[2], rt[2];
+  bool rok[2];
+  float creg[2], hreg[2];
+  const bf16* hs0 = hs + (size_t)d * (T + 1) * BH;
+  const float* cs0 = cs + (size_t)d * (T + 1) * BH;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rt[i] = (lane >> 4) * 4 + 2 * half + i;
+    const int r = r0 + rt[i];
+    rok[i] = r < B;
+    rc[i] = rok[i] ? r : B - 1;
+    ln[i] = rok[i] ? lens[r] : 0;
+    creg[i] = cs0[(size_t)rc[i] * H + u];
+    hreg[i] = bf2f(hs0[(size_t)rc[i] * H + u]);
+  }
+  gu64* xb = xbuf + (size_t)team * 2 * G;
+  bool dead = false;
+  for (int s = 0; s < T; ++s) {
+    const int buf = s & 1;
+    float gz[2][4];
+    const float* gxs = gx + ((size_t)d * T + s) * B * G4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gz[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u] + gb[g];
+    if (s == 0) {
+      for (int idx = threadIdx.x; idx < G; idx += 512) {
+        const int row = idx / HP, p = idx % HP;
+        const int rr = min(r0 + row, B - 1);
+        *reinterpret_cast<unsigned*>(&Ash[0][swz<H>(row, 2 * p)]) =
+            *reinterpret_cast<const unsigned*>(hs0 + (size_t)rr * H + 2 * p);
+      }
+    } else {
+      unsigned v[NPL];
+      sweep<NPL>(xb + (size_t)(s & 1) * G, wid * (G / 8), (unsigned)s, v, dead, err, 1u, lane);
+#pragma unroll
+      for (int j = 0; j < NPL; ++j) {
+        const int idx = wid * (G / 8) + j * 64 + lane;
+        *reinterpret_cast<unsigned*>(&Ash[buf][swz<H>(idx / HP, 2 * (idx % HP))]) = v[j];
+      }
+    }
+    __syncthreads();
+    f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ash[buf][swz<H>(lane & 15, kk * 32 + 8 * (lane >> 4))]);
+      acc[0] = mfma16(a, Wf[0][kk], acc[0]);
+      acc[1] = mfma16(a, Wf[1][kk], acc[1]);
+    }
+    // swap gate halves with the partner lane n ^ 8 (same rows): lanes n < 8 keep rows 0-1 and
+    // receive j, o; lanes n >= 8 keep rows 2-3 and receive i, f
+    float rcv[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      rcv[i] = dpp_f<DPP_ROR8>(half ? acc[0][i] : acc[0][2 + i]);
+      rcv[2 + i] = dpp_f<DPP_ROR8>(half ? acc[1][i] : acc[1][2 + i]);
+    }
+    float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
+    bf16* hnext = hs + ((size_t)d * (T + 1) + s + 1) * BH;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = rc[i];
+      if (s < ln[i]) {
+        const float zi = half ? rcv[i] : acc[0][i], zj = half ? acc[0][2 + i] : rcv[i];
+        const float zf = half ? rcv[2 + i] : acc[1][i], zo = half ? acc[1][2 + i] : rcv[2 + i];
+        const float ig = fsigmoid(zi + gz[i][0]), jg = ftanh(zj + gz[i][1]);
+        const float fg = fsigmoid(zf + gz[i][2] + 1.0f), og = fsigmoid(zo + gz[i][3]);
+        const float cc = fg * creg[i] + ig * jg;
+        const float h = bf2f(f2bf(og * ftanh(cc)));
+        creg[i] = cc;
+        hreg[i] = h;
+        float* a4 = acts + (((size_t)d * T + s) * B + r) * G4;
+        a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
+        const int t = d == 0 ? s : ln[i] - 1 - s;
+        out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(h);
+      }
+      if (rok[i]) {
+        cnext[(size_t)r * H + u] = creg[i];
+        hnext[(size_t)r * H + u] = f2bf(hreg[i]);
+      }
+    }
+    if (s + 1 < T) {
+      gu64* dst = xb + (size_t)((s + 1) & 1) * G;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float hn = dpp_f<DPP_XOR1>(hreg[i]);  // unit u + 1 (lane n ^ 1, same half)
+        if (!(lane & 1)) store_granule(dst + rt[i] * HP + u / 2, (unsigned)(s + 1), pack_bf2(hreg[i], hn));
+      }
+    }
+  }
+}
+
 // Backward.  Exchanging dz (4H gate columns) would cost 4x the forward's traffic, so the
 // recurrent GEMM is split by K instead: workgroup c multiplies ITS dz slice (the 4 gates of
 // its 64 units, 256 columns, written to LDS) by the matching W_hh rows and produces a
 // PARTIAL dh for all H units; wave w's 64 output units are exactly slice w's, and go to
 // workgroup (team, w) as fp32 granules.  Each workgroup sums NC partials for its own units
 // (its own partial stays in LDS): per step a lane reads 4 x (NC-1) granules instead of 32.
-template <int H>
-__global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
+// NW = 4 or 8 waves: the cell update covers the tile's 16 rows x 64 units with RPL = 16 / NW
+// rows per lane (4 or 2); waves < NC run the partial GEMM (at H = 512, NC = 8: all 8 waves).
+template <int H, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
     const float* __restrict__ cs, const int* __restrict__ lens, gu64* xbuf, gu32* err,
     float* __restrict__ dbias,  // [2][4H] nullable: += sum over rows and steps of dz (gate-bias gradient)
-    int T, int B, int ntile) {
+    int T, int B, int ntile, int tile0, int ntile_l) {
   constexpr int G4 = 4 * H, NC = H / 64, KS = 256 / 32, SLOT = 16 * 64, TEAMX = 2 * NC * NC * SLOT;
+  constexpr int RPL = 16 / NW;  // rows per lane in the cell update
+  static_assert((NW == 4 || NW == 8) && NC <= NW && RPL * NC <= 32, "bwd layout");
   __shared__ __attribute__((aligned(16))) bf16 Ash[16 * 256];   // dz slice [16 rows][4 gates x 64 units]
   __shared__ float Pown[16 * 64];                                // own partial dh [16 rows][64 units]
-  int team, c;
-  if (!team_of(NC, 2 * ntile, team, c)) return;
-  const int d = team / ntile, r0 = (team % ntile) * 16;
+  int lt, c;
+  if (!team_of(NC, 2 * ntile_l, lt, c)) return;
+  const int d = lt / ntile_l, tile = tile0 + lt % ntile_l, r0 = tile * 16, team = d * ntile + tile;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ul = wid * 16 + (lane & 15);  // this lane's unit within the slice (cell update)
+  const int ul = (wid & 3) * 16 + (lane & 15);  // this lane's unit within the slice (cell update)
+  const int row0 = (wid >> 2) * (4 * RPL) + (lane >> 4) * RPL;  // its first row within the tile
   const int u = c * 64 + ul;
   const size_t BH = (size_t)B * H;
   // B operand of the partial GEMM: B[k][n] = W_hh[v][gate col(k)], k = g*64 + unit-in-slice,
@@ -235,12 +366,12 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       const int v = min(64 * wid + 16 * t + (lane & 15), H - 1);  // waves >= NC own no output units
       Wp[t][kk] = ld8(Wn + ((size_t)d * H + v) * G4 + g * H + 64 * c + ul0);
     }
-  int rc[4], ln[4];
-  bool rok[4];
-  float dcreg[4];
+  int rc[RPL], ln[RPL];
+  bool rok[RPL];
+  float dcreg[RPL];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = r0 + (lane >> 4) * 4 + i;
+  for (int i = 0; i < RPL; ++i) {
+    const int r = r0 + row0 + i;
     rok[i] = r < B;
     rc[i] = rok[i] ? r : B - 1;
     ln[i] = rok[i] ? lens[r] : 0;
@@ -248,14 +379,14 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   }
   gu64* xb = xbuf + (size_t)team * TEAMX;  // [parity][dest][src][16][64]
   bool dead = false;
-  // gate-bias gradient of (unit u, gate g): the lane's 4 rows summed over all steps in
+  // gate-bias gradient of (unit u, gate g): the lane's rows summed over all steps in
   // registers (fp32, off the recurrence's critical path), reduced over the wave's 4 row
   // groups and added once per team at the end -- replaces a 2 x 210 MB column reduction
   float bacc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int s = T - 1; s >= 0; --s) {
-    float dho[4], dhf[4], a4[4][4], cn[4], cpv[4];
+    float dho[RPL], dhf[RPL], a4[RPL][4], cn[RPL], cpv[RPL];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < RPL; ++i) {
       const size_t ri = (size_t)rc[i] * H + u;
       dho[i] = dout[((size_t)d * T + s) * BH + ri];
       dhf[i] = dh_fin[(size_t)d * BH + ri];
@@ -265,78 +396,82 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       cn[i] = cs[((size_t)d * (T + 1) + s + 1) * BH + ri];
       cpv[i] = cs[((size_t)d * (T + 1) + s) * BH + ri];
     }
-    // ---- recurrent dh for this lane's 4 rows: own partial (LDS) + the peers' (granules)
-    float rec[4] = {0.f, 0.f, 0.f, 0.f};
-    if (s + 1 < T) {
-      const int row0 = (lane >> 4) * 4;
+    // ---- recurrent dh for this lane's rows: own partial (LDS) + the peers' (granules)
+    float rec[RPL];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) rec[i] = Pown[(row0 + i) * 64 + ul];
+    for (int i = 0; i < RPL; ++i) rec[i] = 0.f;
+    if (s + 1 < T) {
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) rec[i] = Pown[(row0 + i) * 64 + ul];
       if constexpr (NC > 1) {
+        // peers in chunks of PC (at H = 512 all 8 at once would hold 32 VGPRs of granules and
+        // spill); each chunk's ready granules keep their value in x (not re-read)
+        constexpr int PC = NC < 4 ? NC : 4;
         const gu64* src = xb + (size_t)((s + 1) & 1) * NC * NC * SLOT + (size_t)c * NC * SLOT;
         const unsigned tag = (unsigned)(T - 1 - s);
-        unsigned ready = 0;
-        float got[NC][4];
-        unsigned long long x[NC][4];
-        for (unsigned spins = 0;;) {
 #pragma unroll
-          for (int p = 0; p < NC; ++p)
+        for (int p0 = 0; p0 < NC; p0 += PC) {
+          unsigned ready = 0;
+          unsigned long long x[PC][RPL];
+          constexpr unsigned allm = RPL * PC >= 32 ? 0xffffffffu : ((1u << (RPL * PC % 32)) - 1);
+          const unsigned need = (c >= p0 && c < p0 + PC) ? allm & ~(((1u << RPL) - 1) << (RPL * (c - p0))) : allm;
+          for (unsigned spins = 0;;) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              if (p != c && !((ready >> (p * 4 + i)) & 1))
-                x[p][i] = __hip_atomic_load(src + (size_t)p * SLOT + (row0 + i) * 64 + ul, RLX_AGENT);
+            for (int q = 0; q < PC; ++q)
 #pragma unroll
-          for (int p = 0; p < NC; ++p)
+              for (int i = 0; i < RPL; ++i)
+                if (p0 + q != c && !((ready >> (q * RPL + i)) & 1))
+                  x[q][i] = __hip_atomic_load(src + (size_t)(p0 + q) * SLOT + (row0 + i) * 64 + ul, RLX_AGENT);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int bit = p * 4 + i;
-              if (p != c && !((ready >> bit) & 1) && (unsigned)(x[p][i] >> 32) == tag) {
-                got[p][i] = __uint_as_float((unsigned)x[p][i]);
-                ready |= 1u << bit;
+            for (int q = 0; q < PC; ++q)
+#pragma unroll
+              for (int i = 0; i < RPL; ++i) {
+                const int bit = q * RPL + i;
+                if (p0 + q != c && !((ready >> bit) & 1) && (unsigned)(x[q][i] >> 32) == tag) ready |= 1u << bit;
               }
+            if (__all((ready & need) == need) || dead) break;
+            if (++spins > kSpinLimit) {
+              if (lane == 0) __hip_atomic_store(err, 2u, RLX_AGENT);
+              dead = true;
+              break;
             }
-          const unsigned need = ((1u << (4 * NC)) - 1) & ~(0xFu << (4 * c));
-          if (__all((ready & need) == need) || dead) break;
-          if (++spins > kSpinLimit) {
-            if (lane == 0) __hip_atomic_store(err, 2u, RLX_AGENT);
-            dead = true;
-            break;
+            __builtin_amdgcn_s_sleep(1);
           }
-          __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+          for (int q = 0; q < PC; ++q)
+#pragma unroll
+            for (int i = 0; i < RPL; ++i)
+              if (p0 + q != c) rec[i] += ((ready >> (q * RPL + i)) & 1) ? __uint_as_float((unsigned)x[q][i]) : 0.f;
         }
-#pragma unroll
-        for (int p = 0; p < NC; ++p)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (p != c) rec[i] += ((ready >> (p * 4 + i)) & 1) ? got[p][i] : 0.f;
       }
     }
-    // ---- cell backward -> dz (4 gates) for (4 rows, unit u)
-    float dzv[4][4];
+    // ---- cell backward -> dz (4 gates) for (the lane's rows, unit u)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < RPL; ++i) {
+      float dzv[4];
       if (s < ln[i]) {
         const float dh = rec[i] + dho[i] + (s + 1 >= ln[i] ? dhf[i] : 0.f);
         const float ig = a4[i][0], jg = a4[i][1], fg = a4[i][2], og = a4[i][3];
         const float tc = ftanh(cn[i]);
         const float dc = dcreg[i] + dh * og * (1.0f - tc * tc);
-        dzv[i][0] = dc * jg * ig * (1.0f - ig);
-        dzv[i][1] = dc * ig * (1.0f - jg * jg);
-        dzv[i][2] = dc * cpv[i] * fg * (1.0f - fg);
-        dzv[i][3] = dh * tc * og * (1.0f - og);
+        dzv[0] = dc * jg * ig * (1.0f - ig);
+        dzv[1] = dc * ig * (1.0f - jg * jg);
+        dzv[2] = dc * cpv[i] * fg * (1.0f - fg);
+        dzv[3] = dh * tc * og * (1.0f - og);
         dcreg[i] = dc * fg;
       } else {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) dzv[i][g] = 0.f;
+        for (int g = 0; g < 4; ++g) dzv[g] = 0.f;
       }
-      const int row = (lane >> 4) * 4 + i;
+      const int row = row0 + i;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) bacc[g] += dzv[i][g];
+      for (int g = 0; g < 4; ++g) bacc[g] += dzv[g];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) Ash[swz<256>(row, g * 64 + ul)] = f2bf(dzv[i][g]);
+      for (int g = 0; g < 4; ++g) Ash[swz<256>(row, g * 64 + ul)] = f2bf(dzv[g]);
       if (rok[i]) {
         bf16* dzr = dz + (((size_t)d * T + s) * B + rc[i]) * G4;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) dzr[g * H + u] = f2bf(dzv[i][g]);
+        for (int g = 0; g < 4; ++g) dzr[g * H + u] = f2bf(dzv[g]);
       }
     }
     if (s == 0) break;
@@ -371,7 +506,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     __syncthreads();  // Pown visible before the next step reads it; Ash free for rewriting
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < RPL; ++i)
     if (rok[i]) dc_carry[(size_t)d * BH + (size_t)rc[i] * H + u] = dcreg[i];
   if (dbias) {
 #pragma unroll
@@ -383,38 +518,68 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
 }
 
 // ---------------------------------------------------------------------- launchers
+// Kernel variant: 4 waves per workgroup (16 units per wave) up to H = 256; 8 waves (8 units
+// per wave in the forward, 2 rows per lane in the backward) at H = 512, where the 4-wave
+// forward would need 256 VGPRs of W_hh per lane.  TSAMD_LSTM_NW=8 selects the 8-wave
+// kernels for smaller H too (A/B experiments).
+static int lstm_nw(int H) {
+  if (H == 512) return 8;
+  const char* e = getenv("TSAMD_LSTM_NW");  // read per call: tests switch it in-process
+  return (e && atoi(e) == 8) ? 8 : 4;
+}
+
+static bool lstm_h_ok(int H) { return H == 64 || H == 128 || H == 256 || H == 512; }
+
 // Workgroups of the persistent kernels the current device keeps resident at once: one per
-// CU (launch bounds (256, 1); the occupancy query must admit at least that), times the CU
+// CU (launch bounds (64 NW, 1); the occupancy query must admit at least that), times the CU
 // count the runtime reports -- not an assumed 256, so a partitioned or smaller device
 // shrinks the admissible grid instead of spinning into the hand-off timeout.
 int lstm_persistent_capacity(int H) {
-  static int cache[64][3] = {};  // [device][H/64 - 1 of {64,128,256}] -> capacity + 1
+  static int cache[64][4][2] = {};  // [device][log2(H/64)][NW == 8] -> capacity + 1
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  const int hi = H == 64 ? 0 : H == 128 ? 1 : H == 256 ? 2 : -1;
-  if (hi < 0) return 0;
-  if (cache[dev][hi]) return cache[dev][hi] - 1;
-  int cus = 0, occ = 0;
+  if (!lstm_h_ok(H) || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  const int hi = H == 64 ? 0 : H == 128 ? 1 : H == 256 ? 2 : 3, nw = lstm_nw(H), wi = nw == 8;
+  if (cache[dev][hi][wi]) return cache[dev][hi][wi] - 1;
+  int cus = 0, ob = 0, of = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
-  hipError_t e = hipErrorInvalidValue;
-  if (H == 64) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lstm_bwd_persistent_kernel<64>, 256, 0);
-  else if (H == 128) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lstm_bwd_persistent_kernel<128>, 256, 0);
-  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, lstm_bwd_persistent_kernel<256>, 256, 0);
-  int occ_f = 0;
-  hipError_t e2 = hipErrorInvalidValue;
-  if (H == 64) e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, lstm_fwd_persistent_kernel<64>, 256, 0);
-  else if (H == 128) e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, lstm_fwd_persistent_kernel<128>, 256, 0);
-  else e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, lstm_fwd_persistent_kernel<256>, 256, 0);
-  const int cap = (e == hipSuccess && e2 == hipSuccess && occ >= 1 && occ_f >= 1) ? cus : 0;
-  cache[dev][hi] = cap + 1;
+  hipError_t eb = hipErrorInvalidValue, ef = hipErrorInvalidValue;
+#define OCC(HH)                                                                                               \
+  if (H == HH) {                                                                                              \
+    if (nw == 8) {                                                                                            \
+      eb = hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, lstm_bwd_persistent_kernel<HH, 8>, 512, 0);      \
+      ef = hipOccupancyMaxActiveBlocksPerMultiprocessor(&of, lstm_fwd_persistent8_kernel<HH>, 512, 0);        \
+    } else if (HH <= 256) {                                                                                   \
+      eb = hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4>, 256, 0); \
+      ef = hipOccupancyMaxActiveBlocksPerMultiprocessor(&of, lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256)>, \
+                                                        256, 0);                                              \
+    }                                                                                                         \
+  }
+  OCC(64) OCC(128) OCC(256) OCC(512)
+#undef OCC
+  const int cap = (eb == hipSuccess && ef == hipSuccess && ob >= 1 && of >= 1) ? cus : 0;
+  cache[dev][hi][wi] = cap + 1;
   return cap;
 }
 
+// 16-row tiles per launch: the most whose grid (NC workgroups per (direction, tile) team,
+// teams dealt 8 at a time so members share an XCD) fits the resident capacity.  Teams are
+// independent, so a larger batch runs as consecutive launches over row-tile ranges.
+static int lstm_tiles_per_launch(int H, int ntile) {
+  const int NC = H / 64, cap = lstm_persistent_capacity(H);
+  int nl = ntile;
+  while (nl > 0 && 8 * NC * ((2 * nl + 7) / 8) > cap) --nl;
+  return nl;
+}
+
 int lstm_persistent_grid(int H, int B) {
-  if (H != 64 && H != 128 && H != 256) return 0;
-  const int NC = H / 64, ntile = (B + 15) / 16;
-  const int grid = 8 * NC * ((2 * ntile + 7) / 8);
-  return grid <= lstm_persistent_capacity(H) ? grid : 0;  // every workgroup co-resident (1 per CU)
+  if (!lstm_h_ok(H) || B < 1) return 0;
+  const int NC = H / 64, nl = lstm_tiles_per_launch(H, (B + 15) / 16);
+  return nl > 0 ? 8 * NC * ((2 * nl + 7) / 8) : 0;  // grid of the largest launch
+}
+
+int lstm_persistent_launches(int H, int B) {
+  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile);
+  return nl > 0 ? (ntile + nl - 1) / nl : 0;
 }
 
 size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {
@@ -426,29 +591,47 @@ size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {
 void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
                                 int H, hipStream_t st) {
-  const int grid = lstm_persistent_grid(H, B), ntile = (B + 15) / 16;
+  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H);
+  if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
-#define LAUNCH_F(HH)                                                                                       \
-  hipLaunchKernelGGL(lstm_fwd_persistent_kernel<HH>, dim3(grid), dim3(256), 0, st, gx, bias, Wt, hs, cs, acts, \
-                     out, lens, xb, e, T, B, ntile)
-  if (H == 64) LAUNCH_F(64);
-  else if (H == 128) LAUNCH_F(128);
-  else LAUNCH_F(256);
+  for (int t0 = 0; t0 < ntile; t0 += nl) {
+    const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
+#define LAUNCH_F(HH)                                                                                            \
+  if (nw == 8)                                                                                                  \
+    hipLaunchKernelGGL(lstm_fwd_persistent8_kernel<HH>, dim3(grid), dim3(512), 0, st, gx, bias, Wt, hs, cs, acts, \
+                       out, lens, xb, e, T, B, ntile, t0, n);                                                   \
+  else                                                                                                          \
+    hipLaunchKernelGGL(lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256)>, dim3(grid), dim3(256), 0, st, gx,    \
+                       bias, Wt, hs, cs, acts, out, lens, xb, e, T, B, ntile, t0, n)
+    if (H == 64) LAUNCH_F(64);
+    else if (H == 128) LAUNCH_F(128);
+    else if (H == 256) LAUNCH_F(256);
+    else LAUNCH_F(512);
 #undef LAUNCH_F
+  }
 }
 
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, float* dbias, int T, int B, int H, hipStream_t st) {
-  const int grid = lstm_persistent_grid(H, B), ntile = (B + 15) / 16;
+  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H);
+  if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
-#define LAUNCH_B(HH)                                                                                          \
-  hipLaunchKernelGGL(lstm_bwd_persistent_kernel<HH>, dim3(grid), dim3(256), 0, st, dz, Wn, dout, dh_fin, dc_carry, \
-                     acts, cs, lens, xb, e, dbias, T, B, ntile)
-  if (H == 64) LAUNCH_B(64);
-  else if (H == 128) LAUNCH_B(128);
-  else LAUNCH_B(256);
+  for (int t0 = 0; t0 < ntile; t0 += nl) {
+    const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
+#define LAUNCH_B(HH)                                                                                                 \
+  if (nw == 8)                                                                                                       \
+    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin,      \
+                       dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n);                                  \
+  else                                                                                                               \
+    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4>), dim3(grid), dim3(256), 0, st, dz, Wn, \
+                       dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+    if (H == 64) LAUNCH_B(64);
+    else if (H == 128) LAUNCH_B(128);
+    else if (H == 256) LAUNCH_B(256);
+    else LAUNCH_B(512);
 #undef LAUNCH_B
+  }
 }

@@ -22,11 +22,20 @@ def _setup(H, B, T, seed):
     return g, r, lens, gx, W.contiguous(), Wn, hs, cs
 
 
-@pytest.mark.parametrize("H,B,T", [(64, 16, 9), (128, 37, 20), (256, 64, 33), (256, 200, 12)])
-def test_persistent_matches_step_kernels(H, B, T):
+# (512, *): the 8-wave kernels (W_hh register-resident at H = 512); (256, 600) and (512, 300):
+# more row tiles than one resident grid holds -> consecutive launches over row-tile ranges;
+# nw8: the 8-wave kernels at H = 256 (TSAMD_LSTM_NW=8)
+@pytest.mark.parametrize("H,B,T,nw8", [(64, 16, 9, False), (128, 37, 20, False), (256, 64, 33, False),
+                                       (256, 200, 12, False), (256, 600, 7, False), (256, 40, 25, True),
+                                       (512, 40, 21, False), (512, 64, 200, False), (512, 300, 9, False)])
+def test_persistent_matches_step_kernels(H, B, T, nw8, monkeypatch):
     from textsummarization_on_flink_amd.ops import ops
+    if nw8:
+        monkeypatch.setenv("TSAMD_LSTM_NW", "8")
     k = ops()
     assert int(k.lstm_persistent_grid(H, B)) > 0
+    if (H, B) in ((256, 600), (512, 300)):
+        assert int(k.lstm_persistent_launches(H, B)) > 1
     g, r, lens, gx, Wt, Wn, hs0, cs0 = _setup(H, B, T, 7 + H + B)
     bias = torch.randn(2, 4 * H, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5)) * 0.2
     res = {}
