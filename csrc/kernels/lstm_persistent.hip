@@ -129,15 +129,25 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   }
   gu64* xb = xbuf + (size_t)team * 2 * G;
   bool dead = false;
-  for (int s = 0; s < T; ++s) {
-    const int buf = s & 1;
-    // gate pre-activations x.W_x + b of this step: independent of the hand-off, issued first
-    float gz[4][4];
-    const float* gxs = gx + ((size_t)d * T + s) * B * G4;
+  // gate pre-activations x.W_x of step s + 1 are loaded during step s (off the recurrence's
+  // critical path: an HBM round trip per step otherwise)
+  float gzn[4][4];
+  auto load_gz = [&](int st) {
+    const float* gxs = gx + ((size_t)d * T + st) * B * G4;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) gz[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u] + gb[g];
+      for (int g = 0; g < 4; ++g) gzn[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u];
+  };
+  load_gz(0);
+  for (int s = 0; s < T; ++s) {
+    const int buf = s & 1;
+    float gz[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gz[i][g] = gzn[i][g] + gb[g];
+    if (s + 1 < T) load_gz(s + 1);
     // ---- h_s of the whole 16-row tile -> LDS
     if (s == 0) {
       for (int idx = threadIdx.x; idx < G; idx += 256) {
@@ -252,14 +262,23 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
   }
   gu64* xb = xbuf + (size_t)team * 2 * G;
   bool dead = false;
-  for (int s = 0; s < T; ++s) {
-    const int buf = s & 1;
-    float gz[2][4];
-    const float* gxs = gx + ((size_t)d * T + s) * B * G4;
+  float gzn[2][4];  // x.W_x of the next step, prefetched as in the 4-wave kernel
+  auto load_gz = [&](int st) {
+    const float* gxs = gx + ((size_t)d * T + st) * B * G4;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) gz[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u] + gb[g];
+      for (int g = 0; g < 4; ++g) gzn[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u];
+  };
+  load_gz(0);
+  for (int s = 0; s < T; ++s) {
+    const int buf = s & 1;
+    float gz[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gz[i][g] = gzn[i][g] + gb[g];
+    if (s + 1 < T) load_gz(s + 1);
     if (s == 0) {
       for (int idx = threadIdx.x; idx < G; idx += 512) {
         const int row = idx / HP, p = idx % HP;
@@ -383,17 +402,23 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
   // registers (fp32, off the recurrence's critical path), reduced over the wave's 4 row
   // groups and added once per team at the end -- replaces a 2 x 210 MB column reduction
   float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+  // dh_fin is step-invariant; c_s of step s is c_{(s-1)+1} of the next (reverse) step
+  float dhf[RPL], cn[RPL];
+#pragma unroll
+  for (int i = 0; i < RPL; ++i) {
+    const size_t ri = (size_t)rc[i] * H + u;
+    dhf[i] = dh_fin[(size_t)d * BH + ri];
+    cn[i] = cs[((size_t)d * (T + 1) + T) * BH + ri];
+  }
   for (int s = T - 1; s >= 0; --s) {
-    float dho[RPL], dhf[RPL], a4[RPL][4], cn[RPL], cpv[RPL];
+    float dho[RPL], a4[RPL][4], cpv[RPL];
 #pragma unroll
     for (int i = 0; i < RPL; ++i) {
       const size_t ri = (size_t)rc[i] * H + u;
       dho[i] = dout[((size_t)d * T + s) * BH + ri];
-      dhf[i] = dh_fin[(size_t)d * BH + ri];
       const float* ap = acts + (((size_t)d * T + s) * B + rc[i]) * G4;
 #pragma unroll
       for (int g = 0; g < 4; ++g) a4[i][g] = ap[g * H + u];
-      cn[i] = cs[((size_t)d * (T + 1) + s + 1) * BH + ri];
       cpv[i] = cs[((size_t)d * (T + 1) + s) * BH + ri];
     }
     // ---- recurrent dh for this lane's rows: own partial (LDS) + the peers' (granules)
@@ -463,6 +488,7 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
 #pragma unroll
         for (int g = 0; g < 4; ++g) dzv[g] = 0.f;
       }
+      cn[i] = cpv[i];
       const int row = row0 + i;
 #pragma unroll
       for (int g = 0; g < 4; ++g) bacc[g] += dzv[g];
@@ -518,46 +544,48 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
 }
 
 // ---------------------------------------------------------------------- launchers
-// Kernel variant: 4 waves per workgroup (16 units per wave) up to H = 256; 8 waves (8 units
-// per wave in the forward, 2 rows per lane in the backward) at H = 512, where the 4-wave
-// forward would need 256 VGPRs of W_hh per lane.  TSAMD_LSTM_NW=8 selects the 8-wave
-// kernels for smaller H too (A/B experiments).
-static int lstm_nw(int H) {
+// Kernel variants (measured, tools/lstm_micro.py): the forward runs 4 waves per workgroup
+// (16 units per wave) up to H = 256 and 8 waves (8 units per wave) at H = 512, where the
+// 4-wave forward would need 256 VGPRs of W_hh per lane; the backward runs 8 waves (2 rows
+// per lane in the cell update) at every H -- 4.0 vs 4.6 us per step at H = 256, B = 256.
+// TSAMD_LSTM_NW=4/8 forces one variant for both below H = 512 (A/B experiments).
+static int lstm_nw(int H, bool bwd) {
   if (H == 512) return 8;
   const char* e = getenv("TSAMD_LSTM_NW");  // read per call: tests switch it in-process
-  return (e && atoi(e) == 8) ? 8 : 4;
+  if (e && (atoi(e) == 4 || atoi(e) == 8)) return atoi(e);
+  return bwd ? 8 : 4;
 }
 
 static bool lstm_h_ok(int H) { return H == 64 || H == 128 || H == 256 || H == 512; }
 
 // Workgroups of the persistent kernels the current device keeps resident at once: one per
-// CU (launch bounds (64 NW, 1); the occupancy query must admit at least that), times the CU
-// count the runtime reports -- not an assumed 256, so a partitioned or smaller device
-// shrinks the admissible grid instead of spinning into the hand-off timeout.
+// CU (launch bounds (64 NW, 1); the occupancy query must admit at least that for every
+// variant), times the CU count the runtime reports -- not an assumed 256, so a partitioned
+// or smaller device shrinks the admissible grid instead of spinning into the hand-off timeout.
 int lstm_persistent_capacity(int H) {
-  static int cache[64][4][2] = {};  // [device][log2(H/64)][NW == 8] -> capacity + 1
+  static int cache[64][4] = {};  // [device][log2(H/64)] -> capacity + 1
   int dev = 0;
   if (!lstm_h_ok(H) || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  const int hi = H == 64 ? 0 : H == 128 ? 1 : H == 256 ? 2 : 3, nw = lstm_nw(H), wi = nw == 8;
-  if (cache[dev][hi][wi]) return cache[dev][hi][wi] - 1;
-  int cus = 0, ob = 0, of = 0;
+  const int hi = H == 64 ? 0 : H == 128 ? 1 : H == 256 ? 2 : 3;
+  if (cache[dev][hi]) return cache[dev][hi] - 1;
+  int cus = 0, o[4] = {1, 1, 1, 1};
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
-  hipError_t eb = hipErrorInvalidValue, ef = hipErrorInvalidValue;
-#define OCC(HH)                                                                                               \
-  if (H == HH) {                                                                                              \
-    if (nw == 8) {                                                                                            \
-      eb = hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, lstm_bwd_persistent_kernel<HH, 8>, 512, 0);      \
-      ef = hipOccupancyMaxActiveBlocksPerMultiprocessor(&of, lstm_fwd_persistent8_kernel<HH>, 512, 0);        \
-    } else if (HH <= 256) {                                                                                   \
-      eb = hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4>, 256, 0); \
-      ef = hipOccupancyMaxActiveBlocksPerMultiprocessor(&of, lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256)>, \
-                                                        256, 0);                                              \
-    }                                                                                                         \
+  bool ok = true;
+#define OCC(HH)                                                                                                    \
+  if (H == HH) {                                                                                                   \
+    ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[0], lstm_bwd_persistent_kernel<HH, 8>, 512, 0) == hipSuccess; \
+    ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[1], lstm_fwd_persistent8_kernel<HH>, 512, 0) == hipSuccess; \
+    if (HH <= 256) {                                                                                               \
+      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[2], lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4>, \
+                                                         256, 0) == hipSuccess;                                    \
+      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[3], lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256)>, \
+                                                         256, 0) == hipSuccess;                                    \
+    }                                                                                                              \
   }
   OCC(64) OCC(128) OCC(256) OCC(512)
 #undef OCC
-  const int cap = (eb == hipSuccess && ef == hipSuccess && ob >= 1 && of >= 1) ? cus : 0;
-  cache[dev][hi][wi] = cap + 1;
+  const int cap = (ok && o[0] >= 1 && o[1] >= 1 && o[2] >= 1 && o[3] >= 1) ? cus : 0;
+  cache[dev][hi] = cap + 1;
   return cap;
 }
 
@@ -591,7 +619,7 @@ size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {
 void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
                                 int H, hipStream_t st) {
-  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H);
+  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H, false);
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
@@ -615,7 +643,7 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, float* dbias, int T, int B, int H, hipStream_t st) {
-  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H);
+  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H, true);
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;

@@ -24,14 +24,16 @@ def _setup(H, B, T, seed):
 
 # (512, *): the 8-wave kernels (W_hh register-resident at H = 512); (256, 600) and (512, 300):
 # more row tiles than one resident grid holds -> consecutive launches over row-tile ranges;
-# nw8: the 8-wave kernels at H = 256 (TSAMD_LSTM_NW=8)
-@pytest.mark.parametrize("H,B,T,nw8", [(64, 16, 9, False), (128, 37, 20, False), (256, 64, 33, False),
-                                       (256, 200, 12, False), (256, 600, 7, False), (256, 40, 25, True),
-                                       (512, 40, 21, False), (512, 64, 200, False), (512, 300, 9, False)])
-def test_persistent_matches_step_kernels(H, B, T, nw8, monkeypatch):
+# nw: TSAMD_LSTM_NW forcing the 8-wave (or the 4-wave) kernels in both directions below H = 512
+# (default: 4-wave forward, 8-wave backward)
+@pytest.mark.parametrize("H,B,T,nw", [(64, 16, 9, None), (128, 37, 20, None), (256, 64, 33, None),
+                                      (256, 200, 12, None), (256, 600, 7, None), (256, 40, 25, "8"),
+                                      (256, 72, 19, "4"), (128, 30, 11, "4"),
+                                      (512, 40, 21, None), (512, 64, 200, None), (512, 300, 9, None)])
+def test_persistent_matches_step_kernels(H, B, T, nw, monkeypatch):
     from textsummarization_on_flink_amd.ops import ops
-    if nw8:
-        monkeypatch.setenv("TSAMD_LSTM_NW", "8")
+    if nw:
+        monkeypatch.setenv("TSAMD_LSTM_NW", nw)
     k = ops()
     assert int(k.lstm_persistent_grid(H, B)) > 0
     if (H, B) in ((256, 600), (512, 300)):
