@@ -18,12 +18,12 @@
 #include "common.h"
 
 __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
-    const float* __restrict__ gx,     // [2][T][B][4H]  x.W_x (step frame, bias-free GEMM)
+    const float* __restrict__ gx,     // [2][T][B][H][4]  x.W_x, gate-interleaved (step frame, bias-free GEMM)
     const float* __restrict__ bias,   // [2][4H]        gate biases b
     const bf16* __restrict__ Wt,      // [2][4H][H]     W_hh^T
     bf16* __restrict__ hs,            // [2][T+1][B][H] h entering step s (bf16)
     float* __restrict__ cs,           // [2][T+1][B][H] c entering step s
-    float* __restrict__ acts,         // [2][T][B][4H]  sig(i) tanh(j) sig(f+1) sig(o)
+    float* __restrict__ acts,         // [2][T][B][H][4]  (sig(i), tanh(j), sig(f+1), sig(o)) per unit
     bf16* __restrict__ out,           // [B][T][2H]
     const int* __restrict__ lens, int s, int T, int B, int H) {
   __shared__ float red[4 * 4 * 256];
@@ -36,13 +36,14 @@ __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
   const bool rok = r < B;
   const int len = rok ? lens[r] : 0;
   const bool active = s < len;
-  const float* gxs = gx + ((size_t)d * T + s) * B * G + (size_t)(rok ? r : 0) * G;
+  const float4 gq = *reinterpret_cast<const float4*>(gx + ((((size_t)d * T + s) * B + (rok ? r : 0)) * H + u) * 4);
+  const float gxv[4] = {gq.x, gq.y, gq.z, gq.w};
   const bf16* hprev = hs + ((size_t)d * (T + 1) + s) * BH;
   const float* cprev = cs + ((size_t)d * (T + 1) + s) * BH;
   const size_t ri = (size_t)(rok ? r : 0) * H + u;
   float gz[4], cp;  // unconditional: no lens -> address dependence on the critical path
 #pragma unroll
-  for (int g = 0; g < 4; ++g) gz[g] = gxs[g * H + u] + bias[(size_t)d * G + g * H + u];
+  for (int g = 0; g < 4; ++g) gz[g] = gxv[g] + bias[(size_t)d * G + g * H + u];
   cp = cprev[ri];
   // ---- h_{s-1} . W_hh, K split over the 4 waves
   const int ar = min(r0 + (lane & 15), B - 1);
@@ -68,8 +69,7 @@ __global__ __launch_bounds__(256) void lstm_enc_fwd_step_kernel(
     const float h = og * ftanh(c);
     cnext[ri] = c;
     hnext[ri] = f2bf(h);
-    float* a4 = acts + ((size_t)d * T + s) * B * G + (size_t)r * G;
-    a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
+    *reinterpret_cast<float4*>(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4) = make_float4(ig, jg, fg, og);
     const int t = d == 0 ? s : len - 1 - s;
     out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(h);
   } else {
@@ -107,9 +107,10 @@ __global__ __launch_bounds__(256) void lstm_enc_bwd_step_kernel(
   float a4[4];
   const float dho = dout[((size_t)d * T + s) * BH + ri];
   const float dhf = dh_fin[(size_t)d * BH + ri];
-  const float* ap = acts + ((size_t)d * T + s) * B * G + (size_t)(rok ? r : 0) * G;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) a4[g] = ap[g * H + u];
+  {
+    const float4 q = *reinterpret_cast<const float4*>(acts + ((((size_t)d * T + s) * B + (rok ? r : 0)) * H + u) * 4);
+    a4[0] = q.x; a4[1] = q.y; a4[2] = q.z; a4[3] = q.w;
+  }
   const float cn = cs[((size_t)d * (T + 1) + s + 1) * BH + ri];
   const float cpv = cs[((size_t)d * (T + 1) + s) * BH + ri];
   const float dcin = dc_carry[(size_t)d * BH + ri];

@@ -21,7 +21,7 @@
 // Every spin is bounded: on timeout the workgroup records a code in *err and stops waiting
 // (results are then garbage, but the grid always drains).
 //
-// Layouts are those of lstm.hip (step frame; hs/cs [2][T+1][B][H], acts [2][T][B][4H],
+// Layouts are those of lstm.hip (step frame; gx and acts [2][T][B][H][4 gates], hs/cs [2][T+1][B][H],
 // out [B][T][2H], dz [2][T][B][4H]), so the two implementations are interchangeable.
 #include "common.h"
 #include <stdlib.h>
@@ -135,9 +135,10 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   auto load_gz = [&](int st) {
     const float* gxs = gx + ((size_t)d * T + st) * B * G4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) gzn[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u];
+    for (int i = 0; i < 4; ++i) {
+      const float4 q = *reinterpret_cast<const float4*>(gxs + ((size_t)rc[i] * H + u) * 4);
+      gzn[i][0] = q.x; gzn[i][1] = q.y; gzn[i][2] = q.z; gzn[i][3] = q.w;
+    }
   };
   load_gz(0);
   for (int s = 0; s < T; ++s) {
@@ -176,27 +177,20 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) acc[g] = mfma16(a, Wf[g][kk], acc[g]);
     }
-    // ---- cell update, 4 rows x 1 unit per lane
-    float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
-    bf16* hnext = hs + ((size_t)d * (T + 1) + s + 1) * BH;
+    // ---- cell update, 4 rows x 1 unit per lane (gates kept in registers: stored after the
+    // hand-off below, so the granule stores are not queued behind ~6 MB of activation stores
+    // per step -- that ordering cost ~4 us per step at H = 512, B = 256)
+    float ga[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int r = rc[i];
       if (s < ln[i]) {
-        const float ig = fsigmoid(acc[0][i] + gz[i][0]), jg = ftanh(acc[1][i] + gz[i][1]);
-        const float fg = fsigmoid(acc[2][i] + gz[i][2] + 1.0f), og = fsigmoid(acc[3][i] + gz[i][3]);
-        const float cc = fg * creg[i] + ig * jg;
-        const float h = bf2f(f2bf(og * ftanh(cc)));
+        ga[i][0] = fsigmoid(acc[0][i] + gz[i][0]);
+        ga[i][1] = ftanh(acc[1][i] + gz[i][1]);
+        ga[i][2] = fsigmoid(acc[2][i] + gz[i][2] + 1.0f);
+        ga[i][3] = fsigmoid(acc[3][i] + gz[i][3]);
+        const float cc = ga[i][2] * creg[i] + ga[i][0] * ga[i][1];
         creg[i] = cc;
-        hreg[i] = h;
-        float* a4 = acts + (((size_t)d * T + s) * B + r) * G4;
-        a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
-        const int t = d == 0 ? s : ln[i] - 1 - s;
-        out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(h);
-      }
-      if (rok[i]) {
-        cnext[(size_t)r * H + u] = creg[i];
-        hnext[(size_t)r * H + u] = f2bf(hreg[i]);
+        hreg[i] = bf2f(f2bf(ga[i][3] * ftanh(cc)));
       }
     }
     // ---- publish h_{s+1}: unit pairs (u, u+1) of adjacent lanes -> one granule
@@ -207,6 +201,22 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         const float hn = __shfl_xor(hreg[i], 1, 64);
         if (!(lane & 1)) store_granule(dst + ((lane >> 4) * 4 + i) * HP + u / 2, (unsigned)(s + 1),
                                        pack_bf2(hreg[i], hn));
+      }
+    }
+    float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
+    bf16* hnext = hs + ((size_t)d * (T + 1) + s + 1) * BH;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rc[i];
+      if (s < ln[i]) {
+        *reinterpret_cast<float4*>(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4) =
+            make_float4(ga[i][0], ga[i][1], ga[i][2], ga[i][3]);  // one 16-byte store per (row, unit)
+        const int t = d == 0 ? s : ln[i] - 1 - s;
+        out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(hreg[i]);
+      }
+      if (rok[i]) {
+        cnext[(size_t)r * H + u] = creg[i];
+        hnext[(size_t)r * H + u] = f2bf(hreg[i]);
       }
     }
   }
@@ -266,9 +276,10 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
   auto load_gz = [&](int st) {
     const float* gxs = gx + ((size_t)d * T + st) * B * G4;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) gzn[i][g] = gxs[(size_t)rc[i] * G4 + g * H + u];
+    for (int i = 0; i < 2; ++i) {
+      const float4 q = *reinterpret_cast<const float4*>(gxs + ((size_t)rc[i] * H + u) * 4);
+      gzn[i][0] = q.x; gzn[i][1] = q.y; gzn[i][2] = q.z; gzn[i][3] = q.w;
+    }
   };
   load_gz(0);
   for (int s = 0; s < T; ++s) {
@@ -311,28 +322,19 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
       rcv[i] = dpp_f<DPP_ROR8>(half ? acc[0][i] : acc[0][2 + i]);
       rcv[2 + i] = dpp_f<DPP_ROR8>(half ? acc[1][i] : acc[1][2 + i]);
     }
-    float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
-    bf16* hnext = hs + ((size_t)d * (T + 1) + s + 1) * BH;
+    float ga[2][4];  // gates: stored after the hand-off (see the 4-wave kernel)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int r = rc[i];
       if (s < ln[i]) {
         const float zi = half ? rcv[i] : acc[0][i], zj = half ? acc[0][2 + i] : rcv[i];
         const float zf = half ? rcv[2 + i] : acc[1][i], zo = half ? acc[1][2 + i] : rcv[2 + i];
-        const float ig = fsigmoid(zi + gz[i][0]), jg = ftanh(zj + gz[i][1]);
-        const float fg = fsigmoid(zf + gz[i][2] + 1.0f), og = fsigmoid(zo + gz[i][3]);
-        const float cc = fg * creg[i] + ig * jg;
-        const float h = bf2f(f2bf(og * ftanh(cc)));
+        ga[i][0] = fsigmoid(zi + gz[i][0]);
+        ga[i][1] = ftanh(zj + gz[i][1]);
+        ga[i][2] = fsigmoid(zf + gz[i][2] + 1.0f);
+        ga[i][3] = fsigmoid(zo + gz[i][3]);
+        const float cc = ga[i][2] * creg[i] + ga[i][0] * ga[i][1];
         creg[i] = cc;
-        hreg[i] = h;
-        float* a4 = acts + (((size_t)d * T + s) * B + r) * G4;
-        a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
-        const int t = d == 0 ? s : ln[i] - 1 - s;
-        out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(h);
-      }
-      if (rok[i]) {
-        cnext[(size_t)r * H + u] = creg[i];
-        hnext[(size_t)r * H + u] = f2bf(hreg[i]);
+        hreg[i] = bf2f(f2bf(ga[i][3] * ftanh(cc)));
       }
     }
     if (s + 1 < T) {
@@ -341,6 +343,22 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
       for (int i = 0; i < 2; ++i) {
         const float hn = dpp_f<DPP_XOR1>(hreg[i]);  // unit u + 1 (lane n ^ 1, same half)
         if (!(lane & 1)) store_granule(dst + rt[i] * HP + u / 2, (unsigned)(s + 1), pack_bf2(hreg[i], hn));
+      }
+    }
+    float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
+    bf16* hnext = hs + ((size_t)d * (T + 1) + s + 1) * BH;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = rc[i];
+      if (s < ln[i]) {
+        *reinterpret_cast<float4*>(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4) =
+            make_float4(ga[i][0], ga[i][1], ga[i][2], ga[i][3]);  // one 16-byte store per (row, unit)
+        const int t = d == 0 ? s : ln[i] - 1 - s;
+        out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(hreg[i]);
+      }
+      if (rok[i]) {
+        cnext[(size_t)r * H + u] = creg[i];
+        hnext[(size_t)r * H + u] = f2bf(hreg[i]);
       }
     }
   }
@@ -416,9 +434,8 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
     for (int i = 0; i < RPL; ++i) {
       const size_t ri = (size_t)rc[i] * H + u;
       dho[i] = dout[((size_t)d * T + s) * BH + ri];
-      const float* ap = acts + (((size_t)d * T + s) * B + rc[i]) * G4;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) a4[i][g] = ap[g * H + u];
+      const float4 q = *reinterpret_cast<const float4*>(acts + ((((size_t)d * T + s) * B + rc[i]) * H + u) * 4);
+      a4[i][0] = q.x; a4[i][1] = q.y; a4[i][2] = q.z; a4[i][3] = q.w;
       cpv[i] = cs[((size_t)d * (T + 1) + s) * BH + ri];
     }
     // ---- recurrent dh for this lane's rows: own partial (LDS) + the peers' (granules)
@@ -494,13 +511,22 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
       for (int g = 0; g < 4; ++g) bacc[g] += dzv[g];
 #pragma unroll
       for (int g = 0; g < 4; ++g) Ash[swz<256>(row, g * 64 + ul)] = f2bf(dzv[g]);
-      if (rok[i]) {
-        bf16* dzr = dz + (((size_t)d * T + s) * B + rc[i]) * G4;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) dzr[g * H + u] = f2bf(dzv[g]);
-      }
     }
-    if (s == 0) break;
+    // dz rows -> global from the LDS copy, issued after this step's hand-off stores (as in the
+    // forward: the granules must not queue behind the activation traffic)
+    auto store_dz = [&]() {
+#pragma unroll
+      for (int i = 0; i < RPL; ++i)
+        if (rok[i]) {
+          bf16* dzr = dz + (((size_t)d * T + s) * B + rc[i]) * G4;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) dzr[g * H + u] = Ash[swz<256>(row0 + i, g * 64 + ul)];
+        }
+    };
+    if (s == 0) {
+      store_dz();  // own-lane LDS values: no barrier needed
+      break;
+    }
     __syncthreads();  // dz slice complete in LDS (and every lane has read Pown)
     // ---- partial dh over this slice's gate columns, for units 64*wid .. +63
     if (wid < NC) {
@@ -529,6 +555,7 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
                         __float_as_uint(acc[t][r]));
     }
     }
+    store_dz();
     __syncthreads();  // Pown visible before the next step reads it; Ash free for rewriting
   }
 #pragma unroll

@@ -162,10 +162,10 @@ class HipPointerGenerator:
             self.enc.append({
                 "din": din,
                 "x_sf": z(2, T, B, din, dt=BF),          # step-frame inputs (bw reversed)
-                "gx": z(2, T, B, 4 * H),
+                "gx": z(2, T, B, 4 * H),                 # [2][T][B][H][4 gates]
                 "hs": z(2, T + 1, B, H, dt=BF),
                 "cs": z(2, T + 1, B, H),
-                "acts": z(2, T, B, 4 * H),
+                "acts": z(2, T, B, 4 * H),               # [2][T][B][H][4 gates]
                 "out": z(B, T, A, dt=BF),
                 "dz": z(2, T, B, 4 * H, dt=BF),
                 "dout": z(B, T, A),
@@ -283,6 +283,9 @@ class HipPointerGenerator:
             for di, d in enumerate(("fw", "bw")):
                 K = p[enc_k(layer, d)]
                 put(f"enc{layer}_Kx{di}", K[:din])
+                # forward copy with gate-interleaved columns (u*4 + g): the x.W_x GEMM then
+                # writes gx as [T][B][H][4], one 16-byte load per (row, unit) in the recurrence
+                put(f"enc{layer}_Kxi{di}", K[:din].reshape(din, 4, self.H).transpose(1, 2).reshape(din, 4 * self.H))
             Kh = torch.stack([p[enc_k(layer, d)][din:] for d in ("fw", "bw")])  # [2][H][4H]
             put(f"enc{layer}_Wn", Kh)
             put(f"enc{layer}_Wt", Kh.transpose(1, 2))
@@ -382,7 +385,7 @@ class HipPointerGenerator:
             else:
                 k.to_step_frame(x, None, rev, xs, B, T, din, 0)
             for di in range(2):  # x.W_x, bias added in the recurrence kernel
-                mm_into(st["gx"][di].view(T * B, 4 * H), xs[di].view(T * B, din), self.pk[f"enc{layer}_Kx{di}"])
+                mm_into(st["gx"][di].view(T * B, 4 * H), xs[di].view(T * B, din), self.pk[f"enc{layer}_Kxi{di}"])
             st["hs"][:, 0].zero_()
             st["cs"][:, 0].zero_()
             st["out"].zero_()
