@@ -186,6 +186,37 @@ def test_linear2_matches_fp32(B, K1, K2, N, use_add):
     assert (outb.float() - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("R", [256, 37])
+def test_linear2_pair_matches_two_linear2(R):
+    """The beam step's pair launch at the shipped shape (H=256, A=512, E=128): problem 0 is the
+    attention query s = [c, h].W_s + b (N = A = 512), problem 1 the in-place x-merge
+    x += ctx.W_in[E:] (M = E = 128 < N, add aliases out; column tiles past M exit early).
+    Both must equal separate linear2 launches and the fp32 reference; R = 37 is not a
+    multiple of 16 (partial row tile)."""
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    torch.manual_seed(3)
+    H, A, E = 256, 512, 128
+    c = torch.randn(R, H, device="cuda").bfloat16()
+    h = torch.randn(R, H, device="cuda").bfloat16()
+    ctx = torch.randn(R, A, device="cuda").bfloat16()
+    WsT = (torch.randn(A, 2 * H, device="cuda") * 0.05).bfloat16()
+    bs = torch.randn(A, device="cuda")
+    WicT = (torch.randn(E, A, device="cuda") * 0.05).bfloat16()
+    x0 = torch.randn(R, E, device="cuda")
+    s_pair, x_pair = torch.zeros(R, A, device="cuda"), x0.clone()
+    k.linear2_pair(c, H, h, H, WsT, bs, None, s_pair, None, A, ctx, A, None, 0, WicT, None, x_pair, x_pair, None, E, R)
+    s_one, x_one = torch.zeros(R, A, device="cuda"), x0.clone()
+    k.linear2(c, H, h, H, WsT, bs, None, s_one, None, R, A)
+    k.linear2(ctx, A, None, 0, WicT, None, x_one, x_one, None, R, E)
+    torch.cuda.synchronize()
+    assert torch.equal(s_pair, s_one) and torch.equal(x_pair, x_one)
+    s_ref = torch.cat([c.float(), h.float()], 1) @ WsT.float().t() + bs
+    x_ref = x0 + ctx.float() @ WicT.float().t()
+    assert (s_pair - s_ref).abs().max().item() < 1e-3 * s_ref.abs().max().item() + 1e-4
+    assert (x_pair - x_ref).abs().max().item() < 1e-3 * x_ref.abs().max().item() + 1e-4
+
+
 def test_pgen_matches_fp32():
     from textsummarization_on_flink_amd.ops import ops
     k = ops()

@@ -164,8 +164,10 @@ def _accessors(cls, info: ParamInfo, short: str, camel: Optional[str] = None):
 
 # ---------------------------------------------------------------------- mixins
 class HasClusterConfig(WithParams):
-    """HasClusterConfig.java:14-53 (ZooKeeper is replaced by a TCPStore rendezvous; the
-    connect string is kept for API parity and used as MASTER_ADDR:port when it names a host)."""
+    """HasClusterConfig.java:14-53.  ZooKeeper is replaced by a torch.distributed TCPStore
+    rendezvous: ``WorkerJob`` (api/worker.py) starts every worker on this host with
+    MASTER_ADDR=127.0.0.1 and a free port.  The connect string is kept for API and JSON parity
+    only; it is not used to locate the rendezvous."""
     ZOOKEEPER_CONNECT_STR = ParamInfo("zookeeper_connect_str", str, "zookeeper address to connect", True,
                                       "127.0.0.1:2181")
     WORKER_NUM = ParamInfo("worker_num", int, "worker number", True, 1)
