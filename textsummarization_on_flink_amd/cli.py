@@ -107,8 +107,29 @@ def load_params_into(hps, params):
     ckpt.load_ckpt(hps.log_root, params, "train", max_retries=hps.load_retries, load_adagrad=False)
 
 
+def loader_workers(hps) -> int:
+    """Worker processes of the multi-process input pipeline for GPU training: ``--loader_workers``
+    (0 = the threaded Batcher), default (-1) min(8, CPUs - 2).  The threaded Batcher builds
+    ~0.7k examples/s under the GIL; the B = 256 step consumes ~12k/s."""
+    if hps.mode != "train" or hps.inference or not hps.pad_enc_to_max or torch.cuda.device_count() == 0:
+        return 0
+    if hps.loader_workers >= 0:
+        return hps.loader_workers
+    return max(1, min(8, (os.cpu_count() or 4) - 2))
+
+
 def main(argv: Optional[Sequence[str]] = None) -> int:
     hps = parse_flags(sys.argv[1:] if argv is None else argv, known_only=True)
+    loader = None
+    nw = loader_workers(hps)
+    if nw:
+        # fork the loader workers before anything initialises the GPU (init_from_env does
+        # under data parallelism); device_count() above does not
+        from .data.loader import ProcessBatcher
+        rank = int(os.environ.get("RANK", "0"))
+        loader = ProcessBatcher(hps.data_path, Vocab(hps.vocab_path, hps.vocab_size), hps,
+                                single_pass=hps.single_pass, workers=nw, seed=hps.seed + rank,
+                                pad_enc_to=hps.max_enc_steps)
     info = init_from_env(timeout_s=hps.dist_timeout_s) if hps.mode == "train" else DistInfo()
     vocab, hps = default_setup(hps, info)
     metrics = metrics_for(hps, info)
@@ -120,11 +141,17 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                 decode_distinct=n > 1, pad_enc_to=pad))
             dec.decode(with_rouge=False)
         elif hps.mode == "train":
-            batcher = Batcher(hps.data_path, vocab, hps, single_pass=hps.single_pass, seed=hps.seed + info.rank,
-                              pad_enc_to=hps.max_enc_steps if (torch.cuda.is_available() and hps.pad_enc_to_max)
-                              else None)
+            if loader is not None:  # Example/Batch construction in the forked workers
+                batcher = loader
+            else:
+                pad = hps.max_enc_steps if (torch.cuda.device_count() > 0 and hps.pad_enc_to_max) else None
+                batcher = Batcher(hps.data_path, vocab, hps, single_pass=hps.single_pass, seed=hps.seed + info.rank,
+                                  pad_enc_to=pad)
             from .train.loop import setup_training
-            setup_training(hps, vocab, batcher, info=info, metrics=metrics)
+            try:
+                setup_training(hps, vocab, batcher, info=info, metrics=metrics)
+            finally:
+                batcher.stop()
         elif hps.mode == "eval":
             batcher = Batcher(hps.data_path, vocab, hps, single_pass=hps.single_pass, seed=hps.seed,
                               pad_enc_to=hps.max_enc_steps if torch.cuda.is_available() else None)

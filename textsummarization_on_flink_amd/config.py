@@ -85,7 +85,8 @@ class HParams:
     log_file: str = ""             # rotating log file, 100 MB x 20 (log4j2.xml); one file per rank
     check_every: int = 10          # host reads loss / NaN / LSTM-error flags every N steps (1 = every step)
     grad_compress: str = "none"    # DP gradient all-reduce wire format: none (fp32) | bf16
-    loader_workers: int = 0        # >0: Example/Batch construction in N worker processes (pinned packs)
+    loader_workers: int = -1       # GPU training input pipeline: N worker processes (0 = threaded Batcher,
+                                   # -1 = min(8, CPUs - 2)); see data/loader.py
 
     # ------------------------------------------------------------------ helpers
     def replace(self, **kw) -> "HParams":

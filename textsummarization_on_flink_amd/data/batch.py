@@ -29,20 +29,20 @@ class Example:
         self.uuid = uuid
         start_decoding = vocab.word2id(START_DECODING)
         stop_decoding = vocab.word2id(STOP_DECODING)
-        article_words = article.split()
+        article_words = article.split(None, hps.max_enc_steps)  # stops after the kept words
         if len(article_words) > hps.max_enc_steps:
             article_words = article_words[:hps.max_enc_steps]
         self.enc_len = len(article_words)
-        self.enc_input = [vocab.word2id(w) for w in article_words]
+        self.enc_input = vocab.ids(article_words)
         abstract = " ".join(abstract_sentences)
         abstract_words = abstract.split()
-        abs_ids = [vocab.word2id(w) for w in abstract_words]
+        abs_ids = vocab.ids(abstract_words)
         self.dec_input, self.target = self.get_dec_inp_targ_seqs(abs_ids, hps.max_dec_steps, start_decoding,
                                                                  stop_decoding)
         self.dec_len = len(self.dec_input)
         if hps.pointer_gen:
-            self.enc_input_extend_vocab, self.article_oovs = article2ids(article_words, vocab)
-            abs_ids_extend_vocab = abstract2ids(abstract_words, vocab, self.article_oovs)
+            self.enc_input_extend_vocab, self.article_oovs = article2ids(article_words, vocab, self.enc_input)
+            abs_ids_extend_vocab = abstract2ids(abstract_words, vocab, self.article_oovs, abs_ids)
             _, self.target = self.get_dec_inp_targ_seqs(abs_ids_extend_vocab, hps.max_dec_steps, start_decoding,
                                                         stop_decoding)
         else:

@@ -50,9 +50,10 @@ def read_bin(path: str) -> Iterator[bytes]:
             yield s
 
 
-def example_generator(data_path: str, single_pass: bool, rng: Optional[random.Random] = None
-                      ) -> Iterator[Dict[str, List]]:
-    """Yield decoded tf.Examples; forever in shuffled file order unless single_pass."""
+def example_generator(data_path: str, single_pass: bool, rng: Optional[random.Random] = None,
+                      decode: bool = True) -> Iterator[Dict[str, List]]:
+    """Yield decoded tf.Examples (raw records with ``decode=False``); forever in shuffled
+    file order unless single_pass."""
     rng = rng or random.Random()
     while True:
         filelist = glob.glob(data_path)
@@ -64,7 +65,7 @@ def example_generator(data_path: str, single_pass: bool, rng: Optional[random.Ra
             rng.shuffle(filelist)
         for fn in filelist:
             for rec in read_bin(fn):
-                yield decode_example(rec)
+                yield decode_example(rec) if decode else rec
         if single_pass:
             log.info("example_generator completed reading all datafiles. No more data.")
             return

@@ -56,6 +56,12 @@ class Vocab:
     def word2id(self, word: str) -> int:
         return self._word_to_id.get(word, 0)
 
+    def ids(self, words: Sequence[str]) -> List[int]:
+        """word2id over a token list (one bound dict lookup per token: the host loader's
+        hot loop)."""
+        get = self._word_to_id.get
+        return [get(w, 0) for w in words]
+
     def id2word(self, word_id: int) -> str:
         if not 0 <= word_id < len(self._id_to_word):
             raise ValueError(f"Id not found in vocab: {word_id}")
@@ -84,33 +90,38 @@ class Vocab:
                 f.write(f"{w} {counts[i] if counts else 1}\n")
 
 
-def article2ids(article_words: Sequence[str], vocab: Vocab) -> Tuple[List[int], List[str]]:
-    """In-article OOVs get temporary ids vocab.size()+k (``data.py:144-168``)."""
-    ids, oovs, index = [], [], {}
+def article2ids(article_words: Sequence[str], vocab: Vocab,
+                ids: Optional[Sequence[int]] = None) -> Tuple[List[int], List[str]]:
+    """In-article OOVs get temporary ids vocab.size()+k (``data.py:144-168``).  ``ids``:
+    the words' plain vocab ids if already computed (only the [UNK] positions are revisited)."""
+    out = list(vocab.ids(article_words) if ids is None else ids)
+    oovs: List[str] = []
+    if 0 not in out:
+        return out, oovs
+    index = {}
     V = vocab.size()
-    for w in article_words:
-        i = vocab.word2id(w)
+    for k, i in enumerate(out):
         if i == 0:
+            w = article_words[k]
             if w not in index:
                 index[w] = len(oovs)
                 oovs.append(w)
-            ids.append(V + index[w])
-        else:
-            ids.append(i)
-    return ids, oovs
+            out[k] = V + index[w]
+    return out, oovs
 
 
-def abstract2ids(abstract_words: Sequence[str], vocab: Vocab, article_oovs: Sequence[str]) -> List[int]:
+def abstract2ids(abstract_words: Sequence[str], vocab: Vocab, article_oovs: Sequence[str],
+                 ids: Optional[Sequence[int]] = None) -> List[int]:
     """In-article OOVs -> temporary id; other OOVs -> [UNK] (``data.py:171-193``)."""
+    out = list(vocab.ids(abstract_words) if ids is None else ids)
+    if not article_oovs or 0 not in out:
+        return out
     index = {w: k for k, w in reversed(list(enumerate(article_oovs)))}
     V = vocab.size()
-    out = []
-    for w in abstract_words:
-        i = vocab.word2id(w)
+    for k, i in enumerate(out):
         if i == 0:
-            out.append(V + index[w] if w in index else 0)
-        else:
-            out.append(i)
+            w = abstract_words[k]
+            out[k] = V + index[w] if w in index else 0
     return out
 
 

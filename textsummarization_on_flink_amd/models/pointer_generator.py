@@ -89,6 +89,72 @@ def mmf(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.mm(a, b, out_dtype=F32)
 
 
+def host_inputs(batch, hps, D: int) -> Dict[str, np.ndarray]:
+    """The engine's per-batch inputs as host arrays (pure numpy: runs in loader worker
+    processes too): token ids, lengths, the reversed-index map of the backward LSTM
+    direction, extended-vocab ids, step-major decoder inputs / targets and the per-(step,
+    row) loss weights of the reference's loss averaging (``model.py:252-268``)."""
+    T = batch.enc_batch.shape[1]
+    lens = batch.enc_lens.astype(np.int64)
+    if lens.min() < 1:
+        raise ValueError("empty article in batch")
+    t = np.arange(T)[None, :]
+    rev = np.where(t < lens[:, None], lens[:, None] - 1 - t, t)
+    valid = batch.valid.astype(np.float64)
+    nvalid = valid.sum()
+    if batch.dec_batch.shape[1] < D:
+        raise ValueError(f"batch has {batch.dec_batch.shape[1]} decoder steps, engine needs {D}")
+    dm = batch.dec_padding_mask[:, :D].astype(np.float64)
+    dec_lens = dm.sum(1)
+    if hps.pointer_gen:
+        rowg = dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
+    else:  # sequence_loss: sum(mask*CE)/sum(mask)
+        wm = dm * valid[:, None]
+        rowg = wm / wm.sum()
+    gcl = hps.cov_loss_wt * dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
+    return {
+        "enc_batch": batch.enc_batch.astype(np.int64),
+        "enc_lens": batch.enc_lens.astype(np.int32),
+        "rev_idx": rev.astype(np.int64),
+        "ext": batch.enc_batch_extend_vocab.astype(np.int32),
+        "dec_batch_t": np.ascontiguousarray(batch.dec_batch[:, :D].T).astype(np.int64),
+        "target_t": np.ascontiguousarray(batch.target_batch[:, :D].T).astype(np.int32),
+        "rowg": np.ascontiguousarray(rowg.T).astype(np.float32),
+        "gcl": np.ascontiguousarray(gcl.T).astype(np.float32),
+    }
+
+
+_NP = {torch.long: np.int64, torch.int32: np.int32, F32: np.float32}
+
+
+def input_layout(B: int, T: int, D: int):
+    """Byte layout of the engine's input pack: [(name, offset, shape, torch dtype, nbytes)],
+    total size (every array 256-byte aligned); the device copy is one buffer with views."""
+    shapes = {"BT": (B, T), "B": (B,), "DB": (D, B)}
+    layout, off = [], 0
+    for name, sk, dt in (("enc_batch", "BT", torch.long), ("enc_lens", "B", torch.int32),
+                         ("rev_idx", "BT", torch.long), ("ext", "BT", torch.int32),
+                         ("dec_batch_t", "DB", torch.long), ("target_t", "DB", torch.int32),
+                         ("rowg", "DB", F32), ("gcl", "DB", F32)):
+        shp = shapes[sk]
+        nb = int(np.prod(shp)) * np.dtype(_NP[dt]).itemsize
+        layout.append((name, off, shp, dt, nb))
+        off += (nb + 255) // 256 * 256
+    return layout, off
+
+
+def pack_host_inputs(host: Dict[str, np.ndarray], layout, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """host_inputs arrays -> one uint8 buffer in ``layout`` order (``out`` if given)."""
+    if out is None:
+        out = np.zeros(layout[-1][1] + (layout[-1][4] + 255) // 256 * 256, dtype=np.uint8)
+    for name, o, shp, dt, nb in layout:
+        a = np.ascontiguousarray(host[name], dtype=_NP[dt])
+        if a.shape != tuple(shp):
+            raise ValueError(f"input {name}: shape {a.shape} != {tuple(shp)}")
+        out[o:o + nb] = a.reshape(-1).view(np.uint8)
+    return out
+
+
 class HipPointerGenerator:
     """Fixed-shape (B rows, T encoder steps, D decoder steps) train/eval engine."""
 
@@ -136,16 +202,7 @@ class HipPointerGenerator:
         # inputs (static, copied into before every replay): views of ONE device buffer, so a
         # batch arrives with one H2D copy from a pinned host pack instead of eight (each
         # in-stream copy costs ~15 us of DMA latency ahead of the step)
-        shapes = {"BT": (B, T), "B": (B,), "DB": (D, B)}
-        layout, off = [], 0
-        for name, sk, dt in (("enc_batch", "BT", torch.long), ("enc_lens", "B", torch.int32),
-                             ("rev_idx", "BT", torch.long), ("ext", "BT", torch.int32),
-                             ("dec_batch_t", "DB", torch.long), ("target_t", "DB", torch.int32),
-                             ("rowg", "DB", F32), ("gcl", "DB", F32)):
-            shp = shapes[sk]
-            nb = int(np.prod(shp)) * torch.empty(0, dtype=dt).element_size()
-            layout.append((name, off, shp, dt, nb))
-            off += (nb + 255) // 256 * 256
+        layout, off = input_layout(B, T, D)
         self._in_layout = layout
         self._in_pack = torch.zeros(off, dtype=torch.uint8, device=self.dev)
         for name, o, shp, dt, nb in layout:
@@ -326,44 +383,23 @@ class HipPointerGenerator:
 
     # ------------------------------------------------------------------ inputs
     def set_batch(self, batch) -> None:
-        """Host batch -> static device buffers (H2D copies; pinned staging)."""
-        import numpy as np
-        hps, w, B, T, D = self.hps, self.w, self.B, self.T, self.D
+        """Host batch -> static device buffers: one H2D copy of a pinned pack.  A batch from
+        the multi-process loader (data/loader.py) arrives with ``host_pack`` already built
+        by a worker process; otherwise it is built here."""
+        B, T = self.B, self.T
         if batch.enc_batch.shape != (B, T):
             raise ValueError(f"batch enc shape {batch.enc_batch.shape} != engine shape {(B, T)}")
-        lens = batch.enc_lens.astype(np.int64)
-        if lens.min() < 1:
-            raise ValueError("empty article in batch")
-        t = np.arange(T)[None, :]
-        rev = np.where(t < lens[:, None], lens[:, None] - 1 - t, t)
-        valid = batch.valid.astype(np.float64)
-        nvalid = valid.sum()
-        if batch.dec_batch.shape[1] < D:
-            raise ValueError(f"batch has {batch.dec_batch.shape[1]} decoder steps, engine needs {D}")
-        dm = batch.dec_padding_mask[:, :D].astype(np.float64)
-        dec_lens = dm.sum(1)
-        if hps.pointer_gen:
-            rowg = dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
-        else:  # sequence_loss: sum(mask*CE)/sum(mask)
-            wm = dm * valid[:, None]
-            rowg = wm / wm.sum()
-        gcl = hps.cov_loss_wt * dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
-        host = {
-            "enc_batch": batch.enc_batch.astype(np.int64),
-            "enc_lens": batch.enc_lens.astype(np.int32),
-            "rev_idx": rev.astype(np.int64),
-            "ext": batch.enc_batch_extend_vocab.astype(np.int32),
-            "dec_batch_t": np.ascontiguousarray(batch.dec_batch[:, :D].T).astype(np.int64),
-            "target_t": np.ascontiguousarray(batch.target_batch[:, :D].T).astype(np.int32),
-            "rowg": np.ascontiguousarray(rowg.T).astype(np.float32),
-            "gcl": np.ascontiguousarray(gcl.T).astype(np.float32),
-        }
+        packed = getattr(batch, "host_pack", None)  # bytes in input_layout order, or None
         i = self._in_i
         if self._in_ev[i] is not None:
             self._in_ev[i].synchronize()  # the copy out of this pack (two batches ago) is done
         hn = self._in_host[i].numpy()
-        for name, o, shp, dt, nb in self._in_layout:
-            hn[o:o + nb] = np.ascontiguousarray(host[name]).reshape(-1).view(np.uint8)
+        if packed is not None:
+            if len(packed) != hn.nbytes:
+                raise ValueError(f"host pack of {len(packed)} bytes, engine expects {hn.nbytes}")
+            hn[:] = np.frombuffer(packed, dtype=np.uint8)
+        else:
+            pack_host_inputs(host_inputs(batch, self.hps, self.D), self._in_layout, hn)
         self._in_pack.copy_(self._in_host[i], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
