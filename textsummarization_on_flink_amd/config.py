@@ -68,6 +68,8 @@ class HParams:
     pad_enc_to_max: bool = True    # static shapes for hipGraph capture (padding is masked)
     graph: bool = True             # capture the train step / decode step in hipGraphs
     decode_batch: int = 64         # articles decoded together (beam-as-batch x articles)
+    stream_max_wait_ms: float = 0.0   # streaming decode: queued requests always share a batch; after
+                                      # the first, wait at most this long for more (0 = no waiting)
     save_model_secs: int = 60      # Supervisor(save_model_secs=60), run_summarization.py:199
     max_to_keep: int = 3           # Saver(max_to_keep=3)
     log_every: int = 1

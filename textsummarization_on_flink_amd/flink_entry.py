@@ -77,7 +77,8 @@ def inference_on_flink(context, hps):
     writer = FlinkWriter(context)
     reader = context.reader()
     dec = cli.build_decoder(hps, vocab, lambda h, n, pad: FlinkInferenceBatcher(
-        reader, vocab, h.replace(batch_size=h.beam_size), n_articles=n, pad_enc_to=pad), writer=writer)
+        reader, vocab, h.replace(batch_size=h.beam_size), n_articles=n, pad_enc_to=pad,
+        max_wait_s=hps.stream_max_wait_ms / 1000.0), writer=writer)
     dec.decode(with_rouge=False)
 
 
