@@ -286,6 +286,41 @@ void cast_colsum(const Tensor& x, const Tensor& xb, const Tensor& colsum, int64_
   launch_cast_colsum(P<float>(x), P<bf16>(xb), P<float>(part), P<float>(colsum), (int)N, (int)C, stream());
 }
 
+// ---------------------------------------------------------------- reduce_states
+// cs / hs: the top encoder layer's step-frame states [2][T+1][B][H]; the kernels read rows T.
+void rs_fwd(const Tensor& cs, const Tensor& hs, int64_t T, const Tensor& RCt, const Tensor& RHt, const Tensor& bc,
+            const Tensor& bh, const Tensor& pre_c, const Tensor& pre_h, const Tensor& c0, const Tensor& c0b,
+            const Tensor& h0b, const OT& cat_c, const OT& cat_h, int64_t B, int64_t H) {
+  chk(cs, F32, "cs"); chk(hs, BF, "hs"); chk(RCt, BF, "RCt"); chk(RHt, BF, "RHt"); chk(bc, F32, "bc"); chk(bh, F32, "bh");
+  chk(pre_c, F32, "pre_c"); chk(pre_h, F32, "pre_h"); chk(c0, F32, "c0"); chk(c0b, BF, "c0b"); chk(h0b, BF, "h0b");
+  TORCH_CHECK(H % 32 == 0 && H <= 512, "reduce_states: H % 32 == 0, H <= 512");
+  numel_eq(cs, 2 * (T + 1) * B * H, "cs"); numel_eq(hs, 2 * (T + 1) * B * H, "hs");
+  numel_eq(RCt, 2 * H * H, "RCt"); numel_eq(RHt, 2 * H * H, "RHt"); numel_eq(bc, H, "bc"); numel_eq(bh, H, "bh");
+  numel_eq(pre_c, B * H, "pre_c"); numel_eq(pre_h, B * H, "pre_h"); numel_eq(c0, B * H, "c0");
+  numel_eq(c0b, B * H, "c0b"); numel_eq(h0b, B * H, "h0b");
+  chko(cat_c, BF, 2 * B * H, "cat_c"); chko(cat_h, BF, 2 * B * H, "cat_h");
+  const size_t off = (size_t)T * B * H, ds = (size_t)(T + 1) * B * H;
+  launch_rs_fwd(P<float>(cs) + off, P<bf16>(hs) + off, ds, P<bf16>(RCt), P<bf16>(RHt), P<float>(bc), P<float>(bh),
+                P<float>(pre_c), P<float>(pre_h), P<float>(c0), P<bf16>(c0b), P<bf16>(h0b), PO<bf16>(cat_c),
+                PO<bf16>(cat_h), (int)B, (int)H, stream());
+}
+
+// dold_c / dold_h: [2][B][H] (fw, bw) seeds of the encoder BPTT
+void rs_bwd(const Tensor& gc, const Tensor& gh, const Tensor& pre_c, const Tensor& pre_h, const Tensor& RC,
+            const Tensor& RH, const Tensor& dpc, const Tensor& dph, const Tensor& gbc, const Tensor& gbh,
+            const Tensor& dold_c, const Tensor& dold_h, int64_t B, int64_t H) {
+  chk(gc, F32, "gc"); chk(gh, F32, "gh"); chk(pre_c, F32, "pre_c"); chk(pre_h, F32, "pre_h"); chk(RC, BF, "RC");
+  chk(RH, BF, "RH"); chk(dpc, BF, "dpc"); chk(dph, BF, "dph"); chk(gbc, F32, "gbc"); chk(gbh, F32, "gbh");
+  chk(dold_c, F32, "dold_c"); chk(dold_h, F32, "dold_h");
+  TORCH_CHECK(H % 32 == 0 && H <= 512, "reduce_states: H % 32 == 0, H <= 512");
+  for (const Tensor* t : {&gc, &gh, &pre_c, &pre_h, &dpc, &dph}) numel_eq(*t, B * H, "[B][H] operand");
+  numel_eq(RC, 2 * H * H, "RC"); numel_eq(RH, 2 * H * H, "RH"); numel_eq(gbc, H, "gbc"); numel_eq(gbh, H, "gbh");
+  numel_eq(dold_c, 2 * B * H, "dold_c"); numel_eq(dold_h, 2 * B * H, "dold_h");
+  launch_rs_bwd(P<float>(gc), P<float>(gh), P<float>(pre_c), P<float>(pre_h), P<bf16>(RC), P<bf16>(RH), P<bf16>(dpc),
+                P<bf16>(dph), P<float>(gbc), P<float>(gbh), P<float>(dold_c), P<float>(dold_h), (size_t)B * H, (int)B,
+                (int)H, stream());
+}
+
 // ---------------------------------------------------------------- embedding gradient
 void emb_grad(const Tensor& gemb, const Tensor& ids0, const Tensor& src0, const Tensor& ids1, const Tensor& src1) {
   chk(gemb, F32, "gemb"); chk(src0, F32, "src0"); chk(src1, F32, "src1");
@@ -598,6 +633,8 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("lstm_persistent_grid", &lstm_persistent_grid_op);
   m.def("lstm_persistent_capacity", &lstm_persistent_capacity_op);
   m.def("lstm_persistent_launches", &lstm_persistent_launches_op);
+  m.def("rs_fwd", &rs_fwd);
+  m.def("rs_bwd", &rs_bwd);
   m.def("lstm_persistent_xbuf", &lstm_persistent_xbuf_op);
   m.def("lstm_fwd_persistent", &lstm_fwd_persistent);
   m.def("lstm_bwd_persistent", &lstm_bwd_persistent);

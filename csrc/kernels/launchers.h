@@ -109,6 +109,14 @@ void launch_ptr_rowfin(const float* pv, const int* target, const float* rowg, co
                        const int* ext, const int* lens, float* loss_row, float* alpha, float* dpre, float* dA, int N,
                        int B, int T, hipStream_t st);
 
+// reduce_states.hip
+void launch_rs_fwd(const float* c_fw, const bf16* h_fw, size_t dstride, const bf16* RCt, const bf16* RHt,
+                   const float* bc, const float* bh, float* pre_c, float* pre_h, float* c0, bf16* c0b, bf16* h0b,
+                   bf16* cat_c, bf16* cat_h, int B, int H, hipStream_t st);
+void launch_rs_bwd(const float* gc, const float* gh, const float* pre_c, const float* pre_h, const bf16* RC,
+                   const bf16* RH, bf16* dpc, bf16* dph, float* gbc, float* gbh, float* dold_c, float* dold_h,
+                   size_t dstride, int B, int H, hipStream_t st);
+
 // embedding.hip
 void launch_emb_grad(float* gemb, const int64_t* ids0, const float* src0, int n0, const int64_t* ids1,
                      const float* src1, int n1, int E, int V, hipStream_t st);

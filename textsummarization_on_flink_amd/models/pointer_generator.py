@@ -240,6 +240,10 @@ class HipPointerGenerator:
             w["lstm_xb"] = z(int(self.k.lstm_persistent_xbuf(H, B, True)), dt=torch.long)
             w["lstm_db"] = z(2, 4 * H)  # gate-bias gradients [fw; bw] accumulated by the BPTT kernel
         w["lstm_err"] = z(1, dt=torch.int32)
+        # reduce_states: pre-activations [c; h], bf16 [fw, bw] inputs and bf16 dp (wgrad operands)
+        w["rs_pre"] = z(2, B, H)
+        w["rs_cat"] = z(2, B, 2 * H, dt=BF)
+        w["rs_dp"] = z(2, B, H, dt=BF)
         # one fused attention-backward kernel per decoder step (attn_bwd_step);
         # TSAMD_ATTN_BWD_FUSED=0 selects the two-kernel path (attn_bwd_da over Et + attn_bwd_tanh)
         self.fused_attn_bwd = os.environ.get("TSAMD_ATTN_BWD_FUSED", "1") != "0"
@@ -349,6 +353,8 @@ class HipPointerGenerator:
         put("Wh", p[WH].reshape(A, A))
         put("RC", p[RC])
         put("RH", p[RH])
+        put("RCt", p[RC].t())  # [H][2H]: "Bt" operand of the fused reduce_states forward
+        put("RHt", p[RH].t())
         M = p[LIN_M]
         put("lin_emb", M[:E])
         put("Wic", M[E:])
@@ -435,16 +441,10 @@ class HipPointerGenerator:
                                         st["out"], lens, s, T, B, H)
             x = st["out"]
         top = self.enc[-1]
-        old_c = torch.cat([top["cs"][0, T], top["cs"][1, T]], 1)
-        old_h = torch.cat([top["hs"][0, T], top["hs"][1, T]], 1).float()
-        # bf16 operands: the fp32 [256 x 512] x [512 x 256] GEMM ran as ONE 256x256 tile (~120 us)
-        pc = mmf(old_c.to(BF), self.pk["RC"]) + self.p[BRC]
-        ph = mmf(old_h.to(BF), self.pk["RH"]) + self.p[BRH]
-        self._red = (old_c, old_h, pc, ph)
-        c0, h0 = torch.relu(pc), torch.relu(ph)
-        w["Cst"][0].copy_(c0)
-        w["Cb"][0].copy_(c0)
-        w["Hb"][0].copy_(h0)
+        # reduce_states: [c_fw, c_bw] / [h_fw, h_bw] -> relu(. W + b) -> the decoder's initial
+        # state, one launch (reduce_states.hip) reading the encoder's final states in place
+        k.rs_fwd(top["cs"], top["hs"], T, self.pk["RCt"], self.pk["RHt"], self.p[BRC], self.p[BRH], w["rs_pre"][0],
+                 w["rs_pre"][1], w["Cst"][0], w["Cb"][0], w["Hb"][0], w["rs_cat"][0], w["rs_cat"][1], B, H)
         mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["Wh"])
         if self.keep_ft:
             if w["Ft"] is None:
@@ -502,10 +502,9 @@ class HipPointerGenerator:
         w["outb"].copy_(out)
         pg = None
         if hps.pointer_gen:
-            pm = p[PG_M][:, 0]
-            pre = (w["CTX"].view(N, A) @ pm[:A] + w["Cst"][1:].reshape(N, H) @ pm[A:A + H]
-                   + Hn.float() @ pm[A + H:A + 2 * H] + w["X"].view(N, E) @ pm[A + 2 * H:] + p[PG_B])
-            w["pg"].view(N).copy_(torch.sigmoid(pre))
+            # p_gen = sigmoid([ctx, c, h, x] . w + b) for all D*B rows, one wave per row (decoder.hip)
+            self.k.pgen(w["CTX"].view(N, A), w["Cst"][1:].reshape(N, H), Hn, w["X"].view(N, E), p[PG_M].view(-1),
+                        p[PG_B], w["pg"].view(N), N, A, H, E)
             pg = w["pg"]
         if self.fused_vocab:
             k, ldx = self.k, H + 8  # outb is the first H columns of outb_ext
@@ -738,16 +737,13 @@ class HipPointerGenerator:
         g = p.g
         dE, d_emb_dec = self._dE, self._d_emb_dec
         lens = w["enc_lens"]
-        # ---- reduce_states
-        old_c, old_h, pc, ph = self._red
-        dpc = w["dc_carry"] * (pc > 0)
-        dph = w["dh_rec"] * (ph > 0)
-        g(RC).copy_(old_c.t() @ dpc)
-        g(BRC).copy_(dpc.sum(0))
-        g(RH).copy_(old_h.t() @ dph)
-        g(BRH).copy_(dph.sum(0))
-        d_old_c = dpc @ self.p[RC].t()
-        d_old_h = dph @ self.p[RH].t()
+        # ---- reduce_states (reduce_states.hip): dp = g [pre > 0], bias gradients, and
+        # d[c_fw, c_bw] / d[h_fw, h_bw] written straight into the top layer's BPTT seeds
+        top = self.enc[-1]
+        k.rs_bwd(w["dc_carry"], w["dh_rec"], w["rs_pre"][0], w["rs_pre"][1], self.pk["RC"], self.pk["RH"],
+                 w["rs_dp"][0], w["rs_dp"][1], g(BRC), g(BRH), top["dc_carry"], top["dh_fin"], B, H)
+        torch.mm(w["rs_cat"][0].t(), w["rs_dp"][0], out_dtype=F32, out=g(RC))
+        torch.mm(w["rs_cat"][1].t(), w["rs_dp"][1], out_dtype=F32, out=g(RH))
         # ---- encoder BPTT, top layer down
         d_in = dE
         gemb = g(EMB)
@@ -756,10 +752,7 @@ class HipPointerGenerator:
             din = st["din"]
             # dL/dh_out in step frame: fw as is, bw reversed within each length
             k.to_step_frame(d_in, None, w["rev_idx"], st["dout"], B, T, H, H)
-            if layer == self.L - 1:
-                st["dh_fin"][0].copy_(d_old_h[:, :H]); st["dh_fin"][1].copy_(d_old_h[:, H:])
-                st["dc_carry"][0].copy_(d_old_c[:, :H]); st["dc_carry"][1].copy_(d_old_c[:, H:])
-            else:
+            if layer != self.L - 1:  # the top layer's seeds came from rs_bwd
                 st["dh_fin"].zero_()
                 st["dc_carry"].zero_()
             if self.persistent_lstm:
