@@ -166,17 +166,19 @@ void attn_bwd_tanh(const Tensor& F, const Tensor& s, const Tensor& v, const OT& 
 bool attn_row_ok(int64_t A, int64_t T) { return attn_row_supported((int)A, (int)T); }
 void attn_fwd_row(const Tensor& F, const Tensor& E, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                   const Tensor& lens, const Tensor& a_out, const OT& cov_out, const OT& covloss, const Tensor& ctx,
-                  const OT& ctx_bf, int64_t B, int64_t T, int64_t A) {
+                  const OT& ctx_bf, int64_t B, int64_t T, int64_t A, int64_t rep) {
+  // rep: hypothesis rows per feature row (beam decode: the rep beams of an article share F/E)
   chk(F, BF, "F"); chk(E, BF, "E"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens");
   chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
   TORCH_CHECK(attn_row_supported((int)A, (int)T), "row attention needs A in {512, 1024} and T <= 2048");
-  numel_eq(F, B * T * A, "F"); numel_eq(E, B * T * A, "E"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v");
-  numel_eq(lens, B, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx");
+  TORCH_CHECK(rep >= 1 && B % rep == 0, "attn_fwd_row: rep must divide B");
+  numel_eq(F, B / rep * T * A, "F"); numel_eq(E, B / rep * T * A, "E"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v");
+  numel_eq(lens, B / rep, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx");
   chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out");
   chko(covloss, F32, B, "covloss"); chko(ctx_bf, BF, B * A, "ctx_bf");
   launch_attn_fwd_row(P<bf16>(F), P<bf16>(E), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens),
                       P<float>(a_out), PO<float>(cov_out), PO<float>(covloss), P<float>(ctx), PO<bf16>(ctx_bf), B, T, A,
-                      stream());
+                      (int)rep, stream());
 }
 void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                   const Tensor& a, const Tensor& dctx, const Tensor& ctx, const OT& Ga, const OT& dcov_next,

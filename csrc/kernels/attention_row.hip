@@ -62,17 +62,18 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     const bf16* __restrict__ F, const bf16* __restrict__ E, const float* __restrict__ s,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
     const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
-    float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T) {
+    float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T, int rep) {
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float es[kRowMaxT];
   __shared__ float part[NW][A];
   __shared__ float wm[NW], wl[NW], red[NW];
   const int b = blockIdx.x;
+  const int fr = b / rep;  // feature row: beam decode shares one encoder row between rep hypotheses
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int len = lens[b];
+  const int len = lens[fr];
   const size_t rb = (size_t)b * T;
-  const bf16* Fb = F + (size_t)b * T * A;
-  const bf16* Eb = E + (size_t)b * T * A;
+  const bf16* Fb = F + (size_t)fr * T * A;
+  const bf16* Eb = E + (size_t)fr * T * A;
   const int ngrp = (len + 3) >> 2;
   const int qm = lane >> 4;  // the position (within a group) whose total this lane's 16-lane group holds
   const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
@@ -350,10 +351,10 @@ bool attn_row_supported(int A, int T) { return (A == 512 || A == 1024) && T >= 1
 
 void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
                          const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
-                         bf16* ctx_bf, int B, int T, int A, hipStream_t st) {
+                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st) {
 #define LF(NK)                                                                                                 \
   hipLaunchKernelGGL((attn_fwd_row_kernel<NK, row_waves<NK, false>()>), dim3(B), dim3(row_waves<NK, false>() * 64), \
-                     0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T)
+                     0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep)
   if (A == 512) LF(1);
   else LF(2);
 #undef LF

@@ -32,7 +32,7 @@ void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, con
 bool attn_row_supported(int A, int T);
 void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
                          const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
-                         bf16* ctx_bf, int B, int T, int A, hipStream_t st);
+                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st);
 void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
                          const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
                          const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,

@@ -52,8 +52,12 @@ class DeviceBeamDecoder:
         self.maxD = hps.max_dec_steps
         self.use_graph, self.chunk, self.keep_attn = use_graph, chunk, keep_attn
         self.eng = HipPointerGenerator(hps, self.V, params, B=self.Na, T=T, D=1)
-        self.eng.keep_ft = True  # the decode-step attention kernels read the transposed features
+        # attention per step: the row-resident kernel (score + softmax + context in one launch,
+        # one workgroup per hypothesis reading its article's F/E rows) when the shape allows
+        # it, else the multi-block kernels over the transposed features (TSAMD_DEC_ROW_ATTN=0)
         self.k = self.eng.k
+        self.row_attn = (os.environ.get("TSAMD_DEC_ROW_ATTN", "1") != "0" and bool(self.k.attn_row_ok(self.eng.A, T)))
+        self.eng.keep_ft = not self.row_attn  # the multi-block score kernel reads transposed features
         self.dev = self.eng.dev
         self._alloc()
         self.refresh_weights()
@@ -68,7 +72,8 @@ class DeviceBeamDecoder:
         self._done_flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
         b = {}
         for name, shape, dt in [
-            ("Ft", (R // self.rep, A, T), BF), ("E", (R // self.rep, T, A), BF),
+            ("Ft" if not self.row_attn else "F", (R // self.rep, A, T) if not self.row_attn else (R // self.rep, T, A),
+             BF), ("E", (R // self.rep, T, A), BF),
             ("lens_att", (R // self.rep,), torch.int32),
             ("c", (R, H), F32), ("h", (R, H), BF), ("ctxs", (R, A), F32), ("ctxs_bf", (R, A), BF),
             ("x", (R, E), F32), ("Cb2", (R, H), BF), ("XG", (R, 4 * H), F32), ("act", (R, 4 * H), F32),
@@ -122,7 +127,8 @@ class DeviceBeamDecoder:
         # all ``beam`` hypotheses of the article (rep = beam)
         r = beam // self.rep
         b["E"].copy_(eng.enc[-1]["out"].repeat_interleave(r, 0) if r > 1 else eng.enc[-1]["out"])
-        b["Ft"].copy_(w["Ft"].repeat_interleave(r, 0) if r > 1 else w["Ft"])
+        fk = "F" if self.row_attn else "Ft"
+        b[fk].copy_(w[fk].repeat_interleave(r, 0) if r > 1 else w[fk])
         b["lens_att"].copy_(w["enc_lens"].repeat_interleave(r, 0) if r > 1 else w["enc_lens"])
         b["lens"].copy_(w["enc_lens"])
         b["ext"].copy_(w["ext"])
@@ -137,8 +143,7 @@ class DeviceBeamDecoder:
         X = self.st[0]
         b["Cb2"].copy_(X["C"])
         k.dec_sproj(b["Cb2"], X["H"], eng.pk["WsT"], self.p[ATT_B], b["s"], R, H, A)
-        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], None, b["lens_att"], b["e"], R, T, A, self.rep)
-        k.attn_softmax_ctx(b["e"], b["E"], b["lens_att"], None, X["ATT"], None, None, X["CTX"], None, R, T, A, self.rep)
+        self._attention(None, X["ATT"], X["CTX"], None)
         X["COV"].zero_()
         b["gidx"].copy_(torch.arange(R, dtype=torch.int32, device=self.dev))
         b["latest"].fill_(self.vocab.word2id(START_DECODING))
@@ -146,6 +151,19 @@ class DeviceBeamDecoder:
         for n in ("done", "res_count", "step", "step_ctr", "tok_hist", "par_hist", "res_len", "res_step", "res_par"):
             b[n].zero_()
         b["res_score"].fill_(-float("inf"))
+
+    def _attention(self, cov, att_out, ctx_out, ctx_bf):
+        """a_t = softmax(e_t), ctx_t = sum_i a_ti E_i for all R hypotheses (coverage, if any,
+        was already accumulated into ``cov`` by beam_gather)."""
+        k, b, eng = self.k, self.b, self.eng
+        R, T, A = self.R, self.T, eng.A
+        if self.row_attn:
+            k.attn_fwd_row(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], cov, b["lens_att"], att_out, None,
+                           None, ctx_out, ctx_bf, R, T, A, self.rep)
+            return
+        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], cov, b["lens_att"], b["e"], R, T, A, self.rep)
+        k.attn_softmax_ctx(b["e"], b["E"], b["lens_att"], None, att_out, None, None, ctx_out, ctx_bf, R, T, A,
+                           self.rep)
 
     def _step(self, parity: int):
         k, b, hps, eng, p = self.k, self.b, self.hps, self.eng, self.p
@@ -164,10 +182,7 @@ class DeviceBeamDecoder:
                            b["ctxs_bf"], A, None, 0, eng.pk["WicT"], None, b["x"], b["x"], None, E, R)
         else:
             k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
-        k.attn_score(b["Ft"], b["s"], eng.f32["v"], eng.f32["wc"], Y["COV"] if cov else None, b["lens_att"],
-                     b["e"], R, T, A, self.rep)
-        k.attn_softmax_ctx(b["e"], b["E"], b["lens_att"], None, Y["ATT"], None, None, Y["CTX"], b["ctx_bf"], R, T, A,
-                           self.rep)
+        self._attention(Y["COV"] if cov else None, Y["ATT"], Y["CTX"], b["ctx_bf"])
         pg = None
         if hps.pointer_gen:
             k.pgen(Y["CTX"], Y["C"], Y["H"], b["x"], self.pg_w, p[PG_B], b["PG"], R, A, H, E)

@@ -477,7 +477,7 @@ class HipPointerGenerator:
                 if self.row_attn:
                     k.attn_fwd_row(F[rs], enc_out[rs], w["S"][t][rs], v, wc, cov_in, lens[rs], w["ATT"][t][rs],
                                    w["COV"][t + 1][rs] if cov else None, w["covloss"][t][rs] if cov else None,
-                                   w["CTX"][t][rs], w["CTXb"][t][rs], Bg, T, A)
+                                   w["CTX"][t][rs], w["CTXb"][t][rs], Bg, T, A, 1)
                     continue
                 k.attn_score(Ft[rs], w["S"][t][rs], v, wc, cov_in, lens[rs], w["e"][rs], Bg, T, A, 1)
                 k.attn_softmax_ctx(w["e"][rs], enc_out[rs], lens[rs], cov_in, w["ATT"][t][rs],
