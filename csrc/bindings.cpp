@@ -516,7 +516,33 @@ void vocab_topk(const Tensor& X, const Tensor& WT, const Tensor& bias, const OT&
   TORCH_CHECK(!PO<float>(pgen) || PO<float>(attn), "pointer mode needs attn");
   launch_vocab_topk(P<bf16>(X), P<bf16>(WT), P<float>(bias), PO<float>(pgen), PO<float>(attn), P<int>(ext),
                     P<int>(lens), P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), R, V, H, T,
-                    K, beam, stream());
+                    K, beam, PgIn{}, stream());
+}
+// vocab_topk with p_gen = sigmoid([ctx, c, h, x] . w + b) computed inside the select kernel
+// (written to pg_out for the beam histories)
+void vocab_topk_pg(const Tensor& X, const Tensor& WT, const Tensor& bias, const Tensor& ctx, const Tensor& c,
+                   const Tensor& h, const Tensor& x, const Tensor& pg_w, const Tensor& pg_b, const Tensor& pg_out,
+                   const Tensor& attn, const Tensor& ext, const Tensor& lens, const Tensor& out_ids,
+                   const Tensor& out_lp, const Tensor& logits, const Tensor& part_ms, int64_t R, int64_t V, int64_t H,
+                   int64_t T, int64_t K, int64_t beam, int64_t A, int64_t E) {
+  chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(ext, I32, "ext"); chk(lens, I32, "lens");
+  chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp"); chk(logits, F32, "logits"); chk(part_ms, F32, "part_ms");
+  chk(ctx, F32, "ctx"); chk(c, F32, "c"); chk(h, BF, "h"); chk(x, F32, "x"); chk(pg_w, F32, "pg_w");
+  chk(pg_b, F32, "pg_b"); chk(pg_out, F32, "pg_out"); chk(attn, F32, "attn");
+  const int64_t nt = vocab_topk_tiles((int)V);
+  TORCH_CHECK(K >= 1 && K <= 8 && beam >= 1 && R % beam == 0 && T <= 2048, "bad vocab_topk args (K <= 8)");
+  TORCH_CHECK(H % 32 == 0 && H <= 256 && nt <= 4096, "vocab_topk: H % 32 == 0, H <= 256, V <= 1M");
+  numel_eq(X, R * H, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias");
+  numel_eq(ext, (R / beam) * T, "ext"); numel_eq(lens, R / beam, "lens");
+  numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
+  numel_eq(logits, R * V, "logits"); numel_eq(part_ms, R * nt * 2, "part_ms"); numel_eq(attn, R * T, "attn");
+  numel_eq(ctx, R * A, "ctx"); numel_eq(c, R * H, "c"); numel_eq(h, R * H, "h"); numel_eq(x, R * E, "x");
+  numel_eq(pg_w, A + 2 * H + E, "pg_w"); numel_eq(pg_b, 1, "pg_b"); numel_eq(pg_out, R, "pg_out");
+  const PgIn pgi{P<float>(ctx), P<float>(c), P<bf16>(h), P<float>(x), P<float>(pg_w), P<float>(pg_b),
+                 P<float>(pg_out), (int)A, (int)H, (int)E};
+  launch_vocab_topk(P<bf16>(X), P<bf16>(WT), P<float>(bias), nullptr, P<float>(attn), P<int>(ext), P<int>(lens),
+                    P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), R, V, H, T, K, beam, pgi,
+                    stream());
 }
 int64_t vocab_topk_parts(int64_t V) { return vocab_topk_tiles((int)V); }
 
@@ -636,6 +662,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("lstm_persistent_capacity", &lstm_persistent_capacity_op);
   m.def("lstm_persistent_launches", &lstm_persistent_launches_op);
   m.def("rs_fwd", &rs_fwd);
+  m.def("vocab_topk_pg", &vocab_topk_pg);
   m.def("rs_bwd", &rs_bwd);
   m.def("lstm_persistent_xbuf", &lstm_persistent_xbuf_op);
   m.def("lstm_fwd_persistent", &lstm_fwd_persistent);

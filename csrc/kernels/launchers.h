@@ -96,9 +96,14 @@ void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, con
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, float* dbias, int T, int B, int H, hipStream_t st);
 int vocab_topk_tiles(int V);
+// p_gen inputs computed inside the vocab select kernel (w == nullptr: p_gen given instead)
+struct PgIn {
+  const float* ctx; const float* c; const bf16* h; const float* x; const float* w; const float* b; float* out;
+  int A, H, E;
+};
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
-                       int R, int V, int H, int T, int K, int beam, hipStream_t st);
+                       int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st);
 int vocab_train_tiles(int V);
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
                             float* zg, float* lse, float* pv, int N, int V, int H, hipStream_t st);

@@ -12,6 +12,7 @@
 //                       union copied ids).
 // Replaces a library GEMM + a separate per-element top-k pass over the logits.
 #include "common.h"
+#include "launchers.h"
 
 #define VT_COLS 256   // vocab columns per workgroup
 #define VT_ROWS 64    // rows per workgroup
@@ -252,10 +253,13 @@ __device__ __forceinline__ void pad4(float* v, int* id, int n) {
 
 // grid R, 1024 threads.  Two global round trips: (partials, copy ids, attention) issued
 // together, then (the K best tiles' logits, the copied words' logits) issued together.
+// With pg.w set the kernel also computes p_gen = sigmoid([ctx, c, h, x] . w + b) of its row
+// (reference attention_decoder.py:164-168; one launch less per decode step) and stores it
+// to pg.out; otherwise p_gen comes from ``pgen`` (nullptr for both: baseline, no pointer).
 __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     const float* __restrict__ logits, const float* __restrict__ part_ms, const float* __restrict__ pgen,
     const float* __restrict__ attn, const int* __restrict__ ext, const int* __restrict__ lens,
-    int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam, int nt) {
+    int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam, int nt, PgIn pgi) {
   __shared__ int hkey[VM_HASH];
   __shared__ float hmass[VM_HASH];
   __shared__ __attribute__((aligned(16))) float cv[VM_CAND + 8];
@@ -272,8 +276,20 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   constexpr int TPT = 2048 / VS_THREADS;     // source positions per thread (T <= 2048)
   constexpr int SPT = VM_HASH / VS_THREADS;  // hash slots per thread
   // ---- round trip 1: tile partials, copy ids and attention, all in flight together
-  const float pg = pgen ? pgen[r] : 1.0f;
-  const int len = pgen ? lens[art] : 0;
+  const bool ptr = pgen || pgi.w;
+  float pg = pgen ? pgen[r] : 1.0f;
+  float pgd = 0.f;  // this thread's share of the p_gen pre-activation
+  if (pgi.w) {
+    const int A = pgi.A, H = pgi.H;
+    for (int i = tid; i < A + 2 * H + pgi.E; i += VS_THREADS) {
+      const float x = i < A ? pgi.ctx[(size_t)r * A + i]
+                    : i < A + H ? pgi.c[(size_t)r * H + i - A]
+                    : i < A + 2 * H ? bf2f(pgi.h[(size_t)r * H + i - A - H])
+                    : pgi.x[(size_t)r * pgi.E + i - A - 2 * H];
+      pgd += x * pgi.w[i];
+    }
+  }
+  const int len = ptr ? lens[art] : 0;
   float2 pm[PPT];
 #pragma unroll
   for (int u = 0; u < PPT; ++u) {
@@ -295,7 +311,11 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   float m = -INFINITY;
 #pragma unroll
   for (int u = 0; u < PPT; ++u) m = fmaxf(m, pm[u].x);
-  __syncthreads();  // hash cleared before the inserts below
+  if (pgi.w) {  // uniform branch: block_sum's barriers are reached by every thread
+    pg = fsigmoid(block_sum<VS_THREADS>(pgd, red) + pgi.b[0]);
+    if (tid == 0 && pgi.out) pgi.out[r] = pg;
+  }
+  __syncthreads();  // hash cleared before the inserts below (and red free for block_max)
   // pointer copy mass per extended-vocab word (LDS hash)
 #pragma unroll
   for (int u = 0; u < TPT; ++u) {
@@ -436,7 +456,7 @@ int vocab_topk_tiles(int V) { return (V + VT_COLS - 1) / VT_COLS; }
 
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
-                       int R, int V, int H, int T, int K, int beam, hipStream_t st) {
+                       int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st) {
   const int nt = vocab_topk_tiles(V);
   const int RB = (R + VT_ROWS - 1) / VT_ROWS;
   static const int occ = getenv("TSAMD_VL_OCC") ? atoi(getenv("TSAMD_VL_OCC")) : 2;
@@ -447,5 +467,5 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
     hipLaunchKernelGGL(vocab_logits_kernel<2>, dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
                        part_ms, R, V, H);
   hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
-                     out_lp, V, T, K, beam, nt);
+                     out_lp, V, T, K, beam, nt, pgi);
 }

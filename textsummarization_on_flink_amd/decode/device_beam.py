@@ -183,14 +183,18 @@ class DeviceBeamDecoder:
         else:
             k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
         self._attention(Y["COV"] if cov else None, Y["ATT"], Y["CTX"], b["ctx_bf"])
-        pg = None
-        if hps.pointer_gen:
+        pg = b["PG"] if hps.pointer_gen else None
+        if hps.pointer_gen and not self.fused_vocab:
             k.pgen(Y["CTX"], Y["C"], Y["H"], b["x"], self.pg_w, p[PG_B], b["PG"], R, A, H, E)
-            pg = b["PG"]
         k.linear2(Y["H"], H, b["ctx_bf"], A, eng.pk["OUTmT"], p[OUT_B], None, None, b["outb"], R, H)
-        if self.fused_vocab:
-            k.vocab_topk(b["outb"], self.owT, p[OV], pg, Y["ATT"] if hps.pointer_gen else None, b["ext"], b["lens"],
-                         b["top_ids"], b["top_lp"], b["logits"], b["vpart_ms"], R, V, H, T, K, self.beam)
+        if self.fused_vocab and hps.pointer_gen:
+            # p_gen is computed inside the select kernel (into b["PG"] for the histories)
+            k.vocab_topk_pg(b["outb"], self.owT, p[OV], Y["CTX"], Y["C"], Y["H"], b["x"], self.pg_w, p[PG_B], b["PG"],
+                            Y["ATT"], b["ext"], b["lens"], b["top_ids"], b["top_lp"], b["logits"], b["vpart_ms"], R,
+                            V, H, T, K, self.beam, A, E)
+        elif self.fused_vocab:
+            k.vocab_topk(b["outb"], self.owT, p[OV], None, None, b["ext"], b["lens"], b["top_ids"], b["top_lp"],
+                         b["logits"], b["vpart_ms"], R, V, H, T, K, self.beam)
         else:
             torch.mm(b["outb"], eng.pk["ow"], out_dtype=F32, out=b["logits"])
             k.final_topk(b["logits"], p[OV], pg, Y["ATT"] if hps.pointer_gen else None, b["ext"], b["lens"],
