@@ -17,6 +17,22 @@
 // K split across the waves (kslice_mma) and summed in LDS (ksplit_reduce).
 #include "common.h"
 
+// XCD-aware tile order for the (column tile, row tile) grids below.  Blocks are dealt to
+// the 8 XCDs round-robin by linear id; every block of a column tile re-reads that tile's
+// weight rows, so the column tiles are split into 8 contiguous ranges, one per XCD: each
+// XCD's L2 then holds 1/8 of the weight matrix (at hidden 512 the cell / dz weights are
+// 6-7 MB, more than one XCD's 4 MB L2).  Falls back to the plain order when gx % 8 != 0.
+__device__ __forceinline__ void xcd_tile(int& tx, int& ty) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  tx = blockIdx.x;
+  ty = blockIdx.y;
+  if (gx % 8) return;
+  const int L = blockIdx.y * gx + blockIdx.x, xcd = L & 7, q = L >> 3, cpx = gx >> 3;
+  tx = xcd * cpx + q % cpx;
+  ty = q / cpx;
+  (void)gy;
+}
+
 // z = XG + [ctx, h] . WcT^T ; cell update.  WcT: [4H][A+H] (cols 0..A-1 = W_comb^T, A.. = W_cell[E:]^T).
 // grid (H/16, ceil(B/16)).
 __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
@@ -30,7 +46,9 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
     int B, int H, int A) {
   __shared__ float red[4 * 4 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
+  int tx, ty;
+  xcd_tile(tx, ty);
+  const int u0 = tx * 16, r0 = ty * 16;
   const int G = 4 * H, K = A + H;
   const int r = r0 + (lane >> 4) * 4 + wid, u = u0 + (lane & 15);
   const bool rok = r < B;
@@ -104,7 +122,9 @@ __device__ __forceinline__ void linear2_body(const L2Args& p, int B, int n0, int
 
 __global__ __launch_bounds__(256) void linear2_kernel(L2Args p, int B) {
   __shared__ float red[4 * 256];
-  linear2_body(p, B, blockIdx.x * 16, blockIdx.y * 16, red);
+  int tx, ty;
+  xcd_tile(tx, ty);
+  linear2_body(p, B, tx * 16, ty * 16, red);
 }
 
 // Two independent linear2 problems on the same rows in one launch (blockIdx.z picks the
@@ -173,7 +193,9 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
     bf16* __restrict__ dz, int B, int H, int A) {
   __shared__ float red[4 * 2 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int u0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
+  int tx, ty;
+  xcd_tile(tx, ty);
+  const int u0 = tx * 16, r0 = ty * 16;
   const int r = r0 + (lane >> 4) * 4 + wid, u = u0 + (lane & 15);
   const bool rok = r < B;
   const size_t ri = (size_t)(rok ? r : 0) * H + u;
@@ -225,7 +247,9 @@ __global__ __launch_bounds__(256) void dec_bwd_dz_kernel(
     float* __restrict__ dh_rec, int B, int E, int H, int A) {
   __shared__ float red[4 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
+  int tx, ty;
+  xcd_tile(tx, ty);
+  const int n0 = tx * 16, r0 = ty * 16;
   if (n0 >= E + H && !dctx_prev_out) return;  // uniform per block
   const int G = 4 * H;
   const int ar = min(r0 + (lane & 15), B - 1);
