@@ -332,11 +332,10 @@ class HipPointerGenerator:
         pk = getattr(self, "pk", None) or {}
 
         def put(name, t):
-            t = t.to(BF)
             if name in pk and pk[name].shape == t.shape:
-                pk[name].copy_(t)
+                pk[name].copy_(t)  # one cast(+transpose) kernel into the persistent bf16 buffer
             else:
-                pk[name] = t.contiguous()
+                pk[name] = t.to(BF).contiguous()
 
         put("emb", p[EMB])
         for layer in range(self.L):

@@ -59,7 +59,7 @@ def main():
     if eng.k.attn_row_ok(eng.A, T):
         res["attn_fwd_row"] = timeit(lambda: eng.k.attn_fwd_row(F, enc_out, w["S"][t], v, wc, w["COV"][t], lens,
                                                                  w["ATT"][t], w["COV"][t + 1], w["covloss"][t],
-                                                                 w["CTX"][t], w["CTXb"][t], B, T, eng.A))
+                                                                 w["CTX"][t], w["CTXb"][t], B, T, eng.A, 1))
         res["attn_bwd_row"] = timeit(lambda: eng.k.attn_bwd_row(enc_out, F, w["S"][t], v, wc, w["COV"][t],
                                                                  w["ATT"][t], w["DCTX"][t], w["CTX"][t], w["dA"][t],
                                                                  w["dcov"][1], w["gcl"][t], lens, w["DE"][t],
