@@ -269,15 +269,15 @@ __device__ __forceinline__ void beam_step_body(
     int* __restrict__ latest, int* __restrict__ gidx, int* __restrict__ tok_hist, int* __restrict__ par_hist,
     int* __restrict__ done, int* __restrict__ res_count, float* __restrict__ res_score, int* __restrict__ res_len,
     int* __restrict__ res_step, int* __restrict__ res_par, float* cval, int* cid, int* srt, int a, int lane, int t,
-    int base, int beam, int K, int stop_id, int min_dec) {
+    int base, int beam, int K, int stop_id, int min_dec, float tot, int tid_cand, int nres0) {
+  // tot / tid_cand / nres0: this lane's candidate and the result count, loaded by the caller
+  // in the same memory round trip as the step counter and the done flag
   const int norig = t == 0 ? 1 : beam;
   const int ncand = norig * K;
-  float tot = -INFINITY;
+  if (lane >= ncand) tot = -INFINITY;
   if (lane < ncand) {
-    const int i = lane / K, j = lane % K;
-    tot = lp_sum[base + i] + top_lp[(size_t)(base + i) * K + j];
     cval[lane] = tot;
-    cid[lane] = top_ids[(size_t)(base + i) * K + j];
+    cid[lane] = tid_cand;
   }
   // stable rank: descending total, ties keep candidate order
   int rank = 0;
@@ -288,7 +288,7 @@ __device__ __forceinline__ void beam_step_body(
   if (lane < ncand) srt[rank] = lane;
   __syncthreads();
   if (lane == 0) {
-    int nres = res_count[a], nh = 0;
+    int nres = nres0, nh = 0;
     float new_lp[TOPK_MAX];
     int new_tok[TOPK_MAX], new_par[TOPK_MAX];
     for (int q = 0; q < ncand; ++q) {
@@ -342,19 +342,31 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
   __shared__ int cid[64];
   __shared__ int srt[64];
   const int a = blockIdx.x, lane = threadIdx.x;
-  const int t = *step;
   const int base = a * beam;
   const size_t R = (size_t)gridDim.x * beam;
+  // one memory round trip for everything the bookkeeping reads: the step counter, the done
+  // flag, the result count and this lane's candidate (rows of step t > 0; at t == 0 only row
+  // base's K candidates are used and the others are masked in the body)
+  const int t = *step;
+  const int is_done = done[a], nres0 = res_count[a];
+  float tot = -INFINITY;
+  int tid_cand = 0;
+  if (lane < beam * K) {
+    const int i = lane / K, j = lane % K;
+    tot = lp_sum[base + i] + top_lp[(size_t)(base + i) * K + j];
+    tid_cand = top_ids[(size_t)(base + i) * K + j];
+  }
   if (att_hist) {  // attention / p_gen history for the visualiser, row t (clamped)
     const size_t th = (size_t)min(t, max_dec - 1);
     for (int i = lane; i < beam * T; i += 64) att_hist[(th * R + base) * T + i] = att[(size_t)base * T + i];
     if (pg_hist && lane < beam) pg_hist[th * R + base + lane] = pg[base + lane];
   }
-  if (done[a] || t >= max_dec) {
+  if (is_done || t >= max_dec) {
     if (lane < beam) gidx[base + lane] = base + lane;
   } else {
     beam_step_body(top_ids, top_lp, lp_sum, latest, gidx, tok_hist, par_hist, done, res_count, res_score, res_len,
-                   res_step, res_par, cval, cid, srt, a, lane, t, base, beam, K, stop_id, min_dec);
+                   res_step, res_par, cval, cid, srt, a, lane, t, base, beam, K, stop_id, min_dec, tot, tid_cand,
+                   nres0);
   }
   // grid-wide step advance: every block read *step above; the last one to arrive bumps it
   if (lane == 0) {
