@@ -165,7 +165,7 @@ def test_row_attention_matches_multiblock_kernels(monkeypatch, coverage, B, T, H
     # backward: row kernel vs multi-block kernel on the row engine's forward state
     bw = []
     for row in (True, False):
-        eng.row_attn = row
+        eng.row_attn_bwd = row
         eng.backward()
         torch.cuda.synchronize()
         bw.append((eng.w["DE"].clone(), eng.w["DS"].clone(), eng.w["dF"].float().clone(), params.grad.clone()))

@@ -252,6 +252,10 @@ class HipPointerGenerator:
         # multi-block-per-row kernels of attention.hip.  TSAMD_ROW_ATTN=0/1 overrides.
         ra = os.environ.get("TSAMD_ROW_ATTN", "")
         self.row_attn = bool(self.k.attn_row_ok(A, T)) and (ra == "1" or (ra != "0" and B >= 128))
+        # backward: the row kernel at A = 1024 (16 features per lane, 8 waves at 256 VGPRs)
+        # hides too little latency -- config #5 decoder backward 79 ms vs 59 ms with the
+        # multi-block attn_bwd_step (tools/phase_micro.py) -- so it is used at A = 512 only
+        self.row_attn_bwd = self.row_attn and (A == 512 or ra == "1")
         w["F"] = z(B, T, A, dt=BF)
         # transposed copy for the lanes-over-positions score kernel (not needed by the row
         # kernels; the beam decoder sets keep_ft to get it from _encoder_forward)
@@ -332,10 +336,11 @@ class HipPointerGenerator:
         pk = getattr(self, "pk", None) or {}
 
         def put(name, t):
+            t = t.to(BF)
             if name in pk and pk[name].shape == t.shape:
-                pk[name].copy_(t)  # one cast(+transpose) kernel into the persistent bf16 buffer
+                pk[name].copy_(t)
             else:
-                pk[name] = t.to(BF).contiguous()
+                pk[name] = t.contiguous()
 
         put("emb", p[EMB])
         for layer in range(self.L):
@@ -656,7 +661,7 @@ class HipPointerGenerator:
         w["dh_rec"].zero_()
         w["dc_carry"].zero_()
         dcov = w["dcov"]
-        if not self.row_attn:
+        if not self.row_attn_bwd:
             w["DS"].zero_()  # accumulated with atomics by the multi-block kernels (the row kernel stores)
         Ga = w["dA"] if hps.pointer_gen else None
         def chain(r0, r1):
@@ -666,7 +671,7 @@ class HipPointerGenerator:
                 cov_t = w["COV"][t][rs] if (cov and t > 0) else None
                 gcl_t = w["gcl"][t][rs] if cov else None
                 ga_t = Ga[t][rs] if Ga is not None else None
-                if self.row_attn:
+                if self.row_attn_bwd:
                     k.attn_bwd_row(enc_out[rs], F[rs], w["S"][t][rs], v, wc, cov_t, w["ATT"][t][rs], w["DCTX"][t][rs],
                                    w["CTX"][t][rs], ga_t, dcov_next, gcl_t, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
                                    dcov[t % 2][rs] if cov else None, Bg, T, A)
