@@ -48,7 +48,8 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (rows)")
+    ap.add_argument("--batch", default="256", help="per-GPU batch (rows), or 'auto': the largest of 1024/512/256/128 "
+                                                   "whose training step fits the GPU's memory (config #5 sizing)")
     ap.add_argument("--no-coverage", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled per rank")
@@ -134,14 +135,28 @@ def main(argv=None):
         print(f"warning: --gpus {args.gpus} but the process group has {info.world} ranks", file=sys.stderr)
     dev_id = info.local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_id)
-    hps = HParams(batch_size=args.batch, max_enc_steps=args.enc, max_dec_steps=args.dec, vocab_size=args.vocab,
+    hps = HParams(batch_size=256 if args.batch == "auto" else int(args.batch), max_enc_steps=args.enc, max_dec_steps=args.dec, vocab_size=args.vocab,
                   hidden_dim=args.hidden, emb_dim=args.emb, coverage=not args.no_coverage, pointer_gen=True,
                   enc_layers=args.layers, grad_compress=args.grad_compress)
     corpus = SyntheticCorpus(vocab_size=args.vocab, seed=1000 + info.rank)
     vocab = corpus.vocab(args.vocab)
-    batches = make_batches(hps, vocab, corpus, args.pool, pad_enc_to=args.enc)
-    tr = GraphTrainer(hps, vocab.size(), B=args.batch, T=args.enc, device=f"cuda:{dev_id}", info=info,
-                      use_graph=not args.no_graph)
+    cands = [1024, 512, 256, 128] if args.batch == "auto" else [int(args.batch)]
+    tr = None
+    for B in cands:  # 'auto': largest batch whose engine + captured step fit (every rank the same shape)
+        try:
+            hps = hps.replace(batch_size=B)
+            args.batch = B
+            batches = make_batches(hps, vocab, corpus, args.pool, pad_enc_to=args.enc)
+            tr = GraphTrainer(hps, vocab.size(), B=B, T=args.enc, device=f"cuda:{dev_id}", info=info,
+                              use_graph=not args.no_graph)
+            if len(cands) > 1:
+                tr.step(batches[0])  # graph capture included: the peak allocation happens here
+            break
+        except torch.cuda.OutOfMemoryError:
+            if B == cands[-1]:
+                raise
+            tr = None
+            torch.cuda.empty_cache()
 
     for i in range(args.warmup):
         out = tr.step(batches[i % len(batches)])
@@ -197,6 +212,8 @@ def main(argv=None):
                 "loss": round(vals.get("total_loss", float("nan")), 4),
                 "graph": not args.no_graph,
                 "persistent_lstm": bool(tr.engine.persistent_lstm),
+                "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
+                "gpu_mem_gb": round(torch.cuda.get_device_properties(dev_id).total_memory / 2 ** 30, 1),
             },
         }
         if dec is not None:

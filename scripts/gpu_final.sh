@@ -17,8 +17,8 @@ for B in 64 128 512; do
   timeout -k 10 300 python bench.py --batch $B --steps 20 --warmup 3 --decode-batches 0 > $OUT/b$B.log 2>&1 || { tail -20 $OUT/b$B.log; exit 1; }
   j $OUT/b$B.log "train B=$B"
 done
-timeout -k 10 300 python bench.py --hidden 512 --layers 2 --enc 800 --batch 512 --steps 5 --warmup 2 --decode-batches 2 > $OUT/cfg5.log 2>&1 || { tail -20 $OUT/cfg5.log; exit 1; }
-j $OUT/cfg5.log "config5 H=512 L=2 enc=800 B=512"
+timeout -k 10 300 python bench.py --hidden 512 --layers 2 --enc 800 --batch auto --steps 3 --warmup 1 --decode-batches 2 > $OUT/cfg5.log 2>&1 || { tail -20 $OUT/cfg5.log; exit 1; }
+j $OUT/cfg5.log "config5 H=512 L=2 enc=800 B=auto"
 timeout -k 10 300 python bench.py --gpus 2 --backend gloo --batch 64 --steps 5 --warmup 2 --decode-batches 1 > $OUT/dp2_gloo.log 2>&1 || { tail -20 $OUT/dp2_gloo.log; exit 1; }
 j $OUT/dp2_gloo.log "dp2 gloo plumbing (self-launched ranks)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --batch 256 --decode-batches 0 > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
