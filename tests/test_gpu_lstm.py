@@ -106,3 +106,51 @@ def test_persistent_repeated_launches_reset_tags():
     torch.cuda.synchronize()
     assert int(err.item()) == 0
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+
+
+def test_persistent_lstm_with_concurrent_kernels():
+    """Co-residency under concurrent work (the data-parallel case: RCCL kernels of an earlier
+    gradient bucket run beside the BPTT).  The persistent launches need all their workgroups
+    resident; a long GEMM stream on a second HIP stream holds CUs while they start, so early
+    team members spin until the others get CUs.  Results must equal the solo launches and no
+    hand-off may time out (lstm_err stays 0)."""
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    H, B, T = 256, 256, 40
+    g, r, lens, gx, Wt, Wn, hs0, cs0 = _setup(H, B, T, 11)
+    bias = torch.zeros(2, 4 * H, device="cuda")
+    xf = torch.zeros(int(k.lstm_persistent_xbuf(H, B, False)), device="cuda", dtype=torch.long)
+    xb = torch.zeros(int(k.lstm_persistent_xbuf(H, B, True)), device="cuda", dtype=torch.long)
+    err = torch.zeros(1, device="cuda", dtype=torch.int32)
+    dout = torch.randn(2, T, B, H, device="cuda", generator=g) * 0.1
+    a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+
+    def run(side_load):
+        hs, cs = hs0.clone(), cs0.clone()
+        acts = torch.zeros(2, T, B, 4 * H, device="cuda")
+        out = torch.zeros(B, T, 2 * H, device="cuda", dtype=torch.bfloat16)
+        dz = torch.zeros(2, T, B, 4 * H, device="cuda", dtype=torch.bfloat16)
+        dcc = torch.zeros(2, B, H, device="cuda")
+        dhf = torch.zeros(2, B, H, device="cuda")
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        if side_load:
+            with torch.cuda.stream(side):
+                for _ in range(30):  # ~ms of GEMMs occupying every CU while the LSTM launches start
+                    a @ a
+        xf.zero_()
+        k.lstm_fwd_persistent(gx, bias, Wt, hs, cs, acts, out, lens, xf, err, T, B, H)
+        if side_load:
+            with torch.cuda.stream(side):
+                for _ in range(30):
+                    a @ a
+        xb.zero_()
+        k.lstm_bwd_persistent(dz, Wn, dout, dhf, dcc, acts, cs, lens, xb, err, None, T, B, H)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        return out.clone(), dz.clone()
+
+    solo = run(False)
+    busy = run(True)
+    assert int(err.item()) == 0
+    assert torch.equal(solo[0], busy[0]) and torch.equal(solo[1], busy[1])
