@@ -51,6 +51,9 @@ class DeviceBeamDecoder:
         self.V = vocab.size()
         self.maxD = hps.max_dec_steps
         self.use_graph, self.chunk, self.keep_attn = use_graph, chunk, keep_attn
+        # decode steps per captured graph: a whole early-exit chunk when it is even (one graph
+        # launch per chunk instead of one per step pair), else 2
+        self.gsteps = chunk if chunk % 2 == 0 else 2
         self.eng = HipPointerGenerator(hps, self.V, params, B=self.Na, T=T, D=1)
         # attention per step: the row-resident kernel (score + softmax + context in one launch,
         # one workgroup per hypothesis reading its article's F/E rows) when the shape allows
@@ -207,20 +210,20 @@ class DeviceBeamDecoder:
                     pg if (hist and pg is not None) else None, b["PG_hist"] if (hist and pg is not None) else None,
                     T, self.Na, self.beam, K, self.vocab.word2id(STOP_DECODING), hps.min_dec_steps, self.maxD)
 
-    def _two_steps(self):
-        self._step(0)
-        self._step(1)
+    def _graph_steps(self):
+        for i in range(self.gsteps):  # parity alternates: gsteps is even
+            self._step(i % 2)
 
     def _capture(self):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            self._two_steps()  # warm-up (state discarded: the prologue re-runs before decoding)
+            self._graph_steps()  # warm-up (state discarded: the prologue re-runs before decoding)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self._two_steps()
+            self._graph_steps()
         torch.cuda.synchronize()
 
     # ------------------------------------------------------------------ driver
@@ -242,9 +245,9 @@ class DeviceBeamDecoder:
             n = min(self.chunk, self.maxD - t)
             i = 0
             while i < n:
-                if self.use_graph and n - i >= 2:
-                    self.graph.replay()  # steps t+i, t+i+1 (parity 0 then 1)
-                    i += 2
+                if self.use_graph and n - i >= self.gsteps and (t + i) % 2 == 0:
+                    self.graph.replay()  # steps t+i .. t+i+gsteps-1 (parity 0, 1, 0, ...)
+                    i += self.gsteps
                 else:
                     self._step((t + i) % 2)
                     i += 1
