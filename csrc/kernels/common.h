@@ -191,6 +191,18 @@ __device__ __forceinline__ float xor16_f(float v) {
 }
 // v + v(l ^ 32), v + v(l ^ 16), max likewise (the two halves are summed in the same order on
 // both sides, so every lane gets the bit-identical result)
+// v_max3_f32 / v_max_f32 without the NaN-quieting canonicalisations fmaxf gets in IEEE mode
+// (for finite or -inf operands: 8 instructions instead of ~29 for 16 values)
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax2(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ float sum_x32(float v) {
   const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(p[0]) + __uint_as_float(p[1]);

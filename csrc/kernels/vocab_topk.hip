@@ -12,6 +12,7 @@
 //                       union copied ids).
 // Replaces a library GEMM + a separate per-element top-k pass over the logits.
 #include "common.h"
+#include "attn_common.h"  // f32x2 packed-FP32 helpers
 #include "launchers.h"
 
 #define VT_COLS 256   // vocab columns per workgroup
@@ -36,85 +37,71 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 
 }  // namespace
 
-// vocab_logits epilogue for one wave: + bias, per-row (max, sum exp) over the wave's 64
-// columns (DPP row reductions), and the fp32 logits stored through the LDS staging St as
-// 4 rows x 256 B per instruction.  Accumulator (i, j, r) holds row 16i + 4(lane>>4) + r,
-// column 16j + (lane&15).
+// vocab_logits epilogue for one wave and one 16-row tile jr.  Operands are swapped relative
+// to a plain logits GEMM (A = W^T fragments, B = X rows, as in vocab_train.hip), so
+// accumulator (i, jr, r) holds logit[row = rb + 16 jr + (lane & 15)][col = cw + 16 i + 4 q + r],
+// q = lane >> 4: every lane owns 16 columns of one row.  The row's (max, sum exp) over the
+// wave's 64 columns is 15 in-lane ops + 2 cross-lane steps (lanes l, l^16, l^32, l^48), and the
+// lane's 4 consecutive columns per i are one 16-byte store (a row's 64 columns = one 256-byte
+// run over the 4 i and 4 q).  Replaced a [row = lane group] layout whose per-row reductions
+// took 16-lane DPP trees for each of the lane's 16 rows and an LDS staging pass for stores.
 template <bool FULL>
-__device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[4][4], const float* __restrict__ bias,
-                                            float* __restrict__ logits, float (*St)[68], float* Pm, float* Ps,
-                                            int rb, int cw, int lane, int R, int V) {
+__device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[4][4], int jr, const f32x2 (&bc)[4][2],
+                                            float* __restrict__ logits, float* Pm, float* Ps, int rb, int cw,
+                                            int lane, int R, int V) {
   constexpr float L2E = 1.4426950408889634f;
-  float bj[4];
-  bool cok[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = cw + 16 * j + (lane & 15);
-    cok[j] = FULL || col < V;
-    bj[j] = cok[j] ? bias[col] : 0.f;
-  }
-  const int c4 = 4 * (lane & 15);
-  // FULL: one base pointer, the per-store offsets (16i + 4q) * V are wave-uniform
-  float* const base = logits + (size_t)(rb + (lane >> 4)) * V + cw + c4;
+  const int row = rb + 16 * jr + (lane & 15), q4 = 4 * (lane >> 4);
+  f32x2 x[4][2];
+  float m = -INFINITY;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float x[4], m = -INFINITY;
+    for (int h = 0; h < 2; ++h) {
+      x[i][h] = f32x2{acc[i][jr][2 * h], acc[i][jr][2 * h + 1]} + bc[i][h];  // bc = -inf past V
+      m = vmax3(m, x[i][h].x, x[i][h].y);
+    }
+  m = max_x32(max_x16(m));
+  f32x2 s2 = f32x2{0.f, 0.f};
+  if (FULL || m > -INFINITY) {
+    const f32x2 mb = f32x2{-m * L2E, -m * L2E};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        x[j] = cok[j] ? acc[i][j][r] + bj[j] : -INFINITY;
-        m = fmaxf(m, x[j]);
-        St[4 * (lane >> 4) + r][16 * j + (lane & 15)] = x[j];
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x2 t = __builtin_elementwise_fma(x[i][h], f32x2{L2E, L2E}, mb);
+        s2 += f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};  // exp(-inf) = 0
       }
-      m = dpp_max16(m);
-      float sm = 0.f;
-      if (FULL || m > -INFINITY) {
-        const float mb = m * L2E;
+  }
+  const float sm = sum_x32(sum_x16(s2.x + s2.y));
+  if (lane < 16) {
+    Pm[16 * jr + lane] = m;
+    Ps[16 * jr + lane] = sm;
+  }
+  if (FULL) {
+    float* dst = logits + (size_t)row * V + cw + q4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sm += __builtin_amdgcn_exp2f(fmaf(x[j], L2E, -mb));  // exp(-inf) = 0
-      }
-      sm = dpp_sum16(sm);
-      if ((lane & 15) == 0) {
-        Pm[16 * i + 4 * (lane >> 4) + r] = m;
-        Ps[16 * i + 4 * (lane >> 4) + r] = sm;
-      }
-      if (r == 3) {
-        // the 16-row tile i is staged: store it as 4 rows x 256 B per instruction
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float4*>(dst + 16 * i) = make_float4(x[i][0].x, x[i][0].y, x[i][1].x, x[i][1].y);
+  } else if (row < R) {
+    float* dst = logits + (size_t)row * V;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int tr = 4 * q + (lane >> 4);
-          if (FULL) {
-            *reinterpret_cast<float4*>(base + (size_t)(16 * i + 4 * q) * V) =
-                *reinterpret_cast<const float4*>(&St[tr][c4]);
-          } else {
-            const int row2 = rb + 16 * i + tr, col = cw + c4;
-            if (row2 < R) {
-              float* dst = logits + (size_t)row2 * V + col;
-              if ((V & 3) == 0 && col + 4 <= V) {
-                *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(&St[tr][c4]);
-              } else {
+    for (int i = 0; i < 4; ++i) {
+      const int col = cw + 16 * i + q4;
+      const float xv[4] = {x[i][0].x, x[i][0].y, x[i][1].x, x[i][1].y};
+      if ((V & 3) == 0 && col + 4 <= V) {
+        *reinterpret_cast<float4*>(dst + col) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+      } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                  if (col + e < V) dst[e] = St[tr][c4 + e];
-              }
-            }
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int e = 0; e < 4; ++e)
+          if (col + e < V) dst[col + e] = xv[e];
       }
     }
+  }
 }
 
-// 36 KB of LDS.  OCC = 2 (206 VGPRs): all 32 W^T fragments of a wave in flight at once, two
-// rounds of workgroups at R = 256, V = 50k (784 tiles).  OCC = 4 (128 VGPRs) fits every tile in
-// one round but the compiler then issues the fragments 4 at a time (8 dependent round trips).
-// Both measure 47.5 us with the select kernel (tools/vocab_micro.py); PMC: the epilogue's
-// ~1500 VALU instructions per wave (bias, row max / sum exp, staging) are the larger cost.
-// TSAMD_VL_OCC=4 selects the other variant.
+// 35 KB of LDS, 2 workgroups per CU (<= 256 VGPRs): all 32 W^T fragments of a wave in flight at
+// once, two rounds of workgroups at R = 256, V = 50k (784 tiles).  (A 4-per-CU variant, 128
+// VGPRs, measured the same before this layout and spills with it.)
 template <int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void vocab_logits_kernel(
     const bf16* __restrict__ X,     // [R][H]  output-projection activations (bf16)
@@ -124,10 +111,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     float* __restrict__ part_ms,    // [R][nt][2]  per tile (max, sum exp)
     int R, int V, int H) {
   __shared__ float Pm[4][VT_ROWS], Ps[4][VT_ROWS];
-  // X tile during the MFMA loop; afterwards reused as the per-wave 16 x 64 store staging
-  __shared__ __attribute__((aligned(16))) bf16 Xs[VT_ROWS * (VT_HMAX + 8)];
-  static_assert(sizeof(float) * 4 * 16 * 68 <= sizeof(bf16) * VT_ROWS * (VT_HMAX + 8), "staging alias");
-  float (*St)[16][68] = reinterpret_cast<float (*)[16][68]>(Xs);
+  __shared__ __attribute__((aligned(16))) bf16 Xs[VT_ROWS * (VT_HMAX + 8)];  // X tile of the block
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // XCD-aware order: the RB row blocks of one vocab tile get block ids equal mod 8 (one XCD
   // under round-robin dealing), so the tile's W^T columns come from HBM once and are then
@@ -138,7 +122,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   const int rb = (slot % RB) * VT_ROWS;
   const int cw = vt * VT_COLS + 64 * wid;  // this wave's first column
   // X rows of this block -> LDS once (shared by the 4 waves)
-  const int kof = 8 * (lane >> 4);
+  const int kof = 8 * (lane >> 4), c16 = lane & 15, q4 = 4 * (lane >> 4);
   constexpr int XPT = VT_ROWS * VT_HMAX / 8 / 256;  // 16-byte X chunks per thread (H <= 256)
   bf16x8 xr[XPT];
 #pragma unroll
@@ -146,45 +130,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     const int c = threadIdx.x + 256 * u, rr = c / (H / 8), k8 = (c % (H / 8)) * 8;
     if (c < VT_ROWS * (H / 8)) xr[u] = ld8(X + (size_t)min(rb + rr, R - 1) * H + k8);
   }
-  // every B fragment of the wave (4 column tiles x H/32 k-steps, H <= 256: 128 VGPRs) is
-  // issued right behind the X loads, before their LDS stores: one memory round trip for both
-  const bf16* brow[4];
+  // every A fragment of the wave (W^T rows = its 4 x 16 vocab columns, H/32 k-steps, H <= 256:
+  // 128 VGPRs) is issued right behind the X loads, before their LDS stores: one memory round
+  // trip for both
+  const bf16* arow[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) brow[j] = WT + (size_t)min(cw + 16 * j + (lane & 15), V - 1) * H + kof;
-  bf16x8 b[8][4];
+  for (int i = 0; i < 4; ++i) arow[i] = WT + (size_t)min(cw + 16 * i + c16, V - 1) * H + kof;
+  bf16x8 wa[8][4];
 #pragma unroll
   for (int h = 0; h < 8; ++h)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[h][j] = ld8(brow[j] + min(32 * h, H - 32));
+    for (int i = 0; i < 4; ++i) wa[h][i] = ld8(arow[i] + min(32 * h, H - 32));
+  // bias of the lane's columns cw + 16 i + q4 + r, pairs (r = 2h, 2h + 1); -inf past V
+  f32x2 bc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = cw + 16 * i + q4 + 2 * h;
+      bc[i][h] = f32x2{col < V ? bias[col] : -INFINITY, col + 1 < V ? bias[col + 1] : -INFINITY};
+    }
 #pragma unroll
   for (int u = 0; u < XPT; ++u) {
     const int c = threadIdx.x + 256 * u, rr = c / (H / 8), k8 = (c % (H / 8)) * 8;
     if (c < VT_ROWS * (H / 8)) *reinterpret_cast<bf16x8*>(&Xs[rr * (H + 8) + k8]) = xr[u];
   }
-  f32x4 acc[4][4];
+  f32x4 acc[4][4];  // [vocab column tile i][row tile jr]
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+    for (int jr = 0; jr < 4; ++jr) acc[i][jr] = f32x4{0, 0, 0, 0};
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < 8; ++h) {
     if (32 * h < H) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Xs[(16 * i + (lane & 15)) * (H + 8) + 32 * h + kof]);
+      for (int jr = 0; jr < 4; ++jr) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&Xs[(16 * jr + c16) * (H + 8) + 32 * h + kof]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a, b[h][j], acc[i][j]);
+        for (int i = 0; i < 4; ++i) acc[i][jr] = mfma16(wa[h][i], xb, acc[i][jr]);
       }
     }
   }
-  __syncthreads();  // every wave is done reading Xs before it becomes the store staging
   // ---- epilogue: + bias, store fp32, per-row (max, sum exp) over this wave's 64 columns.
   // FULL (every tile but the last vocab tile / row block): no column or row guards.
-  if ((vt + 1) * VT_COLS <= V && rb + VT_ROWS <= R && (V & 3) == 0)
-    vl_epilogue<true>(acc, bias, logits, St[wid], Pm[wid], Ps[wid], rb, cw, lane, R, V);
-  else
-    vl_epilogue<false>(acc, bias, logits, St[wid], Pm[wid], Ps[wid], rb, cw, lane, R, V);
+  const bool full = (vt + 1) * VT_COLS <= V && rb + VT_ROWS <= R && (V & 3) == 0;
+#pragma unroll
+  for (int jr = 0; jr < 4; ++jr) {
+    if (full)
+      vl_epilogue<true>(acc, jr, bc, logits, Pm[wid], Ps[wid], rb, cw, lane, R, V);
+    else
+      vl_epilogue<false>(acc, jr, bc, logits, Pm[wid], Ps[wid], rb, cw, lane, R, V);
+  }
   __syncthreads();
   if (wid == 0) {
     const int rr = lane, row = rb + rr;
@@ -459,13 +456,8 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
                        int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st) {
   const int nt = vocab_topk_tiles(V);
   const int RB = (R + VT_ROWS - 1) / VT_ROWS;
-  static const int occ = getenv("TSAMD_VL_OCC") ? atoi(getenv("TSAMD_VL_OCC")) : 2;
-  if (occ == 4)
-    hipLaunchKernelGGL(vocab_logits_kernel<4>, dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
-                       part_ms, R, V, H);
-  else
-    hipLaunchKernelGGL(vocab_logits_kernel<2>, dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
-                       part_ms, R, V, H);
+  hipLaunchKernelGGL(vocab_logits_kernel<2>, dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
+                     part_ms, R, V, H);
   hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
                      out_lp, V, T, K, beam, nt, pgi);
 }

@@ -21,11 +21,14 @@
 // them only at a tile boundary; the 32 x H row block of X is staged in LDS per unit (shared
 // by the 4 waves, each of which owns 64 of the 256 columns).
 #include "common.h"
+#include "attn_common.h"  // f32x2 packed-FP32 helpers
 
 #define VR_ROWS 32   // rows per unit (2 MFMA row tiles)
 #define VR_COLS 256
 #define LOG2E_F 1.4426950408889634f
 #define LN2_F 0.6931471805599453f
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -104,7 +107,8 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
   if (u0 >= u1) return;
   const int kof = 8 * (lane >> 4), c16 = lane & 15, q4 = 4 * (lane >> 4);
   bf16x8 wa[KS][4];   // A fragments: W^T rows (vocab columns) of this wave's 4 column tiles
-  float bcol[4][4];   // log2(e) x bias of the lane's columns cw + 16i + q4 + r (-inf past V in pass 1)
+  f32x2 bc2[4][2];    // log2(e) x bias of the lane's columns cw + 16i + q4 + r, pairs (r = 2h, 2h + 1)
+                      // (-inf past V in pass 1)
   int cur_vt = -1;
   // pass 2: the output-projection bias gradient db = sum_rows dlogits.  Per unit the lane's
   // 16 column partials (its 2 rows) are folded across the 16 lanes that share those columns by
@@ -177,7 +181,9 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int col = cw + 16 * i + q4 + r;
-          bcol[i][r] = col < V ? bias[col] * LOG2E_F : (GRAD ? 0.f : -INFINITY);
+          const float b = col < V ? bias[col] * LOG2E_F : (GRAD ? 0.f : -INFINITY);
+          if (r & 1) bc2[i][r >> 1].y = b;
+          else bc2[i][r >> 1].x = b;
         }
       }
       cur_vt = vt;
@@ -201,38 +207,49 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
       for (int j = 0; j < RJ; ++j) {
         const int rr = 16 * j + c16, row = rb + rr;
         const int wo = Tg[buf][rr] - cw - q4;  // gold column relative to the lane's first one
-        // y = log2(e) x logit (base-2 domain: one FMA per element, exp2 without a multiply)
-        float y[4][4], m = -INFINITY;
+        // y = log2(e) x logit (base-2 domain: one packed FMA per element pair, exp2 without a
+        // multiply); -inf for columns >= V
+        f32x2 y[4][2];
+        float m = -INFINITY;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            y[i][r] = fmaf(acc[i][j][r], LOG2E_F, bcol[i][r]);  // -inf for columns >= V
-            m = fmaxf(m, y[i][r]);
+          for (int h = 0; h < 2; ++h) {
+            y[i][h] = fma2(f32x2{acc[i][j][2 * h], acc[i][j][2 * h + 1]}, splat2(LOG2E_F), bc2[i][h]);
+            m = vmax3(m, y[i][h].x, y[i][h].y);
           }
-          const int o = wo - 16 * i;
-          if ((unsigned)o < 4u && row < N)
-            zg[row] = (o == 0 ? y[i][0] : o == 1 ? y[i][1] : o == 2 ? y[i][2] : y[i][3]) * LN2_F;
-        }
-        m = max_x32(max_x16(m));
-        float sm = 0.f;
-        if (m > -INFINITY) {
+        // the gold logit: at most one of the row's columns lies among the lane's 16
+        // (offsets 16i + r), so the selection runs only on the rare hit
+        if ((unsigned)wo < 64u && (wo & 12) == 0 && row < N) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) sm += __builtin_amdgcn_exp2f(y[i][r] - m);
+            for (int r = 0; r < 4; ++r)
+              if (wo == 16 * i + r) zg[row] = (r & 1 ? y[i][r >> 1].y : y[i][r >> 1].x) * LN2_F;
         }
-        sm = sum_x32(sum_x16(sm));
+        m = max_x32(max_x16(m));
+        f32x2 s2 = splat2(0.f);
+        if (m > -INFINITY) {
+          const f32x2 mm = splat2(m);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const f32x2 t = y[i][h] - mm;
+              s2 += f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+            }
+        }
+        const float sm = sum_x32(sum_x16(s2.x + s2.y));
         if (lane < 16) {
           Pm[buf][wid][rr] = m * LN2_F;  // natural-log domain for the partial
           Ps[buf][wid][rr] = sm;
         }
       }
     } else {
-      const bool vec = (V % 4 == 0);
-      float cs[16];  // this unit's column partials, index 4i + r
+      const bool full = (V % 4 == 0) && cw + 64 <= V;  // wave-uniform: no column guards
+      f32x2 cs[4][2];  // this unit's column partials, index (i, r / 2)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) cs[q] = 0.f;
+      for (int i = 0; i < 4; ++i) cs[i][0] = cs[i][1] = splat2(0.f);
 #pragma unroll
       for (int j = 0; j < RJ; ++j) {
         const int rr = 16 * j + c16, row = rb + rr;
@@ -241,29 +258,61 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
         // alpha exp(z - lse) = exp2(log2(e) z + log2(alpha) - log2(e) lse)   (alpha >= 0)
         const float c = al > 0.f ? __log2f(al) - Ls[buf][rr] * LOG2E_F : -INFINITY;
         if (row < N) {
+          f32x2 d[4][2];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int col = cw + 16 * i + q4;
-            const int o = wo - 16 * i;
-            float d[4];
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              d[r] = __builtin_amdgcn_exp2f(fmaf(acc[i][j][r], LOG2E_F, bcol[i][r] + c)) - (o == r ? al : 0.f);
-              cs[4 * i + r] += d[r];
+            for (int h = 0; h < 2; ++h) {
+              const f32x2 t = fma2(f32x2{acc[i][j][2 * h], acc[i][j][2 * h + 1]}, splat2(LOG2E_F), bc2[i][h] + c);
+              d[i][h] = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
             }
-            bf16* dst = dl + (size_t)row * V + col;
-            if (vec && col + 4 <= V) {
-              typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-              *reinterpret_cast<bf16x4*>(dst) = bf16x4{f2bf(d[0]), f2bf(d[1]), f2bf(d[2]), f2bf(d[3])};
-            } else {
+          // - alpha at the gold column (rare: see pass 1)
+          if ((unsigned)wo < 64u && (wo & 12) == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
               for (int r = 0; r < 4; ++r)
-                if (col + r < V) dst[r] = f2bf(d[r]);
+                if (wo == 16 * i + r) {
+                  if (r & 1) d[i][r >> 1].y -= al;
+                  else d[i][r >> 1].x -= al;
+                }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            cs[i][0] += d[i][0];
+            cs[i][1] += d[i][1];
+          }
+          bf16* dst = dl + (size_t)row * V + cw + q4;
+          if (full) {
+            // (plain stores: the 4 stores of a row's 128-byte line are merged in L2; non-temporal
+            // stores went to HBM as 32-byte pieces, 1.31 -> 1.75 ms)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              *reinterpret_cast<bf16x4*>(dst + 16 * i) =
+                  bf16x4{f2bf(d[i][0].x), f2bf(d[i][0].y), f2bf(d[i][1].x), f2bf(d[i][1].y)};
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int col = cw + 16 * i + q4;
+              const float dv[4] = {d[i][0].x, d[i][0].y, d[i][1].x, d[i][1].y};
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (col + r < V) dst[16 * i + r] = f2bf(dv[r]);
             }
           }
         }
       }
-      if (dbias) cacc += row_transpose_sum(cs, c16);
+      if (dbias) {
+        float cv[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          cv[4 * i] = cs[i][0].x;
+          cv[4 * i + 1] = cs[i][0].y;
+          cv[4 * i + 2] = cs[i][1].x;
+          cv[4 * i + 3] = cs[i][1].y;
+        }
+        cacc += row_transpose_sum(cv, c16);
+      }
     }
     if (u + 1 < u1) stash(buf ^ 1);
     __syncthreads();
