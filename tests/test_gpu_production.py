@@ -79,9 +79,12 @@ def test_bench_shape_matches_fp32_oracle():
     assert not bad, bad
 
 
-def test_graph_replay_equals_eager_train_step():
-    """Three optimizer steps through the captured graphs == the same steps launched eagerly."""
+@pytest.mark.parametrize("overlap_dw", ["0", "1"])
+def test_graph_replay_equals_eager_train_step(monkeypatch, overlap_dw):
+    """Three optimizer steps through the captured graphs == the same steps launched eagerly
+    (also with the output-projection dW forked onto a side stream inside backward_mid)."""
     from textsummarization_on_flink_amd.train.trainer import GraphTrainer
+    monkeypatch.setenv("TSAMD_OVERLAP_DW", overlap_dw)
     B = 256
     hps = _hps(B)
     vocab, batches = _batches(hps, 3, seed=12)

@@ -175,10 +175,11 @@ class HipPointerGenerator:
         self.k = _ops()
         self.grad_scale = 1.0  # set to 1/world by a data-parallel trainer (see optimizer_step)
         self.nchunk = int(self.k.attn_chunks(T))
-        # the output-projection weight gradient runs on a side stream, overlapped with the
-        # decoder backward loop (joined at the end of backward_mid) when TSAMD_OVERLAP_DW=1.
-        # Off by default: the graph-captured B=256 bench with the fork/join stalled on MI355X
-        # (no progress for 180 s) and the GEMM is ~0.7 ms of a ~27 ms step.
+        # the output-projection weight gradient (a ~0.7 ms GEMM that only the all-reduce and the
+        # optimizer need) runs on a side stream beside the decoder backward loop -- forked and
+        # joined inside backward_mid, so the phase graphs stay self-contained -- when
+        # TSAMD_OVERLAP_DW=1
+        self._dw_pending = None
         self._side = torch.cuda.Stream(self.dev) if os.environ.get("TSAMD_OVERLAP_DW", "0") == "1" else None
         # The decoder recurrences (forward: cell -> s-projection -> score -> softmax/context;
         # backward: attention step -> cell backward -> dz backward) are independent across
@@ -602,10 +603,8 @@ class HipPointerGenerator:
                 torch.sum(parts, 0, out=dst)
             else:
                 torch.mm(w["outb_ext"][:, :m].t(), dl, out_dtype=F32, out=dst)
-        if self._side is not None:  # off the critical path: only the all-reduce bucket needs it
-            self._side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self._side):
-                dw()
+        if self._side is not None:  # deferred to backward_mid's side branch
+            self._dw_pending = dw
         else:
             dw()
         self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
@@ -630,6 +629,11 @@ class HipPointerGenerator:
         g = p.g
         cov = hps.coverage
         dout = self._dout
+        if self._side is not None and self._dw_pending is not None:
+            self._side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._side):
+                self._dw_pending()
+            self._dw_pending = None
         # ---- output projection [h, ctx]
         Hn = w["Hb"][1:].reshape(N, H)
         ctxb = w["CTXb"].view(N, A)

@@ -118,22 +118,13 @@ class GraphTrainer:
         self.engine.pack()
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        if self.engine._side is None:
-            # three graphs (forward + vocab backward | decoder backward | encoder backward) so
-            # each gradient bucket's all-reduce overlaps the next phase
-            self.g_fb = [torch.cuda.CUDAGraph() for _ in range(3)]
-            with torch.cuda.graph(self.g_fb[0], pool=pool):
-                self.out = self._fwd_head()
-            with torch.cuda.graph(self.g_fb[1], pool=pool):
-                self.engine.backward_mid()
-        else:
-            # TSAMD_OVERLAP_DW=1: two graphs (forward + vocab backward + decoder backward, with
-            # the output-projection weight gradient forked onto a side stream and joined inside
-            # the graph) | encoder backward
-            self.g_fb = [torch.cuda.CUDAGraph() for _ in range(2)]
-            with torch.cuda.graph(self.g_fb[0], pool=pool):
-                self.out = self._fwd_head()
-                self.engine.backward_mid()
+        # three graphs (forward + vocab backward | decoder backward | encoder backward) so each
+        # gradient bucket's all-reduce overlaps the next phase
+        self.g_fb = [torch.cuda.CUDAGraph() for _ in range(3)]
+        with torch.cuda.graph(self.g_fb[0], pool=pool):
+            self.out = self._fwd_head()
+        with torch.cuda.graph(self.g_fb[1], pool=pool):
+            self.engine.backward_mid()
         with torch.cuda.graph(self.g_fb[-1], pool=pool):
             self.engine.backward_tail()
         self.g_opt = torch.cuda.CUDAGraph()
@@ -157,10 +148,11 @@ class GraphTrainer:
                 g.replay()
                 if ev:
                     ev[i + 1].record()
-                if ng == 3 and i < 2:
-                    self.reducer.bucket_ready(i)
-                elif ng == 2 and i == 0:  # the merged graph finalises both buckets
+                if i == 0 and self.engine._side is None:
                     self.reducer.bucket_ready(0)
+                elif i == 1:
+                    if self.engine._side is not None:  # the output-projection dW ran beside backward_mid
+                        self.reducer.bucket_ready(0)
                     self.reducer.bucket_ready(1)
             self._maybe_poison()
             self.reducer()
@@ -185,15 +177,11 @@ class GraphTrainer:
 
     def phase_ms(self) -> Dict[str, float]:
         """Time of each phase of the last step (host-synchronising): forward + vocab backward,
-        decoder backward, encoder backward, exposed all-reduce wait, optimizer (the first two
-        are one phase, ``ms_fwd_bwd_dec``, under TSAMD_OVERLAP_DW=1)."""
+        decoder backward, encoder backward, exposed all-reduce wait, optimizer."""
         if not self._ev:
             return {}
         self._ev[-1].synchronize()
-        if len(self._ev) == 6:
-            names = ("ms_fwd_head", "ms_bwd_dec", "ms_bwd_enc", "ms_allreduce", "ms_optimizer")
-        else:
-            names = ("ms_fwd_bwd_dec", "ms_bwd_enc", "ms_allreduce", "ms_optimizer")
+        names = ("ms_fwd_head", "ms_bwd_dec", "ms_bwd_enc", "ms_allreduce", "ms_optimizer")
         return {n: self._ev[i].elapsed_time(self._ev[i + 1]) for i, n in enumerate(names)}
 
     def _maybe_poison(self):
