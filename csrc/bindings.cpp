@@ -265,7 +265,7 @@ void to_step_frame(const Tensor& src, const OT& ids, const Tensor& rev, const Te
   }
   numel_eq(out, 2 * T * B * W, "out");
   launch_to_step_frame(src.data_ptr(), es, PO<int64_t>(ids), P<int64_t>(rev), out.data_ptr(), (int)B, (int)T, (int)W,
-                       (int)S, (int)doff, stream());
+                       (int)S, (int)doff, src.numel() / S, stream());
 }
 void from_step_frame(const Tensor& in, const Tensor& rev, const Tensor& out, int64_t B, int64_t T, int64_t W) {
   chk(in, F32, "in"); chk(out, F32, "out");
@@ -415,6 +415,18 @@ void ptr_loss(const Tensor& logits, const OT& bias, const Tensor& target, const 
                   P<int>(ext), P<int>(lens), P<float>(loss_row), PO<bf16>(dlogits), PO<float>(dpre), PO<float>(dA), N,
                   B, T, V, stream());
 }
+
+// debug build (dcheck.h / debug.hip): first failed bounds check (id, block, thread, value)
+int64_t debug_enabled() { return tsamd_debug_enabled(); }
+Tensor debug_status() {
+  unsigned v[4];
+  tsamd_debug_read(v);  // synchronous copy from the device record
+  Tensor t = at::empty({4}, at::TensorOptions().dtype(at::kLong));
+  int64_t* d = t.data_ptr<int64_t>();
+  for (int i = 0; i < 4; ++i) d[i] = (int64_t)v[i];
+  return t;
+}
+void debug_clear() { tsamd_debug_clear(); }
 
 // fused training vocab head (vocab_train.hip): logits never materialised
 int64_t vocab_train_tiles_op(int64_t V) { return vocab_train_tiles((int)V); }
@@ -682,6 +694,9 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("dec_bwd_cell", &dec_bwd_cell);
   m.def("dec_bwd_dz", &dec_bwd_dz);
   m.def("ptr_loss", &ptr_loss);
+  m.def("debug_enabled", &debug_enabled);
+  m.def("debug_status", &debug_status);
+  m.def("debug_clear", &debug_clear);
   m.def("vocab_train_tiles", &vocab_train_tiles_op);
   m.def("vocab_train_fwd", &vocab_train_fwd);
   m.def("vocab_train_bwd", &vocab_train_bwd);

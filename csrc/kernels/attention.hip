@@ -54,7 +54,7 @@ __global__ __launch_bounds__(SW * 64) void attn_score_kernel(
   }
   const int b = by;  // Ft row (article)
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int len = lens[b];
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const int pb = bx * SCORE_POS;
   if (pb >= len) return;  // uniform: masked positions are never read by the softmax
   const int p = pb + 2 * lane;
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void attn_softmax_ctx_kernel(
   __shared__ float part[4][REP][64];
   const int b = blockIdx.y;  // E row (article)
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int len = lens[b];
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
 #pragma unroll
   for (int q = 0; q < REP; ++q) {
     const size_t row = (size_t)b * REP + q;
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(SW * 64) void attn_bwd_da_kernel(
   __shared__ float red[SW][SCORE_POS];
   const int b = blockIdx.y;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int len = lens[b];
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const int pb = blockIdx.x * SCORE_POS;
   if (pb >= len) return;
   const int p = pb + 2 * lane;
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void attn_bwd_tanh_kernel(
   __shared__ float part[4][512 * NK];
   const int b = blockIdx.y;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int len = lens[b];
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
   const int p0 = blockIdx.x * 64 + wid * 16;
   if (blockIdx.x * 64 >= len) {  // whole block masked: only pass dcov through
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step_kernel(
   __shared__ float part[4][512 * NK];
   const int b = blockIdx.y;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int len = lens[b];
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
   const int p0 = blockIdx.x * PB + wid * 8 * NG;
   if (blockIdx.x * PB >= len) {  // whole block masked: only pass dcov through
@@ -646,7 +646,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
   __shared__ float part[4][512];
   const int b = blockIdx.y;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int len = lens[b];
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
   const int p0 = blockIdx.x * PB + wid * PW;
   if (blockIdx.x * PB >= len) {  // whole block masked: only pass dcov through
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
   __shared__ float pw[4][512];
   const int b = blockIdx.y;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int len = lens[b];
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const int kbase = blockIdx.z * 512;
   const int k0 = kbase + lane * 8;
   const bool kok = k0 < A;

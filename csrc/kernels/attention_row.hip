@@ -70,7 +70,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
   const int b = blockIdx.x;
   const int fr = b / rep;  // feature row: beam decode shares one encoder row between rep hypotheses
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int len = lens[fr];
+  const int len = (int)DCHECK_IDX(lens[fr], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
   const bf16* Fb = F + (size_t)fr * T * A;
   const bf16* Eb = E + (size_t)fr * T * A;
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
   __shared__ float red[NW];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int len = lens[b];
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
   const float g = gcl ? gcl[b] : 0.f;
   const bf16* Eb = E + (size_t)b * T * A;

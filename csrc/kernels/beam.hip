@@ -209,7 +209,7 @@ __global__ __launch_bounds__(TOPK_THREADS) void final_topk_merge_kernel(
   __syncthreads();
   const float lse = s_lse;
   const float pg = pgen ? pgen[r] : 1.0f;
-  const int len = pgen ? lens[art] : 0;
+  const int len = pgen ? (int)DCHECK_IDX(lens[art], 0, T + 1, CHK_LOSS_LEN) : 0;
   // copy mass per distinct id
   for (int i = tid; i < len; i += TOPK_THREADS) {
     const int w = ext[(size_t)art * T + i];
@@ -394,8 +394,8 @@ __global__ __launch_bounds__(256) void beam_gather_kernel(
     float* __restrict__ cov_out, float* __restrict__ XG_out, float* __restrict__ x_out,
     int H, int A, int T, int E, int V, int unk) {
   const int r = blockIdx.x, tid = threadIdx.x;
-  const int g = gidx[r];
-  int tok = latest[r];
+  const int g = (int)DCHECK_IDX(gidx[r], 0, (int)gridDim.x, CHK_BEAM_PARENT);
+  int tok = (int)DCHECK_IDX(latest[r], 0, 0x7fffffff, CHK_BEAM_TOKEN);
   tok = tok < V ? tok : unk;
   for (int i = tid; i < H; i += 256) {
     c_out[(size_t)r * H + i] = c_src[(size_t)g * H + i];

@@ -14,6 +14,7 @@ __global__ __launch_bounds__(256) void emb_grad_kernel(float* __restrict__ gemb,
   const bool first = row < n0;
   const int r = first ? row : row - n0;
   const int64_t id = first ? ids0[r] : ids1[r];
+  DCHECK_IN(id, 0, V, CHK_EMB_ID);
   if (id < 0 || id >= V) return;  // defensive: ids come from the vocab (< V)
   const float* s = (first ? src0 : src1) + (size_t)r * E;
   float* d = gemb + (size_t)id * E;
@@ -58,6 +59,7 @@ __global__ __launch_bounds__(256) void emb_grad_sorted_kernel(float* __restrict_
     for (int u = 0; u < 8; ++u) {
       const int r = min(rb + u, r1 - 1);
       idv[u] = rb + u < r1 ? sid[r] : -1;
+      if (rb + u < r1) DCHECK_IN(idv[u], 0, V, CHK_EMB_ID);
       const int64_t q = perm[r];
       const float* srow = q < n0 ? src0 + (size_t)q * E : src1 + (size_t)(q - n0) * E;
 #pragma unroll

@@ -15,7 +15,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <int ES>
 __global__ __launch_bounds__(256) void to_step_frame_kernel(const char* __restrict__ src, const int64_t* __restrict__ ids,
                                                             const int64_t* __restrict__ rev, char* __restrict__ out,
-                                                            int B, int T, int W, int S, int doff) {
+                                                            int B, int T, int W, int S, int doff, long nsrc) {
   const int cpr = W * ES / 16;  // 16-byte chunks per row
   const long n = 2L * T * B * cpr;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
@@ -24,8 +24,8 @@ __global__ __launch_bounds__(256) void to_step_frame_kernel(const char* __restri
     const int b = (int)(rowo % B);
     const int t = (int)((rowo / B) % T);
     const int d = (int)(rowo / ((long)B * T));
-    const int tt = d == 0 ? t : (int)rev[(size_t)b * T + t];
-    const long srow = ids ? ids[(size_t)b * T + tt] : (long)b * T + tt;
+    const int tt = d == 0 ? t : (int)DCHECK_IDX(rev[(size_t)b * T + t], 0, T, CHK_FRAME_REV);
+    const long srow = ids ? DCHECK_IDX(ids[(size_t)b * T + tt], 0, nsrc, CHK_FRAME_ID) : (long)b * T + tt;
     const u32x4 v = *reinterpret_cast<const u32x4*>(src + ((size_t)srow * S + (size_t)d * doff) * ES + (size_t)c * 16);
     *reinterpret_cast<u32x4*>(out + (size_t)rowo * W * ES + (size_t)c * 16) = v;
   }
@@ -41,7 +41,7 @@ __global__ __launch_bounds__(256) void from_step_frame_kernel(const float* __res
     const int c = (int)(i % cpr);
     const long bt = i / cpr;
     const int t = (int)(bt % T), b = (int)(bt / T);
-    const int rt = (int)rev[(size_t)b * T + t];
+    const int rt = (int)DCHECK_IDX(rev[(size_t)b * T + t], 0, T, CHK_FRAME_REV);
     const float4 x = *reinterpret_cast<const float4*>(in + ((size_t)t * B + b) * W + 4 * c);
     const float4 y = *reinterpret_cast<const float4*>(in + plane + ((size_t)rt * B + b) * W + 4 * c);
     *reinterpret_cast<float4*>(out + (size_t)bt * W + 4 * c) = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
@@ -85,14 +85,14 @@ static int grid_for(long n) {
 }
 
 void launch_to_step_frame(const void* src, int es, const int64_t* ids, const int64_t* rev, void* out, int B, int T,
-                          int W, int S, int doff, hipStream_t st) {
+                          int W, int S, int doff, long nsrc, hipStream_t st) {
   const long n = 2L * T * B * (W * es / 16);
   if (es == 2)
     hipLaunchKernelGGL(to_step_frame_kernel<2>, dim3(grid_for(n)), dim3(256), 0, st, (const char*)src, ids, rev,
-                       (char*)out, B, T, W, S, doff);
+                       (char*)out, B, T, W, S, doff, nsrc);
   else
     hipLaunchKernelGGL(to_step_frame_kernel<4>, dim3(grid_for(n)), dim3(256), 0, st, (const char*)src, ids, rev,
-                       (char*)out, B, T, W, S, doff);
+                       (char*)out, B, T, W, S, doff, nsrc);
 }
 
 void launch_from_step_frame(const float* in, const int64_t* rev, float* out, int B, int T, int W, hipStream_t st) {

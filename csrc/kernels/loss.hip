@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void ptr_loss_kernel(
   float c = 0.f;
   const float pg = pgen ? pgen[n] : 1.0f;
   if (pgen) {
-    const int len = lens[b];
+    const int len = (int)DCHECK_IDX(lens[b], 0, T + 1, CHK_LOSS_LEN);
     const float* ar = attn + (size_t)n * T;
     const int* er = ext + (size_t)b * T;
     for (int i = tid; i < len; i += 256) c += er[i] == w ? ar[i] : 0.f;
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void ptr_loss_kernel(
   }
   if (pgen) {
     if (tid == 0) dpre[n] = g != 0.f ? -g * (pv - c) * invP * pg * (1.0f - pg) : 0.f;
-    const int len = lens[b];
+    const int len = (int)DCHECK_IDX(lens[b], 0, T + 1, CHK_LOSS_LEN);
     const float coef = g != 0.f ? -g * (1.0f - pg) * invP : 0.f;
     const int* er = ext + (size_t)b * T;
     float* dar = dA + (size_t)n * T;
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void ptr_loss_bf16_kernel(
   float cm = 0.f;
   const float pg = pgen ? pgen[n] : 1.0f;
   if (pgen) {
-    const int len = lens[b];
+    const int len = (int)DCHECK_IDX(lens[b], 0, T + 1, CHK_LOSS_LEN);
     const float* ar = attn + (size_t)n * T;
     const int* er = ext + (size_t)b * T;
     for (int i = tid; i < len; i += 256) cm += er[i] == w ? ar[i] : 0.f;
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void ptr_loss_bf16_kernel(
   }
   if (pgen) {
     if (tid == 0) dpre[n] = g != 0.f ? -g * (pv - cm) * invP * pg * (1.0f - pg) : 0.f;
-    const int len = lens[b];
+    const int len = (int)DCHECK_IDX(lens[b], 0, T + 1, CHK_LOSS_LEN);
     const float coef = g != 0.f ? -g * (1.0f - pg) * invP : 0.f;
     const int* er = ext + (size_t)b * T;
     float* dar = dA + (size_t)n * T;

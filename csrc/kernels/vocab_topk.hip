@@ -286,7 +286,7 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
       pgd += x * pgi.w[i];
     }
   }
-  const int len = ptr ? lens[art] : 0;
+  const int len = ptr ? (int)DCHECK_IDX(lens[art], 0, T + 1, CHK_LOSS_LEN) : 0;
   float2 pm[PPT];
 #pragma unroll
   for (int u = 0; u < PPT; ++u) {

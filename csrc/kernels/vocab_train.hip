@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256) void ptr_rowfin_kernel(
     float* __restrict__ dA, int N, int B, int T) {
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (n >= N) return;
-  const int b = n % B, w = target[n], len = lens[b];
+  const int b = n % B, w = target[n], len = (int)DCHECK_IDX(lens[b], 0, T + 1, CHK_LOSS_LEN);
   const float g = rowg[n], pv = pv_in[n];
   const float pg = pgen ? pgen[n] : 1.0f;
   const int* er = ext + (size_t)b * T;

@@ -5,7 +5,9 @@ Two shared objects are produced next to this file:
 * ``_C.so``  -- the HIP/CDNA4 kernels (``csrc/kernels/*.hip``) plus the torch op
   registrations (``csrc/bindings.cpp``).  Compiled with ``hipcc --offload-arch=gfx950``;
   no hipify, no CUDA shims.  Loaded with ``torch.ops.load_library`` so every op is a
-  ``torch.ops.tsamd.*`` call that can be captured into a hipGraph.
+  ``torch.ops.tsamd.*`` call that can be captured into a hipGraph.  ``_C_debug.so`` is the
+  same library with the bounds checks of ``csrc/kernels/dcheck.h`` compiled in
+  (TSAMD_KERNEL_DEBUG=1 loads it).
 * ``_rt.so`` -- the host-side native runtime (``csrc/runtime/*.cpp``): shared-memory
   SPSC ring buffer (replaces Flink-AI-Extended's JVM<->Python mmap queue),
   TF tensor-bundle checkpoint reader/writer with crc32c, record codec.
@@ -73,31 +75,39 @@ def _headers(d):
     return out
 
 
-def build_kernels(verbose=False, jobs=8):
-    """Compile csrc/kernels/*.hip + csrc/bindings.cpp into textsummarization_on_flink_amd/_C.so."""
-    os.makedirs(BUILD, exist_ok=True)
+def build_kernels(verbose=False, jobs=8, debug=False):
+    """Compile csrc/kernels/*.hip + csrc/bindings.cpp into textsummarization_on_flink_amd/_C.so.
+
+    ``debug``: the bounds-checked variant ``_C_debug.so`` (-DTSAMD_DEBUG, csrc/kernels/dcheck.h;
+    relocatable device code so every kernel shares the one check record in debug.hip),
+    loaded instead of ``_C.so`` when TSAMD_KERNEL_DEBUG=1."""
+    bdir = BUILD + ("_debug" if debug else "")
+    os.makedirs(bdir, exist_ok=True)
     kdir = os.path.join(CSRC, "kernels")
     hips = sorted(os.path.join(kdir, f) for f in os.listdir(kdir) if f.endswith(".hip"))
     hdrs = _headers(kdir)
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
               "-Wno-unused-result", "-munsafe-fp-atomics", f"-I{kdir}"]
+    if debug:
+        common += ["-DTSAMD_DEBUG", "-fgpu-rdc"]
     objs, jobsl = [], []
     for src in hips:
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(bdir, os.path.basename(src) + ".o")
         objs.append(obj)
         if _newer([src] + hdrs, obj):
             jobsl.append([HIPCC, *common, "-c", src, "-o", obj])
     tflags, tld = _torch_flags()
     bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.o")
+    bobj = os.path.join(bdir, "bindings.o")
     objs.append(bobj)
     if _newer([bsrc] + hdrs, bobj):
         jobsl.append([HIPCC, "-O2", "-std=c++17", "-fPIC", f"-I{kdir}", *tflags, "-c", bsrc, "-o", bobj])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobsl))
-    so = os.path.join(PKG_DIR, "_C.so")
+    so = os.path.join(PKG_DIR, "_C_debug.so" if debug else "_C.so")
     if jobsl or not os.path.exists(so):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", so, *tld], verbose)
+        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + (["-fgpu-rdc"] if debug else [])
+        _run([*link, *objs, "-o", so, *tld], verbose)
     return so
 
 
@@ -115,11 +125,14 @@ def build_runtime(verbose=False):
     return so
 
 
-def build(verbose=False):
+def build(verbose=False, debug=True):
+    """Host runtime, release kernel library and (``debug``) its bounds-checked variant."""
     rt = build_runtime(verbose)
     c = build_kernels(verbose)
+    if debug:
+        build_kernels(verbose, debug=True)
     return rt, c
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    print(build(verbose="-v" in sys.argv, debug="--no-debug" not in sys.argv))
