@@ -154,3 +154,46 @@ def test_persistent_lstm_with_concurrent_kernels():
     busy = run(True)
     assert int(err.item()) == 0
     assert torch.equal(solo[0], busy[0]) and torch.equal(solo[1], busy[1])
+
+
+@pytest.mark.parametrize("H,B", [(256, 512), (512, 256)])
+def test_persistent_lstm_stress_full_grid(H, B):
+    """Stress of the inter-workgroup hand-off: 40 back-to-back forward + BPTT
+    launches at a grid that fills the chip (B = 512 at H = 256: 256 workgroups, one per CU;
+    H = 512: 8-wave teams), each bit-identical to the first and without a hand-off timeout.
+    A stale read of a peer's granule (XCD-local L2 coherence, tag reuse across launches)
+    would show up as a differing launch."""
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    T = 48
+    assert int(k.lstm_persistent_grid(H, B)) > 0
+    g, r, lens, gx, Wt, Wn, hs0, cs0 = _setup(H, B, T, 21 + H)
+    bias = torch.randn(2, 4 * H, device="cuda", generator=g) * 0.1
+    xf = torch.zeros(int(k.lstm_persistent_xbuf(H, B, False)), device="cuda", dtype=torch.long)
+    xb = torch.zeros(int(k.lstm_persistent_xbuf(H, B, True)), device="cuda", dtype=torch.long)
+    err = torch.zeros(1, device="cuda", dtype=torch.int32)
+    dout = torch.randn(2, T, B, H, device="cuda", generator=g) * 0.1
+    hs, cs = hs0.clone(), cs0.clone()
+    acts = torch.zeros(2, T, B, 4 * H, device="cuda")
+    out = torch.zeros(B, T, 2 * H, device="cuda", dtype=torch.bfloat16)
+    dz = torch.zeros(2, T, B, 4 * H, device="cuda", dtype=torch.bfloat16)
+    dcc = torch.zeros(2, B, H, device="cuda")
+    dhf = torch.zeros(2, B, H, device="cuda")
+    ref = None
+    for it in range(40):
+        hs.copy_(hs0)
+        cs.copy_(cs0)
+        xf.zero_()
+        k.lstm_fwd_persistent(gx, bias, Wt, hs, cs, acts, out, lens, xf, err, T, B, H)
+        dcc.zero_()
+        dhf.zero_()
+        xb.zero_()
+        k.lstm_bwd_persistent(dz, Wn, dout, dhf, dcc, acts, cs, lens, xb, err, None, T, B, H)
+        if ref is None:
+            ref = (out.clone(), dz.clone(), dcc.clone())
+        elif it % 8 == 0 or it == 39:
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref[0]) and torch.equal(dz, ref[1]) and torch.equal(dcc, ref[2]), it
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert torch.equal(out, ref[0]) and torch.equal(dz, ref[1])
