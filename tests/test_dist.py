@@ -1,4 +1,4 @@
-"""Data parallelism on CPU (gloo, world_size 2): bucketed async all-reduce and DP=2 training
+"""Data parallelism on CPU (gloo, world_size 2 and 8): bucketed async all-reduce and DP=2 training
 equivalent to DP=1 on the concatenated batch (SURVEY 4 "distributed tier", 7.5-6)."""
 import os
 
@@ -87,25 +87,32 @@ def test_bf16_compressed_allreduce_sums():
     assert res[0][0] == pytest.approx(want, rel=1e-2) and res[1][0] == res[0][0]
 
 
-def test_dp2_matches_dp1_on_concatenated_batch():
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_matches_dp1_on_concatenated_batch(world):
+    """DP=world (2, and the 8-rank node layout rehearsed over gloo on the CPU) == DP=1 on the
+    concatenated batch: every rank ends with the same parameters as one process stepping on
+    all the rows (gradient sum over ranks, 1/world average, clip and Adagrad after it)."""
     from textsummarization_on_flink_amd.config import HParams
     from textsummarization_on_flink_amd.data.batch import Batch, Example
     from textsummarization_on_flink_amd.data.vocab import abstract2sents
     from textsummarization_on_flink_amd.train.cpu_trainer import CpuTrainer
     c = tiny_corpus(3)
     vocab = c.vocab()
-    hps = HParams(hidden_dim=16, emb_dim=8, vocab_size=200, max_enc_steps=30, max_dec_steps=8, batch_size=4,
+    n = 16  # rows per step over all ranks
+    bs = n // world
+    hps = HParams(hidden_dim=16, emb_dim=8, vocab_size=200, max_enc_steps=30, max_dec_steps=8, batch_size=bs,
                   coverage=True)
-    exs = [Example(a, [x.strip() for x in abstract2sents(s)], vocab, hps) for a, s in c.examples(16)]
-    # two steps; each step: rank r gets rows [8k + 4r, 8k + 4r + 4); DP1 gets all 8 rows (same max enc len padding)
-    per_rank = {r: [Batch(exs[8 * k + 4 * r: 8 * k + 4 * r + 4], hps, vocab, pad_enc_to=30) for k in range(2)]
-                for r in range(2)}
-    res = _spawn(_train_worker, 2, (hps, vocab.size(), per_rank))
-    hps8 = hps.replace(batch_size=8)
-    tr = CpuTrainer(hps8, vocab.size())
+    exs = [Example(a, [x.strip() for x in abstract2sents(s)], vocab, hps) for a, s in c.examples(2 * n)]
+    # two steps; each step: rank r gets rows [n k + bs r, n k + bs (r + 1)); DP1 gets all n rows (same padding)
+    per_rank = {r: [Batch(exs[n * k + bs * r: n * k + bs * (r + 1)], hps, vocab, pad_enc_to=30) for k in range(2)]
+                for r in range(world)}
+    res = _spawn(_train_worker, world, (hps, vocab.size(), per_rank))
+    hpsn = hps.replace(batch_size=n)
+    tr = CpuTrainer(hpsn, vocab.size())
     for k in range(2):
-        tr.step(Batch(exs[8 * k: 8 * k + 8], hps8, vocab, pad_enc_to=30))
-    assert (res[0][0] == res[1][0]).all()  # ranks stay identical
+        tr.step(Batch(exs[n * k: n * (k + 1)], hpsn, vocab, pad_enc_to=30))
+    for r in range(1, world):
+        assert (res[0][0] == res[r][0]).all()  # ranks stay identical
     assert torch.allclose(torch.from_numpy(res[0][0]), tr.params.flat, atol=1e-5, rtol=1e-4)
 
 
