@@ -146,3 +146,38 @@ def test_row_split_streams_match_single_chain(monkeypatch, split):
     assert abs(got[0][0] - got[1][0]) < 1e-5 * abs(got[0][0])
     assert _rel(got[1][1], got[0][1]) < 1e-6
     assert _rel(got[1][2], got[0][2]) < 1e-4
+
+
+def test_deferred_weight_gradients_match_inline(monkeypatch):
+    """The decoder-side weight gradients deferred onto a side stream beside the encoder BPTT
+    (TSAMD_DEFER_WGRAD, default on) give the gradients of the inline order, in eager mode
+    and through the captured phase graphs."""
+    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
+    B = 128
+    hps = _hps(B, trunc_norm_init_std=0.05).replace(max_dec_steps=24)
+    vocab, (batch,) = _batches(hps, 1, seed=15)
+    got = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("TSAMD_DEFER_WGRAD", defer)
+        params = build_params(hps, vocab.size(), device="cuda", seed=6).enable_grad()
+        eng = HipPointerGenerator(hps, vocab.size(), params, B=B, T=T, D=24)
+        assert eng.defer_wgrad == (defer == "1")
+        eng.set_batch(batch)
+        eng.forward(need_grad=True)
+        eng.backward()
+        torch.cuda.synchronize()
+        eager = params.grad.clone()
+        g = [torch.cuda.CUDAGraph() for _ in range(3)]
+        with torch.cuda.graph(g[0]):
+            eng.forward(need_grad=True)
+            eng.backward_head()
+        with torch.cuda.graph(g[1]):
+            eng.backward_mid()
+        with torch.cuda.graph(g[2]):
+            eng.backward_tail()
+        for x in g:
+            x.replay()
+        torch.cuda.synchronize()
+        got.append((eager, params.grad.clone()))
+    for a, b in ((got[0][0], got[1][0]), (got[0][0], got[1][1]), (got[0][0], got[0][1])):
+        assert _rel(b, a) < 1e-5, _rel(b, a)

@@ -241,6 +241,15 @@ class HipPointerGenerator:
             w["lstm_xb"] = z(int(self.k.lstm_persistent_xbuf(H, B, True)), dt=torch.long)
             w["lstm_db"] = z(2, 4 * H)  # gate-bias gradients [fw; bw] accumulated by the BPTT kernel
         w["lstm_err"] = z(1, dt=torch.int32)
+        # decoder-side weight gradients that nothing later in the step reads (output projection,
+        # cell, input merge, attention query, W_h) run on a side stream beside the encoder BPTT,
+        # which leaves half the CUs idle at B <= 256 (forked and joined inside backward_tail);
+        # not when the persistent BPTT grid fills the chip.  TSAMD_DEFER_WGRAD=0: inline.
+        self._late = []
+        self.defer_wgrad = (os.environ.get("TSAMD_DEFER_WGRAD", "1") != "0" and (
+            not self.persistent_lstm or
+            int(self.k.lstm_persistent_grid(H, B)) <= int(self.k.lstm_persistent_capacity(H)) - 64))
+        self._late_stream = torch.cuda.Stream(self.dev) if self.defer_wgrad else None
         # reduce_states: pre-activations [c; h], bf16 [fw, bw] inputs and bf16 dp (wgrad operands)
         w["rs_pre"] = z(2, B, H)
         w["rs_cat"] = z(2, B, 2 * H, dt=BF)
@@ -305,6 +314,7 @@ class HipPointerGenerator:
         w["DX"] = z(D, B, E)
         w["DZ"] = z(D, B, 4 * H, dt=BF)
         w["DS"] = z(D, B, A)
+        w["d_emb_dec"] = z(D * B, E)  # decoder-input embedding gradient rows
         w["DE"] = z(D, B, T)
         w["da"] = None if self.fused_attn_bwd else z(B, T)
         w["dcov"] = z(2, B, T)
@@ -638,8 +648,13 @@ class HipPointerGenerator:
         Hn = w["Hb"][1:].reshape(N, H)
         ctxb = w["CTXb"].view(N, A)
         doutb = self._cast_colsum(dout, g(OUT_B))
-        wgrad_into(g(OUT_M)[:H], Hn, doutb)
-        wgrad_into(g(OUT_M)[H:], ctxb, doutb)
+        late = self._late = []  # deferred weight gradients (see defer_wgrad)
+        run = late.append if self.defer_wgrad else (lambda f: f())
+
+        def out_proj_wgrad():
+            wgrad_into(g(OUT_M)[:H], Hn, doutb)
+            wgrad_into(g(OUT_M)[H:], ctxb, doutb)
+        run(out_proj_wgrad)
         dH_dir = mmf(doutb, self.pk["OUTm"][:H].t()).view(D, B, H)
         dCTX_dir = mmf(doutb, self.pk["OUTm"][H:].t()).view(D, B, A)
         dC_dir = None
@@ -698,24 +713,26 @@ class HipPointerGenerator:
 
         self._row_groups(chain)
         # ---- decoder weight gradients (one GEMM each over all D*B rows)
-        DZ = w["DZ"].view(N, 4 * H)
-        gk = g(CELL_K)
-        wgrad_into(gk[:E], w["Xb"].view(N, E), DZ)
-        wgrad_into(gk[E:], w["Hb"][:D].reshape(N, H), DZ)
-        g(CELL_B).copy_(DZ.sum(0, dtype=F32))
-        DX = w["DX"].view(N, E)
-        DXb = self._cast_colsum(DX, g(LIN_B))
-        gl = g(LIN_M)
-        wgrad_into(gl[:E], self._emb_dec, DXb)
-        gl[E:].zero_()
-        if D > 1:
-            wgrad_into(gl[E:], w["CTXb"][:D - 1].reshape((D - 1) * B, A), DXb[B:])
-        d_emb_dec = mmf(DXb, self.pk["lin_emb"].t())  # [N,E]
-        DS = w["DS"].view(N, A)
-        DSb = self._cast_colsum(DS, g(ATT_B))
-        gs = g(ATT_M)
-        wgrad_into(gs[:H], w["Cb"][1:].reshape(N, H), DSb)
-        wgrad_into(gs[H:], Hn, DSb)
+        emb_dec = self._emb_dec
+
+        def dec_wgrad():
+            DZ = w["DZ"].view(N, 4 * H)
+            gk = g(CELL_K)
+            wgrad_into(gk[:E], w["Xb"].view(N, E), DZ)
+            wgrad_into(gk[E:], w["Hb"][:D].reshape(N, H), DZ)
+            torch.sum(DZ, 0, dtype=F32, out=g(CELL_B))
+            DXb = self._cast_colsum(w["DX"].view(N, E), g(LIN_B))
+            gl = g(LIN_M)
+            wgrad_into(gl[:E], emb_dec, DXb)
+            gl[E:].zero_()
+            if D > 1:
+                wgrad_into(gl[E:], w["CTXb"][:D - 1].reshape((D - 1) * B, A), DXb[B:])
+            torch.mm(DXb, self.pk["lin_emb"].t(), out_dtype=F32, out=w["d_emb_dec"])  # [N,E]
+            DSb = self._cast_colsum(w["DS"].view(N, A), g(ATT_B))
+            gs = g(ATT_M)
+            wgrad_into(gs[:H], w["Cb"][1:].reshape(N, H), DSb)
+            wgrad_into(gs[H:], Hn, DSb)
+        run(dec_wgrad)
         # ---- attention feature gradients (tanh recomputed once over all steps)
         w["dv"].zero_()
         w["dwc"].zero_()
@@ -726,7 +743,7 @@ class HipPointerGenerator:
             g(WCOV).view(A).copy_(w["dwc"].sum(0))
         dFb = w["dF"].view(B * T, A)
         top = self.enc[-1]
-        wgrad_into(g(WH).view(A, A), top["out"].view(B * T, A), dFb)
+        run(lambda: wgrad_into(g(WH).view(A, A), top["out"].view(B * T, A), dFb))
         dE = self._dE
         # dE = a^T . dctx (bf16 batched GEMM, fp32 out) + dF . W_h^T (accumulated in place)
         w["ATTb"].copy_(w["ATT"])
@@ -734,7 +751,7 @@ class HipPointerGenerator:
         torch.bmm(w["ATTb"].permute(1, 2, 0), w["DCTXb"].permute(1, 0, 2), out_dtype=F32, out=dE)
         dE2 = dE.view(B * T, A)
         torch.addmm(dE2, dFb, self.pk["Wh"].t(), out_dtype=F32, out=dE2)
-        self._dE, self._d_emb_dec = dE, d_emb_dec
+        self._dE = dE
         if self._side is not None:  # join the output-projection weight gradient
             torch.cuda.current_stream().wait_stream(self._side)
 
@@ -743,8 +760,15 @@ class HipPointerGenerator:
         k, w, p = self.k, self.w, self.p
         B, T, H = self.B, self.T, self.H
         g = p.g
-        dE, d_emb_dec = self._dE, self._d_emb_dec
+        dE = self._dE
         lens = w["enc_lens"]
+        late, self._late = self._late, []
+        if late:  # the deferred decoder weight gradients, beside the encoder BPTT
+            side = self._late_stream
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for f in late:
+                    f()
         # ---- reduce_states (reduce_states.hip): dp = g [pre > 0], bias gradients, and
         # d[c_fw, c_bw] / d[h_fw, h_bw] written straight into the top layer's BPTT seeds
         top = self.enc[-1]
@@ -790,7 +814,9 @@ class HipPointerGenerator:
         # atomics only where the id changes, so Zipf-hot tokens do not serialise
         ids = torch.cat([w["enc_batch"].view(-1), w["dec_batch_t"].view(-1)]).to(torch.int32)
         sid, perm = torch.sort(ids)
-        k.emb_grad_sorted(gemb, sid, perm, d_in.reshape(B * T, self.E), d_emb_dec.contiguous())
+        if late:
+            torch.cuda.current_stream().wait_stream(self._late_stream)  # d_emb_dec and the weight gradients
+        k.emb_grad_sorted(gemb, sid, perm, d_in.reshape(B * T, self.E), w["d_emb_dec"])
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_step(self):

@@ -153,7 +153,8 @@ class GraphTrainer:
                 elif i == 1:
                     if self.engine._side is not None:  # the output-projection dW ran beside backward_mid
                         self.reducer.bucket_ready(0)
-                    self.reducer.bucket_ready(1)
+                    if not self.engine.defer_wgrad:  # else bucket 1 completes beside the encoder BPTT
+                        self.reducer.bucket_ready(1)
             self._maybe_poison()
             self.reducer()
             if ev:
