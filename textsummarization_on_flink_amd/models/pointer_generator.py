@@ -244,9 +244,13 @@ class HipPointerGenerator:
         # decoder-side weight gradients that nothing later in the step reads (output projection,
         # cell, input merge, attention query, W_h) run on a side stream beside the encoder BPTT,
         # which leaves half the CUs idle at B <= 256 (forked and joined inside backward_tail);
-        # not when the persistent BPTT grid fills the chip.  TSAMD_DEFER_WGRAD=0: inline.
+        # not when the persistent BPTT grid fills the chip.  Opt-in (TSAMD_DEFER_WGRAD=1): the
+        # library GEMMs on that stream are stream-K kernels (hipBLASLt SK3: a tile owner spins on
+        # flags of higher-numbered workgroups), and two such kernels -- or one beside the
+        # persistent BPTT, which spins on its own peers -- can each hold CUs the other's waiting
+        # workgroups need; two concurrent library GEMMs in the vocab backward did hang.
         self._late = []
-        self.defer_wgrad = (os.environ.get("TSAMD_DEFER_WGRAD", "1") != "0" and (
+        self.defer_wgrad = (os.environ.get("TSAMD_DEFER_WGRAD", "0") == "1" and (
             not self.persistent_lstm or
             int(self.k.lstm_persistent_grid(H, B)) <= int(self.k.lstm_persistent_capacity(H)) - 64))
         self._late_stream = torch.cuda.Stream(self.dev) if self.defer_wgrad else None
