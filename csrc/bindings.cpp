@@ -416,6 +416,22 @@ void ptr_loss(const Tensor& logits, const OT& bias, const Tensor& target, const 
                   B, T, V, stream());
 }
 
+// weight gradient out[M][N] += a[K][M]^T . b[K][N] (wgrad.hip): 2-D row-major views with unit
+// column stride (row strides free), out fp32 and already zero (split-K atomics)
+void wgrad_tn(const Tensor& a, const Tensor& b, const Tensor& out) {
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "wgrad_tn: 2-D views");
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "wgrad_tn: GPU tensors");
+  TORCH_CHECK(a.scalar_type() == BF && b.scalar_type() == BF && out.scalar_type() == F32, "wgrad_tn: bf16, bf16 -> fp32");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.stride(1) == 1, "wgrad_tn: unit column stride");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "wgrad_tn: shapes");
+  TORCH_CHECK(M % 128 == 0 && N % 128 == 0 && K >= 1, "wgrad_tn: M, N multiples of 128");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && (uintptr_t)a.data_ptr() % 16 == 0 &&
+              (uintptr_t)b.data_ptr() % 16 == 0, "wgrad_tn: 16-byte aligned rows");
+  launch_wgrad_tn(P<bf16>(a), (int)a.stride(0), P<bf16>(b), (int)b.stride(0), P<float>(out), (int)out.stride(0),
+                  (int)M, (int)N, (int)K, stream());
+}
+
 // debug build (dcheck.h / debug.hip): first failed bounds check (id, block, thread, value)
 int64_t debug_enabled() { return tsamd_debug_enabled(); }
 Tensor debug_status() {
@@ -694,6 +710,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("dec_bwd_cell", &dec_bwd_cell);
   m.def("dec_bwd_dz", &dec_bwd_dz);
   m.def("ptr_loss", &ptr_loss);
+  m.def("wgrad_tn", &wgrad_tn);
   m.def("debug_enabled", &debug_enabled);
   m.def("debug_status", &debug_status);
   m.def("debug_clear", &debug_clear);

@@ -140,3 +140,8 @@ void launch_emb_grad_sorted(float* gemb, const int* sid, const int64_t* perm, co
 int tsamd_debug_enabled();
 void tsamd_debug_read(unsigned* out4);
 void tsamd_debug_clear();
+
+// weight-gradient GEMM out[M][N] += a[K][M]^T b[K][N] (wgrad.hip; out pre-zeroed, M, N % 128 == 0)
+int wgrad_tn_splits(int M, int N, int K);
+void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out, int ldo, int M, int N, int K,
+                     hipStream_t st);

@@ -244,13 +244,14 @@ class HipPointerGenerator:
         # decoder-side weight gradients that nothing later in the step reads (output projection,
         # cell, input merge, attention query, W_h) run on a side stream beside the encoder BPTT,
         # which leaves half the CUs idle at B <= 256 (forked and joined inside backward_tail);
-        # not when the persistent BPTT grid fills the chip.  Opt-in (TSAMD_DEFER_WGRAD=1): the
-        # library GEMMs on that stream are stream-K kernels (hipBLASLt SK3: a tile owner spins on
-        # flags of higher-numbered workgroups), and two such kernels -- or one beside the
-        # persistent BPTT, which spins on its own peers -- can each hold CUs the other's waiting
-        # workgroups need; two concurrent library GEMMs in the vocab backward did hang.
+        # not when the persistent BPTT grid fills the chip.  Only custom kernels run on that
+        # stream (wgrad.hip, cast_colsum, reductions): the library GEMMs are stream-K kernels
+        # (hipBLASLt SK3: a tile owner spins on flags of higher-numbered workgroups), and two
+        # such kernels -- or one beside the persistent BPTT, which spins on its own peers -- can
+        # each hold CUs the other's waiting workgroups need (two concurrent library GEMMs in the
+        # vocab backward hung on MI355X).  TSAMD_DEFER_WGRAD=0: inline.
         self._late = []
-        self.defer_wgrad = (os.environ.get("TSAMD_DEFER_WGRAD", "0") == "1" and (
+        self.defer_wgrad = (os.environ.get("TSAMD_DEFER_WGRAD", "1") != "0" and E % 128 == 0 and H % 128 == 0 and (
             not self.persistent_lstm or
             int(self.k.lstm_persistent_grid(H, B)) <= int(self.k.lstm_persistent_capacity(H)) - 64))
         self._late_stream = torch.cuda.Stream(self.dev) if self.defer_wgrad else None
@@ -654,10 +655,13 @@ class HipPointerGenerator:
         doutb = self._cast_colsum(dout, g(OUT_B))
         late = self._late = []  # deferred weight gradients (see defer_wgrad)
         run = late.append if self.defer_wgrad else (lambda f: f())
+        # the deferred ones go through wgrad_tn (wgrad.hip: no inter-workgroup waits) into the
+        # zeroed gradient slices; inline, the library split-K path
+        wg = (lambda out, a, b: k.wgrad_tn(a, b, out)) if self.defer_wgrad else wgrad_into
 
         def out_proj_wgrad():
-            wgrad_into(g(OUT_M)[:H], Hn, doutb)
-            wgrad_into(g(OUT_M)[H:], ctxb, doutb)
+            wg(g(OUT_M)[:H], Hn, doutb)
+            wg(g(OUT_M)[H:], ctxb, doutb)
         run(out_proj_wgrad)
         dH_dir = mmf(doutb, self.pk["OUTm"][:H].t()).view(D, B, H)
         dCTX_dir = mmf(doutb, self.pk["OUTm"][H:].t()).view(D, B, A)
@@ -719,23 +723,24 @@ class HipPointerGenerator:
         # ---- decoder weight gradients (one GEMM each over all D*B rows)
         emb_dec = self._emb_dec
 
+        DXb = self._cast_colsum(w["DX"].view(N, E), g(LIN_B))
+        torch.mm(DXb, self.pk["lin_emb"].t(), out_dtype=F32, out=w["d_emb_dec"])  # [N,E] (embedding gradient)
+
         def dec_wgrad():
             DZ = w["DZ"].view(N, 4 * H)
             gk = g(CELL_K)
-            wgrad_into(gk[:E], w["Xb"].view(N, E), DZ)
-            wgrad_into(gk[E:], w["Hb"][:D].reshape(N, H), DZ)
+            wg(gk[:E], w["Xb"].view(N, E), DZ)
+            wg(gk[E:], w["Hb"][:D].reshape(N, H), DZ)
             torch.sum(DZ, 0, dtype=F32, out=g(CELL_B))
-            DXb = self._cast_colsum(w["DX"].view(N, E), g(LIN_B))
             gl = g(LIN_M)
-            wgrad_into(gl[:E], emb_dec, DXb)
+            wg(gl[:E], emb_dec, DXb)
             gl[E:].zero_()
             if D > 1:
-                wgrad_into(gl[E:], w["CTXb"][:D - 1].reshape((D - 1) * B, A), DXb[B:])
-            torch.mm(DXb, self.pk["lin_emb"].t(), out_dtype=F32, out=w["d_emb_dec"])  # [N,E]
+                wg(gl[E:], w["CTXb"][:D - 1].reshape((D - 1) * B, A), DXb[B:])
             DSb = self._cast_colsum(w["DS"].view(N, A), g(ATT_B))
             gs = g(ATT_M)
-            wgrad_into(gs[:H], w["Cb"][1:].reshape(N, H), DSb)
-            wgrad_into(gs[H:], Hn, DSb)
+            wg(gs[:H], w["Cb"][1:].reshape(N, H), DSb)
+            wg(gs[H:], Hn, DSb)
         run(dec_wgrad)
         # ---- attention feature gradients (tanh recomputed once over all steps)
         w["dv"].zero_()
@@ -747,7 +752,7 @@ class HipPointerGenerator:
             g(WCOV).view(A).copy_(w["dwc"].sum(0))
         dFb = w["dF"].view(B * T, A)
         top = self.enc[-1]
-        run(lambda: wgrad_into(g(WH).view(A, A), top["out"].view(B * T, A), dFb))
+        run(lambda: wg(g(WH).view(A, A), top["out"].view(B * T, A), dFb))
         dE = self._dE
         # dE = a^T . dctx (bf16 batched GEMM, fp32 out) + dF . W_h^T (accumulated in place)
         w["ATTb"].copy_(w["ATT"])
