@@ -153,7 +153,7 @@ def test_deferred_weight_gradients_match_inline(monkeypatch):
     (TSAMD_DEFER_WGRAD, default on) give the gradients of the inline order, in eager mode
     and through the captured phase graphs."""
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
-    B = 128
+    B = 256
     hps = _hps(B, trunc_norm_init_std=0.05).replace(max_dec_steps=24)
     vocab, (batch,) = _batches(hps, 1, seed=15)
     got = []

@@ -251,7 +251,10 @@ class HipPointerGenerator:
         # each hold CUs the other's waiting workgroups need (two concurrent library GEMMs in the
         # vocab backward hung on MI355X).  TSAMD_DEFER_WGRAD=0: inline.
         self._late = []
-        self.defer_wgrad = (os.environ.get("TSAMD_DEFER_WGRAD", "1") != "0" and E % 128 == 0 and H % 128 == 0 and (
+        # Measured (bench A/B): +0.6-1.3% at B = 256; at B = 64 / 128 the BPTT it runs beside
+        # slows more (its hand-offs are latency-bound) than the moved work saves, so B >= 256.
+        self.defer_wgrad = (os.environ.get("TSAMD_DEFER_WGRAD", "1") != "0" and B >= 256 and E % 128 == 0
+                            and H % 128 == 0 and (
             not self.persistent_lstm or
             int(self.k.lstm_persistent_grid(H, B)) <= int(self.k.lstm_persistent_capacity(H)) - 64))
         self._late_stream = torch.cuda.Stream(self.dev) if self.defer_wgrad else None
