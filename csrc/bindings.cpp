@@ -432,6 +432,15 @@ void wgrad_tn(const Tensor& a, const Tensor& b, const Tensor& out) {
                   (int)M, (int)N, (int)K, stream());
 }
 
+// weight repack (pack.hip): jobs [nj][13] int64 on the device (see the kernel for the layout)
+int64_t pack_max_jobs_op() { return pack_max_jobs(); }
+void pack_cast(const Tensor& jobs, int64_t total) {
+  TORCH_CHECK(jobs.is_cuda() && jobs.scalar_type() == at::kLong && jobs.is_contiguous() && jobs.dim() == 2 &&
+              jobs.size(1) == 13, "pack_cast: jobs [nj][13] int64 on the GPU");
+  TORCH_CHECK(jobs.size(0) >= 1 && jobs.size(0) <= pack_max_jobs(), "pack_cast: 1..", pack_max_jobs(), " jobs");
+  launch_pack_cast(P<long>(jobs), (int)jobs.size(0), (long)total, stream());
+}
+
 // debug build (dcheck.h / debug.hip): first failed bounds check (id, block, thread, value)
 int64_t debug_enabled() { return tsamd_debug_enabled(); }
 Tensor debug_status() {
@@ -711,6 +720,8 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("dec_bwd_dz", &dec_bwd_dz);
   m.def("ptr_loss", &ptr_loss);
   m.def("wgrad_tn", &wgrad_tn);
+  m.def("pack_cast", &pack_cast);
+  m.def("pack_max_jobs", &pack_max_jobs_op);
   m.def("debug_enabled", &debug_enabled);
   m.def("debug_status", &debug_status);
   m.def("debug_clear", &debug_clear);

@@ -145,3 +145,7 @@ void tsamd_debug_clear();
 int wgrad_tn_splits(int M, int N, int K);
 void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out, int ldo, int M, int N, int K,
                      hipStream_t st);
+
+// weight repack as one launch over a job table (pack.hip)
+int pack_max_jobs();
+void launch_pack_cast(const long* jobs, int nj, long total, hipStream_t st);

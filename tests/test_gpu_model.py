@@ -172,3 +172,26 @@ def test_row_attention_matches_multiblock_kernels(monkeypatch, coverage, B, T, H
     # ds_k = sum_i de_i q_ik cancels (sum_i de_i = 0), so summation order shows at ~1e-3
     for n, a, b, tol in zip(("DE", "DS", "dF", "grad"), bw[0], bw[1], (2e-3, 1e-2, 1e-2, 2e-3)):
         assert _rel(a, b) < tol, (n, _rel(a, b))
+
+
+@pytest.mark.parametrize("layers,H", [(1, 256), (2, 128)])
+def test_fast_pack_matches_torch_pack(layers, H):
+    """pack() after the first call = one pack_cast launch over the job table (pack.hip): every
+    bf16 / fp32 layout bit-identical to the torch cast / transpose / cat path."""
+    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
+    hps = HParams(batch_size=16, max_enc_steps=32, max_dec_steps=6, vocab_size=2000, emb_dim=128, hidden_dim=H,
+                  coverage=True, pointer_gen=True, enc_layers=layers)
+    params = build_params(hps, 2000, device="cuda", seed=2).enable_grad()
+    eng = HipPointerGenerator(hps, 2000, params, B=16, T=32, D=6)
+    assert eng._pack_jobs is not None
+    params.flat.add_(torch.randn_like(params.flat) * 0.01)  # new master weights
+    eng.pack()  # fast path
+    torch.cuda.synchronize()
+    fast = {k: v.clone() for k, v in eng.pk.items()}
+    fastf = {k: v.clone() for k, v in eng.f32.items() if v is not None}
+    eng._pack_torch()
+    torch.cuda.synchronize()
+    for k, v in eng.pk.items():
+        assert torch.equal(fast[k], v), k
+    for k, v in fastf.items():
+        assert torch.equal(v, eng.f32[k]), k

@@ -350,7 +350,62 @@ class HipPointerGenerator:
 
     # ------------------------------------------------------------------ weights
     def pack(self):
-        """fp32 master -> bf16 kernel layouts (recomputed after every optimizer step)."""
+        """fp32 master -> bf16 kernel layouts (recomputed after every optimizer step).  The
+        first call allocates the layouts through torch ops; later calls (the optimizer graph)
+        recompute W_comb with one GEMM and refresh every layout with ONE pack_cast launch over a
+        job table (pack.hip) instead of ~50 cast / copy / cat launches.  TSAMD_PACK_FAST=0: the
+        torch path every time."""
+        jobs = getattr(self, "_pack_jobs", None)
+        if jobs is not None:
+            E = self.E
+            torch.mm(self.p[LIN_M][E:], self.p[CELL_K][:E], out=self._wcomb)
+            self.k.pack_cast(jobs, self._pack_total)
+            return
+        self._pack_torch()
+        if os.environ.get("TSAMD_PACK_FAST", "1") != "0" and self.p.flat.is_cuda:
+            self._build_pack_jobs()
+
+    def _pack_job_pairs(self):
+        """(destination view, fp32 source view) of every layout pack() maintains."""
+        p, E, H, A, pk, f32 = self.p, self.E, self.H, self.A, self.pk, self.f32
+        M, K, W = p[LIN_M], p[CELL_K], self._wcomb
+        pairs = [(pk["emb"], p[EMB])]
+        for layer in range(self.L):
+            din = E if layer == 0 else A
+            for di, d in enumerate(("fw", "bw")):
+                Kd = p[enc_k(layer, d)]
+                pairs += [(pk[f"enc{layer}_Kx{di}"], Kd[:din]),
+                          (pk[f"enc{layer}_Kxi{di}"].view(din, H, 4), Kd[:din].view(din, 4, H).permute(0, 2, 1)),
+                          (pk[f"enc{layer}_Wn"][di], Kd[din:]), (pk[f"enc{layer}_Wt"][di], Kd[din:].t()),
+                          (f32[f"enc{layer}_b"][di], p[enc_b(layer, d)])]
+        pairs += [(pk["Wh"], p[WH].reshape(A, A)), (pk["RC"], p[RC]), (pk["RH"], p[RH]), (pk["RCt"], p[RC].t()),
+                  (pk["RHt"], p[RH].t()), (pk["lin_emb"], M[:E]), (pk["Wic"], M[E:]), (pk["WicT"], M[E:].t()),
+                  (pk["cell_x"], K[:E]), (pk["WcT2"][:, :A], W.t()), (pk["WcT2"][:, A:], K[E:].t()),
+                  (pk["Wbig"][:E + H], K), (pk["Wbig"][E + H:], W), (pk["Ws"], p[ATT_M]), (pk["WsT"], p[ATT_M].t()),
+                  (pk["OUTm"], p[OUT_M]), (pk["OUTmT"], p[OUT_M].t()), (pk["ow"], p[OW]), (pk["ovb"], p[OV])]
+        if "owT" in pk:
+            pairs.append((pk["owT"], p[OW].t()))
+        return pairs
+
+    def _build_pack_jobs(self):
+        E = self.E
+        self._wcomb = torch.mm(self.p[LIN_M][E:], self.p[CELL_K][:E])
+        rows, off = [], 0
+        for dst, src in self._pack_job_pairs():
+            assert dst.shape == src.shape and src.dtype == F32 and dst.dtype in (BF, F32) and dst.dim() <= 3, \
+                (dst.shape, src.shape)
+            shape = [1] * (3 - dst.dim()) + list(dst.shape)
+            ss = [0] * (3 - src.dim()) + list(src.stride())
+            ts = [0] * (3 - dst.dim()) + list(dst.stride())
+            n = dst.numel()
+            rows.append([src.data_ptr(), dst.data_ptr(), *shape, *ss, *ts, off, int(dst.dtype == F32)])
+            off += n
+        if len(rows) > int(self.k.pack_max_jobs()):
+            return  # keep the torch path
+        self._pack_jobs = torch.tensor(rows, dtype=torch.long, device=self.dev)
+        self._pack_total = off
+
+    def _pack_torch(self):
         p, E, H, A = self.p, self.E, self.H, self.A
         pk = getattr(self, "pk", None) or {}
 
