@@ -690,6 +690,17 @@ void pgen_bwd(const Tensor& ctx, const Tensor& c, const Tensor& h, const Tensor&
                   stream());
 }
 
+// gb (+)= sum(dpre) with atomics: pass the zeroed p_gen bias-gradient slot
+void pgen_dirs(const Tensor& dpre, const Tensor& w, const Tensor& dctx, const Tensor& dc, const Tensor& dh,
+               const Tensor& dx, const Tensor& gb, int64_t N, int64_t A, int64_t H, int64_t E) {
+  chk(dpre, F32, "dpre"); chk(w, F32, "w"); chk(dctx, F32, "dctx"); chk(dc, F32, "dc"); chk(dh, F32, "dh");
+  chk(dx, F32, "dx"); chk(gb, F32, "gb");
+  numel_eq(dpre, N, "dpre"); numel_eq(w, A + 2 * H + E, "w"); numel_eq(dctx, N * A, "dctx"); numel_eq(dc, N * H, "dc");
+  numel_eq(dh, N * H, "dh"); numel_eq(dx, N * E, "dx"); numel_eq(gb, 1, "gb");
+  launch_pgen_dirs(P<float>(dpre), P<float>(w), P<float>(dctx), P<float>(dc), P<float>(dh), P<float>(dx), P<float>(gb),
+                   (int)N, (int)A, (int)H, (int)E, stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tsamd, m) {
@@ -720,6 +731,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("dec_bwd_dz", &dec_bwd_dz);
   m.def("ptr_loss", &ptr_loss);
   m.def("wgrad_tn", &wgrad_tn);
+  m.def("pgen_dirs", &pgen_dirs);
   m.def("pack_cast", &pack_cast);
   m.def("pack_max_jobs", &pack_max_jobs_op);
   m.def("debug_enabled", &debug_enabled);

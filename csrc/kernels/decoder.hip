@@ -181,6 +181,37 @@ __global__ __launch_bounds__(256) void pgen_bwd_kernel(const float* __restrict__
   atomicAdd(gw + k, acc);
 }
 
+// p_gen gradient into the decoder inputs, all D*B rows in one launch (the hoisted per-step
+// "direct" terms of the reverse loop):  with dp = dL/d(p_gen pre-activation) and the p_gen
+// weight w = [w_ctx | w_c | w_h | w_x],
+//   dCTX_dir += dp w_ctx,  dC_dir = dp w_c,  dH_dir += dp w_h,  dX_dir = dp w_x,
+// plus the p_gen bias gradient sum(dp) (one atomic per workgroup).  Replaces a reduction,
+// four broadcast products, two adds and two copies.  One wave per row.
+__global__ __launch_bounds__(256) void pgen_dirs_kernel(const float* __restrict__ dpre, const float* __restrict__ w,
+                                                        float* __restrict__ dctx, float* __restrict__ dc,
+                                                        float* __restrict__ dh, float* __restrict__ dx,
+                                                        float* __restrict__ gb, int N, int A, int H, int E) {
+  __shared__ float red[4];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + wid;
+  float d = 0.f;
+  if (n < N) {
+    d = dpre[n];
+    const float* wc = w + A;
+    const float* wh = w + A + H;
+    const float* wx = w + A + 2 * H;
+    for (int k = lane; k < A; k += 64) dctx[(size_t)n * A + k] += d * w[k];
+    for (int k = lane; k < H; k += 64) {
+      dc[(size_t)n * H + k] = d * wc[k];
+      dh[(size_t)n * H + k] += d * wh[k];
+    }
+    for (int k = lane; k < E; k += 64) dx[(size_t)n * E + k] = d * wx[k];
+  }
+  if (lane == 0) red[wid] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(gb, (red[0] + red[1]) + (red[2] + red[3]));
+}
+
 // Backward of s-projection + LSTM cell for step t.  grid (H/16, ceil(B/16)).
 //   dc_t = ds . W_s[0:H]^T + dC_dir + dc_carry ;  dh_t = ds . W_s[H:2H]^T + dH_dir + dh_rec
 //   cell backward -> dz_t (bf16), dc_carry <- dc_total * f
@@ -307,6 +338,10 @@ void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const floa
   const int rows_per = (N + nsplit - 1) / nsplit;
   hipLaunchKernelGGL(pgen_bwd_kernel, dim3(cols, nsplit), dim3(256), 0, st, ctx, c, h, x, dpre, gw, N, A, H, E,
                      rows_per);
+}
+void launch_pgen_dirs(const float* dpre, const float* w, float* dctx, float* dc, float* dh, float* dx, float* gb,
+                      int N, int A, int H, int E, hipStream_t st) {
+  hipLaunchKernelGGL(pgen_dirs_kernel, dim3((N + 3) / 4), dim3(256), 0, st, dpre, w, dctx, dc, dh, dx, gb, N, A, H, E);
 }
 void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x, const float* w, const float* b,
                  float* pg, int R, int A, int H, int E, hipStream_t st) {

@@ -149,3 +149,7 @@ void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out,
 // weight repack as one launch over a job table (pack.hip)
 int pack_max_jobs();
 void launch_pack_cast(const long* jobs, int nj, long total, hipStream_t st);
+
+// p_gen gradient into the decoder inputs' direct terms + bias gradient (decoder.hip)
+void launch_pgen_dirs(const float* dpre, const float* w, float* dctx, float* dc, float* dh, float* dx, float* gb,
+                      int N, int A, int H, int E, hipStream_t st);

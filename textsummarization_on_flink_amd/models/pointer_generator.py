@@ -323,6 +323,10 @@ class HipPointerGenerator:
         w["DZ"] = z(D, B, 4 * H, dt=BF)
         w["DS"] = z(D, B, A)
         w["d_emb_dec"] = z(D * B, E)  # decoder-input embedding gradient rows
+        w["out_f32"] = z(D * B, H)  # output projection [h, ctx] . W_o + b (fp32, before the bf16 copy)
+        if self.hps.pointer_gen:  # p_gen direct terms of the decoder backward (pgen_dirs)
+            w["dC_dir"] = z(D, B, H)
+            w["dX_dir"] = z(D, B, E)
         w["DE"] = z(D, B, T)
         w["da"] = None if self.fused_attn_bwd else z(B, T)
         w["dcov"] = z(2, B, T)
@@ -575,8 +579,10 @@ class HipPointerGenerator:
         N = D * B
         Hn = w["Hb"][1:].reshape(N, H)
         ctxb = w["CTXb"].view(N, A)
-        out = mmf(Hn, self.pk["OUTm"][:H]) + mmf(ctxb, self.pk["OUTm"][H:]) + p[OUT_B]
-        self._out = out
+        # out = [h, ctx] . W_o + b: bias-epilogue GEMM, second GEMM accumulating (beta = 1)
+        out = w["out_f32"]
+        torch.addmm(p[OUT_B], Hn, self.pk["OUTm"][:H], out_dtype=F32, out=out)
+        torch.addmm(out, ctxb, self.pk["OUTm"][H:], out_dtype=F32, out=out)
         w["outb"].copy_(out)
         pg = None
         if hps.pointer_gen:
@@ -727,18 +733,15 @@ class HipPointerGenerator:
         dX_dir = None
         if hps.pointer_gen:
             dpre = w["dpre"].view(N)
-            pm = p[PG_M][:, 0]
+            pm = p[PG_M].view(-1)
             # one fused column-reduction kernel for the four p_gen weight slices (gw zeroed above)
             k.pgen_bwd(w["CTX"].view(N, A), w["Cst"][1:].reshape(N, H), Hn, w["X"].view(N, E), dpre,
                        g(PG_M).view(-1), N, A, H, E)
-            g(PG_B).copy_(dpre.sum().view(1))
-            dp = dpre.view(D, B, 1)
-            dCTX_dir.add_(dp * pm[:A])
-            dC_dir = (dp * pm[A:A + H]).contiguous()
-            dH_dir.add_(dp * pm[A + H:A + 2 * H])
-            dX_dir = (dp * pm[A + 2 * H:]).contiguous()
+            # direct terms dCTX/dH += dp w_ctx/h, dC/dX = dp w_c/x and the bias gradient, one launch
+            dC_dir, dX_dir = w["dC_dir"], w["dX_dir"]
+            k.pgen_dirs(dpre, pm, dCTX_dir, dC_dir, dH_dir, dX_dir, g(PG_B).view(1), N, A, H, E)
         if dX_dir is not None and D > 1:  # p_gen path into ctx_{t-1} through x_t (hoisted out of the loop)
-            dCTX_dir[:D - 1].view((D - 1) * B, A).add_(dX_dir[1:].view((D - 1) * B, E) @ p[LIN_M][E:].t())
+            dCTX_dir[:D - 1].view((D - 1) * B, A).addmm_(dX_dir[1:].view((D - 1) * B, E), p[LIN_M][E:].t())
         # ---- decoder reverse loop
         enc_out, lens, F, Et = self.enc[-1]["out"], w["enc_lens"], w["F"], w["Et"]
         v, wc = self.f32["v"], self.f32["wc"]
