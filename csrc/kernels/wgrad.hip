@@ -9,17 +9,18 @@
 // workgroup, so it can run on a side stream beside the encoder BPTT (pointer_generator.py,
 // TSAMD_DEFER_WGRAD).
 //
-// Tile 128 (m) x 128 (n) per workgroup, 4 waves of 64 x 64, k-steps of 32 staged through
+// Tile 128 (m) x 128 (n) per workgroup, 4 waves of 64 x 64, k-steps of 64 (TSAMD_WGRAD_BK=32: 32; 3-5% slower) staged through
 // double-buffered LDS as [k][m] / [k][n] rows (coalesced 16-byte global loads).  The MFMA wants
 // each lane's 8 consecutive k of one m (A) or one n (B): gfx950's ds_read_b64_tr_b16 reads a
 // 4-row x 16-column block and hands lane i of each 16-lane group column i of the 4 rows, so two
 // transposed reads per fragment turn the k-major image into MFMA operands without a transpose
 // pass.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
-constexpr int WBM = 128, WBN = 128, WBK = 32;
+constexpr int WBM = 128, WBN = 128;
 constexpr int WPAD = 16;  // bf16 per LDS row: 288-byte rows put rows r and r + 1 eight banks apart
 constexpr int WLD = WBM + WPAD;
 
@@ -28,7 +29,7 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 // lane l: rows 8 (l >> 4) + 4 half + ((l & 15) >> 2) and columns c0 + 4 (l & 3) of the image;
 // returns 4 bf16 of column c0 + (l & 15), rows 8 (l >> 4) + 4 half .. + 3
 __device__ __forceinline__ v4i16 tr_read(const bf16* img, int c0, int half, int lane) {
-  const int row = 8 * (lane >> 4) + 4 * half + ((lane & 15) >> 2);
+  const int row = 8 * (lane >> 4) + 4 * half + ((lane & 15) >> 2);  // within a 32-row k-slice
   const bf16* p = img + row * WLD + c0 + 4 * (lane & 3);
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(const_cast<bf16*>(p)));
 }
@@ -44,8 +45,10 @@ __device__ __forceinline__ bf16x8 frag(const bf16* img, int c0, int lane) {
 
 // grid (M / 128, N / 128, splits); M, N multiples of 128; any K (rows past the chunk end are
 // zero-filled); lda / ldb / ldo in elements
+template <int WBK>
 __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16* __restrict__ a, int lda, const bf16* __restrict__ b,
                                                        int ldb, float* __restrict__ out, int ldo, int K, int kchunk) {
+  constexpr int CPT = WBK * 16 / 256;  // 16-byte chunks per thread per operand and stage
   __shared__ __attribute__((aligned(16))) bf16 As[2][WBK * WLD];
   __shared__ __attribute__((aligned(16))) bf16 Bs[2][WBK * WLD];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
@@ -53,11 +56,11 @@ __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16* __restrict__ 
   const int k0 = blockIdx.z * kchunk, k1 = min(K, k0 + kchunk);
   if (k0 >= k1) return;
   const int wm = (wid & 1) * 64, wn = (wid >> 1) * 64;
-  // staging: 32 rows x 128 columns = 512 chunks of 16 B per operand, 2 per thread
-  bf16x8 ra[2], rb[2];
+  // staging: WBK rows x 128 columns = WBK * 16 chunks of 16 B per operand, CPT per thread
+  bf16x8 ra[CPT], rb[CPT];
   auto fetch = [&](int kb) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < CPT; ++u) {
       const int c = tid + 256 * u, r = c >> 4, col = (c & 15) * 8, k = kb + r;
       if (k < k1) {
         ra[u] = ld8(a + (size_t)k * lda + m0 + col);
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16* __restrict__ 
   };
   auto stash = [&](int buf) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < CPT; ++u) {
       const int c = tid + 256 * u, r = c >> 4, col = (c & 15) * 8;
       *reinterpret_cast<bf16x8*>(&As[buf][r * WLD + col]) = ra[u];
       *reinterpret_cast<bf16x8*>(&Bs[buf][r * WLD + col]) = rb[u];
@@ -88,15 +91,20 @@ __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16* __restrict__ 
   for (int kb = k0; kb < k1; kb += WBK) {
     const bool more = kb + WBK < k1;
     if (more) fetch(kb + WBK);  // in flight during this step's MFMAs
-    bf16x8 fa[4], fb[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = frag(As[buf], wm + 16 * i, lane);
+    for (int ks = 0; ks < WBK / 32; ++ks) {
+      const bf16* Ak = As[buf] + ks * 32 * WLD;
+      const bf16* Bk = Bs[buf] + ks * 32 * WLD;
+      bf16x8 fa[4], fb[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = frag(Bs[buf], wn + 16 * j, lane);
+      for (int i = 0; i < 4; ++i) fa[i] = frag(Ak, wm + 16 * i, lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) fb[j] = frag(Bk, wn + 16 * j, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
+    }
     if (more) stash(buf ^ 1);
     __syncthreads();
     buf ^= 1;
@@ -122,9 +130,14 @@ int wgrad_tn_splits(int M, int N, int K) {
 
 void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out, int ldo, int M, int N, int K,
                      hipStream_t st) {
+  static const int bk = getenv("TSAMD_WGRAD_BK") ? atoi(getenv("TSAMD_WGRAD_BK")) : 64;
+  const int WBK = bk == 32 ? 32 : 64;
   const int s = wgrad_tn_splits(M, N, K);
   const int kchunk = ((K + s - 1) / s + WBK - 1) / WBK * WBK;
   const int splits = (K + kchunk - 1) / kchunk;
-  hipLaunchKernelGGL(wgrad_tn_kernel, dim3(M / WBM, N / WBN, splits), dim3(256), 0, st, a, lda, b, ldb, out, ldo, K,
-                     kchunk);
+  const dim3 grid(M / WBM, N / WBN, splits);
+  if (WBK == 32)
+    hipLaunchKernelGGL(wgrad_tn_kernel<32>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, K, kchunk);
+  else
+    hipLaunchKernelGGL(wgrad_tn_kernel<64>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, K, kchunk);
 }
