@@ -64,3 +64,25 @@ def test_cast_colsum(N, C):
     torch.testing.assert_close(xb, x.to(torch.bfloat16), rtol=0, atol=0)
     ref = x.double().sum(0) + 0.5
     torch.testing.assert_close(cs.double(), ref, rtol=1e-5, atol=1e-4 * (N ** 0.5))
+
+
+@pytest.mark.parametrize("K,M,N,strided", [(1000, 128, 128, False), (25600, 256, 512, False), (3001, 128, 256, True),
+                                           (130, 512, 128, True)])
+def test_wgrad_tn_matches_fp32(K, M, N, strided):
+    """wgrad.hip: out[M][N] += a[K][M]^T b[K][N] (split-K MFMA, transposed LDS reads, fp32
+    atomics) vs an fp32 matmul, including K not a multiple of the k-step, row-strided operand
+    views and an output slice of a wider matrix."""
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    g = torch.Generator(device="cuda").manual_seed(K + M)
+    pad = 8 if strided else 0
+    a = (torch.randn(K, M + pad, device="cuda", generator=g) * 0.2).bfloat16()[:, :M]
+    b = (torch.randn(K, N + pad, device="cuda", generator=g) * 0.2).bfloat16()[:, :N]
+    big = torch.zeros(M, N + 2 * pad, device="cuda")
+    out = big[:, pad:pad + N] if strided else big[:, :N]
+    k.wgrad_tn(a, b, out)
+    ref = a.float().t() @ b.float()
+    err = float((out - ref).abs().max() / ref.abs().max())
+    assert err < 1e-4, err
+    if strided:  # nothing written outside the slice
+        assert float(big[:, :pad].abs().max()) == 0 and float(big[:, pad + N:].abs().max()) == 0
