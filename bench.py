@@ -243,11 +243,12 @@ def bench_decode(args, info, D, torch, dev_id):
     dec.decode(pool[0])  # warm-up: graph capture
 
     def loop():
+        # pipelined: batch i's host backtracking runs while batch i+1 is on the GPU; the loop
+        # ends when the last batch's results are on the host
         n = steps = 0
-        for i in range(args.decode_batches):
-            hyps = dec.decode(pool[1 + i % 2])  # synchronous: results() reads the device buffers
+        for hyps in dec.decode_batches([pool[1 + i % 2] for i in range(args.decode_batches)]):
             n += len(hyps)
-            steps += dec.steps_run
+            steps += dec.finished_steps
         return n, steps
 
     (n, steps), el = _timed(loop, info, D, torch)

@@ -229,6 +229,12 @@ class DeviceBeamDecoder:
     # ------------------------------------------------------------------ driver
     def run(self, batch) -> None:
         """Decode one engine batch (n_articles rows) fully on the device."""
+        for _ in self.run_chunks(batch):
+            pass
+
+    def run_chunks(self, batch):
+        """Generator form of ``run``: each iteration queues one early-exit chunk of decode steps
+        on the current stream and yields (``decode_batches`` does host work in between)."""
         if self.use_graph and self.graph is None:
             self._encode(batch)
             self._prologue()
@@ -259,6 +265,8 @@ class DeviceBeamDecoder:
             ev = torch.cuda.Event()
             ev.record()
             pend.append((ev, flag))
+            self.steps_run = t
+            yield
             if len(pend) == 2:
                 ev0, f0 = pend.pop(0)
                 ev0.synchronize()
@@ -281,14 +289,64 @@ class DeviceBeamDecoder:
         torch.cuda.current_stream().synchronize()
         return {k: self._pinned[k].numpy() for k in names}
 
+    def _result_names(self):
+        names = ["res_count", "res_score", "res_step", "res_par", "lp_sum", "tok_hist", "par_hist", "step"]
+        return names + (["ATT_hist", "PG_hist"] if self.keep_attn else [])
+
     def results(self, n_valid: int = None) -> List[Hypothesis]:
         """Best hypothesis per article (host).  The winner is picked from the device scores
         first and only the winners are backtracked, vectorised over articles (one numpy
         gather per step instead of a Python walk per candidate)."""
-        names = ["res_count", "res_score", "res_step", "res_par", "lp_sum", "tok_hist", "par_hist", "step"]
-        if self.keep_attn:
-            names += ["ATT_hist", "PG_hist"]
-        b = self._fetch(names)
+        return self._backtrack(self._fetch(self._result_names()), n_valid)
+
+    def _snapshot(self, slot: int):
+        """Queue device -> pinned copies of the result buffers into pinned set ``slot`` (0/1)
+        on the current stream and return (arrays, event): the next batch's prologue, queued
+        after these copies, may then reset the device buffers."""
+        if not hasattr(self, "_snap"):
+            self._snap = [{}, {}]
+        pin = self._snap[slot]
+        srcs = {k: self.b[k] for k in self._result_names()}
+        srcs["lstm_err"] = self.eng.w["lstm_err"]  # checked with the results, one batch late
+        for k, src in srcs.items():
+            h = pin.get(k)
+            if h is None or h.shape != src.shape or h.dtype != src.dtype:
+                h = pin[k] = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+            h.copy_(src, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return {k: v.numpy() for k, v in pin.items()}, ev
+
+    def decode_batches(self, batches):
+        """Decode a sequence of Batches, yielding each batch's hypotheses, with the host work
+        pipelined behind the GPU: a batch's result buffers are snapshotted into pinned memory
+        (double-buffered) before the next batch's prologue, and backtracked on the host while
+        the next batch's encoder and first decode chunk run.  Same results as ``decode`` per
+        batch; the last batch is finished after the loop."""
+        pending, slot = None, 0
+        for batch in batches:
+            if batch.enc_batch.shape[0] != self.Na:
+                raise ValueError(f"batch has {batch.enc_batch.shape[0]} rows, engine expects {self.Na}")
+            first = True
+            for _ in self.run_chunks(batch):
+                if first and pending is not None:  # the GPU has this batch's work queued
+                    yield self._finish(pending)
+                    pending = None
+                first = False
+            arrays, ev = self._snapshot(slot)
+            slot ^= 1
+            pending = (arrays, ev, int(batch.valid.sum()), self.steps_run)
+        if pending is not None:
+            yield self._finish(pending)
+
+    def _finish(self, pending) -> List[Hypothesis]:
+        arrays, ev, nv, self.finished_steps = pending
+        ev.synchronize()
+        if int(arrays["lstm_err"][0]):  # never emit garbage summaries (see check_lstm_err)
+            self.eng.check_lstm_err()
+        return self._backtrack(arrays, nv)
+
+    def _backtrack(self, b, n_valid: int = None) -> List[Hypothesis]:
         beam, start, stop = self.beam, self.vocab.word2id(START_DECODING), self.vocab.word2id(STOP_DECODING)
         nsteps = int(min(b["step"][0], self.maxD))
         na = n_valid if n_valid is not None else self.Na
