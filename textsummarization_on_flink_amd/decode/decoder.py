@@ -146,6 +146,11 @@ class BeamSearchDecoder:
     def decode(self, with_rouge: bool = True, max_examples: Optional[int] = None):
         t0 = time.time()
         self.counter = 0
+        if self.device_beam is not None and (self.hps.single_pass or self.reload_fn is None):
+            # pipelined device decode: batch i's summaries are written while batch i+1 runs on
+            # the GPU (no checkpoint reload can fall between them in this mode)
+            self._decode_pipelined(max_examples)
+            return self._finish_decode(with_rouge)
         while max_examples is None or self.counter < max_examples:
             if self.device_beam is not None:
                 batch = self.batcher.next_batch()  # n_articles distinct examples per batch
@@ -161,6 +166,27 @@ class BeamSearchDecoder:
             if not self.hps.single_pass and self.reload_fn and time.time() - t0 > SECS_UNTIL_NEW_CKPT:
                 self.reload_fn()
                 t0 = time.time()
+        return self._finish_decode(with_rouge)
+
+    def _decode_pipelined(self, max_examples: Optional[int]):
+        queued = []
+
+        def batches():
+            n = 0
+            while max_examples is None or n < max_examples:
+                batch = self.batcher.next_batch()  # n_articles distinct examples per batch
+                if batch is None:
+                    return
+                n += int(batch.valid.sum())
+                queued.append(batch)
+                yield batch
+
+        for hyps in self.device_beam.decode_batches(batches()):
+            batch = queued.pop(0)
+            for row, best in enumerate(hyps):
+                self.handle(best, batch, row)
+
+    def _finish_decode(self, with_rouge: bool):
         if self.hps.single_pass and with_rouge and isinstance(self.writer, NullWriter) and self.decode_dir:
             res = rouge.rouge_eval(self.rouge_ref_dir, self.rouge_dec_dir)
             log.info(rouge.rouge_log(res, self.decode_dir))
