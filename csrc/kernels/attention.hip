@@ -631,7 +631,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step_kernel(
 
 // Same math with 4 positions per group (NG4 groups per wave): the E/F rows in flight per
 // lane halve (32 instead of 64 VGPRs), which buys a third wave per SIMD at the 168-VGPR cap.
-template <int NG4, int OCC>
+// NK feature blocks of 512 per lane (NK = 2: A = 1024, config #5).
+template <int NG4, int OCC, int NK>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
     const bf16* __restrict__ E, const bf16* __restrict__ F, const float* __restrict__ s,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
@@ -643,7 +644,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
   constexpr int PB = 4 * PW;   // positions per block
   static_assert(PW == 32 || PW == 16 || PW == 64, "lane -> position map needs a power of two <= 64");
   __shared__ float red[8];
-  __shared__ float part[4][512];
+  __shared__ float part[4][512 * NK];
   const int b = blockIdx.y;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
@@ -662,24 +663,28 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
   const float g = gcl ? gcl[b] : 0.f;
   const bf16* Eb = E + (size_t)b * T * A;
   const bf16* Fb = F + (size_t)b * T * A;
-  const int k0c = min(lane * 8, A - 8);
+  int k0c[NK];
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) k0c[kb] = min(kb * 512 + lane * 8, A - 8);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 fr[4], er[4];
-#define LOAD4(dst, base, pg)                                                             \
-  {                                                                                      \
-    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                      \
-      const int pq = min((pg) + q, len - 1);                                             \
-      dst[q] = __builtin_bit_cast(u32x4, ld8(base + (size_t)pq * A + k0c));              \
-    }                                                                                    \
+  u32x4 fr[NK][4], er[NK][4];
+#define LOAD4(dst, base, pg)                                                               \
+  {                                                                                        \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                        \
+      const int pq = min((pg) + q, len - 1);                                               \
+      _Pragma("unroll") for (int kb = 0; kb < NK; ++kb) dst[kb][q] =                       \
+          __builtin_bit_cast(u32x4, ld8(base + (size_t)pq * A + k0c[kb]));                 \
+    }                                                                                      \
   }
   if (p0 < len) {
     LOAD4(er, Eb, p0);
     LOAD4(fr, Fb, p0);
   }
-  float dk[8];
-  f32x2 s2[4], w2[4], v4w[4], acc[4];
-  {
-    const int k0 = lane * 8;
+  float dk[NK][8];
+  f32x2 s2[NK][4], w2[NK][4], v4w[NK][4], acc[NK][4];
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) {
+    const int k0 = kb * 512 + lane * 8;
 #pragma unroll
     for (int jp = 0; jp < 4; ++jp) {
       float sv[2], wv[2], vv[2];
@@ -690,12 +695,12 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
         sv[h] = ok ? s[(size_t)b * A + k] : 0.f;
         vv[h] = ok ? v[k] : 0.f;
         wv[h] = (ok && wc) ? wc[k] : 0.f;
-        dk[2 * jp + h] = ok ? dctx[(size_t)b * A + k] : 0.f;
+        dk[kb][2 * jp + h] = ok ? dctx[(size_t)b * A + k] : 0.f;
       }
-      s2[jp] = f32x2{sv[0], sv[1]} * K2LOG2E;
-      w2[jp] = f32x2{wv[0], wv[1]} * K2LOG2E;
-      v4w[jp] = f32x2{4.f * vv[0] * wv[0], 4.f * vv[1] * wv[1]};
-      acc[jp] = f32x2{0.f, 0.f};
+      s2[kb][jp] = f32x2{sv[0], sv[1]} * K2LOG2E;
+      w2[kb][jp] = f32x2{wv[0], wv[1]} * K2LOG2E;
+      v4w[kb][jp] = f32x2{4.f * vv[0] * wv[0], 4.f * vv[1] * wv[1]};
+      acc[kb][jp] = f32x2{0.f, 0.f};
     }
   }
   float a_l = 0.f, r_l = 0.f, c_l = 0.f, dn_l = 0.f;
@@ -741,7 +746,10 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
     for (int q = 0; q < 4; ++q) {
       f32x2 d2 = f32x2{0.f, 0.f};
 #pragma unroll
-      for (int jp = 0; jp < 4; ++jp) d2 = fma2(bf2pair(er[q][jp]), f32x2{dk[2 * jp], dk[2 * jp + 1]}, d2);
+      for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp)
+          d2 = fma2(bf2pair(er[kb][q][jp]), f32x2{dk[kb][2 * jp], dk[kb][2 * jp + 1]}, d2);
       pd[q] = d2.x + d2.y;
     }
     if (more) LOAD4(er, Eb, pg + 4);
@@ -757,13 +765,15 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
       const float c = rdlane(c_l, grp * 4 + q);
       f32x2 dc2 = f32x2{0.f, 0.f};
 #pragma unroll
-      for (int jp = 0; jp < 4; ++jp) {
-        const f32x2 y = fma2(bf2pair(fr[q][jp]), splat2(K2LOG2E), fma2(w2[jp], splat2(c), s2[jp]));
-        const f32x2 r = rsig2(y);
-        const f32x2 qv = fma2(-r, r, r);
-        acc[jp] = fma2(qv, splat2(de), acc[jp]);
-        dc2 = fma2(qv, v4w[jp], dc2);
-      }
+      for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          const f32x2 y = fma2(bf2pair(fr[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          const f32x2 r = rsig2(y);
+          const f32x2 qv = fma2(-r, r, r);
+          acc[kb][jp] = fma2(qv, splat2(de), acc[kb][jp]);
+          dc2 = fma2(qv, v4w[kb][jp], dc2);
+        }
       dcv[q] = dc2.x + dc2.y;
     }
     if (more) LOAD4(fr, Fb, pg + 4);
@@ -785,12 +795,13 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
     }
   }
 #undef LOAD4
-  {
-    const int k0 = lane * 8;
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) {
+    const int k0 = kb * 512 + lane * 8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const bool ok = k0 + j < A;
-      part[wid][lane * 8 + j] = ok ? 4.f * v[ok ? k0 + j : 0] * acc[j >> 1][j & 1] : 0.f;
+      part[wid][kb * 512 + lane * 8 + j] = ok ? 4.f * v[ok ? k0 + j : 0] * acc[kb][j >> 1][j & 1] : 0.f;
     }
   }
   __syncthreads();
@@ -987,15 +998,34 @@ void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const fl
   // 61 us for the 8-position kernel at B = 256, T = 400 (tools/attn_micro.py).  TSAMD_ATTN_P4=0
   // selects the 8-position kernel; 1 / 3 the 4-position one uncapped / at 3 waves per SIMD.
   static const int p4 = [] { const char* e = getenv("TSAMD_ATTN_P4"); return e ? atoi(e) : 2; }();
+  // A = 1024 (config #5): 4-position groups with 16 features per lane at 208 VGPRs (2 waves per
+  // SIMD; the 8-position kernel below needs 316 registers, 1 wave), 64 positions per wave = 256
+  // per block so each row's S prologue is paid by 4 blocks, not 7: 198 us vs 250 us per launch
+  // at 256 rows x T = 800 (tools/attn_bwd_a1024_micro.py; 32 positions per wave: 217 us).
+  // TSAMD_ATTN_P4K2 = 0 selects the 8-position kernel; 1 / 2 / 3 / 4 the 32-position-per-wave
+  // kernel uncapped / OCC 2 / OCC 3 / 16 positions per wave (A/B runs).
+  static const int p4k2 = [] { const char* e = getenv("TSAMD_ATTN_P4K2"); return e ? atoi(e) : 5; }();
+#define L4(OC, NK) hipLaunchKernelGGL((attn_bwd_step4_kernel<8, OC, NK>), dim3((T + 127) / 128, B), dim3(256), 0, st, E, \
+                                      F, s, v, wc, cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A)
   if (A <= 512 && p4 > 0) {
-#define L4(OC) hipLaunchKernelGGL((attn_bwd_step4_kernel<8, OC>), dim3((T + 127) / 128, B), dim3(256), 0, st, E, F, s, v, \
-                                  wc, cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A)
-    if (p4 == 3) L4(3);
-    else if (p4 == 2) L4(2);
-    else L4(1);
-#undef L4
+    if (p4 == 3) L4(3, 1);
+    else if (p4 == 2) L4(2, 1);
+    else L4(1, 1);
     return;
   }
+  if (A > 512 && A <= 1024 && p4k2 > 0) {
+    if (p4k2 == 4) {
+      hipLaunchKernelGGL((attn_bwd_step4_kernel<4, 2, 2>), dim3((T + 63) / 64, B), dim3(256), 0, st, E, F, s, v, wc, cov,
+                         a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A);
+    } else if (p4k2 == 5) {
+      hipLaunchKernelGGL((attn_bwd_step4_kernel<16, 2, 2>), dim3((T + 255) / 256, B), dim3(256), 0, st, E, F, s, v, wc,
+                         cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A);
+    } else if (p4k2 == 3) L4(3, 2);
+    else if (p4k2 == 2) L4(2, 2);
+    else L4(1, 2);
+    return;
+  }
+#undef L4
   if (A <= 512) {
     if (ng == 2) LB(1, 2, 1);
     else if (occ == 3) LB(1, 4, 3);

@@ -1,0 +1,59 @@
+"""attn_bwd_step (one launch per decoder step: da, de, ds, dcov) against a plain PyTorch fp32
+reference of the same math, at A = 512 (bench, 4-position kernel) and A = 1024 (config #5,
+16 features per lane, 256 positions per block).  T = 300 leaves partial blocks; lens of 1, a
+few, and T leave fully masked blocks and masked tail groups.
+
+Reference semantics (attention_decoder.py:79-129, model.py:463-480 of the reference): scores
+e_i = v . tanh(F_i + s + w_c cov_i), a = masked softmax(e), ctx = sum_i a_i E_i, coverage loss
+sum_i min(a_i, cov_i), cov_{t+1} = cov_t + a_t.
+"""
+import pytest
+import torch
+
+from textsummarization_on_flink_amd.ops import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _reference(E, F, s, v, wc, cov, a, dctx, Ga, dnext, g, lens):
+    B, T, A = E.shape
+    mask = torch.arange(T, device=E.device)[None, :] < lens[:, None].long()
+    u = F.float() + s[:, None, :] + wc[None, None, :] * cov[:, :, None]
+    sech2 = 1 - torch.tanh(u) ** 2
+    r = Ga + dnext + g[:, None] * (a <= cov).float()
+    da = r + torch.einsum("bta,ba->bt", E.float(), dctx)
+    da = torch.where(mask, da, torch.zeros_like(da))
+    S = (a * da).sum(1, keepdim=True)
+    de = torch.where(mask, a * (da - S), torch.zeros_like(da))
+    ds = torch.einsum("bt,bta->ba", de, sech2) * v[None, :]
+    hc = torch.einsum("bta,a->bt", sech2, v * wc)
+    dcov = dnext + torch.where(mask, g[:, None] * (a > cov).float() + de * hc, torch.zeros_like(de))
+    return de, ds, dcov
+
+
+@pytest.mark.parametrize("A", [512, 1024])
+def test_attn_bwd_step_matches_fp32(A):
+    k = ops()
+    B, T = 6, 300
+    gen = torch.Generator(device="cuda").manual_seed(A)
+    dev = "cuda"
+
+    def r(*shape, s=1.0):
+        return torch.randn(*shape, generator=gen, device=dev) * s
+
+    lens = torch.tensor([T, 1, 5, 129, 257, 300], dtype=torch.int32, device=dev)
+    mask = torch.arange(T, device=dev)[None, :] < lens[:, None].long()
+    E, F = r(B, T, A, s=0.5).bfloat16(), r(B, T, A, s=0.5).bfloat16()
+    s, v, wc = r(B, A, s=0.3), r(A, s=0.1), r(A, s=0.1)
+    cov = torch.rand(B, T, generator=gen, device=dev) * mask
+    a = torch.softmax(r(B, T).masked_fill(~mask, float("-inf")), -1)
+    ctx = torch.einsum("bt,bta->ba", a, E.float())
+    dctx, Ga, dnext = r(B, A, s=0.1), r(B, T, s=0.1), r(B, T, s=0.1)
+    g = torch.full((B,), 0.7, device=dev)
+    de, ds, dcov = torch.zeros(B, T, device=dev), torch.zeros(B, A, device=dev), torch.zeros(B, T, device=dev)
+    k.attn_bwd_step(E, F, s, v, wc, cov, a, dctx, ctx, Ga, dnext, g, lens, de, ds, dcov, B, T, A)
+    torch.cuda.synchronize()
+    want = _reference(E, F, s, v, wc, cov, a, dctx, Ga, dnext, g, lens)
+    for name, got, ref in zip(("de", "ds", "dcov"), (de, ds, dcov), want):
+        err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        assert err < 2e-3, (name, err)
