@@ -26,6 +26,7 @@
 //   ds_k = sum_i de_i v_k sech2(u_ik), dcov_i = dcov_next_i + g [a_i > cov_i] +
 //   de_i sum_k v_k w_k sech2(u_ik)  (S = sum_j a_j r_j + dctx . ctx, see attention.hip).
 #include "attn_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -62,12 +63,15 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     const bf16* __restrict__ F, const bf16* __restrict__ E, const float* __restrict__ s,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
     const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
-    float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T, int rep) {
+    float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T, int rep, int xper) {
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float es[kRowMaxT];
   __shared__ float part[NW][A];
   __shared__ float wm[NW], wl[NW], red[NW];
-  const int b = blockIdx.x;
+  // xper > 0 (beam decode): workgroups are dispatched to the 8 XCDs round-robin, so workgroup
+  // i runs on XCD i % 8; give XCD x the xper consecutive rows x * xper .. -- whole articles --
+  // so the rep hypotheses of an article read its F / E rows through ONE XCD's L2
+  const int b = xper ? (int)(blockIdx.x & 7) * xper + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   const int fr = b / rep;  // feature row: beam decode shares one encoder row between rep hypotheses
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = (int)DCHECK_IDX(lens[fr], 1, T + 1, CHK_ATTN_LEN);
@@ -352,9 +356,12 @@ bool attn_row_supported(int A, int T) { return (A == 512 || A == 1024) && T >= 1
 void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
                          const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
                          bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st) {
+  // TSAMD_ATTN_XCD=0 keeps the identity workgroup -> row map for beam decode (A/B runs)
+  static const bool xcd = [] { const char* e = getenv("TSAMD_ATTN_XCD"); return !(e && atoi(e) == 0); }();
+  const int xper = (xcd && rep > 1 && B % 8 == 0 && (B / 8) % rep == 0) ? B / 8 : 0;
 #define LF(NK)                                                                                                 \
   hipLaunchKernelGGL((attn_fwd_row_kernel<NK, row_waves<NK, false>()>), dim3(B), dim3(row_waves<NK, false>() * 64), \
-                     0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep)
+                     0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep, xper)
   if (A == 512) LF(1);
   else LF(2);
 #undef LF

@@ -57,3 +57,38 @@ def test_attn_bwd_step_matches_fp32(A):
     for name, got, ref in zip(("de", "ds", "dcov"), (de, ds, dcov), want):
         err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         assert err < 2e-3, (name, err)
+
+
+@pytest.mark.parametrize("A,Na,rep", [(512, 16, 4), (512, 6, 4), (1024, 8, 4), (512, 64, 1)])
+def test_attn_fwd_row_matches_fp32(A, Na, rep):
+    """attn_fwd_row: scores, masked softmax, context, coverage update and coverage loss against
+    fp32, with rep hypothesis rows per encoder row (beam decode).  Na * rep = 64 and 32 rows take
+    the XCD-grouped workgroup -> row map (rows of one article on one XCD), 24 the identity map."""
+    k = ops()
+    T, B = 300, Na * rep
+    gen = torch.Generator(device="cuda").manual_seed(A + Na)
+    dev = "cuda"
+
+    def r(*shape, s=1.0):
+        return torch.randn(*shape, generator=gen, device=dev) * s
+
+    lens = torch.randint(1, T + 1, (Na,), generator=gen, device=dev, dtype=torch.int32)
+    lens[0] = T
+    E, F = r(Na, T, A, s=0.5).bfloat16(), r(Na, T, A, s=0.5).bfloat16()
+    s, v, wc = r(B, A, s=0.3), r(A, s=0.1), r(A, s=0.5)
+    rl = lens.long().repeat_interleave(rep)
+    mask = torch.arange(T, device=dev)[None, :] < rl[:, None]
+    cov = torch.rand(B, T, generator=gen, device=dev) * mask
+    a, cov_out, cl = torch.zeros(B, T, device=dev), torch.zeros(B, T, device=dev), torch.zeros(B, device=dev)
+    ctx, ctx_bf = torch.zeros(B, A, device=dev), torch.zeros(B, A, device=dev, dtype=torch.bfloat16)
+    k.attn_fwd_row(F, E, s, v, wc, cov, lens, a, cov_out, cl, ctx, ctx_bf, B, T, A, rep)
+    torch.cuda.synchronize()
+    Fr, Er = F.float().repeat_interleave(rep, 0), E.float().repeat_interleave(rep, 0)
+    e = torch.einsum("bta,a->bt", torch.tanh(Fr + s[:, None, :] + wc[None, None, :] * cov[:, :, None]), v)
+    a_ref = torch.softmax(e.masked_fill(~mask, float("-inf")), -1)
+    ctx_ref = torch.einsum("bt,bta->ba", a_ref, Er)
+    checks = (("a", a, a_ref), ("ctx", ctx, ctx_ref), ("cov_out", cov_out, cov + a_ref),
+              ("covloss", cl, torch.minimum(a_ref, cov).sum(1)), ("ctx_bf", ctx_bf.float(), ctx_ref))
+    for name, got, ref in checks:
+        err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        assert err < (1e-2 if name == "ctx_bf" else 2e-3), (name, err)
