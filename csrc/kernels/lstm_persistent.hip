@@ -74,6 +74,28 @@ __device__ __forceinline__ void sweep(const gu64* g, int first, unsigned tag, un
   }
 }
 
+// Streaming activation traffic (gx / dout / acts / cs reads, acts / out / cs / hs / dz writes:
+// ~10 MB per step at H = 512, B = 256, each byte touched once per launch).  nt = 1 issues it
+// non-temporal so it does not evict the hand-off granules and W-side lines from L2 (the
+// per-step hand-off latency grows from 4.2 us with 2 teams to 7.1 us with 32 at H = 512).
+__device__ __forceinline__ void st_f4(float* p, float a, float b, float c, float d, bool nt) {
+  if (nt) __builtin_nontemporal_store(f32x4{a, b, c, d}, reinterpret_cast<f32x4*>(p));
+  else *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void st_f(float* p, float v, bool nt) {
+  if (nt) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ void st_b(bf16* p, bf16 v, bool nt) {
+  if (nt) __builtin_nontemporal_store(__builtin_bit_cast(unsigned short, v), reinterpret_cast<unsigned short*>(p));
+  else *p = v;
+}
+__device__ __forceinline__ f32x4 ld_f4(const float* p, bool nt) {
+  if (nt) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return *reinterpret_cast<const f32x4*>(p);
+}
+__device__ __forceinline__ float ld_f(const float* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
+
 // LDS tile [16 rows][RS] bf16 with the 16-byte chunk index XOR-swizzled by row (no padding:
 // the backward tile is exactly 2 x 32 KB at H = 256).
 template <int RS>
@@ -91,7 +113,7 @@ __device__ __forceinline__ bool team_of(int NC, int nteams, int& team, int& c) {
 
 }  // namespace
 
-template <int H>
+template <int H, bool NT>
 __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     const float* __restrict__ gx, const float* __restrict__ bias, const bf16* __restrict__ Wt,
     bf16* __restrict__ hs, float* __restrict__ cs, float* __restrict__ acts, bf16* __restrict__ out,
@@ -136,8 +158,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     const float* gxs = gx + ((size_t)d * T + st) * B * G4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float4 q = *reinterpret_cast<const float4*>(gxs + ((size_t)rc[i] * H + u) * 4);
-      gzn[i][0] = q.x; gzn[i][1] = q.y; gzn[i][2] = q.z; gzn[i][3] = q.w;
+      const f32x4 q = ld_f4(gxs + ((size_t)rc[i] * H + u) * 4, NT);
+      gzn[i][0] = q[0]; gzn[i][1] = q[1]; gzn[i][2] = q[2]; gzn[i][3] = q[3];
     }
   };
   load_gz(0);
@@ -209,14 +231,14 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     for (int i = 0; i < 4; ++i) {
       const int r = rc[i];
       if (s < ln[i]) {
-        *reinterpret_cast<float4*>(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4) =
-            make_float4(ga[i][0], ga[i][1], ga[i][2], ga[i][3]);  // one 16-byte store per (row, unit)
+        st_f4(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4, ga[i][0], ga[i][1], ga[i][2], ga[i][3],
+              NT);  // one 16-byte store per (row, unit)
         const int t = d == 0 ? s : ln[i] - 1 - s;
-        out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(hreg[i]);
+        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(hreg[i]), NT);
       }
       if (rok[i]) {
-        cnext[(size_t)r * H + u] = creg[i];
-        hnext[(size_t)r * H + u] = f2bf(hreg[i]);
+        st_f(cnext + (size_t)r * H + u, creg[i], NT);
+        st_b(hnext + (size_t)r * H + u, f2bf(hreg[i]), NT);
       }
     }
   }
@@ -230,7 +252,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 // j, o of the same unit for the same 4 rows; four row_ror:8 DPP moves swap half of them, and
 // each lane then updates the cell for 2 of the 4 rows (lanes n < 8: rows 0-1, n >= 8: 2-3).
 // Hand-off, layouts and tags are the 4-wave kernel's.
-template <int H>
+template <int H, bool NT>
 __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
     const float* __restrict__ gx, const float* __restrict__ bias, const bf16* __restrict__ Wt,
     bf16* __restrict__ hs, float* __restrict__ cs, float* __restrict__ acts, bf16* __restrict__ out,
@@ -277,8 +299,8 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
     const float* gxs = gx + ((size_t)d * T + st) * B * G4;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const float4 q = *reinterpret_cast<const float4*>(gxs + ((size_t)rc[i] * H + u) * 4);
-      gzn[i][0] = q.x; gzn[i][1] = q.y; gzn[i][2] = q.z; gzn[i][3] = q.w;
+      const f32x4 q = ld_f4(gxs + ((size_t)rc[i] * H + u) * 4, NT);
+      gzn[i][0] = q[0]; gzn[i][1] = q[1]; gzn[i][2] = q[2]; gzn[i][3] = q[3];
     }
   };
   // Step outputs (gates, h, c) are stored one step late: issued right after the next step's
@@ -294,14 +316,13 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
     for (int i = 0; i < 2; ++i) {
       const int r = rc[i];
       if (ss < ln[i]) {
-        *reinterpret_cast<float4*>(acts + ((((size_t)d * T + ss) * B + r) * H + u) * 4) =
-            make_float4(ga[i][0], ga[i][1], ga[i][2], ga[i][3]);
+        st_f4(acts + ((((size_t)d * T + ss) * B + r) * H + u) * 4, ga[i][0], ga[i][1], ga[i][2], ga[i][3], NT);
         const int t = d == 0 ? ss : ln[i] - 1 - ss;
-        out[((size_t)r * T + t) * 2 * H + d * H + u] = f2bf(hreg[i]);
+        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(hreg[i]), NT);
       }
       if (rok[i]) {
-        cnext[(size_t)r * H + u] = creg[i];
-        hnext[(size_t)r * H + u] = f2bf(hreg[i]);
+        st_f(cnext + (size_t)r * H + u, creg[i], NT);
+        st_b(hnext + (size_t)r * H + u, f2bf(hreg[i]), NT);
       }
     }
   };
@@ -381,7 +402,7 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
 // (its own partial stays in LDS): per step a lane reads 4 x (NC-1) granules instead of 32.
 // NW = 4 or 8 waves: the cell update covers the tile's 16 rows x 64 units with RPL = 16 / NW
 // rows per lane (4 or 2); waves < NC run the partial GEMM (at H = 512, NC = 8: all 8 waves).
-template <int H, int NW>
+template <int H, int NW, bool NT>
 __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
@@ -442,10 +463,17 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
 #pragma unroll
     for (int i = 0; i < RPL; ++i) {
       const size_t ri = (size_t)rc[i] * H + u;
-      dho[i] = dout[((size_t)d * T + s) * BH + ri];
-      const float4 q = *reinterpret_cast<const float4*>(acts + ((((size_t)d * T + s) * B + rc[i]) * H + u) * 4);
-      a4[i][0] = q.x; a4[i][1] = q.y; a4[i][2] = q.z; a4[i][3] = q.w;
-      cpv[i] = cs[((size_t)d * (T + 1) + s) * BH + ri];
+      if constexpr (NT) {
+        dho[i] = ld_f(dout + ((size_t)d * T + s) * BH + ri, true);
+        const f32x4 q = ld_f4(acts + ((((size_t)d * T + s) * B + rc[i]) * H + u) * 4, true);
+        a4[i][0] = q[0]; a4[i][1] = q[1]; a4[i][2] = q[2]; a4[i][3] = q[3];
+        cpv[i] = ld_f(cs + ((size_t)d * (T + 1) + s) * BH + ri, true);
+      } else {
+        dho[i] = dout[((size_t)d * T + s) * BH + ri];
+        const float4 q = *reinterpret_cast<const float4*>(acts + ((((size_t)d * T + s) * B + rc[i]) * H + u) * 4);
+        a4[i][0] = q.x; a4[i][1] = q.y; a4[i][2] = q.z; a4[i][3] = q.w;
+        cpv[i] = cs[((size_t)d * (T + 1) + s) * BH + ri];
+      }
     }
     // ---- recurrent dh for this lane's rows: own partial (LDS) + the peers' (granules)
     float rec[RPL];
@@ -529,7 +557,10 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
         if (rok[i]) {
           bf16* dzr = dz + (((size_t)d * T + s) * B + rc[i]) * G4;
 #pragma unroll
-          for (int g = 0; g < 4; ++g) dzr[g * H + u] = Ash[swz<256>(row0 + i, g * 64 + ul)];
+          for (int g = 0; g < 4; ++g) {
+            if constexpr (NT) st_b(dzr + g * H + u, Ash[swz<256>(row0 + i, g * 64 + ul)], true);
+            else dzr[g * H + u] = Ash[swz<256>(row0 + i, g * 64 + ul)];
+          }
         }
     };
     if (s == 0) {
@@ -592,6 +623,15 @@ static int lstm_nw(int H, bool bwd) {
   return bwd ? 8 : 4;
 }
 
+// Non-temporal activation traffic: forward yes (H = 512, B = 256: 7.06 -> 6.83 us per step;
+// H = 256: 3.14 -> 3.00), BPTT no (8.22 -> 8.41: its NT variant spills 20 bytes).
+// TSAMD_LSTM_NT = 0 / 1 / 2: none / both / forward only (default; read per call, A/B runs).
+static int lstm_nt(bool bwd) {
+  const char* e = getenv("TSAMD_LSTM_NT");
+  const int v = e ? atoi(e) : 2;
+  return v == 1 || (v == 2 && !bwd) ? 1 : 0;
+}
+
 static bool lstm_h_ok(int H) { return H == 64 || H == 128 || H == 256 || H == 512; }
 
 // Workgroups of the persistent kernels the current device keeps resident at once: one per
@@ -609,12 +649,12 @@ int lstm_persistent_capacity(int H) {
   bool ok = true;
 #define OCC(HH)                                                                                                    \
   if (H == HH) {                                                                                                   \
-    ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[0], lstm_bwd_persistent_kernel<HH, 8>, 512, 0) == hipSuccess; \
-    ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[1], lstm_fwd_persistent8_kernel<HH>, 512, 0) == hipSuccess; \
+    ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[0], lstm_bwd_persistent_kernel<HH, 8, false>, 512, 0) == hipSuccess; \
+    ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[1], lstm_fwd_persistent8_kernel<HH, false>, 512, 0) == hipSuccess; \
     if (HH <= 256) {                                                                                               \
-      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[2], lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4>, \
+      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[2], lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4, false>, \
                                                          256, 0) == hipSuccess;                                    \
-      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[3], lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256)>, \
+      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[3], lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), false>, \
                                                          256, 0) == hipSuccess;                                    \
     }                                                                                                              \
   }
@@ -656,22 +696,30 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
                                 int H, hipStream_t st) {
   const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H, false);
+  const int nt = lstm_nt(false);
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
   for (int t0 = 0; t0 < ntile; t0 += nl) {
     const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
-#define LAUNCH_F(HH)                                                                                            \
+#define LAUNCH_F(HH, NTV)                                                                                            \
   if (nw == 8)                                                                                                  \
-    hipLaunchKernelGGL(lstm_fwd_persistent8_kernel<HH>, dim3(grid), dim3(512), 0, st, gx, bias, Wt, hs, cs, acts, \
-                       out, lens, xb, e, T, B, ntile, t0, n);                                                   \
+    hipLaunchKernelGGL((lstm_fwd_persistent8_kernel<HH, NTV>), dim3(grid), dim3(512), 0, st, gx, bias, Wt, hs, cs, \
+                       acts, out, lens, xb, e, T, B, ntile, t0, n);                                             \
   else                                                                                                          \
-    hipLaunchKernelGGL(lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256)>, dim3(grid), dim3(256), 0, st, gx,    \
-                       bias, Wt, hs, cs, acts, out, lens, xb, e, T, B, ntile, t0, n)
-    if (H == 64) LAUNCH_F(64);
-    else if (H == 128) LAUNCH_F(128);
-    else if (H == 256) LAUNCH_F(256);
-    else LAUNCH_F(512);
+    hipLaunchKernelGGL((lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), NTV>), dim3(grid), dim3(256), 0, st, \
+                       gx, bias, Wt, hs, cs, acts, out, lens, xb, e, T, B, ntile, t0, n)
+    if (nt) {
+      if (H == 64) LAUNCH_F(64, true);
+      else if (H == 128) LAUNCH_F(128, true);
+      else if (H == 256) LAUNCH_F(256, true);
+      else LAUNCH_F(512, true);
+    } else {
+      if (H == 64) LAUNCH_F(64, false);
+      else if (H == 128) LAUNCH_F(128, false);
+      else if (H == 256) LAUNCH_F(256, false);
+      else LAUNCH_F(512, false);
+    }
 #undef LAUNCH_F
   }
 }
@@ -680,22 +728,30 @@ void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, con
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, float* dbias, int T, int B, int H, hipStream_t st) {
   const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H, true);
+  const int nt = lstm_nt(true);
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
   for (int t0 = 0; t0 < ntile; t0 += nl) {
     const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
-#define LAUNCH_B(HH)                                                                                                 \
+#define LAUNCH_B(HH, NTV)                                                                                                 \
   if (nw == 8)                                                                                                       \
-    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin,      \
+    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin, \
                        dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n);                                  \
   else                                                                                                               \
-    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4>), dim3(grid), dim3(256), 0, st, dz, Wn, \
-                       dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
-    if (H == 64) LAUNCH_B(64);
-    else if (H == 128) LAUNCH_B(128);
-    else if (H == 256) LAUNCH_B(256);
-    else LAUNCH_B(512);
+    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4, NTV>), dim3(grid), dim3(256), 0, st, dz, \
+                       Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+    if (nt) {
+      if (H == 64) LAUNCH_B(64, true);
+      else if (H == 128) LAUNCH_B(128, true);
+      else if (H == 256) LAUNCH_B(256, true);
+      else LAUNCH_B(512, true);
+    } else {
+      if (H == 64) LAUNCH_B(64, false);
+      else if (H == 128) LAUNCH_B(128, false);
+      else if (H == 256) LAUNCH_B(256, false);
+      else LAUNCH_B(512, false);
+    }
 #undef LAUNCH_B
   }
 }
