@@ -65,12 +65,17 @@ __device__ __forceinline__ void sweep(const gu64* g, int first, unsigned tag, un
         ready |= 1u << j;
       }
     if (__all(ready == all) || dead) return;
-    if (++spins > kSpinLimit) {
+    if (++spins > kSpinLimit / 4) {  // the longer sleep below: about the same wall-time bound
       if (lane == 0) __hip_atomic_store(err, code, RLX_AGENT);
       dead = true;
       return;
     }
-    __builtin_amdgcn_s_sleep(1);
+    // s_sleep(24) (~1500 clocks) between passes: the polls of 32 teams are a large share of
+    // the L2 traffic, and fewer of them lower every team's hand-off latency (tools/lstm_micro.py,
+    // per step: H = 512, B = 256: 6.82 us with s_sleep(1), 6.65 with 8, 6.28 with 24, 6.27 with
+    // 48; H = 256, B = 256: 3.01 / 2.97 / 2.97 / 3.46).  Spinning on one granule per lane first
+    // and sweeping once it is ready costs one more L2 round trip: 6.8 -> 8.3 us.
+    __builtin_amdgcn_s_sleep(24);
   }
 }
 
@@ -509,12 +514,15 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
                 if (p0 + q != c && !((ready >> bit) & 1) && (unsigned)(x[q][i] >> 32) == tag) ready |= 1u << bit;
               }
             if (__all((ready & need) == need) || dead) break;
-            if (++spins > kSpinLimit) {
+            if (++spins > kSpinLimit / 4) {
               if (lane == 0) __hip_atomic_store(err, 2u, RLX_AGENT);
               dead = true;
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            // see sweep(): BPTT per step at H = 512, B = 256: 8.22 us with s_sleep(1), 8.09
+            // with 8, 8.14 with 24, 8.13 with 48, 7.52 with 96; H = 256, B = 256: 4.04 / 3.83 /
+            // 3.63 / 3.64 / 4.94; B = 512: 5.52 / 5.26 / 4.90 / 4.57 / 5.38
+            __builtin_amdgcn_s_sleep(H >= 512 ? 96 : 48);
           }
 #pragma unroll
           for (int q = 0; q < PC; ++q)
