@@ -146,9 +146,11 @@ class BeamSearchDecoder:
     def decode(self, with_rouge: bool = True, max_examples: Optional[int] = None):
         t0 = time.time()
         self.counter = 0
-        if self.device_beam is not None and (self.hps.single_pass or self.reload_fn is None):
+        if self.device_beam is not None and self.hps.single_pass and isinstance(self.writer, NullWriter):
             # pipelined device decode: batch i's summaries are written while batch i+1 runs on
-            # the GPU (no checkpoint reload can fall between them in this mode)
+            # the GPU.  Offline single pass only: no checkpoint reload falls between batches,
+            # and batch i's results wait for batch i+1 to be fetched -- a streaming source
+            # (flink writer) must emit each batch as soon as it is decoded (Issue-6 analogue)
             self._decode_pipelined(max_examples)
             return self._finish_decode(with_rouge)
         while max_examples is None or self.counter < max_examples:
