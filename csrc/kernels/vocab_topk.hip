@@ -99,10 +99,12 @@ __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[4][4], int jr, co
   }
 }
 
-// 35 KB of LDS, 2 workgroups per CU (<= 256 VGPRs): all 32 W^T fragments of a wave in flight at
-// once, two rounds of workgroups at R = 256, V = 50k (784 tiles).  (A 4-per-CU variant, 128
+// 35 KB (RH = 1) / 70 KB (RH = 2) of LDS, 2 workgroups per CU (<= 256 VGPRs): all 32 W^T fragments
+// of a wave in flight at once.  (A 4-per-CU variant, 128
 // VGPRs, measured the same before this layout and spills with it.)
-template <int OCC>
+// RH = 2: 128 rows per workgroup, the W^T fragments reused for two 64-row halves (half the
+// workgroups and W^T fetches: 392 tiles at R = 256 = one round), X tile 68 KB of LDS.
+template <int OCC, int RH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void vocab_logits_kernel(
     const bf16* __restrict__ X,     // [R][H]  output-projection activations (bf16)
     const bf16* __restrict__ WT,    // [V][H]  output_projection/w transposed ("Bt")
@@ -110,25 +112,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     float* __restrict__ logits,     // [R][V]  fp32 (bias added)
     float* __restrict__ part_ms,    // [R][nt][2]  per tile (max, sum exp)
     int R, int V, int H) {
-  __shared__ float Pm[4][VT_ROWS], Ps[4][VT_ROWS];
-  __shared__ __attribute__((aligned(16))) bf16 Xs[VT_ROWS * (VT_HMAX + 8)];  // X tile of the block
+  constexpr int BR = VT_ROWS * RH;  // rows per block
+  __shared__ float Pm[4][BR], Ps[4][BR];
+  __shared__ __attribute__((aligned(16))) bf16 Xs[BR * (VT_HMAX + 8)];  // X tile of the block
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // XCD-aware order: the RB row blocks of one vocab tile get block ids equal mod 8 (one XCD
   // under round-robin dealing), so the tile's W^T columns come from HBM once and are then
   // served from that XCD's L2 to the other row blocks
-  const int RB = (R + VT_ROWS - 1) / VT_ROWS, nt = (V + VT_COLS - 1) / VT_COLS;
+  const int RB = (R + BR - 1) / BR, nt = (V + VT_COLS - 1) / VT_COLS;
   const int slot = blockIdx.x >> 3, vt = (slot / RB) * 8 + (blockIdx.x & 7);
   if (vt >= nt) return;
-  const int rb = (slot % RB) * VT_ROWS;
+  const int rb = (slot % RB) * BR;
   const int cw = vt * VT_COLS + 64 * wid;  // this wave's first column
   // X rows of this block -> LDS once (shared by the 4 waves)
   const int kof = 8 * (lane >> 4), c16 = lane & 15, q4 = 4 * (lane >> 4);
-  constexpr int XPT = VT_ROWS * VT_HMAX / 8 / 256;  // 16-byte X chunks per thread (H <= 256)
+  constexpr int XPT = BR * VT_HMAX / 8 / 256;  // 16-byte X chunks per thread (H <= 256)
   bf16x8 xr[XPT];
 #pragma unroll
   for (int u = 0; u < XPT; ++u) {
     const int c = threadIdx.x + 256 * u, rr = c / (H / 8), k8 = (c % (H / 8)) * 8;
-    if (c < VT_ROWS * (H / 8)) xr[u] = ld8(X + (size_t)min(rb + rr, R - 1) * H + k8);
+    if (c < BR * (H / 8)) xr[u] = ld8(X + (size_t)min(rb + rr, R - 1) * H + k8);
   }
   // every A fragment of the wave (W^T rows = its 4 x 16 vocab columns, H/32 k-steps, H <= 256:
   // 128 VGPRs) is issued right behind the X loads, before their LDS stores: one memory round
@@ -153,38 +156,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
   for (int u = 0; u < XPT; ++u) {
     const int c = threadIdx.x + 256 * u, rr = c / (H / 8), k8 = (c % (H / 8)) * 8;
-    if (c < VT_ROWS * (H / 8)) *reinterpret_cast<bf16x8*>(&Xs[rr * (H + 8) + k8]) = xr[u];
+    if (c < BR * (H / 8)) *reinterpret_cast<bf16x8*>(&Xs[rr * (H + 8) + k8]) = xr[u];
   }
-  f32x4 acc[4][4];  // [vocab column tile i][row tile jr]
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int jr = 0; jr < 4; ++jr) acc[i][jr] = f32x4{0, 0, 0, 0};
   __syncthreads();
 #pragma unroll
-  for (int h = 0; h < 8; ++h) {
-    if (32 * h < H) {
+  for (int h2 = 0; h2 < RH; ++h2) {
+    const int rbh = rb + VT_ROWS * h2;
+    f32x4 acc[4][4];  // [vocab column tile i][row tile jr]
 #pragma unroll
-      for (int jr = 0; jr < 4; ++jr) {
-        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&Xs[(16 * jr + c16) * (H + 8) + 32 * h + kof]);
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][jr] = mfma16(wa[h][i], xb, acc[i][jr]);
+      for (int jr = 0; jr < 4; ++jr) acc[i][jr] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      if (32 * h < H) {
+#pragma unroll
+        for (int jr = 0; jr < 4; ++jr) {
+          const bf16x8 xb =
+              *reinterpret_cast<const bf16x8*>(&Xs[(VT_ROWS * h2 + 16 * jr + c16) * (H + 8) + 32 * h + kof]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][jr] = mfma16(wa[h][i], xb, acc[i][jr]);
+        }
       }
     }
-  }
-  // ---- epilogue: + bias, store fp32, per-row (max, sum exp) over this wave's 64 columns.
-  // FULL (every tile but the last vocab tile / row block): no column or row guards.
-  const bool full = (vt + 1) * VT_COLS <= V && rb + VT_ROWS <= R && (V & 3) == 0;
+    // ---- epilogue: + bias, store fp32, per-row (max, sum exp) over this wave's 64 columns.
+    // FULL (every tile but the last vocab tile / row block): no column or row guards.
+    const bool full = (vt + 1) * VT_COLS <= V && rbh + VT_ROWS <= R && (V & 3) == 0;
 #pragma unroll
-  for (int jr = 0; jr < 4; ++jr) {
-    if (full)
-      vl_epilogue<true>(acc, jr, bc, logits, Pm[wid], Ps[wid], rb, cw, lane, R, V);
-    else
-      vl_epilogue<false>(acc, jr, bc, logits, Pm[wid], Ps[wid], rb, cw, lane, R, V);
+    for (int jr = 0; jr < 4; ++jr) {
+      if (full)
+        vl_epilogue<true>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
+      else
+        vl_epilogue<false>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
+    }
   }
   __syncthreads();
-  if (wid == 0) {
-    const int rr = lane, row = rb + rr;
+  for (int rr = threadIdx.x; rr < BR; rr += 256) {
+    const int row = rb + rr;
     float m = Pm[0][rr], sm = Ps[0][rr];
 #pragma unroll
     for (int w = 1; w < 4; ++w) ms_combine(m, sm, Pm[w][rr], Ps[w][rr]);
@@ -455,9 +463,17 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
                        int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st) {
   const int nt = vocab_topk_tiles(V);
-  const int RB = (R + VT_ROWS - 1) / VT_ROWS;
-  hipLaunchKernelGGL(vocab_logits_kernel<2>, dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
-                     part_ms, R, V, H);
+  // default: 128-row workgroups (392 at R = 256, V = 50k: one round at 2 per CU; W^T fragments
+  // fetched once per 128 rows): decode 5610 -> 5927 summaries/s at 64 articles, 6940 -> 7300 at
+  // 128.  TSAMD_VL_RH = 1: 64-row workgroups (784 at R = 256: 1.5 rounds)
+  static const int rh = [] { const char* e = getenv("TSAMD_VL_RH"); return e && atoi(e) == 1 ? 1 : 2; }();
+  const int RB = (R + VT_ROWS * rh - 1) / (VT_ROWS * rh);
+  if (rh == 2)
+    hipLaunchKernelGGL((vocab_logits_kernel<2, 2>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
+                       part_ms, R, V, H);
+  else
+    hipLaunchKernelGGL((vocab_logits_kernel<2, 1>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
+                       part_ms, R, V, H);
   hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
                      out_lp, V, T, K, beam, nt, pgi);
 }
