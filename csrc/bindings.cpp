@@ -425,7 +425,7 @@ void wgrad_tn(const Tensor& a, const Tensor& b, const Tensor& out) {
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.stride(1) == 1, "wgrad_tn: unit column stride");
   const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
   TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "wgrad_tn: shapes");
-  TORCH_CHECK(M % 128 == 0 && N % 128 == 0 && K >= 1, "wgrad_tn: M, N multiples of 128");
+  TORCH_CHECK(M % 128 == 0 && N % 8 == 0 && K >= 1, "wgrad_tn: M a multiple of 128, N of 8");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && (uintptr_t)a.data_ptr() % 16 == 0 &&
               (uintptr_t)b.data_ptr() % 16 == 0, "wgrad_tn: 16-byte aligned rows");
   launch_wgrad_tn(P<bf16>(a), (int)a.stride(0), P<bf16>(b), (int)b.stride(0), P<float>(out), (int)out.stride(0),

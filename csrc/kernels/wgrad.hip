@@ -1,6 +1,7 @@
 // Weight-gradient GEMM  out[M][N] += sum_k a[k][m] b[k][n]  (both operands K-major: rows are
-// tokens / decoder steps x batch, K = 25.6k-102k; M, N <= 1024), split-K over workgroups with
-// fp32 atomics into the pre-zeroed gradient buffer (SURVEY K22 weight gradients).
+// tokens / decoder steps x batch, K = 25.6k-102k; M <= 1024, N up to the 50k vocabulary),
+// split-K over workgroups with fp32 atomics into the pre-zeroed gradient buffer (SURVEY K22
+// weight gradients, incl. the vocab projection dW = X^T . dlogits of model.py:229-236).
 //
 // Why not the library GEMM: hipBLASLt runs these shapes as stream-K kernels whose tile owners
 // spin on flags of higher-numbered workgroups.  Beside another spinning kernel (a second
@@ -43,17 +44,27 @@ __device__ __forceinline__ bf16x8 frag(const bf16* img, int c0, int lane) {
 
 }  // namespace
 
-// grid (M / 128, N / 128, splits); M, N multiples of 128; any K (rows past the chunk end are
-// zero-filled); lda / ldb / ldo in elements
+// 1-D grid of gm x ceil8(ny) blocks, ny = ceil(N / 128) x splits (see the block map below); M a
+// multiple of 128, N a multiple of 8 (column chunks past N are zero-filled and not stored), any
+// K (rows past the chunk end are zero-filled); lda / ldb / ldo in elements
 template <int WBK>
 __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16* __restrict__ a, int lda, const bf16* __restrict__ b,
-                                                       int ldb, float* __restrict__ out, int ldo, int K, int kchunk) {
+                                                       int ldb, float* __restrict__ out, int ldo, int N, int K,
+                                                       int kchunk, int gm, int gn, int ny) {
   constexpr int CPT = WBK * 16 / 256;  // 16-byte chunks per thread per operand and stage
   __shared__ __attribute__((aligned(16))) bf16 As[2][WBK * WLD];
   __shared__ __attribute__((aligned(16))) bf16 Bs[2][WBK * WLD];
+  // XCD-aware block map: workgroups are dealt to the 8 XCDs round-robin by linear id, so
+  // blocks L and L + 8 share an XCD.  The gm row tiles of one (column tile, k-chunk) pair get
+  // ids 8 (gm j + i) + x (i < gm): they run on ONE XCD at about the same time and the b-operand
+  // rows (the tall K x N operand, e.g. the 2.56 GB vocab dlogits) come from HBM once and from
+  // that XCD's L2 for the other row tiles.
+  const int L = blockIdx.x, xcd = L & 7, q = L >> 3;
+  const int yi = (q / gm) * 8 + xcd;
+  if (yi >= ny) return;  // padding of ny to a multiple of 8 (uniform per block, before any barrier)
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int m0 = blockIdx.x * WBM, n0 = blockIdx.y * WBN;
-  const int k0 = blockIdx.z * kchunk, k1 = min(K, k0 + kchunk);
+  const int m0 = (q % gm) * WBM, n0 = (yi % gn) * WBN;
+  const int k0 = (yi / gn) * kchunk, k1 = min(K, k0 + kchunk);
   if (k0 >= k1) return;
   const int wm = (wid & 1) * 64, wn = (wid >> 1) * 64;
   // staging: WBK rows x 128 columns = WBK * 16 chunks of 16 B per operand, CPT per thread
@@ -64,7 +75,7 @@ __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16* __restrict__ 
       const int c = tid + 256 * u, r = c >> 4, col = (c & 15) * 8, k = kb + r;
       if (k < k1) {
         ra[u] = ld8(a + (size_t)k * lda + m0 + col);
-        rb[u] = ld8(b + (size_t)k * ldb + n0 + col);
+        rb[u] = n0 + col < N ? ld8(b + (size_t)k * ldb + n0 + col) : zero8();
       } else {
         ra[u] = zero8();
         rb[u] = zero8();
@@ -116,13 +127,14 @@ __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16* __restrict__ 
     for (int r = 0; r < 4; ++r) {
       float* row = out + (size_t)(m0 + wm + 16 * i + 4 * (lane >> 4) + r) * ldo + n0 + wn + (lane & 15);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) atomicAdd(row + 16 * j, acc[i][j][r]);
+      for (int j = 0; j < 4; ++j)
+        if (n0 + wn + 16 * j + (lane & 15) < N) atomicAdd(row + 16 * j, acc[i][j][r]);
     }
 }
 
 // splits: enough workgroups for ~2 per CU, each at least 512 rows of K
 int wgrad_tn_splits(int M, int N, int K) {
-  const int tiles = (M / WBM) * (N / WBN);
+  const int tiles = (M / WBM) * ((N + WBN - 1) / WBN);
   int s = (512 + tiles - 1) / tiles;
   const int smax = (K + 511) / 512;
   return s < 1 ? 1 : (s > smax ? smax : s);
@@ -135,9 +147,10 @@ void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out,
   const int s = wgrad_tn_splits(M, N, K);
   const int kchunk = ((K + s - 1) / s + WBK - 1) / WBK * WBK;
   const int splits = (K + kchunk - 1) / kchunk;
-  const dim3 grid(M / WBM, N / WBN, splits);
+  const int gm = M / WBM, gn = (N + WBN - 1) / WBN, ny = gn * splits;
+  const dim3 grid(gm * ((ny + 7) / 8 * 8));
   if (WBK == 32)
-    hipLaunchKernelGGL(wgrad_tn_kernel<32>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, K, kchunk);
+    hipLaunchKernelGGL(wgrad_tn_kernel<32>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, N, K, kchunk, gm, gn, ny);
   else
-    hipLaunchKernelGGL(wgrad_tn_kernel<64>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, K, kchunk);
+    hipLaunchKernelGGL(wgrad_tn_kernel<64>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, N, K, kchunk, gm, gn, ny);
 }

@@ -67,11 +67,12 @@ def test_cast_colsum(N, C):
 
 
 @pytest.mark.parametrize("K,M,N,strided", [(1000, 128, 128, False), (25600, 256, 512, False), (3001, 128, 256, True),
-                                           (130, 512, 128, True)])
+                                           (130, 512, 128, True), (25600, 256, 5000, False), (3001, 256, 200, True)])
 def test_wgrad_tn_matches_fp32(K, M, N, strided):
     """wgrad.hip: out[M][N] += a[K][M]^T b[K][N] (split-K MFMA, transposed LDS reads, fp32
-    atomics) vs an fp32 matmul, including K not a multiple of the k-step, row-strided operand
-    views and an output slice of a wider matrix."""
+    atomics) vs an fp32 matmul, including K not a multiple of the k-step, N not a multiple of
+    the 128-column tile (the vocab dW shape: M = 256, N = V), row-strided operand views and an
+    output slice of a wider matrix."""
     from textsummarization_on_flink_amd.ops import ops
     k = ops()
     g = torch.Generator(device="cuda").manual_seed(K + M)

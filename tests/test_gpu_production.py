@@ -157,8 +157,8 @@ def test_row_split_streams_match_single_chain(monkeypatch, split):
 
 def test_deferred_weight_gradients_match_inline(monkeypatch):
     """The decoder-side weight gradients deferred onto a side stream beside the encoder BPTT
-    (TSAMD_DEFER_WGRAD, default on) give the gradients of the inline order, in eager mode
-    and through the captured phase graphs."""
+    (TSAMD_DEFER_WGRAD, default on; with the opt-in TSAMD_DEFER_VOCAB_DW the vocab dW too) give
+    the gradients of the inline order, in eager mode and through the captured phase graphs."""
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
     B = 256
     hps = _hps(B, trunc_norm_init_std=0.05).replace(max_dec_steps=24)
@@ -166,6 +166,7 @@ def test_deferred_weight_gradients_match_inline(monkeypatch):
     got = []
     for defer in ("0", "1"):
         monkeypatch.setenv("TSAMD_DEFER_WGRAD", defer)
+        monkeypatch.setenv("TSAMD_DEFER_VOCAB_DW", defer)  # the opt-in vocab dW through wgrad_tn too
         params = build_params(hps, vocab.size(), device="cuda", seed=6).enable_grad()
         eng = HipPointerGenerator(hps, vocab.size(), params, B=B, T=T, D=24)
         assert eng.defer_wgrad == (defer == "1")

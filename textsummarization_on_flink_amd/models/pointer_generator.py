@@ -258,6 +258,14 @@ class HipPointerGenerator:
             not self.persistent_lstm or
             int(self.k.lstm_persistent_grid(H, B)) <= int(self.k.lstm_persistent_capacity(H)) - 64))
         self._late_stream = torch.cuda.Stream(self.dev) if self.defer_wgrad else None
+        # TSAMD_DEFER_VOCAB_DW=1 (opt-in) adds the vocab projection's weight gradient
+        # dW = X^T . dlogits (a 0.74 ms library GEMM at B = 256 on the critical path of
+        # backward_head), through wgrad_tn (its XCD-paired row tiles read the 2.56 GB dlogits from
+        # HBM once).  Measured at B = 256: 19.63-19.80 ms inline vs 19.96-20.01 deferred -- 2.6 GB
+        # of HBM traffic beside the latency-bound BPTT slows it more than the GEMM costs inline
+        # (profiles/r2/ab/vocab_dw_deferred.jsonl).  Its bucket (0) is then complete only after
+        # backward_tail, so a data-parallel trainer always keeps it inline (GraphTrainer).
+        self._vocab_dw_late = None  # (defer_vocab_dw: set with the vocab head below)
         # reduce_states: pre-activations [c; h], bf16 [fw, bw] inputs and bf16 dp (wgrad operands)
         w["rs_pre"] = z(2, B, H)
         w["rs_cat"] = z(2, B, 2 * H, dt=BF)
@@ -313,6 +321,8 @@ class HipPointerGenerator:
             for n in ("zg", "lse", "pv", "alpha"):
                 w[n] = z(N)
             w["dbias"] = z(V)  # output_projection/v gradient, column sums taken inside pass 2
+        self.defer_vocab_dw = (self.defer_wgrad and os.environ.get("TSAMD_DEFER_VOCAB_DW", "0") == "1"
+                               and self.fused_vocab and H % 128 == 0 and V % 8 == 0)
         w["logits"] = z(D * B, V, dt=BF)
         # backward
         w["dlogits"] = w["logits"]
@@ -682,7 +692,10 @@ class HipPointerGenerator:
                 torch.sum(parts, 0, out=dst)
             else:
                 torch.mm(w["outb_ext"][:, :m].t(), dl, out_dtype=F32, out=dst)
-        if self._side is not None:  # deferred to backward_mid's side branch
+        if self.defer_vocab_dw:  # beside the encoder BPTT (backward_tail)
+            xh, gw = w["outb_ext"][:, :H], dst
+            self._vocab_dw_late = lambda: self.k.wgrad_tn(xh, dl, gw)
+        elif self._side is not None:  # deferred to backward_mid's side branch
             self._dw_pending = dw
         else:
             dw()
@@ -833,6 +846,9 @@ class HipPointerGenerator:
         dE = self._dE
         lens = w["enc_lens"]
         late, self._late = self._late, []
+        if self._vocab_dw_late is not None:  # the largest one first: it starts with the BPTT
+            late.insert(0, self._vocab_dw_late)
+            self._vocab_dw_late = None
         if late:  # the deferred decoder weight gradients, beside the encoder BPTT
             side = self._late_stream
             side.wait_stream(torch.cuda.current_stream())
