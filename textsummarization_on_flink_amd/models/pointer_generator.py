@@ -321,6 +321,11 @@ class HipPointerGenerator:
             for n in ("zg", "lse", "pv", "alpha"):
                 w[n] = z(N)
             w["dbias"] = z(V)  # output_projection/v gradient, column sums taken inside pass 2
+        # split-K factors of the two vocab-gradient GEMMs (batched GEMM + a sum; A/B knobs).
+        # Measured at B = 256 (profiles/r2/ab/vocab_grad_split.jsonl): dX unsplit 19.47-19.53 ms
+        # per step vs 19.67-20.02 split 2 / 4 / 8; dW split 8 = split 4 within noise
+        self.dx_split = int(os.environ.get("TSAMD_VOCAB_DX_SPLIT", "1"))
+        self.dw_split = int(os.environ.get("TSAMD_VOCAB_DW_SPLIT", "4"))
         self.defer_vocab_dw = (self.defer_wgrad and os.environ.get("TSAMD_DEFER_VOCAB_DW", "0") == "1"
                                and self.fused_vocab and H % 128 == 0 and V % 8 == 0)
         w["logits"] = z(D * B, V, dt=BF)
@@ -685,10 +690,11 @@ class HipPointerGenerator:
         N = self.D * self.B
 
         def dw():
-            if m == H and N % 4 == 0:
-                # split K = N in 4 (one batched GEMM + a sum): 0.82 -> 0.74 ms at B = 256
-                xe = w["outb_ext"].view(4, N // 4, H + 8)[:, :, :H]
-                parts = torch.bmm(xe.transpose(1, 2), dl.view(4, N // 4, V), out_dtype=F32)
+            Sw = self.dw_split
+            if m == H and Sw > 1 and N % Sw == 0:
+                # split K = N in Sw = 4 (one batched GEMM + a sum): 0.82 -> 0.74 ms at B = 256
+                xe = w["outb_ext"].view(Sw, N // Sw, H + 8)[:, :, :H]
+                parts = torch.bmm(xe.transpose(1, 2), dl.view(Sw, N // Sw, V), out_dtype=F32)
                 torch.sum(parts, 0, out=dst)
             else:
                 torch.mm(w["outb_ext"][:, :m].t(), dl, out_dtype=F32, out=dst)
@@ -699,7 +705,16 @@ class HipPointerGenerator:
             self._dw_pending = dw
         else:
             dw()
-        self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
+        S = self.dx_split
+        if S > 1 and V % S == 0:
+            # dX = dlogits . W^T split over S vocab chunks (one batched GEMM + a sum): the plain
+            # [N, V] x [V, H] product has only N/256 x 1 output tiles of 256 x 256
+            Vs = V // S
+            parts = torch.bmm(dl.view(N, S, Vs).permute(1, 0, 2), self.pk["ow"].view(H, S, Vs).permute(1, 2, 0),
+                              out_dtype=F32)
+            self._dout = parts.sum(0)
+        else:
+            self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
 
     def _cast_colsum(self, x, bias_grad):
         """bf16 copy of x [N, C] plus bias_grad += its column sums in one read of x (the
