@@ -176,9 +176,28 @@ void attn_fwd_row(const Tensor& F, const Tensor& E, const Tensor& s, const Tenso
   numel_eq(lens, B / rep, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx");
   chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out");
   chko(covloss, F32, B, "covloss"); chko(ctx_bf, BF, B * A, "ctx_bf");
-  launch_attn_fwd_row(P<bf16>(F), P<bf16>(E), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens),
-                      P<float>(a_out), PO<float>(cov_out), PO<float>(covloss), P<float>(ctx), PO<bf16>(ctx_bf), B, T, A,
-                      (int)rep, stream());
+  launch_attn_fwd_row(P<bf16>(F), P<bf16>(E), P<float>(s), nullptr, nullptr, nullptr, nullptr, P<float>(v), PO<float>(wc),
+                      PO<float>(cov), P<int>(lens), P<float>(a_out), PO<float>(cov_out), PO<float>(covloss), P<float>(ctx),
+                      PO<bf16>(ctx_bf), B, T, A, (int)rep, stream());
+}
+// the same with the attention query projection inside the kernel: s_out = [cb, hb] . WsT^T + bs
+// (replaces dec_sproj + attn_fwd_row in the training decoder loop)
+void attn_fwd_row_sproj(const Tensor& F, const Tensor& E, const Tensor& cb, const Tensor& hb, const Tensor& WsT,
+                        const Tensor& bs, const Tensor& s_out, const Tensor& v, const OT& wc, const OT& cov,
+                        const Tensor& lens, const Tensor& a_out, const OT& cov_out, const OT& covloss, const Tensor& ctx,
+                        const OT& ctx_bf, int64_t B, int64_t T, int64_t A) {
+  chk(F, BF, "F"); chk(E, BF, "E"); chk(s_out, F32, "s_out"); chk(v, F32, "v"); chk(lens, I32, "lens");
+  chk(cb, BF, "cb"); chk(hb, BF, "hb"); chk(WsT, BF, "WsT"); chk(bs, F32, "bs");
+  chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
+  TORCH_CHECK(attn_row_supported((int)A, (int)T), "row attention needs A in {512, 1024} and T <= 2048");
+  numel_eq(F, B * T * A, "F"); numel_eq(E, B * T * A, "E"); numel_eq(s_out, B * A, "s_out"); numel_eq(v, A, "v");
+  numel_eq(cb, B * A / 2, "cb"); numel_eq(hb, B * A / 2, "hb"); numel_eq(WsT, A * A, "WsT"); numel_eq(bs, A, "bs");
+  numel_eq(lens, B, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx");
+  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out");
+  chko(covloss, F32, B, "covloss"); chko(ctx_bf, BF, B * A, "ctx_bf");
+  launch_attn_fwd_row(P<bf16>(F), P<bf16>(E), P<float>(s_out), P<bf16>(cb), P<bf16>(hb), P<bf16>(WsT), P<float>(bs),
+                      P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens), P<float>(a_out), PO<float>(cov_out),
+                      PO<float>(covloss), P<float>(ctx), PO<bf16>(ctx_bf), B, T, A, 1, stream());
 }
 void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                   const Tensor& a, const Tensor& dctx, const Tensor& ctx, const OT& Ga, const OT& dcov_next,
@@ -722,6 +741,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("attn_bwd_step", &attn_bwd_step);
   m.def("attn_row_ok", &attn_row_ok);
   m.def("attn_fwd_row", &attn_fwd_row);
+  m.def("attn_fwd_row_sproj", &attn_fwd_row_sproj);
   m.def("attn_bwd_row", &attn_bwd_row);
   m.def("attn_bwd_feat", &attn_bwd_feat);
   m.def("attn_chunks", &attn_chunks);

@@ -58,9 +58,22 @@ __device__ __forceinline__ void load_rows(Rows<NK>& r, const bf16* base, int p0,
 }  // namespace
 
 // ------------------------------------------------------------------------------ forward
+// Optional attention-query projection in the prologue (training, rep = 1): with WsT set, the
+// row's s = [c, h] . W_s + b_s (reference attention_decoder.py:93; K = 2H = A) is computed here
+// -- 8 lanes per output feature, each reading 128 contiguous bytes of its W_s^T row per load,
+// dpp_sum8 across them -- and stored to s (the backward reads it), instead of by a separate
+// linear2 launch between the decoder cell and this kernel.  Group 0's F / E rows are already in
+// flight while it runs.
+struct SProj {
+  const bf16* c;    // [B][H] bf16 (nullptr: s is an input)
+  const bf16* h;    // [B][H] bf16
+  const bf16* WsT;  // [A][2H] bf16
+  const float* bs;  // [A]
+};
+
 template <int NK, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
-    const bf16* __restrict__ F, const bf16* __restrict__ E, const float* __restrict__ s,
+    const bf16* __restrict__ F, const bf16* __restrict__ E, float* __restrict__ s, SProj sp,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
     const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
     float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T, int rep, int xper) {
@@ -68,6 +81,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
   __shared__ float es[kRowMaxT];
   __shared__ float part[NW][A];
   __shared__ float wm[NW], wl[NW], red[NW];
+  __shared__ float s_sh[A];
   // xper > 0 (beam decode): workgroups are dispatched to the 8 XCDs round-robin, so workgroup
   // i runs on XCD i % 8; give XCD x the xper consecutive rows x * xper .. -- whole articles --
   // so the rep hypotheses of an article read its F / E rows through ONE XCD's L2
@@ -90,6 +104,35 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     c = cov ? cov[rb + p] : 0.f;
   };
   if (wid < ngrp) load(wid, fA, eA, cA);
+  const float* srow = s + (size_t)b * A;
+  if (sp.WsT) {
+    constexpr int H = A / 2;
+    const int l8 = lane & 7;
+    bf16x8 xr[A / 64];  // this lane's K chunks of x = [c, h]: elements 64 j + 8 l8 .. + 7
+#pragma unroll
+    for (int j = 0; j < A / 64; ++j) {
+      const int kx = 64 * j + 8 * l8;
+      xr[j] = kx < H ? ld8(sp.c + (size_t)b * H + kx) : ld8(sp.h + (size_t)b * H + kx - H);
+    }
+    for (int n = tid >> 3; n < A; n += NT / 8) {
+      const bf16* wr = sp.WsT + (size_t)n * A + 8 * l8;
+      f32x2 d2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < A / 64; ++j) {
+        const u32x4 wv = __builtin_bit_cast(u32x4, ld8(wr + 64 * j));
+        const u32x4 xv = __builtin_bit_cast(u32x4, xr[j]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d2 = fma2(bf2pair(wv[q]), bf2pair(xv[q]), d2);
+      }
+      const float sn = dpp_sum8(d2.x + d2.y) + sp.bs[n];
+      if (l8 == 0) {
+        s_sh[n] = sn;
+        s[(size_t)b * A + n] = sn;
+      }
+    }
+    __syncthreads();
+    srow = s_sh;
+  }
   // per-lane feature parameters, pre-scaled for the r-form (attn_common.h)
   f32x2 s2[NK][4], w2[NK][4], v2[NK][4], acc[NK][4];
   float vsum = 0.f;
@@ -98,7 +141,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     const int k0 = kb * 512 + lane * 8;
 #pragma unroll
     for (int jp = 0; jp < 4; ++jp) {
-      const float2 sv = *reinterpret_cast<const float2*>(s + (size_t)b * A + k0 + 2 * jp);
+      const float2 sv = *reinterpret_cast<const float2*>(srow + k0 + 2 * jp);
       const float2 vv = *reinterpret_cast<const float2*>(v + k0 + 2 * jp);
       const float2 wv = wc ? *reinterpret_cast<const float2*>(wc + k0 + 2 * jp) : make_float2(0.f, 0.f);
       s2[kb][jp] = f32x2{sv.x, sv.y} * K2LOG2E;
@@ -353,15 +396,17 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
 // ------------------------------------------------------------------------------ launchers
 bool attn_row_supported(int A, int T) { return (A == 512 || A == 1024) && T >= 1 && T <= kRowMaxT; }
 
-void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
-                         const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
-                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st) {
+void launch_attn_fwd_row(const bf16* F, const bf16* E, float* s, const bf16* sc, const bf16* sh, const bf16* WsT,
+                         const float* bs, const float* v, const float* wc, const float* cov, const int* lens,
+                         float* a_out, float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A,
+                         int rep, hipStream_t st) {
+  const SProj sp{sc, sh, WsT, bs};
   // TSAMD_ATTN_XCD=0 keeps the identity workgroup -> row map for beam decode (A/B runs)
   static const bool xcd = [] { const char* e = getenv("TSAMD_ATTN_XCD"); return !(e && atoi(e) == 0); }();
   const int xper = (xcd && rep > 1 && B % 8 == 0 && (B / 8) % rep == 0) ? B / 8 : 0;
 #define LF(NK)                                                                                                 \
   hipLaunchKernelGGL((attn_fwd_row_kernel<NK, row_waves<NK, false>()>), dim3(B), dim3(row_waves<NK, false>() * 64), \
-                     0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep, xper)
+                     0, st, F, E, s, sp, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep, xper)
   if (A == 512) LF(1);
   else LF(2);
 #undef LF

@@ -30,9 +30,12 @@ void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, con
                           int A, int nslot, hipStream_t st);
 
 bool attn_row_supported(int A, int T);
-void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
-                         const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
-                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st);
+// s: the attention query [B][A] -- an input, or (WsT set: s = [sc, sh] . WsT^T + bs computed in
+// the kernel, rep = 1) an output
+void launch_attn_fwd_row(const bf16* F, const bf16* E, float* s, const bf16* sc, const bf16* sh, const bf16* WsT,
+                         const float* bs, const float* v, const float* wc, const float* cov, const int* lens,
+                         float* a_out, float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A,
+                         int rep, hipStream_t st);
 void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
                          const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
                          const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,

@@ -282,6 +282,12 @@ class HipPointerGenerator:
         # hides too little latency -- config #5 decoder backward 79 ms vs 59 ms with the
         # multi-block attn_bwd_step (tools/phase_micro.py) -- so it is used at A = 512 only
         self.row_attn_bwd = self.row_attn and (A == 512 or ra == "1")
+        # TSAMD_FUSED_SPROJ=1 (opt-in): the attention query projection s = [c, h] . W_s + b inside
+        # the row forward kernel instead of its own linear2 launch.  Measured slower
+        # (profiles/r2/ab/fused_sproj_rejected.jsonl): B = 256 19.7-19.8 -> 21.0-21.1 ms, config #5
+        # 158 -> 173 ms -- every row's workgroup streams all of W_s (512 KB-2 MB) through its CU
+        # before its first score, where the 16 x 16-tile linear2 reads each W_s row 8-16 times in all
+        self.fused_sproj = self.row_attn and os.environ.get("TSAMD_FUSED_SPROJ", "0") == "1"
         w["F"] = z(B, T, A, dt=BF)
         # transposed copy for the lanes-over-positions score kernel (not needed by the row
         # kernels; the beam decoder sets keep_ft to get it from _encoder_forward)
@@ -568,9 +574,15 @@ class HipPointerGenerator:
                 k.dec_cell_fwd(w["XG"][t][rs], w["CTXb"][t - 1][rs] if t > 0 else None, w["Hb"][t][rs],
                                w["Cst"][t][rs], self.pk["WcT2"], w["Cst"][t + 1][rs], w["Cb"][t + 1][rs],
                                w["Hb"][t + 1][rs], w["ACT"][t][rs], Bg, H, A)
+                cov_in = w["COV"][t][rs] if (cov and t > 0) else None
+                if self.fused_sproj:  # s = [c, h] . W_s + b computed inside the row attention kernel
+                    k.attn_fwd_row_sproj(F[rs], enc_out[rs], w["Cb"][t + 1][rs], w["Hb"][t + 1][rs], self.pk["WsT"],
+                                         self.p[ATT_B], w["S"][t][rs], v, wc, cov_in, lens[rs], w["ATT"][t][rs],
+                                         w["COV"][t + 1][rs] if cov else None, w["covloss"][t][rs] if cov else None,
+                                         w["CTX"][t][rs], w["CTXb"][t][rs], Bg, T, A)
+                    continue
                 k.dec_sproj(w["Cb"][t + 1][rs], w["Hb"][t + 1][rs], self.pk["WsT"], self.p[ATT_B], w["S"][t][rs], Bg,
                             H, A)
-                cov_in = w["COV"][t][rs] if (cov and t > 0) else None
                 if self.row_attn:
                     k.attn_fwd_row(F[rs], enc_out[rs], w["S"][t][rs], v, wc, cov_in, lens[rs], w["ATT"][t][rs],
                                    w["COV"][t + 1][rs] if cov else None, w["covloss"][t][rs] if cov else None,
