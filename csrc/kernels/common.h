@@ -106,16 +106,17 @@ __device__ __forceinline__ f32x4 mfma_k(const bf16* a_row, const bf16* b_row, in
 }
 
 // K-slice of NB tiles that share the A fragment: acc[j] += A[:, k0:k1] . Bt_j[:, k0:k1].
-// Loads are issued in batches of 4 k-steps before the MFMAs of the batch; a batch step
-// past k1 loads a valid (clamped) address and is zeroed, so the code is branch-free.
-// a(k) / b(j, k): pointers for this lane at absolute k (must include the 8*(l>>4) offset).
-template <int NB, typename FA, typename FB>
+// Loads are issued in batches of KB k-steps before the MFMAs of the batch (one L2 round trip
+// per batch); a batch step past k1 loads a valid (clamped) address and is zeroed, so the code
+// is branch-free.  a(k) / b(j, k): pointers for this lane at absolute k (must include the
+// 8*(l>>4) offset).
+template <int NB, int KB = 4, typename FA, typename FB>
 __device__ __forceinline__ void kslice_mma(FA a, FB b, int k0, int k1, f32x4 (&acc)[NB]) {
-  for (int k = k0; k < k1; k += 128) {
-    bf16x8 af[4];
-    bf16x8 bfr[NB][4];
+  for (int k = k0; k < k1; k += 32 * KB) {
+    bf16x8 af[KB];
+    bf16x8 bfr[NB][KB];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < KB; ++i) {
       const int kk = k + 32 * i;
       const int kc = kk < k1 ? kk : k0;
       af[i] = a(kc);
@@ -123,7 +124,7 @@ __device__ __forceinline__ void kslice_mma(FA a, FB b, int k0, int k1, f32x4 (&a
       for (int j = 0; j < NB; ++j) bfr[j][i] = b(j, kc);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < KB; ++i) {
       if (k + 32 * i < k1) {
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[j] = mfma16(af[i], bfr[j][i], acc[j]);

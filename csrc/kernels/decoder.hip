@@ -16,6 +16,7 @@
 // Every kernel: one block = 4 waves on a 16x16 output tile (x 4 gates for the cell),
 // K split across the waves (kslice_mma) and summed in LDS (ksplit_reduce).
 #include "common.h"
+#include <stdlib.h>
 
 // XCD-aware tile order for the (column tile, row tile) grids below.  Blocks are dealt to
 // the 8 XCDs round-robin by linear id; every block of a column tile re-reads that tile's
@@ -34,7 +35,9 @@ __device__ __forceinline__ void xcd_tile(int& tx, int& ty) {
 }
 
 // z = XG + [ctx, h] . WcT^T ; cell update.  WcT: [4H][A+H] (cols 0..A-1 = W_comb^T, A.. = W_cell[E:]^T).
-// grid (H/16, ceil(B/16)).
+// grid (H/16, ceil(B/16)).  KB: k-steps per load batch (kslice_mma) -- 6 covers a wave's
+// K / 4 = 192 at hidden 256 in one L2 round trip instead of two.
+template <int KB>
 __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
     const float* __restrict__ XG,      // [B][4H]
     const bf16* __restrict__ ctxp,     // [B][A]   ctx_{t-1} (nullptr at t==0)
@@ -71,7 +74,7 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
   f32x4 acc[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) acc[g] = f32x4{0, 0, 0, 0};
-  kslice_mma<4>([&](int k) { return k < A ? ld8(crow + k) : ld8(hrow + k); },
+  kslice_mma<4, KB>([&](int k) { return k < A ? ld8(crow + k) : ld8(hrow + k); },
                 [&](int g, int k) { return ld8(W + (size_t)g * H * K + k); }, k0, k1, acc);
   float z[4];
   ksplit_reduce<4>(acc, red, z);
@@ -268,7 +271,8 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
 }
 
 // [dx_t | dh_{t-1} | dctx_{t-1}] = dz_t . Wbig^T, Wbig = [W_cell ; W_comb]: [E+H+A][4H].
-// grid ((E+H+A)/16, ceil(B/16)).
+// grid ((E+H+A)/16, ceil(B/16)).  KB: k-steps per load batch (see the launcher).
+template <int KB>
 __global__ __launch_bounds__(256) void dec_bwd_dz_kernel(
     const bf16* __restrict__ dz, const bf16* __restrict__ Wbig,
     const float* __restrict__ dX_dir,        // [B][E] nullable
@@ -290,7 +294,7 @@ __global__ __launch_bounds__(256) void dec_bwd_dz_kernel(
   const int nst = G / 32;
   const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
   f32x4 acc[1] = {f32x4{0, 0, 0, 0}};
-  kslice_mma<1>([&](int k) { return ld8(arow + k); }, [&](int, int k) { return ld8(brow + k); }, k0, k1, acc);
+  kslice_mma<1, KB>([&](int k) { return ld8(arow + k); }, [&](int, int k) { return ld8(brow + k); }, k0, k1, acc);
   float o[1];
   ksplit_reduce<1>(acc, red, o);
   const int r = r0 + (lane >> 4) * 4 + wid, n = n0 + (lane & 15);
@@ -305,11 +309,23 @@ __global__ __launch_bounds__(256) void dec_bwd_dz_kernel(
   }
 }
 
+// dec_cell_fwd with 6-step load batches: 7.67 -> 6.79 us per call at hidden 256 / 128 rows (one
+// L2 round trip instead of two), equal at hidden 512; B = 256 train 19.71-19.77 -> 19.63-19.67 ms
+// (profiles/r2/ab/dec_cell_kb.jsonl).  TSAMD_DEC_KB=0 keeps 4-step batches (A/B runs).
+static bool dec_deep_batches() {
+  static const bool on = [] { const char* e = getenv("TSAMD_DEC_KB"); return !(e && atoi(e) == 0); }();
+  return on;
+}
+
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16);
-  hipLaunchKernelGGL(dec_cell_fwd_kernel, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out, hb_out,
-                     act, B, H, A);
+  if (dec_deep_batches())
+    hipLaunchKernelGGL(dec_cell_fwd_kernel<6>, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out,
+                       hb_out, act, B, H, A);
+  else
+    hipLaunchKernelGGL(dec_cell_fwd_kernel<4>, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out,
+                       hb_out, act, B, H, A);
 }
 void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
                     const float* add, float* out, bf16* outb, int B, int N, hipStream_t st) {
@@ -358,6 +374,8 @@ void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, co
                        float* dx_out, float* dctx_prev_out, float* dh_rec, int B, int E, int H, int A,
                        hipStream_t st) {
   dim3 grid((E + H + A) / 16, (B + 15) / 16);
-  hipLaunchKernelGGL(dec_bwd_dz_kernel, grid, dim3(256), 0, st, dz, Wbig, dX_dir, dCTX_dir_prev, dx_out,
+  // KB = 8 measured equal (5.68 vs 5.74 us at 128 rows, tools/dec_kernels_micro.py) at 96 instead
+  // of 41 VGPRs, so this one keeps 4-step batches
+  hipLaunchKernelGGL(dec_bwd_dz_kernel<4>, grid, dim3(256), 0, st, dz, Wbig, dX_dir, dCTX_dir_prev, dx_out,
                      dctx_prev_out, dh_rec, B, E, H, A);
 }
