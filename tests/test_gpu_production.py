@@ -131,20 +131,23 @@ def test_loss_curve_tracks_fp32_oracle_50_steps():
     assert lh[-5:].mean() < lh[:5].mean()  # and it learns
 
 
-@pytest.mark.parametrize("split", ["2", "4"])
+@pytest.mark.parametrize("split", ["2", "4", "2/1", "1/2"])
 def test_row_split_streams_match_single_chain(monkeypatch, split):
-    """The decoder recurrences run as ``split`` row groups on parallel streams; the result
-    must equal the single-chain launch sequence (same kernels on row slices)."""
+    """The decoder recurrences run as ``split`` row groups on parallel streams (``fwd/bwd``: a
+    different group count for the backward loop, TSAMD_SPLIT_BWD); the result must equal the
+    single-chain launch sequence (same kernels on row slices)."""
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
     B = 64
     hps = _hps(B, trunc_norm_init_std=0.05).replace(max_dec_steps=20)
     vocab, (batch,) = _batches(hps, 1, seed=14)
     got = []
-    for sp in ("1", split):
-        monkeypatch.setenv("TSAMD_SPLIT", sp)
+    for sp in ("1/1", split if "/" in split else f"{split}/{split}"):
+        fw, bw = sp.split("/")
+        monkeypatch.setenv("TSAMD_SPLIT", fw)
+        monkeypatch.setenv("TSAMD_SPLIT_BWD", bw)
         params = build_params(hps, vocab.size(), device="cuda", seed=5).enable_grad()
         eng = HipPointerGenerator(hps, vocab.size(), params, B=B, T=T, D=20)
-        assert eng.split == int(sp)
+        assert (eng.split, eng.split_bwd) == (int(fw), int(bw))
         eng.set_batch(batch)
         out = eng.forward(need_grad=True)
         eng.backward()

@@ -190,8 +190,13 @@ class HipPointerGenerator:
         # kernels instead of serialising behind them.  TSAMD_SPLIT overrides (1 = one chain).
         sp = int(os.environ.get("TSAMD_SPLIT", "0")) or (2 if B >= 128 and B % 32 == 0 else 1)
         self.split = sp if (sp > 1 and B % (16 * sp) == 0) else 1
-        self._rows = [(B * g // self.split, B * (g + 1) // self.split) for g in range(self.split)]
-        self._streams = [torch.cuda.Stream(self.dev) for _ in range(self.split)] if self.split > 1 else []
+        # TSAMD_SPLIT_BWD: the decoder backward loop's own group count (default: split; at B = 256
+        # 2 groups 19.59-19.62 ms per step, 1 group 20.02-20.07, 4 groups 20.09:
+        # profiles/r2/ab/split_bwd.jsonl)
+        spb = int(os.environ.get("TSAMD_SPLIT_BWD", "0")) or self.split
+        self.split_bwd = spb if (spb > 1 and B % (16 * spb) == 0) else 1
+        ns = max(self.split, self.split_bwd)
+        self._streams = [torch.cuda.Stream(self.dev) for _ in range(ns)] if ns > 1 else []
         self._alloc()
         self.pack()
 
@@ -636,17 +641,20 @@ class HipPointerGenerator:
                         w["dpre"] if (need_grad and hps.pointer_gen) else None,
                         w["dA"] if (need_grad and hps.pointer_gen) else None, N, B, T, V)
 
-    def _row_groups(self, chain):
-        """Run ``chain(r0, r1)`` for every row group: inline when split == 1, else each group
-        on its own stream, forked from and joined back to the current stream."""
-        if self.split == 1:
+    def _row_groups(self, chain, split=None):
+        """Run ``chain(r0, r1)`` for every row group (``split`` groups, default self.split):
+        inline when split == 1, else each group on its own stream, forked from and joined back
+        to the current stream."""
+        n = self.split if split is None else split
+        if n == 1:
             return chain(0, self.B)
         cur = torch.cuda.current_stream()
-        for st, (r0, r1) in zip(self._streams, self._rows):
+        rows = [(self.B * g // n, self.B * (g + 1) // n) for g in range(n)]
+        for st, (r0, r1) in zip(self._streams, rows):
             st.wait_stream(cur)
             with torch.cuda.stream(st):
                 chain(r0, r1)
-        for st in self._streams:
+        for st in self._streams[:n]:
             cur.wait_stream(st)
 
     def forward(self, need_grad: bool = False):
@@ -820,7 +828,7 @@ class HipPointerGenerator:
                              dCTX_dir[t - 1][rs] if t > 0 else None, w["DX"][t][rs],
                              w["DCTX"][t - 1][rs] if t > 0 else None, w["dh_rec"][rs], Bg, E, H, A)
 
-        self._row_groups(chain)
+        self._row_groups(chain, self.split_bwd)
         # ---- decoder weight gradients (one GEMM each over all D*B rows)
         emb_dec = self._emb_dec
 
