@@ -202,7 +202,9 @@ void attn_fwd_row_sproj(const Tensor& F, const Tensor& E, const Tensor& cb, cons
 void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                   const Tensor& a, const Tensor& dctx, const Tensor& ctx, const OT& Ga, const OT& dcov_next,
                   const OT& gcl, const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out,
-                  int64_t B, int64_t T, int64_t A) {
+                  int64_t B, int64_t T, int64_t A, const OT& ds1) {
+  // ds1 given: two workgroups per row, partial ds in ds and ds1 (dec_bwd_cell sums them)
+  chko(ds1, F32, B * A, "ds1");
   chk(E, BF, "E"); chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(dctx, F32, "dctx");
   chk(ctx, F32, "ctx"); chk(lens, I32, "lens"); chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
   TORCH_CHECK(attn_row_supported((int)A, (int)T), "row attention needs A in {512, 1024} and T <= 2048");
@@ -213,7 +215,8 @@ void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tenso
   chko(dcov_next, F32, B * T, "dcov_next"); chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
   launch_attn_bwd_row(P<bf16>(E), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
                       P<float>(dctx), P<float>(ctx), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl),
-                      P<int>(lens), P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, stream());
+                      P<int>(lens), P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, PO<float>(ds1),
+                      stream());
 }
 
 void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
@@ -380,7 +383,8 @@ void dec_sproj(const Tensor& cb, const Tensor& hb, const Tensor& WsT, const Tens
 
 void dec_bwd_cell(const Tensor& ds, const Tensor& Ws, const OT& dC_dir, const OT& dH_dir, const Tensor& dh_rec,
                   const Tensor& dc_carry, const Tensor& act, const Tensor& c_now, const Tensor& c_prev,
-                  const Tensor& dz, int64_t B, int64_t H, int64_t A) {
+                  const Tensor& dz, int64_t B, int64_t H, int64_t A, const OT& ds2) {
+  chko(ds2, F32, B * A, "ds2");  // second partial of ds (attn_bwd_row with two workgroups per row)
   chk(ds, F32, "ds"); chk(Ws, BF, "Ws"); chk(dh_rec, F32, "dh_rec"); chk(dc_carry, F32, "dc_carry");
   chk(act, F32, "act"); chk(c_now, F32, "c_now"); chk(c_prev, F32, "c_prev"); chk(dz, BF, "dz");
   TORCH_CHECK(H % 16 == 0 && A % 32 == 0, "bad dims");
@@ -388,7 +392,7 @@ void dec_bwd_cell(const Tensor& ds, const Tensor& Ws, const OT& dC_dir, const OT
   chko(dH_dir, F32, B * H, "dH_dir"); numel_eq(dh_rec, B * H, "dh_rec"); numel_eq(dc_carry, B * H, "dc_carry");
   numel_eq(act, B * 4 * H, "act"); numel_eq(c_now, B * H, "c_now"); numel_eq(c_prev, B * H, "c_prev");
   numel_eq(dz, B * 4 * H, "dz");
-  launch_dec_bwd_cell(P<float>(ds), P<bf16>(Ws), PO<float>(dC_dir), PO<float>(dH_dir), P<float>(dh_rec),
+  launch_dec_bwd_cell(P<float>(ds), PO<float>(ds2), P<bf16>(Ws), PO<float>(dC_dir), PO<float>(dH_dir), P<float>(dh_rec),
                       P<float>(dc_carry), P<float>(act), P<float>(c_now), P<float>(c_prev), P<bf16>(dz), B, H, A,
                       stream());
 }

@@ -254,11 +254,15 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
     const float* __restrict__ a, const float* __restrict__ dctx, const float* __restrict__ ctx,
     const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
     const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
-    float* __restrict__ dcov_out, int T) {
+    float* __restrict__ dcov_out, int T, float* __restrict__ ds1) {
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float part[NW][A];
   __shared__ float red[NW];
-  const int b = blockIdx.x;
+  // ds1 set: TWO workgroups per row (blocks 2b, 2b + 1), their 2 NW waves dealing the row's
+  // position groups round-robin, so a row's chain of groups runs on two CUs; each stores its
+  // partial ds (to ds / ds1: the consumer, dec_bwd_cell, adds them).  S is computed by both.
+  const int parts = ds1 ? 2 : 1;
+  const int b = blockIdx.x / parts, pt = blockIdx.x % parts;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
@@ -283,7 +287,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
     x.dn = dcov_next ? dcov_next[ix] : 0.f;
     x.r = (Ga ? Ga[ix] : 0.f) + x.dn + ((gcl && x.a <= x.c) ? g : 0.f);
   };
-  if (wid < ngrp) load(wid, eA, fA, xA);
+  const int gw = pt * NW + wid, NWT = parts * NW;  // this wave's index among the row's waves
+  if (gw < ngrp) load(gw, eA, fA, xA);
   float dk[NK][8];
   f32x2 s2[NK][4], w2[NK][4], v4w[NK][4], acc[NK][4];
 #pragma unroll
@@ -362,18 +367,18 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
       }
     }
   };
-  for (int gi = wid; gi < ngrp;) {
-    const int g1 = gi + NW;
+  for (int gi = gw; gi < ngrp;) {
+    const int g1 = gi + NWT;
     if (g1 < ngrp) load(g1, eB, fB, xB);
     compute(gi, eA, fA, xA);
     if (g1 >= ngrp) break;
-    const int g2 = g1 + NW;
+    const int g2 = g1 + NWT;
     if (g2 < ngrp) load(g2, eA, fA, xA);
     compute(g1, eB, fB, xB);
     gi = g2;
   }
   // positions past the last group: de = 0, dcov passes through
-  for (int p = 4 * ngrp + tid; p < T; p += NT) {
+  for (int p = 4 * ngrp + tid; pt == 0 && p < T; p += NT) {
     de_out[rb + p] = 0.f;
     if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
   }
@@ -385,11 +390,12 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
       *reinterpret_cast<float2*>(&part[wid][kb * 512 + lane * 8 + 2 * jp]) =
           make_float2(acc[kb][jp].x, acc[kb][jp].y);
   __syncthreads();
+  float* dsp = pt ? ds1 : ds;
   for (int k = tid; k < A; k += NT) {
     float x = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) x += part[w][k];
-    ds[(size_t)b * A + k] = 4.f * v[k] * x;
+    dsp[(size_t)b * A + k] = 4.f * v[k] * x;
   }
 }
 
@@ -415,10 +421,11 @@ void launch_attn_fwd_row(const bf16* F, const bf16* E, float* s, const bf16* sc,
 void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
                          const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
                          const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                         float* dcov_out, int B, int T, int A, hipStream_t st) {
+                         float* dcov_out, int B, int T, int A, float* ds1, hipStream_t st) {
+  const int nb = ds1 ? 2 * B : B;
 #define LB(NK)                                                                                                \
-  hipLaunchKernelGGL((attn_bwd_row_kernel<NK, row_waves<NK, true>()>), dim3(B), dim3(row_waves<NK, true>() * 64), \
-                     0, st, E, F, s, v, wc, cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T)
+  hipLaunchKernelGGL((attn_bwd_row_kernel<NK, row_waves<NK, true>()>), dim3(nb), dim3(row_waves<NK, true>() * 64), \
+                     0, st, E, F, s, v, wc, cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, ds1)
   if (A == 512) LB(1);
   else LB(2);
 #undef LB

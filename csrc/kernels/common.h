@@ -44,6 +44,16 @@ __device__ __forceinline__ bf16x8 ld8f(const float* p) {
   return r;
 }
 
+// the same for the sum of two fp32 partials p + q
+__device__ __forceinline__ bf16x8 ld8f2(const float* p, const float* q) {
+  const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
+  const float4 u = *reinterpret_cast<const float4*>(q), w = *reinterpret_cast<const float4*>(q + 4);
+  bf16x8 r;
+  r[0] = f2bf(x.x + u.x); r[1] = f2bf(x.y + u.y); r[2] = f2bf(x.z + u.z); r[3] = f2bf(x.w + u.w);
+  r[4] = f2bf(y.x + w.x); r[5] = f2bf(y.y + w.y); r[6] = f2bf(y.z + w.z); r[7] = f2bf(y.w + w.w);
+  return r;
+}
+
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 z;
 #pragma unroll

@@ -218,9 +218,11 @@ __global__ __launch_bounds__(256) void pgen_dirs_kernel(const float* __restrict_
 // Backward of s-projection + LSTM cell for step t.  grid (H/16, ceil(B/16)).
 //   dc_t = ds . W_s[0:H]^T + dC_dir + dc_carry ;  dh_t = ds . W_s[H:2H]^T + dH_dir + dh_rec
 //   cell backward -> dz_t (bf16), dc_carry <- dc_total * f
-// ds (fp32 [B][A]) was accumulated by attn_bwd_tanh's blocks with atomics.
+// ds (fp32 [B][A]) was accumulated by attn_bwd_tanh's blocks with atomics, or stored by
+// attn_bwd_row -- as two partials ds + ds2 when that kernel runs two workgroups per row.
 __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
-    const float* __restrict__ ds, const bf16* __restrict__ Ws,                 // Ws: [2H][A] (TF Matrix)
+    const float* __restrict__ ds, const float* __restrict__ ds2,
+    const bf16* __restrict__ Ws,                                               // Ws: [2H][A] (TF Matrix)
     const float* __restrict__ dC_dir, const float* __restrict__ dH_dir,       // [B][H] (nullable)
     const float* __restrict__ dh_rec, float* __restrict__ dc_carry,            // [B][H]
     const float* __restrict__ act, const float* __restrict__ c_now, const float* __restrict__ c_prev,
@@ -246,12 +248,13 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
   const int ar = min(r0 + (lane & 15), B - 1);
   const int kof = 8 * (lane >> 4);
   const float* arow = ds + (size_t)ar * A + kof;
+  const float* arow2 = ds2 ? ds2 + (size_t)ar * A + kof : arow;
   const bf16* bc = Ws + (size_t)(u0 + (lane & 15)) * A + kof;
   const bf16* bh = Ws + (size_t)(H + u0 + (lane & 15)) * A + kof;
   const int nst = A / 32;
   const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
   f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
-  kslice_mma<2>([&](int k) { return ld8f(arow + k); },
+  kslice_mma<2>([&](int k) { return ds2 ? ld8f2(arow + k, arow2 + k) : ld8f(arow + k); },
                 [&](int j, int k) { return ld8((j == 0 ? bc : bh) + k); }, k0, k1, acc);
   float o[2];
   ksplit_reduce<2>(acc, red, o);
@@ -363,11 +366,11 @@ void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x
                  float* pg, int R, int A, int H, int E, hipStream_t st) {
   hipLaunchKernelGGL(pgen_kernel, dim3((R + 3) / 4), dim3(256), 0, st, ctx, c, h, x, w, b, pg, R, A, H, E);
 }
-void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
+void launch_dec_bwd_cell(const float* ds, const float* ds2, const bf16* Ws, const float* dC_dir, const float* dH_dir,
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,
                          const float* c_prev, bf16* dz, int B, int H, int A, hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16);
-  hipLaunchKernelGGL(dec_bwd_cell_kernel, grid, dim3(256), 0, st, ds, Ws, dC_dir, dH_dir, dh_rec, dc_carry, act,
+  hipLaunchKernelGGL(dec_bwd_cell_kernel, grid, dim3(256), 0, st, ds, ds2, Ws, dC_dir, dH_dir, dh_rec, dc_carry, act,
                      c_now, c_prev, dz, B, H, A);
 }
 void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, const float* dCTX_dir_prev,

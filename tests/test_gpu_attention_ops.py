@@ -129,3 +129,36 @@ def test_attn_fwd_row_sproj_matches_fp32(A, B):
     for name, got, ref in checks:
         err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         assert err < 2e-3, (name, err)
+
+
+@pytest.mark.parametrize("parts", [1, 2])
+def test_attn_bwd_row_matches_fp32(parts):
+    """attn_bwd_row (one workgroup per row, or two with partial ds in ds / ds1) against the fp32
+    reference of the fused attention backward step, A = 512; lens of 1, a few and T."""
+    k = ops()
+    B, T, A = 6, 300, 512
+    gen = torch.Generator(device="cuda").manual_seed(77 + parts)
+    dev = "cuda"
+
+    def r(*shape, s=1.0):
+        return torch.randn(*shape, generator=gen, device=dev) * s
+
+    lens = torch.tensor([T, 1, 5, 129, 257, 300], dtype=torch.int32, device=dev)
+    mask = torch.arange(T, device=dev)[None, :] < lens[:, None].long()
+    E, F = r(B, T, A, s=0.5).bfloat16(), r(B, T, A, s=0.5).bfloat16()
+    s, v, wc = r(B, A, s=0.3), r(A, s=0.1), r(A, s=0.1)
+    cov = torch.rand(B, T, generator=gen, device=dev) * mask
+    a = torch.softmax(r(B, T).masked_fill(~mask, float("-inf")), -1)
+    ctx = torch.einsum("bt,bta->ba", a, E.float())
+    dctx, Ga, dnext = r(B, A, s=0.1), r(B, T, s=0.1), r(B, T, s=0.1)
+    g = torch.full((B,), 0.7, device=dev)
+    de, dcov = torch.full((B, T), float("nan"), device=dev), torch.full((B, T), float("nan"), device=dev)
+    ds, ds1 = torch.full((B, A), float("nan"), device=dev), torch.full((B, A), float("nan"), device=dev)
+    k.attn_bwd_row(E, F, s, v, wc, cov, a, dctx, ctx, Ga, dnext, g, lens, de, ds, dcov, B, T, A,
+                   ds1 if parts == 2 else None)
+    torch.cuda.synchronize()
+    got_ds = ds + ds1 if parts == 2 else ds
+    want = _reference(E, F, s, v, wc, cov, a, dctx, Ga, dnext, g, lens)
+    for name, got, ref in zip(("de", "ds", "dcov"), (de, got_ds, dcov), want):
+        err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        assert err < 2e-3, (name, err)

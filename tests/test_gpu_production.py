@@ -158,6 +158,27 @@ def test_row_split_streams_match_single_chain(monkeypatch, split):
     assert _rel(got[1][2], got[0][2]) < 1e-4
 
 
+def test_two_workgroup_attention_backward_matches(monkeypatch):
+    """TSAMD_ATTN_BWD_PARTS=2 (attn_bwd_row with two workgroups per row, partial ds summed by
+    dec_bwd_cell and after the loop) gives the gradients of the one-workgroup kernel."""
+    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
+    B = 256
+    hps = _hps(B, trunc_norm_init_std=0.05).replace(max_dec_steps=24)
+    vocab, (batch,) = _batches(hps, 1, seed=16)
+    got = []
+    for parts in ("1", "2"):
+        monkeypatch.setenv("TSAMD_ATTN_BWD_PARTS", parts)
+        params = build_params(hps, vocab.size(), device="cuda", seed=7).enable_grad()
+        eng = HipPointerGenerator(hps, vocab.size(), params, B=B, T=T, D=24)
+        assert eng.row_attn_bwd and eng.attn_bwd_parts == int(parts)
+        eng.set_batch(batch)
+        eng.forward(need_grad=True)
+        eng.backward()
+        torch.cuda.synchronize()
+        got.append(params.grad.clone())
+    assert _rel(got[1], got[0]) < 1e-4, _rel(got[1], got[0])
+
+
 def test_deferred_weight_gradients_match_inline(monkeypatch):
     """The decoder-side weight gradients deferred onto a side stream beside the encoder BPTT
     (TSAMD_DEFER_WGRAD, default on; with the opt-in TSAMD_DEFER_VOCAB_DW the vocab dW too) give

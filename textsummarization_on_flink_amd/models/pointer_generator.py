@@ -287,6 +287,13 @@ class HipPointerGenerator:
         # hides too little latency -- config #5 decoder backward 79 ms vs 59 ms with the
         # multi-block attn_bwd_step (tools/phase_micro.py) -- so it is used at A = 512 only
         self.row_attn_bwd = self.row_attn and (A == 512 or ra == "1")
+        # attn_bwd_row with two workgroups per row (opt-in TSAMD_ATTN_BWD_PARTS=2): a row's chain of
+        # position groups is dealt over 2 x 12 waves on two CUs; partial ds summed by dec_bwd_cell.
+        # Measured slower at B = 256 (19.58-19.63 -> 20.46-20.56 ms,
+        # profiles/r2/ab/attn_bwd_two_wg_rejected.jsonl): the loop is bound by the chip's VALU /
+        # transcendental issue over all rows, not by one row's chain, so a split only adds the
+        # per-workgroup prologue (S) and epilogue
+        self.attn_bwd_parts = 2 if os.environ.get("TSAMD_ATTN_BWD_PARTS", "1") == "2" else 1
         # TSAMD_FUSED_SPROJ=1 (opt-in): the attention query projection s = [c, h] . W_s + b inside
         # the row forward kernel instead of its own linear2 launch.  Measured slower
         # (profiles/r2/ab/fused_sproj_rejected.jsonl): B = 256 19.7-19.8 -> 21.0-21.1 ms, config #5
@@ -348,6 +355,7 @@ class HipPointerGenerator:
         w["DX"] = z(D, B, E)
         w["DZ"] = z(D, B, 4 * H, dt=BF)
         w["DS"] = z(D, B, A)
+        w["DS2"] = z(D, B, A) if (self.row_attn_bwd and self.attn_bwd_parts == 2) else None
         w["d_emb_dec"] = z(D * B, E)  # decoder-input embedding gradient rows
         w["out_f32"] = z(D * B, H)  # output projection [h, ctx] . W_o + b (fp32, before the bf16 copy)
         if self.hps.pointer_gen:  # p_gen direct terms of the decoder backward (pgen_dirs)
@@ -800,6 +808,7 @@ class HipPointerGenerator:
         if not self.row_attn_bwd:
             w["DS"].zero_()  # accumulated with atomics by the multi-block kernels (the row kernel stores)
         Ga = w["dA"] if hps.pointer_gen else None
+        ds2 = w["DS2"] if self.row_attn_bwd and self.attn_bwd_parts == 2 else None
         def chain(r0, r1):
             Bg, rs = r1 - r0, slice(r0, r1)
             for t in reversed(range(D)):
@@ -810,7 +819,7 @@ class HipPointerGenerator:
                 if self.row_attn_bwd:
                     k.attn_bwd_row(enc_out[rs], F[rs], w["S"][t][rs], v, wc, cov_t, w["ATT"][t][rs], w["DCTX"][t][rs],
                                    w["CTX"][t][rs], ga_t, dcov_next, gcl_t, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
-                                   dcov[t % 2][rs] if cov else None, Bg, T, A)
+                                   dcov[t % 2][rs] if cov else None, Bg, T, A, ds2[t][rs] if ds2 is not None else None)
                 elif self.fused_attn_bwd:
                     k.attn_bwd_step(enc_out[rs], F[rs], w["S"][t][rs], v, wc, cov_t, w["ATT"][t][rs], w["DCTX"][t][rs],
                                     w["CTX"][t][rs], ga_t, dcov_next, gcl_t, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
@@ -823,12 +832,14 @@ class HipPointerGenerator:
                                     A)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
-                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A)
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, ds2[t][rs] if ds2 is not None else None)
                 k.dec_bwd_dz(w["DZ"][t][rs], self.pk["Wbig"], dX_dir[t][rs] if dX_dir is not None else None,
                              dCTX_dir[t - 1][rs] if t > 0 else None, w["DX"][t][rs],
                              w["DCTX"][t - 1][rs] if t > 0 else None, w["dh_rec"][rs], Bg, E, H, A)
 
         self._row_groups(chain, self.split_bwd)
+        if ds2 is not None:  # the two per-row partials of ds, for the weight gradients below
+            w["DS"].add_(ds2)
         # ---- decoder weight gradients (one GEMM each over all D*B rows)
         emb_dec = self._emb_dec
 
