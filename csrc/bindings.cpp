@@ -607,33 +607,34 @@ void vocab_topk_pg(const Tensor& X, const Tensor& WT, const Tensor& bias, const 
 int64_t vocab_topk_parts(int64_t V) { return vocab_topk_tiles((int)V); }
 
 
-// Advances step[0] by one (the last block to finish); ctr: one zeroed uint32 scratch word.
+// Advances step[0] by one (the last block to finish) when ctr (one zeroed uint32 scratch word)
+// is given; without ctr, beam_gather advanced it at the start of the decode step (t = step - 1).
 // att/att_hist/pg/pg_hist (optional): this step's attention rows and p_gen copied into row
 // min(step, max_dec - 1) of the histories.
 void beam_step(const Tensor& top_ids, const Tensor& top_lp, const Tensor& lp_sum, const Tensor& latest,
                const Tensor& gidx, const Tensor& tok_hist, const Tensor& par_hist, const Tensor& done,
                const Tensor& res_count, const Tensor& res_score, const Tensor& res_len, const Tensor& res_step,
-               const Tensor& res_par, const Tensor& step, const Tensor& ctr, const OT& att, const OT& att_hist,
+               const Tensor& res_par, const Tensor& step, const OT& ctr, const OT& att, const OT& att_hist,
                const OT& pg, const OT& pg_hist, int64_t T, int64_t Na, int64_t beam, int64_t K, int64_t stop_id,
                int64_t min_dec, int64_t max_dec) {
   chk(top_ids, I32, "top_ids"); chk(top_lp, F32, "top_lp"); chk(lp_sum, F32, "lp_sum"); chk(latest, I32, "latest");
   chk(gidx, I32, "gidx"); chk(tok_hist, I32, "tok_hist"); chk(par_hist, I32, "par_hist"); chk(done, I32, "done");
   chk(res_count, I32, "res_count"); chk(res_score, F32, "res_score"); chk(res_len, I32, "res_len");
-  chk(res_step, I32, "res_step"); chk(res_par, I32, "res_par"); chk(step, I32, "step"); chk(ctr, I32, "ctr");
+  chk(res_step, I32, "res_step"); chk(res_par, I32, "res_par"); chk(step, I32, "step"); chko(ctr, I32, 1, "ctr");
   const int64_t R = Na * beam;
   TORCH_CHECK(beam >= 1 && beam <= 16 && K >= 1 && K <= 16 && beam * K <= 64, "bad beam args");
   numel_eq(top_ids, R * K, "top_ids"); numel_eq(top_lp, R * K, "top_lp"); numel_eq(lp_sum, R, "lp_sum");
   numel_eq(latest, R, "latest"); numel_eq(gidx, R, "gidx"); numel_eq(tok_hist, max_dec * R, "tok_hist");
   numel_eq(par_hist, max_dec * R, "par_hist"); numel_eq(done, Na, "done"); numel_eq(res_count, Na, "res_count");
   numel_eq(res_score, R, "res_score"); numel_eq(res_len, R, "res_len"); numel_eq(res_step, R, "res_step");
-  numel_eq(res_par, R, "res_par"); numel_eq(step, 1, "step"); numel_eq(ctr, 1, "ctr");
+  numel_eq(res_par, R, "res_par"); numel_eq(step, 1, "step");
   TORCH_CHECK(att.has_value() == att_hist.has_value() && pg.has_value() == pg_hist.has_value() &&
               (!pg.has_value() || att.has_value()), "att/att_hist and pg/pg_hist come in pairs (pg needs att)");
   chko(att, F32, R * T, "att"); chko(att_hist, F32, max_dec * R * T, "att_hist");
   chko(pg, F32, R, "pg"); chko(pg_hist, F32, max_dec * R, "pg_hist");
   launch_beam_step(P<int>(top_ids), P<float>(top_lp), P<float>(lp_sum), P<int>(latest), P<int>(gidx), P<int>(tok_hist),
                    P<int>(par_hist), P<int>(done), P<int>(res_count), P<float>(res_score), P<int>(res_len),
-                   P<int>(res_step), P<int>(res_par), P<int>(step), (unsigned*)ctr.data_ptr(), PO<float>(att),
+                   P<int>(res_step), P<int>(res_par), P<int>(step), (unsigned*)PO<int>(ctr), PO<float>(att),
                    PO<float>(att_hist), PO<float>(pg), PO<float>(pg_hist), (int)T, Na, beam, K, stop_id, min_dec,
                    max_dec, stream());
 }
@@ -642,7 +643,8 @@ void beam_gather(const Tensor& gidx, const Tensor& latest, const Tensor& c_src, 
                  const Tensor& ctx_src, const Tensor& a_src, const OT& cov_src, const Tensor& XGtab, const Tensor& Xtab,
                  const Tensor& c_out, const Tensor& h_out, const Tensor& ctx_out, const Tensor& ctxb_out,
                  const OT& cov_out, const Tensor& XG_out, const Tensor& x_out, int64_t R, int64_t H, int64_t A,
-                 int64_t T, int64_t E, int64_t V, int64_t unk) {
+                 int64_t T, int64_t E, int64_t V, int64_t unk, const OT& step) {
+  chko(step, I32, 1, "step");  // optional decode-step counter advanced by this launch
   chk(gidx, I32, "gidx"); chk(latest, I32, "latest"); chk(c_src, F32, "c_src"); chk(h_src, BF, "h_src");
   chk(ctx_src, F32, "ctx_src"); chk(a_src, F32, "a_src"); chk(XGtab, F32, "XGtab"); chk(Xtab, F32, "Xtab");
   chk(c_out, F32, "c_out"); chk(h_out, BF, "h_out"); chk(ctx_out, F32, "ctx_out"); chk(ctxb_out, BF, "ctxb_out");
@@ -657,7 +659,7 @@ void beam_gather(const Tensor& gidx, const Tensor& latest, const Tensor& c_src, 
   launch_beam_gather(P<int>(gidx), P<int>(latest), P<float>(c_src), P<bf16>(h_src), P<float>(ctx_src), P<float>(a_src),
                      PO<float>(cov_src), P<float>(XGtab), P<float>(Xtab), P<float>(c_out), P<bf16>(h_out),
                      P<float>(ctx_out), P<bf16>(ctxb_out), PO<float>(cov_out), P<float>(XG_out), P<float>(x_out), R, H,
-                     A, T, E, V, unk, stream());
+                     A, T, E, V, unk, PO<int>(step), stream());
 }
 
 void linear2(const Tensor& a1, int64_t K1, const OT& a2, int64_t K2, const Tensor& Wt, const OT& bias, const OT& add,

@@ -347,7 +347,8 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
   // one memory round trip for everything the bookkeeping reads: the step counter, the done
   // flag, the result count and this lane's candidate (rows of step t > 0; at t == 0 only row
   // base's K candidates are used and the others are masked in the body)
-  const int t = *step;
+  // ctr == nullptr: beam_gather advanced the counter at the start of this decode step
+  const int t = ctr ? *step : *step - 1;
   const int is_done = done[a], nres0 = res_count[a];
   float tot = -INFINITY;
   int tid_cand = 0;
@@ -368,8 +369,10 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
                    res_step, res_par, cval, cid, srt, a, lane, t, base, beam, K, stop_id, min_dec, tot, tid_cand,
                    nres0);
   }
-  // grid-wide step advance: every block read *step above; the last one to arrive bumps it
-  if (lane == 0) {
+  // grid-wide step advance (standalone use): every block read *step above; the last one to
+  // arrive bumps it -- a fence plus one same-address atomic per article (64 serialised L2
+  // atomics at 64 articles), which the decoder avoids by letting beam_gather advance it
+  if (ctr && lane == 0) {
     __threadfence();
     if (atomicAdd(ctr, 1u) == gridDim.x - 1) {
       *step = t + 1;
@@ -392,8 +395,11 @@ __global__ __launch_bounds__(256) void beam_gather_kernel(
     const float* __restrict__ XGtab, const float* __restrict__ Xtab,
     float* __restrict__ c_out, bf16* __restrict__ h_out, float* __restrict__ ctx_out, bf16* __restrict__ ctxb_out,
     float* __restrict__ cov_out, float* __restrict__ XG_out, float* __restrict__ x_out,
-    int H, int A, int T, int E, int V, int unk) {
+    int H, int A, int T, int E, int V, int unk, int* __restrict__ step) {
   const int r = blockIdx.x, tid = threadIdx.x;
+  // step (optional): the decode-step counter, advanced here -- one plain store by one thread,
+  // the kernel boundary orders it before this step's beam_step (which then reads t = step - 1)
+  if (step && r == 0 && tid == 0) *step += 1;
   const int g = (int)DCHECK_IDX(gidx[r], 0, (int)gridDim.x, CHK_BEAM_PARENT);
   int tok = (int)DCHECK_IDX(latest[r], 0, 0x7fffffff, CHK_BEAM_TOKEN);
   tok = tok < V ? tok : unk;
@@ -416,10 +422,10 @@ void launch_beam_gather(const int* gidx, const int* latest, const float* c_src, 
                         const float* ctx_src, const float* a_src, const float* cov_src, const float* XGtab,
                         const float* Xtab, float* c_out, bf16* h_out, float* ctx_out, bf16* ctxb_out, float* cov_out,
                         float* XG_out, float* x_out, int R, int H, int A, int T, int E, int V, int unk,
-                        hipStream_t st) {
+                        int* step, hipStream_t st) {
   hipLaunchKernelGGL(beam_gather_kernel, dim3(R), dim3(256), 0, st, gidx, latest, c_src, h_src, ctx_src, a_src,
                      cov_src, XGtab, Xtab, c_out, h_out, ctx_out, ctxb_out, cov_out, XG_out, x_out, H, A, T, E, V,
-                     unk);
+                     unk, step);
 }
 
 int topk_split(int V) { return (V + TOPK_THREADS * PER_THREAD - 1) / (TOPK_THREADS * PER_THREAD); }

@@ -77,7 +77,7 @@ void launch_beam_gather(const int* gidx, const int* latest, const float* c_src, 
                         const float* ctx_src, const float* a_src, const float* cov_src, const float* XGtab,
                         const float* Xtab, float* c_out, bf16* h_out, float* ctx_out, bf16* ctxb_out, float* cov_out,
                         float* XG_out, float* x_out, int R, int H, int A, int T, int E, int V, int unk,
-                        hipStream_t st);
+                        int* step, hipStream_t st);
 void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
                     const float* add, float* out, bf16* outb, int B, int N, hipStream_t st);
 void launch_linear2_pair(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,

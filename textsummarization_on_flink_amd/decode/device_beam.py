@@ -175,7 +175,7 @@ class DeviceBeamDecoder:
         cov = hps.coverage
         k.beam_gather(b["gidx"], b["latest"], X["C"], X["H"], X["CTX"], X["ATT"], X["COV"] if cov else None,
                       self.XGtab, self.Xtab, b["c"], b["h"], b["ctxs"], b["ctxs_bf"], Y["COV"] if cov else None,
-                      b["XG"], b["x"], R, H, A, T, E, V, self.vocab.word2id(UNKNOWN_TOKEN))
+                      b["XG"], b["x"], R, H, A, T, E, V, self.vocab.word2id(UNKNOWN_TOKEN), b["step"])
         k.dec_cell_fwd(b["XG"], b["ctxs_bf"], b["h"], b["c"], eng.pk["WcT2"], Y["C"], b["Cb2"], Y["H"], b["act"],
                        R, H, A)
         if hps.pointer_gen:
@@ -202,11 +202,12 @@ class DeviceBeamDecoder:
             torch.mm(b["outb"], eng.pk["ow"], out_dtype=F32, out=b["logits"])
             k.final_topk(b["logits"], p[OV], pg, Y["ATT"] if hps.pointer_gen else None, b["ext"], b["lens"],
                          b["top_ids"], b["top_lp"], b["part_ms"], b["part_v"], b["part_i"], R, V, T, K, self.beam)
-        # beam bookkeeping; also appends a_t / p_gen to the histories and advances b["step"]
+        # beam bookkeeping; also appends a_t / p_gen to the histories (b["step"] was advanced by
+        # this step's beam_gather: no grid-wide counter here)
         hist = self.keep_attn
         k.beam_step(b["top_ids"], b["top_lp"], b["lp_sum"], b["latest"], b["gidx"], b["tok_hist"], b["par_hist"],
                     b["done"], b["res_count"], b["res_score"], b["res_len"], b["res_step"], b["res_par"], b["step"],
-                    b["step_ctr"], Y["ATT"] if hist else None, b["ATT_hist"] if hist else None,
+                    None, Y["ATT"] if hist else None, b["ATT_hist"] if hist else None,
                     pg if (hist and pg is not None) else None, b["PG_hist"] if (hist and pg is not None) else None,
                     T, self.Na, self.beam, K, self.vocab.word2id(STOP_DECODING), hps.min_dec_steps, self.maxD)
 
