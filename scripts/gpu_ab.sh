@@ -4,6 +4,9 @@
 #   cfg5      attention tests + config #5 bench, default vs TSAMD_ATTN_P4K2=0
 #   cfg5prof  rocprofv3 kernel stats of the config #5 bench
 #   decode    bench_decode with $AB_ENV = 1 / 0 at 64 and 128 articles, twice
+#   train     GPU tests matching $AB_K, then the B = 256 train bench for each $AB_ENV value in
+#             $AB_VALUES (default "1 0 1 0"), and config #5 at B = 512 too when AB_CFG5=1
+#             (e.g. AB_ENV=TSAMD_DEC_KB AB_K="model or decode" bash scripts/gpu_ab.sh train)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -32,5 +35,24 @@ decode)
     env $AB_ENV=$v timeout -k 10 200 python bench_decode.py --articles $a --batches 10 --warmup 2 > $L 2>&1 || { tail -20 $L; exit 1; }
     echo "$AB_ENV=$v articles=$a $(python -c "import json;d=json.loads(open('$L').read().strip().splitlines()[-1]);print(d['value'], d.get('ms_per_batch'))")"
   done; done; done ;;
+train)
+  if [ -n "$AB_K" ]; then
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$AB_K" \
+      > $OUT/pytest.log 2>&1
+    rc=$?; tail -3 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
+  fi
+  j() { python -c "import json;d=json.loads(open('$1').read().strip().splitlines()[-1]);print('$2', d['ms_per_step'], d['value'])"; }
+  i=0
+  for v in ${AB_VALUES:-1 0 1 0}; do
+    i=$((i+1))
+    env $AB_ENV=$v timeout -k 10 300 python bench.py --decode-batches 0 --steps 40 --warmup 5 > $OUT/b$i.log 2>&1 \
+      || { tail -20 $OUT/b$i.log; exit 1; }
+    j $OUT/b$i.log "B=256 $AB_ENV=$v"
+    if [ -n "$AB_CFG5" ]; then
+      env $AB_ENV=$v timeout -k 10 300 python bench.py --hidden 512 --layers 2 --enc 800 --batch 512 --steps 4 \
+        --warmup 1 --decode-batches 0 > $OUT/c$i.log 2>&1 || { tail -20 $OUT/c$i.log; exit 1; }
+      j $OUT/c$i.log "cfg5 B=512 $AB_ENV=$v"
+    fi
+  done ;;
 *) echo "unknown: $1"; exit 2 ;;
 esac
