@@ -155,3 +155,42 @@ def test_dead_rank_surfaces_and_training_restarts_from_latest(tmp_path):
     with um.patch("torch.cuda.is_available", lambda: False):
         assert cli.main([f for f in flags if not f.startswith("--fault_kill")] + ["--num_steps=2"]) == 0
     assert ckpt.latest_checkpoint(f"{tmp_path}/log/exp/train").endswith("model.ckpt-3")
+
+
+def _cli_rank_report(rank, world, port, q, flags):
+    """One CLI training rank that reports its parameter checksum and global step at the end."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    from textsummarization_on_flink_amd.train import loop
+    seen = {}
+    orig = loop.run_training
+
+    def spy(trainer, *a, **k):
+        seen["start"] = trainer.global_step
+        out = orig(trainer, *a, **k)
+        seen["end"] = trainer.global_step
+        seen["sum"] = float(trainer.params.flat.double().sum())
+        return out
+    loop.run_training = spy
+    from textsummarization_on_flink_amd import cli
+    cli.main(flags)
+    q.put((rank, seen))
+
+
+def test_dp_checkpoint_saved_on_rank0_resumes_on_all_ranks(tmp_path):
+    """SURVEY 4 distributed tier: a 2-rank job checkpoints on rank 0 only; a relaunched 2-rank job
+    resumes every rank from that checkpoint (same start step, identical parameters after the
+    resumed steps)."""
+    from helpers import TINY_FLAGS, make_dataset
+    from textsummarization_on_flink_amd.train import checkpoint as ckpt
+    d, vp, _ = make_dataset(str(tmp_path))
+    flags = [f"--data_path={d}/train_*", f"--vocab_path={vp}", f"--log_root={tmp_path}/log", "--exp_name=exp",
+             *TINY_FLAGS, "--mode=train", "--num_steps=2"]
+    first = _spawn(_cli_rank_report, 2, flags)
+    assert first[0][0]["start"] == first[1][0]["start"] == 0
+    assert ckpt.latest_checkpoint(f"{tmp_path}/log/exp/train").endswith("model.ckpt-2")
+    second = _spawn(_cli_rank_report, 2, flags)
+    assert second[0][0]["start"] == second[1][0]["start"] == 2  # both ranks resumed from rank 0's checkpoint
+    assert second[0][0]["end"] == second[1][0]["end"] == 4
+    assert second[0][0]["sum"] == second[1][0]["sum"]  # the ranks stay identical
+    assert ckpt.latest_checkpoint(f"{tmp_path}/log/exp/train").endswith("model.ckpt-4")

@@ -73,6 +73,17 @@ def broadcast_params(flat: torch.Tensor, info: DistInfo) -> None:
         dist.broadcast(flat, src=0)
 
 
+def broadcast_scalar(x: int, info: DistInfo, device=None) -> int:
+    """Rank 0's value of an integer (e.g. the restored global step) on every rank."""
+    if not info.enabled:
+        return int(x)
+    if device is None:
+        device = f"cuda:{info.local_rank}" if info.backend == "nccl" else "cpu"
+    t = torch.tensor([int(x)], dtype=torch.int64, device=device)
+    dist.broadcast(t, src=0)
+    return int(t.item())
+
+
 class GradAllReducer:
     """Bucketed sum (or average) of a flat gradient buffer.
 

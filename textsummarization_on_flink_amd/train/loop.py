@@ -29,7 +29,7 @@ from typing import Dict, Optional
 
 import torch
 
-from ..parallel.dist import DistInfo, all_reduce_scalar, barrier
+from ..parallel.dist import DistInfo, all_reduce_scalar, barrier, broadcast_params, broadcast_scalar
 from ..utils.debug import NonFiniteWatch
 from . import checkpoint as ckpt
 from .trainer import NonFiniteLossError
@@ -196,6 +196,15 @@ def setup_training(hps, vocab, batcher, info: Optional[DistInfo] = None, metrics
         if hasattr(trainer, "engine"):
             trainer.engine.pack()
         log.info("Restored %s at step %d", latest, trainer.global_step)
+    if info.enabled:
+        # resume on every rank from the chief's state: rank 0 wrote the checkpoints, so its
+        # restore is authoritative even where another rank cannot see (or sees an older) file
+        broadcast_params(trainer.params.flat, info)
+        if trainer.params.accum is not None:
+            broadcast_params(trainer.params.accum, info)
+        trainer.global_step = broadcast_scalar(trainer.global_step, info, trainer.params.flat.device)
+        if hasattr(trainer, "engine"):
+            trainer.engine.pack()
     saver = ckpt.Saver(train_dir, max_to_keep=hps.max_to_keep) if info.is_chief else None
     if info.is_chief:
         write_embedding_projector(train_dir, vocab)
