@@ -188,7 +188,11 @@ class HipPointerGenerator:
         # current stream, so a captured hipGraph holds parallel branches): one group's small
         # latency-bound cell kernels run beside another group's bandwidth-bound attention
         # kernels instead of serialising behind them.  TSAMD_SPLIT overrides (1 = one chain).
-        sp = int(os.environ.get("TSAMD_SPLIT", "0")) or (2 if B >= 128 and B % 32 == 0 else 1)
+        # Default: 2 groups from B = 128, 4 from B = 512 (config #5, H = 512: B = 512 161.6 -> 156.9 ms
+        # per step, B = 1024 309.0 -> 301.1-301.9 ms; 8 groups 303.2; B = 256: 2 and 4 equal within
+        # noise, 19.64 / 19.71 ms; profiles/r2/ab/split_groups.jsonl)
+        sp = int(os.environ.get("TSAMD_SPLIT", "0")) or (4 if B >= 512 and B % 64 == 0 else
+                                                         2 if B >= 128 and B % 32 == 0 else 1)
         self.split = sp if (sp > 1 and B % (16 * sp) == 0) else 1
         # TSAMD_SPLIT_BWD: the decoder backward loop's own group count (default: split; at B = 256
         # 2 groups 19.59-19.62 ms per step, 1 group 20.02-20.07, 4 groups 20.09:
