@@ -723,7 +723,11 @@ class HipPointerGenerator:
 
         def dw():
             Sw = self.dw_split
-            if m == H and Sw > 1 and N % Sw == 0:
+            # keep the batched operand's batch stride (N / Sw rows of dlogits) below 2^31
+            # elements: the library's strided-batched path is not trusted past 32-bit strides
+            while Sw > 1 and (N // Sw) * V >= 2 ** 31 and N % (2 * Sw) == 0:
+                Sw *= 2
+            if m == H and Sw > 1 and N % Sw == 0 and (N // Sw) * V < 2 ** 31:
                 # split K = N in Sw = 4 (one batched GEMM + a sum): 0.82 -> 0.74 ms at B = 256
                 xe = w["outb_ext"].view(Sw, N // Sw, H + 8)[:, :, :H]
                 parts = torch.bmm(xe.transpose(1, 2), dl.view(Sw, N // Sw, V), out_dtype=F32)
