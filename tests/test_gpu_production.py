@@ -213,3 +213,13 @@ def test_deferred_weight_gradients_match_inline(monkeypatch):
         got.append((eager, params.grad.clone()))
     for a, b in ((got[0][0], got[1][0]), (got[0][0], got[1][1]), (got[0][0], got[0][1])):
         assert _rel(b, a) < 1e-5, _rel(b, a)
+
+
+def test_unverified_huge_shape_refused():
+    """Shapes past the verified per-GPU envelope (config #5 at batch 2048 faulted the device)
+    are refused with a ValueError before anything is allocated or launched."""
+    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
+    hps = _hps(8).replace(hidden_dim=512, enc_layers=2, max_enc_steps=800, max_dec_steps=100)
+    params = build_params(hps, V, device="cuda", seed=1)
+    with pytest.raises(ValueError, match="verified per-GPU envelope"):
+        HipPointerGenerator(hps, V, params, B=2048, T=800, D=100)

@@ -172,6 +172,16 @@ class HipPointerGenerator:
             raise ValueError("emb_dim and hidden_dim must be multiples of 32 for the MFMA kernels")
         if T > 2048:
             raise ValueError("max_enc_steps > 2048 not supported by the attention kernels")
+        # Verified envelope: per-GPU encoder activations B x T x A up to 2^30 elements (config #5
+        # at batch 1024: 0.84G).  Config #5 at batch 2048 (1.68G: the fp32 attention-input
+        # gradient alone is 6.7 GB) ended in a GPU memory-aperture fault on MI355X, cause not yet
+        # isolated -- refuse such shapes loudly instead of faulting the device (split the batch
+        # over more GPUs or steps).  TSAMD_UNVERIFIED_SHAPES=1 lifts the check for debugging.
+        # (the [D x B, V] logits / dlogits, 5.1G elements at batch 1024, likewise up to 2^33)
+        if os.environ.get("TSAMD_UNVERIFIED_SHAPES", "0") != "1" and (
+                B * T * self.A > 2 ** 30 or self.D * B * self.V > 2 ** 33):
+            raise ValueError(f"batch {B} x enc {T} x attention width {self.A} (or x dec {self.D} x vocab {self.V}) "
+                             "exceeds the verified per-GPU envelope; use a smaller per-GPU batch")
         self.k = _ops()
         self.grad_scale = 1.0  # set to 1/world by a data-parallel trainer (see optimizer_step)
         self.nchunk = int(self.k.attn_chunks(T))
