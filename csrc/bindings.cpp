@@ -258,13 +258,13 @@ int64_t attn_chunks(int64_t T) { return attn_nchunk(T); }
 void emb_grad_sorted(const Tensor& gemb, const Tensor& sid, const Tensor& perm, const Tensor& src0, const Tensor& src1) {
   chk(gemb, F32, "gemb"); chk(src0, F32, "src0"); chk(src1, F32, "src1");
   TORCH_CHECK(gemb.dim() == 2 && gemb.size(1) <= 512, "gemb must be [V][E], E <= 512");
-  TORCH_CHECK(sid.scalar_type() == at::kInt && perm.scalar_type() == at::kLong && sid.is_contiguous() &&
-              perm.is_contiguous() && sid.numel() == perm.numel(), "sid int32 / perm int64, contiguous, one length");
+  TORCH_CHECK(sid.scalar_type() == at::kInt && perm.scalar_type() == at::kInt && sid.is_contiguous() &&
+              perm.is_contiguous() && sid.numel() == perm.numel(), "sid / perm int32, contiguous, one length");
   const int64_t E = gemb.size(1), V = gemb.size(0);
   TORCH_CHECK(src0.numel() % E == 0 && src1.numel() % E == 0, "src rows");
   const int64_t n0 = src0.numel() / E, n1 = src1.numel() / E;
   TORCH_CHECK(sid.numel() == n0 + n1, "sid must cover src0 and src1 rows");
-  launch_emb_grad_sorted(P<float>(gemb), P<int>(sid), P<int64_t>(perm), P<float>(src0), (int)n0, P<float>(src1),
+  launch_emb_grad_sorted(P<float>(gemb), P<int>(sid), P<int>(perm), P<float>(src0), (int)n0, P<float>(src1),
                          (int)n1, (int)E, (int)V, stream());
 }
 

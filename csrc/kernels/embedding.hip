@@ -40,7 +40,7 @@ void launch_emb_grad(float* gemb, const int64_t* ids0, const float* src0, int n0
 template <int PER>
 __global__ __launch_bounds__(256) void emb_grad_sorted_kernel(float* __restrict__ gemb,
                                                               const int* __restrict__ sid,
-                                                              const int64_t* __restrict__ perm,
+                                                              const int* __restrict__ perm,
                                                               const float* __restrict__ src0, int n0,
                                                               const float* __restrict__ src1, int n1, int E, int V) {
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void emb_grad_sorted_kernel(float* __restrict_
       const int r = min(rb + u, r1 - 1);
       idv[u] = rb + u < r1 ? sid[r] : -1;
       if (rb + u < r1) DCHECK_IN(idv[u], 0, V, CHK_EMB_ID);
-      const int64_t q = perm[r];
+      const int q = perm[r];
       const float* srow = q < n0 ? src0 + (size_t)q * E : src1 + (size_t)(q - n0) * E;
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void emb_grad_sorted_kernel(float* __restrict_
   }
 }
 
-void launch_emb_grad_sorted(float* gemb, const int* sid, const int64_t* perm, const float* src0, int n0,
+void launch_emb_grad_sorted(float* gemb, const int* sid, const int* perm, const float* src0, int n0,
                             const float* src1, int n1, int E, int V, hipStream_t st) {
   const int n = n0 + n1;
   if (n <= 0) return;

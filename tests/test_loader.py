@@ -76,3 +76,78 @@ def test_endless_mode_stops_promptly(tmp_path):
     procs = list(pb.procs)
     pb.stop()
     assert all(not p.is_alive() for p in procs)
+
+
+def _ref_inputs(pattern, vocab, hps):
+    return [tuple(Example(a, [s.strip() for s in abstract2sents(b)], vocab, hps).enc_input)
+            for a, b in binfmt.text_generator(binfmt.example_generator(pattern, True))]
+
+
+def test_dp_ranks_read_disjoint_shares(tmp_path):
+    """2 data-parallel ranks x 3 loader workers, single pass: every record is read exactly once
+    over the whole job (record k -> rank k % world -> worker (k // world) % workers)."""
+    d, vp, _ = make_dataset(str(tmp_path), n_files=3, per_file=7)
+    vocab = Vocab(vp, 500)
+    T, D, B = 48, 12, 2
+    hps = HParams(batch_size=B, max_enc_steps=T, max_dec_steps=D, vocab_size=500, pointer_gen=True, coverage=True)
+    pattern = f"{d}/train_*.bin"
+    layout, _ = input_layout(B, T, D)
+    per_rank = []
+    for rank in range(2):
+        got = []
+        for pb in ProcessBatcher(pattern, vocab, hps, single_pass=True, workers=3, seed=5, pad_enc_to=T,
+                                 rank=rank, world=2):
+            h = _unpack(pb, layout)
+            got += [tuple(int(x) for x in h["enc_batch"][r, :h["enc_lens"][r]]) for r in range(pb.n_valid)]
+        per_rank.append(got)
+    ref = _ref_inputs(pattern, vocab, hps)
+    assert len(per_rank[0]) == 11 and len(per_rank[1]) == 10  # 21 records: k % 2
+    assert sorted(per_rank[0] + per_rank[1]) == sorted(ref)
+
+
+def test_dp_ranks_threaded_batcher_disjoint(tmp_path):
+    from textsummarization_on_flink_amd.data.batcher import Batcher
+    d, vp, _ = make_dataset(str(tmp_path), n_files=2, per_file=9)
+    vocab = Vocab(vp, 500)
+    hps = HParams(batch_size=3, max_enc_steps=48, max_dec_steps=12, vocab_size=500)
+    pattern = f"{d}/train_*.bin"
+    got = []
+    for rank in range(3):
+        bt = Batcher(pattern, vocab, hps, single_pass=True, seed=11, rank=rank, world=3)
+        for b in bt:
+            got += [tuple(int(x) for x in b.enc_batch[r, :b.enc_lens[r]]) for r in range(int(b.valid.sum()))]
+        bt.stop()
+    assert sorted(got) == sorted(_ref_inputs(pattern, vocab, hps))
+
+
+def test_crashed_worker_is_not_end_of_data(tmp_path, monkeypatch):
+    """A worker that dies without delivering its error record (exit code 1, ring closed) makes
+    next_batch raise instead of silently dropping 1/n of the stream."""
+    import json as _json
+
+    import textsummarization_on_flink_amd.data.loader as L
+
+    class _Json:
+        loads = staticmethod(_json.loads)
+
+        @staticmethod
+        def dumps(obj, *a, **k):
+            if isinstance(obj, dict) and "error" in obj:
+                raise OSError("cannot report")
+            return _json.dumps(obj, *a, **k)
+
+    def boom(*a, **k):
+        raise IOError("disk gone")
+        yield  # noqa: unreachable -- generator
+
+    d, vp, _ = make_dataset(str(tmp_path), n_files=1, per_file=4)
+    monkeypatch.setattr(L, "json", _Json)
+    monkeypatch.setattr(L.binfmt, "example_generator", boom)  # inherited by the forked workers
+    hps = HParams(batch_size=2, max_enc_steps=32, max_dec_steps=8, vocab_size=500)
+    pb = ProcessBatcher(f"{d}/train_*.bin", Vocab(vp, 500), hps, single_pass=False, workers=2, seed=1,
+                        pad_enc_to=32, ring_bytes=1 << 20)
+    try:
+        with pytest.raises(RuntimeError, match="stopped|died"):
+            pb.next_batch(timeout=30)
+    finally:
+        pb.stop()

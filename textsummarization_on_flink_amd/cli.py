@@ -126,9 +126,11 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         # fork the loader workers before anything initialises the GPU (init_from_env does
         # under data parallelism); device_count() above does not
         from .data.loader import ProcessBatcher
-        rank = int(os.environ.get("RANK", "0"))
+        # rank-disjoint shares of the records: every rank uses the same seed (the shared
+        # file order) and reads the records k with k % WORLD_SIZE == RANK
+        rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
         loader = ProcessBatcher(hps.data_path, Vocab(hps.vocab_path, hps.vocab_size), hps,
-                                single_pass=hps.single_pass, workers=nw, seed=hps.seed + rank,
+                                single_pass=hps.single_pass, workers=nw, seed=hps.seed, rank=rank, world=world,
                                 pad_enc_to=hps.max_enc_steps)
     info = init_from_env(timeout_s=hps.dist_timeout_s) if hps.mode == "train" else DistInfo()
     vocab, hps = default_setup(hps, info)
@@ -145,8 +147,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                 batcher = loader
             else:
                 pad = hps.max_enc_steps if (torch.cuda.device_count() > 0 and hps.pad_enc_to_max) else None
-                batcher = Batcher(hps.data_path, vocab, hps, single_pass=hps.single_pass, seed=hps.seed + info.rank,
-                                  pad_enc_to=pad)
+                batcher = Batcher(hps.data_path, vocab, hps, single_pass=hps.single_pass, seed=hps.seed,
+                                  pad_enc_to=pad, rank=info.rank, world=info.world)
             from .train.loop import setup_training
             try:
                 setup_training(hps, vocab, batcher, info=info, metrics=metrics)

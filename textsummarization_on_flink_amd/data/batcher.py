@@ -58,7 +58,15 @@ class Batcher:
                  example_source: Optional[Callable[[], Iterator[Tuple[str, List[str], Optional[str]]]]] = None,
                  decode_distinct: bool = False, num_example_threads: Optional[int] = None,
                  num_batch_threads: Optional[int] = None, bucketing_cache_size: Optional[int] = None,
-                 watchdog_secs: float = 60.0, seed: Optional[int] = None, pad_enc_to: Optional[int] = None):
+                 watchdog_secs: float = 60.0, seed: Optional[int] = None, pad_enc_to: Optional[int] = None,
+                 rank: int = 0, world: int = 1):
+        """``rank`` / ``world``: read only this data-parallel rank's share of the .bin records
+        (record k of a pass goes to rank k % world; every rank passes the same ``seed``, which
+        fixes the shared file order)."""
+        if not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside world {world}")
+        self._shard = (rank, world)
+        self._file_seed = seed
         self._data_path = data_path
         self._vocab = vocab
         self._hps = hps
@@ -66,7 +74,7 @@ class Batcher:
         self._source = example_source or self._bin_source
         self._decode_distinct = decode_distinct
         self._pad_enc_to = pad_enc_to
-        self._rng = random.Random(seed)
+        self._rng = random.Random(seed if world == 1 else (None if seed is None else seed * 1009 + rank + 1))
         self._batch_queue: "queue.Queue" = queue.Queue(self.BATCH_QUEUE_MAX)
         self._example_queue: "queue.Queue" = queue.Queue(self.BATCH_QUEUE_MAX * hps.batch_size)
         if single_pass:
@@ -105,8 +113,9 @@ class Batcher:
         return run
 
     def _bin_source(self) -> Iterator[Tuple[str, List[str], Optional[str]]]:
-        gen = binfmt.text_generator(binfmt.example_generator(self._data_path, self._single_pass,
-                                                            random.Random(self._rng.random())))
+        file_rng = random.Random(self._rng.random() if self._shard[1] == 1 else random.Random(self._file_seed).random())
+        gen = binfmt.text_generator(binfmt.example_generator(self._data_path, self._single_pass, file_rng,
+                                                            shard=self._shard))
         for article, abstract in gen:
             yield article, [s.strip() for s in abstract2sents(abstract)], None
 

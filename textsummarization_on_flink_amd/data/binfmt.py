@@ -51,10 +51,20 @@ def read_bin(path: str) -> Iterator[bytes]:
 
 
 def example_generator(data_path: str, single_pass: bool, rng: Optional[random.Random] = None,
-                      decode: bool = True) -> Iterator[Dict[str, List]]:
+                      decode: bool = True, shard: Tuple[int, int] = (0, 1)) -> Iterator[Dict[str, List]]:
     """Yield decoded tf.Examples (raw records with ``decode=False``); forever in shuffled
-    file order unless single_pass."""
+    file order unless single_pass.
+
+    ``shard = (index, count)``: only the records k of each pass with k % count == index (k
+    counts records in the pass's file order).  Readers that share ``rng``'s seed walk the same
+    file order, so ``count`` of them with distinct indices see disjoint records that together
+    cover every record once per pass -- the data-parallel split of the reference's Flink
+    job, where each of ``worker_num`` flatMap instances receives its own share of the row
+    stream (``doc/deprecated/About StreamExeEnv in AI-Extended Issue.md:68-74``)."""
     rng = rng or random.Random()
+    index, count = shard
+    if not 0 <= index < count:
+        raise ValueError(f"bad shard {shard}")
     while True:
         filelist = glob.glob(data_path)
         if not filelist:
@@ -63,9 +73,13 @@ def example_generator(data_path: str, single_pass: bool, rng: Optional[random.Ra
             filelist = sorted(filelist)
         else:
             rng.shuffle(filelist)
+        k = 0
         for fn in filelist:
             for rec in read_bin(fn):
-                yield decode_example(rec) if decode else rec
+                mine = k % count == index
+                k += 1
+                if mine:
+                    yield decode_example(rec) if decode else rec
         if single_pass:
             log.info("example_generator completed reading all datafiles. No more data.")
             return

@@ -6,8 +6,10 @@ under the GIL, beside the thread that replays the train-step graphs; at B = 256 
 per step it would have to sustain ~12k examples/s.  ``ProcessBatcher`` moves all of it into
 ``workers`` forked processes:
 
-  worker w:  .bin records k with k % workers == w (every worker walks the same shuffled
-             file order per pass, so each record is read by exactly one worker per pass)
+  worker w:  .bin records k with k % world == rank and (k // world) % workers == w: every
+             worker of every data-parallel rank walks the same shuffled file order per pass
+             (one shared file-order seed), so each record is read by exactly one worker of
+             one rank per pass
              -> Example -> length-bucketed batches (``bucketing_cache_size`` batches sorted by
              encoder length, shuffled) -> ``host_inputs`` -> ONE byte buffer in the engine's
              ``input_layout`` order -> a shared-memory SPSC ring (``runtime/ring.py``, native)
@@ -76,18 +78,20 @@ def _push(ring, data: bytes) -> None:
 
 
 def _worker(w: int, n: int, ring_name: str, data_path: str, vocab: Vocab, hps, single_pass: bool, seed: int,
-            pad_enc_to: Optional[int], D: int, cache: int) -> None:
+            pad_enc_to: Optional[int], D: int, cache: int, rank: int = 0, world: int = 1) -> None:
     from ..models.pointer_generator import host_inputs, input_layout, pack_host_inputs
     from ..runtime.ring import RecordRing, RingClosed
     ring = RecordRing.open(ring_name)
     B, T = hps.batch_size, pad_enc_to or hps.max_enc_steps
     layout, _ = input_layout(B, T, D)
-    file_rng = random.Random(seed)            # identical in every worker: same file order per pass
-    rng = random.Random(seed * 1009 + w + 1)  # this worker's batch order
+    file_rng = random.Random(seed)  # identical in every worker of every rank: same file order per pass
+    rng = random.Random(seed * 1009 + rank * n + w + 1)  # this worker's batch order
+    failed = False
     try:
         def examples():
-            k = 0
-            for rec in binfmt.example_generator(data_path, single_pass, file_rng, decode=False):
+            k = 0  # index among this rank's records
+            for rec in binfmt.example_generator(data_path, single_pass, file_rng, decode=False,
+                                                shard=(rank, world)):
                 mine = k % n == w
                 k += 1
                 if not mine:
@@ -123,6 +127,7 @@ def _worker(w: int, n: int, ring_name: str, data_path: str, vocab: Vocab, hps, s
     except RingClosed:
         pass
     except BaseException as e:  # noqa: BLE001 -- reported to the trainer through the ring
+        failed = True
         log.exception("loader worker %d failed", w)
         try:
             err = json.dumps({"error": repr(e)}).encode()
@@ -135,7 +140,9 @@ def _worker(w: int, n: int, ring_name: str, data_path: str, vocab: Vocab, hps, s
         except Exception:  # noqa: BLE001
             pass
         ring.release(unlink=False)
-        os._exit(0)  # no atexit / finalizers of the parent's state in a forked child
+        # no atexit / finalizers of the parent's state in a forked child; a failed worker
+        # exits non-zero so the trainer can tell a crash from the end of a pass
+        os._exit(1 if failed else 0)
 
 
 class ProcessBatcher:
@@ -143,10 +150,14 @@ class ProcessBatcher:
 
     def __init__(self, data_path: str, vocab: Vocab, hps, single_pass: bool, workers: int, seed: int = 0,
                  pad_enc_to: Optional[int] = None, bucketing_cache_size: Optional[int] = None,
-                 ring_bytes: int = 128 << 20):
+                 ring_bytes: int = 128 << 20, rank: int = 0, world: int = 1):
+        """``rank`` / ``world``: this process's data-parallel share of the records (the same
+        ``seed`` on every rank: it fixes the shared file order)."""
         from ..runtime.ring import RecordRing
         if workers < 1:
             raise ValueError("workers must be >= 1")
+        if not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside world {world}")
         self.hps = hps
         self.D = hps.max_dec_steps
         self.single_pass = single_pass
@@ -157,7 +168,7 @@ class ProcessBatcher:
         for w in range(workers):
             ring = RecordRing.create(f"/tsamd_ld_{tag}_{w}", ring_bytes)
             p = ctx.Process(target=_worker, args=(w, workers, ring.name, data_path, vocab, hps, single_pass, seed,
-                                                  pad_enc_to, self.D, cache), daemon=True)
+                                                  pad_enc_to, self.D, cache, rank, world), daemon=True)
             p.start()
             self.rings.append(ring)
             self.procs.append(p)
@@ -180,7 +191,11 @@ class ProcessBatcher:
                             and not self.rings[w].closed:
                         raise RuntimeError(f"loader worker {w} died (exit code {self.procs[w].exitcode})")
                     continue
-                if rec is None:  # this worker finished its single pass
+                if rec is None:  # ring closed: the end of this worker's single pass, or a crash
+                    self.procs[w].join(timeout=5)
+                    code = self.procs[w].exitcode
+                    if code or not self.single_pass:  # outside single_pass a worker never ends by itself
+                        raise RuntimeError(f"loader worker {w} stopped (exit code {code})")
                     self._live.remove(w)
                     break
                 self._rr = (self._rr + j + 1) % max(1, n)

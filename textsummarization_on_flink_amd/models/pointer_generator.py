@@ -112,16 +112,39 @@ def host_inputs(batch, hps, D: int) -> Dict[str, np.ndarray]:
         wm = dm * valid[:, None]
         rowg = wm / wm.sum()
     gcl = hps.cov_loss_wt * dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
+    dec_t = np.ascontiguousarray(batch.dec_batch[:, :D].T).astype(np.int64)
+    sid, perm = emb_sort(batch.enc_batch, dec_t)
     return {
         "enc_batch": batch.enc_batch.astype(np.int64),
         "enc_lens": batch.enc_lens.astype(np.int32),
         "rev_idx": rev.astype(np.int64),
         "ext": batch.enc_batch_extend_vocab.astype(np.int32),
-        "dec_batch_t": np.ascontiguousarray(batch.dec_batch[:, :D].T).astype(np.int64),
+        "dec_batch_t": dec_t,
         "target_t": np.ascontiguousarray(batch.target_batch[:, :D].T).astype(np.int32),
         "rowg": np.ascontiguousarray(rowg.T).astype(np.float32),
         "gcl": np.ascontiguousarray(gcl.T).astype(np.float32),
+        "emb_sid": sid,
+        "emb_perm": perm,
     }
+
+
+def emb_sort(enc_batch: np.ndarray, dec_t: np.ndarray):
+    """Stable id order of the step's embedding-gradient rows: the encoder tokens (row b*T + t)
+    then the decoder inputs (row B*T + t*B + b).  Returns (sorted ids, row permutation), int32.
+
+    Computed on the host with the batch (a loader worker process when one is used) instead of
+    a device sort inside the captured backward: torch.sort of more than ~1M keys (rocprim's
+    onesweep radix sort) faulted the GPU on the second replay of the captured graph at config #5
+    batch 2048 (memory-aperture violation at that kernel, three runs; the same step eager and
+    kernel-serialised ran clean: profiles/r3/b2048_fault.md).  The stable order also makes the
+    gradient's per-id summation order a function of the batch alone (deterministic mode)."""
+    ids = np.concatenate([np.asarray(enc_batch).reshape(-1), np.asarray(dec_t).reshape(-1)])
+    if ids.size and (ids.min() < 0 or ids.max() >= 2 ** 31):
+        raise ValueError("token ids out of range")
+    # numpy's stable sort is a radix sort for 16-bit keys: ~5 ms for 230k ids, 28 ms for 1.8M
+    key = ids.astype(np.uint16) if ids.size == 0 or ids.max() < 65536 else ids.astype(np.int32)
+    perm = np.argsort(key, kind="stable").astype(np.int32)
+    return ids[perm].astype(np.int32), perm
 
 
 _NP = {torch.long: np.int64, torch.int32: np.int32, F32: np.float32}
@@ -130,12 +153,13 @@ _NP = {torch.long: np.int64, torch.int32: np.int32, F32: np.float32}
 def input_layout(B: int, T: int, D: int):
     """Byte layout of the engine's input pack: [(name, offset, shape, torch dtype, nbytes)],
     total size (every array 256-byte aligned); the device copy is one buffer with views."""
-    shapes = {"BT": (B, T), "B": (B,), "DB": (D, B)}
+    shapes = {"BT": (B, T), "B": (B,), "DB": (D, B), "R": (B * T + D * B,)}
     layout, off = [], 0
     for name, sk, dt in (("enc_batch", "BT", torch.long), ("enc_lens", "B", torch.int32),
                          ("rev_idx", "BT", torch.long), ("ext", "BT", torch.int32),
                          ("dec_batch_t", "DB", torch.long), ("target_t", "DB", torch.int32),
-                         ("rowg", "DB", F32), ("gcl", "DB", F32)):
+                         ("rowg", "DB", F32), ("gcl", "DB", F32),
+                         ("emb_sid", "R", torch.int32), ("emb_perm", "R", torch.int32)):
         shp = shapes[sk]
         nb = int(np.prod(shp)) * np.dtype(_NP[dt]).itemsize
         layout.append((name, off, shp, dt, nb))
@@ -172,16 +196,11 @@ class HipPointerGenerator:
             raise ValueError("emb_dim and hidden_dim must be multiples of 32 for the MFMA kernels")
         if T > 2048:
             raise ValueError("max_enc_steps > 2048 not supported by the attention kernels")
-        # Verified envelope: per-GPU encoder activations B x T x A up to 2^30 elements (config #5
-        # at batch 1024: 0.84G).  Config #5 at batch 2048 (1.68G: the fp32 attention-input
-        # gradient alone is 6.7 GB) ended in a GPU memory-aperture fault on MI355X, cause not yet
-        # isolated -- refuse such shapes loudly instead of faulting the device (split the batch
-        # over more GPUs or steps).  TSAMD_UNVERIFIED_SHAPES=1 lifts the check for debugging.
-        # (the [D x B, V] logits / dlogits, 5.1G elements at batch 1024, likewise up to 2^33)
-        if os.environ.get("TSAMD_UNVERIFIED_SHAPES", "0") != "1" and (
-                B * T * self.A > 2 ** 30 or self.D * B * self.V > 2 ** 33):
-            raise ValueError(f"batch {B} x enc {T} x attention width {self.A} (or x dec {self.D} x vocab {self.V}) "
-                             "exceeds the verified per-GPU envelope; use a smaller per-GPU batch")
+        # Row counts (tokens B*T, decoder rows D*B) are int32 kernel arguments; every element
+        # offset is 64-bit (config #5 at batch 2048 runs 3.4G-element gate buffers and 10G-element
+        # dlogits: tools/big_batch_steps.py, tests/test_gpu_production.py).
+        if B * T >= 2 ** 31 or self.D * B * max(self.V, 4 * self.H) >= 2 ** 62:
+            raise ValueError(f"batch {B} x enc {T} exceeds the kernels' 32-bit row counts")
         self.k = _ops()
         self.grad_scale = 1.0  # set to 1/world by a data-parallel trainer (see optimizer_step)
         self.nchunk = int(self.k.attn_chunks(T))
@@ -960,13 +979,12 @@ class HipPointerGenerator:
             dx = st["dx"]
             k.from_step_frame(dxs, w["rev_idx"], dx, B, T, din)  # fw + reversed bw, batch frame
             d_in = dx
-        # encoder + decoder token rows in id order (one radix sort + one launch, embedding.hip):
-        # atomics only where the id changes, so Zipf-hot tokens do not serialise
-        ids = torch.cat([w["enc_batch"].view(-1), w["dec_batch_t"].view(-1)]).to(torch.int32)
-        sid, perm = torch.sort(ids)
+        # encoder + decoder token rows in id order (the order is sorted on the host with the
+        # batch, emb_sort; one launch, embedding.hip): atomics only where the id changes, so
+        # Zipf-hot tokens do not serialise
         if late:
             torch.cuda.current_stream().wait_stream(self._late_stream)  # d_emb_dec and the weight gradients
-        k.emb_grad_sorted(gemb, sid, perm, d_in.reshape(B * T, self.E), w["d_emb_dec"])
+        k.emb_grad_sorted(gemb, w["emb_sid"], w["emb_perm"], d_in.reshape(B * T, self.E), w["d_emb_dec"])
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_step(self):
