@@ -135,32 +135,6 @@ void attn_softmax_ctx(const Tensor& e, const Tensor& E, const Tensor& lens, cons
                           PO<float>(covloss), P<float>(ctx), PO<bf16>(ctx_bf), B, T, A, rep, stream());
 }
 
-void attn_bwd_da(const Tensor& E, const Tensor& dctx, const OT& Ga, const OT& dcov_next, const Tensor& a,
-                 const OT& cov, const OT& gcl, const Tensor& lens, const Tensor& da, int64_t B, int64_t T, int64_t A) {
-  chk(E, BF, "Et"); chk(dctx, F32, "dctx"); chk(a, F32, "a"); chk(lens, I32, "lens"); chk(da, F32, "da");
-  TORCH_CHECK(A % 64 == 0 && A <= 1024 && T % 2 == 0, "bad A/T");
-  numel_eq(E, B * T * A, "E"); numel_eq(dctx, B * A, "dctx"); numel_eq(a, B * T, "a"); numel_eq(da, B * T, "da");
-  chko(Ga, F32, B * T, "Ga"); chko(dcov_next, F32, B * T, "dcov_next"); chko(cov, F32, B * T, "cov");
-  chko(gcl, F32, B, "gcl");
-  launch_attn_bwd_da(P<bf16>(E), P<float>(dctx), PO<float>(Ga), PO<float>(dcov_next), P<float>(a), PO<float>(cov),
-                     PO<float>(gcl), P<int>(lens), P<float>(da), B, T, A, stream());
-}
-
-void attn_bwd_tanh(const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov, const Tensor& a,
-                   const Tensor& da, const OT& dcov_next, const OT& gcl, const Tensor& lens, const Tensor& de_out,
-                   const Tensor& ds, const OT& dcov_out, int64_t B, int64_t T, int64_t A) {
-  chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(da, F32, "da"); chk(lens, I32, "lens");
-  chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
-  TORCH_CHECK(A % 64 == 0 && A <= 1024, "bad A");
-  numel_eq(F, B * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(a, B * T, "a"); numel_eq(da, B * T, "da");
-  numel_eq(de_out, B * T, "de_out"); numel_eq(ds, B * A, "ds");
-  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(dcov_next, F32, B * T, "dcov_next");
-  chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
-  launch_attn_bwd_tanh(P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a), P<float>(da),
-                       PO<float>(dcov_next), PO<float>(gcl), P<int>(lens), P<float>(de_out), P<float>(ds),
-                       PO<float>(dcov_out), B, T, A, stream());
-}
-
 // one workgroup per row (attention_row.hip): forward score + softmax + coverage + context in
 // one launch, backward step without atomics (ds stored, not accumulated)
 bool attn_row_ok(int64_t A, int64_t T) { return attn_row_supported((int)A, (int)T); }
@@ -176,35 +150,14 @@ void attn_fwd_row(const Tensor& F, const Tensor& E, const Tensor& s, const Tenso
   numel_eq(lens, B / rep, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx");
   chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out");
   chko(covloss, F32, B, "covloss"); chko(ctx_bf, BF, B * A, "ctx_bf");
-  launch_attn_fwd_row(P<bf16>(F), P<bf16>(E), P<float>(s), nullptr, nullptr, nullptr, nullptr, P<float>(v), PO<float>(wc),
+  launch_attn_fwd_row(P<bf16>(F), P<bf16>(E), P<float>(s), P<float>(v), PO<float>(wc),
                       PO<float>(cov), P<int>(lens), P<float>(a_out), PO<float>(cov_out), PO<float>(covloss), P<float>(ctx),
                       PO<bf16>(ctx_bf), B, T, A, (int)rep, stream());
-}
-// the same with the attention query projection inside the kernel: s_out = [cb, hb] . WsT^T + bs
-// (replaces dec_sproj + attn_fwd_row in the training decoder loop)
-void attn_fwd_row_sproj(const Tensor& F, const Tensor& E, const Tensor& cb, const Tensor& hb, const Tensor& WsT,
-                        const Tensor& bs, const Tensor& s_out, const Tensor& v, const OT& wc, const OT& cov,
-                        const Tensor& lens, const Tensor& a_out, const OT& cov_out, const OT& covloss, const Tensor& ctx,
-                        const OT& ctx_bf, int64_t B, int64_t T, int64_t A) {
-  chk(F, BF, "F"); chk(E, BF, "E"); chk(s_out, F32, "s_out"); chk(v, F32, "v"); chk(lens, I32, "lens");
-  chk(cb, BF, "cb"); chk(hb, BF, "hb"); chk(WsT, BF, "WsT"); chk(bs, F32, "bs");
-  chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
-  TORCH_CHECK(attn_row_supported((int)A, (int)T), "row attention needs A in {512, 1024} and T <= 2048");
-  numel_eq(F, B * T * A, "F"); numel_eq(E, B * T * A, "E"); numel_eq(s_out, B * A, "s_out"); numel_eq(v, A, "v");
-  numel_eq(cb, B * A / 2, "cb"); numel_eq(hb, B * A / 2, "hb"); numel_eq(WsT, A * A, "WsT"); numel_eq(bs, A, "bs");
-  numel_eq(lens, B, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx");
-  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out");
-  chko(covloss, F32, B, "covloss"); chko(ctx_bf, BF, B * A, "ctx_bf");
-  launch_attn_fwd_row(P<bf16>(F), P<bf16>(E), P<float>(s_out), P<bf16>(cb), P<bf16>(hb), P<bf16>(WsT), P<float>(bs),
-                      P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens), P<float>(a_out), PO<float>(cov_out),
-                      PO<float>(covloss), P<float>(ctx), PO<bf16>(ctx_bf), B, T, A, 1, stream());
 }
 void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                   const Tensor& a, const Tensor& dctx, const Tensor& ctx, const OT& Ga, const OT& dcov_next,
                   const OT& gcl, const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out,
-                  int64_t B, int64_t T, int64_t A, const OT& ds1) {
-  // ds1 given: two workgroups per row, partial ds in ds and ds1 (dec_bwd_cell sums them)
-  chko(ds1, F32, B * A, "ds1");
+                  int64_t B, int64_t T, int64_t A) {
   chk(E, BF, "E"); chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(dctx, F32, "dctx");
   chk(ctx, F32, "ctx"); chk(lens, I32, "lens"); chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
   TORCH_CHECK(attn_row_supported((int)A, (int)T), "row attention needs A in {512, 1024} and T <= 2048");
@@ -215,8 +168,7 @@ void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tenso
   chko(dcov_next, F32, B * T, "dcov_next"); chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
   launch_attn_bwd_row(P<bf16>(E), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
                       P<float>(dctx), P<float>(ctx), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl),
-                      P<int>(lens), P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, PO<float>(ds1),
-                      stream());
+                      P<int>(lens), P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, stream());
 }
 
 void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
@@ -383,8 +335,7 @@ void dec_sproj(const Tensor& cb, const Tensor& hb, const Tensor& WsT, const Tens
 
 void dec_bwd_cell(const Tensor& ds, const Tensor& Ws, const OT& dC_dir, const OT& dH_dir, const Tensor& dh_rec,
                   const Tensor& dc_carry, const Tensor& act, const Tensor& c_now, const Tensor& c_prev,
-                  const Tensor& dz, int64_t B, int64_t H, int64_t A, const OT& ds2) {
-  chko(ds2, F32, B * A, "ds2");  // second partial of ds (attn_bwd_row with two workgroups per row)
+                  const Tensor& dz, int64_t B, int64_t H, int64_t A) {
   chk(ds, F32, "ds"); chk(Ws, BF, "Ws"); chk(dh_rec, F32, "dh_rec"); chk(dc_carry, F32, "dc_carry");
   chk(act, F32, "act"); chk(c_now, F32, "c_now"); chk(c_prev, F32, "c_prev"); chk(dz, BF, "dz");
   TORCH_CHECK(H % 16 == 0 && A % 32 == 0, "bad dims");
@@ -392,7 +343,7 @@ void dec_bwd_cell(const Tensor& ds, const Tensor& Ws, const OT& dC_dir, const OT
   chko(dH_dir, F32, B * H, "dH_dir"); numel_eq(dh_rec, B * H, "dh_rec"); numel_eq(dc_carry, B * H, "dc_carry");
   numel_eq(act, B * 4 * H, "act"); numel_eq(c_now, B * H, "c_now"); numel_eq(c_prev, B * H, "c_prev");
   numel_eq(dz, B * 4 * H, "dz");
-  launch_dec_bwd_cell(P<float>(ds), PO<float>(ds2), P<bf16>(Ws), PO<float>(dC_dir), PO<float>(dH_dir), P<float>(dh_rec),
+  launch_dec_bwd_cell(P<float>(ds), P<bf16>(Ws), PO<float>(dC_dir), PO<float>(dH_dir), P<float>(dh_rec),
                       P<float>(dc_carry), P<float>(act), P<float>(c_now), P<float>(c_prev), P<bf16>(dz), B, H, A,
                       stream());
 }
@@ -742,12 +693,9 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("lstm_bwd_persistent", &lstm_bwd_persistent);
   m.def("attn_score", &attn_score);
   m.def("attn_softmax_ctx", &attn_softmax_ctx);
-  m.def("attn_bwd_da", &attn_bwd_da);
-  m.def("attn_bwd_tanh", &attn_bwd_tanh);
   m.def("attn_bwd_step", &attn_bwd_step);
   m.def("attn_row_ok", &attn_row_ok);
   m.def("attn_fwd_row", &attn_fwd_row);
-  m.def("attn_fwd_row_sproj", &attn_fwd_row_sproj);
   m.def("attn_bwd_row", &attn_bwd_row);
   m.def("attn_bwd_feat", &attn_bwd_feat);
   m.def("attn_chunks", &attn_chunks);

@@ -6,12 +6,14 @@
 //   cov'  = cov + a           covloss = sum_i min(a_i, cov_i)
 //   ctx   = sum_i a_i E[i,:]
 //
-// Two layouts of the [B,T,A] encoder tensors are kept (both fit trivially in HBM):
+// Two layouts of the [B,T,A] encoder features are used (both fit trivially in HBM):
 //  * row-major F/E [B][T][A] -- lanes on the feature axis (8 bf16 = one 16-B load);
-//  * transposed Ft/Et [B][A][T] -- lanes on the position axis, so the score e_i and
-//    da_i = dctx . E_i reduce over k inside a lane (no cross-lane reduction at all), the
-//    per-k parameters (s_k, v_k, w_c_k, dctx_k) are wave-uniform scalar loads, and the 8
-//    waves of a block split the k axis (summed once in LDS).
+//  * transposed Ft [B][A][T] (score kernel) -- lanes on the position axis, so the score e_i
+//    reduces over k inside a lane (no cross-lane reduction at all), the per-k parameters
+//    (s_k, v_k, w_c_k) are wave-uniform scalar loads, and the 8 waves of a block split the
+//    k axis (summed once in LDS).
+// These multi-block-per-row kernels serve B < 128 and the A = 1024 backward; the row-resident
+// kernels of attention_row.hip take the rest.
 // The v / w_c / F gradients are NOT accumulated per step: the backward step stores
 // de_t, and attn_bwd_feat recomputes tanh once over all steps after the loop.  The
 // recurrent path only carries ds_t (atomically accumulated across position chunks) and
@@ -218,204 +220,6 @@ __global__ __launch_bounds__(256) void attn_softmax_ctx_kernel(
   }
 }
 
-// ------------------------------------------------------------- backward step: da
-//   da_i = Ga_i + dcov_next_i + g_cl*[a_i <= cov_i] + dctx . E[i,:]     (Et: [B][A][T])
-template <int SW>
-__global__ __launch_bounds__(SW * 64) void attn_bwd_da_kernel(
-    const bf16* __restrict__ Et, const float* __restrict__ dctx, const float* __restrict__ Ga,
-    const float* __restrict__ dcov_next, const float* __restrict__ a, const float* __restrict__ cov,
-    const float* __restrict__ gcl, const int* __restrict__ lens, float* __restrict__ da, int T, int A) {
-  __shared__ float red[SW][SCORE_POS];
-  const int b = blockIdx.y;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
-  const int pb = blockIdx.x * SCORE_POS;
-  if (pb >= len) return;
-  const int p = pb + 2 * lane;
-  const int pc = p < T ? p : 0;
-  const int ka = wid * (A / SW), kb = ka + A / SW;
-  const bf16* ep = Et + ((size_t)b * A) * T + pc;
-  const float* db = dctx + (size_t)b * A;
-  float d0 = 0.f, d1 = 0.f;
-  for (int k = ka; k < kb; k += 8) {
-    uint32_t raw[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) raw[i] = *reinterpret_cast<const uint32_t*>(ep + (size_t)(k + i) * T);
-    float dk[8];
-    *reinterpret_cast<float4*>(dk) = *reinterpret_cast<const float4*>(db + k);
-    *reinterpret_cast<float4*>(dk + 4) = *reinterpret_cast<const float4*>(db + k + 4);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      d0 += dk[i] * lo_bf(raw[i]);
-      d1 += dk[i] * hi_bf(raw[i]);
-    }
-  }
-  red[wid][2 * lane] = d0;
-  red[wid][2 * lane + 1] = d1;
-  __syncthreads();
-  if (threadIdx.x < SCORE_POS) {
-    const int q = pb + threadIdx.x;
-    if (q < len) {
-      const size_t ix = (size_t)b * T + q;
-      float r = 0.f;
-#pragma unroll
-      for (int w = 0; w < SW; ++w) r += red[w][threadIdx.x];
-      if (Ga) r += Ga[ix];
-      if (dcov_next) r += dcov_next[ix];
-      if (gcl && a[ix] <= (cov ? cov[ix] : 0.f)) r += gcl[b];
-      da[ix] = r;
-    }
-  }
-}
-
-// ----------------------------------------------------- backward step: de, ds, dcov
-// de_i = a_i (da_i - sum_j a_j da_j);  ds_k += sum_i de_i v_k sech2(u_ik) (atomic into
-// ds[b][k], pre-zeroed);  dcov_i = dcov_next_i + g_cl*[a_i > cov_i] + de_i sum_k v_k w_c_k sech2(u_ik).
-// Lanes on the feature axis (8 per lane, NK blocks of 512); each wave takes 16 positions
-// in groups of 8 and reduces the 8 per-position dcov partials across the 64 lanes with a
-// butterfly reduce-scatter (10 shuffles per 8 positions instead of 48).
-template <int NK>
-__global__ __launch_bounds__(256) void attn_bwd_tanh_kernel(
-    const bf16* __restrict__ F, const float* __restrict__ s, const float* __restrict__ v,
-    const float* __restrict__ wc, const float* __restrict__ cov, const float* __restrict__ a,
-    const float* __restrict__ da, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
-    const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
-    float* __restrict__ dcov_out, int T, int A) {
-  __shared__ float red[8];
-  __shared__ float part[4][512 * NK];
-  const int b = blockIdx.y;
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
-  const size_t rb = (size_t)b * T;
-  const int p0 = blockIdx.x * 64 + wid * 16;
-  if (blockIdx.x * 64 >= len) {  // whole block masked: only pass dcov through
-    if (dcov_out)
-      for (int i = tid; i < 64; i += 256) {
-        const int p = blockIdx.x * 64 + i;
-        if (p < T) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
-      }
-    for (int i = tid; i < 64; i += 256) {
-      const int p = blockIdx.x * 64 + i;
-      if (p < T) de_out[rb + p] = 0.f;
-    }
-    return;
-  }
-  float S = 0.f;
-  for (int i = tid; i < len; i += 256) S += a[rb + i] * da[rb + i];
-  S = block_sum<256>(S, red);
-  const float g = gcl ? gcl[b] : 0.f;
-  float sk[NK][8], vk[NK][8], wk[NK][8], acc[NK][8];
-#pragma unroll
-  for (int kb = 0; kb < NK; ++kb) {
-    const int k0 = kb * 512 + lane * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bool ok = k0 + j < A;
-      sk[kb][j] = ok ? s[(size_t)b * A + k0 + j] : 0.f;
-      vk[kb][j] = ok ? v[k0 + j] : 0.f;
-      wk[kb][j] = (ok && wc) ? wc[k0 + j] : 0.f;
-      acc[kb][j] = 0.f;
-    }
-  }
-  const bf16* Fb = F + (size_t)b * T * A;
-  const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1;
-  // per-position scalars of this wave's 16 positions, one per lane (lanes 0..15), all
-  // loaded at once and later broadcast with v_readlane (no dependent loads per position)
-  float de_l = 0.f, c_l = 0.f, a_l = 0.f, dn_l = 0.f;
-  {
-    const int p = p0 + (lane & 15);
-    if (p < len) {
-      const size_t ix = rb + p;
-      a_l = a[ix];
-      de_l = a_l * (da[ix] - S);
-      c_l = cov ? cov[ix] : 0.f;
-    }
-    if (p < T && dcov_next) dn_l = dcov_next[rb + p];
-  }
-  for (int grp = 0; grp < 2; ++grp) {
-    const int pg = p0 + grp * 8;
-    bf16x8 f[NK][8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int pq = min(pg + q, len - 1);
-#pragma unroll
-      for (int kb = 0; kb < NK; ++kb) {
-        const int k0 = min(kb * 512 + lane * 8, A - 8);
-        f[kb][q] = ld8(Fb + (size_t)pq * A + k0);
-      }
-    }
-    float dcv[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float de = rdlane(de_l, grp * 8 + q);
-      const float c = rdlane(c_l, grp * 8 + q);
-      dcv[q] = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < NK; ++kb) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float th = ftanh(bf2f(f[kb][q][j]) + sk[kb][j] + wk[kb][j] * c);
-          const float gs = de * vk[kb][j] * (1.0f - th * th);
-          acc[kb][j] += gs;
-          dcv[q] += gs * wk[kb][j];
-        }
-      }
-    }
-    // butterfly reduce-scatter of dcv[0..7] over 64 lanes
-    float h4[4], h2[2], h1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float send = b5 ? dcv[i] : dcv[i + 4];
-      const float keep = b5 ? dcv[i + 4] : dcv[i];
-      h4[i] = keep + xor32_f(send);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float send = b4 ? h4[i] : h4[i + 2];
-      const float keep = b4 ? h4[i + 2] : h4[i];
-      h2[i] = keep + xor16_f(send);
-    }
-    {
-      const float send = b3 ? h2[0] : h2[1];
-      const float keep = b3 ? h2[1] : h2[0];
-      h1 = keep + dpp_f<DPP_ROR8>(send);
-    }
-    h1 = dpp_sum8(h1);
-    // position q's total sits in lanes 8q' .. 8q'+7 with q = 4*b5 + 2*b4 + b3; fetch the
-    // per-position scalars of q from lane (grp*8 + q) and let lane 8*(...) write.
-    const int q = 4 * b5 + 2 * b4 + b3;
-    const int src = grp * 8 + q;
-    const float de_q = __shfl(de_l, src, 64), a_q = __shfl(a_l, src, 64);
-    const float c_q = __shfl(c_l, src, 64), dn_q = __shfl(dn_l, src, 64);
-    if ((lane & 7) == 0) {
-      const int p = pg + q;
-      if (p < T) {
-        const size_t ix = rb + p;
-        de_out[ix] = p < len ? de_q : 0.f;
-        if (dcov_out) {
-          float r = dn_q;
-          if (p < len) {
-            r += h1;
-            if (gcl && a_q > c_q) r += g;
-          }
-          dcov_out[ix] = r;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int kb = 0; kb < NK; ++kb) {
-    const int k0 = kb * 512 + lane * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) part[wid][kb * 512 + lane * 8 + j] = (k0 + j < A) ? acc[kb][j] : 0.f;
-  }
-  __syncthreads();
-  float* out = ds + (size_t)b * A;
-  for (int k = tid; k < A; k += 256) {
-    const float x = part[0][k] + part[1][k] + part[2][k] + part[3][k];
-    atomicAdd(out + k, x);
-  }
-}
 
 // ------------------------------------------ backward step, fused: da, de, ds, dcov
 // One pass over the rows E_i (encoder outputs) and F_i (W_h features) of a block's positions:
@@ -424,210 +228,13 @@ __global__ __launch_bounds__(256) void attn_bwd_tanh_kernel(
 //   de_i   = a_i (da_i - S)
 //   ds_k  += sum_i de_i v_k sech2(u_ik)                        (atomic, ds pre-zeroed)
 //   dcov_i = dcov_next_i + g_cl [a_i > cov_i] + de_i sum_k v_k w_c_k sech2(u_ik)
-// S needs no pass over da (its dctx.E half is dctx.ctx), so the da kernel over the
-// transposed Et and the tanh kernel over F collapse into ONE launch per decoder step and
-// every block is independent.  Lanes on the feature axis (8 per lane, NK blocks of 512);
-// each wave takes NG groups of 8 positions.  Per group: the 8 partial dctx.E_i
-// dots are reduced with the butterfly reduce-scatter (the lanes of position q end up
-// holding its total), de_q is broadcast with v_readlane, then the r-form tanh pass
-// (packed fp32, see rsig2) accumulates ds and the 8 dcov partials, reduced the same way.
-//   v_k sech2(u) = 4 v_k r (1 - r)  ->  ds_k = 4 v_k sum_i de_i q_ik,  q = r - r^2.
-// NG groups of 8 positions per wave (a block = 4 waves = 32*NG positions).  The loads are
-// software-pipelined: group 0's E/F rows are issued before the S reduction (whose global
-// loads and block barriers then overlap them); group g+1's E rows are issued right after
-// group g's dots, its F rows right after group g's tanh pass.
-template <int NK, int NG, int OCC>
-__global__ __launch_bounds__(256, OCC) void attn_bwd_step_kernel(
-    const bf16* __restrict__ E, const bf16* __restrict__ F, const float* __restrict__ s,
-    const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
-    const float* __restrict__ a, const float* __restrict__ dctx, const float* __restrict__ ctx,
-    const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
-    const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
-    float* __restrict__ dcov_out, int T, int A) {
-  constexpr int PB = 32 * NG;  // positions per block
-  static_assert(NG >= 1 && 8 * NG <= 64, "one lane per position of a wave");
-  __shared__ float red[8];
-  __shared__ float part[4][512 * NK];
-  const int b = blockIdx.y;
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
-  const size_t rb = (size_t)b * T;
-  const int p0 = blockIdx.x * PB + wid * 8 * NG;
-  if (blockIdx.x * PB >= len) {  // whole block masked: only pass dcov through
-    for (int i = tid; i < PB; i += 256) {
-      const int p = blockIdx.x * PB + i;
-      if (p < T) {
-        if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
-        de_out[rb + p] = 0.f;
-      }
-    }
-    return;
-  }
-  const float g = gcl ? gcl[b] : 0.f;
-  const bf16* Eb = E + (size_t)b * T * A;
-  const bf16* Fb = F + (size_t)b * T * A;
-  int k0c[NK];
-#pragma unroll
-  for (int kb = 0; kb < NK; ++kb) k0c[kb] = min(kb * 512 + lane * 8, A - 8);
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 fr[NK][8], er[NK][8];
-  auto load_e = [&](int pg) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int pq = min(pg + q, len - 1);
-#pragma unroll
-      for (int kb = 0; kb < NK; ++kb) er[kb][q] = __builtin_bit_cast(u32x4, ld8(Eb + (size_t)pq * A + k0c[kb]));
-    }
-  };
-  auto load_f = [&](int pg) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int pq = min(pg + q, len - 1);
-#pragma unroll
-      for (int kb = 0; kb < NK; ++kb) fr[kb][q] = __builtin_bit_cast(u32x4, ld8(Fb + (size_t)pq * A + k0c[kb]));
-    }
-  };
-  // group 0 rows first: nothing below depends on them until the first dot
-  if (p0 < len) {
-    load_e(p0);
-    load_f(p0);
-  }
-  // per-lane feature parameters (pre-scaled for the r-form)
-  float dk[NK][8];
-  f32x2 s2[NK][4], w2[NK][4], v4w[NK][4], acc[NK][4];
-#pragma unroll
-  for (int kb = 0; kb < NK; ++kb) {
-    const int k0 = kb * 512 + lane * 8;
-#pragma unroll
-    for (int jp = 0; jp < 4; ++jp) {
-      float sv[2], wv[2], vv[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = k0 + 2 * jp + h;
-        const bool ok = k < A;
-        sv[h] = ok ? s[(size_t)b * A + k] : 0.f;
-        vv[h] = ok ? v[k] : 0.f;
-        wv[h] = (ok && wc) ? wc[k] : 0.f;
-        dk[kb][2 * jp + h] = ok ? dctx[(size_t)b * A + k] : 0.f;
-      }
-      s2[kb][jp] = f32x2{sv[0], sv[1]} * K2LOG2E;
-      w2[kb][jp] = f32x2{wv[0], wv[1]} * K2LOG2E;
-      v4w[kb][jp] = f32x2{4.f * vv[0] * wv[0], 4.f * vv[1] * wv[1]};
-      acc[kb][jp] = f32x2{0.f, 0.f};
-    }
-  }
-  // per-position scalars of this wave's 8*NG positions, one per lane
-  float a_l = 0.f, r_l = 0.f, c_l = 0.f, dn_l = 0.f;
-  {
-    const int p = p0 + (lane & (8 * NG - 1));
-    if (p < len) {
-      const size_t ix = rb + p;
-      a_l = a[ix];
-      c_l = cov ? cov[ix] : 0.f;
-      r_l = (Ga ? Ga[ix] : 0.f) + (dcov_next ? dcov_next[ix] : 0.f);
-      if (gcl && a_l <= c_l) r_l += g;
-    }
-    if (p < T && dcov_next) dn_l = dcov_next[rb + p];
-  }
-  // S = sum_j a_j r_j + dctx . ctx
-  float S = 0.f;
-  for (int i = tid; i < len; i += 256) {
-    const size_t ix = rb + i;
-    const float ai = a[ix];
-    float r = (Ga ? Ga[ix] : 0.f) + (dcov_next ? dcov_next[ix] : 0.f);
-    if (gcl && ai <= (cov ? cov[ix] : 0.f)) r += g;
-    S += ai * r;
-  }
-  for (int k = tid; k < A; k += 256) S += dctx[(size_t)b * A + k] * ctx[(size_t)b * A + k];
-  S = block_sum<256>(S, red);
-  const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1;
-  const int qm = 4 * b5 + 2 * b4 + b3;  // the position whose totals this lane's group holds
-#pragma unroll
-  for (int grp = 0; grp < NG; ++grp) {
-    const int pg = p0 + grp * 8;
-    if (pg >= len) {  // wave-uniform: this and every later group lie past len -> pass dcov through
-      for (int i = lane; i < 8 * (NG - grp); i += 64) {
-        const int p = pg + i;
-        if (p < T) {
-          de_out[rb + p] = 0.f;
-          if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
-        }
-      }
-      break;
-    }
-    const bool more = grp + 1 < NG && pg + 8 < len;
-    // da: partial dctx . E_q, reduced
-    float pd[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      f32x2 d2 = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int kb = 0; kb < NK; ++kb)
-#pragma unroll
-        for (int jp = 0; jp < 4; ++jp)
-          d2 = fma2(bf2pair(er[kb][q][jp]), f32x2{dk[kb][2 * jp], dk[kb][2 * jp + 1]}, d2);
-      pd[q] = d2.x + d2.y;
-    }
-    if (more) load_e(pg + 8);
-    const float dot = bfly8(pd, b5, b4, b3);
-    const int src = grp * 8 + qm;
-    const float a_q = __shfl(a_l, src, 64), r_q = __shfl(r_l, src, 64);
-    const float c_q = __shfl(c_l, src, 64), dn_q = __shfl(dn_l, src, 64);
-    const float de_q = (pg + qm < len) ? a_q * (r_q + dot - S) : 0.f;
-    // tanh pass: ds accumulation and dcov partials
-    float dcv[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      // the lanes holding position q's totals start at 32*b5 + 16*b4 + 8*b3
-      const float de = rdlane(de_q, ((q >> 2) << 5) | (((q >> 1) & 1) << 4) | ((q & 1) << 3));
-      const float c = rdlane(c_l, grp * 8 + q);
-      f32x2 dc2 = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int kb = 0; kb < NK; ++kb)
-#pragma unroll
-        for (int jp = 0; jp < 4; ++jp) {
-          const f32x2 y = fma2(bf2pair(fr[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
-          const f32x2 r = rsig2(y);
-          const f32x2 qv = fma2(-r, r, r);
-          acc[kb][jp] = fma2(qv, splat2(de), acc[kb][jp]);
-          dc2 = fma2(qv, v4w[kb][jp], dc2);
-        }
-      dcv[q] = dc2.x + dc2.y;
-    }
-    if (more) load_f(pg + 8);
-    const float hc = bfly8(dcv, b5, b4, b3);
-    if ((lane & 7) == 0) {
-      const int p = pg + qm;
-      if (p < T) {
-        const size_t ix = rb + p;
-        de_out[ix] = de_q;
-        if (dcov_out) {
-          float r = dn_q;
-          if (p < len) {
-            r += de_q * hc;
-            if (gcl && a_q > c_q) r += g;
-          }
-          dcov_out[ix] = r;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int kb = 0; kb < NK; ++kb) {
-    const int k0 = kb * 512 + lane * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bool ok = k0 + j < A;
-      part[wid][kb * 512 + lane * 8 + j] = ok ? 4.f * v[ok ? k0 + j : 0] * acc[kb][j >> 1][j & 1] : 0.f;
-    }
-  }
-  __syncthreads();
-  float* out = ds + (size_t)b * A;
-  for (int k = tid; k < A; k += 256) {
-    const float x = part[0][k] + part[1][k] + part[2][k] + part[3][k];
-    atomicAdd(out + k, x);
-  }
-}
+// S needs no pass over da (its dctx.E half is dctx.ctx), so every block is independent and one
+// launch per decoder step does it all.  Lanes on the feature axis (8 per lane, NK blocks of 512);
+// per group of positions the partial dctx.E_i dots are reduced with a butterfly
+// reduce-scatter (the lanes of position q end up holding its total), de_q is broadcast with
+// v_readlane, then the r-form tanh pass (packed fp32, see rsig2) accumulates ds and the dcov
+// partials, reduced the same way.   v_k sech2(u) = 4 v_k r (1 - r)  ->  ds_k = 4 v_k sum_i de_i q_ik.
+// The row-resident attn_bwd_row (attention_row.hip) replaces this kernel at A = 512 and B >= 128.
 
 // Same math with 4 positions per group (NG4 groups per wave): the E/F rows in flight per
 // lane halve (32 instead of 64 VGPRs), which buys a third wave per SIMD at the 168-VGPR cap.
@@ -929,21 +536,13 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
   }
 }
 
-// A/B switch for tuning runs: TSAMD_ATTN_SW=8 forces the 8-wave variants.
-static int attn_sw(int A) {
-  static const int forced = [] { const char* e = getenv("TSAMD_ATTN_SW"); return e ? atoi(e) : 0; }();
-  if (forced == 8) return 8;
-  return A % 128 == 0 ? 16 : 8;
-}
-
 void launch_attn_score(const bf16* Ft, const float* s, const float* v, const float* wc, const float* cov,
                        const int* lens, float* e, int B, int T, int A, int rep, hipStream_t st) {
   dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B / rep);
-  // rep = 1 (training, B = 256): 8 waves per block measured 23.3 vs 24.5 us; rep = 4 (beam
-  // decode, 64 articles): 16 waves, 14.5 vs 14.7 ms per batch
-  const bool w16 = attn_sw(A) == 16 && rep > 1;
-  static const int xcd = getenv("TSAMD_SCORE_XCD") ? atoi(getenv("TSAMD_SCORE_XCD")) : 1;
-#define LS(SW, RP) hipLaunchKernelGGL((attn_score_kernel<SW, RP>), grid, dim3(SW * 64), 0, st, Ft, s, v, wc, cov, lens, e, T, A, xcd)
+  // rep = 1 (training, B < 128): 8 waves per block measured 23.3 vs 24.5 us; rep = 4 (beam
+  // decode through these kernels): 16 waves when A % 128 == 0, 14.5 vs 14.7 ms per batch
+  const bool w16 = A % 128 == 0 && rep > 1;
+#define LS(SW, RP) hipLaunchKernelGGL((attn_score_kernel<SW, RP>), grid, dim3(SW * 64), 0, st, Ft, s, v, wc, cov, lens, e, T, A, 1)
   if (rep == 4) { if (w16) LS(16, 4); else LS(8, 4); }
   else if (rep == 2) { if (w16) LS(16, 2); else LS(8, 2); }
   else { if (w16) LS(16, 1); else LS(8, 1); }
@@ -960,100 +559,30 @@ void launch_attn_softmax_ctx(const float* e, const bf16* E, const int* lens, con
   else LC(1);
 #undef LC
 }
-void launch_attn_bwd_da(const bf16* Et, const float* dctx, const float* Ga, const float* dcov_next, const float* a,
-                        const float* cov, const float* gcl, const int* lens, float* da, int B, int T, int A,
-                        hipStream_t st) {
-  dim3 grid((T + SCORE_POS - 1) / SCORE_POS, B);
-  if (attn_sw(A) == 16)
-    hipLaunchKernelGGL(attn_bwd_da_kernel<16>, grid, dim3(1024), 0, st, Et, dctx, Ga, dcov_next, a, cov, gcl, lens, da,
-                       T, A);
-  else
-    hipLaunchKernelGGL(attn_bwd_da_kernel<8>, grid, dim3(512), 0, st, Et, dctx, Ga, dcov_next, a, cov, gcl, lens, da,
-                       T, A);
-}
 int attn_nchunk(int T) { return (T + 63) / 64; }
-void launch_attn_bwd_tanh(const bf16* F, const float* s, const float* v, const float* wc, const float* cov,
-                          const float* a, const float* da, const float* dcov_next, const float* gcl, const int* lens,
-                          float* de_out, float* ds, float* dcov_out, int B, int T, int A, hipStream_t st) {
-  dim3 grid(attn_nchunk(T), B);
-  if (A <= 512)
-    hipLaunchKernelGGL(attn_bwd_tanh_kernel<1>, grid, dim3(256), 0, st, F, s, v, wc, cov, a, da, dcov_next, gcl, lens,
-                       de_out, ds, dcov_out, T, A);
-  else
-    hipLaunchKernelGGL(attn_bwd_tanh_kernel<2>, grid, dim3(256), 0, st, F, s, v, wc, cov, a, da, dcov_next, gcl, lens,
-                       de_out, ds, dcov_out, T, A);
-}
 void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
                           float* dcov_out, int B, int T, int A, hipStream_t st) {
-  // groups of 8 positions per wave; TSAMD_ATTN_NG=2 selects 64-position blocks (A/B runs).
-  // TSAMD_ATTN_OCC=3|4 caps the registers for 3|4 waves per SIMD (tuning runs).
-  static const int ng = [] { const char* e = getenv("TSAMD_ATTN_NG"); return e && atoi(e) == 2 ? 2 : 4; }();
-  static const int occ = [] { const char* e = getenv("TSAMD_ATTN_OCC"); return e ? atoi(e) : 0; }();
-  dim3 grid((T + 32 * ng - 1) / (32 * ng), B);
-#define LB(NK, NG, OC) hipLaunchKernelGGL((attn_bwd_step_kernel<NK, NG, OC>), grid, dim3(256), 0, st, E, F, s, v, wc, \
-                                          cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A)
-  // Default: the 4-positions-per-group kernel capped at 126 VGPRs (4 waves per SIMD): 54 us vs
-  // 61 us for the 8-position kernel at B = 256, T = 400 (tools/attn_micro.py).  TSAMD_ATTN_P4=0
-  // selects the 8-position kernel; 1 / 3 the 4-position one uncapped / at 3 waves per SIMD.
-  static const int p4 = [] { const char* e = getenv("TSAMD_ATTN_P4"); return e ? atoi(e) : 2; }();
-  // A = 1024 (config #5): 4-position groups with 16 features per lane at 208 VGPRs (2 waves per
-  // SIMD; the 8-position kernel below needs 316 registers, 1 wave), 64 positions per wave = 256
-  // per block so each row's S prologue is paid by 4 blocks, not 7: 198 us vs 250 us per launch
-  // at 256 rows x T = 800 (tools/attn_bwd_a1024_micro.py; 32 positions per wave: 217 us).
-  // TSAMD_ATTN_P4K2 = 0 selects the 8-position kernel; 1 / 2 / 3 / 4 the 32-position-per-wave
-  // kernel uncapped / OCC 2 / OCC 3 / 16 positions per wave (A/B runs).
-  static const int p4k2 = [] { const char* e = getenv("TSAMD_ATTN_P4K2"); return e ? atoi(e) : 5; }();
-#define L4(OC, NK) hipLaunchKernelGGL((attn_bwd_step4_kernel<8, OC, NK>), dim3((T + 127) / 128, B), dim3(256), 0, st, E, \
-                                      F, s, v, wc, cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A)
-  if (A <= 512 && p4 > 0) {
-    if (p4 == 3) L4(3, 1);
-    else if (p4 == 2) L4(2, 1);
-    else L4(1, 1);
-    return;
-  }
-  if (A > 512 && A <= 1024 && p4k2 > 0) {
-    if (p4k2 == 4) {
-      hipLaunchKernelGGL((attn_bwd_step4_kernel<4, 2, 2>), dim3((T + 63) / 64, B), dim3(256), 0, st, E, F, s, v, wc, cov,
-                         a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A);
-    } else if (p4k2 == 5) {
-      hipLaunchKernelGGL((attn_bwd_step4_kernel<16, 2, 2>), dim3((T + 255) / 256, B), dim3(256), 0, st, E, F, s, v, wc,
-                         cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A);
-    } else if (p4k2 == 3) L4(3, 2);
-    else if (p4k2 == 2) L4(2, 2);
-    else L4(1, 2);
-    return;
-  }
-#undef L4
-  if (A <= 512) {
-    if (ng == 2) LB(1, 2, 1);
-    else if (occ == 3) LB(1, 4, 3);
-    else if (occ == 4) LB(1, 4, 4);
-    else LB(1, 4, 1);
-  } else {
-    if (ng == 2) LB(2, 2, 1); else LB(2, 4, 1);
-  }
-#undef LB
+  // A <= 512: 4-position groups, 8 groups per wave (128 positions per block), 2 waves per SIMD
+  // cap: 54 us vs 61 us for an 8-position kernel at B = 256, T = 400 (tools/attn_micro.py).
+  // A = 1024 (config #5): 16 features per lane at 208 VGPRs (2 waves per SIMD), 64 positions
+  // per wave = 256 per block so each row's S prologue is paid by 4 blocks, not 7: 198 us vs
+  // 250 us per launch at 256 rows x T = 800 (tools/attn_bwd_a1024_micro.py).
+  if (A <= 512)
+    hipLaunchKernelGGL((attn_bwd_step4_kernel<8, 2, 1>), dim3((T + 127) / 128, B), dim3(256), 0, st, E, F, s, v, wc,
+                       cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A);
+  else
+    hipLaunchKernelGGL((attn_bwd_step4_kernel<16, 2, 2>), dim3((T + 255) / 256, B), dim3(256), 0, st, E, F, s, v, wc,
+                       cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, A);
 }
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, bf16* dF, float* dv, float* dwc, int D, int B, int T,
                           int A, int nslot, hipStream_t st) {
-  // Default (2): 4 positions per wave capped at 128 VGPRs = 4 waves/SIMD (a few prologue
-  // spills): 1.51 ms vs 1.64 ms uncapped at 3 waves/SIMD (B = 256, T = 400, D = 100).
-  // TSAMD_FEAT_V=0: uncapped; 1: 2 positions per wave (1.65 ms).
-  static const int fv = [] { const char* e = getenv("TSAMD_FEAT_V"); return e ? atoi(e) : 2; }();
-  if (fv == 1) {
-    dim3 grid((T + 7) / 8, B, (A + 511) / 512);
-    hipLaunchKernelGGL((attn_bwd_feat_kernel<2, 1>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
-                       dv, dwc, D, B, T, A, nslot);
-  } else if (fv == 2) {
-    dim3 grid((T + 15) / 16, B, (A + 511) / 512);
-    hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 4>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
-                       dv, dwc, D, B, T, A, nslot);
-  } else {
-    dim3 grid((T + 15) / 16, B, (A + 511) / 512);
-    hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 1>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
-                       dv, dwc, D, B, T, A, nslot);
-  }
+  // 4 positions per wave capped at 128 VGPRs = 4 waves/SIMD (a few prologue spills): 1.51 ms
+  // vs 1.64 ms uncapped at 3 waves/SIMD and 1.65 ms with 2 positions per wave (B = 256,
+  // T = 400, D = 100)
+  dim3 grid((T + 15) / 16, B, (A + 511) / 512);
+  hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 4>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
+                     dv, dwc, D, B, T, A, nslot);
 }

@@ -58,22 +58,9 @@ __device__ __forceinline__ void load_rows(Rows<NK>& r, const bf16* base, int p0,
 }  // namespace
 
 // ------------------------------------------------------------------------------ forward
-// Optional attention-query projection in the prologue (training, rep = 1): with WsT set, the
-// row's s = [c, h] . W_s + b_s (reference attention_decoder.py:93; K = 2H = A) is computed here
-// -- 8 lanes per output feature, each reading 128 contiguous bytes of its W_s^T row per load,
-// dpp_sum8 across them -- and stored to s (the backward reads it), instead of by a separate
-// linear2 launch between the decoder cell and this kernel.  Group 0's F / E rows are already in
-// flight while it runs.
-struct SProj {
-  const bf16* c;    // [B][H] bf16 (nullptr: s is an input)
-  const bf16* h;    // [B][H] bf16
-  const bf16* WsT;  // [A][2H] bf16
-  const float* bs;  // [A]
-};
-
 template <int NK, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
-    const bf16* __restrict__ F, const bf16* __restrict__ E, float* __restrict__ s, SProj sp,
+    const bf16* __restrict__ F, const bf16* __restrict__ E, const float* __restrict__ s,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
     const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
     float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T, int rep, int xper) {
@@ -81,7 +68,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
   __shared__ float es[kRowMaxT];
   __shared__ float part[NW][A];
   __shared__ float wm[NW], wl[NW], red[NW];
-  __shared__ float s_sh[A];
   // xper > 0 (beam decode): workgroups are dispatched to the 8 XCDs round-robin, so workgroup
   // i runs on XCD i % 8; give XCD x the xper consecutive rows x * xper .. -- whole articles --
   // so the rep hypotheses of an article read its F / E rows through ONE XCD's L2
@@ -105,34 +91,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
   };
   if (wid < ngrp) load(wid, fA, eA, cA);
   const float* srow = s + (size_t)b * A;
-  if (sp.WsT) {
-    constexpr int H = A / 2;
-    const int l8 = lane & 7;
-    bf16x8 xr[A / 64];  // this lane's K chunks of x = [c, h]: elements 64 j + 8 l8 .. + 7
-#pragma unroll
-    for (int j = 0; j < A / 64; ++j) {
-      const int kx = 64 * j + 8 * l8;
-      xr[j] = kx < H ? ld8(sp.c + (size_t)b * H + kx) : ld8(sp.h + (size_t)b * H + kx - H);
-    }
-    for (int n = tid >> 3; n < A; n += NT / 8) {
-      const bf16* wr = sp.WsT + (size_t)n * A + 8 * l8;
-      f32x2 d2 = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < A / 64; ++j) {
-        const u32x4 wv = __builtin_bit_cast(u32x4, ld8(wr + 64 * j));
-        const u32x4 xv = __builtin_bit_cast(u32x4, xr[j]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) d2 = fma2(bf2pair(wv[q]), bf2pair(xv[q]), d2);
-      }
-      const float sn = dpp_sum8(d2.x + d2.y) + sp.bs[n];
-      if (l8 == 0) {
-        s_sh[n] = sn;
-        s[(size_t)b * A + n] = sn;
-      }
-    }
-    __syncthreads();
-    srow = s_sh;
-  }
   // per-lane feature parameters, pre-scaled for the r-form (attn_common.h)
   f32x2 s2[NK][4], w2[NK][4], v2[NK][4], acc[NK][4];
   float vsum = 0.f;
@@ -254,15 +212,11 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
     const float* __restrict__ a, const float* __restrict__ dctx, const float* __restrict__ ctx,
     const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
     const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
-    float* __restrict__ dcov_out, int T, float* __restrict__ ds1) {
+    float* __restrict__ dcov_out, int T) {
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float part[NW][A];
   __shared__ float red[NW];
-  // ds1 set: TWO workgroups per row (blocks 2b, 2b + 1), their 2 NW waves dealing the row's
-  // position groups round-robin, so a row's chain of groups runs on two CUs; each stores its
-  // partial ds (to ds / ds1: the consumer, dec_bwd_cell, adds them).  S is computed by both.
-  const int parts = ds1 ? 2 : 1;
-  const int b = blockIdx.x / parts, pt = blockIdx.x % parts;
+  const int b = blockIdx.x;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
@@ -287,8 +241,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
     x.dn = dcov_next ? dcov_next[ix] : 0.f;
     x.r = (Ga ? Ga[ix] : 0.f) + x.dn + ((gcl && x.a <= x.c) ? g : 0.f);
   };
-  const int gw = pt * NW + wid, NWT = parts * NW;  // this wave's index among the row's waves
-  if (gw < ngrp) load(gw, eA, fA, xA);
+  if (wid < ngrp) load(wid, eA, fA, xA);
   float dk[NK][8];
   f32x2 s2[NK][4], w2[NK][4], v4w[NK][4], acc[NK][4];
 #pragma unroll
@@ -367,18 +320,18 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
       }
     }
   };
-  for (int gi = gw; gi < ngrp;) {
-    const int g1 = gi + NWT;
+  for (int gi = wid; gi < ngrp;) {
+    const int g1 = gi + NW;
     if (g1 < ngrp) load(g1, eB, fB, xB);
     compute(gi, eA, fA, xA);
     if (g1 >= ngrp) break;
-    const int g2 = g1 + NWT;
+    const int g2 = g1 + NW;
     if (g2 < ngrp) load(g2, eA, fA, xA);
     compute(g1, eB, fB, xB);
     gi = g2;
   }
   // positions past the last group: de = 0, dcov passes through
-  for (int p = 4 * ngrp + tid; pt == 0 && p < T; p += NT) {
+  for (int p = 4 * ngrp + tid; p < T; p += NT) {
     de_out[rb + p] = 0.f;
     if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
   }
@@ -390,29 +343,25 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
       *reinterpret_cast<float2*>(&part[wid][kb * 512 + lane * 8 + 2 * jp]) =
           make_float2(acc[kb][jp].x, acc[kb][jp].y);
   __syncthreads();
-  float* dsp = pt ? ds1 : ds;
   for (int k = tid; k < A; k += NT) {
     float x = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) x += part[w][k];
-    dsp[(size_t)b * A + k] = 4.f * v[k] * x;
+    ds[(size_t)b * A + k] = 4.f * v[k] * x;
   }
 }
 
 // ------------------------------------------------------------------------------ launchers
 bool attn_row_supported(int A, int T) { return (A == 512 || A == 1024) && T >= 1 && T <= kRowMaxT; }
 
-void launch_attn_fwd_row(const bf16* F, const bf16* E, float* s, const bf16* sc, const bf16* sh, const bf16* WsT,
-                         const float* bs, const float* v, const float* wc, const float* cov, const int* lens,
-                         float* a_out, float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A,
-                         int rep, hipStream_t st) {
-  const SProj sp{sc, sh, WsT, bs};
-  // TSAMD_ATTN_XCD=0 keeps the identity workgroup -> row map for beam decode (A/B runs)
-  static const bool xcd = [] { const char* e = getenv("TSAMD_ATTN_XCD"); return !(e && atoi(e) == 0); }();
-  const int xper = (xcd && rep > 1 && B % 8 == 0 && (B / 8) % rep == 0) ? B / 8 : 0;
+void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
+                         const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
+                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st) {
+  // beam decode: each XCD takes whole articles (their hypotheses share F / E rows in its L2)
+  const int xper = (rep > 1 && B % 8 == 0 && (B / 8) % rep == 0) ? B / 8 : 0;
 #define LF(NK)                                                                                                 \
   hipLaunchKernelGGL((attn_fwd_row_kernel<NK, row_waves<NK, false>()>), dim3(B), dim3(row_waves<NK, false>() * 64), \
-                     0, st, F, E, s, sp, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep, xper)
+                     0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep, xper)
   if (A == 512) LF(1);
   else LF(2);
 #undef LF
@@ -421,11 +370,10 @@ void launch_attn_fwd_row(const bf16* F, const bf16* E, float* s, const bf16* sc,
 void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
                          const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
                          const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                         float* dcov_out, int B, int T, int A, float* ds1, hipStream_t st) {
-  const int nb = ds1 ? 2 * B : B;
+                         float* dcov_out, int B, int T, int A, hipStream_t st) {
 #define LB(NK)                                                                                                \
-  hipLaunchKernelGGL((attn_bwd_row_kernel<NK, row_waves<NK, true>()>), dim3(nb), dim3(row_waves<NK, true>() * 64), \
-                     0, st, E, F, s, v, wc, cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, ds1)
+  hipLaunchKernelGGL((attn_bwd_row_kernel<NK, row_waves<NK, true>()>), dim3(B), dim3(row_waves<NK, true>() * 64), \
+                     0, st, E, F, s, v, wc, cov, a, dctx, ctx, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T)
   if (A == 512) LB(1);
   else LB(2);
 #undef LB

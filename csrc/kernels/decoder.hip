@@ -218,10 +218,10 @@ __global__ __launch_bounds__(256) void pgen_dirs_kernel(const float* __restrict_
 // Backward of s-projection + LSTM cell for step t.  grid (H/16, ceil(B/16)).
 //   dc_t = ds . W_s[0:H]^T + dC_dir + dc_carry ;  dh_t = ds . W_s[H:2H]^T + dH_dir + dh_rec
 //   cell backward -> dz_t (bf16), dc_carry <- dc_total * f
-// ds (fp32 [B][A]) was accumulated by attn_bwd_tanh's blocks with atomics, or stored by
-// attn_bwd_row -- as two partials ds + ds2 when that kernel runs two workgroups per row.
+// ds (fp32 [B][A]) was accumulated by attn_bwd_step's blocks with atomics, or stored by
+// attn_bwd_row.
 __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
-    const float* __restrict__ ds, const float* __restrict__ ds2,
+    const float* __restrict__ ds,
     const bf16* __restrict__ Ws,                                               // Ws: [2H][A] (TF Matrix)
     const float* __restrict__ dC_dir, const float* __restrict__ dH_dir,       // [B][H] (nullable)
     const float* __restrict__ dh_rec, float* __restrict__ dc_carry,            // [B][H]
@@ -248,13 +248,12 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
   const int ar = min(r0 + (lane & 15), B - 1);
   const int kof = 8 * (lane >> 4);
   const float* arow = ds + (size_t)ar * A + kof;
-  const float* arow2 = ds2 ? ds2 + (size_t)ar * A + kof : arow;
   const bf16* bc = Ws + (size_t)(u0 + (lane & 15)) * A + kof;
   const bf16* bh = Ws + (size_t)(H + u0 + (lane & 15)) * A + kof;
   const int nst = A / 32;
   const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
   f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
-  kslice_mma<2>([&](int k) { return ds2 ? ld8f2(arow + k, arow2 + k) : ld8f(arow + k); },
+  kslice_mma<2>([&](int k) { return ld8f(arow + k); },
                 [&](int j, int k) { return ld8((j == 0 ? bc : bh) + k); }, k0, k1, acc);
   float o[2];
   ksplit_reduce<2>(acc, red, o);
@@ -313,22 +312,13 @@ __global__ __launch_bounds__(256) void dec_bwd_dz_kernel(
 }
 
 // dec_cell_fwd with 6-step load batches: 7.67 -> 6.79 us per call at hidden 256 / 128 rows (one
-// L2 round trip instead of two), equal at hidden 512; B = 256 train 19.71-19.77 -> 19.63-19.67 ms
-// (profiles/r2/ab/dec_cell_kb.jsonl).  TSAMD_DEC_KB=0 keeps 4-step batches (A/B runs).
-static bool dec_deep_batches() {
-  static const bool on = [] { const char* e = getenv("TSAMD_DEC_KB"); return !(e && atoi(e) == 0); }();
-  return on;
-}
-
+// L2 round trip instead of two with 4-step batches), equal at hidden 512; B = 256 train
+// 19.71-19.77 -> 19.63-19.67 ms (profiles/r2/ab/dec_cell_kb.jsonl)
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16);
-  if (dec_deep_batches())
-    hipLaunchKernelGGL(dec_cell_fwd_kernel<6>, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out,
-                       hb_out, act, B, H, A);
-  else
-    hipLaunchKernelGGL(dec_cell_fwd_kernel<4>, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out,
-                       hb_out, act, B, H, A);
+  hipLaunchKernelGGL(dec_cell_fwd_kernel<6>, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out,
+                     hb_out, act, B, H, A);
 }
 void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
                     const float* add, float* out, bf16* outb, int B, int N, hipStream_t st) {
@@ -366,11 +356,11 @@ void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x
                  float* pg, int R, int A, int H, int E, hipStream_t st) {
   hipLaunchKernelGGL(pgen_kernel, dim3((R + 3) / 4), dim3(256), 0, st, ctx, c, h, x, w, b, pg, R, A, H, E);
 }
-void launch_dec_bwd_cell(const float* ds, const float* ds2, const bf16* Ws, const float* dC_dir, const float* dH_dir,
+void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,
                          const float* c_prev, bf16* dz, int B, int H, int A, hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16);
-  hipLaunchKernelGGL(dec_bwd_cell_kernel, grid, dim3(256), 0, st, ds, ds2, Ws, dC_dir, dH_dir, dh_rec, dc_carry, act,
+  hipLaunchKernelGGL(dec_bwd_cell_kernel, grid, dim3(256), 0, st, ds, Ws, dC_dir, dH_dir, dh_rec, dc_carry, act,
                      c_now, c_prev, dz, B, H, A);
 }
 void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, const float* dCTX_dir_prev,

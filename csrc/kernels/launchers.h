@@ -14,13 +14,7 @@ void launch_attn_score(const bf16* F, const float* s, const float* v, const floa
 void launch_attn_softmax_ctx(const float* e, const bf16* E, const int* lens, const float* cov, float* a_out,
                              float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A, int rep,
                              hipStream_t st);
-void launch_attn_bwd_da(const bf16* E, const float* dctx, const float* Ga, const float* dcov_next, const float* a,
-                        const float* cov, const float* gcl, const int* lens, float* da, int B, int T, int A,
-                        hipStream_t st);
 int attn_nchunk(int T);
-void launch_attn_bwd_tanh(const bf16* F, const float* s, const float* v, const float* wc, const float* cov,
-                          const float* a, const float* da, const float* dcov_next, const float* gcl, const int* lens,
-                          float* de_out, float* ds, float* dcov_out, int B, int T, int A, hipStream_t st);
 void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
@@ -30,22 +24,19 @@ void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, con
                           int A, int nslot, hipStream_t st);
 
 bool attn_row_supported(int A, int T);
-// s: the attention query [B][A] -- an input, or (WsT set: s = [sc, sh] . WsT^T + bs computed in
-// the kernel, rep = 1) an output
-void launch_attn_fwd_row(const bf16* F, const bf16* E, float* s, const bf16* sc, const bf16* sh, const bf16* WsT,
-                         const float* bs, const float* v, const float* wc, const float* cov, const int* lens,
-                         float* a_out, float* cov_out, float* covloss, float* ctx, bf16* ctx_bf, int B, int T, int A,
-                         int rep, hipStream_t st);
+void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
+                         const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
+                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st);
 void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
                          const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
                          const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                         float* dcov_out, int B, int T, int A, float* ds1, hipStream_t st);
+                         float* dcov_out, int B, int T, int A, hipStream_t st);
 
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st);
 void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out, int B, int H,
                       int A, hipStream_t st);
-void launch_dec_bwd_cell(const float* ds, const float* ds2, const bf16* Ws, const float* dC_dir, const float* dH_dir,
+void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,
                          const float* c_prev, bf16* dz, int B, int H, int A, hipStream_t st);
 void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, const float* dCTX_dir_prev,

@@ -622,23 +622,11 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
 // Kernel variants (measured, tools/lstm_micro.py): the forward runs 4 waves per workgroup
 // (16 units per wave) up to H = 256 and 8 waves (8 units per wave) at H = 512, where the
 // 4-wave forward would need 256 VGPRs of W_hh per lane; the backward runs 8 waves (2 rows
-// per lane in the cell update) at every H -- 4.0 vs 4.6 us per step at H = 256, B = 256.
-// TSAMD_LSTM_NW=4/8 forces one variant for both below H = 512 (A/B experiments).
-static int lstm_nw(int H, bool bwd) {
-  if (H == 512) return 8;
-  const char* e = getenv("TSAMD_LSTM_NW");  // read per call: tests switch it in-process
-  if (e && (atoi(e) == 4 || atoi(e) == 8)) return atoi(e);
-  return bwd ? 8 : 4;
-}
-
-// Non-temporal activation traffic: forward yes (H = 512, B = 256: 7.06 -> 6.83 us per step;
-// H = 256: 3.14 -> 3.00), BPTT no (8.22 -> 8.41: its NT variant spills 20 bytes).
-// TSAMD_LSTM_NT = 0 / 1 / 2: none / both / forward only (default; read per call, A/B runs).
-static int lstm_nt(bool bwd) {
-  const char* e = getenv("TSAMD_LSTM_NT");
-  const int v = e ? atoi(e) : 2;
-  return v == 1 || (v == 2 && !bwd) ? 1 : 0;
-}
+// per lane in the cell update) at every H -- 4.0 vs 4.6 us per step for 4 waves at H = 256,
+// B = 256.  Activation traffic is non-temporal in the forward (H = 512, B = 256: 7.06 -> 6.83
+// us per step; H = 256: 3.14 -> 3.00) and cached in the BPTT (its NT variant spills: 8.22 ->
+// 8.41).
+static int lstm_nw(int H) { return H == 512 ? 8 : 4; }  // forward waves per workgroup
 
 static bool lstm_h_ok(int H) { return H == 64 || H == 128 || H == 256 || H == 512; }
 
@@ -658,11 +646,9 @@ int lstm_persistent_capacity(int H) {
 #define OCC(HH)                                                                                                    \
   if (H == HH) {                                                                                                   \
     ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[0], lstm_bwd_persistent_kernel<HH, 8, false>, 512, 0) == hipSuccess; \
-    ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[1], lstm_fwd_persistent8_kernel<HH, false>, 512, 0) == hipSuccess; \
+    ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[1], lstm_fwd_persistent8_kernel<HH, true>, 512, 0) == hipSuccess; \
     if (HH <= 256) {                                                                                               \
-      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[2], lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4, false>, \
-                                                         256, 0) == hipSuccess;                                    \
-      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[3], lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), false>, \
+      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[3], lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), true>, \
                                                          256, 0) == hipSuccess;                                    \
     }                                                                                                              \
   }
@@ -703,8 +689,7 @@ size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {
 void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
                                 int H, hipStream_t st) {
-  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H, false);
-  const int nt = lstm_nt(false);
+  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H);
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
@@ -717,17 +702,10 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
   else                                                                                                          \
     hipLaunchKernelGGL((lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), NTV>), dim3(grid), dim3(256), 0, st, \
                        gx, bias, Wt, hs, cs, acts, out, lens, xb, e, T, B, ntile, t0, n)
-    if (nt) {
-      if (H == 64) LAUNCH_F(64, true);
-      else if (H == 128) LAUNCH_F(128, true);
-      else if (H == 256) LAUNCH_F(256, true);
-      else LAUNCH_F(512, true);
-    } else {
-      if (H == 64) LAUNCH_F(64, false);
-      else if (H == 128) LAUNCH_F(128, false);
-      else if (H == 256) LAUNCH_F(256, false);
-      else LAUNCH_F(512, false);
-    }
+    if (H == 64) LAUNCH_F(64, true);
+    else if (H == 128) LAUNCH_F(128, true);
+    else if (H == 256) LAUNCH_F(256, true);
+    else LAUNCH_F(512, true);
 #undef LAUNCH_F
   }
 }
@@ -735,31 +713,19 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, float* dbias, int T, int B, int H, hipStream_t st) {
-  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H, true);
-  const int nt = lstm_nt(true);
+  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64;
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
   for (int t0 = 0; t0 < ntile; t0 += nl) {
     const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
 #define LAUNCH_B(HH, NTV)                                                                                                 \
-  if (nw == 8)                                                                                                       \
-    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin, \
-                       dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n);                                  \
-  else                                                                                                               \
-    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<(HH <= 256 ? HH : 256), 4, NTV>), dim3(grid), dim3(256), 0, st, dz, \
-                       Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
-    if (nt) {
-      if (H == 64) LAUNCH_B(64, true);
-      else if (H == 128) LAUNCH_B(128, true);
-      else if (H == 256) LAUNCH_B(256, true);
-      else LAUNCH_B(512, true);
-    } else {
-      if (H == 64) LAUNCH_B(64, false);
-      else if (H == 128) LAUNCH_B(128, false);
-      else if (H == 256) LAUNCH_B(256, false);
-      else LAUNCH_B(512, false);
-    }
+  hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin,   \
+                     dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+    if (H == 64) LAUNCH_B(64, false);
+    else if (H == 128) LAUNCH_B(128, false);
+    else if (H == 256) LAUNCH_B(256, false);
+    else LAUNCH_B(512, false);
 #undef LAUNCH_B
   }
 }

@@ -465,15 +465,10 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
   const int nt = vocab_topk_tiles(V);
   // default: 128-row workgroups (392 at R = 256, V = 50k: one round at 2 per CU; W^T fragments
   // fetched once per 128 rows): decode 5610 -> 5927 summaries/s at 64 articles, 6940 -> 7300 at
-  // 128.  TSAMD_VL_RH = 1: 64-row workgroups (784 at R = 256: 1.5 rounds)
-  static const int rh = [] { const char* e = getenv("TSAMD_VL_RH"); return e && atoi(e) == 1 ? 1 : 2; }();
-  const int RB = (R + VT_ROWS * rh - 1) / (VT_ROWS * rh);
-  if (rh == 2)
-    hipLaunchKernelGGL((vocab_logits_kernel<2, 2>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
-                       part_ms, R, V, H);
-  else
-    hipLaunchKernelGGL((vocab_logits_kernel<2, 1>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
-                       part_ms, R, V, H);
+  // 128 (64-row workgroups, 784 at R = 256, run 1.5 rounds)
+  const int RB = (R + VT_ROWS * 2 - 1) / (VT_ROWS * 2);
+  hipLaunchKernelGGL((vocab_logits_kernel<2, 2>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
+                     part_ms, R, V, H);
   hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
                      out_lp, V, T, K, beam, nt, pgi);
 }

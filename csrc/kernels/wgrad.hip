@@ -10,7 +10,7 @@
 // workgroup, so it can run on a side stream beside the encoder BPTT (pointer_generator.py,
 // TSAMD_DEFER_WGRAD).
 //
-// Tile 128 (m) x 128 (n) per workgroup, 4 waves of 64 x 64, k-steps of 64 (TSAMD_WGRAD_BK=32: 32; 3-5% slower) staged through
+// Tile 128 (m) x 128 (n) per workgroup, 4 waves of 64 x 64, k-steps of 64 (32: 3-5% slower) staged through
 // double-buffered LDS as [k][m] / [k][n] rows (coalesced 16-byte global loads).  The MFMA wants
 // each lane's 8 consecutive k of one m (A) or one n (B): gfx950's ds_read_b64_tr_b16 reads a
 // 4-row x 16-column block and hands lane i of each 16-lane group column i of the 4 rows, so two
@@ -142,15 +142,11 @@ int wgrad_tn_splits(int M, int N, int K) {
 
 void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out, int ldo, int M, int N, int K,
                      hipStream_t st) {
-  static const int bk = getenv("TSAMD_WGRAD_BK") ? atoi(getenv("TSAMD_WGRAD_BK")) : 64;
-  const int WBK = bk == 32 ? 32 : 64;
+  constexpr int WBK = 64;
   const int s = wgrad_tn_splits(M, N, K);
   const int kchunk = ((K + s - 1) / s + WBK - 1) / WBK * WBK;
   const int splits = (K + kchunk - 1) / kchunk;
   const int gm = M / WBM, gn = (N + WBN - 1) / WBN, ny = gn * splits;
   const dim3 grid(gm * ((ny + 7) / 8 * 8));
-  if (WBK == 32)
-    hipLaunchKernelGGL(wgrad_tn_kernel<32>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, N, K, kchunk, gm, gn, ny);
-  else
-    hipLaunchKernelGGL(wgrad_tn_kernel<64>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, N, K, kchunk, gm, gn, ny);
+  hipLaunchKernelGGL(wgrad_tn_kernel<WBK>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, N, K, kchunk, gm, gn, ny);
 }

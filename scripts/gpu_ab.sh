@@ -1,12 +1,12 @@
 #!/bin/bash
 # A/B and profiling runs used while tuning (one GPU).  Usage: bash scripts/gpu_ab.sh <what>
-#   attn1024  attn_bwd_step variants at A = 1024 (TSAMD_ATTN_P4K2), random and full lengths
-#   cfg5      attention tests + config #5 bench, default vs TSAMD_ATTN_P4K2=0
+#   attn1024  attn_bwd_step at A = 1024, random and full lengths
+#   cfg5      attention tests + config #5 bench
 #   cfg5prof  rocprofv3 kernel stats of the config #5 bench
 #   decode    bench_decode with $AB_ENV = 1 / 0 at 64 and 128 articles, twice
 #   train     GPU tests matching $AB_K, then the B = 256 train bench for each $AB_ENV value in
 #             $AB_VALUES (default "1 0 1 0"), and config #5 at B = 512 too when AB_CFG5=1
-#             (e.g. AB_ENV=TSAMD_DEC_KB AB_K="model or decode" bash scripts/gpu_ab.sh train)
+#             (e.g. AB_ENV=TSAMD_DEFER_WGRAD AB_K="model or decode" bash scripts/gpu_ab.sh train)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -14,17 +14,15 @@ OUT=gpurun_out/${OUTD:-ab_$1}; mkdir -p $OUT
 CFG5="--hidden 512 --layers 2 --enc 800 --batch auto --steps 3 --warmup 1 --decode-batches 0"
 case "$1" in
 attn1024)
-  for full in "" 1; do for v in 0 2 4 5; do
-    MICRO_FULL=$full TSAMD_ATTN_P4K2=$v timeout -k 10 120 python tools/attn_bwd_a1024_micro.py >> $OUT/a1024.jsonl || exit 1
-  done; done; cat $OUT/a1024.jsonl ;;
+  for full in "" 1; do
+    MICRO_FULL=$full timeout -k 10 120 python tools/attn_bwd_a1024_micro.py >> $OUT/a1024.jsonl || exit 1
+  done; cat $OUT/a1024.jsonl ;;
 cfg5)
   timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_attention_ops.py \
     tests/test_gpu_model.py -k "attn or attention" > $OUT/pytest.log 2>&1
   rc=$?; tail -3 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
-  for v in 5 0; do
-    TSAMD_ATTN_P4K2=$v timeout -k 10 300 python bench.py $CFG5 > $OUT/cfg5_$v.log 2>&1 || { tail -20 $OUT/cfg5_$v.log; exit 1; }
-    tail -1 $OUT/cfg5_$v.log
-  done ;;
+  timeout -k 10 300 python bench.py $CFG5 > $OUT/cfg5.log 2>&1 || { tail -20 $OUT/cfg5.log; exit 1; }
+  tail -1 $OUT/cfg5.log ;;
 cfg5prof)
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py $CFG5 \
     > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }

@@ -23,21 +23,11 @@ def _setup(H, B, T, seed):
 
 
 # (512, *): the 8-wave kernels (W_hh register-resident at H = 512); (256, 600) and (512, 300):
-# more row tiles than one resident grid holds -> consecutive launches over row-tile ranges;
-# nw: TSAMD_LSTM_NW forcing the 8-wave (or the 4-wave) kernels in both directions below H = 512
-# (default: 4-wave forward, 8-wave backward)
-# nt: TSAMD_LSTM_NT (default 2: non-temporal activation traffic in the forward only; 0 none, 1 both)
-@pytest.mark.parametrize("H,B,T,nw,nt", [(64, 16, 9, None, None), (128, 37, 20, None, None), (256, 64, 33, None, None),
-                                         (256, 200, 12, None, None), (256, 600, 7, None, None), (256, 40, 25, "8", None),
-                                         (256, 72, 19, "4", None), (128, 30, 11, "4", None),
-                                         (512, 40, 21, None, None), (512, 64, 200, None, None), (512, 300, 9, None, None),
-                                         (256, 64, 33, None, "1"), (512, 40, 21, None, "1"), (256, 64, 33, None, "0")])
-def test_persistent_matches_step_kernels(H, B, T, nw, nt, monkeypatch):
+# more row tiles than one resident grid holds -> consecutive launches over row-tile ranges
+@pytest.mark.parametrize("H,B,T", [(64, 16, 9), (128, 37, 20), (256, 64, 33), (256, 200, 12), (256, 600, 7),
+                                   (256, 40, 25), (128, 30, 11), (512, 40, 21), (512, 64, 200), (512, 300, 9)])
+def test_persistent_matches_step_kernels(H, B, T):
     from textsummarization_on_flink_amd.ops import ops
-    if nw:
-        monkeypatch.setenv("TSAMD_LSTM_NW", nw)
-    if nt:
-        monkeypatch.setenv("TSAMD_LSTM_NT", nt)
     k = ops()
     assert int(k.lstm_persistent_grid(H, B)) > 0
     if (H, B) in ((256, 600), (512, 300)):

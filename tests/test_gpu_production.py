@@ -50,7 +50,7 @@ def test_bench_shape_matches_fp32_oracle():
     eng_params = params
     eng_params.enable_grad()
     eng = HipPointerGenerator(hps, vocab.size(), eng_params, B=B, T=T)
-    assert eng.persistent_lstm and eng.fused_vocab and eng.fused_attn_bwd
+    assert eng.persistent_lstm and eng.fused_vocab and eng.row_attn_bwd
     eng.set_batch(batch)
     out = eng.forward(need_grad=True)
     eng.backward()
@@ -81,12 +81,9 @@ def test_bench_shape_matches_fp32_oracle():
     assert not bad, bad
 
 
-@pytest.mark.parametrize("overlap_dw", ["0", "1"])
-def test_graph_replay_equals_eager_train_step(monkeypatch, overlap_dw):
-    """Three optimizer steps through the captured graphs == the same steps launched eagerly
-    (also with the output-projection dW forked onto a side stream inside backward_mid)."""
+def test_graph_replay_equals_eager_train_step():
+    """Three optimizer steps through the captured graphs == the same steps launched eagerly."""
     from textsummarization_on_flink_amd.train.trainer import GraphTrainer
-    monkeypatch.setenv("TSAMD_OVERLAP_DW", overlap_dw)
     B = 256
     hps = _hps(B)
     vocab, batches = _batches(hps, 3, seed=12)
@@ -160,30 +157,9 @@ def test_row_split_streams_match_single_chain(monkeypatch, split):
     assert _rel(got[1][2], got[0][2]) < 1e-4
 
 
-def test_two_workgroup_attention_backward_matches(monkeypatch):
-    """TSAMD_ATTN_BWD_PARTS=2 (attn_bwd_row with two workgroups per row, partial ds summed by
-    dec_bwd_cell and after the loop) gives the gradients of the one-workgroup kernel."""
-    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
-    B = 256
-    hps = _hps(B, trunc_norm_init_std=0.05).replace(max_dec_steps=24)
-    vocab, (batch,) = _batches(hps, 1, seed=16)
-    got = []
-    for parts in ("1", "2"):
-        monkeypatch.setenv("TSAMD_ATTN_BWD_PARTS", parts)
-        params = build_params(hps, vocab.size(), device="cuda", seed=7).enable_grad()
-        eng = HipPointerGenerator(hps, vocab.size(), params, B=B, T=T, D=24)
-        assert eng.row_attn_bwd and eng.attn_bwd_parts == int(parts)
-        eng.set_batch(batch)
-        eng.forward(need_grad=True)
-        eng.backward()
-        torch.cuda.synchronize()
-        got.append(params.grad.clone())
-    assert _rel(got[1], got[0]) < 1e-4, _rel(got[1], got[0])
-
-
 def test_deferred_weight_gradients_match_inline(monkeypatch):
     """The decoder-side weight gradients deferred onto a side stream beside the encoder BPTT
-    (TSAMD_DEFER_WGRAD, default on; with the opt-in TSAMD_DEFER_VOCAB_DW the vocab dW too) give
+    (TSAMD_DEFER_WGRAD, default on) give
     the gradients of the inline order, in eager mode and through the captured phase graphs."""
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
     B = 256
@@ -192,7 +168,6 @@ def test_deferred_weight_gradients_match_inline(monkeypatch):
     got = []
     for defer in ("0", "1"):
         monkeypatch.setenv("TSAMD_DEFER_WGRAD", defer)
-        monkeypatch.setenv("TSAMD_DEFER_VOCAB_DW", defer)  # the opt-in vocab dW through wgrad_tn too
         params = build_params(hps, vocab.size(), device="cuda", seed=6).enable_grad()
         eng = HipPointerGenerator(hps, vocab.size(), params, B=B, T=T, D=24)
         assert eng.defer_wgrad == (defer == "1")

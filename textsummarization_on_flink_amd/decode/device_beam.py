@@ -21,7 +21,6 @@ unchanged: cov'_t = cov'_{t-1}[parent] + a_{t-1}[parent].
 """
 from __future__ import annotations
 
-import os
 
 from typing import List
 
@@ -57,9 +56,9 @@ class DeviceBeamDecoder:
         self.eng = HipPointerGenerator(hps, self.V, params, B=self.Na, T=T, D=1)
         # attention per step: the row-resident kernel (score + softmax + context in one launch,
         # one workgroup per hypothesis reading its article's F/E rows) when the shape allows
-        # it, else the multi-block kernels over the transposed features (TSAMD_DEC_ROW_ATTN=0)
+        # it, else the multi-block kernels over the transposed features (EngineConfig.decode_row_attn)
         self.k = self.eng.k
-        self.row_attn = (os.environ.get("TSAMD_DEC_ROW_ATTN", "1") != "0" and bool(self.k.attn_row_ok(self.eng.A, T)))
+        self.row_attn = self.eng.cfg.decode_row_attn and bool(self.k.attn_row_ok(self.eng.A, T))
         self.eng.keep_ft = not self.row_attn  # the multi-block score kernel reads transposed features
         self.dev = self.eng.dev
         self._alloc()
@@ -93,10 +92,9 @@ class DeviceBeamDecoder:
             ("part_i", (R, int(self.k.topk_parts(V)), K), torch.int32),
         ]:
             b[name] = z(*shape, dt=dt)
-        # fused vocab head (vocab_topk.hip) partials; TSAMD_FUSED_VOCAB=0 selects the
-        # materialised-logits path (GEMM + final_topk) instead
-        self.fused_vocab = (os.environ.get("TSAMD_FUSED_VOCAB", "1") != "0" and self.K <= 8
-                            and self.eng.H <= 256)
+        # fused vocab head (vocab_topk.hip) partials; EngineConfig.fused_vocab_decode = False
+        # selects the materialised-logits path (GEMM + final_topk) instead
+        self.fused_vocab = self.eng.cfg.fused_vocab_decode and self.K <= 8 and self.eng.H <= 256
         if self.fused_vocab:
             b["vpart_ms"] = z(R, int(self.k.vocab_topk_parts(V)), 2)
         # ping-pong decoder state: step t reads set t%2 and writes set (t+1)%2, so a

@@ -20,7 +20,6 @@ Reference semantics: ``model.py:76-305``, ``attention_decoder.py:27-180``.
 """
 from __future__ import annotations
 
-import os
 
 from typing import Dict, List, Optional
 
@@ -28,6 +27,7 @@ import numpy as np
 import torch
 
 from ..ops import ops as _ops
+from .engine_config import EngineConfig
 from .params import DEC, P, FlatParams, enc_prefix
 
 BF = torch.bfloat16
@@ -182,8 +182,10 @@ def pack_host_inputs(host: Dict[str, np.ndarray], layout, out: Optional[np.ndarr
 class HipPointerGenerator:
     """Fixed-shape (B rows, T encoder steps, D decoder steps) train/eval engine."""
 
-    def __init__(self, hps, vsize: int, params: FlatParams, B: int, T: int, D: Optional[int] = None):
+    def __init__(self, hps, vsize: int, params: FlatParams, B: int, T: int, D: Optional[int] = None,
+                 cfg: Optional[EngineConfig] = None):
         self.hps = hps
+        self.cfg = cfg = cfg or EngineConfig.from_env()
         self.V, self.E, self.H = vsize, hps.emb_dim, hps.hidden_dim
         self.A = 2 * self.H
         self.B, self.T, self.D = B, T, D or hps.max_dec_steps
@@ -204,29 +206,22 @@ class HipPointerGenerator:
         self.k = _ops()
         self.grad_scale = 1.0  # set to 1/world by a data-parallel trainer (see optimizer_step)
         self.nchunk = int(self.k.attn_chunks(T))
-        # the output-projection weight gradient (a ~0.7 ms GEMM that only the all-reduce and the
-        # optimizer need) runs on a side stream beside the decoder backward loop -- forked and
-        # joined inside backward_mid, so the phase graphs stay self-contained -- when
-        # TSAMD_OVERLAP_DW=1
-        self._dw_pending = None
-        self._side = torch.cuda.Stream(self.dev) if os.environ.get("TSAMD_OVERLAP_DW", "0") == "1" else None
         # The decoder recurrences (forward: cell -> s-projection -> score -> softmax/context;
         # backward: attention step -> cell backward -> dz backward) are independent across
         # batch rows.  With ``split`` > 1 the rows are cut into that many groups, each group's
         # chain of per-step launches runs on its own stream (forked from and joined to the
         # current stream, so a captured hipGraph holds parallel branches): one group's small
         # latency-bound cell kernels run beside another group's bandwidth-bound attention
-        # kernels instead of serialising behind them.  TSAMD_SPLIT overrides (1 = one chain).
+        # kernels instead of serialising behind them.  cfg.split overrides (1 = one chain).
         # Default: 2 groups from B = 128, 4 from B = 512 (config #5, H = 512: B = 512 161.6 -> 156.9 ms
         # per step, B = 1024 309.0 -> 301.1-301.9 ms; 8 groups 303.2; B = 256: 2 and 4 equal within
         # noise, 19.64 / 19.71 ms; profiles/r2/ab/split_groups.jsonl)
-        sp = int(os.environ.get("TSAMD_SPLIT", "0")) or (4 if B >= 512 and B % 64 == 0 else
-                                                         2 if B >= 128 and B % 32 == 0 else 1)
+        sp = cfg.split or (4 if B >= 512 and B % 64 == 0 else 2 if B >= 128 and B % 32 == 0 else 1)
         self.split = sp if (sp > 1 and B % (16 * sp) == 0) else 1
-        # TSAMD_SPLIT_BWD: the decoder backward loop's own group count (default: split; at B = 256
+        # cfg.split_bwd: the decoder backward loop's own group count (default: split; at B = 256
         # 2 groups 19.59-19.62 ms per step, 1 group 20.02-20.07, 4 groups 20.09:
         # profiles/r2/ab/split_bwd.jsonl)
-        spb = int(os.environ.get("TSAMD_SPLIT_BWD", "0")) or self.split
+        spb = cfg.split_bwd or self.split
         self.split_bwd = spb if (spb > 1 and B % (16 * spb) == 0) else 1
         ns = max(self.split, self.split_bwd)
         self._streams = [torch.cuda.Stream(self.dev) for _ in range(ns)] if ns > 1 else []
@@ -271,9 +266,9 @@ class HipPointerGenerator:
                 "dx": z(B, T, din),
             })
         # persistent weight-resident recurrence (lstm_persistent.hip) when the shape allows
-        # it; TSAMD_LSTM_PERSISTENT=0 forces the per-step kernels
-        self.persistent_lstm = (os.environ.get("TSAMD_LSTM_PERSISTENT", "1") != "0"
-                                and int(self.k.lstm_persistent_grid(H, B)) > 0)
+        # it; cfg.persistent_lstm = False forces the per-step kernels
+        cfg = self.cfg
+        self.persistent_lstm = cfg.persistent_lstm and int(self.k.lstm_persistent_grid(H, B)) > 0
         if self.persistent_lstm:
             w["lstm_xf"] = z(int(self.k.lstm_persistent_xbuf(H, B, False)), dt=torch.long)
             w["lstm_xb"] = z(int(self.k.lstm_persistent_xbuf(H, B, True)), dt=torch.long)
@@ -287,58 +282,32 @@ class HipPointerGenerator:
         # (hipBLASLt SK3: a tile owner spins on flags of higher-numbered workgroups), and two
         # such kernels -- or one beside the persistent BPTT, which spins on its own peers -- can
         # each hold CUs the other's waiting workgroups need (two concurrent library GEMMs in the
-        # vocab backward hung on MI355X).  TSAMD_DEFER_WGRAD=0: inline.
+        # vocab backward hung on MI355X).  cfg.defer_wgrad = False: inline.
         self._late = []
         # Measured (bench A/B): +0.6-1.3% at B = 256; at B = 64 / 128 the BPTT it runs beside
         # slows more (its hand-offs are latency-bound) than the moved work saves, so B >= 256.
-        self.defer_wgrad = (os.environ.get("TSAMD_DEFER_WGRAD", "1") != "0" and B >= 256 and E % 128 == 0
+        self.defer_wgrad = (cfg.defer_wgrad and B >= 256 and E % 128 == 0
                             and H % 128 == 0 and (
             not self.persistent_lstm or
             int(self.k.lstm_persistent_grid(H, B)) <= int(self.k.lstm_persistent_capacity(H)) - 64))
         self._late_stream = torch.cuda.Stream(self.dev) if self.defer_wgrad else None
-        # TSAMD_DEFER_VOCAB_DW=1 (opt-in) adds the vocab projection's weight gradient
-        # dW = X^T . dlogits (a 0.74 ms library GEMM at B = 256 on the critical path of
-        # backward_head), through wgrad_tn (its XCD-paired row tiles read the 2.56 GB dlogits from
-        # HBM once).  Measured at B = 256: 19.63-19.80 ms inline vs 19.96-20.01 deferred -- 2.6 GB
-        # of HBM traffic beside the latency-bound BPTT slows it more than the GEMM costs inline
-        # (profiles/r2/ab/vocab_dw_deferred.jsonl).  Its bucket (0) is then complete only after
-        # backward_tail, so a data-parallel trainer always keeps it inline (GraphTrainer).
-        self._vocab_dw_late = None  # (defer_vocab_dw: set with the vocab head below)
         # reduce_states: pre-activations [c; h], bf16 [fw, bw] inputs and bf16 dp (wgrad operands)
         w["rs_pre"] = z(2, B, H)
         w["rs_cat"] = z(2, B, 2 * H, dt=BF)
         w["rs_dp"] = z(2, B, H, dt=BF)
-        # one fused attention-backward kernel per decoder step (attn_bwd_step);
-        # TSAMD_ATTN_BWD_FUSED=0 selects the two-kernel path (attn_bwd_da over Et + attn_bwd_tanh)
-        self.fused_attn_bwd = os.environ.get("TSAMD_ATTN_BWD_FUSED", "1") != "0"
         # row-resident attention (attention_row.hip: one workgroup per row and step, forward
         # score + softmax + context in one launch) when the batch fills the CUs; else the
-        # multi-block-per-row kernels of attention.hip.  TSAMD_ROW_ATTN=0/1 overrides.
-        ra = os.environ.get("TSAMD_ROW_ATTN", "")
-        self.row_attn = bool(self.k.attn_row_ok(A, T)) and (ra == "1" or (ra != "0" and B >= 128))
+        # multi-block-per-row kernels of attention.hip.  cfg.row_attn forces it on / off.
+        self.row_attn = bool(self.k.attn_row_ok(A, T)) and (cfg.row_attn if cfg.row_attn is not None else B >= 128)
         # backward: the row kernel at A = 1024 (16 features per lane, 8 waves at 256 VGPRs)
         # hides too little latency -- config #5 decoder backward 79 ms vs 59 ms with the
         # multi-block attn_bwd_step (tools/phase_micro.py) -- so it is used at A = 512 only
-        self.row_attn_bwd = self.row_attn and (A == 512 or ra == "1")
-        # attn_bwd_row with two workgroups per row (opt-in TSAMD_ATTN_BWD_PARTS=2): a row's chain of
-        # position groups is dealt over 2 x 12 waves on two CUs; partial ds summed by dec_bwd_cell.
-        # Measured slower at B = 256 (19.58-19.63 -> 20.46-20.56 ms,
-        # profiles/r2/ab/attn_bwd_two_wg_rejected.jsonl): the loop is bound by the chip's VALU /
-        # transcendental issue over all rows, not by one row's chain, so a split only adds the
-        # per-workgroup prologue (S) and epilogue
-        self.attn_bwd_parts = 2 if os.environ.get("TSAMD_ATTN_BWD_PARTS", "1") == "2" else 1
-        # TSAMD_FUSED_SPROJ=1 (opt-in): the attention query projection s = [c, h] . W_s + b inside
-        # the row forward kernel instead of its own linear2 launch.  Measured slower
-        # (profiles/r2/ab/fused_sproj_rejected.jsonl): B = 256 19.7-19.8 -> 21.0-21.1 ms, config #5
-        # 158 -> 173 ms -- every row's workgroup streams all of W_s (512 KB-2 MB) through its CU
-        # before its first score, where the 16 x 16-tile linear2 reads each W_s row 8-16 times in all
-        self.fused_sproj = self.row_attn and os.environ.get("TSAMD_FUSED_SPROJ", "0") == "1"
+        self.row_attn_bwd = self.row_attn and (A == 512 or cfg.row_attn is True)
         w["F"] = z(B, T, A, dt=BF)
         # transposed copy for the lanes-over-positions score kernel (not needed by the row
         # kernels; the beam decoder sets keep_ft to get it from _encoder_forward)
         self.keep_ft = not self.row_attn
         w["Ft"] = z(B, A, T, dt=BF) if self.keep_ft else None
-        w["Et"] = None if self.fused_attn_bwd else z(B, A, T, dt=BF)
         w["XG"] = z(D, B, 4 * H)
         # decoder forward state
         w["xe"] = z(D, B, E)
@@ -363,22 +332,15 @@ class HipPointerGenerator:
         w["pg"] = z(D, B)
         w["loss_row"] = z(D, B)
         # fused vocab head (vocab_train.hip): logits live only in MFMA accumulators, the
-        # [N, V] buffer receives dlogits; TSAMD_FUSED_VOCAB_TRAIN=0 selects the library GEMM
+        # [N, V] buffer receives dlogits; cfg.fused_vocab_train = False selects the library GEMM
         # (bf16 logits, bias in the epilogue) + ptr_loss, which rewrites them in place
-        self.fused_vocab = (os.environ.get("TSAMD_FUSED_VOCAB_TRAIN", "1") != "0" and H in (128, 256))
+        self.fused_vocab = cfg.fused_vocab_train and H in (128, 256)
         if self.fused_vocab:
             N = D * B
             w["vpart"] = z(int(self.k.vocab_train_tiles(V)) * N * 2)
             for n in ("zg", "lse", "pv", "alpha"):
                 w[n] = z(N)
             w["dbias"] = z(V)  # output_projection/v gradient, column sums taken inside pass 2
-        # split-K factors of the two vocab-gradient GEMMs (batched GEMM + a sum; A/B knobs).
-        # Measured at B = 256 (profiles/r2/ab/vocab_grad_split.jsonl): dX unsplit 19.47-19.53 ms
-        # per step vs 19.67-20.02 split 2 / 4 / 8; dW split 8 = split 4 within noise
-        self.dx_split = int(os.environ.get("TSAMD_VOCAB_DX_SPLIT", "1"))
-        self.dw_split = int(os.environ.get("TSAMD_VOCAB_DW_SPLIT", "4"))
-        self.defer_vocab_dw = (self.defer_wgrad and os.environ.get("TSAMD_DEFER_VOCAB_DW", "0") == "1"
-                               and self.fused_vocab and H % 128 == 0 and V % 8 == 0)
         w["logits"] = z(D * B, V, dt=BF)
         # backward
         w["dlogits"] = w["logits"]
@@ -388,14 +350,12 @@ class HipPointerGenerator:
         w["DX"] = z(D, B, E)
         w["DZ"] = z(D, B, 4 * H, dt=BF)
         w["DS"] = z(D, B, A)
-        w["DS2"] = z(D, B, A) if (self.row_attn_bwd and self.attn_bwd_parts == 2) else None
         w["d_emb_dec"] = z(D * B, E)  # decoder-input embedding gradient rows
         w["out_f32"] = z(D * B, H)  # output projection [h, ctx] . W_o + b (fp32, before the bf16 copy)
         if self.hps.pointer_gen:  # p_gen direct terms of the decoder backward (pgen_dirs)
             w["dC_dir"] = z(D, B, H)
             w["dX_dir"] = z(D, B, E)
         w["DE"] = z(D, B, T)
-        w["da"] = None if self.fused_attn_bwd else z(B, T)
         w["dcov"] = z(2, B, T)
         w["dh_rec"] = z(B, H)
         w["dc_carry"] = z(B, H)
@@ -417,15 +377,15 @@ class HipPointerGenerator:
         kernel skipped the update, and eval / decode must not report them."""
         if int(self.w["lstm_err"].item()):
             raise LstmHandoffError("persistent LSTM hand-off timed out (a workgroup was not co-resident); "
-                                   "results of that launch were discarded -- set TSAMD_LSTM_PERSISTENT=0")
+                                   "results of that launch were discarded -- set TSAMD_LSTM_PERSISTENT=0 "
+                                   "(EngineConfig.persistent_lstm)")
 
     # ------------------------------------------------------------------ weights
     def pack(self):
         """fp32 master -> bf16 kernel layouts (recomputed after every optimizer step).  The
         first call allocates the layouts through torch ops; later calls (the optimizer graph)
         recompute W_comb with one GEMM and refresh every layout with ONE pack_cast launch over a
-        job table (pack.hip) instead of ~50 cast / copy / cat launches.  TSAMD_PACK_FAST=0: the
-        torch path every time."""
+        job table (pack.hip) instead of ~50 cast / copy / cat launches."""
         jobs = getattr(self, "_pack_jobs", None)
         if jobs is not None:
             E = self.E
@@ -433,7 +393,7 @@ class HipPointerGenerator:
             self.k.pack_cast(jobs, self._pack_total)
             return
         self._pack_torch()
-        if os.environ.get("TSAMD_PACK_FAST", "1") != "0" and self.p.flat.is_cuda:
+        if self.p.flat.is_cuda:
             self._build_pack_jobs()
 
     def _pack_job_pairs(self):
@@ -599,8 +559,6 @@ class HipPointerGenerator:
             if w["Ft"] is None:
                 w["Ft"] = torch.empty(B, A, T, dtype=BF, device=self.dev)
             k.transpose_bta(w["F"], w["Ft"], B, T, A)
-        if w["Et"] is not None:
-            k.transpose_bta(top["out"], w["Et"], B, T, A)
 
     def _decoder_forward(self):
         k, w, hps = self.k, self.w, self.hps
@@ -621,12 +579,6 @@ class HipPointerGenerator:
                                w["Cst"][t][rs], self.pk["WcT2"], w["Cst"][t + 1][rs], w["Cb"][t + 1][rs],
                                w["Hb"][t + 1][rs], w["ACT"][t][rs], Bg, H, A)
                 cov_in = w["COV"][t][rs] if (cov and t > 0) else None
-                if self.fused_sproj:  # s = [c, h] . W_s + b computed inside the row attention kernel
-                    k.attn_fwd_row_sproj(F[rs], enc_out[rs], w["Cb"][t + 1][rs], w["Hb"][t + 1][rs], self.pk["WsT"],
-                                         self.p[ATT_B], w["S"][t][rs], v, wc, cov_in, lens[rs], w["ATT"][t][rs],
-                                         w["COV"][t + 1][rs] if cov else None, w["covloss"][t][rs] if cov else None,
-                                         w["CTX"][t][rs], w["CTXb"][t][rs], Bg, T, A)
-                    continue
                 k.dec_sproj(w["Cb"][t + 1][rs], w["Hb"][t + 1][rs], self.pk["WsT"], self.p[ATT_B], w["S"][t][rs], Bg,
                             H, A)
                 if self.row_attn:
@@ -751,7 +703,7 @@ class HipPointerGenerator:
         N = self.D * self.B
 
         def dw():
-            Sw = self.dw_split
+            Sw = 4
             # keep the batched operand's batch stride (N / Sw rows of dlogits) below 2^31
             # elements: the library's strided-batched path is not trusted past 32-bit strides
             while Sw > 1 and (N // Sw) * V >= 2 ** 31 and N % (2 * Sw) == 0:
@@ -763,23 +715,10 @@ class HipPointerGenerator:
                 torch.sum(parts, 0, out=dst)
             else:
                 torch.mm(w["outb_ext"][:, :m].t(), dl, out_dtype=F32, out=dst)
-        if self.defer_vocab_dw:  # beside the encoder BPTT (backward_tail)
-            xh, gw = w["outb_ext"][:, :H], dst
-            self._vocab_dw_late = lambda: self.k.wgrad_tn(xh, dl, gw)
-        elif self._side is not None:  # deferred to backward_mid's side branch
-            self._dw_pending = dw
-        else:
-            dw()
-        S = self.dx_split
-        if S > 1 and V % S == 0:
-            # dX = dlogits . W^T split over S vocab chunks (one batched GEMM + a sum): the plain
-            # [N, V] x [V, H] product has only N/256 x 1 output tiles of 256 x 256
-            Vs = V // S
-            parts = torch.bmm(dl.view(N, S, Vs).permute(1, 0, 2), self.pk["ow"].view(H, S, Vs).permute(1, 2, 0),
-                              out_dtype=F32)
-            self._dout = parts.sum(0)
-        else:
-            self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
+        dw()
+        # dX = dlogits . W^T unsplit (split-K over vocab chunks measured slower at B = 256:
+        # profiles/r2/ab/vocab_grad_split.jsonl)
+        self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
 
     def _cast_colsum(self, x, bias_grad):
         """bf16 copy of x [N, C] plus bias_grad += its column sums in one read of x (the
@@ -801,11 +740,6 @@ class HipPointerGenerator:
         g = p.g
         cov = hps.coverage
         dout = self._dout
-        if self._side is not None and self._dw_pending is not None:
-            self._side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self._side):
-                self._dw_pending()
-            self._dw_pending = None
         # ---- output projection [h, ctx]
         Hn = w["Hb"][1:].reshape(N, H)
         ctxb = w["CTXb"].view(N, A)
@@ -836,7 +770,7 @@ class HipPointerGenerator:
         if dX_dir is not None and D > 1:  # p_gen path into ctx_{t-1} through x_t (hoisted out of the loop)
             dCTX_dir[:D - 1].view((D - 1) * B, A).addmm_(dX_dir[1:].view((D - 1) * B, E), p[LIN_M][E:].t())
         # ---- decoder reverse loop
-        enc_out, lens, F, Et = self.enc[-1]["out"], w["enc_lens"], w["F"], w["Et"]
+        enc_out, lens, F = self.enc[-1]["out"], w["enc_lens"], w["F"]
         v, wc = self.f32["v"], self.f32["wc"]
         w["DCTX"][D - 1].copy_(dCTX_dir[D - 1])
         w["dh_rec"].zero_()
@@ -845,7 +779,6 @@ class HipPointerGenerator:
         if not self.row_attn_bwd:
             w["DS"].zero_()  # accumulated with atomics by the multi-block kernels (the row kernel stores)
         Ga = w["dA"] if hps.pointer_gen else None
-        ds2 = w["DS2"] if self.row_attn_bwd and self.attn_bwd_parts == 2 else None
         def chain(r0, r1):
             Bg, rs = r1 - r0, slice(r0, r1)
             for t in reversed(range(D)):
@@ -856,27 +789,19 @@ class HipPointerGenerator:
                 if self.row_attn_bwd:
                     k.attn_bwd_row(enc_out[rs], F[rs], w["S"][t][rs], v, wc, cov_t, w["ATT"][t][rs], w["DCTX"][t][rs],
                                    w["CTX"][t][rs], ga_t, dcov_next, gcl_t, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
-                                   dcov[t % 2][rs] if cov else None, Bg, T, A, ds2[t][rs] if ds2 is not None else None)
-                elif self.fused_attn_bwd:
+                                   dcov[t % 2][rs] if cov else None, Bg, T, A)
+                else:
                     k.attn_bwd_step(enc_out[rs], F[rs], w["S"][t][rs], v, wc, cov_t, w["ATT"][t][rs], w["DCTX"][t][rs],
                                     w["CTX"][t][rs], ga_t, dcov_next, gcl_t, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
                                     dcov[t % 2][rs] if cov else None, Bg, T, A)
-                else:
-                    k.attn_bwd_da(Et[rs], w["DCTX"][t][rs], ga_t, dcov_next, w["ATT"][t][rs], cov_t, gcl_t, lens[rs],
-                                  w["da"][rs], Bg, T, A)
-                    k.attn_bwd_tanh(F[rs], w["S"][t][rs], v, wc, cov_t, w["ATT"][t][rs], w["da"][rs], dcov_next, gcl_t,
-                                    lens[rs], w["DE"][t][rs], w["DS"][t][rs], dcov[t % 2][rs] if cov else None, Bg, T,
-                                    A)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
-                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, ds2[t][rs] if ds2 is not None else None)
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A)
                 k.dec_bwd_dz(w["DZ"][t][rs], self.pk["Wbig"], dX_dir[t][rs] if dX_dir is not None else None,
                              dCTX_dir[t - 1][rs] if t > 0 else None, w["DX"][t][rs],
                              w["DCTX"][t - 1][rs] if t > 0 else None, w["dh_rec"][rs], Bg, E, H, A)
 
         self._row_groups(chain, self.split_bwd)
-        if ds2 is not None:  # the two per-row partials of ds, for the weight gradients below
-            w["DS"].add_(ds2)
         # ---- decoder weight gradients (one GEMM each over all D*B rows)
         emb_dec = self._emb_dec
 
@@ -918,8 +843,6 @@ class HipPointerGenerator:
         dE2 = dE.view(B * T, A)
         torch.addmm(dE2, dFb, self.pk["Wh"].t(), out_dtype=F32, out=dE2)
         self._dE = dE
-        if self._side is not None:  # join the output-projection weight gradient
-            torch.cuda.current_stream().wait_stream(self._side)
 
     def backward_tail(self):
         """reduce_states, encoder BPTT, embedding (the last bucket)."""
@@ -929,9 +852,6 @@ class HipPointerGenerator:
         dE = self._dE
         lens = w["enc_lens"]
         late, self._late = self._late, []
-        if self._vocab_dw_late is not None:  # the largest one first: it starts with the BPTT
-            late.insert(0, self._vocab_dw_late)
-            self._vocab_dw_late = None
         if late:  # the deferred decoder weight gradients, beside the encoder BPTT
             side = self._late_stream
             side.wait_stream(torch.cuda.current_stream())

@@ -72,8 +72,6 @@ class GraphTrainer:
                                       compress=getattr(hps, "grad_compress", "none"))
         self.engine.grad_scale = 1.0 / self.info.world
         eng = self.engine
-        if self.info.enabled:  # keep bucket 0 (vocab projection) complete after the first phase graph
-            eng.defer_vocab_dw = False
         self.lstm_exclusive = False
         if self.info.enabled and eng.persistent_lstm:
             grid = int(eng.k.lstm_persistent_grid(eng.H, eng.B))
@@ -150,13 +148,10 @@ class GraphTrainer:
                 g.replay()
                 if ev:
                     ev[i + 1].record()
-                if i == 0 and self.engine._side is None and not self.engine.defer_vocab_dw:
+                if i == 0:
                     self.reducer.bucket_ready(0)
-                elif i == 1:
-                    if self.engine._side is not None:  # the output-projection dW ran beside backward_mid
-                        self.reducer.bucket_ready(0)
-                    if not self.engine.defer_wgrad:  # else bucket 1 completes beside the encoder BPTT
-                        self.reducer.bucket_ready(1)
+                elif i == 1 and not self.engine.defer_wgrad:  # else bucket 1 completes beside the encoder BPTT
+                    self.reducer.bucket_ready(1)
             self._maybe_poison()
             self.reducer()
             if ev:

@@ -1,8 +1,6 @@
-"""attn_bwd_step at config #5's shape (A = 1024, T = 800, 256 rows per launch), variants chosen
-by TSAMD_ATTN_P4K2 (0: 8-position kernel, 1/2/3: 4-position kernel with 16 features per lane,
-uncapped / OCC 2 / OCC 3).  Random operands; one process per variant (the launcher reads the
-env once).  Prints one JSON line: microseconds per launch, effective E+F bandwidth and a digest
-of the outputs for cross-variant agreement (tools only; the tests compare the paths).
+"""attn_bwd_step at config #5's shape (A = 1024, T = 800, 256 rows per launch).  Random
+operands.  Prints one JSON line: microseconds per launch, effective E+F bandwidth and a digest
+of the outputs (tools only; the tests compare the paths).
 """
 import json
 import os
@@ -50,10 +48,10 @@ def main():
     torch.cuda.synchronize()
     us = st.elapsed_time(en) * 1e3 / it
     gb = 2 * float(lens.sum()) * A * 2 / 1e9
-    print(json.dumps({"variant": os.environ.get("TSAMD_ATTN_P4K2", "0"), "full": bool(os.environ.get("MICRO_FULL")), "B": B, "T": T, "A": A,
+    print(json.dumps({"variant": "default", "full": bool(os.environ.get("MICRO_FULL")), "B": B, "T": T, "A": A,
                       "us": round(us, 1), "ef_TBps": round(gb / us * 1e3, 2),
                       "digest": [round(float(x.double().abs().sum()), 4) for x in out]}), flush=True)
-    torch.save([x.cpu() for x in out], f"gpurun_out/attn_a1024_{os.environ.get('TSAMD_ATTN_P4K2', '0')}.pt")
+    torch.save([x.cpu() for x in out], f"gpurun_out/attn_a1024_{'default'}.pt")
 
 
 if __name__ == "__main__":

@@ -3,7 +3,7 @@
 Builds the bench-shaped engine (pointer-gen + coverage, H=256, T=400, D=100, V=50k), runs one
 forward + backward so every buffer holds realistic values, then re-launches single kernels
 with the engine's own buffers at decoder step t=50.  Variants are chosen by the kernels'
-env switches (TSAMD_ATTN_SW, TSAMD_ATTN_NG, TSAMD_ATTN_OCC), so run one process per variant.
+engine switches (EngineConfig, TSAMD_*), so run one process per variant.
 Prints one JSON line of microseconds per launch.
 """
 import json

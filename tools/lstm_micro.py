@@ -2,7 +2,7 @@
 per shape with the microseconds per launch and per recurrence step.
 
   python tools/lstm_micro.py 256:256:400 512:256:400 512:128:800
-TSAMD_LSTM_NW=8 selects the 8-wave kernels below H = 512 (run one process per variant).
+(The 4-wave forward runs below H = 512, the 8-wave one at H = 512; the BPTT always has 8 waves.)
 """
 import json
 import os
@@ -58,7 +58,7 @@ def main():
             k.lstm_bwd_persistent(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, xb, err, db, T, B, H)
 
         tf, tb = timeit(fwd), timeit(bwd)
-        print(json.dumps({"H": H, "B": B, "T": T, "nw": os.environ.get("TSAMD_LSTM_NW", "auto"),
+        print(json.dumps({"H": H, "B": B, "T": T, "nw": "auto",
                           "grid": int(k.lstm_persistent_grid(H, B)), "launches": int(k.lstm_persistent_launches(H, B)),
                           "fwd_us": round(tf, 1), "bwd_us": round(tb, 1), "fwd_us_per_step": round(tf / T, 2),
                           "bwd_us_per_step": round(tb / T, 2), "err": int(err.item())}), flush=True)
