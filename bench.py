@@ -48,8 +48,8 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", default="256", help="per-GPU batch (rows), or 'auto': the largest of 1024/512/256/128 "
-                                                   "whose training step fits the GPU's memory (config #5 sizing)")
+    ap.add_argument("--batch", default="256", help="per-GPU batch (rows), or 'auto': the largest of 2048/1024/512/256/128 "
+                                                   "whose training step fits every rank's GPU memory (config #5 sizing)")
     ap.add_argument("--no-coverage", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled per rank")
@@ -140,23 +140,15 @@ def main(argv=None):
                   enc_layers=args.layers, grad_compress=args.grad_compress)
     corpus = SyntheticCorpus(vocab_size=args.vocab, seed=1000 + info.rank)
     vocab = corpus.vocab(args.vocab)
-    cands = [1024, 512, 256, 128] if args.batch == "auto" else [int(args.batch)]
-    tr = None
-    for B in cands:  # 'auto': largest batch whose engine + captured step fit (every rank the same shape)
-        try:
-            hps = hps.replace(batch_size=B)
-            args.batch = B
-            batches = make_batches(hps, vocab, corpus, args.pool, pad_enc_to=args.enc)
-            tr = GraphTrainer(hps, vocab.size(), B=B, T=args.enc, device=f"cuda:{dev_id}", info=info,
-                              use_graph=not args.no_graph)
-            if len(cands) > 1:
-                tr.step(batches[0])  # graph capture included: the peak allocation happens here
-            break
-        except torch.cuda.OutOfMemoryError:
-            if B == cands[-1]:
-                raise
-            tr = None
-            torch.cuda.empty_cache()
+    if args.batch == "auto":
+        B = pick_batch(args, hps, vocab, corpus, info, D, torch, dev_id)
+    else:
+        B = int(args.batch)
+    args.batch = B
+    hps = hps.replace(batch_size=B)
+    batches = make_batches(hps, vocab, corpus, args.pool, pad_enc_to=args.enc)
+    tr = GraphTrainer(hps, vocab.size(), B=B, T=args.enc, device=f"cuda:{dev_id}", info=info,
+                      use_graph=not args.no_graph)
 
     for i in range(args.warmup):
         out = tr.step(batches[i % len(batches)])
@@ -176,6 +168,18 @@ def main(argv=None):
     (out, tokens, padded), elapsed = _timed(train_loop, info, D, torch)
     vals = tr.check_finite(out)
     elapsed_max = D.all_reduce_scalar(elapsed, info, op="max", device=tr.device)
+    elapsed_min = D.all_reduce_scalar(elapsed, info, op="min", device=tr.device)
+    # diagnostics, after the timed region: per-phase wall time of a few more steps (HIP events
+    # between the phase graphs; ms_allreduce = the all-reduce wait exposed after the backward)
+    tr.timing = True
+    ph = {}
+    nph = 3
+    for i in range(nph):
+        tr.step(batches[i % len(batches)])
+        for k_, v_ in tr.phase_ms().items():
+            ph[k_] = ph.get(k_, 0.0) + v_ / nph
+    tr.timing = False
+    ph = {k_: round(D.all_reduce_scalar(v_, info, op="max", device=tr.device), 3) for k_, v_ in ph.items()}
     tok_all = D.all_reduce_scalar(float(tokens), info, op="sum", device=tr.device)
     pad_all = D.all_reduce_scalar(float(padded), info, op="sum", device=tr.device)
     value = tok_all / elapsed_max
@@ -209,6 +213,9 @@ def main(argv=None):
                 "backend": info.backend if info.enabled else "none",
                 "grad_allreduce": ("bf16" if args.grad_compress == "bf16" else "fp32") if info.enabled else "none",
                 "padded_tokens_per_sec": round(pad_all / elapsed_max, 1),
+                "ms_per_step_rank_min": round(1000.0 * elapsed_min / args.steps, 3),
+                "ms_allreduce_exposed": ph.get("ms_allreduce"),
+                "phase_ms_max_over_ranks": ph,
                 "loss": round(vals.get("total_loss", float("nan")), 4),
                 "graph": not args.no_graph,
                 "persistent_lstm": bool(tr.engine.persistent_lstm),
@@ -222,6 +229,35 @@ def main(argv=None):
     if info.enabled:
         torch.distributed.destroy_process_group()
     return 0
+
+
+AUTO_BATCHES = (2048, 1024, 512, 256, 128)
+
+
+def pick_batch(args, hps, vocab, corpus, info, D, torch, dev_id) -> int:
+    """``--batch auto``: the largest per-GPU batch whose captured training step fits EVERY
+    rank's memory.  Each candidate is tried rank-locally (a trainer without collectives, one
+    captured step) and kept only if it fit on all ranks (all-reduce MIN of the success flag),
+    so the ranks agree before any gradient collective runs."""
+    from textsummarization_on_flink_amd.data.synthetic import make_batches
+    from textsummarization_on_flink_amd.parallel.dist import DistInfo
+    from textsummarization_on_flink_amd.train.trainer import GraphTrainer
+    for B in AUTO_BATCHES:
+        h = hps.replace(batch_size=B)
+        ok = 1.0
+        try:
+            b = make_batches(h, vocab, corpus, 1, pad_enc_to=args.enc)[0]
+            tr = GraphTrainer(h, vocab.size(), B=B, T=args.enc, device=f"cuda:{dev_id}", info=DistInfo(),
+                              use_graph=not args.no_graph)
+            tr.step(b)  # graph capture included: the peak allocation happens here
+            torch.cuda.synchronize()
+            del tr
+        except (torch.cuda.OutOfMemoryError, ValueError):
+            ok = 0.0
+        torch.cuda.empty_cache()
+        if D.all_reduce_scalar(ok, info, op="min", device=f"cuda:{dev_id}") > 0 or B == AUTO_BATCHES[-1]:
+            return B
+    return AUTO_BATCHES[-1]
 
 
 def bench_decode(args, info, D, torch, dev_id):

@@ -194,3 +194,29 @@ def test_dp_checkpoint_saved_on_rank0_resumes_on_all_ranks(tmp_path):
     assert second[0][0]["end"] == second[1][0]["end"] == 4
     assert second[0][0]["sum"] == second[1][0]["sum"]  # the ranks stay identical
     assert ckpt.latest_checkpoint(f"{tmp_path}/log/exp/train").endswith("model.ckpt-4")
+
+
+def _poison_worker(rank, world, port, q):
+    """Rank 1 alone sees a persistent-LSTM error word: after poison_where on its last bucket and
+    the bucketed all-reduce, EVERY rank holds a non-finite gradient (so every rank's optimizer
+    kernel skips the step and every rank raises at the same check)."""
+    info = _init(rank, world, port)
+    from textsummarization_on_flink_amd.parallel.dist import GradAllReducer, poison_where
+    g = torch.ones(100)
+    err = torch.tensor([1 if rank == 1 else 0], dtype=torch.int32)
+    red = GradAllReducer(g, info, bounds=[30, 70], average=False)
+    red.bucket_ready(0)
+    red.bucket_ready(1)
+    poison_where(err, g[-1:])
+    red()
+    healthy = torch.ones(10)
+    poison_where(torch.zeros(1, dtype=torch.int32), healthy[-1:])
+    q.put((rank, bool(torch.isfinite(g).all()), float(g[0]), bool(torch.isfinite(healthy).all())))
+    torch.distributed.destroy_process_group()
+
+
+def test_lstm_error_on_one_rank_skips_the_step_on_all_ranks():
+    res = _spawn(_poison_worker, 2)
+    for r in (0, 1):
+        finite, g0, healthy_finite = res[r]
+        assert not finite and g0 == 2.0 and healthy_finite

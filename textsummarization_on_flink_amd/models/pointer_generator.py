@@ -205,6 +205,9 @@ class HipPointerGenerator:
             raise ValueError(f"batch {B} x enc {T} exceeds the kernels' 32-bit row counts")
         self.k = _ops()
         self.grad_scale = 1.0  # set to 1/world by a data-parallel trainer (see optimizer_step)
+        # set by a data-parallel trainer: a persistent-LSTM timeout poisons the last gradient
+        # element before its bucket's all-reduce, so every rank skips that update (poison_where)
+        self.poison_on_lstm_err = False
         self.nchunk = int(self.k.attn_chunks(T))
         # The decoder recurrences (forward: cell -> s-projection -> score -> softmax/context;
         # backward: attention step -> cell backward -> dz backward) are independent across
@@ -905,6 +908,9 @@ class HipPointerGenerator:
         if late:
             torch.cuda.current_stream().wait_stream(self._late_stream)  # d_emb_dec and the weight gradients
         k.emb_grad_sorted(gemb, w["emb_sid"], w["emb_perm"], d_in.reshape(B * T, self.E), w["d_emb_dec"])
+        if self.poison_on_lstm_err:
+            from ..parallel.dist import poison_where
+            poison_where(w["lstm_err"], p.grad[-1:])
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_step(self):

@@ -155,14 +155,27 @@ class GradAllReducer:
             self.grad.mul_(1.0 / self.info.world)
 
 
+_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+
 def all_reduce_scalar(x: float, info: DistInfo, op="sum", device=None) -> float:
     if not info.enabled:
         return x
     if device is None:
         device = f"cuda:{info.local_rank}" if info.backend == "nccl" else "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=_OPS[op])
     return float(t.item())
+
+
+def poison_where(flag: torch.Tensor, buf: torch.Tensor) -> None:
+    """``buf[:] = NaN`` where the device word ``flag`` is non-zero (device-side, no host sync,
+    capturable).  A data-parallel trainer applies it to one element of its last gradient bucket
+    before that bucket's all-reduce: a rank whose persistent-LSTM launch timed out then hands
+    every rank a non-finite gradient sum, so ALL ranks' optimizer kernels skip the update (and
+    all raise at the next check) instead of the healthy ranks applying the faulty rank's
+    garbage and diverging from it, with mismatched collectives at the next check."""
+    buf.copy_(torch.where(flag.view(-1)[:1] != 0, torch.full_like(buf, float("nan")), buf))
 
 
 def barrier(info: DistInfo, device=None):

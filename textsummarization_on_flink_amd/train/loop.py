@@ -190,15 +190,16 @@ def setup_training(hps, vocab, batcher, info: Optional[DistInfo] = None, metrics
         return ckpt.convert_to_coverage_model(hps.log_root, trainer.params) if info.is_chief else None
     if hps.restore_best_model:
         return ckpt.restore_best_model(hps.log_root, trainer.params) if info.is_chief else None
-    latest = ckpt.latest_checkpoint(train_dir)
+    # only the chief reads the checkpoint (it wrote them): another rank may not see the file, or
+    # see it half-written, and a restore error there would leave rank 0 blocked in the broadcast
+    latest = ckpt.latest_checkpoint(train_dir) if info.is_chief else None
     if latest:
         trainer.global_step = ckpt.restore(latest, trainer.params, load_adagrad=True)
         if hasattr(trainer, "engine"):
             trainer.engine.pack()
         log.info("Restored %s at step %d", latest, trainer.global_step)
     if info.enabled:
-        # resume on every rank from the chief's state: rank 0 wrote the checkpoints, so its
-        # restore is authoritative even where another rank cannot see (or sees an older) file
+        # resume on every rank from the chief's state
         broadcast_params(trainer.params.flat, info)
         if trainer.params.accum is not None:
             broadcast_params(trainer.params.accum, info)

@@ -16,7 +16,9 @@ Replaces ``FlinkTrainer`` / ``run_training`` (``train.py:57-125``,
     and gradients are all-reduced, the encoder-backward graph is ordered behind the
     in-flight bucket all-reduces (a device-side stream wait), so no RCCL kernel shares the
     GPU with the persistent launch; a hand-off timeout anyway sets the sticky ``lstm_err``
-    word, which makes the optimizer kernel skip the update and ``check_finite`` raise;
+    word, which poisons the last gradient bucket before its all-reduce (``poison_where``):
+    every rank's optimizer kernel skips that update and every rank's ``check_finite`` raises
+    at the same check;
   * eval mode is the same engine with forward only.
 """
 from __future__ import annotations
@@ -71,6 +73,7 @@ class GraphTrainer:
                                       bounds=self.engine.phase_bounds(), average=False,
                                       compress=getattr(hps, "grad_compress", "none"))
         self.engine.grad_scale = 1.0 / self.info.world
+        self.engine.poison_on_lstm_err = self.info.enabled  # a hand-off timeout skips the step on every rank
         eng = self.engine
         self.lstm_exclusive = False
         if self.info.enabled and eng.persistent_lstm:
