@@ -428,7 +428,7 @@ Tensor debug_status() {
 void debug_clear() { tsamd_debug_clear(); }
 
 // fused training vocab head (vocab_train.hip): logits never materialised
-int64_t vocab_train_tiles_op(int64_t V) { return vocab_train_tiles((int)V); }
+int64_t vocab_train_tiles_op(int64_t V, int64_t H) { return vocab_train_tiles((int)V, (int)H); }
 
 // X: [N][ldx] bf16 (the first H columns are the activations; ldx >= H, ldx % 8 == 0)
 void vocab_train_fwd(const Tensor& X, const Tensor& WT, const Tensor& bias, const Tensor& target, const Tensor& part,
@@ -436,10 +436,10 @@ void vocab_train_fwd(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
                      int64_t ldx) {
   chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(target, I32, "target"); chk(part, F32, "part");
   chk(zg, F32, "zg"); chk(lse, F32, "lse"); chk(pv, F32, "pv");
-  TORCH_CHECK(H == 128 || H == 256, "fused training vocab head: hidden size 128 or 256");
+  TORCH_CHECK(H == 128 || H == 256 || H == 512, "fused training vocab head: hidden size 128, 256 or 512");
   TORCH_CHECK(N >= 1 && V >= 1 && ldx >= H && ldx % 8 == 0, "bad N/V/ldx");
   numel_eq(X, N * ldx, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias"); numel_eq(target, N, "target");
-  numel_eq(part, (int64_t)vocab_train_tiles((int)V) * N * 2, "part"); numel_eq(zg, N, "zg"); numel_eq(lse, N, "lse");
+  numel_eq(part, (int64_t)vocab_train_tiles((int)V, (int)H) * N * 2, "part"); numel_eq(zg, N, "zg"); numel_eq(lse, N, "lse");
   numel_eq(pv, N, "pv");
   launch_vocab_train_fwd(P<bf16>(X), (int)ldx, P<bf16>(WT), P<float>(bias), P<int>(target), P<float>(part), P<float>(zg),
                          P<float>(lse), P<float>(pv), N, V, H, stream());
@@ -450,7 +450,7 @@ void vocab_train_bwd(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
                      int64_t ldx) {
   chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(target, I32, "target"); chk(lse, F32, "lse");
   chk(alpha, F32, "alpha"); chk(dl, BF, "dl");
-  TORCH_CHECK(H == 128 || H == 256, "fused training vocab head: hidden size 128 or 256");
+  TORCH_CHECK(H == 128 || H == 256 || H == 512, "fused training vocab head: hidden size 128, 256 or 512");
   TORCH_CHECK(N >= 1 && V >= 1 && ldx >= H && ldx % 8 == 0, "bad N/V/ldx");
   numel_eq(X, N * ldx, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias"); numel_eq(target, N, "target");
   numel_eq(lse, N, "lse"); numel_eq(alpha, N, "alpha"); numel_eq(dl, N * V, "dl"); chko(dbias, F32, V, "dbias");

@@ -98,7 +98,7 @@ struct PgIn {
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
                        int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st);
-int vocab_train_tiles(int V);
+int vocab_train_tiles(int V, int H);
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
                             float* zg, float* lse, float* pv, int N, int V, int H, hipStream_t st);
 void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,

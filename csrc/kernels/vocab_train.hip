@@ -17,14 +17,19 @@
 //
 // Both passes run a persistent grid: the (vocab tile, row block) units are laid out vocab-
 // tile-major and every workgroup takes one contiguous range, so a workgroup keeps one W^T
-// tile's fragments in registers (128 VGPRs at H = 256) across many row blocks and reloads
-// them only at a tile boundary; the 32 x H row block of X is staged in LDS per unit (shared
-// by the 4 waves, each of which owns 64 of the 256 columns).
+// tile's fragments in registers (128 VGPRs) across many row blocks and reloads them only at a
+// tile boundary; the 32 x H row block of X is staged in LDS per unit (shared by the 4 waves).
+// Each wave owns NI 16-column MFMA tiles: NI = 4 (a 256-column vocab tile) up to H = 256, NI = 2
+// (128 columns) at H = 512, so the W^T fragments stay at KS x NI = 32 registers of 8 bf16 either
+// way (config #5, reference model.py:229 with hidden 512).
 #include "common.h"
 #include "attn_common.h"  // f32x2 packed-FP32 helpers
 
 #define VR_ROWS 32   // rows per unit (2 MFMA row tiles)
-#define VR_COLS 256
+
+// 16-column MFMA tiles per wave and vocab columns per unit (4 waves) at hidden size H
+__host__ __device__ constexpr int vr_ni(int H) { return H <= 256 ? 4 : 2; }
+__host__ __device__ constexpr int vr_cols(int H) { return 64 * vr_ni(H); }
 #define LOG2E_F 1.4426950408889634f
 #define LN2_F 0.6931471805599453f
 
@@ -66,6 +71,25 @@ __device__ __forceinline__ float row_transpose_sum(float (&v)[16], int c16) {
   return keep + dpp_f<DPP_XOR1>(send);
 }
 
+// 8 values per lane (q = 4i + r) summed over the 16 lanes of a DPP row: lane l returns the total
+// of value q = 4 b3 + 2 b2 + b1 (bits of l & 15); lanes l and l ^ 1 return the same total.
+__device__ __forceinline__ float row_transpose_sum8(float (&v)[8], int c16) {
+  const bool b3 = c16 & 8, b2 = c16 & 4, b1 = c16 & 2;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const float keep = b3 ? v[a + 4] : v[a], send = b3 ? v[a] : v[a + 4];
+    v[a] = keep + dpp_f<DPP_MIRROR>(send);
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const float keep = b2 ? v[a + 2] : v[a], send = b2 ? v[a] : v[a + 2];
+    v[a] = keep + dpp_f<DPP_HALF_MIRROR>(send);
+  }
+  const float keep = b1 ? v[1] : v[0], send = b1 ? v[0] : v[1];
+  const float t = keep + dpp_f<DPP_XOR2>(send);
+  return t + dpp_f<DPP_XOR1>(t);
+}
+
 }  // namespace
 
 // Operands are swapped relative to a plain logits GEMM: A = W^T fragments (16 vocab
@@ -92,6 +116,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     float* __restrict__ dbias,        // [V]      pass 2 (nullable): += column sums of dlogits
     int N, int V, int ldx) {
   constexpr int KS = H / 32;          // k-steps of 32
+  constexpr int NI = vr_ni(H), VR_COLS = vr_cols(H);
   constexpr int XS = H + 8;           // padded LDS row (bank spread)
   constexpr int RJ = VR_ROWS / 16;    // 16-row MFMA tiles per unit
   constexpr int CH = VR_ROWS * H / 8 / 256;  // 16-byte X chunks per thread per unit
@@ -106,20 +131,22 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
   const int u0 = (int)(units * blockIdx.x / gridDim.x), u1 = (int)(units * (blockIdx.x + 1) / gridDim.x);
   if (u0 >= u1) return;
   const int kof = 8 * (lane >> 4), c16 = lane & 15, q4 = 4 * (lane >> 4);
-  bf16x8 wa[KS][4];   // A fragments: W^T rows (vocab columns) of this wave's 4 column tiles
-  f32x2 bc2[4][2];    // log2(e) x bias of the lane's columns cw + 16i + q4 + r, pairs (r = 2h, 2h + 1)
+  bf16x8 wa[KS][NI];  // A fragments: W^T rows (vocab columns) of this wave's NI column tiles
+  f32x2 bc2[NI][2];   // log2(e) x bias of the lane's columns cw + 16i + q4 + r, pairs (r = 2h, 2h + 1)
                       // (-inf past V in pass 1)
   int cur_vt = -1;
   // pass 2: the output-projection bias gradient db = sum_rows dlogits.  Per unit the lane's
-  // 16 column partials (its 2 rows) are folded across the 16 lanes that share those columns by
-  // a halving butterfly (8 + 4 + 2 + 1 DPP exchanges), which leaves lane l with the full
-  // column sum for column index c16 = l & 15 -- ONE accumulator register per lane, carried
-  // over the workgroup's units of a vocab tile and flushed with one atomic per column when
-  // the tile changes (a 16-register accumulator spilled at 256 VGPRs).
+  // 4 NI column partials (its 2 rows) are folded across the 16 lanes that share those columns
+  // by a halving butterfly (8 + 4 + 2 + 1 DPP exchanges), which leaves lane l with the full
+  // column sum for column index c16 = l & 15 (NI = 2: q = c16 >> 1, lane pairs agree) -- ONE
+  // accumulator register per lane, carried over the workgroup's units of a vocab tile and
+  // flushed with one atomic per column when the tile changes (a 16-register accumulator
+  // spilled at 256 VGPRs).
   float cacc = 0.f;
   auto flush_bias = [&](int vt_old) {
-    const int col = vt_old * VR_COLS + 64 * wid + 16 * (c16 >> 2) + q4 + (c16 & 3);
-    if (col < V) atomicAdd(dbias + col, cacc);
+    const int q = NI == 4 ? c16 : c16 >> 1;
+    const int col = vt_old * VR_COLS + 16 * NI * wid + 16 * (q >> 2) + q4 + (q & 3);
+    if (col < V && (NI == 4 || !(c16 & 1))) atomicAdd(dbias + col, cacc);
     cacc = 0.f;
   };
   bf16x8 xr[CH];      // prefetched X chunks of the next unit
@@ -170,11 +197,11 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
   for (int u = u0; u < u1; ++u) {
     const int buf = (u - u0) & 1;
     const int vt = u / RB, rb = (u % RB) * VR_ROWS;
-    const int cw = vt * VR_COLS + 64 * wid;  // this wave's first column
+    const int cw = vt * VR_COLS + 16 * NI * wid;  // this wave's first column
     if (vt != cur_vt) {  // new vocab tile: its A fragments and bias into registers
       if (GRAD && dbias && cur_vt >= 0) flush_bias(cur_vt);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
         const bf16* arow = WT + (size_t)min(cw + 16 * i + c16, V - 1) * H + kof;
 #pragma unroll
         for (int h = 0; h < KS; ++h) wa[h][i] = ld8(arow + 32 * h);
@@ -189,9 +216,9 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
       cur_vt = vt;
     }
     if (u + 1 < u1) fetch(u + 1);
-    f32x4 acc[4][RJ];
+    f32x4 acc[NI][RJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < RJ; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
 #pragma unroll
@@ -200,7 +227,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
       for (int j = 0; j < RJ; ++j) {
         const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&Xs[buf][(16 * j + c16) * XS + 32 * h + kof]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16(wa[h][i], xb, acc[i][j]);
+        for (int i = 0; i < NI; ++i) acc[i][j] = mfma16(wa[h][i], xb, acc[i][j]);
       }
     if constexpr (!GRAD) {
 #pragma unroll
@@ -209,10 +236,10 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
         const int wo = Tg[buf][rr] - cw - q4;  // gold column relative to the lane's first one
         // y = log2(e) x logit (base-2 domain: one packed FMA per element pair, exp2 without a
         // multiply); -inf for columns >= V
-        f32x2 y[4][2];
+        f32x2 y[NI][2];
         float m = -INFINITY;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < NI; ++i)
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             y[i][h] = fma2(f32x2{acc[i][j][2 * h], acc[i][j][2 * h + 1]}, splat2(LOG2E_F), bc2[i][h]);
@@ -220,9 +247,9 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
           }
         // the gold logit: at most one of the row's columns lies among the lane's 16
         // (offsets 16i + r), so the selection runs only on the rare hit
-        if ((unsigned)wo < 64u && (wo & 12) == 0 && row < N) {
+        if ((unsigned)wo < 16u * NI && (wo & 12) == 0 && row < N) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (wo == 16 * i + r) zg[row] = (r & 1 ? y[i][r >> 1].y : y[i][r >> 1].x) * LN2_F;
@@ -232,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
         if (m > -INFINITY) {
           const f32x2 mm = splat2(m);
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const f32x2 t = y[i][h] - mm;
@@ -246,10 +273,10 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
         }
       }
     } else {
-      const bool full = (V % 4 == 0) && cw + 64 <= V;  // wave-uniform: no column guards
-      f32x2 cs[4][2];  // this unit's column partials, index (i, r / 2)
+      const bool full = (V % 4 == 0) && cw + 16 * NI <= V;  // wave-uniform: no column guards
+      f32x2 cs[NI][2];  // this unit's column partials, index (i, r / 2)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) cs[i][0] = cs[i][1] = splat2(0.f);
+      for (int i = 0; i < NI; ++i) cs[i][0] = cs[i][1] = splat2(0.f);
 #pragma unroll
       for (int j = 0; j < RJ; ++j) {
         const int rr = 16 * j + c16, row = rb + rr;
@@ -258,18 +285,18 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
         // alpha exp(z - lse) = exp2(log2(e) z + log2(alpha) - log2(e) lse)   (alpha >= 0)
         const float c = al > 0.f ? __log2f(al) - Ls[buf][rr] * LOG2E_F : -INFINITY;
         if (row < N) {
-          f32x2 d[4][2];
+          f32x2 d[NI][2];
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const f32x2 t = fma2(f32x2{acc[i][j][2 * h], acc[i][j][2 * h + 1]}, splat2(LOG2E_F), bc2[i][h] + c);
               d[i][h] = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
             }
           // - alpha at the gold column (rare: see pass 1)
-          if ((unsigned)wo < 64u && (wo & 12) == 0) {
+          if ((unsigned)wo < 16u * NI && (wo & 12) == 0) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < NI; ++i)
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 if (wo == 16 * i + r) {
@@ -278,7 +305,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
                 }
           }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+          for (int i = 0; i < NI; ++i) {
             cs[i][0] += d[i][0];
             cs[i][1] += d[i][1];
           }
@@ -287,12 +314,12 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
             // (plain stores: the 4 stores of a row's 128-byte line are merged in L2; non-temporal
             // stores went to HBM as 32-byte pieces, 1.31 -> 1.75 ms)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < NI; ++i)
               *reinterpret_cast<bf16x4*>(dst + 16 * i) =
                   bf16x4{f2bf(d[i][0].x), f2bf(d[i][0].y), f2bf(d[i][1].x), f2bf(d[i][1].y)};
           } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < NI; ++i) {
               const int col = cw + 16 * i + q4;
               const float dv[4] = {d[i][0].x, d[i][0].y, d[i][1].x, d[i][1].y};
 #pragma unroll
@@ -303,15 +330,16 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
         }
       }
       if (dbias) {
-        float cv[16];
+        float cv[4 * NI];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NI; ++i) {
           cv[4 * i] = cs[i][0].x;
           cv[4 * i + 1] = cs[i][0].y;
           cv[4 * i + 2] = cs[i][1].x;
           cv[4 * i + 3] = cs[i][1].y;
         }
-        cacc += row_transpose_sum(cv, c16);
+        if constexpr (NI == 4) cacc += row_transpose_sum(cv, c16);
+        else cacc += row_transpose_sum8(cv, c16);
       }
     }
     if (u + 1 < u1) stash(buf ^ 1);
@@ -383,37 +411,38 @@ __global__ __launch_bounds__(256) void ptr_rowfin_kernel(
   }
 }
 
-int vocab_train_tiles(int V) { return (V + VR_COLS - 1) / VR_COLS; }
+int vocab_train_tiles(int V, int H) { return (V + vr_cols(H) - 1) / vr_cols(H); }
 
-// 2 workgroups per CU (<= 256 VGPRs, ~36 KB LDS each): 512 persistent workgroups
-static int vocab_train_grid(int N, int V) {
-  const long units = (long)((N + VR_ROWS - 1) / VR_ROWS) * vocab_train_tiles(V);
+// 2 workgroups per CU (<= 256 VGPRs, ~36 KB LDS each at H = 256, ~67 KB at H = 512): 512
+// persistent workgroups
+static int vocab_train_grid(int N, int V, int H) {
+  const long units = (long)((N + VR_ROWS - 1) / VR_ROWS) * vocab_train_tiles(V, H);
   return (int)(units < 512 ? units : 512);
 }
 
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
                             float* zg, float* lse, float* pv, int N, int V, int H, hipStream_t st) {
-  const int grid = vocab_train_grid(N, V);
-  if (H == 256)
-    hipLaunchKernelGGL((vocab_train_kernel<256, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, part, zg,
-                       nullptr, nullptr, nullptr, nullptr, N, V, ldx);
-  else
-    hipLaunchKernelGGL((vocab_train_kernel<128, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, part, zg,
-                       nullptr, nullptr, nullptr, nullptr, N, V, ldx);
+  const int grid = vocab_train_grid(N, V, H);
+#define VF(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
+                                  part, zg, nullptr, nullptr, nullptr, nullptr, N, V, ldx)
+  if (H == 512) VF(512);
+  else if (H == 256) VF(256);
+  else VF(128);
+#undef VF
   hipLaunchKernelGGL(vocab_rowstats_kernel, dim3((N + 31) / 32), dim3(256), 0, st, part, zg, target, lse, pv, N, V,
-                     vocab_train_tiles(V));
+                     vocab_train_tiles(V, H));
 }
 
 void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
                             const float* lse, const float* alpha, bf16* dl, float* dbias, int N, int V, int H,
                             hipStream_t st) {
-  const int grid = vocab_train_grid(N, V);
-  if (H == 256)
-    hipLaunchKernelGGL((vocab_train_kernel<256, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, nullptr,
-                       nullptr, lse, alpha, dl, dbias, N, V, ldx);
-  else
-    hipLaunchKernelGGL((vocab_train_kernel<128, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, nullptr,
-                       nullptr, lse, alpha, dl, dbias, N, V, ldx);
+  const int grid = vocab_train_grid(N, V, H);
+#define VB(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
+                                  nullptr, nullptr, lse, alpha, dl, dbias, N, V, ldx)
+  if (H == 512) VB(512);
+  else if (H == 256) VB(256);
+  else VB(128);
+#undef VB
 }
 
 void launch_ptr_rowfin(const float* pv, const int* target, const float* rowg, const float* pgen, const float* attn,

@@ -77,7 +77,7 @@ def test_hip_matches_reference(coverage, pointer_gen, layers, B, E, H):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("coverage,pointer_gen,H", [(True, True, 256), (False, False, 128)])
+@pytest.mark.parametrize("coverage,pointer_gen,H", [(True, True, 256), (False, False, 128), (True, True, 512)])
 def test_fused_vocab_head_matches_library_path(monkeypatch, coverage, pointer_gen, H):
     """vocab_train (MFMA logits in registers, per-tile LSE partials, recomputed dlogits) ==
     library GEMM + ptr_loss.  V = 2000 leaves a partial 256-column tile, N = 150 a partial

@@ -45,7 +45,7 @@ def main():
     WT = (torch.randn(V, H, generator=g) * 0.1).to(dev, torch.bfloat16)
     bias = (torch.randn(V, generator=g) * 0.1).to(dev)
     target = torch.randint(0, V + 50, (N,), generator=g).to(dev, torch.int32)
-    nt = int(k.vocab_train_tiles(V))
+    nt = int(k.vocab_train_tiles(V, H))
     part = torch.empty(nt * N * 2, device=dev)
     zg, lse, pv = (torch.empty(N, device=dev) for _ in range(3))
     alpha = torch.rand(N, generator=g).to(dev)
