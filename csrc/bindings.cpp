@@ -195,9 +195,10 @@ void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const 
   chk(dF, BF, "dF"); chk(dv, F32, "dv");
   TORCH_CHECK(A % 64 == 0, "bad A");
   numel_eq(F, B * T * A, "F"); numel_eq(S_all, D * B * A, "S_all"); numel_eq(de_all, D * B * T, "de_all");
-  // dv / dwc: [nslot][A] partial rows (nslot a power of two <= 1024; the caller sums them)
+  // dv / dwc: [nslot][A] partial rows (nslot a power of two; the caller sums them).  With nslot >=
+  // the number of workgroups every slot has one writer (deterministic mode)
   const int64_t nslot = dv.numel() / A;
-  TORCH_CHECK(nslot >= 1 && nslot <= 1024 && (nslot & (nslot - 1)) == 0 && dv.numel() == nslot * A,
+  TORCH_CHECK(nslot >= 1 && nslot <= (1 << 20) && (nslot & (nslot - 1)) == 0 && dv.numel() == nslot * A,
               "dv: [nslot, A] with nslot a power of two");
   numel_eq(dF, B * T * A, "dF");
   chko(wc, F32, A, "wc"); chko(cov_all, F32, D * B * T, "cov_all"); chko(dwc, F32, nslot * A, "dwc");
@@ -218,6 +219,24 @@ void emb_grad_sorted(const Tensor& gemb, const Tensor& sid, const Tensor& perm, 
   TORCH_CHECK(sid.numel() == n0 + n1, "sid must cover src0 and src1 rows");
   launch_emb_grad_sorted(P<float>(gemb), P<int>(sid), P<int>(perm), P<float>(src0), (int)n0, P<float>(src1),
                          (int)n1, (int)E, (int)V, stream());
+}
+
+// deterministic variant (no atomics): pf / pl are [chunks][E] fp32 scratch, chunks = ceil(rows / 64)
+int64_t emb_grad_det_chunks_op(int64_t n) { return emb_grad_det_chunks((int)n); }
+void emb_grad_det(const Tensor& gemb, const Tensor& sid, const Tensor& perm, const Tensor& src0, const Tensor& src1,
+                  const Tensor& pf, const Tensor& pl) {
+  chk(gemb, F32, "gemb"); chk(src0, F32, "src0"); chk(src1, F32, "src1"); chk(pf, F32, "pf"); chk(pl, F32, "pl");
+  TORCH_CHECK(gemb.dim() == 2 && gemb.size(1) <= 512, "gemb must be [V][E], E <= 512");
+  TORCH_CHECK(sid.scalar_type() == at::kInt && perm.scalar_type() == at::kInt && sid.is_contiguous() &&
+              perm.is_contiguous() && sid.numel() == perm.numel(), "sid / perm int32, contiguous, one length");
+  const int64_t E = gemb.size(1), V = gemb.size(0);
+  TORCH_CHECK(src0.numel() % E == 0 && src1.numel() % E == 0, "src rows");
+  const int64_t n0 = src0.numel() / E, n1 = src1.numel() / E;
+  TORCH_CHECK(sid.numel() == n0 + n1, "sid must cover src0 and src1 rows");
+  const int64_t nc = emb_grad_det_chunks((int)(n0 + n1));
+  numel_eq(pf, nc * E, "pf"); numel_eq(pl, nc * E, "pl");
+  launch_emb_grad_det(P<float>(gemb), P<int>(sid), P<int>(perm), P<float>(src0), (int)n0, P<float>(src1), (int)n1,
+                      (int)E, (int)V, P<float>(pf), P<float>(pl), stream());
 }
 
 // ---------------------------------------------------------------- frames (frames.hip)
@@ -283,17 +302,18 @@ void rs_fwd(const Tensor& cs, const Tensor& hs, int64_t T, const Tensor& RCt, co
 
 // dold_c / dold_h: [2][B][H] (fw, bw) seeds of the encoder BPTT
 void rs_bwd(const Tensor& gc, const Tensor& gh, const Tensor& pre_c, const Tensor& pre_h, const Tensor& RC,
-            const Tensor& RH, const Tensor& dpc, const Tensor& dph, const Tensor& gbc, const Tensor& gbh,
+            const Tensor& RH, const Tensor& dpc, const Tensor& dph, const OT& gbc, const OT& gbh,
             const Tensor& dold_c, const Tensor& dold_h, int64_t B, int64_t H) {
+  // gbc / gbh: bias gradients accumulated with atomics, or None (the caller sums: deterministic mode)
   chk(gc, F32, "gc"); chk(gh, F32, "gh"); chk(pre_c, F32, "pre_c"); chk(pre_h, F32, "pre_h"); chk(RC, BF, "RC");
-  chk(RH, BF, "RH"); chk(dpc, BF, "dpc"); chk(dph, BF, "dph"); chk(gbc, F32, "gbc"); chk(gbh, F32, "gbh");
+  chk(RH, BF, "RH"); chk(dpc, BF, "dpc"); chk(dph, BF, "dph"); chko(gbc, F32, H, "gbc"); chko(gbh, F32, H, "gbh");
   chk(dold_c, F32, "dold_c"); chk(dold_h, F32, "dold_h");
   TORCH_CHECK(H % 32 == 0 && H <= 512, "reduce_states: H % 32 == 0, H <= 512");
   for (const Tensor* t : {&gc, &gh, &pre_c, &pre_h, &dpc, &dph}) numel_eq(*t, B * H, "[B][H] operand");
-  numel_eq(RC, 2 * H * H, "RC"); numel_eq(RH, 2 * H * H, "RH"); numel_eq(gbc, H, "gbc"); numel_eq(gbh, H, "gbh");
+  numel_eq(RC, 2 * H * H, "RC"); numel_eq(RH, 2 * H * H, "RH");
   numel_eq(dold_c, 2 * B * H, "dold_c"); numel_eq(dold_h, 2 * B * H, "dold_h");
   launch_rs_bwd(P<float>(gc), P<float>(gh), P<float>(pre_c), P<float>(pre_h), P<bf16>(RC), P<bf16>(RH), P<bf16>(dpc),
-                P<bf16>(dph), P<float>(gbc), P<float>(gbh), P<float>(dold_c), P<float>(dold_h), (size_t)B * H, (int)B,
+                P<bf16>(dph), PO<float>(gbc), PO<float>(gbh), P<float>(dold_c), P<float>(dold_h), (size_t)B * H, (int)B,
                 (int)H, stream());
 }
 
@@ -656,24 +676,25 @@ void pgen(const Tensor& ctx, const Tensor& c, const Tensor& h, const Tensor& x, 
               stream());
 }
 
+// det: one workgroup row split (each gw column summed by one thread in row order, no atomics race)
 void pgen_bwd(const Tensor& ctx, const Tensor& c, const Tensor& h, const Tensor& x, const Tensor& dpre,
-              const Tensor& gw, int64_t N, int64_t A, int64_t H, int64_t E) {
+              const Tensor& gw, int64_t N, int64_t A, int64_t H, int64_t E, bool det) {
   chk(ctx, F32, "ctx"); chk(c, F32, "c"); chk(h, BF, "h"); chk(x, F32, "x"); chk(dpre, F32, "dpre");
   chk(gw, F32, "gw");
   numel_eq(ctx, N * A, "ctx"); numel_eq(c, N * H, "c"); numel_eq(h, N * H, "h"); numel_eq(x, N * E, "x");
   numel_eq(dpre, N, "dpre"); numel_eq(gw, A + 2 * H + E, "gw");
   launch_pgen_bwd(P<float>(ctx), P<float>(c), P<bf16>(h), P<float>(x), P<float>(dpre), P<float>(gw), N, A, H, E,
-                  stream());
+                  det, stream());
 }
 
-// gb (+)= sum(dpre) with atomics: pass the zeroed p_gen bias-gradient slot
+// gb (+)= sum(dpre) with atomics: pass the zeroed p_gen bias-gradient slot (or None: the caller sums)
 void pgen_dirs(const Tensor& dpre, const Tensor& w, const Tensor& dctx, const Tensor& dc, const Tensor& dh,
-               const Tensor& dx, const Tensor& gb, int64_t N, int64_t A, int64_t H, int64_t E) {
+               const Tensor& dx, const OT& gb, int64_t N, int64_t A, int64_t H, int64_t E) {
   chk(dpre, F32, "dpre"); chk(w, F32, "w"); chk(dctx, F32, "dctx"); chk(dc, F32, "dc"); chk(dh, F32, "dh");
-  chk(dx, F32, "dx"); chk(gb, F32, "gb");
+  chk(dx, F32, "dx"); chko(gb, F32, 1, "gb");
   numel_eq(dpre, N, "dpre"); numel_eq(w, A + 2 * H + E, "w"); numel_eq(dctx, N * A, "dctx"); numel_eq(dc, N * H, "dc");
-  numel_eq(dh, N * H, "dh"); numel_eq(dx, N * E, "dx"); numel_eq(gb, 1, "gb");
-  launch_pgen_dirs(P<float>(dpre), P<float>(w), P<float>(dctx), P<float>(dc), P<float>(dh), P<float>(dx), P<float>(gb),
+  numel_eq(dh, N * H, "dh"); numel_eq(dx, N * E, "dx");
+  launch_pgen_dirs(P<float>(dpre), P<float>(w), P<float>(dctx), P<float>(dc), P<float>(dh), P<float>(dx), PO<float>(gb),
                    (int)N, (int)A, (int)H, (int)E, stream());
 }
 
@@ -716,6 +737,8 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("vocab_train_bwd", &vocab_train_bwd);
   m.def("emb_grad", &emb_grad);
   m.def("emb_grad_sorted", &emb_grad_sorted);
+  m.def("emb_grad_det", &emb_grad_det);
+  m.def("emb_grad_det_chunks", &emb_grad_det_chunks_op);
   m.def("to_step_frame", &to_step_frame);
   m.def("from_step_frame", &from_step_frame);
   m.def("transpose_bta", &transpose_bta);

@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) void pgen_dirs_kernel(const float* __restrict_
   }
   if (lane == 0) red[wid] = d;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(gb, (red[0] + red[1]) + (red[2] + red[3]));
+  if (gb && threadIdx.x == 0) atomicAdd(gb, (red[0] + red[1]) + (red[2] + red[3]));
 }
 
 // Backward of s-projection + LSTM cell for step t.  grid (H/16, ceil(B/16)).
@@ -340,10 +340,10 @@ void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const flo
   launch_linear2(cb, H, hb, H, WsT, bs, nullptr, s_out, nullptr, B, A, st);
 }
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
-                     int N, int A, int H, int E, hipStream_t st) {
+                     int N, int A, int H, int E, bool det, hipStream_t st) {
   const int Kt = A + 2 * H + E;
   const int cols = (Kt + 255) / 256;
-  const int nsplit = max(1, min((N + 63) / 64, 2048 / cols));
+  const int nsplit = det ? 1 : max(1, min((N + 63) / 64, 2048 / cols));
   const int rows_per = (N + nsplit - 1) / nsplit;
   hipLaunchKernelGGL(pgen_bwd_kernel, dim3(cols, nsplit), dim3(256), 0, st, ctx, c, h, x, dpre, gw, N, A, H, E,
                      rows_per);

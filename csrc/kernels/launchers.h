@@ -78,7 +78,7 @@ void launch_linear2_pair(const bf16* a1, int K1, const bf16* a2, int K2, const b
 void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x, const float* w, const float* b,
                  float* pg, int R, int A, int H, int E, hipStream_t st);
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
-                     int N, int A, int H, int E, hipStream_t st);
+                     int N, int A, int H, int E, bool det, hipStream_t st);
 int lstm_persistent_grid(int H, int B);
 int lstm_persistent_capacity(int H);
 int lstm_persistent_launches(int H, int B);
@@ -129,6 +129,9 @@ int cast_colsum_blocks(int N, int C);
 void launch_cast_colsum(const float* x, bf16* xb, float* part, float* colsum, int N, int C, hipStream_t st);
 void launch_emb_grad_sorted(float* gemb, const int* sid, const int* perm, const float* src0, int n0,
                             const float* src1, int n1, int E, int V, hipStream_t st);
+int emb_grad_det_chunks(int n);
+void launch_emb_grad_det(float* gemb, const int* sid, const int* perm, const float* src0, int n0, const float* src1,
+                         int n1, int E, int V, float* pf, float* pl, hipStream_t st);
 
 // debug build record (debug.hip, dcheck.h)
 int tsamd_debug_enabled();

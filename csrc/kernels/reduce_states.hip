@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void rs_bwd_kernel(
       cs += v;
       Ds[rr][col] = f2bf(v);
     }
-    atomicAdd(gb + col, cs);
+    if (gb) atomicAdd(gb + col, cs);
   }
   __syncthreads();
   // d_old[r][j] = sum_u dp[r][u] R[j][u], j < 2H: MFMA A = dp rows (LDS), B = R rows

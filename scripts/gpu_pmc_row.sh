@@ -4,12 +4,13 @@
 # (VALU, transcendental, VMEM), bytes fetched.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/pmc_row; mkdir -p $OUT
+OUT=gpurun_out/${OUTD:-pmc_row}; mkdir -p $OUT
 export TMPDIR=/tmp
-R="attn_fwd_row|attn_bwd_row|attn_bwd_feat"
+R="attn_fwd_row|attn_bwd_row|attn_bwd_feat|attn_bwd_step4"
+PROG=${PROG:-tools/attn_micro.py}
 p() {  # name counters...
   local n=$1; shift
-  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$R" -d $OUT/$n -o run --output-format csv -- python3 tools/attn_micro.py > $OUT/$n.log 2>&1 || { tail -5 $OUT/$n.log; return 1; }
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$R" -d $OUT/$n -o run --output-format csv -- python3 $PROG > $OUT/$n.log 2>&1 || { tail -5 $OUT/$n.log; return 1; }
   python scripts/pmc_sum.py $(find $OUT/$n -name "*counter_collection.csv") | tee $OUT/$n.txt
 }
 p p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD &&

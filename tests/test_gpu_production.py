@@ -234,3 +234,27 @@ def test_config5_batch2048_graph_replays():
         del tr
         torch.cuda.empty_cache()
     assert all(math.isfinite(x) for x in losses) and losses[-1] < losses[0], losses
+
+
+@pytest.mark.parametrize("B", [64, 256])
+def test_deterministic_mode_bit_identical(monkeypatch, B):
+    """TSAMD_DETERMINISTIC=1: no fp32 atomics in the step (fixed-order embedding / bias /
+    attention-parameter reductions, row attention backward, inline weight gradients), so two
+    trainings from the same init on the same batches end with bit-identical parameters and
+    Adagrad accumulators after 5 captured steps; and the result stays close to the default
+    (atomic) path."""
+    from textsummarization_on_flink_amd.train.trainer import GraphTrainer
+    hps = _hps(B)
+    vocab, batches = _batches(hps, 3, seed=17)
+    res = {}
+    for mode, det in (("det1", "1"), ("det2", "1"), ("atomic", "0")):
+        monkeypatch.setenv("TSAMD_DETERMINISTIC", det)
+        tr = GraphTrainer(hps, vocab.size(), B=B, T=T, device="cuda:0")
+        assert tr.engine.det == (det == "1")
+        for i in range(5):
+            tr.check_finite(tr.step(batches[i % len(batches)]))
+        res[mode] = (tr.params.flat.clone(), tr.params.accum.clone())
+        del tr
+        torch.cuda.empty_cache()
+    assert torch.equal(res["det1"][0], res["det2"][0]) and torch.equal(res["det1"][1], res["det2"][1])
+    assert _rel(res["det1"][0], res["atomic"][0]) < 1e-3

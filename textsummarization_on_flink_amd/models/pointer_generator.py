@@ -295,7 +295,11 @@ class HipPointerGenerator:
         self._late = []
         # Measured (bench A/B): +0.6-1.3% at B = 256; at B = 64 / 128 the BPTT it runs beside
         # slows more (its hand-offs are latency-bound) than the moved work saves, so B >= 256.
-        self.defer_wgrad = (cfg.defer_wgrad and B >= 256 and E % 128 == 0
+        # deterministic mode (cfg.deterministic): no fp32 atomics anywhere in the step -- fixed-order
+        # reductions for the embedding, bias and attention-parameter gradients, the row-resident
+        # attention backward (no atomics over position blocks), the weight gradients inline
+        self.det = cfg.deterministic
+        self.defer_wgrad = (not self.det and cfg.defer_wgrad and B >= 256 and E % 128 == 0
                             and H % 128 == 0 and (
             not self.persistent_lstm or
             int(self.k.lstm_persistent_grid(H, B)) <= int(self.k.lstm_persistent_capacity(H)) - 64))
@@ -307,11 +311,12 @@ class HipPointerGenerator:
         # row-resident attention (attention_row.hip: one workgroup per row and step, forward
         # score + softmax + context in one launch) when the batch fills the CUs; else the
         # multi-block-per-row kernels of attention.hip.  cfg.row_attn forces it on / off.
-        self.row_attn = bool(self.k.attn_row_ok(A, T)) and (cfg.row_attn if cfg.row_attn is not None else B >= 128)
+        self.row_attn = bool(self.k.attn_row_ok(A, T)) and (
+            cfg.row_attn if cfg.row_attn is not None else (B >= 128 or self.det))
         # backward: the row kernel at A = 1024 (16 features per lane, 8 waves at 256 VGPRs)
         # hides too little latency -- config #5 decoder backward 79 ms vs 59 ms with the
         # multi-block attn_bwd_step (tools/phase_micro.py) -- so it is used at A = 512 only
-        self.row_attn_bwd = self.row_attn and (A == 512 or cfg.row_attn is True)
+        self.row_attn_bwd = self.row_attn and (A == 512 or cfg.row_attn is True or self.det)
         w["F"] = z(B, T, A, dt=BF)
         # transposed copy for the lanes-over-positions score kernel (not needed by the row
         # kernels; the beam decoder sets keep_ft to get it from _encoder_forward)
@@ -372,8 +377,16 @@ class HipPointerGenerator:
         w["ATTb"] = z(D, B, T, dt=BF)
         w["DCTXb"] = z(D, B, A, dt=BF)
         self._dE = z(B, T, A)
-        w["dv"] = z(32, A)   # attn_bwd_feat partial rows (spread the atomics), summed after
-        w["dwc"] = z(32, A)
+        # attn_bwd_feat partial rows (spread the atomics), summed after; deterministic mode: one
+        # row per workgroup (a single writer per slot)
+        nfeat = ((T + 15) // 16) * B
+        nslot = 1 << (nfeat - 1).bit_length() if self.det else 32
+        w["dv"] = z(nslot, A)
+        w["dwc"] = z(nslot, A)
+        if self.det:  # embedding-gradient chunk partials (emb_grad_det)
+            nc = int(self.k.emb_grad_det_chunks(B * T + D * B))
+            w["emb_pf"] = z(nc, E)
+            w["emb_pl"] = z(nc, E)
         # optimizer
         w["opt_part"] = z(int(self.k.opt_parts()))
         w["gnorm"] = z(1)
@@ -645,7 +658,9 @@ class HipPointerGenerator:
             if need_grad:
                 w["dbias"].zero_()
                 k.vocab_train_bwd(w["outb_ext"], self.pk["owT"], p[OV], w["target_t"], w["lse"], w["alpha"],
-                                  w["dlogits"], w["dbias"], N, V, H, ldx)
+                                  w["dlogits"], None if self.det else w["dbias"], N, V, H, ldx)
+                if self.det:  # column sums of the bf16 dlogits in a fixed order
+                    torch.sum(w["dlogits"], 0, dtype=F32, out=w["dbias"])
             return
         torch.addmm(self.pk["ovb"], w["outb"], self.pk["ow"], out=w["logits"])
         self.k.ptr_loss(w["logits"], None, w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None,
@@ -782,10 +797,12 @@ class HipPointerGenerator:
             pm = p[PG_M].view(-1)
             # one fused column-reduction kernel for the four p_gen weight slices (gw zeroed above)
             k.pgen_bwd(w["CTX"].view(N, A), w["Cst"][1:].reshape(N, H), Hn, w["X"].view(N, E), dpre,
-                       g(PG_M).view(-1), N, A, H, E)
+                       g(PG_M).view(-1), N, A, H, E, self.det)
             # direct terms dCTX/dH += dp w_ctx/h, dC/dX = dp w_c/x and the bias gradient, one launch
             dC_dir, dX_dir = w["dC_dir"], w["dX_dir"]
-            k.pgen_dirs(dpre, pm, dCTX_dir, dC_dir, dH_dir, dX_dir, g(PG_B).view(1), N, A, H, E)
+            k.pgen_dirs(dpre, pm, dCTX_dir, dC_dir, dH_dir, dX_dir, None if self.det else g(PG_B).view(1), N, A, H, E)
+            if self.det:
+                torch.sum(dpre, 0, keepdim=True, out=g(PG_B).view(1))
         if dX_dir is not None and D > 1:  # p_gen path into ctx_{t-1} through x_t (hoisted out of the loop)
             dCTX_dir[:D - 1].view((D - 1) * B, A).addmm_(dX_dir[1:].view((D - 1) * B, E), p[LIN_M][E:].t())
         # ---- decoder reverse loop
@@ -881,7 +898,11 @@ class HipPointerGenerator:
         # d[c_fw, c_bw] / d[h_fw, h_bw] written straight into the top layer's BPTT seeds
         top = self.enc[-1]
         k.rs_bwd(w["dc_carry"], w["dh_rec"], w["rs_pre"][0], w["rs_pre"][1], self.pk["RC"], self.pk["RH"],
-                 w["rs_dp"][0], w["rs_dp"][1], g(BRC), g(BRH), top["dc_carry"], top["dh_fin"], B, H)
+                 w["rs_dp"][0], w["rs_dp"][1], None if self.det else g(BRC), None if self.det else g(BRH),
+                 top["dc_carry"], top["dh_fin"], B, H)
+        if self.det:  # bias gradients: relu'-masked row sums in a fixed order
+            for pre, gsrc, dst in ((w["rs_pre"][0], w["dc_carry"], g(BRC)), (w["rs_pre"][1], w["dh_rec"], g(BRH))):
+                torch.sum(torch.where(pre > 0, gsrc, torch.zeros_like(gsrc)), 0, out=dst)
         torch.mm(w["rs_cat"][0].t(), w["rs_dp"][0], out_dtype=F32, out=g(RC))
         torch.mm(w["rs_cat"][1].t(), w["rs_dp"][1], out_dtype=F32, out=g(RH))
         # ---- encoder BPTT, top layer down
@@ -899,7 +920,8 @@ class HipPointerGenerator:
                 w["lstm_xb"].zero_()
                 w["lstm_db"].zero_()
                 k.lstm_bwd_persistent(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"], st["dc_carry"],
-                                      st["acts"], st["cs"], lens, w["lstm_xb"], w["lstm_err"], w["lstm_db"], T, B, H)
+                                      st["acts"], st["cs"], lens, w["lstm_xb"], w["lstm_err"],
+                                      None if self.det else w["lstm_db"], T, B, H)
             else:
                 for s in reversed(range(T)):
                     k.lstm_enc_bwd_step(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"],
@@ -910,7 +932,7 @@ class HipPointerGenerator:
                 gkd = g(enc_k(layer, d))
                 wgrad_into(gkd[:din], st["x_sf"][di].view(T * B, din), dzd)
                 wgrad_into(gkd[din:], st["hs"][di, :T].reshape(T * B, H), dzd)
-                if self.persistent_lstm:
+                if self.persistent_lstm and not self.det:
                     g(enc_b(layer, d)).copy_(w["lstm_db"][di])
                 else:
                     g(enc_b(layer, d)).copy_(dzd.sum(0, dtype=F32))
@@ -923,7 +945,11 @@ class HipPointerGenerator:
         # Zipf-hot tokens do not serialise
         if late:
             torch.cuda.current_stream().wait_stream(self._late_stream)  # d_emb_dec and the weight gradients
-        k.emb_grad_sorted(gemb, w["emb_sid"], w["emb_perm"], d_in.reshape(B * T, self.E), w["d_emb_dec"])
+        if self.det:
+            k.emb_grad_det(gemb, w["emb_sid"], w["emb_perm"], d_in.reshape(B * T, self.E), w["d_emb_dec"],
+                           w["emb_pf"], w["emb_pl"])
+        else:
+            k.emb_grad_sorted(gemb, w["emb_sid"], w["emb_perm"], d_in.reshape(B * T, self.E), w["d_emb_dec"])
         if self.poison_on_lstm_err:
             from ..parallel.dist import poison_where
             poison_where(w["lstm_err"], p.grad[-1:])
