@@ -536,9 +536,9 @@ void vocab_topk(const Tensor& X, const Tensor& WT, const Tensor& bias, const OT&
                 int64_t beam) {
   chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(ext, I32, "ext"); chk(lens, I32, "lens");
   chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp"); chk(logits, F32, "logits"); chk(part_ms, F32, "part_ms");
-  const int64_t nt = vocab_topk_tiles((int)V);
+  const int64_t nt = vocab_topk_tiles((int)V, (int)H);
   TORCH_CHECK(K >= 1 && K <= 8 && beam >= 1 && R % beam == 0 && T <= 2048, "bad vocab_topk args (K <= 8)");
-  TORCH_CHECK(H % 32 == 0 && H <= 256 && nt <= 4096, "vocab_topk: H % 32 == 0, H <= 256, V <= 1M");
+  TORCH_CHECK(H % 32 == 0 && (H <= 256 || H == 512) && nt <= 4096, "vocab_topk: H % 32 == 0, H <= 256 or 512, V <= 512k");
   numel_eq(X, R * H, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias");
   numel_eq(ext, (R / beam) * T, "ext"); numel_eq(lens, R / beam, "lens");
   numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
@@ -560,9 +560,9 @@ void vocab_topk_pg(const Tensor& X, const Tensor& WT, const Tensor& bias, const 
   chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp"); chk(logits, F32, "logits"); chk(part_ms, F32, "part_ms");
   chk(ctx, F32, "ctx"); chk(c, F32, "c"); chk(h, BF, "h"); chk(x, F32, "x"); chk(pg_w, F32, "pg_w");
   chk(pg_b, F32, "pg_b"); chk(pg_out, F32, "pg_out"); chk(attn, F32, "attn");
-  const int64_t nt = vocab_topk_tiles((int)V);
+  const int64_t nt = vocab_topk_tiles((int)V, (int)H);
   TORCH_CHECK(K >= 1 && K <= 8 && beam >= 1 && R % beam == 0 && T <= 2048, "bad vocab_topk args (K <= 8)");
-  TORCH_CHECK(H % 32 == 0 && H <= 256 && nt <= 4096, "vocab_topk: H % 32 == 0, H <= 256, V <= 1M");
+  TORCH_CHECK(H % 32 == 0 && (H <= 256 || H == 512) && nt <= 4096, "vocab_topk: H % 32 == 0, H <= 256 or 512, V <= 512k");
   numel_eq(X, R * H, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias");
   numel_eq(ext, (R / beam) * T, "ext"); numel_eq(lens, R / beam, "lens");
   numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
@@ -575,7 +575,122 @@ void vocab_topk_pg(const Tensor& X, const Tensor& WT, const Tensor& bias, const 
                     P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), R, V, H, T, K, beam, pgi,
                     stream());
 }
-int64_t vocab_topk_parts(int64_t V) { return vocab_topk_tiles((int)V); }
+int64_t vocab_topk_parts(int64_t V, int64_t H) { return vocab_topk_tiles((int)V, (int)H); }
+
+// One beam-decode step's head: vocab_topk (p_gen inside when the pointer inputs are given) with
+// the beam bookkeeping fused into the select kernel's per-article tail (replaces vocab_topk_pg +
+// beam_step).  The step counter was advanced at the start of the step (dec_cell_fwd_beam).
+void vocab_topk_beam(const Tensor& X, const Tensor& WT, const Tensor& bias, const OT& ctx, const OT& c, const OT& h,
+                     const OT& x, const OT& pg_w, const OT& pg_b, const OT& pg_out, const OT& attn, const Tensor& ext,
+                     const Tensor& lens, const Tensor& out_ids, const Tensor& out_lp, const Tensor& logits,
+                     const Tensor& part_ms, const Tensor& lp_sum, const Tensor& latest, const Tensor& gidx,
+                     const Tensor& tok_hist, const Tensor& par_hist, const Tensor& done, const Tensor& res_count,
+                     const Tensor& res_score, const Tensor& res_len, const Tensor& res_step, const Tensor& res_par,
+                     const Tensor& step, const Tensor& art_ctr, const Tensor& gran, const Tensor& err,
+                     const OT& att_hist, const OT& pg_hist, int64_t R,
+                     int64_t V, int64_t H, int64_t T, int64_t K, int64_t beam, int64_t A, int64_t E, int64_t stop_id,
+                     int64_t min_dec, int64_t max_dec) {
+  chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(ext, I32, "ext"); chk(lens, I32, "lens");
+  chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp"); chk(logits, F32, "logits"); chk(part_ms, F32, "part_ms");
+  const int64_t nt = vocab_topk_tiles((int)V, (int)H), Na = R / beam;
+  TORCH_CHECK(K >= 1 && K <= 8 && beam >= 1 && R % beam == 0 && T <= 2048 && beam * K <= 64, "bad vocab_topk_beam args");
+  TORCH_CHECK(H % 32 == 0 && (H <= 256 || H == 512) && nt <= 4096, "vocab_topk: H % 32 == 0, H <= 256 or 512, V <= 512k");
+  numel_eq(X, R * H, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias");
+  numel_eq(ext, Na * T, "ext"); numel_eq(lens, Na, "lens");
+  numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
+  numel_eq(logits, R * V, "logits"); numel_eq(part_ms, R * nt * 2, "part_ms"); chko(attn, F32, R * T, "attn");
+  const bool ptr = pg_w.has_value() && pg_w->defined();
+  PgIn pgi{};
+  if (ptr) {
+    chko(ctx, F32, R * A, "ctx"); chko(c, F32, R * H, "c"); chko(h, BF, R * H, "h"); chko(x, F32, R * E, "x");
+    chko(pg_w, F32, A + 2 * H + E, "pg_w"); chko(pg_b, F32, 1, "pg_b"); chko(pg_out, F32, R, "pg_out");
+    TORCH_CHECK(PO<float>(ctx) && PO<float>(c) && PO<bf16>(h) && PO<float>(x) && PO<float>(pg_b) && PO<float>(attn),
+                "pointer mode needs ctx, c, h, x, pg_b and attn");
+    pgi = PgIn{PO<float>(ctx), PO<float>(c), PO<bf16>(h), PO<float>(x), PO<float>(pg_w), PO<float>(pg_b),
+               PO<float>(pg_out), (int)A, (int)H, (int)E};
+  }
+  chk(lp_sum, F32, "lp_sum"); chk(latest, I32, "latest"); chk(gidx, I32, "gidx"); chk(tok_hist, I32, "tok_hist");
+  chk(par_hist, I32, "par_hist"); chk(done, I32, "done"); chk(res_count, I32, "res_count");
+  chk(res_score, F32, "res_score"); chk(res_len, I32, "res_len"); chk(res_step, I32, "res_step");
+  chk(res_par, I32, "res_par"); chk(step, I32, "step"); chk(art_ctr, I32, "art_ctr");
+  numel_eq(lp_sum, R, "lp_sum"); numel_eq(latest, R, "latest"); numel_eq(gidx, R, "gidx");
+  numel_eq(tok_hist, max_dec * R, "tok_hist"); numel_eq(par_hist, max_dec * R, "par_hist"); numel_eq(done, Na, "done");
+  numel_eq(res_count, Na, "res_count"); numel_eq(res_score, R, "res_score"); numel_eq(res_len, R, "res_len");
+  numel_eq(res_step, R, "res_step"); numel_eq(res_par, R, "res_par"); numel_eq(step, 1, "step");
+  numel_eq(art_ctr, Na, "art_ctr"); chk(gran, at::kLong, "gran"); numel_eq(gran, R * K, "gran");
+  chk(err, I32, "err"); numel_eq(err, 1, "err");
+  TORCH_CHECK(V + T < (1 << 17), "vocab_topk_beam: extended ids must fit 17 bits");
+  chko(att_hist, F32, max_dec * R * T, "att_hist"); chko(pg_hist, F32, max_dec * R, "pg_hist");
+  TORCH_CHECK(!PO<float>(att_hist) || PO<float>(attn), "att_hist needs attn");
+  TORCH_CHECK(!PO<float>(pg_hist) || (ptr && PO<float>(att_hist)), "pg_hist needs the pointer inputs and att_hist");
+  const BeamTail bt{P<float>(lp_sum), P<int>(latest), P<int>(gidx), P<int>(tok_hist), P<int>(par_hist), P<int>(done),
+                    P<int>(res_count), P<float>(res_score), P<int>(res_len), P<int>(res_step), P<int>(res_par),
+                    P<int>(step), (unsigned*)P<int>(art_ctr), (unsigned long long*)gran.data_ptr(), P<int>(err),
+                    PO<float>(attn), PO<float>(att_hist), PO<float>(pg_out),
+                    PO<float>(pg_hist), (int)T, (int)Na, (int)beam, (int)K, (int)stop_id, (int)min_dec, (int)max_dec};
+  launch_vocab_topk(P<bf16>(X), P<bf16>(WT), P<float>(bias), nullptr, ptr ? PO<float>(attn) : nullptr, P<int>(ext),
+                    P<int>(lens), P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), R, V, H, T, K,
+                    beam, pgi, stream(), &bt);
+}
+
+// decoder cell of a beam-decode step with the parent / token gathers inside (dec_cell_fwd +
+// the former beam_gather): rows read c/h/ctx of parent gidx[r] from the previous state set and
+// XGtab[latest[r]]; step[0] += 1
+void dec_cell_fwd_beam(const Tensor& gidx, const Tensor& latest, const Tensor& XGtab, const Tensor& ctx_src,
+                       const Tensor& h_src, const Tensor& c_src, const Tensor& WcT, const Tensor& c_out,
+                       const Tensor& cb_out, const Tensor& hb_out, const Tensor& step, int64_t R, int64_t H, int64_t A,
+                       int64_t V, int64_t unk) {
+  chk(gidx, I32, "gidx"); chk(latest, I32, "latest"); chk(XGtab, F32, "XGtab"); chk(ctx_src, BF, "ctx_src");
+  chk(h_src, BF, "h_src"); chk(c_src, F32, "c_src"); chk(WcT, BF, "WcT"); chk(c_out, F32, "c_out");
+  chk(cb_out, BF, "cb_out"); chk(hb_out, BF, "hb_out"); chk(step, I32, "step");
+  TORCH_CHECK(H % 16 == 0 && A % 32 == 0 && H % 32 == 0 && unk >= 0 && unk < V, "bad dims");
+  numel_eq(gidx, R, "gidx"); numel_eq(latest, R, "latest"); numel_eq(XGtab, V * 4 * H, "XGtab");
+  numel_eq(ctx_src, R * A, "ctx_src"); numel_eq(h_src, R * H, "h_src"); numel_eq(c_src, R * H, "c_src");
+  numel_eq(WcT, 4 * H * (A + H), "WcT"); numel_eq(c_out, R * H, "c_out"); numel_eq(cb_out, R * H, "cb_out");
+  numel_eq(hb_out, R * H, "hb_out"); numel_eq(step, 1, "step");
+  launch_dec_cell_fwd_beam(P<int>(gidx), P<int>(latest), P<float>(XGtab), P<bf16>(ctx_src), P<bf16>(h_src),
+                           P<float>(c_src), P<bf16>(WcT), P<float>(c_out), P<bf16>(cb_out), P<bf16>(hb_out),
+                           P<int>(step), (int)R, (int)H, (int)A, (int)V, (int)unk, stream());
+}
+
+// s = [cb, hb] . WsT^T + bs  and  x = Xtab[latest] + ctx_src[gidx] . WicT^T  in one launch
+void beam_sproj_xmerge(const Tensor& cb, const Tensor& hb, const Tensor& WsT, const Tensor& bs, const Tensor& s_out,
+                       const Tensor& ctx_src, const Tensor& WicT, const Tensor& Xtab, const Tensor& gidx,
+                       const Tensor& latest, const Tensor& x_out, int64_t R, int64_t H, int64_t A, int64_t E,
+                       int64_t V, int64_t unk) {
+  chk(cb, BF, "cb"); chk(hb, BF, "hb"); chk(WsT, BF, "WsT"); chk(bs, F32, "bs"); chk(s_out, F32, "s_out");
+  chk(ctx_src, BF, "ctx_src"); chk(WicT, BF, "WicT"); chk(Xtab, F32, "Xtab"); chk(gidx, I32, "gidx");
+  chk(latest, I32, "latest"); chk(x_out, F32, "x_out");
+  TORCH_CHECK(H % 32 == 0 && A % 32 == 0 && A % 16 == 0 && E % 16 == 0 && unk >= 0 && unk < V, "bad dims");
+  numel_eq(cb, R * H, "cb"); numel_eq(hb, R * H, "hb"); numel_eq(WsT, A * 2 * H, "WsT"); numel_eq(bs, A, "bs");
+  numel_eq(s_out, R * A, "s_out"); numel_eq(ctx_src, R * A, "ctx_src"); numel_eq(WicT, E * A, "WicT");
+  numel_eq(Xtab, V * E, "Xtab"); numel_eq(gidx, R, "gidx"); numel_eq(latest, R, "latest"); numel_eq(x_out, R * E, "x_out");
+  launch_beam_sproj_xmerge(P<bf16>(cb), P<bf16>(hb), P<bf16>(WsT), P<float>(bs), P<float>(s_out), P<bf16>(ctx_src),
+                           P<bf16>(WicT), P<float>(Xtab), P<int>(gidx), P<int>(latest), P<float>(x_out), (int)R,
+                           (int)H, (int)A, (int)E, (int)V, (int)unk, stream());
+}
+
+// attn_fwd_row of a beam-decode step with the coverage gather: cov = cov_src[g] + a_src[g]
+// (g = gidx[row]) used for the scores and kept in cov_keep for the next step
+void attn_fwd_row_beam(const Tensor& F, const Tensor& E, const Tensor& s, const Tensor& v, const OT& wc,
+                       const OT& cov_src, const OT& a_src, const OT& cov_keep, const Tensor& gidx, const Tensor& lens,
+                       const Tensor& a_out, const Tensor& ctx, const OT& ctx_bf, int64_t B, int64_t T, int64_t A,
+                       int64_t rep) {
+  chk(F, BF, "F"); chk(E, BF, "E"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens"); chk(gidx, I32, "gidx");
+  chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
+  TORCH_CHECK(attn_row_supported((int)A, (int)T), "row attention needs A in {512, 1024} and T <= 2048");
+  TORCH_CHECK(rep >= 1 && B % rep == 0, "attn_fwd_row_beam: rep must divide B");
+  numel_eq(F, B / rep * T * A, "F"); numel_eq(E, B / rep * T * A, "E"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v");
+  numel_eq(lens, B / rep, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * A, "ctx"); numel_eq(gidx, B, "gidx");
+  chko(wc, F32, A, "wc"); chko(cov_src, F32, B * T, "cov_src"); chko(a_src, F32, B * T, "a_src");
+  chko(cov_keep, F32, B * T, "cov_keep"); chko(ctx_bf, BF, B * A, "ctx_bf");
+  const bool cov = PO<float>(cov_src) != nullptr;
+  TORCH_CHECK(cov == (PO<float>(a_src) != nullptr) && cov == (PO<float>(cov_keep) != nullptr),
+              "coverage gather: cov_src, a_src and cov_keep together");
+  launch_attn_fwd_row(P<bf16>(F), P<bf16>(E), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov_src), P<int>(lens),
+                      P<float>(a_out), nullptr, nullptr, P<float>(ctx), PO<bf16>(ctx_bf), B, T, A, (int)rep, stream(),
+                      cov ? P<int>(gidx) : nullptr, PO<float>(a_src), PO<float>(cov_keep));
+}
 
 
 // Advances step[0] by one (the last block to finish) when ctr (one zeroed uint32 scratch word)
@@ -755,5 +870,9 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("pgen", &pgen);
   m.def("vocab_topk", &vocab_topk);
   m.def("vocab_topk_parts", &vocab_topk_parts);
+  m.def("vocab_topk_beam", &vocab_topk_beam);
+  m.def("dec_cell_fwd_beam", &dec_cell_fwd_beam);
+  m.def("beam_sproj_xmerge", &beam_sproj_xmerge);
+  m.def("attn_fwd_row_beam", &attn_fwd_row_beam);
   m.def("pgen_bwd", &pgen_bwd);
 }

@@ -63,7 +63,11 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     const bf16* __restrict__ F, const bf16* __restrict__ E, const float* __restrict__ s,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
     const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
-    float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T, int rep, int xper) {
+    float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T, int rep, int xper,
+    const int* __restrict__ cg, const float* __restrict__ asrc, float* __restrict__ cov_keep) {
+  // cg set (beam decode): the coverage of hypothesis row b is its parent's coverage plus the
+  // parent's last attention, cov = cov[g] + asrc[g] with g = cg[b] (the gather of the former
+  // beam_gather kernel); cov_keep receives it for the next step
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float es[kRowMaxT];
   __shared__ float part[NW][A];
@@ -76,6 +80,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = (int)DCHECK_IDX(lens[fr], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
+  const size_t cb = cg ? (size_t)DCHECK_IDX(cg[b], 0, (int)gridDim.x, CHK_BEAM_PARENT) * T : rb;
   const bf16* Fb = F + (size_t)fr * T * A;
   const bf16* Eb = E + (size_t)fr * T * A;
   const int ngrp = (len + 3) >> 2;
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     load_rows<NK>(f, Fb, 4 * grp, len, lane);
     load_rows<NK>(e, Eb, 4 * grp, len, lane);
     const int p = min(4 * grp + qm, len - 1);
-    c = cov ? cov[rb + p] : 0.f;
+    c = cov ? cov[cb + p] + (cg ? asrc[cb + p] : 0.f) : 0.f;
   };
   if (wid < ngrp) load(wid, fA, eA, cA);
   const float* srow = s + (size_t)b * A;
@@ -192,6 +197,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
   for (int i = tid; i < T; i += NT) {
     const float a = i < len ? fexp(es[i] - m) * invL : 0.f;
     a_out[rb + i] = a;
+    if (cov_keep) cov_keep[rb + i] = cov[cb + i] + asrc[cb + i];
     if (cov_out) {
       const float c = cov ? cov[rb + i] : 0.f;
       cov_out[rb + i] = c + a;
@@ -356,12 +362,13 @@ bool attn_row_supported(int A, int T) { return (A == 512 || A == 1024) && T >= 1
 
 void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
                          const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
-                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st) {
+                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st, const int* cg, const float* asrc,
+                         float* cov_keep) {
   // beam decode: each XCD takes whole articles (their hypotheses share F / E rows in its L2)
   const int xper = (rep > 1 && B % 8 == 0 && (B / 8) % rep == 0) ? B / 8 : 0;
 #define LF(NK)                                                                                                 \
   hipLaunchKernelGGL((attn_fwd_row_kernel<NK, row_waves<NK, false>()>), dim3(B), dim3(row_waves<NK, false>() * 64), \
-                     0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep, xper)
+                     0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep, xper, cg, asrc, cov_keep)
   if (A == 512) LF(1);
   else LF(2);
 #undef LF

@@ -17,6 +17,7 @@
 // Parents / tokens / scores of the new hyps are written for the next step's gather, plus
 // the (token, parent) history used to backtrack the final sequences on the host.
 #include "common.h"
+#include "beam_common.h"
 
 #define TOPK_MAX 16
 #define TOPK_THREADS 256
@@ -263,68 +264,6 @@ __global__ __launch_bounds__(TOPK_THREADS) void final_topk_merge_kernel(
   }
 }
 
-// ------------------------------------------------------------------ beam bookkeeping
-__device__ __forceinline__ void beam_step_body(
-    const int* __restrict__ top_ids, const float* __restrict__ top_lp, float* __restrict__ lp_sum,
-    int* __restrict__ latest, int* __restrict__ gidx, int* __restrict__ tok_hist, int* __restrict__ par_hist,
-    int* __restrict__ done, int* __restrict__ res_count, float* __restrict__ res_score, int* __restrict__ res_len,
-    int* __restrict__ res_step, int* __restrict__ res_par, float* cval, int* cid, int* srt, int a, int lane, int t,
-    int base, int beam, int K, int stop_id, int min_dec, float tot, int tid_cand, int nres0) {
-  // tot / tid_cand / nres0: this lane's candidate and the result count, loaded by the caller
-  // in the same memory round trip as the step counter and the done flag
-  const int norig = t == 0 ? 1 : beam;
-  const int ncand = norig * K;
-  if (lane >= ncand) tot = -INFINITY;
-  if (lane < ncand) {
-    cval[lane] = tot;
-    cid[lane] = tid_cand;
-  }
-  // stable rank: descending total, ties keep candidate order
-  int rank = 0;
-  for (int q = 0; q < ncand; ++q) {
-    const float v = __shfl(tot, q, 64);
-    if (v > tot || (v == tot && q < lane)) ++rank;
-  }
-  if (lane < ncand) srt[rank] = lane;
-  __syncthreads();
-  if (lane == 0) {
-    int nres = nres0, nh = 0;
-    float new_lp[TOPK_MAX];
-    int new_tok[TOPK_MAX], new_par[TOPK_MAX];
-    for (int q = 0; q < ncand; ++q) {
-      const int cnd = srt[q];
-      const int i = cnd / K, tok = cid[cnd];
-      const float v = cval[cnd];
-      if (tok == stop_id) {
-        if (t >= min_dec && nres < beam) {
-          res_score[a * beam + nres] = v / (float)(t + 2);
-          res_len[a * beam + nres] = t + 2;
-          res_step[a * beam + nres] = t;
-          res_par[a * beam + nres] = i;
-          ++nres;
-        }
-      } else if (nh < beam) {
-        new_lp[nh] = v;
-        new_tok[nh] = tok;
-        new_par[nh] = i;
-        ++nh;
-      }
-      if (nh == beam || nres == beam) break;
-    }
-    res_count[a] = nres;
-    if (nres >= beam) done[a] = 1;
-    for (int k = 0; k < beam; ++k) {
-      const int kk = k < nh ? k : (nh > 0 ? nh - 1 : 0);
-      const int par = nh > 0 ? new_par[kk] : 0;
-      lp_sum[base + k] = nh > 0 ? new_lp[kk] : -INFINITY;
-      latest[base + k] = nh > 0 ? new_tok[kk] : stop_id;
-      gidx[base + k] = base + par;
-      tok_hist[(size_t)t * gridDim.x * beam + base + k] = nh > 0 ? new_tok[kk] : stop_id;
-      par_hist[(size_t)t * gridDim.x * beam + base + k] = par;
-    }
-  }
-}
-
 __global__ __launch_bounds__(64) void beam_step_kernel(
     const int* __restrict__ top_ids, const float* __restrict__ top_lp,  // [R][K]
     float* __restrict__ lp_sum,        // [R] in: per live hyp; out: per new hyp
@@ -367,7 +306,7 @@ __global__ __launch_bounds__(64) void beam_step_kernel(
   } else {
     beam_step_body(top_ids, top_lp, lp_sum, latest, gidx, tok_hist, par_hist, done, res_count, res_score, res_len,
                    res_step, res_par, cval, cid, srt, a, lane, t, base, beam, K, stop_id, min_dec, tot, tid_cand,
-                   nres0);
+                   nres0, (int)gridDim.x);
   }
   // grid-wide step advance (standalone use): every block read *step above; the last one to
   // arrive bumps it -- a fence plus one same-address atomic per article (64 serialised L2

@@ -37,6 +37,23 @@ __device__ __forceinline__ void xcd_tile(int& tx, int& ty) {
 // z = XG + [ctx, h] . WcT^T ; cell update.  WcT: [4H][A+H] (cols 0..A-1 = W_comb^T, A.. = W_cell[E:]^T).
 // grid (H/16, ceil(B/16)).  KB: k-steps per load batch (kslice_mma) -- 6 covers a wave's
 // K / 4 = 192 at hidden 256 in one L2 round trip instead of two.
+// Beam-decode gather (optional): row r of the step reads its parent row g = gidx[r] of the
+// previous state set (c, h, ctx) and the per-token table row of its latest token (in-article
+// OOV ids -> [UNK]); thread 0 of block 0 advances the decode-step counter.  Replaces a separate
+// beam_gather launch per decode step (device_beam.py).
+struct BeamGather {
+  const int* gidx;      // [B] parent rows (nullptr: no gather, row r reads row r)
+  const int* latest;    // [B] latest token ids
+  const float* XGtab;   // [V][4H] per-token gate inputs (replaces XG)
+  int V, unk;
+  int* step;            // decode-step counter (nullable)
+};
+
+__device__ __forceinline__ int bg_tok(const BeamGather& bg, int r) {
+  const int t = (int)DCHECK_IDX(bg.latest[r], 0, 0x7fffffff, CHK_BEAM_TOKEN);
+  return t < bg.V ? t : bg.unk;
+}
+
 template <int KB>
 __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
     const float* __restrict__ XG,      // [B][4H]
@@ -45,10 +62,11 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
     const float* __restrict__ cprev,   // [B][H]
     const bf16* __restrict__ WcT,      // [4H][A+H]
     float* __restrict__ c_out, bf16* __restrict__ cb_out, bf16* __restrict__ hb_out,  // [B][H]
-    float* __restrict__ act,           // [B][4H]
-    int B, int H, int A) {
+    float* __restrict__ act,           // [B][4H] (nullable)
+    int B, int H, int A, BeamGather bg) {
   __shared__ float red[4 * 4 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (bg.step && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *bg.step += 1;
   int tx, ty;
   xcd_tile(tx, ty);
   const int u0 = tx * 16, r0 = ty * 16;
@@ -56,14 +74,17 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
   const int r = r0 + (lane >> 4) * 4 + wid, u = u0 + (lane & 15);
   const bool rok = r < B;
   const size_t ri = (size_t)(rok ? r : 0) * H + u;
+  // parent row of r (gather mode) for the previous state
+  const int rp = bg.gidx ? (int)DCHECK_IDX(bg.gidx[rok ? r : 0], 0, B, CHK_BEAM_PARENT) : (rok ? r : 0);
   float xg[4], cp;
   {
-    const float* xr = XG + (size_t)(rok ? r : 0) * G;
+    const float* xr = bg.gidx ? bg.XGtab + (size_t)bg_tok(bg, rok ? r : 0) * G : XG + (size_t)(rok ? r : 0) * G;
 #pragma unroll
     for (int g = 0; g < 4; ++g) xg[g] = xr[g * H + u];
-    cp = cprev[ri];
+    cp = cprev[(size_t)rp * H + u];
   }
-  const int ar = min(r0 + (lane & 15), B - 1);
+  const int ar0 = min(r0 + (lane & 15), B - 1);
+  const int ar = bg.gidx ? (int)DCHECK_IDX(bg.gidx[ar0], 0, B, CHK_BEAM_PARENT) : ar0;
   const int kof = 8 * (lane >> 4);
   const bf16* crow = ctxp ? ctxp + (size_t)ar * A + kof : nullptr;
   const bf16* hrow = hprev + (size_t)ar * H + kof - A;  // indexed with absolute k >= A
@@ -86,8 +107,10 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
   c_out[ri] = c;
   cb_out[ri] = f2bf(c);
   hb_out[ri] = f2bf(h);
-  float* a4 = act + (size_t)r * G;
-  a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
+  if (act) {
+    float* a4 = act + (size_t)r * G;
+    a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og;
+  }
 }
 
 // Generic small-M linear on two concatenated bf16 inputs (the shape of every per-step
@@ -95,14 +118,19 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
 //   out[r][n] = sum_{k<K1} a1[r][k] Wt[n][k] + sum_{k<K2} a2[r][k] Wt[n][K1+k] + bias[n] + add[r][n]
 // Wt: [N][K1+K2] bf16 ("Bt" layout).  fp32 and/or bf16 outputs.  grid (N/16, ceil(B/16)),
 // 4 waves split K (kslice_mma) and reduce in LDS.  add may alias out (same element, same lane).
+// Beam-decode gathers (optional): ga -- operand rows read through a parent index (a1 / a2 row
+// ga[r]); gtok -- the add term is a per-token table (add row = table row of token gtok[r], ids
+// >= V -> unk), as the x-merge x = x0[token] + ctx_parent . W_in[E:].
 struct L2Args {
   const bf16* a1; int K1; const bf16* a2; int K2; const bf16* Wt;
   const float* bias; const float* add; float* out; bf16* outb; int N;
+  const int* ga = nullptr; const int* gtok = nullptr; int V = 0, unk = 0;
 };
 
 __device__ __forceinline__ void linear2_body(const L2Args& p, int B, int n0, int r0, float* red) {
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ar = min(r0 + (lane & 15), B - 1);
+  const int ar0 = min(r0 + (lane & 15), B - 1);
+  const int ar = p.ga ? (int)DCHECK_IDX(p.ga[ar0], 0, B, CHK_BEAM_PARENT) : ar0;
   const int kof = 8 * (lane >> 4);
   const int K1 = p.K1, K = p.K1 + p.K2, N = p.N;
   const bf16* r1 = p.a1 + (size_t)ar * K1 + kof;
@@ -118,7 +146,12 @@ __device__ __forceinline__ void linear2_body(const L2Args& p, int B, int n0, int
   const int r = r0 + (lane >> 4) * 4 + wid, n = n0 + (lane & 15);
   if (r >= B) return;
   const size_t ix = (size_t)r * N + n;
-  const float v = o[0] + (p.bias ? p.bias[n] : 0.f) + (p.add ? p.add[ix] : 0.f);
+  size_t ia = ix;
+  if (p.gtok) {
+    const int t = (int)DCHECK_IDX(p.gtok[r], 0, 0x7fffffff, CHK_BEAM_TOKEN);
+    ia = (size_t)(t < p.V ? t : p.unk) * N + n;
+  }
+  const float v = o[0] + (p.bias ? p.bias[n] : 0.f) + (p.add ? p.add[ia] : 0.f);
   if (p.out) p.out[ix] = v;
   if (p.outb) p.outb[ix] = f2bf(v);
 }
@@ -318,7 +351,28 @@ void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, c
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16);
   hipLaunchKernelGGL(dec_cell_fwd_kernel<6>, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out,
-                     hb_out, act, B, H, A);
+                     hb_out, act, B, H, A, BeamGather{nullptr, nullptr, nullptr, 0, 0, nullptr});
+}
+void launch_dec_cell_fwd_beam(const int* gidx, const int* latest, const float* XGtab, const bf16* ctxp,
+                              const bf16* hprev, const float* cprev, const bf16* WcT, float* c_out, bf16* cb_out,
+                              bf16* hb_out, int* step, int B, int H, int A, int V, int unk, hipStream_t st) {
+  dim3 grid(H / 16, (B + 15) / 16);
+  hipLaunchKernelGGL(dec_cell_fwd_kernel<6>, grid, dim3(256), 0, st, nullptr, ctxp, hprev, cprev, WcT, c_out, cb_out,
+                     hb_out, nullptr, B, H, A, BeamGather{gidx, latest, XGtab, V, unk, step});
+}
+// the beam-decode pair: s = [cb, hb] . WsT^T + bs, and x = Xtab[token] + ctx_parent . WicT^T
+void launch_beam_sproj_xmerge(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out,
+                              const bf16* ctx_src, const bf16* WicT, const float* Xtab, const int* gidx,
+                              const int* latest, float* x_out, int B, int H, int A, int E, int V, int unk,
+                              hipStream_t st) {
+  dim3 grid((A > E ? A : E) / 16, (B + 15) / 16, 2);
+  L2Args p0{cb, H, hb, H, WsT, bs, nullptr, s_out, nullptr, A};
+  L2Args p1{ctx_src, A, nullptr, 0, WicT, nullptr, Xtab, x_out, nullptr, E};
+  p1.ga = gidx;
+  p1.gtok = latest;
+  p1.V = V;
+  p1.unk = unk;
+  hipLaunchKernelGGL(linear2_pair_kernel, grid, dim3(256), 0, st, p0, p1, B);
 }
 void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
                     const float* add, float* out, bf16* outb, int B, int N, hipStream_t st) {

@@ -26,7 +26,8 @@ void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, con
 bool attn_row_supported(int A, int T);
 void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
                          const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
-                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st);
+                         bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st, const int* cg = nullptr,
+                         const float* asrc = nullptr, float* cov_keep = nullptr);
 void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,
                          const float* cov, const float* a, const float* dctx, const float* ctx, const float* Ga,
                          const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
@@ -34,6 +35,13 @@ void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const flo
 
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st);
+void launch_dec_cell_fwd_beam(const int* gidx, const int* latest, const float* XGtab, const bf16* ctxp,
+                              const bf16* hprev, const float* cprev, const bf16* WcT, float* c_out, bf16* cb_out,
+                              bf16* hb_out, int* step, int B, int H, int A, int V, int unk, hipStream_t st);
+void launch_beam_sproj_xmerge(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out,
+                              const bf16* ctx_src, const bf16* WicT, const float* Xtab, const int* gidx,
+                              const int* latest, float* x_out, int B, int H, int A, int E, int V, int unk,
+                              hipStream_t st);
 void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out, int B, int H,
                       int A, hipStream_t st);
 void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
@@ -89,7 +97,20 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, float* dbias, int T, int B, int H, hipStream_t st);
-int vocab_topk_tiles(int V);
+int vocab_topk_tiles(int V, int H);
+
+
+// Beam bookkeeping fused into the vocab select kernel (the last row workgroup of each article
+// runs it): lp_sum == nullptr disables it
+struct BeamTail {
+  float* lp_sum; int* latest; int* gidx; int* tok_hist; int* par_hist; int* done; int* res_count;
+  float* res_score; int* res_len; int* res_step; int* res_par; int* step;
+  unsigned* art_ctr;  // [Na] arrival counters (zeroed; reset by the last arrival)
+  unsigned long long* gran;  // [R][K] candidate granules {step tag | id, log-prob} (zeroed per batch)
+  int* err;           // poll-timeout flag
+  const float* att; float* att_hist; const float* pg; float* pg_hist;
+  int T, Na, beam, K, stop_id, min_dec, max_dec;
+};
 // p_gen inputs computed inside the vocab select kernel (w == nullptr: p_gen given instead)
 struct PgIn {
   const float* ctx; const float* c; const bf16* h; const float* x; const float* w; const float* b; float* out;
@@ -97,7 +118,8 @@ struct PgIn {
 };
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
-                       int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st);
+                       int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st,
+                       const BeamTail* bt = nullptr);
 int vocab_train_tiles(int V, int H);
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
                             float* zg, float* lse, float* pv, int N, int V, int H, hipStream_t st);

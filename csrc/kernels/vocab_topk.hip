@@ -13,14 +13,18 @@
 // Replaces a library GEMM + a separate per-element top-k pass over the logits.
 #include "common.h"
 #include "attn_common.h"  // f32x2 packed-FP32 helpers
+#include "beam_common.h"  // beam bookkeeping fused into the select kernel's tail
 #include "launchers.h"
 
-#define VT_COLS 256   // vocab columns per workgroup
-#define VT_ROWS 64    // rows per workgroup
+#define VT_ROWS 64    // rows per workgroup half
 #define VT_K 8        // max K (= 2 * beam, beam <= 4)
-#define VM_CAND 4096  // tile maxima (nt <= 4096), then <= K * VT_COLS survivors + copied ids
+#define VM_CAND 4096  // tile maxima (nt <= 4096), then <= K * 256 survivors + copied ids
 #define VM_HASH 2048
-#define VT_HMAX 256   // hidden size limit of the logits kernel (X tile staged in LDS)
+
+// vocab columns per workgroup: 4 MFMA column tiles per wave up to hidden 256, 2 at hidden 512
+// (the wave's W^T fragments stay at 32 registers of 8 bf16: H/32 k-steps x NI tiles)
+__host__ __device__ constexpr int vt_ni(int HMAX) { return HMAX <= 256 ? 4 : 2; }
+__host__ __device__ constexpr int vt_cols(int HMAX) { return 64 * vt_ni(HMAX); }
 
 namespace {
 
@@ -45,16 +49,16 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 // lane's 4 consecutive columns per i are one 16-byte store (a row's 64 columns = one 256-byte
 // run over the 4 i and 4 q).  Replaced a [row = lane group] layout whose per-row reductions
 // took 16-lane DPP trees for each of the lane's 16 rows and an LDS staging pass for stores.
-template <bool FULL>
-__device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[4][4], int jr, const f32x2 (&bc)[4][2],
+template <bool FULL, int NI>
+__device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[NI][4], int jr, const f32x2 (&bc)[NI][2],
                                             float* __restrict__ logits, float* Pm, float* Ps, int rb, int cw,
                                             int lane, int R, int V) {
   constexpr float L2E = 1.4426950408889634f;
   const int row = rb + 16 * jr + (lane & 15), q4 = 4 * (lane >> 4);
-  f32x2 x[4][2];
+  f32x2 x[NI][2];
   float m = -INFINITY;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       x[i][h] = f32x2{acc[i][jr][2 * h], acc[i][jr][2 * h + 1]} + bc[i][h];  // bc = -inf past V
@@ -65,7 +69,7 @@ __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[4][4], int jr, co
   if (FULL || m > -INFINITY) {
     const f32x2 mb = f32x2{-m * L2E, -m * L2E};
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const f32x2 t = __builtin_elementwise_fma(x[i][h], f32x2{L2E, L2E}, mb);
@@ -80,12 +84,12 @@ __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[4][4], int jr, co
   if (FULL) {
     float* dst = logits + (size_t)row * V + cw + q4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
       *reinterpret_cast<float4*>(dst + 16 * i) = make_float4(x[i][0].x, x[i][0].y, x[i][1].x, x[i][1].y);
   } else if (row < R) {
     float* dst = logits + (size_t)row * V;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int col = cw + 16 * i + q4;
       const float xv[4] = {x[i][0].x, x[i][0].y, x[i][1].x, x[i][1].y};
       if ((V & 3) == 0 && col + 4 <= V) {
@@ -104,7 +108,7 @@ __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[4][4], int jr, co
 // VGPRs, measured the same before this layout and spills with it.)
 // RH = 2: 128 rows per workgroup, the W^T fragments reused for two 64-row halves (half the
 // workgroups and W^T fetches: 392 tiles at R = 256 = one round), X tile 68 KB of LDS.
-template <int OCC, int RH>
+template <int OCC, int RH, int HMAX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void vocab_logits_kernel(
     const bf16* __restrict__ X,     // [R][H]  output-projection activations (bf16)
     const bf16* __restrict__ WT,    // [V][H]  output_projection/w transposed ("Bt")
@@ -113,8 +117,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     float* __restrict__ part_ms,    // [R][nt][2]  per tile (max, sum exp)
     int R, int V, int H) {
   constexpr int BR = VT_ROWS * RH;  // rows per block
+  constexpr int NI = vt_ni(HMAX), VT_COLS = vt_cols(HMAX), KS = HMAX / 32;
   __shared__ float Pm[4][BR], Ps[4][BR];
-  __shared__ __attribute__((aligned(16))) bf16 Xs[BR * (VT_HMAX + 8)];  // X tile of the block
+  __shared__ __attribute__((aligned(16))) bf16 Xs[BR * (HMAX + 8)];  // X tile of the block
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // XCD-aware order: the RB row blocks of one vocab tile get block ids equal mod 8 (one XCD
   // under round-robin dealing), so the tile's W^T columns come from HBM once and are then
@@ -123,10 +128,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   const int slot = blockIdx.x >> 3, vt = (slot / RB) * 8 + (blockIdx.x & 7);
   if (vt >= nt) return;
   const int rb = (slot % RB) * BR;
-  const int cw = vt * VT_COLS + 64 * wid;  // this wave's first column
+  const int cw = vt * VT_COLS + 16 * NI * wid;  // this wave's first column
   // X rows of this block -> LDS once (shared by the 4 waves)
   const int kof = 8 * (lane >> 4), c16 = lane & 15, q4 = 4 * (lane >> 4);
-  constexpr int XPT = BR * VT_HMAX / 8 / 256;  // 16-byte X chunks per thread (H <= 256)
+  constexpr int XPT = BR * HMAX / 8 / 256;  // 16-byte X chunks per thread (H <= HMAX)
   bf16x8 xr[XPT];
 #pragma unroll
   for (int u = 0; u < XPT; ++u) {
@@ -136,18 +141,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   // every A fragment of the wave (W^T rows = its 4 x 16 vocab columns, H/32 k-steps, H <= 256:
   // 128 VGPRs) is issued right behind the X loads, before their LDS stores: one memory round
   // trip for both
-  const bf16* arow[4];
+  const bf16* arow[NI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) arow[i] = WT + (size_t)min(cw + 16 * i + c16, V - 1) * H + kof;
-  bf16x8 wa[8][4];
+  for (int i = 0; i < NI; ++i) arow[i] = WT + (size_t)min(cw + 16 * i + c16, V - 1) * H + kof;
+  bf16x8 wa[KS][NI];
 #pragma unroll
-  for (int h = 0; h < 8; ++h)
+  for (int h = 0; h < KS; ++h)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) wa[h][i] = ld8(arow[i] + min(32 * h, H - 32));
+    for (int i = 0; i < NI; ++i) wa[h][i] = ld8(arow[i] + min(32 * h, H - 32));
   // bias of the lane's columns cw + 16 i + q4 + r, pairs (r = 2h, 2h + 1); -inf past V
-  f32x2 bc[4][2];
+  f32x2 bc[NI][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int col = cw + 16 * i + q4 + 2 * h;
@@ -162,20 +167,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
   for (int h2 = 0; h2 < RH; ++h2) {
     const int rbh = rb + VT_ROWS * h2;
-    f32x4 acc[4][4];  // [vocab column tile i][row tile jr]
+    f32x4 acc[NI][4];  // [vocab column tile i][row tile jr]
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int jr = 0; jr < 4; ++jr) acc[i][jr] = f32x4{0, 0, 0, 0};
 #pragma unroll
-    for (int h = 0; h < 8; ++h) {
+    for (int h = 0; h < KS; ++h) {
       if (32 * h < H) {
 #pragma unroll
         for (int jr = 0; jr < 4; ++jr) {
           const bf16x8 xb =
               *reinterpret_cast<const bf16x8*>(&Xs[(VT_ROWS * h2 + 16 * jr + c16) * (H + 8) + 32 * h + kof]);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i][jr] = mfma16(wa[h][i], xb, acc[i][jr]);
+          for (int i = 0; i < NI; ++i) acc[i][jr] = mfma16(wa[h][i], xb, acc[i][jr]);
         }
       }
     }
@@ -185,9 +190,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
       if (full)
-        vl_epilogue<true>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
+        vl_epilogue<true, NI>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
       else
-        vl_epilogue<false>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
+        vl_epilogue<false, NI>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
     }
   }
   __syncthreads();
@@ -261,10 +266,18 @@ __device__ __forceinline__ void pad4(float* v, int* id, int n) {
 // With pg.w set the kernel also computes p_gen = sigmoid([ctx, c, h, x] . w + b) of its row
 // (reference attention_decoder.py:164-168; one launch less per decode step) and stores it
 // to pg.out; otherwise p_gen comes from ``pgen`` (nullptr for both: baseline, no pointer).
+//
+// BeamTail (bt.lp_sum set): the last of an article's ``beam`` row workgroups to finish (one
+// arrival counter per article) then runs that article's beam bookkeeping (beam_common.h) --
+// one kernel boundary less per decode step than a separate beam_step launch.
 __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     const float* __restrict__ logits, const float* __restrict__ part_ms, const float* __restrict__ pgen,
     const float* __restrict__ attn, const int* __restrict__ ext, const int* __restrict__ lens,
-    int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam, int nt, PgIn pgi) {
+    int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam, int nt, int tcols, PgIn pgi,
+    BeamTail bt) {
+  __shared__ float bt_cval[64];
+  __shared__ int bt_cid[64], bt_srt[64];
+  __shared__ int bt_last;
   __shared__ int hkey[VM_HASH];
   __shared__ float hmass[VM_HASH];
   __shared__ __attribute__((aligned(16))) float cv[VM_CAND + 8];
@@ -372,14 +385,14 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   if (tid == 0) ncand = 0;
   const float tau = pv_s[0][K - 1];
   // ---- round trip 2: the K selected tiles' logits and the copied words' logits
-  constexpr int EPT = VT_K * VT_COLS / VS_THREADS;
+  constexpr int EPT = VT_K * 256 / VS_THREADS;  // tiles of <= 256 columns
   float zs[EPT];
   int cs[EPT];
 #pragma unroll
   for (int u = 0; u < EPT; ++u) {
     const int e = tid + u * VS_THREADS;
-    const int tq = e < K * VT_COLS ? pi_s[0][e / VT_COLS] : VS_NONE;
-    cs[u] = tq < nt ? tq * VT_COLS + (e % VT_COLS) : V;
+    const int tq = e < K * tcols ? pi_s[0][e / tcols] : VS_NONE;
+    cs[u] = tq < nt ? tq * tcols + (e % tcols) : V;
     zs[u] = cs[u] < V ? z[cs[u]] : -INFINITY;
   }
   int wk[SPT];
@@ -455,20 +468,45 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     out_ids[(size_t)r * K + tid] = pi_s[2][tid];
     out_lp[(size_t)r * K + tid] = __logf(pv_s[2][tid]);
   }
+  if (bt.lp_sum) {  // uniform
+    if (tid < K) {  // this row's candidates as tagged granules (see beam_article_tail)
+      const unsigned long long hi = ((unsigned long long)((unsigned)(*bt.step) & 0x7fffu) << 17) |
+                                    (unsigned)(pi_s[2][tid] & 0x1ffff);
+      __hip_atomic_store(bt.gran + (size_t)r * K + tid, (hi << 32) | __float_as_uint(__logf(pv_s[2][tid])),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (tid == 0)
+      bt_last = __hip_atomic_fetch_add(&bt.art_ctr[art], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                (unsigned)(beam - 1);
+    __syncthreads();
+    if (bt_last) {
+      if (tid == 0) __hip_atomic_store(&bt.art_ctr[art], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      beam_article_tail(bt, art, bt_cval, bt_cid, bt_srt);
+    }
+  }
 }
 
-int vocab_topk_tiles(int V) { return (V + VT_COLS - 1) / VT_COLS; }
+int vocab_topk_tiles(int V, int H) { return (V + vt_cols(H) - 1) / vt_cols(H); }
 
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
-                       int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st) {
-  const int nt = vocab_topk_tiles(V);
+                       int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st, const BeamTail* bt) {
+  const int nt = vocab_topk_tiles(V, H), tcols = vt_cols(H);
+  const BeamTail none{};
   // default: 128-row workgroups (392 at R = 256, V = 50k: one round at 2 per CU; W^T fragments
   // fetched once per 128 rows): decode 5610 -> 5927 summaries/s at 64 articles, 6940 -> 7300 at
   // 128 (64-row workgroups, 784 at R = 256, run 1.5 rounds)
-  const int RB = (R + VT_ROWS * 2 - 1) / (VT_ROWS * 2);
-  hipLaunchKernelGGL((vocab_logits_kernel<2, 2>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias, logits,
-                     part_ms, R, V, H);
+  // hidden 512: 64-row workgroups (the X tile is 66 KB), 128 columns each
+  if (H <= 256) {
+    const int RB = (R + VT_ROWS * 2 - 1) / (VT_ROWS * 2);
+    hipLaunchKernelGGL((vocab_logits_kernel<2, 2, 256>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
+                       logits, part_ms, R, V, H);
+  } else {
+    const int RB = (R + VT_ROWS - 1) / VT_ROWS;
+    hipLaunchKernelGGL((vocab_logits_kernel<2, 1, 512>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
+                       logits, part_ms, R, V, H);
+  }
   hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
-                     out_lp, V, T, K, beam, nt, pgi);
+                     out_lp, V, T, K, beam, nt, tcols, pgi, bt ? *bt : none);
 }

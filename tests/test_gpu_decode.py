@@ -249,7 +249,7 @@ def test_pgen_matches_fp32():
 
 
 @pytest.mark.parametrize("pointer,V,H", [(True, 3000, 128), (False, 3000, 128), (True, 600, 64), (False, 600, 64),
-                                         (False, 50000, 256)])
+                                         (False, 50000, 256), (True, 50000, 512), (False, 3000, 512)])
 def test_fused_vocab_topk_matches_materialised_path(pointer, V, H):
     """vocab_topk (MFMA logits + per-tile (max, sum exp) partials, then a select that reads
     only the K best tiles of each row) == the library GEMM + final_topk path; V=600 has
@@ -279,7 +279,7 @@ def test_fused_vocab_topk_matches_materialised_path(pointer, V, H):
     k.final_topk(logits, bias, pg, attn, ext, lens, ids0, lp0, torch.zeros(R, S, 2, device="cuda"),
                  torch.zeros(R, S, K, device="cuda"), torch.zeros(R, S, K, dtype=torch.int32, device="cuda"),
                  R, V, T, K, beam)
-    nt = int(k.vocab_topk_parts(V))
+    nt = int(k.vocab_topk_parts(V, H))
     ids1 = torch.zeros(R, K, dtype=torch.int32, device="cuda")
     lp1 = torch.zeros(R, K, device="cuda")
     lg = torch.zeros(R, V, device="cuda")
@@ -332,3 +332,33 @@ def test_row_attention_decode_production_width(coverage, monkeypatch):
         b1 = Batch([ex] * hps.beam_size, hps1, vocab, pad_enc_to=T)
         agree += run_beam_search(model, vocab, b1, hps).tokens[:6] == hr[a].tokens[:6]
     assert agree >= 0.7 * Na, agree
+
+
+@pytest.mark.parametrize("coverage,pointer_gen,H", [(True, True, 256), (False, True, 256), (False, False, 256),
+                                                    (True, True, 512)])
+def test_fused_decode_step_equals_unfused(coverage, pointer_gen, H):
+    """The 6-launch decode step (parent / token gathers inside the cell, x-merge and attention
+    kernels; beam bookkeeping in the vocab select kernel's tail) == the 8-launch step
+    (beam_gather ... beam_step): same arithmetic on the same values, so the same summaries and
+    attention histories bit for bit (scores to 1e-6: the bookkeeping's final division may be
+    compiled differently inside the select kernel); graph-captured."""
+    from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
+    Na, T, V = 16, 120, 3000
+    hps = HParams(mode="decode", batch_size=Na, max_enc_steps=T, max_dec_steps=30, min_dec_steps=5, beam_size=4,
+                  vocab_size=V, emb_dim=128, hidden_dim=H, coverage=coverage, pointer_gen=pointer_gen,
+                  trunc_norm_init_std=0.05)
+    corpus = SyntheticCorpus(vocab_size=V, raw_vocab=3 * V, seed=8, art_mean=100, art_sd=20, sent_mean=5)
+    vocab = corpus.vocab(V)
+    batch = make_batches(hps, vocab, corpus, 1, pad_enc_to=T)[0]
+    params = build_params(hps, vocab.size(), device="cuda", seed=9)
+    res = []
+    for fused in (True, False):
+        d = DeviceBeamDecoder(hps, vocab, params, n_articles=Na, T=T, use_graph=True)
+        assert d.fused_step
+        d.fused_step = fused
+        hy = d.decode(batch)
+        res.append(([h.tokens for h in hy], [h.avg_log_prob for h in hy], [np.stack(h.attn_dists) for h in hy]))
+    assert res[0][0] == res[1][0]
+    np.testing.assert_allclose(res[0][1], res[1][1], rtol=1e-6)
+    for a, b in zip(res[0][2], res[1][2]):
+        np.testing.assert_array_equal(a, b)

@@ -94,13 +94,19 @@ class DeviceBeamDecoder:
             b[name] = z(*shape, dt=dt)
         # fused vocab head (vocab_topk.hip) partials; EngineConfig.fused_vocab_decode = False
         # selects the materialised-logits path (GEMM + final_topk) instead
-        self.fused_vocab = self.eng.cfg.fused_vocab_decode and self.K <= 8 and self.eng.H <= 256
+        self.fused_vocab = self.eng.cfg.fused_vocab_decode and self.K <= 8 and (self.eng.H <= 256 or self.eng.H == 512)
         if self.fused_vocab:
-            b["vpart_ms"] = z(R, int(self.k.vocab_topk_parts(V)), 2)
+            b["vpart_ms"] = z(R, int(self.k.vocab_topk_parts(V, H)), 2)
+        # fused step (5 + 1 launches): the parent / token gathers inside the cell, x-merge and
+        # attention kernels, the beam bookkeeping in the vocab select kernel's tail
+        self.fused_step = self.fused_vocab and self.row_attn and self.beam * self.K <= 64
+        b["art_ctr"] = z(Na, dt=torch.int32)
+        b["gran"] = z(R, K, dt=torch.long)  # tagged candidate granules of the fused beam tail
+        b["tail_err"] = z(1, dt=torch.int32)
         # ping-pong decoder state: step t reads set t%2 and writes set (t+1)%2, so a
         # captured 2-step graph needs no copies between steps
-        self.st = [{"C": z(R, H), "H": z(R, H, dt=BF), "CTX": z(R, A), "ATT": z(R, T), "COV": z(R, T)}
-                   for _ in range(2)]
+        self.st = [{"C": z(R, H), "H": z(R, H, dt=BF), "CTX": z(R, A), "CTXb": z(R, A, dt=BF), "ATT": z(R, T),
+                    "COV": z(R, T)} for _ in range(2)]
         if self.keep_attn:
             b["ATT_hist"] = z(D, R, T)
             b["PG_hist"] = z(D, R)
@@ -144,12 +150,13 @@ class DeviceBeamDecoder:
         X = self.st[0]
         b["Cb2"].copy_(X["C"])
         k.dec_sproj(b["Cb2"], X["H"], eng.pk["WsT"], self.p[ATT_B], b["s"], R, H, A)
-        self._attention(None, X["ATT"], X["CTX"], None)
+        self._attention(None, X["ATT"], X["CTX"], X["CTXb"])
         X["COV"].zero_()
         b["gidx"].copy_(torch.arange(R, dtype=torch.int32, device=self.dev))
         b["latest"].fill_(self.vocab.word2id(START_DECODING))
         b["lp_sum"].zero_()
-        for n in ("done", "res_count", "step", "step_ctr", "tok_hist", "par_hist", "res_len", "res_step", "res_par"):
+        for n in ("done", "res_count", "step", "step_ctr", "tok_hist", "par_hist", "res_len", "res_step", "res_par",
+                  "art_ctr", "gran"):
             b[n].zero_()
         b["res_score"].fill_(-float("inf"))
 
@@ -167,6 +174,8 @@ class DeviceBeamDecoder:
                            self.rep)
 
     def _step(self, parity: int):
+        if self.fused_step:
+            return self._step_fused(parity)
         k, b, hps, eng, p = self.k, self.b, self.hps, self.eng, self.p
         R, T, H, A, E, V, K = self.R, self.T, eng.H, eng.A, eng.E, self.V, self.K
         X, Y = self.st[parity], self.st[1 - parity]
@@ -208,6 +217,44 @@ class DeviceBeamDecoder:
                     None, Y["ATT"] if hist else None, b["ATT_hist"] if hist else None,
                     pg if (hist and pg is not None) else None, b["PG_hist"] if (hist and pg is not None) else None,
                     T, self.Na, self.beam, K, self.vocab.word2id(STOP_DECODING), hps.min_dec_steps, self.maxD)
+
+    def _step_fused(self, parity: int):
+        """One decode step in 6 launches (reference model.py:367-443 decode_onestep + the beam
+        update of beam_search.py:110-156): cell with the parent / token gathers (and the step
+        counter), attention query + x-merge, row attention with the coverage gather, output
+        projection, vocab logits, vocab select + p_gen + per-article beam bookkeeping."""
+        k, b, hps, eng, p = self.k, self.b, self.hps, self.eng, self.p
+        R, T, H, A, E, V, K = self.R, self.T, eng.H, eng.A, eng.E, self.V, self.K
+        X, Y = self.st[parity], self.st[1 - parity]
+        cov = hps.coverage
+        unk = self.vocab.word2id(UNKNOWN_TOKEN)
+        k.dec_cell_fwd_beam(b["gidx"], b["latest"], self.XGtab, X["CTXb"], X["H"], X["C"], eng.pk["WcT2"], Y["C"],
+                            b["Cb2"], Y["H"], b["step"], R, H, A, V, unk)
+        if hps.pointer_gen:
+            k.beam_sproj_xmerge(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], X["CTXb"], eng.pk["WicT"],
+                                self.Xtab, b["gidx"], b["latest"], b["x"], R, H, A, E, V, unk)
+        else:
+            k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
+        k.attn_fwd_row_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], X["COV"] if cov else None,
+                            X["ATT"] if cov else None, Y["COV"] if cov else None, b["gidx"], b["lens_att"], Y["ATT"],
+                            Y["CTX"], Y["CTXb"], R, T, A, self.rep)
+        k.linear2(Y["H"], H, Y["CTXb"], A, eng.pk["OUTmT"], p[OUT_B], None, None, b["outb"], R, H)
+        ptr, hist = hps.pointer_gen, self.keep_attn
+        k.vocab_topk_beam(b["outb"], self.owT, p[OV], Y["CTX"] if ptr else None, Y["C"] if ptr else None,
+                          Y["H"] if ptr else None, b["x"] if ptr else None, self.pg_w if ptr else None,
+                          p[PG_B] if ptr else None, b["PG"] if ptr else None, Y["ATT"] if (ptr or hist) else None,
+                          b["ext"], b["lens"], b["top_ids"], b["top_lp"], b["logits"], b["vpart_ms"], b["lp_sum"],
+                          b["latest"], b["gidx"], b["tok_hist"], b["par_hist"], b["done"], b["res_count"],
+                          b["res_score"], b["res_len"], b["res_step"], b["res_par"], b["step"], b["art_ctr"],
+                          b["gran"], b["tail_err"],
+                          b["ATT_hist"] if hist else None, b["PG_hist"] if (hist and ptr) else None, R, V, H, T, K,
+                          self.beam, A, E, self.vocab.word2id(STOP_DECODING), hps.min_dec_steps, self.maxD)
+
+    @staticmethod
+    def _check_tail(err: int) -> None:
+        if err:
+            raise RuntimeError("beam decode: a fused beam-tail poll timed out (candidates of an article never "
+                               "arrived); results discarded -- set TSAMD_DEC_ROW_ATTN=0 for the unfused step")
 
     def _graph_steps(self):
         for i in range(self.gsteps):  # parity alternates: gsteps is even
@@ -307,6 +354,7 @@ class DeviceBeamDecoder:
         pin = self._snap[slot]
         srcs = {k: self.b[k] for k in self._result_names()}
         srcs["lstm_err"] = self.eng.w["lstm_err"]  # checked with the results, one batch late
+        srcs["tail_err"] = self.b["tail_err"]
         for k, src in srcs.items():
             h = pin.get(k)
             if h is None or h.shape != src.shape or h.dtype != src.dtype:
@@ -343,6 +391,7 @@ class DeviceBeamDecoder:
         ev.synchronize()
         if int(arrays["lstm_err"][0]):  # never emit garbage summaries (see check_lstm_err)
             self.eng.check_lstm_err()
+        self._check_tail(int(arrays["tail_err"][0]))
         return self._backtrack(arrays, nv)
 
     def _backtrack(self, b, n_valid: int = None) -> List[Hypothesis]:
@@ -443,4 +492,5 @@ class DeviceBeamDecoder:
         self.run(batch)
         hyps = self.results(int(batch.valid.sum()))  # synchronises
         self.eng.check_lstm_err()  # the encoder ran the persistent LSTM: never emit garbage summaries
+        self._check_tail(int(self.b["tail_err"].item()))
         return hyps

@@ -63,7 +63,7 @@ def main():
         res["attn_bwd_row"] = timeit(lambda: eng.k.attn_bwd_row(enc_out, F, w["S"][t], v, wc, w["COV"][t],
                                                                  w["ATT"][t], w["DCTX"][t], w["CTX"][t], w["dA"][t],
                                                                  w["dcov"][1], w["gcl"][t], lens, w["DE"][t],
-                                                                 w["DS"][t], w["dcov"][0], B, T, eng.A, None))
+                                                                 w["DS"][t], w["dcov"][0], B, T, eng.A))
     res["attn_score"] = timeit(lambda: k.attn_score(Ft, w["S"][t], v, wc, w["COV"][t], lens, w["e"], B, T, A, 1))
     res["attn_softmax_ctx"] = timeit(lambda: k.attn_softmax_ctx(w["e"], enc_out, lens, w["COV"][t], w["ATT"][t],
                                                                 w["COV"][t + 1], w["covloss"][t], w["CTX"][t],

@@ -35,7 +35,7 @@ def main():
     ids = torch.empty(R, K, dtype=torch.int32, device=dev)
     lp = torch.empty(R, K, device=dev)
     lg = torch.empty(R, V, device=dev)
-    nt = int(k.vocab_topk_parts(V))
+    nt = int(k.vocab_topk_parts(V, H))
     pms = torch.empty(R, nt, 2, device=dev)
 
     def run():
