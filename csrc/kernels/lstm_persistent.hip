@@ -118,16 +118,25 @@ __device__ __forceinline__ bool team_of(int NC, int nteams, int& team, int& c) {
 
 }  // namespace
 
-template <int H, bool NT>
+// RT row tiles per team (RT = 2 at H = 512: a team owns 32 rows, so a batch of 1024 runs in
+// 2 launches instead of 4).  At H = 512 the 4 waves x 16 units x 4 gates need 256 VGPRs of
+// W_hh B fragments per lane: launch bounds (256, 1) leave one wave per SIMD and the 512
+// unified registers (arch + acc) for them.
+template <int H, bool NT, int RT = 1>
 __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     const float* __restrict__ gx, const float* __restrict__ bias, const bf16* __restrict__ Wt,
     bf16* __restrict__ hs, float* __restrict__ cs, float* __restrict__ acts, bf16* __restrict__ out,
     const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile, int tile0, int ntile_l) {
-  constexpr int KS = H / 32, NC = H / 64, HP = H / 2, G = 16 * HP, NPL = G / 256;
-  __shared__ __attribute__((aligned(16))) bf16 Ash[2][16 * H];
+  constexpr int KS = H / 32, NC = H / 64, HP = H / 2, R = 16 * RT, G = R * HP, NPL = G / 256;
+  constexpr int CH = NPL < 8 ? NPL : 8;  // granules per lane per sweep (chunks keep x[] at 16 VGPRs)
+  constexpr int NR = 4 * RT;             // rows per lane
+  static_assert(NPL % CH == 0, "sweep chunks");
+  __shared__ __attribute__((aligned(16))) bf16 Ash[2][R * H];
+  // RT = 2: the step's gate activations wait here (not in registers) until the hand-off is out
+  __shared__ __attribute__((aligned(16))) float Gsh[RT > 1 ? 256 * NR * 4 : 4];
   int lt, c;
   if (!team_of(NC, 2 * ntile_l, lt, c)) return;
-  const int d = lt / ntile_l, tile = tile0 + lt % ntile_l, r0 = tile * 16, team = d * ntile + tile;
+  const int d = lt / ntile_l, tile = tile0 + lt % ntile_l, r0 = tile * R, team = d * ntile + tile;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int u = c * 64 + wid * 16 + (lane & 15);
   const size_t G4 = 4 * (size_t)H, BH = (size_t)B * H;
@@ -140,43 +149,57 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   float gb[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) gb[g] = bias[(size_t)d * G4 + g * H + u];
-  int rc[4], ln[4];
-  bool rok[4];
-  float creg[4], hreg[4];
+  // lane rows: tile-local row rt * 16 + (lane >> 4) * 4 + i  (index j = rt * 4 + i)
+  // rc / ln: recomputed / read from LDS (lnsh) rather than held in 2 x NR registers
+  __shared__ int lnsh[R];
+  if (threadIdx.x < R) lnsh[threadIdx.x] = r0 + (int)threadIdx.x < B ? lens[r0 + threadIdx.x] : 0;
+  auto rowof = [&](int j) { return r0 + (j >> 2) * 16 + (lane >> 4) * 4 + (j & 3); };
+  float creg[NR], hreg[NR];
   const bf16* hs0 = hs + (size_t)d * (T + 1) * BH;
   const float* cs0 = cs + (size_t)d * (T + 1) * BH;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = r0 + (lane >> 4) * 4 + i;
-    rok[i] = r < B;
-    rc[i] = rok[i] ? r : B - 1;
-    ln[i] = rok[i] ? lens[r] : 0;
-    creg[i] = cs0[(size_t)rc[i] * H + u];
-    hreg[i] = bf2f(hs0[(size_t)rc[i] * H + u]);
+  for (int j = 0; j < NR; ++j) {
+    const int r = rowof(j);
+    const int rr = r < B ? r : B - 1;
+    creg[j] = cs0[(size_t)rr * H + u];
+    hreg[j] = bf2f(hs0[(size_t)rr * H + u]);
   }
   gu64* xb = xbuf + (size_t)team * 2 * G;
   bool dead = false;
   // gate pre-activations x.W_x of step s + 1 are loaded during step s (off the recurrence's
   // critical path: an HBM round trip per step otherwise)
-  float gzn[4][4];
+  // RT = 1: in registers (gzn); RT = 2: straight into LDS (Gxsh, one global_load_lds_dwordx4
+  // per row and lane: lane-linear 1 KB per wave instruction), no VGPRs
+  float gzn[RT > 1 ? 1 : NR][4];
+  __shared__ __attribute__((aligned(16))) float Gxsh[RT > 1 ? 4 * NR * 64 * 4 : 4];
   auto load_gz = [&](int st) {
     const float* gxs = gx + ((size_t)d * T + st) * B * G4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x4 q = ld_f4(gxs + ((size_t)rc[i] * H + u) * 4, NT);
-      gzn[i][0] = q[0]; gzn[i][1] = q[1]; gzn[i][2] = q[2]; gzn[i][3] = q[3];
+    for (int j = 0; j < NR; ++j) {
+      const float* src = gxs + ((size_t)min(rowof(j), B - 1) * H + u) * 4;
+      if constexpr (RT > 1) {
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)&Gxsh[(wid * NR + j) * 256], 16, 0, 0);
+      } else {
+        const f32x4 q = ld_f4(src, NT);
+        gzn[j][0] = q[0]; gzn[j][1] = q[1]; gzn[j][2] = q[2]; gzn[j][3] = q[3];
+      }
     }
   };
   load_gz(0);
   for (int s = 0; s < T; ++s) {
     const int buf = s & 1;
-    float gz[4][4];
+    // RT = 1: the next step's x.W_x is requested now and the current one kept in gz; RT = 2
+    // (no registers for two copies): requested after this step's cell update consumed gzn
+    float gz[RT > 1 ? 1 : NR][4];
+    if constexpr (RT == 1) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < NR; ++j)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) gz[i][g] = gzn[i][g] + gb[g];
-    if (s + 1 < T) load_gz(s + 1);
-    // ---- h_s of the whole 16-row tile -> LDS
+        for (int g = 0; g < 4; ++g) gz[j][g] = gzn[j][g];
+      if (s + 1 < T) load_gz(s + 1);
+    }
+    // ---- h_s of the whole R-row tile -> LDS
     if (s == 0) {
       for (int idx = threadIdx.x; idx < G; idx += 256) {
         const int row = idx / HP, p = idx % HP;
@@ -185,65 +208,98 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
             *reinterpret_cast<const unsigned*>(hs0 + (size_t)rr * H + 2 * p);
       }
     } else {
-      unsigned v[NPL];
-      sweep<NPL>(xb + (size_t)(s & 1) * G, wid * (G / 4), (unsigned)s, v, dead, err, 1u, lane);
 #pragma unroll
-      for (int j = 0; j < NPL; ++j) {
-        const int idx = wid * (G / 4) + j * 64 + lane;
-        *reinterpret_cast<unsigned*>(&Ash[buf][swz<H>(idx / HP, 2 * (idx % HP))]) = v[j];
+      for (int ch = 0; ch < NPL / CH; ++ch) {
+        unsigned v[CH];
+        const int first = wid * (G / 4) + ch * CH * 64;
+        sweep<CH>(xb + (size_t)(s & 1) * G, first, (unsigned)s, v, dead, err, 1u, lane);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          const int idx = first + j * 64 + lane;
+          *reinterpret_cast<unsigned*>(&Ash[buf][swz<H>(idx / HP, 2 * (idx % HP))]) = v[j];
+        }
       }
     }
     __syncthreads();
+    if constexpr (RT > 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's Gxsh landed
     // ---- z = h_s . W_hh for this wave's 16 units x 4 gates (B operands in registers)
-    f32x4 acc[4];
+    f32x4 acc[RT][4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) acc[g] = f32x4{0, 0, 0, 0};
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[rt][g] = f32x4{0, 0, 0, 0};
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ash[buf][swz<H>(lane & 15, kk * 32 + 8 * (lane >> 4))]);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = mfma16(a, Wf[g][kk], acc[g]);
+      for (int rt = 0; rt < RT; ++rt) {
+        const bf16x8 a =
+            *reinterpret_cast<const bf16x8*>(&Ash[buf][swz<H>(rt * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4))]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[rt][g] = mfma16(a, Wf[g][kk], acc[rt][g]);
+      }
     }
-    // ---- cell update, 4 rows x 1 unit per lane (gates kept in registers: stored after the
+    // ---- cell update, NR rows x 1 unit per lane (gates kept in registers: stored after the
     // hand-off below, so the granule stores are not queued behind ~6 MB of activation stores
     // per step -- that ordering cost ~4 us per step at H = 512, B = 256)
-    float ga[4][4];
+    float ga[RT > 1 ? 1 : NR][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (s < ln[i]) {
-        ga[i][0] = fsigmoid(acc[0][i] + gz[i][0]);
-        ga[i][1] = ftanh(acc[1][i] + gz[i][1]);
-        ga[i][2] = fsigmoid(acc[2][i] + gz[i][2] + 1.0f);
-        ga[i][3] = fsigmoid(acc[3][i] + gz[i][3]);
-        const float cc = ga[i][2] * creg[i] + ga[i][0] * ga[i][1];
-        creg[i] = cc;
-        hreg[i] = bf2f(f2bf(ga[i][3] * ftanh(cc)));
+    for (int j = 0; j < NR; ++j) {
+      const int rt = j >> 2, i = j & 3;
+      if (s < lnsh[rowof(j) - r0]) {
+        float* z = ga[RT > 1 ? 0 : j];
+        float xv[4];
+        if constexpr (RT > 1) {
+          const float4 q = *reinterpret_cast<const float4*>(&Gxsh[((wid * NR + j) * 64 + lane) * 4]);
+          xv[0] = q.x; xv[1] = q.y; xv[2] = q.z; xv[3] = q.w;
+        } else {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) xv[g] = gz[RT > 1 ? 0 : j][g];
+        }
+        const float* x = xv;
+        z[0] = fsigmoid(acc[rt][0][i] + x[0] + gb[0]);
+        z[1] = ftanh(acc[rt][1][i] + x[1] + gb[1]);
+        z[2] = fsigmoid(acc[rt][2][i] + x[2] + gb[2] + 1.0f);
+        z[3] = fsigmoid(acc[rt][3][i] + x[3] + gb[3]);
+        const float cc = z[2] * creg[j] + z[0] * z[1];
+        creg[j] = cc;
+        hreg[j] = bf2f(f2bf(z[3] * ftanh(cc)));
+        if constexpr (RT > 1)
+          *reinterpret_cast<float4*>(&Gsh[(j * 256 + threadIdx.x) * 4]) = make_float4(z[0], z[1], z[2], z[3]);
       }
+    }
+    if constexpr (RT > 1) {
+      if (s + 1 < T) load_gz(s + 1);
     }
     // ---- publish h_{s+1}: unit pairs (u, u+1) of adjacent lanes -> one granule
     if (s + 1 < T) {
       gu64* dst = xb + (size_t)((s + 1) & 1) * G;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float hn = __shfl_xor(hreg[i], 1, 64);
-        if (!(lane & 1)) store_granule(dst + ((lane >> 4) * 4 + i) * HP + u / 2, (unsigned)(s + 1),
-                                       pack_bf2(hreg[i], hn));
+      for (int j = 0; j < NR; ++j) {
+        const float hn = __shfl_xor(hreg[j], 1, 64);
+        if (!(lane & 1))
+          store_granule(dst + ((j >> 2) * 16 + (lane >> 4) * 4 + (j & 3)) * HP + u / 2, (unsigned)(s + 1),
+                        pack_bf2(hreg[j], hn));
       }
     }
     float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
     bf16* hnext = hs + ((size_t)d * (T + 1) + s + 1) * BH;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = rc[i];
-      if (s < ln[i]) {
-        st_f4(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4, ga[i][0], ga[i][1], ga[i][2], ga[i][3],
-              NT);  // one 16-byte store per (row, unit)
-        const int t = d == 0 ? s : ln[i] - 1 - s;
-        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(hreg[i]), NT);
+    for (int j = 0; j < NR; ++j) {
+      const int r = rowof(j), lj = lnsh[r - r0];
+      if (s < lj) {
+        if constexpr (RT > 1) {
+          const float4 z = *reinterpret_cast<const float4*>(&Gsh[(j * 256 + threadIdx.x) * 4]);
+          st_f4(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4, z.x, z.y, z.z, z.w, NT);
+        } else {
+          st_f4(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4, ga[j][0], ga[j][1], ga[j][2], ga[j][3],
+                NT);  // one 16-byte store per (row, unit)
+        }
+        const int t = d == 0 ? s : lj - 1 - s;
+        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(hreg[j]), NT);
       }
-      if (rok[i]) {
-        st_f(cnext + (size_t)r * H + u, creg[i], NT);
-        st_b(hnext + (size_t)r * H + u, f2bf(hreg[i]), NT);
+      if (r < B) {
+        st_f(cnext + (size_t)r * H + u, creg[j], NT);
+        st_b(hnext + (size_t)r * H + u, f2bf(hreg[j]), NT);
       }
     }
   }
@@ -650,6 +706,8 @@ int lstm_persistent_capacity(int H) {
     if (HH <= 256) {                                                                                               \
       ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[3], lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), true>, \
                                                          256, 0) == hipSuccess;                                    \
+    } else {                                                                                                       \
+      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[2], lstm_fwd_persistent_kernel<512, true, 2>, 256, 0) == hipSuccess; \
     }                                                                                                              \
   }
   OCC(64) OCC(128) OCC(256) OCC(512)
@@ -659,7 +717,13 @@ int lstm_persistent_capacity(int H) {
   return cap;
 }
 
-// 16-row tiles per launch: the most whose grid (NC workgroups per (direction, tile) team,
+// Rows per team: 16, or 32 for the H = 512 forward above batch 256 (the 4-wave RT = 2 kernel:
+// batch 1024 in 2 launches instead of 4; tools/lstm_micro.py, T = 800: B = 1024 19.1 -> 12.7 ms,
+// B = 512 9.7 -> 6.4 ms per launch sequence, 7.9 us per step vs 6.0 for 16-row teams).  The
+// backward keeps 16.
+static int lstm_rows(int H, int B, bool bwd) { return (!bwd && H == 512 && B > 256) ? 32 : 16; }
+
+// Row tiles per launch: the most whose grid (NC workgroups per (direction, tile) team,
 // teams dealt 8 at a time so members share an XCD) fits the resident capacity.  Teams are
 // independent, so a larger batch runs as consecutive launches over row-tile ranges.
 static int lstm_tiles_per_launch(int H, int ntile) {
@@ -671,25 +735,36 @@ static int lstm_tiles_per_launch(int H, int ntile) {
 
 int lstm_persistent_grid(int H, int B) {
   if (!lstm_h_ok(H) || B < 1) return 0;
-  const int NC = H / 64, nl = lstm_tiles_per_launch(H, (B + 15) / 16);
-  return nl > 0 ? 8 * NC * ((2 * nl + 7) / 8) : 0;  // grid of the largest launch
+  int grid = 0;
+  for (int bwd = 0; bwd < 2; ++bwd) {
+    const int R = lstm_rows(H, B, bwd), NC = H / 64, nl = lstm_tiles_per_launch(H, (B + R - 1) / R);
+    if (nl <= 0) return 0;
+    grid = max(grid, 8 * NC * ((2 * nl + 7) / 8));  // grid of the largest launch
+  }
+  return grid;
 }
 
 int lstm_persistent_launches(int H, int B) {
-  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile);
-  return nl > 0 ? (ntile + nl - 1) / nl : 0;
+  int n = 0;
+  for (int bwd = 0; bwd < 2; ++bwd) {
+    const int R = lstm_rows(H, B, bwd), ntile = (B + R - 1) / R, nl = lstm_tiles_per_launch(H, ntile);
+    if (nl <= 0) return 0;
+    n = max(n, (ntile + nl - 1) / nl);
+  }
+  return n;
 }
 
 size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {
-  const int ntile = (B + 15) / 16, NC = H / 64;
-  // fwd: [team][parity][16 rows][H/2 unit pairs]; bwd: [team][parity][dest][src][16][64]
-  return (size_t)2 * ntile * 2 * (bwd ? (size_t)NC * NC * 16 * 64 : (size_t)16 * (H / 2));
+  const int R = lstm_rows(H, B, bwd), ntile = (B + R - 1) / R, NC = H / 64;
+  // fwd: [team][parity][R rows][H/2 unit pairs]; bwd: [team][parity][dest][src][16][64]
+  return (size_t)2 * ntile * 2 * (bwd ? (size_t)NC * NC * 16 * 64 : (size_t)R * (H / 2));
 }
 
 void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
                                 int H, hipStream_t st) {
-  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64, nw = lstm_nw(H);
+  const int R = lstm_rows(H, B, false), ntile = (B + R - 1) / R, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64;
+  const int nw = R == 32 ? 4 : lstm_nw(H);
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
@@ -699,6 +774,9 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
   if (nw == 8)                                                                                                  \
     hipLaunchKernelGGL((lstm_fwd_persistent8_kernel<HH, NTV>), dim3(grid), dim3(512), 0, st, gx, bias, Wt, hs, cs, \
                        acts, out, lens, xb, e, T, B, ntile, t0, n);                                             \
+  else if (R == 32)                                                                                             \
+    hipLaunchKernelGGL((lstm_fwd_persistent_kernel<512, NTV, 2>), dim3(grid), dim3(256), 0, st, gx, bias, Wt, hs, \
+                       cs, acts, out, lens, xb, e, T, B, ntile, t0, n);                                         \
   else                                                                                                          \
     hipLaunchKernelGGL((lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), NTV>), dim3(grid), dim3(256), 0, st, \
                        gx, bias, Wt, hs, cs, acts, out, lens, xb, e, T, B, ntile, t0, n)
