@@ -211,6 +211,10 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
 }
 
 // ------------------------------------------------------------------------------ backward
+// The per-feature parameters (s, w, 4 v w, dctx: 32 NK floats per lane) live in LDS, not in
+// registers: with them in registers the double-buffered rows spilled 65 VGPRs at A = 1024
+// (tools/attn_micro_c5.py, 256 rows, T = 800: 323 -> 162 us; A = 512, T = 400: 51.0 -> 48.7 us).
+// The parameter-major loop order (feature pair outer, position inner) reads each once per group.
 template <int NK, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
     const bf16* __restrict__ E, const bf16* __restrict__ F, const float* __restrict__ s,
@@ -248,25 +252,30 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
     x.r = (Ga ? Ga[ix] : 0.f) + x.dn + ((gcl && x.a <= x.c) ? g : 0.f);
   };
   if (wid < ngrp) load(wid, eA, fA, xA);
-  float dk[NK][8];
-  f32x2 s2[NK][4], w2[NK][4], v4w[NK][4], acc[NK][4];
+  // parameters in LDS [param][kb][jp][lane] (one copy: every wave has the same lane -> feature
+  // map), written by wave 0 before the block_sum barrier below
+  f32x2 acc[NK][4];
+  __shared__ f32x2 prm[4 * NK * 4 * 64];
 #pragma unroll
   for (int kb = 0; kb < NK; ++kb) {
     const int k0 = kb * 512 + lane * 8;
 #pragma unroll
     for (int jp = 0; jp < 4; ++jp) {
+      acc[kb][jp] = f32x2{0.f, 0.f};
+      if (wid != 0) continue;
       const float2 sv = *reinterpret_cast<const float2*>(s + (size_t)b * A + k0 + 2 * jp);
       const float2 vv = *reinterpret_cast<const float2*>(v + k0 + 2 * jp);
       const float2 wv = wc ? *reinterpret_cast<const float2*>(wc + k0 + 2 * jp) : make_float2(0.f, 0.f);
       const float2 dv = *reinterpret_cast<const float2*>(dctx + (size_t)b * A + k0 + 2 * jp);
-      s2[kb][jp] = f32x2{sv.x, sv.y} * K2LOG2E;
-      w2[kb][jp] = f32x2{wv.x, wv.y} * K2LOG2E;
-      v4w[kb][jp] = f32x2{4.f * vv.x * wv.x, 4.f * vv.y * wv.y};
-      dk[kb][2 * jp] = dv.x;
-      dk[kb][2 * jp + 1] = dv.y;
-      acc[kb][jp] = f32x2{0.f, 0.f};
+      const f32x2 ps = f32x2{sv.x, sv.y} * K2LOG2E, pw = f32x2{wv.x, wv.y} * K2LOG2E;
+      const f32x2 pv = f32x2{4.f * vv.x * wv.x, 4.f * vv.y * wv.y}, pd = f32x2{dv.x, dv.y};
+      prm[((0 * NK + kb) * 4 + jp) * 64 + lane] = ps;
+      prm[((1 * NK + kb) * 4 + jp) * 64 + lane] = pw;
+      prm[((2 * NK + kb) * 4 + jp) * 64 + lane] = pv;
+      prm[((3 * NK + kb) * 4 + jp) * 64 + lane] = pd;
     }
   }
+  auto par = [&](int which, int kb, int jp) -> f32x2 { return prm[((which * NK + kb) * 4 + jp) * 64 + lane]; };
   // S = sum_j a_j r_j + dctx . ctx  (the row's group-0 loads are already in flight)
   float S = 0.f;
   for (int i = tid; i < len; i += NT) {
@@ -279,38 +288,49 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
   for (int k = tid; k < A; k += NT) S += dctx[(size_t)b * A + k] * ctx[(size_t)b * A + k];
   S = block_sum<NT>(S, red);
   auto compute = [&](int grp, const Rows<NK>& e, const Rows<NK>& f, const Scal& x) {
+    f32x2 d2[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d2[q] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        const f32x2 dk = par(3, kb, jp);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d2[q] = fma2(bf2pair(e.x[kb][q][jp]), dk, d2[q]);
+      }
     float pd[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f32x2 d2 = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int kb = 0; kb < NK; ++kb)
-#pragma unroll
-        for (int jp = 0; jp < 4; ++jp)
-          d2 = fma2(bf2pair(e.x[kb][q][jp]), f32x2{dk[kb][2 * jp], dk[kb][2 * jp + 1]}, d2);
-      pd[q] = d2.x + d2.y;
-    }
+    for (int q = 0; q < 4; ++q) pd[q] = d2[q].x + d2[q].y;
     const float dot = bfly4(pd, b5, b4);
     const int p = 4 * grp + qm;
     const float de_q = p < len ? x.a * (x.r + dot - S) : 0.f;
-    float dcv[4];
+    float deq[4], cq[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float de = rdlane(de_q, 16 * q);
-      const float c = rdlane(x.c, 16 * q);
-      f32x2 dc2 = f32x2{0.f, 0.f};
+      deq[q] = rdlane(de_q, 16 * q);
+      cq[q] = rdlane(x.c, 16 * q);
+    }
+    f32x2 dc2[4];
 #pragma unroll
-      for (int kb = 0; kb < NK; ++kb)
+    for (int q = 0; q < 4; ++q) dc2[q] = f32x2{0.f, 0.f};
 #pragma unroll
-        for (int jp = 0; jp < 4; ++jp) {
-          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+    for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        const f32x2 ps = par(0, kb, jp), pw = par(1, kb, jp), pv = par(2, kb, jp);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(pw, splat2(cq[q]), ps));
           const f32x2 r = rsig2(y);
           const f32x2 qv = fma2(-r, r, r);
-          acc[kb][jp] = fma2(qv, splat2(de), acc[kb][jp]);
-          dc2 = fma2(qv, v4w[kb][jp], dc2);
+          acc[kb][jp] = fma2(qv, splat2(deq[q]), acc[kb][jp]);
+          dc2[q] = fma2(qv, pv, dc2[q]);
         }
-      dcv[q] = dc2.x + dc2.y;
-    }
+      }
+    float dcv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dcv[q] = dc2[q].x + dc2[q].y;
     const float hc = bfly4(dcv, b5, b4);
     if ((lane & 15) == 0 && p < T) {
       de_out[rb + p] = de_q;

@@ -94,11 +94,12 @@ def test_attn_fwd_row_matches_fp32(A, Na, rep):
         assert err < (1e-2 if name == "ctx_bf" else 2e-3), (name, err)
 
 
-def test_attn_bwd_row_matches_fp32():
+@pytest.mark.parametrize("A", [512, 1024])
+def test_attn_bwd_row_matches_fp32(A):
     """attn_bwd_row (one workgroup per row) against the fp32 reference of the fused attention
-    backward step, A = 512; lens of 1, a few and T."""
+    backward step, A = 512 (parameters in registers) and 1024 (in LDS); lens of 1, a few and T."""
     k = ops()
-    B, T, A = 6, 300, 512
+    B, T = 6, 300
     gen = torch.Generator(device="cuda").manual_seed(78)
     dev = "cuda"
 

@@ -313,10 +313,10 @@ class HipPointerGenerator:
         # multi-block-per-row kernels of attention.hip.  cfg.row_attn forces it on / off.
         self.row_attn = bool(self.k.attn_row_ok(A, T)) and (
             cfg.row_attn if cfg.row_attn is not None else (B >= 128 or self.det))
-        # backward: the row kernel at A = 1024 (16 features per lane, 8 waves at 256 VGPRs)
-        # hides too little latency -- config #5 decoder backward 79 ms vs 59 ms with the
-        # multi-block attn_bwd_step (tools/phase_micro.py) -- so it is used at A = 512 only
-        self.row_attn_bwd = self.row_attn and (A == 512 or cfg.row_attn is True or self.det)
+        # backward: the row kernel too (its per-feature parameters in LDS: at A = 1024, 256 rows,
+        # T = 800 it streams E and F at 5.2 TB/s, 162 us vs 206 us for the multi-block
+        # attn_bwd_step -- tools/attn_micro_c5.py)
+        self.row_attn_bwd = self.row_attn
         w["F"] = z(B, T, A, dt=BF)
         # transposed copy for the lanes-over-positions score kernel (not needed by the row
         # kernels; the beam decoder sets keep_ft to get it from _encoder_forward)
