@@ -720,7 +720,9 @@ int lstm_persistent_capacity(int H) {
 // Rows per team: 16, or 32 for the H = 512 forward above batch 256 (the 4-wave RT = 2 kernel:
 // batch 1024 in 2 launches instead of 4; tools/lstm_micro.py, T = 800: B = 1024 19.1 -> 12.7 ms,
 // B = 512 9.7 -> 6.4 ms per launch sequence, 7.9 us per step vs 6.0 for 16-row teams).  The
-// backward keeps 16.
+// backward keeps 16: a 32-row BPTT (4 waves with two output slices each, 256 registers of W_hh,
+// inputs staged through LDS) still spilled ~40 registers and ran 36 us per step against 7.6 --
+// B = 1024: 29.1 vs 24.4 ms.
 static int lstm_rows(int H, int B, bool bwd) { return (!bwd && H == 512 && B > 256) ? 32 : 16; }
 
 // Row tiles per launch: the most whose grid (NC workgroups per (direction, tile) team,
