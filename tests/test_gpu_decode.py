@@ -165,9 +165,11 @@ def test_device_beam_graph_equals_eager_and_tracks_oracle(coverage, pointer_gen)
         assert len(hg[0].attn_dists) == len(hg[0].tokens) - 1
 
 
-def test_pipelined_decode_batches_equal_batch_by_batch():
+@pytest.mark.parametrize("overlap", [False, True])
+def test_pipelined_decode_batches_equal_batch_by_batch(overlap):
     """decode_batches (results snapshotted to pinned memory, backtracked while the next batch
-    runs) == decode() batch by batch: same summaries in the same order."""
+    runs; overlap: the next batch's encoder on a side stream beside the decode steps) ==
+    decode() batch by batch: same summaries in the same order."""
     from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
     hps, vocab, batch, params = _peaked_setup(True, pointer_gen=True)
     corpus = SyntheticCorpus(vocab_size=hps.vocab_size, raw_vocab=3 * hps.vocab_size, seed=9, art_mean=40, art_sd=10,
@@ -176,6 +178,7 @@ def test_pipelined_decode_batches_equal_batch_by_batch():
     batches = [batch] + more
     d = DeviceBeamDecoder(hps, vocab, params, n_articles=hps.batch_size, T=hps.max_enc_steps, use_graph=True)
     seq = [[h.tokens for h in d.decode(b)] for b in batches]
+    d.overlap_encoder = overlap
     piped = [[h.tokens for h in hy] for hy in d.decode_batches(batches)]
     assert piped == seq
 

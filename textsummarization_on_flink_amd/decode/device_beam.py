@@ -61,9 +61,15 @@ class DeviceBeamDecoder:
         self.row_attn = self.eng.cfg.decode_row_attn and bool(self.k.attn_row_ok(self.eng.A, T))
         self.eng.keep_ft = not self.row_attn  # the multi-block score kernel reads transposed features
         self.dev = self.eng.dev
+        # decode_batches: run batch n + 1's encoder on a side stream beside batch n's decode
+        # steps when the encoder is long enough to pay for the CUs its persistent LSTM holds
+        # (bench, 64 articles: hidden 512 / 2 layers / T = 800 2263 -> 2550 summaries/s; hidden
+        # 256 / 1 layer / T = 400, a 1.1 ms encoder: 6016 -> 5817, so off)
+        self.overlap_encoder = self.eng.L > 1 or self.eng.H >= 512
         self._alloc()
         self.refresh_weights()
         self.graph = None
+        self._captured_now = False
 
     # ------------------------------------------------------------------ setup
     def _alloc(self):
@@ -126,9 +132,29 @@ class DeviceBeamDecoder:
 
     # ------------------------------------------------------------------ per-chunk phases
     def _encode(self, batch):
+        self.eng.set_batch(batch)
+        self.eng._encoder_forward()
+        self._encode_copy()
+
+    def _encode_launch(self, batch):
+        """The encoder forward of ``batch`` into the engine's own buffers, queued on a side
+        stream behind everything the current stream has queued so far (in particular the
+        previous batch's ``_encode_copy`` out of those buffers).  The decode steps touch none
+        of them, so the next batch's encoder runs beside the current batch's decode steps
+        (``decode_batches``); ``_encode_copy`` after waiting on ``self._enc_ev`` picks it up."""
+        if not hasattr(self, "_enc_stream"):
+            self._enc_stream = torch.cuda.Stream(self.dev)
+        s = self._enc_stream
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.eng.set_batch(batch)
+            self.eng._encoder_forward()
+        self._enc_ev = torch.cuda.Event()
+        self._enc_ev.record(s)
+
+    def _encode_copy(self):
+        """Encoder outputs (engine buffers) -> the decoder's feature and initial-state buffers."""
         eng, b, beam = self.eng, self.b, self.beam
-        eng.set_batch(batch)
-        eng._encoder_forward()
         w = eng.w
         # encoder features stay one row per article: the attention kernels read them once for
         # all ``beam`` hypotheses of the article (rep = beam)
@@ -271,6 +297,7 @@ class DeviceBeamDecoder:
         with torch.cuda.graph(self.graph):
             self._graph_steps()
         torch.cuda.synchronize()
+        self._captured_now = True  # the warm-up consumed the encoded state: re-encode once
 
     # ------------------------------------------------------------------ driver
     def run(self, batch) -> None:
@@ -278,14 +305,24 @@ class DeviceBeamDecoder:
         for _ in self.run_chunks(batch):
             pass
 
-    def run_chunks(self, batch):
+    def run_chunks(self, batch, pre_encoded: bool = False, next_batch=None):
         """Generator form of ``run``: each iteration queues one early-exit chunk of decode steps
-        on the current stream and yields (``decode_batches`` does host work in between)."""
+        on the current stream and yields (``decode_batches`` does host work in between).
+        ``pre_encoded``: ``batch``'s encoder was queued by ``_encode_launch``; ``next_batch``:
+        queue its encoder (side stream) once this batch's encoder outputs are copied out."""
+        if pre_encoded:
+            torch.cuda.current_stream().wait_event(self._enc_ev)
         if self.use_graph and self.graph is None:
             self._encode(batch)
             self._prologue()
             self._capture()
-        self._encode(batch)
+        if pre_encoded and not self._captured_now:
+            self._encode_copy()
+        else:
+            self._encode(batch)
+        self._captured_now = False
+        if next_batch is not None:
+            self._encode_launch(next_batch)
         self._prologue()
         # early exit when every article is done, checked one chunk late: the all-done flag of
         # chunk c is copied to pinned memory behind an event and read once chunk c+1 is queued,
@@ -371,11 +408,22 @@ class DeviceBeamDecoder:
         the next batch's encoder and first decode chunk run.  Same results as ``decode`` per
         batch; the last batch is finished after the loop."""
         pending, slot = None, 0
-        for batch in batches:
-            if batch.enc_batch.shape[0] != self.Na:
-                raise ValueError(f"batch has {batch.enc_batch.shape[0]} rows, engine expects {self.Na}")
+
+        def rows_ok(bt):
+            if bt is not None and bt.enc_batch.shape[0] != self.Na:
+                raise ValueError(f"batch has {bt.enc_batch.shape[0]} rows, engine expects {self.Na}")
+            return bt
+
+        it = iter(batches)
+        ov = self.overlap_encoder
+        batch = rows_ok(next(it, None))
+        if batch is not None and ov:
+            self._encode_launch(batch)
+        # overlap_encoder: batch n + 1's encoder runs on a side stream beside batch n's decode steps
+        while batch is not None:
+            nxt = rows_ok(next(it, None))
             first = True
-            for _ in self.run_chunks(batch):
+            for _ in self.run_chunks(batch, pre_encoded=ov, next_batch=nxt if ov else None):
                 if first and pending is not None:  # the GPU has this batch's work queued
                     yield self._finish(pending)
                     pending = None
@@ -383,6 +431,7 @@ class DeviceBeamDecoder:
             arrays, ev = self._snapshot(slot)
             slot ^= 1
             pending = (arrays, ev, int(batch.valid.sum()), self.steps_run)
+            batch = nxt
         if pending is not None:
             yield self._finish(pending)
 
