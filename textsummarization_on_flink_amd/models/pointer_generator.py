@@ -216,14 +216,14 @@ class HipPointerGenerator:
         # current stream, so a captured hipGraph holds parallel branches): one group's small
         # latency-bound cell kernels run beside another group's bandwidth-bound attention
         # kernels instead of serialising behind them.  cfg.split overrides (1 = one chain).
-        # Default: 2 groups from B = 128, 4 from B = 512 (config #5, H = 512: B = 512 161.6 -> 156.9 ms
-        # per step, B = 1024 309.0 -> 301.1-301.9 ms; 8 groups 303.2; B = 256: 2 and 4 equal within
-        # noise, 19.64 / 19.71 ms; profiles/r2/ab/split_groups.jsonl)
-        sp = cfg.split or (4 if B >= 512 and B % 64 == 0 else 2 if B >= 128 and B % 32 == 0 else 1)
+        # Default: 2 groups from B = 128, 4 from B = 256 (config #5, H = 512: B = 512 161.6 -> 156.9 ms
+        # per step, B = 1024 309.0 -> 301.1-301.9 ms; 8 groups 303.2 (profiles/r2/ab/split_groups.jsonl);
+        # B = 256 since the LDS-parameter row backward: 4 groups 19.35 / 19.49 ms, 2 groups 20.21 /
+        # 19.99, 8 groups 27.2, 1 group 20.75 (profiles/r3/ab/split_b256.txt))
+        sp = cfg.split or (4 if B >= 256 and B % 64 == 0 else 2 if B >= 128 and B % 32 == 0 else 1)
         self.split = sp if (sp > 1 and B % (16 * sp) == 0) else 1
-        # cfg.split_bwd: the decoder backward loop's own group count (default: split; at B = 256
-        # 2 groups 19.59-19.62 ms per step, 1 group 20.02-20.07, 4 groups 20.09:
-        # profiles/r2/ab/split_bwd.jsonl)
+        # cfg.split_bwd: the decoder backward loop's own group count (default: split; B = 256 with
+        # 4 forward groups: 4 backward groups 19.48 ms per step, 2 groups 19.79)
         spb = cfg.split_bwd or self.split
         self.split_bwd = spb if (spb > 1 and B % (16 * spb) == 0) else 1
         ns = max(self.split, self.split_bwd)
