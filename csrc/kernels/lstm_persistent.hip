@@ -520,6 +520,10 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
     cn[i] = cs[((size_t)d * (T + 1) + T) * BH + ri];
   }
   for (int s = T - 1; s >= 0; --s) {
+    // row0v = row0, opaque to the optimizer each step: otherwise every per-peer / per-row
+    // granule address is hoisted out of the step loop as a 64-bit register pair
+    int row0v = row0;
+    asm volatile("" : "+v"(row0v));
     float dho[RPL], a4[RPL][4], cpv[RPL];
 #pragma unroll
     for (int i = 0; i < RPL; ++i) {
@@ -546,6 +550,7 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
       if constexpr (NC > 1) {
         // peers in chunks of PC (at H = 512 all 8 at once would hold 32 VGPRs of granules and
         // spill); each chunk's ready granules keep their value in x (not re-read)
+        // (all 8 peers at once at H = 512 spills 19 VGPRs: 8.9 vs 7.4 us per step)
         constexpr int PC = NC < 4 ? NC : 4;
         const gu64* src = xb + (size_t)((s + 1) & 1) * NC * NC * SLOT + (size_t)c * NC * SLOT;
         const unsigned tag = (unsigned)(T - 1 - s);
@@ -561,7 +566,7 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
 #pragma unroll
               for (int i = 0; i < RPL; ++i)
                 if (p0 + q != c && !((ready >> (q * RPL + i)) & 1))
-                  x[q][i] = __hip_atomic_load(src + (size_t)(p0 + q) * SLOT + (row0 + i) * 64 + ul, RLX_AGENT);
+                  x[q][i] = __hip_atomic_load(src + (size_t)(p0 + q) * SLOT + (row0v + i) * 64 + ul, RLX_AGENT);
 #pragma unroll
             for (int q = 0; q < PC; ++q)
 #pragma unroll
