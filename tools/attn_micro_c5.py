@@ -8,6 +8,7 @@ batch NG * rows; NG = 1 re-reads one group (warm).  A plain reduction over the s
 
   MB=256 T=800 A=1024 NG=4 python tools/attn_micro_c5.py     (config #5, one row group)
   MB=256 T=400 A=512  NG=1 python tools/attn_micro_c5.py     (bench default, warm)
+(FEAT=0 skips the post-loop feature-gradient pass, D decoder steps, timed in ms.)
 Prints one JSON line: microseconds per launch and the effective GB/s of F + E.
 """
 import json
@@ -68,6 +69,15 @@ def main():
                                                          de, ds, dco, MB, T, A), NG)
     res["bwd_step"] = timeit(lambda i: (ds.zero_(), k.attn_bwd_step(E[i], F[i], s, v, wc, cov, att, dctx, ctx, ga, dcn,
                                                                     gcl, lens, de, ds, dco, MB, T, A)), NG)
+    if os.environ.get("FEAT", "1") == "1":  # the post-loop dF / dv / dwc pass over D decoder steps
+        D = int(os.environ.get("D", "100"))
+        S_all = torch.randn(D, MB, A, device=dev, generator=g) * 0.5
+        cov_all = torch.rand(D, MB, T, device=dev, generator=g)
+        de_all = torch.randn(D, MB, T, device=dev, generator=g) * 0.01
+        dF = torch.empty(MB, T, A, device=dev, dtype=torch.bfloat16)
+        dv, dwc = torch.zeros(64, A, device=dev), torch.zeros(64, A, device=dev)
+        res["bwd_feat_ms"] = round(timeit(lambda i: k.attn_bwd_feat(F[i], S_all, v, wc, cov_all, de_all, lens, dF, dv,
+                                                                     dwc, D, MB, T, A), NG, it=3) / 1e3, 3)
     for key in ("sum_FE", "fwd_row", "bwd_row", "bwd_step"):
         if key in res:
             res[key + "_GBs"] = bw(res[key])
