@@ -108,14 +108,17 @@ __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[NI][4], int jr, c
 // VGPRs, measured the same before this layout and spills with it.)
 // RH = 2: 128 rows per workgroup, the W^T fragments reused for two 64-row halves (half the
 // workgroups and W^T fetches: 392 tiles at R = 256 = one round), X tile 68 KB of LDS.
-template <int OCC, int RH, int HMAX>
+// HFIX: H == HMAX, known at compile time (the X-staging row / chunk split by H / 8 is then a
+// shift instead of an integer division per 16-byte chunk)
+template <int OCC, int RH, int HMAX, bool HFIX = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void vocab_logits_kernel(
     const bf16* __restrict__ X,     // [R][H]  output-projection activations (bf16)
     const bf16* __restrict__ WT,    // [V][H]  output_projection/w transposed ("Bt")
     const float* __restrict__ bias, // [V]
     float* __restrict__ logits,     // [R][V]  fp32 (bias added)
     float* __restrict__ part_ms,    // [R][nt][2]  per tile (max, sum exp)
-    int R, int V, int H) {
+    int R, int V, int Hrt) {
+  const int H = HFIX ? HMAX : Hrt;
   constexpr int BR = VT_ROWS * RH;  // rows per block
   constexpr int NI = vt_ni(HMAX), VT_COLS = vt_cols(HMAX), KS = HMAX / 32;
   __shared__ float Pm[4][BR], Ps[4][BR];
@@ -500,12 +503,13 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
   // hidden 512: 64-row workgroups (the X tile is 66 KB), 128 columns each
   if (H <= 256) {
     const int RB = (R + VT_ROWS * 2 - 1) / (VT_ROWS * 2);
+    // (HFIX at 256 spills 16 VGPRs: the constant split lets all 16 X chunks be hoisted in flight)
     hipLaunchKernelGGL((vocab_logits_kernel<2, 2, 256>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
                        logits, part_ms, R, V, H);
   } else {
     const int RB = (R + VT_ROWS - 1) / VT_ROWS;
-    hipLaunchKernelGGL((vocab_logits_kernel<2, 1, 512>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
-                       logits, part_ms, R, V, H);
+    hipLaunchKernelGGL((vocab_logits_kernel<2, 1, 512, true>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT,
+                       bias, logits, part_ms, R, V, H);
   }
   hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
                      out_lp, V, T, K, beam, nt, tcols, pgi, bt ? *bt : none);
