@@ -5,6 +5,7 @@
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
+#include <algorithm>
 #include <optional>
 
 #include "launchers.h"
@@ -169,6 +170,44 @@ void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tenso
   launch_attn_bwd_row(P<bf16>(E), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
                       P<float>(dctx), P<float>(ctx), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl),
                       P<int>(lens), P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, stream());
+}
+
+// projected-context row attention (training): G = enc_out . W_in[E:] ([B, T, 128]) replaces E in
+// the recurrence; the kernels output / consume g_t = sum_i a_i G_i and dx_{t+1} (attention_row.hip)
+bool attn_rowp_ok(int64_t A, int64_t T, int64_t EG) { return attn_rowp_supported((int)A, (int)T, (int)EG); }
+void attn_fwd_rowp(const Tensor& F, const Tensor& G, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
+                   const Tensor& lens, const Tensor& a_out, const OT& cov_out, const OT& covloss, const Tensor& gx,
+                   const Tensor& gx_bf, int64_t B, int64_t T, int64_t A) {
+  chk(F, BF, "F"); chk(G, BF, "G"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens");
+  chk(a_out, F32, "a_out"); chk(gx, F32, "gx"); chk(gx_bf, BF, "gx_bf");
+  const int64_t EG = gx.numel() / std::max<int64_t>(B, 1);
+  TORCH_CHECK(attn_rowp_supported((int)A, (int)T, (int)EG), "projected row attention needs A in {512, 1024}, "
+              "T <= 2048 and a 128-wide projection");
+  numel_eq(F, B * T * A, "F"); numel_eq(G, B * T * EG, "G"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v");
+  numel_eq(lens, B, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(gx, B * EG, "gx"); numel_eq(gx_bf, B * EG, "gx_bf");
+  chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out");
+  chko(covloss, F32, B, "covloss");
+  launch_attn_fwd_rowp(P<bf16>(F), P<bf16>(G), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens),
+                       P<float>(a_out), PO<float>(cov_out), PO<float>(covloss), P<float>(gx), P<bf16>(gx_bf), B, T, A,
+                       stream());
+}
+void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
+                   const Tensor& a, const OT& dx, const Tensor& gv, const OT& Ga, const OT& dcov_next, const OT& gcl,
+                   const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out, int64_t B, int64_t T,
+                   int64_t A) {
+  chk(G, BF, "G"); chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(gv, F32, "gv");
+  chk(lens, I32, "lens"); chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
+  const int64_t EG = gv.numel() / std::max<int64_t>(B, 1);
+  TORCH_CHECK(attn_rowp_supported((int)A, (int)T, (int)EG), "projected row attention needs A in {512, 1024}, "
+              "T <= 2048 and a 128-wide projection");
+  numel_eq(G, B * T * EG, "G"); numel_eq(F, B * T * A, "F"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v");
+  numel_eq(a, B * T, "a"); numel_eq(gv, B * EG, "gv"); numel_eq(lens, B, "lens");
+  numel_eq(de_out, B * T, "de_out"); numel_eq(ds, B * A, "ds");
+  chko(dx, F32, B * EG, "dx"); chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(Ga, F32, B * T, "Ga");
+  chko(dcov_next, F32, B * T, "dcov_next"); chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
+  launch_attn_bwd_rowp(P<bf16>(G), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
+                       PO<float>(dx), P<float>(gv), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl), P<int>(lens),
+                       P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, stream());
 }
 
 void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
@@ -833,6 +872,9 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("attn_row_ok", &attn_row_ok);
   m.def("attn_fwd_row", &attn_fwd_row);
   m.def("attn_bwd_row", &attn_bwd_row);
+  m.def("attn_rowp_ok", &attn_rowp_ok);
+  m.def("attn_fwd_rowp", &attn_fwd_rowp);
+  m.def("attn_bwd_rowp", &attn_bwd_rowp);
   m.def("attn_bwd_feat", &attn_bwd_feat);
   m.def("attn_chunks", &attn_chunks);
   m.def("dec_cell_fwd", &dec_cell_fwd);

@@ -377,8 +377,339 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------ projected context
+// Training variant of the two kernels above that never reads E (reference
+// attention_decoder.py:79-129,138-158).  Inside the decoder recurrence the context vector is only
+// consumed through the input merge x_{t+1} = [emb, ctx_t] . W_in, so the loop needs
+//   g_t = ctx_t . W_in[E:] = sum_i a_i G_i,   G = enc_out . W_in[E:]   ([T, EG], EG = emb_dim = 128)
+// instead of ctx_t (A = 512 / 1024 features).  G is one GEMM before the loop; the full ctx_t of all
+// steps (output projection, p_gen, weight gradients) is one batched GEMM a . enc_out after it.  The
+// backward splits  da_i = dctx_t . E_i  into the part known before the loop (output projection and
+// p_gen terms: one batched GEMM, folded into r_i = Ga_i) and the recurrent part
+//   dctx_rec_t . E_i = (dx_{t+1} . W_in[E:]^T) . E_i = dx_{t+1} . G_i.
+// Per (step, row, position) the loop then streams F_i (A features) and G_i (128) instead of F_i and
+// E_i: 1.25 KB instead of 2 KB at A = 512, 2.25 KB instead of 4 KB at A = 1024 -- the row kernels run
+// at the HBM rate, so the bytes are the time (profiles/r3/attention_analysis.md).
+// Lane layout of G: a 4-position group is 4 x 128 bf16 = one 16-byte chunk per lane, lane l holding
+// features (l & 15) * 8 .. + 8 of position l >> 4 -- the position whose score the lane holds after
+// bfly4, so the context update needs no cross-lane traffic.
+constexpr int kEG = 128;
+
+template <int NK, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
+    const bf16* __restrict__ F, const bf16* __restrict__ G, const float* __restrict__ s,
+    const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
+    const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
+    float* __restrict__ covloss, float* __restrict__ gx, bf16* __restrict__ gx_bf, int T) {
+  constexpr int A = 512 * NK, NT = NW * 64;
+  __shared__ float es[kRowMaxT];
+  __shared__ float part[NW][4][kEG];
+  __shared__ float wm[NW], wl[NW], red[NW];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
+  const size_t rb = (size_t)b * T;
+  const bf16* Fb = F + (size_t)b * T * A;
+  const bf16* Gb = G + (size_t)b * T * kEG + (lane & 15) * 8;
+  const int ngrp = (len + 3) >> 2;
+  const int qm = lane >> 4;
+  const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
+  Rows<NK> fA, fB;
+  u32x4 gA, gB;
+  float cA = 0.f, cB = 0.f;
+  auto load = [&](int grp, Rows<NK>& f, u32x4& gq, float& c) {
+    load_rows<NK>(f, Fb, 4 * grp, len, lane);
+    const int p = min(4 * grp + qm, len - 1);
+    gq = __builtin_bit_cast(u32x4, ld8(Gb + (size_t)p * kEG));
+    c = cov ? cov[rb + p] : 0.f;
+  };
+  if (wid < ngrp) load(wid, fA, gA, cA);
+  const float* srow = s + (size_t)b * A;
+  f32x2 s2[NK][4], w2[NK][4], v2[NK][4], acc[4];
+  float vsum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) {
+    const int k0 = kb * 512 + lane * 8;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      const float2 sv = *reinterpret_cast<const float2*>(srow + k0 + 2 * jp);
+      const float2 vv = *reinterpret_cast<const float2*>(v + k0 + 2 * jp);
+      const float2 wv = wc ? *reinterpret_cast<const float2*>(wc + k0 + 2 * jp) : make_float2(0.f, 0.f);
+      s2[kb][jp] = f32x2{sv.x, sv.y} * K2LOG2E;
+      w2[kb][jp] = f32x2{wv.x, wv.y} * K2LOG2E;
+      v2[kb][jp] = f32x2{vv.x, vv.y};
+      vsum += vv.x + vv.y;
+    }
+  }
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp) acc[jp] = f32x2{0.f, 0.f};
+  // online softmax: m_w is wave-uniform, l_l is the lane's own position's share of the wave sum
+  float m_w = -INFINITY, l_l = 0.f;
+  auto compute = [&](int grp, const Rows<NK>& f, const u32x4& gq, float c_l) {
+    float pd[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float c = rdlane(c_l, 16 * q);
+      f32x2 d2 = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          d2 = fma2(v2[kb][jp], rsig2(y), d2);
+        }
+      pd[q] = vsum - 2.0f * (d2.x + d2.y);
+    }
+    float eq = bfly4(pd, b5, b4);
+    const int p = 4 * grp + qm;
+    if (p >= len) eq = -INFINITY;
+    if ((lane & 15) == 0 && p < len) es[p] = eq;
+    const float e0 = rdlane(eq, 0), e1 = rdlane(eq, 16), e2 = rdlane(eq, 32), e3 = rdlane(eq, 48);
+    const float mn = fmaxf(m_w, fmaxf(fmaxf(e0, e1), fmaxf(e2, e3)));  // e0 is always valid (p0 < len)
+    const float sc = m_w == -INFINITY ? 0.f : fexp(m_w - mn);
+    const float pq = fexp(eq - mn);
+    l_l = fmaf(l_l, sc, pq);
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) acc[jp] = fma2(bf2pair(gq[jp]), splat2(pq), acc[jp] * sc);
+    m_w = mn;
+  };
+  for (int g = wid; g < ngrp;) {
+    const int g1 = g + NW;
+    if (g1 < ngrp) load(g1, fB, gB, cB);
+    compute(g, fA, gA, cA);
+    if (g1 >= ngrp) break;
+    const int g2 = g1 + NW;
+    if (g2 < ngrp) load(g2, fA, gA, cA);
+    compute(g1, fB, gB, cB);
+    g = g2;
+  }
+  // merge: the 4 position quads of a wave hold the same features, then the waves
+  const float lw = (rdlane(l_l, 0) + rdlane(l_l, 16)) + (rdlane(l_l, 32) + rdlane(l_l, 48));
+  if (lane == 0) {
+    wm[wid] = m_w;
+    wl[wid] = lw;
+  }
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp)
+    *reinterpret_cast<float2*>(&part[wid][qm][(lane & 15) * 8 + 2 * jp]) = make_float2(acc[jp].x, acc[jp].y);
+  __syncthreads();
+  float m = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) m = fmaxf(m, wm[w]);
+  float L = 0.f, wsc[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    wsc[w] = wm[w] == -INFINITY ? 0.f : fexp(wm[w] - m);
+    L += wl[w] * wsc[w];
+  }
+  const float invL = 1.0f / L;
+  for (int k = tid; k < kEG; k += NT) {
+    float c = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) c += ((part[w][0][k] + part[w][1][k]) + (part[w][2][k] + part[w][3][k])) * wsc[w];
+    c *= invL;
+    gx[(size_t)b * kEG + k] = c;
+    gx_bf[(size_t)b * kEG + k] = f2bf(c);
+  }
+  float cl = 0.f;
+  for (int i = tid; i < T; i += NT) {
+    const float a = i < len ? fexp(es[i] - m) * invL : 0.f;
+    a_out[rb + i] = a;
+    if (cov_out) {
+      const float c = cov ? cov[rb + i] : 0.f;
+      cov_out[rb + i] = c + a;
+      cl += fminf(a, c);
+    }
+  }
+  if (covloss) {
+    cl = block_sum<NT>(cl, red);
+    if (tid == 0) covloss[b] = cl;
+  }
+}
+
+// backward: da_i = r_i + dx . G_i (r_i already holds the output-projection / p_gen part of
+// dctx . E_i), S = sum_j a_j r_j + dx . g_t; the rest as attn_bwd_row.  dx == nullptr: last step.
+template <int NK, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
+    const bf16* __restrict__ G, const bf16* __restrict__ F, const float* __restrict__ s,
+    const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
+    const float* __restrict__ a, const float* __restrict__ dx, const float* __restrict__ gv,
+    const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
+    const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
+    float* __restrict__ dcov_out, int T) {
+  constexpr int A = 512 * NK, NT = NW * 64;
+  __shared__ float part[NW][A];
+  __shared__ float red[NW];
+  __shared__ f32x2 prm[3 * NK * 4 * 64];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
+  const size_t rb = (size_t)b * T;
+  const float g = gcl ? gcl[b] : 0.f;
+  const bf16* Gb = G + (size_t)b * T * kEG + (lane & 15) * 8;
+  const bf16* Fb = F + (size_t)b * T * A;
+  const int ngrp = (len + 3) >> 2;
+  const int qm = lane >> 4;
+  const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
+  struct Scal {
+    float a, r, c, dn;
+  };
+  Rows<NK> fA, fB;
+  u32x4 gA, gB;
+  Scal xA{}, xB{};
+  auto load = [&](int grp, Rows<NK>& f, u32x4& gq, Scal& x) {
+    load_rows<NK>(f, Fb, 4 * grp, len, lane);
+    const int p = 4 * grp + qm;
+    const int pc = min(p, len - 1);
+    gq = __builtin_bit_cast(u32x4, ld8(Gb + (size_t)pc * kEG));
+    const size_t ix = rb + pc;
+    x.a = a[ix];
+    x.c = cov ? cov[ix] : 0.f;
+    x.dn = dcov_next ? dcov_next[ix] : 0.f;
+    x.r = (Ga ? Ga[ix] : 0.f) + x.dn + ((gcl && x.a <= x.c) ? g : 0.f);
+  };
+  if (wid < ngrp) load(wid, fA, gA, xA);
+  f32x2 acc[NK][4];
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb) {
+    const int k0 = kb * 512 + lane * 8;
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      acc[kb][jp] = f32x2{0.f, 0.f};
+      if (wid != 0) continue;
+      const float2 sv = *reinterpret_cast<const float2*>(s + (size_t)b * A + k0 + 2 * jp);
+      const float2 vv = *reinterpret_cast<const float2*>(v + k0 + 2 * jp);
+      const float2 wv = wc ? *reinterpret_cast<const float2*>(wc + k0 + 2 * jp) : make_float2(0.f, 0.f);
+      prm[((0 * NK + kb) * 4 + jp) * 64 + lane] = f32x2{sv.x, sv.y} * K2LOG2E;
+      prm[((1 * NK + kb) * 4 + jp) * 64 + lane] = f32x2{wv.x, wv.y} * K2LOG2E;
+      prm[((2 * NK + kb) * 4 + jp) * 64 + lane] = f32x2{4.f * vv.x * wv.x, 4.f * vv.y * wv.y};
+    }
+  }
+  auto par = [&](int which, int kb, int jp) -> f32x2 { return prm[((which * NK + kb) * 4 + jp) * 64 + lane]; };
+  // the lane's 8 features of dx (position-independent)
+  f32x2 dx2[4];
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp) {
+    const float2 d = dx ? *reinterpret_cast<const float2*>(dx + (size_t)b * kEG + (lane & 15) * 8 + 2 * jp)
+                        : make_float2(0.f, 0.f);
+    dx2[jp] = f32x2{d.x, d.y};
+  }
+  float S = 0.f;
+  for (int i = tid; i < len; i += NT) {
+    const size_t ix = rb + i;
+    const float ai = a[ix];
+    float r = (Ga ? Ga[ix] : 0.f) + (dcov_next ? dcov_next[ix] : 0.f);
+    if (gcl && ai <= (cov ? cov[ix] : 0.f)) r += g;
+    S += ai * r;
+  }
+  if (dx)
+    for (int k = tid; k < kEG; k += NT) S += dx[(size_t)b * kEG + k] * gv[(size_t)b * kEG + k];
+  S = block_sum<NT>(S, red);
+  auto compute = [&](int grp, const Rows<NK>& f, const u32x4& gq, const Scal& x) {
+    f32x2 d2 = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) d2 = fma2(bf2pair(gq[jp]), dx2[jp], d2);
+    const float dot = dpp_sum16(d2.x + d2.y);
+    const int p = 4 * grp + qm;
+    const float de_q = p < len ? x.a * (x.r + dot - S) : 0.f;
+    float deq[4], cq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      deq[q] = rdlane(de_q, 16 * q);
+      cq[q] = rdlane(x.c, 16 * q);
+    }
+    f32x2 dc2[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dc2[q] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+      for (int jp = 0; jp < 4; ++jp) {
+        const f32x2 ps = par(0, kb, jp), pw = par(1, kb, jp), pv = par(2, kb, jp);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(pw, splat2(cq[q]), ps));
+          const f32x2 r = rsig2(y);
+          const f32x2 qv = fma2(-r, r, r);
+          acc[kb][jp] = fma2(qv, splat2(deq[q]), acc[kb][jp]);
+          dc2[q] = fma2(qv, pv, dc2[q]);
+        }
+      }
+    float dcv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dcv[q] = dc2[q].x + dc2[q].y;
+    const float hc = bfly4(dcv, b5, b4);
+    if ((lane & 15) == 0 && p < T) {
+      de_out[rb + p] = de_q;
+      if (dcov_out) {
+        float r = x.dn;
+        if (p < len) {
+          r += de_q * hc;
+          if (gcl && x.a > x.c) r += g;
+        } else {
+          r = dcov_next ? dcov_next[rb + p] : 0.f;
+        }
+        dcov_out[rb + p] = r;
+      }
+    }
+  };
+  for (int gi = wid; gi < ngrp;) {
+    const int g1 = gi + NW;
+    if (g1 < ngrp) load(g1, fB, gB, xB);
+    compute(gi, fA, gA, xA);
+    if (g1 >= ngrp) break;
+    const int g2 = g1 + NW;
+    if (g2 < ngrp) load(g2, fA, gA, xA);
+    compute(g1, fB, gB, xB);
+    gi = g2;
+  }
+  for (int p = 4 * ngrp + tid; p < T; p += NT) {
+    de_out[rb + p] = 0.f;
+    if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
+  }
+#pragma unroll
+  for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp)
+      *reinterpret_cast<float2*>(&part[wid][kb * 512 + lane * 8 + 2 * jp]) =
+          make_float2(acc[kb][jp].x, acc[kb][jp].y);
+  __syncthreads();
+  for (int k = tid; k < A; k += NT) {
+    float x = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) x += part[w][k];
+    ds[(size_t)b * A + k] = 4.f * v[k] * x;
+  }
+}
+
 // ------------------------------------------------------------------------------ launchers
 bool attn_row_supported(int A, int T) { return (A == 512 || A == 1024) && T >= 1 && T <= kRowMaxT; }
+bool attn_rowp_supported(int A, int T, int EG) { return attn_row_supported(A, T) && EG == kEG; }
+
+void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const float* v, const float* wc,
+                          const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* gx,
+                          bf16* gx_bf, int B, int T, int A, hipStream_t st) {
+#define LF(NK)                                                                                            \
+  hipLaunchKernelGGL((attn_fwd_rowp_kernel<NK, row_waves<NK, false>()>), dim3(B),                        \
+                     dim3(row_waves<NK, false>() * 64), 0, st, F, G, s, v, wc, cov, lens, a_out, cov_out, covloss, \
+                     gx, gx_bf, T)
+  if (A == 512) LF(1);
+  else LF(2);
+#undef LF
+}
+
+void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const float* v, const float* wc,
+                          const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
+                          const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
+                          float* dcov_out, int B, int T, int A, hipStream_t st) {
+#define LB(NK)                                                                                            \
+  hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, row_waves<NK, true>()>), dim3(B),                         \
+                     dim3(row_waves<NK, true>() * 64), 0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, \
+                     lens, de_out, ds, dcov_out, T)
+  if (A == 512) LB(1);
+  else LB(2);
+#undef LB
+}
 
 void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
                          const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,

@@ -124,3 +124,70 @@ def test_attn_bwd_row_matches_fp32(A):
     for name, got, ref in zip(("de", "ds", "dcov"), (de, got_ds, dcov), want):
         err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         assert err < 2e-3, (name, err)
+
+
+@pytest.mark.parametrize("A", [512, 1024])
+def test_attn_fwd_rowp_matches_fp32(A):
+    """attn_fwd_rowp (projected context, training): a, coverage, coverage loss and
+    g = sum_i a_i G_i against fp32; lens of 1, a few, a partial last group and T."""
+    k = ops()
+    B, T, EG = 6, 300, 128
+    gen = torch.Generator(device="cuda").manual_seed(A + 5)
+    dev = "cuda"
+
+    def r(*shape, s=1.0):
+        return torch.randn(*shape, generator=gen, device=dev) * s
+
+    lens = torch.tensor([T, 1, 5, 130, 257, 299], dtype=torch.int32, device=dev)
+    mask = torch.arange(T, device=dev)[None, :] < lens[:, None].long()
+    F, G = r(B, T, A, s=0.5).bfloat16(), r(B, T, EG, s=0.5).bfloat16()
+    s, v, wc = r(B, A, s=0.3), r(A, s=0.1), r(A, s=0.5)
+    cov = torch.rand(B, T, generator=gen, device=dev) * mask
+    a, cov_out, cl = (torch.full((B, T), float("nan"), device=dev), torch.zeros(B, T, device=dev),
+                      torch.zeros(B, device=dev))
+    gx, gxb = torch.zeros(B, EG, device=dev), torch.zeros(B, EG, device=dev, dtype=torch.bfloat16)
+    k.attn_fwd_rowp(F, G, s, v, wc, cov, lens, a, cov_out, cl, gx, gxb, B, T, A)
+    torch.cuda.synchronize()
+    e = torch.einsum("bta,a->bt", torch.tanh(F.float() + s[:, None, :] + wc[None, None, :] * cov[:, :, None]), v)
+    a_ref = torch.softmax(e.masked_fill(~mask, float("-inf")), -1)
+    g_ref = torch.einsum("bt,bte->be", a_ref, G.float())
+    checks = (("a", a, a_ref), ("g", gx, g_ref), ("cov_out", cov_out, cov + a_ref),
+              ("covloss", cl, torch.minimum(a_ref, cov).sum(1)), ("g_bf", gxb.float(), g_ref))
+    for name, got, ref in checks:
+        err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        assert err < (1e-2 if name == "g_bf" else 2e-3), (name, err)
+
+
+@pytest.mark.parametrize("A", [512, 1024])
+@pytest.mark.parametrize("last", [False, True])
+def test_attn_bwd_rowp_matches_fp32(A, last):
+    """attn_bwd_rowp: the backward step with da_i = r_i + dx . G_i (dx = None: the last decoder
+    step) against the fp32 reference, which is the E-form with dctx . E_i = dx . G_i when
+    G = E . W and dctx = W . dx."""
+    k = ops()
+    B, T, EG = 6, 300, 128
+    gen = torch.Generator(device="cuda").manual_seed(91 + A)
+    dev = "cuda"
+
+    def r(*shape, s=1.0):
+        return torch.randn(*shape, generator=gen, device=dev) * s
+
+    lens = torch.tensor([T, 1, 5, 129, 258, 300], dtype=torch.int32, device=dev)
+    mask = torch.arange(T, device=dev)[None, :] < lens[:, None].long()
+    G, F = r(B, T, EG, s=0.5).bfloat16(), r(B, T, A, s=0.5).bfloat16()
+    s, v, wc = r(B, A, s=0.3), r(A, s=0.1), r(A, s=0.1)
+    cov = torch.rand(B, T, generator=gen, device=dev) * mask
+    a = torch.softmax(r(B, T).masked_fill(~mask, float("-inf")), -1)
+    gv = torch.einsum("bt,bte->be", a, G.float())
+    dx = None if last else r(B, EG, s=0.1)
+    Ga, dnext = r(B, T, s=0.1), r(B, T, s=0.1)
+    g = torch.full((B,), 0.7, device=dev)
+    de, dcov = torch.full((B, T), float("nan"), device=dev), torch.full((B, T), float("nan"), device=dev)
+    ds = torch.full((B, A), float("nan"), device=dev)
+    k.attn_bwd_rowp(G, F, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A)
+    torch.cuda.synchronize()
+    # the E-form reference with "E" = G and "dctx" = dx (zero at the last step)
+    want = _reference(G, F, s, v, wc, cov, a, torch.zeros(B, EG, device=dev) if last else dx, Ga, dnext, g, lens)
+    for name, got, ref in zip(("de", "ds", "dcov"), (de, ds, dcov), want):
+        err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        assert err < 2e-3, (name, err)

@@ -149,6 +149,41 @@ def test_row_attention_matches_multiblock_kernels(monkeypatch, coverage, B, T, H
         assert _rel(a, b) < tol, (n, _rel(a, b))
 
 
+@pytest.mark.parametrize("coverage,pointer_gen,B,T,H", [(True, True, 24, 200, 256), (False, True, 16, 64, 256),
+                                                       (True, True, 8, 38, 512), (False, False, 16, 130, 256)])
+def test_projected_context_matches_enc_out_path(monkeypatch, coverage, pointer_gen, B, T, H):
+    """Row attention with the projected context (attn_fwd_rowp / attn_bwd_rowp: the loop streams
+    F and G = enc_out . W_in[E:], ctx of all steps is a batched GEMM after it, the p_gen / output
+    part of da a batched GEMM before the backward) == the row kernels over enc_out: forward state,
+    loss and every parameter gradient, emb_dim 128."""
+    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
+    hps, vocab, batch, params = _setup(coverage, pointer_gen, B=B, T=T, D=6, H=H, E=128)
+    monkeypatch.setenv("TSAMD_ROW_ATTN", "1")
+    got = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("TSAMD_PROJ_ATTN", flag)
+        params.enable_grad()
+        eng = HipPointerGenerator(hps, vocab.size(), params, B=hps.batch_size, T=hps.max_enc_steps)
+        assert eng.row_attn and eng.proj_attn == (flag == "1")
+        eng.set_batch(batch)
+        out = eng.forward(need_grad=True)
+        eng.backward()
+        torch.cuda.synchronize()
+        got.append([out["total_loss"].detach().clone(), eng.w["ATT"].clone(), eng.w["CTX"].clone(),
+                    eng.w["X"].clone(), eng.w["Hb"].float().clone(), params.grad.clone()])
+        if coverage:
+            got[-1].append(eng.w["COV"].clone())
+    names = ("loss", "ATT", "CTX", "X", "Hb", "grad", "COV")
+    # bf16 G / a . enc_out vs the kernel's fp32 a x bf16 E: agreement at the bf16 rounding level
+    for n, a, b in zip(names, got[1], got[0]):
+        assert _rel(a, b) < 1e-2, (n, _rel(a, b))
+    g1, g0 = got[1][5], got[0][5]
+    for n in params.names:
+        o, c = params.offsets[n]
+        r = _rel(g1[o:o + c], g0[o:o + c])
+        assert r < 3e-2 or (float(g0[o:o + c].norm()) < 1e-5 and r < 0.2), (n, r)
+
+
 @pytest.mark.parametrize("layers,H", [(1, 256), (2, 128)])
 def test_fast_pack_matches_torch_pack(layers, H):
     """pack() after the first call = one pack_cast launch over the job table (pack.hip): every

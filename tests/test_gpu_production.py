@@ -62,7 +62,7 @@ def _oracle_check(hps, B, T_, D_, seed, cov_tol=2e-2):
     g_hip = params.grad.clone()
     att, pg = eng.w["ATT"].clone(), eng.w["pg"].clone()
     kinds = {"persistent_lstm": eng.persistent_lstm, "fused_vocab": eng.fused_vocab, "row_attn": eng.row_attn,
-             "row_attn_bwd": eng.row_attn_bwd, "split": eng.split}
+             "row_attn_bwd": eng.row_attn_bwd, "split": eng.split, "proj_attn": eng.proj_attn}
     del eng
     torch.cuda.empty_cache()
     flat = params.flat.detach().clone().requires_grad_(True)
@@ -87,7 +87,7 @@ def _oracle_check(hps, B, T_, D_, seed, cov_tol=2e-2):
 
 def test_bench_shape_matches_fp32_oracle():
     kinds = _oracle_check(_hps(256, trunc_norm_init_std=0.05), 256, T, D, seed=11)
-    assert kinds["persistent_lstm"] and kinds["fused_vocab"] and kinds["row_attn_bwd"]
+    assert kinds["persistent_lstm"] and kinds["fused_vocab"] and kinds["row_attn_bwd"] and kinds["proj_attn"]
 
 
 @pytest.mark.parametrize("B", [8, 128, 512])
@@ -100,7 +100,7 @@ def test_config5_shape_matches_fp32_oracle(B):
                   hidden_dim=512, emb_dim=128, enc_layers=2, trunc_norm_init_std=0.05)
     kinds = _oracle_check(hps, B, 800, 20, seed=21)
     assert kinds["persistent_lstm"] and kinds["fused_vocab"]
-    assert kinds["row_attn"] == (B >= 128) and kinds["row_attn_bwd"] == (B >= 128)
+    assert kinds["row_attn"] == (B >= 128) and kinds["row_attn_bwd"] == (B >= 128) and kinds["proj_attn"] == (B >= 128)
 
 
 def test_graph_replay_equals_eager_train_step():

@@ -23,6 +23,7 @@ from __future__ import annotations
 
 
 from typing import List
+from dataclasses import replace
 
 import numpy as np
 import torch
@@ -30,6 +31,7 @@ import torch
 from ..data.vocab import START_DECODING, STOP_DECODING, UNKNOWN_TOKEN
 from ..models.pointer_generator import (ATT_B, CELL_B, CELL_K, EMB, LIN_B, LIN_M, OUT_B, OV, PG_B, PG_M,
                                         HipPointerGenerator, mmf)
+from ..models.engine_config import EngineConfig
 from .beam_search import Hypothesis
 
 BF = torch.bfloat16
@@ -53,7 +55,9 @@ class DeviceBeamDecoder:
         # decode steps per captured graph: a whole early-exit chunk when it is even (one graph
         # launch per chunk instead of one per step pair), else 2
         self.gsteps = chunk if chunk % 2 == 0 else 2
-        self.eng = HipPointerGenerator(hps, self.V, params, B=self.Na, T=T, D=1)
+        # the encoder side of the engine only (the projected-context G of the training loop is not used)
+        self.eng = HipPointerGenerator(hps, self.V, params, B=self.Na, T=T, D=1,
+                                       cfg=replace(EngineConfig.from_env(), proj_attn=False))
         # attention per step: the row-resident kernel (score + softmax + context in one launch,
         # one workgroup per hypothesis reading its article's F/E rows) when the shape allows
         # it, else the multi-block kernels over the transposed features (EngineConfig.decode_row_attn)

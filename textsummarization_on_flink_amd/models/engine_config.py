@@ -13,6 +13,7 @@ engine is built); code can also pass a config explicitly.
 | TSAMD_SPLIT_BWD           | split_bwd          | auto (= split): row groups of the decoder backward loop |
 | TSAMD_FUSED_VOCAB_TRAIN   | fused_vocab_train  | 1: training vocab head with the logits only in MFMA accumulators; 0: library GEMM + ptr_loss |
 | TSAMD_FUSED_VOCAB         | fused_vocab_decode | 1: decode vocab head + top-k fused; 0: GEMM + final_topk |
+| TSAMD_PROJ_ATTN           | proj_attn          | 1: training row attention streams G = enc_out . W_in[E:] (emb_dim wide) instead of enc_out; 0: enc_out |
 | TSAMD_DEC_ROW_ATTN        | decode_row_attn    | 1: beam-decode attention through the row kernel; 0: score + softmax kernels |
 | TSAMD_DEFER_WGRAD         | defer_wgrad        | 1: decoder-side weight gradients beside the encoder BPTT (B >= 256); 0: inline |
 | TSAMD_DETERMINISTIC       | deterministic      | 0; 1: fixed-order reductions instead of fp32 atomics (bit-reproducible steps) |
@@ -43,6 +44,7 @@ class EngineConfig:
     split_bwd: int = 0
     fused_vocab_train: bool = True
     fused_vocab_decode: bool = True
+    proj_attn: bool = True
     decode_row_attn: bool = True
     defer_wgrad: bool = True
     deterministic: bool = False
@@ -57,6 +59,7 @@ class EngineConfig:
             split_bwd=int(env.get("TSAMD_SPLIT_BWD", "0") or 0),
             fused_vocab_train=_flag(env, "TSAMD_FUSED_VOCAB_TRAIN", True),
             fused_vocab_decode=_flag(env, "TSAMD_FUSED_VOCAB", True),
+            proj_attn=_flag(env, "TSAMD_PROJ_ATTN", True),
             decode_row_attn=_flag(env, "TSAMD_DEC_ROW_ATTN", True),
             defer_wgrad=_flag(env, "TSAMD_DEFER_WGRAD", True),
             deterministic=_flag(env, "TSAMD_DETERMINISTIC", False),

@@ -317,6 +317,16 @@ class HipPointerGenerator:
         # T = 800 it streams E and F at 5.2 TB/s, 162 us vs 206 us for the multi-block
         # attn_bwd_step -- tools/attn_micro_c5.py)
         self.row_attn_bwd = self.row_attn
+        # projected context (attention_row.hip, attn_*_rowp): the recurrence streams F and
+        # G = enc_out . W_in[E:] ([B, T, E]) instead of F and enc_out; ctx of all steps is one batched
+        # GEMM after the loop, the output-projection / p_gen part of dctx . E_i one before the backward
+        self.proj_attn = self.row_attn and cfg.proj_attn and bool(self.k.attn_rowp_ok(A, T, E))
+        if self.proj_attn:
+            w["Genc"] = z(B, T, E, dt=BF)
+            w["GV"] = z(D, B, E)         # g_t = sum_i a_ti G_i = ctx_t . W_in[E:]
+            w["GVb"] = z(D, B, E, dt=BF)
+            w["bd_tmp"] = z(B * D * max(A, T))  # [B, D, A] ctx / [B, D, T] da_dir GEMM outputs
+            w["DXb"] = z(D, B, E, dt=BF)
         w["F"] = z(B, T, A, dt=BF)
         # transposed copy for the lanes-over-positions score kernel (not needed by the row
         # kernels; the beam decoder sets keep_ft to get it from _encoder_forward)
@@ -433,7 +443,7 @@ class HipPointerGenerator:
                           (f32[f"enc{layer}_b"][di], p[enc_b(layer, d)])]
         pairs += [(pk["Wh"], p[WH].reshape(A, A)), (pk["RC"], p[RC]), (pk["RH"], p[RH]), (pk["RCt"], p[RC].t()),
                   (pk["RHt"], p[RH].t()), (pk["lin_emb"], M[:E]), (pk["Wic"], M[E:]), (pk["WicT"], M[E:].t()),
-                  (pk["cell_x"], K[:E]), (pk["WcT2"][:, :A], W.t()), (pk["WcT2"][:, A:], K[E:].t()),
+                  (pk["cell_x"], K[:E]), (pk["KcT"], K.t()), (pk["WcT2"][:, :A], W.t()), (pk["WcT2"][:, A:], K[E:].t()),
                   (pk["Wbig"][:E + H], K), (pk["Wbig"][E + H:], W), (pk["Ws"], p[ATT_M]), (pk["WsT"], p[ATT_M].t()),
                   (pk["OUTm"], p[OUT_M]), (pk["OUTmT"], p[OUT_M].t()), (pk["ow"], p[OW]), (pk["ovb"], p[OV])]
         if "owT" in pk:
@@ -493,6 +503,7 @@ class HipPointerGenerator:
         K = p[CELL_K]
         Wcomb = M[E:] @ K[:E]                      # [A][4H]: ctx_{t-1} -> z through x_t
         put("cell_x", K[:E])
+        put("KcT", K.t())  # [4H][E+H]: the cell weights of the projected-context recurrence
         put("WcT2", torch.cat([Wcomb, K[E:]], 0).t())  # [4H][A+H]
         put("Wbig", torch.cat([K, Wcomb], 0))          # [E+H+A][4H]
         put("Ws", p[ATT_M])
@@ -587,6 +598,8 @@ class HipPointerGenerator:
         k.rs_fwd(top["cs"], top["hs"], T, self.pk["RCt"], self.pk["RHt"], self.p[BRC], self.p[BRH], w["rs_pre"][0],
                  w["rs_pre"][1], w["Cst"][0], w["Cb"][0], w["Hb"][0], w["rs_cat"][0], w["rs_cat"][1], B, H)
         mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["Wh"])
+        if self.proj_attn:
+            mm_into(w["Genc"].view(B * T, self.E), top["out"].view(B * T, A), self.pk["Wic"])
         if self.keep_ft:
             if w["Ft"] is None:
                 w["Ft"] = torch.empty(B, A, T, dtype=BF, device=self.dev)
@@ -603,6 +616,9 @@ class HipPointerGenerator:
         self._emb_dec = emb_dec
         enc_out, lens, Ft, F = self.enc[-1]["out"], w["enc_lens"], w["Ft"], w["F"]
         v, wc = self.f32["v"], self.f32["wc"]
+
+        if self.proj_attn:
+            return self._decoder_forward_proj()
 
         def chain(r0, r1):
             Bg, rs = r1 - r0, slice(r0, r1)
@@ -629,6 +645,40 @@ class HipPointerGenerator:
         if D > 1:
             w["X"][1:].view((D - 1) * B, E).add_(mmf(w["CTXb"][:D - 1].reshape((D - 1) * B, A), self.pk["Wic"]))
         w["Xb"].copy_(w["X"])
+
+    def _decoder_forward_proj(self):
+        """Decoder forward loop with the projected context: per step the cell (its ctx input is
+        g_{t-1}, E wide, against W_cell^T), the s-projection and attn_fwd_rowp (F and G); then
+        x_t = xe_t + g_{t-1} and ctx_t = a_t . enc_out for all steps as one batched GEMM."""
+        k, w, hps = self.k, self.w, self.hps
+        B, T, D, E, H, A = self.B, self.T, self.D, self.E, self.H, self.A
+        cov = hps.coverage
+        enc_out, lens, F, G = self.enc[-1]["out"], w["enc_lens"], w["F"], w["Genc"]
+        v, wc = self.f32["v"], self.f32["wc"]
+
+        def chain(r0, r1):
+            Bg, rs = r1 - r0, slice(r0, r1)
+            for t in range(D):
+                k.dec_cell_fwd(w["XG"][t][rs], w["GVb"][t - 1][rs] if t > 0 else None, w["Hb"][t][rs],
+                               w["Cst"][t][rs], self.pk["KcT"], w["Cst"][t + 1][rs], w["Cb"][t + 1][rs],
+                               w["Hb"][t + 1][rs], w["ACT"][t][rs], Bg, H, E)
+                k.dec_sproj(w["Cb"][t + 1][rs], w["Hb"][t + 1][rs], self.pk["WsT"], self.p[ATT_B], w["S"][t][rs], Bg,
+                            H, A)
+                k.attn_fwd_rowp(F[rs], G[rs], w["S"][t][rs], v, wc, w["COV"][t][rs] if (cov and t > 0) else None,
+                                lens[rs], w["ATT"][t][rs], w["COV"][t + 1][rs] if cov else None,
+                                w["covloss"][t][rs] if cov else None, w["GV"][t][rs], w["GVb"][t][rs], Bg, T, A)
+
+        self._row_groups(chain)
+        w["X"][0].copy_(w["xe"][0])
+        if D > 1:
+            torch.add(w["xe"][1:], w["GV"][:D - 1], out=w["X"][1:])
+        w["Xb"].copy_(w["X"])
+        # ctx_t = a_t . enc_out for every step: [B][D, T] x [B][T, A] (bf16 a, fp32 accumulate)
+        w["ATTb"].copy_(w["ATT"])
+        ctx = w["bd_tmp"][:B * D * A].view(B, D, A)
+        torch.bmm(w["ATTb"].permute(1, 0, 2), enc_out, out_dtype=F32, out=ctx)
+        w["CTX"].copy_(ctx.transpose(0, 1))
+        w["CTXb"].copy_(w["CTX"])
 
     def _head_forward(self, need_grad: bool):
         w, hps, p = self.w, self.hps, self.p
@@ -803,6 +853,8 @@ class HipPointerGenerator:
             k.pgen_dirs(dpre, pm, dCTX_dir, dC_dir, dH_dir, dX_dir, None if self.det else g(PG_B).view(1), N, A, H, E)
             if self.det:
                 torch.sum(dpre, 0, keepdim=True, out=g(PG_B).view(1))
+        if self.proj_attn:
+            return self._backward_mid_proj(dCTX_dir, dH_dir, dC_dir, dX_dir, Hn, wg, run)
         if dX_dir is not None and D > 1:  # p_gen path into ctx_{t-1} through x_t (hoisted out of the loop)
             dCTX_dir[:D - 1].view((D - 1) * B, A).addmm_(dX_dir[1:].view((D - 1) * B, E), p[LIN_M][E:].t())
         # ---- decoder reverse loop
@@ -838,6 +890,66 @@ class HipPointerGenerator:
                              w["DCTX"][t - 1][rs] if t > 0 else None, w["dh_rec"][rs], Bg, E, H, A)
 
         self._row_groups(chain, self.split_bwd)
+        self._backward_mid_rest(Hn, wg, run)
+
+    def _backward_mid_proj(self, dCTX_dir, dH_dir, dC_dir, dX_dir, Hn, wg, run):
+        """Decoder reverse loop with the projected context.  Before it, the part of
+        da_ti = dctx_t . E_i that does not wait on the recurrence (output projection + p_gen:
+        dCTX_dir) as one batched GEMM, added to the pointer-path gradient dA; in it, attn_bwd_rowp
+        adds dx_{t+1} . G_i and dec_bwd_dz produces dx_t (no dctx output); after it,
+        dctx_t = dCTX_dir_t + dx_{t+1} . W_in[E:]^T for the dE GEMM."""
+        k, w, hps = self.k, self.w, self.hps
+        B, T, D, E, H, A = self.B, self.T, self.D, self.E, self.H, self.A
+        N = D * B
+        cov = hps.coverage
+        enc_out, lens, F, G = self.enc[-1]["out"], w["enc_lens"], w["F"], w["Genc"]
+        v, wc = self.f32["v"], self.f32["wc"]
+        w["DCTXb"].copy_(dCTX_dir)
+        da = w["bd_tmp"][:B * D * T].view(B, D, T)
+        torch.bmm(w["DCTXb"].permute(1, 0, 2), enc_out.transpose(1, 2), out_dtype=F32, out=da)
+        Ga = w["dA"]
+        if hps.pointer_gen:
+            Ga.add_(da.transpose(0, 1))
+        else:
+            Ga.copy_(da.transpose(0, 1))
+        w["dh_rec"].zero_()
+        w["dc_carry"].zero_()
+        dcov = w["dcov"]
+        Kc = self.pk["Wbig"][:E + H]  # W_cell: [dx | dh] = dz . W_cell^T
+
+        def chain(r0, r1):
+            Bg, rs = r1 - r0, slice(r0, r1)
+            for t in reversed(range(D)):
+                k.attn_bwd_rowp(G[rs], F[rs], w["S"][t][rs], v, wc, w["COV"][t][rs] if (cov and t > 0) else None,
+                                w["ATT"][t][rs], w["DX"][t + 1][rs] if t < D - 1 else None, w["GV"][t][rs],
+                                Ga[t][rs], dcov[(t + 1) % 2][rs] if (cov and t < D - 1) else None,
+                                w["gcl"][t][rs] if cov else None, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
+                                dcov[t % 2][rs] if cov else None, Bg, T, A)
+                k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
+                               dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A)
+                k.dec_bwd_dz(w["DZ"][t][rs], Kc, dX_dir[t][rs] if dX_dir is not None else None, None,
+                             w["DX"][t][rs], None, w["dh_rec"][rs], Bg, E, H, 0)
+
+        self._row_groups(chain, self.split_bwd)
+        w["DCTX"].copy_(dCTX_dir)
+        if D > 1:
+            dctx = w["DCTX"][:D - 1].view((D - 1) * B, A)
+            dxb = w["DXb"][1:].view((D - 1) * B, E)
+            dxb.copy_(w["DX"][1:].view((D - 1) * B, E))
+            torch.addmm(dctx, dxb, self.pk["WicT"], out_dtype=F32, out=dctx)
+        self._backward_mid_rest(Hn, wg, run)
+
+    def _backward_mid_rest(self, Hn, wg, run):
+        """Decoder / attention weight gradients, attention feature gradient and dE after the
+        decoder reverse loop."""
+        k, w, hps, p = self.k, self.w, self.hps, self.p
+        B, T, D, E, H, A = self.B, self.T, self.D, self.E, self.H, self.A
+        N = D * B
+        g = p.g
+        cov = hps.coverage
+        v, wc = self.f32["v"], self.f32["wc"]
+        lens, F = w["enc_lens"], w["F"]
         # ---- decoder weight gradients (one GEMM each over all D*B rows)
         emb_dec = self._emb_dec
 
@@ -873,7 +985,8 @@ class HipPointerGenerator:
         run(lambda: wg(g(WH).view(A, A), top["out"].view(B * T, A), dFb))
         dE = self._dE
         # dE = a^T . dctx (bf16 batched GEMM, fp32 out) + dF . W_h^T (accumulated in place)
-        w["ATTb"].copy_(w["ATT"])
+        if not self.proj_attn:  # (the projected-context forward made ATTb already)
+            w["ATTb"].copy_(w["ATT"])
         w["DCTXb"].copy_(w["DCTX"])
         torch.bmm(w["ATTb"].permute(1, 2, 0), w["DCTXb"].permute(1, 0, 2), out_dtype=F32, out=dE)
         dE2 = dE.view(B * T, A)
