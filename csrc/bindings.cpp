@@ -177,7 +177,7 @@ void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tenso
 bool attn_rowp_ok(int64_t A, int64_t T, int64_t EG) { return attn_rowp_supported((int)A, (int)T, (int)EG); }
 void attn_fwd_rowp(const Tensor& F, const Tensor& G, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                    const Tensor& lens, const Tensor& a_out, const OT& cov_out, const OT& covloss, const Tensor& gx,
-                   const Tensor& gx_bf, int64_t B, int64_t T, int64_t A) {
+                   const Tensor& gx_bf, int64_t B, int64_t T, int64_t A, const OT& dlen, int64_t step) {
   chk(F, BF, "F"); chk(G, BF, "G"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens");
   chk(a_out, F32, "a_out"); chk(gx, F32, "gx"); chk(gx_bf, BF, "gx_bf");
   const int64_t EG = gx.numel() / std::max<int64_t>(B, 1);
@@ -186,15 +186,15 @@ void attn_fwd_rowp(const Tensor& F, const Tensor& G, const Tensor& s, const Tens
   numel_eq(F, B * T * A, "F"); numel_eq(G, B * T * EG, "G"); numel_eq(s, B * A, "s"); numel_eq(v, A, "v");
   numel_eq(lens, B, "lens"); numel_eq(a_out, B * T, "a_out"); numel_eq(gx, B * EG, "gx"); numel_eq(gx_bf, B * EG, "gx_bf");
   chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(cov_out, F32, B * T, "cov_out");
-  chko(covloss, F32, B, "covloss");
+  chko(covloss, F32, B, "covloss"); chko(dlen, I32, B, "dlen");
   launch_attn_fwd_rowp(P<bf16>(F), P<bf16>(G), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens),
                        P<float>(a_out), PO<float>(cov_out), PO<float>(covloss), P<float>(gx), P<bf16>(gx_bf), B, T, A,
-                       stream());
+                       PO<int>(dlen), (int)step, stream());
 }
 void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                    const Tensor& a, const OT& dx, const Tensor& gv, const OT& Ga, const OT& dcov_next, const OT& gcl,
                    const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out, int64_t B, int64_t T,
-                   int64_t A) {
+                   int64_t A, const OT& dlen, int64_t step) {
   chk(G, BF, "G"); chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(gv, F32, "gv");
   chk(lens, I32, "lens"); chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
   const int64_t EG = gv.numel() / std::max<int64_t>(B, 1);
@@ -205,9 +205,10 @@ void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tens
   numel_eq(de_out, B * T, "de_out"); numel_eq(ds, B * A, "ds");
   chko(dx, F32, B * EG, "dx"); chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(Ga, F32, B * T, "Ga");
   chko(dcov_next, F32, B * T, "dcov_next"); chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
+  chko(dlen, I32, B, "dlen");
   launch_attn_bwd_rowp(P<bf16>(G), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
                        PO<float>(dx), P<float>(gv), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl), P<int>(lens),
-                       P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, stream());
+                       P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, PO<int>(dlen), (int)step, stream());
 }
 
 void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
@@ -229,7 +230,7 @@ void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tens
 
 void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const OT& wc, const OT& cov_all,
                    const Tensor& de_all, const Tensor& lens, const Tensor& dF, const Tensor& dv, const OT& dwc,
-                   int64_t D, int64_t B, int64_t T, int64_t A) {
+                   int64_t D, int64_t B, int64_t T, int64_t A, const OT& dlen) {
   chk(F, BF, "F"); chk(S_all, F32, "S_all"); chk(v, F32, "v"); chk(de_all, F32, "de_all"); chk(lens, I32, "lens");
   chk(dF, BF, "dF"); chk(dv, F32, "dv");
   TORCH_CHECK(A % 64 == 0, "bad A");
@@ -241,8 +242,10 @@ void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const 
               "dv: [nslot, A] with nslot a power of two");
   numel_eq(dF, B * T * A, "dF");
   chko(wc, F32, A, "wc"); chko(cov_all, F32, D * B * T, "cov_all"); chko(dwc, F32, nslot * A, "dwc");
+  chko(dlen, I32, B, "dlen");
   launch_attn_bwd_feat(P<bf16>(F), P<float>(S_all), P<float>(v), PO<float>(wc), PO<float>(cov_all), P<float>(de_all),
-                       P<int>(lens), P<bf16>(dF), P<float>(dv), PO<float>(dwc), D, B, T, A, (int)nslot, stream());
+                       P<int>(lens), P<bf16>(dF), P<float>(dv), PO<float>(dwc), D, B, T, A, (int)nslot, stream(),
+                       PO<int>(dlen));
 }
 
 int64_t attn_chunks(int64_t T) { return attn_nchunk(T); }

@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
     const bf16* __restrict__ F, const float* __restrict__ S_all, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov_all, const float* __restrict__ de_all,
     const int* __restrict__ lens, bf16* __restrict__ dF, float* __restrict__ dv, float* __restrict__ dwc,
-    int D, int B, int T, int A, int nslot) {
+    int D, int B, int T, int A, int nslot, const int* __restrict__ dlen) {
   __shared__ float pv[4][512];
   __shared__ float pw[4][512];
   const int b = blockIdx.y;
@@ -471,7 +471,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
         acc[q][jp] = f32x2{0.f, 0.f};
       }
     }
-    for (int t = 0; t < D; ++t) {
+    // steps past the row's last loss-weighted decoder step have de = 0 (dlen, nullable)
+    const int Dl = dlen ? min(D, dlen[b]) : D;
+    for (int t = 0; t < Dl; ++t) {
       const float* st = S_all + ((size_t)t * B + b) * A + k0;
       const float4 s0 = *reinterpret_cast<const float4*>(st);
       const float4 s1 = *reinterpret_cast<const float4*>(st + 4);
@@ -578,11 +580,11 @@ void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const fl
 }
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, bf16* dF, float* dv, float* dwc, int D, int B, int T,
-                          int A, int nslot, hipStream_t st) {
+                          int A, int nslot, hipStream_t st, const int* dlen) {
   // 4 positions per wave capped at 128 VGPRs = 4 waves/SIMD (a few prologue spills): 1.51 ms
   // vs 1.64 ms uncapped at 3 waves/SIMD and 1.65 ms with 2 positions per wave (B = 256,
   // T = 400, D = 100)
   dim3 grid((T + 15) / 16, B, (A + 511) / 512);
   hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 4>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
-                     dv, dwc, D, B, T, A, nslot);
+                     dv, dwc, D, B, T, A, nslot, dlen);
 }

@@ -400,7 +400,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
     const bf16* __restrict__ F, const bf16* __restrict__ G, const float* __restrict__ s,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
     const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
-    float* __restrict__ covloss, float* __restrict__ gx, bf16* __restrict__ gx_bf, int T) {
+    float* __restrict__ covloss, float* __restrict__ gx, bf16* __restrict__ gx_bf, int T,
+    const int* __restrict__ dlen, int step) {
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float es[kRowMaxT];
   __shared__ float part[NW][4][kEG];
@@ -409,6 +410,20 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
+  if (dlen && step >= dlen[b]) {
+    // a step past the row's last loss-weighted decoder step (block-uniform exit): nothing it
+    // computes reaches the loss, so write zeros (a, g, coverage loss) and carry the coverage
+    for (int i = tid; i < T; i += NT) {
+      a_out[rb + i] = 0.f;
+      if (cov_out) cov_out[rb + i] = cov ? cov[rb + i] : 0.f;
+    }
+    for (int k = tid; k < kEG; k += NT) {
+      gx[(size_t)b * kEG + k] = 0.f;
+      gx_bf[(size_t)b * kEG + k] = f2bf(0.f);
+    }
+    if (covloss && tid == 0) covloss[b] = 0.f;
+    return;
+  }
   const bf16* Fb = F + (size_t)b * T * A;
   const bf16* Gb = G + (size_t)b * T * kEG + (lane & 15) * 8;
   const int ngrp = (len + 3) >> 2;
@@ -536,7 +551,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     const float* __restrict__ a, const float* __restrict__ dx, const float* __restrict__ gv,
     const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
     const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
-    float* __restrict__ dcov_out, int T) {
+    float* __restrict__ dcov_out, int T, const int* __restrict__ dlen, int step) {
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float part[NW][A];
   __shared__ float red[NW];
@@ -545,6 +560,15 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
+  if (dlen && step >= dlen[b]) {
+    // past the row's last loss-weighted step every gradient is exactly zero (block-uniform exit)
+    for (int i = tid; i < T; i += NT) {
+      de_out[rb + i] = 0.f;
+      if (dcov_out) dcov_out[rb + i] = 0.f;
+    }
+    for (int k = tid; k < A; k += NT) ds[(size_t)b * A + k] = 0.f;
+    return;
+  }
   const float g = gcl ? gcl[b] : 0.f;
   const bf16* Gb = G + (size_t)b * T * kEG + (lane & 15) * 8;
   const bf16* Fb = F + (size_t)b * T * A;
@@ -688,11 +712,11 @@ bool attn_rowp_supported(int A, int T, int EG) { return attn_row_supported(A, T)
 
 void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const float* v, const float* wc,
                           const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* gx,
-                          bf16* gx_bf, int B, int T, int A, hipStream_t st) {
+                          bf16* gx_bf, int B, int T, int A, const int* dlen, int step, hipStream_t st) {
 #define LF(NK)                                                                                            \
   hipLaunchKernelGGL((attn_fwd_rowp_kernel<NK, row_waves<NK, false>()>), dim3(B),                        \
                      dim3(row_waves<NK, false>() * 64), 0, st, F, G, s, v, wc, cov, lens, a_out, cov_out, covloss, \
-                     gx, gx_bf, T)
+                     gx, gx_bf, T, dlen, step)
   if (A == 512) LF(1);
   else LF(2);
 #undef LF
@@ -701,11 +725,11 @@ void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const fl
 void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                          float* dcov_out, int B, int T, int A, hipStream_t st) {
+                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st) {
 #define LB(NK)                                                                                            \
   hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, row_waves<NK, true>()>), dim3(B),                         \
                      dim3(row_waves<NK, true>() * 64), 0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, \
-                     lens, de_out, ds, dcov_out, T)
+                     lens, de_out, ds, dcov_out, T, dlen, step)
   if (A == 512) LB(1);
   else LB(2);
 #undef LB

@@ -21,7 +21,7 @@ void launch_attn_bwd_step(const bf16* E, const bf16* F, const float* s, const fl
                           float* dcov_out, int B, int T, int A, hipStream_t st);
 void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, const float* wc, const float* cov_all,
                           const float* de_all, const int* lens, bf16* dF, float* dv, float* dwc, int D, int B, int T,
-                          int A, int nslot, hipStream_t st);
+                          int A, int nslot, hipStream_t st, const int* dlen = nullptr);
 
 bool attn_row_supported(int A, int T);
 void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
@@ -36,11 +36,11 @@ void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const flo
 bool attn_rowp_supported(int A, int T, int EG);
 void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const float* v, const float* wc,
                           const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* gx,
-                          bf16* gx_bf, int B, int T, int A, hipStream_t st);
+                          bf16* gx_bf, int B, int T, int A, const int* dlen, int step, hipStream_t st);
 void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                          float* dcov_out, int B, int T, int A, hipStream_t st);
+                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st);
 
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st);

@@ -146,7 +146,7 @@ def test_attn_fwd_rowp_matches_fp32(A):
     a, cov_out, cl = (torch.full((B, T), float("nan"), device=dev), torch.zeros(B, T, device=dev),
                       torch.zeros(B, device=dev))
     gx, gxb = torch.zeros(B, EG, device=dev), torch.zeros(B, EG, device=dev, dtype=torch.bfloat16)
-    k.attn_fwd_rowp(F, G, s, v, wc, cov, lens, a, cov_out, cl, gx, gxb, B, T, A)
+    k.attn_fwd_rowp(F, G, s, v, wc, cov, lens, a, cov_out, cl, gx, gxb, B, T, A, None, 0)
     torch.cuda.synchronize()
     e = torch.einsum("bta,a->bt", torch.tanh(F.float() + s[:, None, :] + wc[None, None, :] * cov[:, :, None]), v)
     a_ref = torch.softmax(e.masked_fill(~mask, float("-inf")), -1)
@@ -184,7 +184,7 @@ def test_attn_bwd_rowp_matches_fp32(A, last):
     g = torch.full((B,), 0.7, device=dev)
     de, dcov = torch.full((B, T), float("nan"), device=dev), torch.full((B, T), float("nan"), device=dev)
     ds = torch.full((B, A), float("nan"), device=dev)
-    k.attn_bwd_rowp(G, F, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A)
+    k.attn_bwd_rowp(G, F, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, None, 0)
     torch.cuda.synchronize()
     # the E-form reference with "E" = G and "dctx" = dx (zero at the last step)
     want = _reference(G, F, s, v, wc, cov, a, torch.zeros(B, EG, device=dev) if last else dx, Ga, dnext, g, lens)

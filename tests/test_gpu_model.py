@@ -159,6 +159,7 @@ def test_projected_context_matches_enc_out_path(monkeypatch, coverage, pointer_g
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
     hps, vocab, batch, params = _setup(coverage, pointer_gen, B=B, T=T, D=6, H=H, E=128)
     monkeypatch.setenv("TSAMD_ROW_ATTN", "1")
+    monkeypatch.setenv("TSAMD_SKIP_PAD_STEPS", "0")  # every step computed: whole-tensor comparison
     got = []
     for flag in ("0", "1"):
         monkeypatch.setenv("TSAMD_PROJ_ATTN", flag)
@@ -182,6 +183,35 @@ def test_projected_context_matches_enc_out_path(monkeypatch, coverage, pointer_g
         o, c = params.offsets[n]
         r = _rel(g1[o:o + c], g0[o:o + c])
         assert r < 3e-2 or (float(g0[o:o + c].norm()) < 1e-5 and r < 0.2), (n, r)
+
+
+@pytest.mark.parametrize("coverage,pointer_gen", [(True, True), (False, False)])
+def test_skip_pad_steps_same_loss_and_gradients(monkeypatch, coverage, pointer_gen):
+    """Skipping (row, step) pairs past a row's last loss-weighted decoder step (the projected
+    attention kernels exit, attn_bwd_feat stops at the row's length) leaves the loss, every
+    parameter gradient and the live steps' attention unchanged.  D = 40 decoder steps with
+    summaries of ~15-30 tokens: most rows have dead steps, some rows none."""
+    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
+    hps, vocab, batch, params = _setup(coverage, pointer_gen, B=24, T=120, D=40, H=256, E=128)
+    monkeypatch.setenv("TSAMD_ROW_ATTN", "1")
+    got = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("TSAMD_SKIP_PAD_STEPS", flag)
+        params.enable_grad()
+        eng = HipPointerGenerator(hps, vocab.size(), params, B=hps.batch_size, T=hps.max_enc_steps)
+        assert eng.proj_attn and eng.skip_pad == (flag == "1")
+        eng.set_batch(batch)
+        out = eng.forward(need_grad=True)
+        eng.backward()
+        torch.cuda.synchronize()
+        got.append((out["total_loss"].detach().clone(), params.grad.clone(), eng.w["ATT"].clone()))
+    dlen = eng.w["dlen"].long()
+    live = torch.arange(eng.D, device="cuda")[:, None] < dlen[None, :]
+    assert int((dlen < eng.D).sum()) > 0 and int((dlen == 0).sum()) == 0
+    assert _rel(got[1][0], got[0][0]) < 1e-6
+    assert _rel(got[1][1], got[0][1]) < 1e-5, _rel(got[1][1], got[0][1])
+    assert _rel(got[1][2][live], got[0][2][live]) < 1e-6
+    assert float(got[1][2][~live].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("layers,H", [(1, 256), (2, 128)])

@@ -14,6 +14,7 @@ engine is built); code can also pass a config explicitly.
 | TSAMD_FUSED_VOCAB_TRAIN   | fused_vocab_train  | 1: training vocab head with the logits only in MFMA accumulators; 0: library GEMM + ptr_loss |
 | TSAMD_FUSED_VOCAB         | fused_vocab_decode | 1: decode vocab head + top-k fused; 0: GEMM + final_topk |
 | TSAMD_PROJ_ATTN           | proj_attn          | 1: training row attention streams G = enc_out . W_in[E:] (emb_dim wide) instead of enc_out; 0: enc_out |
+| TSAMD_SKIP_PAD_STEPS      | skip_pad_steps     | 1: the projected-context attention kernels skip (row, step) pairs past the row's last loss-weighted decoder step; 0: compute them |
 | TSAMD_DEC_ROW_ATTN        | decode_row_attn    | 1: beam-decode attention through the row kernel; 0: score + softmax kernels |
 | TSAMD_DEFER_WGRAD         | defer_wgrad        | 1: decoder-side weight gradients beside the encoder BPTT (B >= 256); 0: inline |
 | TSAMD_DETERMINISTIC       | deterministic      | 0; 1: fixed-order reductions instead of fp32 atomics (bit-reproducible steps) |
@@ -45,6 +46,7 @@ class EngineConfig:
     fused_vocab_train: bool = True
     fused_vocab_decode: bool = True
     proj_attn: bool = True
+    skip_pad_steps: bool = True
     decode_row_attn: bool = True
     defer_wgrad: bool = True
     deterministic: bool = False
@@ -60,6 +62,7 @@ class EngineConfig:
             fused_vocab_train=_flag(env, "TSAMD_FUSED_VOCAB_TRAIN", True),
             fused_vocab_decode=_flag(env, "TSAMD_FUSED_VOCAB", True),
             proj_attn=_flag(env, "TSAMD_PROJ_ATTN", True),
+            skip_pad_steps=_flag(env, "TSAMD_SKIP_PAD_STEPS", True),
             decode_row_attn=_flag(env, "TSAMD_DEC_ROW_ATTN", True),
             defer_wgrad=_flag(env, "TSAMD_DEFER_WGRAD", True),
             deterministic=_flag(env, "TSAMD_DETERMINISTIC", False),

@@ -114,6 +114,11 @@ def host_inputs(batch, hps, D: int) -> Dict[str, np.ndarray]:
     gcl = hps.cov_loss_wt * dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
     dec_t = np.ascontiguousarray(batch.dec_batch[:, :D].T).astype(np.int64)
     sid, perm = emb_sort(batch.enc_batch, dec_t)
+    # live decoder steps per row: 1 + the last step with a nonzero loss weight (0: none).  Steps
+    # past it reach only masked loss terms (model.py:252-268), so their forward values and
+    # gradients need not be computed (EngineConfig.skip_pad_steps)
+    live = (rowg != 0) | (gcl != 0)  # [B, D]
+    dlen = np.where(live.any(1), D - np.argmax(live[:, ::-1], 1), 0)
     return {
         "enc_batch": batch.enc_batch.astype(np.int64),
         "enc_lens": batch.enc_lens.astype(np.int32),
@@ -125,6 +130,7 @@ def host_inputs(batch, hps, D: int) -> Dict[str, np.ndarray]:
         "gcl": np.ascontiguousarray(gcl.T).astype(np.float32),
         "emb_sid": sid,
         "emb_perm": perm,
+        "dlen": dlen.astype(np.int32),
     }
 
 
@@ -159,7 +165,7 @@ def input_layout(B: int, T: int, D: int):
                          ("rev_idx", "BT", torch.long), ("ext", "BT", torch.int32),
                          ("dec_batch_t", "DB", torch.long), ("target_t", "DB", torch.int32),
                          ("rowg", "DB", F32), ("gcl", "DB", F32),
-                         ("emb_sid", "R", torch.int32), ("emb_perm", "R", torch.int32)):
+                         ("emb_sid", "R", torch.int32), ("emb_perm", "R", torch.int32), ("dlen", "B", torch.int32)):
         shp = shapes[sk]
         nb = int(np.prod(shp)) * np.dtype(_NP[dt]).itemsize
         layout.append((name, off, shp, dt, nb))
@@ -327,6 +333,9 @@ class HipPointerGenerator:
             w["GVb"] = z(D, B, E, dt=BF)
             w["bd_tmp"] = z(B * D * max(A, T))  # [B, D, A] ctx / [B, D, T] da_dir GEMM outputs
             w["DXb"] = z(D, B, E, dt=BF)
+        # (row, step) pairs past the row's last loss-weighted step are skipped by the projected
+        # kernels (their outputs are written as zeros; loss and gradients are unchanged)
+        self.skip_pad = self.proj_attn and cfg.skip_pad_steps
         w["F"] = z(B, T, A, dt=BF)
         # transposed copy for the lanes-over-positions score kernel (not needed by the row
         # kernels; the beam decoder sets keep_ft to get it from _encoder_forward)
@@ -655,6 +664,7 @@ class HipPointerGenerator:
         cov = hps.coverage
         enc_out, lens, F, G = self.enc[-1]["out"], w["enc_lens"], w["F"], w["Genc"]
         v, wc = self.f32["v"], self.f32["wc"]
+        dlen = w["dlen"] if self.skip_pad else None
 
         def chain(r0, r1):
             Bg, rs = r1 - r0, slice(r0, r1)
@@ -666,7 +676,8 @@ class HipPointerGenerator:
                             H, A)
                 k.attn_fwd_rowp(F[rs], G[rs], w["S"][t][rs], v, wc, w["COV"][t][rs] if (cov and t > 0) else None,
                                 lens[rs], w["ATT"][t][rs], w["COV"][t + 1][rs] if cov else None,
-                                w["covloss"][t][rs] if cov else None, w["GV"][t][rs], w["GVb"][t][rs], Bg, T, A)
+                                w["covloss"][t][rs] if cov else None, w["GV"][t][rs], w["GVb"][t][rs], Bg, T, A,
+                                dlen[rs] if dlen is not None else None, t)
 
         self._row_groups(chain)
         w["X"][0].copy_(w["xe"][0])
@@ -916,6 +927,7 @@ class HipPointerGenerator:
         w["dc_carry"].zero_()
         dcov = w["dcov"]
         Kc = self.pk["Wbig"][:E + H]  # W_cell: [dx | dh] = dz . W_cell^T
+        dlen = w["dlen"] if self.skip_pad else None
 
         def chain(r0, r1):
             Bg, rs = r1 - r0, slice(r0, r1)
@@ -924,7 +936,7 @@ class HipPointerGenerator:
                                 w["ATT"][t][rs], w["DX"][t + 1][rs] if t < D - 1 else None, w["GV"][t][rs],
                                 Ga[t][rs], dcov[(t + 1) % 2][rs] if (cov and t < D - 1) else None,
                                 w["gcl"][t][rs] if cov else None, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
-                                dcov[t % 2][rs] if cov else None, Bg, T, A)
+                                dcov[t % 2][rs] if cov else None, Bg, T, A, dlen[rs] if dlen is not None else None, t)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
                                w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A)
@@ -976,7 +988,7 @@ class HipPointerGenerator:
         w["dv"].zero_()
         w["dwc"].zero_()
         k.attn_bwd_feat(F, w["S"], v, wc, w["COV"][:D] if cov else None, w["DE"], lens, w["dF"], w["dv"],
-                        w["dwc"] if cov else None, D, B, T, A)
+                        w["dwc"] if cov else None, D, B, T, A, w["dlen"] if self.skip_pad else None)
         g(VATT).copy_(w["dv"].sum(0).view_as(g(VATT)))
         if cov:
             g(WCOV).view(A).copy_(w["dwc"].sum(0))

@@ -73,7 +73,7 @@ def main():
                                                           w["DCTX"][t], w["CTX"][t], w["dA"][t], dcov[1], w["gcl"][t],
                                                           lens, w["DE"][t], w["DS"][t], dcov[0], B, T, A))
     res["attn_bwd_feat"] = timeit(lambda: k.attn_bwd_feat(F, w["S"], v, wc, w["COV"][:D], w["DE"], lens, w["dF"],
-                                                          w["dv"], w["dwc"], D, B, T, A), it=5)
+                                                          w["dv"], w["dwc"], D, B, T, A, None), it=5)
     # d out = dlogits . W^T (K = V): library GEMM vs split-K batched GEMM
     dl, ow = w["dlogits"], eng.pk["ow"]
     N = D * B

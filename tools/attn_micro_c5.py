@@ -77,7 +77,7 @@ def main():
         dF = torch.empty(MB, T, A, device=dev, dtype=torch.bfloat16)
         dv, dwc = torch.zeros(64, A, device=dev), torch.zeros(64, A, device=dev)
         res["bwd_feat_ms"] = round(timeit(lambda i: k.attn_bwd_feat(F[i], S_all, v, wc, cov_all, de_all, lens, dF, dv,
-                                                                     dwc, D, MB, T, A), NG, it=3) / 1e3, 3)
+                                                                     dwc, D, MB, T, A, None), NG, it=3) / 1e3, 3)
     for key in ("sum_FE", "fwd_row", "bwd_row", "bwd_step"):
         if key in res:
             res[key + "_GBs"] = bw(res[key])
