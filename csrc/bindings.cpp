@@ -375,51 +375,54 @@ void emb_grad(const Tensor& gemb, const Tensor& ids0, const Tensor& src0, const 
 // ---------------------------------------------------------------- decoder cell
 void dec_cell_fwd(const Tensor& XG, const OT& ctxp, const Tensor& hprev, const Tensor& cprev, const Tensor& WcT,
                   const Tensor& c_out, const Tensor& cb_out, const Tensor& hb_out, const Tensor& act, int64_t B,
-                  int64_t H, int64_t A) {
+                  int64_t H, int64_t A, const OT& dlen, int64_t step) {
   chk(XG, F32, "XG"); chk(hprev, BF, "hprev"); chk(cprev, F32, "cprev"); chk(WcT, BF, "WcT"); chk(c_out, F32, "c_out");
   chk(cb_out, BF, "cb_out"); chk(hb_out, BF, "hb_out"); chk(act, F32, "act");
   TORCH_CHECK(H % 32 == 0 && A % 32 == 0, "dims must be multiples of 32");
   numel_eq(XG, B * 4 * H, "XG"); chko(ctxp, BF, B * A, "ctxp"); numel_eq(hprev, B * H, "hprev");
   numel_eq(cprev, B * H, "cprev"); numel_eq(WcT, 4 * H * (A + H), "WcT"); numel_eq(c_out, B * H, "c_out");
   numel_eq(cb_out, B * H, "cb_out"); numel_eq(hb_out, B * H, "hb_out"); numel_eq(act, B * 4 * H, "act");
+  chko(dlen, I32, B, "dlen");
   launch_dec_cell_fwd(P<float>(XG), PO<bf16>(ctxp), P<bf16>(hprev), P<float>(cprev), P<bf16>(WcT), P<float>(c_out),
-                      P<bf16>(cb_out), P<bf16>(hb_out), P<float>(act), B, H, A, stream());
+                      P<bf16>(cb_out), P<bf16>(hb_out), P<float>(act), B, H, A, PO<int>(dlen), (int)step, stream());
 }
 
 void dec_sproj(const Tensor& cb, const Tensor& hb, const Tensor& WsT, const Tensor& bs, const Tensor& s_out, int64_t B,
-               int64_t H, int64_t A) {
+               int64_t H, int64_t A, const OT& dlen, int64_t step) {
   chk(cb, BF, "cb"); chk(hb, BF, "hb"); chk(WsT, BF, "WsT"); chk(bs, F32, "bs"); chk(s_out, F32, "s_out");
   TORCH_CHECK(H % 32 == 0 && A % 16 == 0, "bad dims");
   numel_eq(cb, B * H, "cb"); numel_eq(hb, B * H, "hb"); numel_eq(WsT, A * 2 * H, "WsT"); numel_eq(bs, A, "bs");
-  numel_eq(s_out, B * A, "s_out");
-  launch_dec_sproj(P<bf16>(cb), P<bf16>(hb), P<bf16>(WsT), P<float>(bs), P<float>(s_out), B, H, A, stream());
+  numel_eq(s_out, B * A, "s_out"); chko(dlen, I32, B, "dlen");
+  launch_dec_sproj(P<bf16>(cb), P<bf16>(hb), P<bf16>(WsT), P<float>(bs), P<float>(s_out), B, H, A, PO<int>(dlen),
+                   (int)step, stream());
 }
 
 void dec_bwd_cell(const Tensor& ds, const Tensor& Ws, const OT& dC_dir, const OT& dH_dir, const Tensor& dh_rec,
                   const Tensor& dc_carry, const Tensor& act, const Tensor& c_now, const Tensor& c_prev,
-                  const Tensor& dz, int64_t B, int64_t H, int64_t A) {
+                  const Tensor& dz, int64_t B, int64_t H, int64_t A, const OT& dlen, int64_t step) {
   chk(ds, F32, "ds"); chk(Ws, BF, "Ws"); chk(dh_rec, F32, "dh_rec"); chk(dc_carry, F32, "dc_carry");
   chk(act, F32, "act"); chk(c_now, F32, "c_now"); chk(c_prev, F32, "c_prev"); chk(dz, BF, "dz");
   TORCH_CHECK(H % 16 == 0 && A % 32 == 0, "bad dims");
   numel_eq(ds, B * A, "ds"); numel_eq(Ws, 2 * H * A, "Ws"); chko(dC_dir, F32, B * H, "dC_dir");
   chko(dH_dir, F32, B * H, "dH_dir"); numel_eq(dh_rec, B * H, "dh_rec"); numel_eq(dc_carry, B * H, "dc_carry");
   numel_eq(act, B * 4 * H, "act"); numel_eq(c_now, B * H, "c_now"); numel_eq(c_prev, B * H, "c_prev");
-  numel_eq(dz, B * 4 * H, "dz");
+  numel_eq(dz, B * 4 * H, "dz"); chko(dlen, I32, B, "dlen");
   launch_dec_bwd_cell(P<float>(ds), P<bf16>(Ws), PO<float>(dC_dir), PO<float>(dH_dir), P<float>(dh_rec),
                       P<float>(dc_carry), P<float>(act), P<float>(c_now), P<float>(c_prev), P<bf16>(dz), B, H, A,
-                      stream());
+                      PO<int>(dlen), (int)step, stream());
 }
 
 void dec_bwd_dz(const Tensor& dz, const Tensor& Wbig, const OT& dX_dir, const OT& dCTX_dir_prev, const Tensor& dx_out,
-                const OT& dctx_prev_out, const Tensor& dh_rec, int64_t B, int64_t E, int64_t H, int64_t A) {
+                const OT& dctx_prev_out, const Tensor& dh_rec, int64_t B, int64_t E, int64_t H, int64_t A,
+                const OT& dlen, int64_t step) {
   chk(dz, BF, "dz"); chk(Wbig, BF, "Wbig"); chk(dx_out, F32, "dx_out"); chk(dh_rec, F32, "dh_rec");
   TORCH_CHECK(E % 16 == 0 && H % 32 == 0 && A % 16 == 0, "bad dims");
   numel_eq(dz, B * 4 * H, "dz"); numel_eq(Wbig, (E + H + A) * 4 * H, "Wbig");
   chko(dX_dir, F32, B * E, "dX_dir"); chko(dCTX_dir_prev, F32, B * A, "dCTX_dir_prev");
   numel_eq(dx_out, B * E, "dx_out"); chko(dctx_prev_out, F32, B * A, "dctx_prev_out");
-  numel_eq(dh_rec, B * H, "dh_rec");
+  numel_eq(dh_rec, B * H, "dh_rec"); chko(dlen, I32, B, "dlen");
   launch_dec_bwd_dz(P<bf16>(dz), P<bf16>(Wbig), PO<float>(dX_dir), PO<float>(dCTX_dir_prev), P<float>(dx_out),
-                    PO<float>(dctx_prev_out), P<float>(dh_rec), B, E, H, A, stream());
+                    PO<float>(dctx_prev_out), P<float>(dh_rec), B, E, H, A, PO<int>(dlen), (int)step, stream());
 }
 
 // ---------------------------------------------------------------- loss / optimizer

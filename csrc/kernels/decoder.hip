@@ -49,6 +49,15 @@ struct BeamGather {
   int* step;            // decode-step counter (nullable)
 };
 
+// Training: a 16-row tile whose rows are all past their last loss-weighted decoder step
+// (step >= dlen[r], EngineConfig.skip_pad_steps) has nothing to compute.  Every wave of the
+// block votes on the same 16 rows, so the result is block-uniform (safe before barriers).
+__device__ __forceinline__ bool tile_dead(const int* dlen, int step, int r0, int B) {
+  if (!dlen) return false;
+  const int r = min(r0 + (int)(threadIdx.x & 15), B - 1);
+  return __all(step >= dlen[r]);
+}
+
 __device__ __forceinline__ int bg_tok(const BeamGather& bg, int r) {
   const int t = (int)DCHECK_IDX(bg.latest[r], 0, 0x7fffffff, CHK_BEAM_TOKEN);
   return t < bg.V ? t : bg.unk;
@@ -63,7 +72,7 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
     const bf16* __restrict__ WcT,      // [4H][A+H]
     float* __restrict__ c_out, bf16* __restrict__ cb_out, bf16* __restrict__ hb_out,  // [B][H]
     float* __restrict__ act,           // [B][4H] (nullable)
-    int B, int H, int A, BeamGather bg) {
+    int B, int H, int A, BeamGather bg, const int* __restrict__ dlen, int step) {
   __shared__ float red[4 * 4 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (bg.step && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *bg.step += 1;
@@ -74,6 +83,18 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
   const int r = r0 + (lane >> 4) * 4 + wid, u = u0 + (lane & 15);
   const bool rok = r < B;
   const size_t ri = (size_t)(rok ? r : 0) * H + u;
+  if (tile_dead(dlen, step, r0, B)) {  // finite zeros: the head reads every row's state
+    if (rok) {
+      c_out[ri] = 0.f;
+      cb_out[ri] = f2bf(0.f);
+      hb_out[ri] = f2bf(0.f);
+      if (act) {
+        float* a4 = act + (size_t)r * G;
+        a4[u] = 0.f; a4[H + u] = 0.f; a4[2 * H + u] = 0.f; a4[3 * H + u] = 0.f;
+      }
+    }
+    return;
+  }
   // parent row of r (gather mode) for the previous state
   const int rp = bg.gidx ? (int)DCHECK_IDX(bg.gidx[rok ? r : 0], 0, B, CHK_BEAM_PARENT) : (rok ? r : 0);
   float xg[4], cp;
@@ -125,9 +146,11 @@ struct L2Args {
   const bf16* a1; int K1; const bf16* a2; int K2; const bf16* Wt;
   const float* bias; const float* add; float* out; bf16* outb; int N;
   const int* ga = nullptr; const int* gtok = nullptr; int V = 0, unk = 0;
+  const int* dlen = nullptr; int step = 0;  // training: skip tiles of rows past their last live step
 };
 
 __device__ __forceinline__ void linear2_body(const L2Args& p, int B, int n0, int r0, float* red) {
+  if (tile_dead(p.dlen, p.step, r0, B)) return;  // (nothing reads a dead row's s)
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ar0 = min(r0 + (lane & 15), B - 1);
   const int ar = p.ga ? (int)DCHECK_IDX(p.ga[ar0], 0, B, CHK_BEAM_PARENT) : ar0;
@@ -259,7 +282,7 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
     const float* __restrict__ dC_dir, const float* __restrict__ dH_dir,       // [B][H] (nullable)
     const float* __restrict__ dh_rec, float* __restrict__ dc_carry,            // [B][H]
     const float* __restrict__ act, const float* __restrict__ c_now, const float* __restrict__ c_prev,
-    bf16* __restrict__ dz, int B, int H, int A) {
+    bf16* __restrict__ dz, int B, int H, int A, const int* __restrict__ dlen, int step) {
   __shared__ float red[4 * 2 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int tx, ty;
@@ -267,6 +290,13 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
   const int u0 = tx * 16, r0 = ty * 16;
   const int r = r0 + (lane >> 4) * 4 + wid, u = u0 + (lane & 15);
   const bool rok = r < B;
+  if (tile_dead(dlen, step, r0, B)) {  // dz = 0 (read by the weight-gradient GEMMs); dc_carry stays 0
+    if (rok) {
+      bf16* dzr = dz + (size_t)r * 4 * H;
+      dzr[u] = f2bf(0.f); dzr[H + u] = f2bf(0.f); dzr[2 * H + u] = f2bf(0.f); dzr[3 * H + u] = f2bf(0.f);
+    }
+    return;
+  }
   const size_t ri = (size_t)(rok ? r : 0) * H + u;
   float dh0, dc0, a4[4], cn, cpv;
   {
@@ -314,13 +344,22 @@ __global__ __launch_bounds__(256) void dec_bwd_dz_kernel(
     const float* __restrict__ dCTX_dir_prev, // [B][A] nullable (already includes dX_dir[t].W_in[E:]^T)
     float* __restrict__ dx_out,              // [B][E]
     float* __restrict__ dctx_prev_out,       // [B][A] nullable (t == 0)
-    float* __restrict__ dh_rec, int B, int E, int H, int A) {
+    float* __restrict__ dh_rec, int B, int E, int H, int A, const int* __restrict__ dlen, int step) {
   __shared__ float red[4 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int tx, ty;
   xcd_tile(tx, ty);
   const int n0 = tx * 16, r0 = ty * 16;
   if (n0 >= E + H && !dctx_prev_out) return;  // uniform per block
+  if (tile_dead(dlen, step, r0, B)) {  // every output is an exact zero past the last live step
+    const int r = r0 + (lane >> 4) * 4 + wid, n = n0 + (lane & 15);
+    if (r < B) {
+      if (n < E) dx_out[(size_t)r * E + n] = 0.f;
+      else if (n < E + H) dh_rec[(size_t)r * H + n - E] = 0.f;
+      else dctx_prev_out[(size_t)r * A + n - E - H] = 0.f;
+    }
+    return;
+  }
   const int G = 4 * H;
   const int ar = min(r0 + (lane & 15), B - 1);
   const int kof = 8 * (lane >> 4);
@@ -348,17 +387,18 @@ __global__ __launch_bounds__(256) void dec_bwd_dz_kernel(
 // L2 round trip instead of two with 4-step batches), equal at hidden 512; B = 256 train
 // 19.71-19.77 -> 19.63-19.67 ms (profiles/r2/ab/dec_cell_kb.jsonl)
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
-                         float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st) {
+                         float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, const int* dlen,
+                         int step, hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16);
   hipLaunchKernelGGL(dec_cell_fwd_kernel<6>, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out,
-                     hb_out, act, B, H, A, BeamGather{nullptr, nullptr, nullptr, 0, 0, nullptr});
+                     hb_out, act, B, H, A, BeamGather{nullptr, nullptr, nullptr, 0, 0, nullptr}, dlen, step);
 }
 void launch_dec_cell_fwd_beam(const int* gidx, const int* latest, const float* XGtab, const bf16* ctxp,
                               const bf16* hprev, const float* cprev, const bf16* WcT, float* c_out, bf16* cb_out,
                               bf16* hb_out, int* step, int B, int H, int A, int V, int unk, hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16);
   hipLaunchKernelGGL(dec_cell_fwd_kernel<6>, grid, dim3(256), 0, st, nullptr, ctxp, hprev, cprev, WcT, c_out, cb_out,
-                     hb_out, nullptr, B, H, A, BeamGather{gidx, latest, XGtab, V, unk, step});
+                     hb_out, nullptr, B, H, A, BeamGather{gidx, latest, XGtab, V, unk, step}, nullptr, 0);
 }
 // the beam-decode pair: s = [cb, hb] . WsT^T + bs, and x = Xtab[token] + ctx_parent . WicT^T
 void launch_beam_sproj_xmerge(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out,
@@ -390,8 +430,12 @@ void launch_linear2_pair(const bf16* a1, int K1, const bf16* a2, int K2, const b
   hipLaunchKernelGGL(linear2_pair_kernel, grid, dim3(256), 0, st, p0, p1, B);
 }
 void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out, int B, int H,
-                      int A, hipStream_t st) {
-  launch_linear2(cb, H, hb, H, WsT, bs, nullptr, s_out, nullptr, B, A, st);
+                      int A, const int* dlen, int step, hipStream_t st) {
+  dim3 grid(A / 16, (B + 15) / 16);
+  L2Args p{cb, H, hb, H, WsT, bs, nullptr, s_out, nullptr, A};
+  p.dlen = dlen;
+  p.step = step;
+  hipLaunchKernelGGL(linear2_kernel, grid, dim3(256), 0, st, p, B);
 }
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
                      int N, int A, int H, int E, bool det, hipStream_t st) {
@@ -412,17 +456,18 @@ void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x
 }
 void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,
-                         const float* c_prev, bf16* dz, int B, int H, int A, hipStream_t st) {
+                         const float* c_prev, bf16* dz, int B, int H, int A, const int* dlen, int step,
+                         hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16);
   hipLaunchKernelGGL(dec_bwd_cell_kernel, grid, dim3(256), 0, st, ds, Ws, dC_dir, dH_dir, dh_rec, dc_carry, act,
-                     c_now, c_prev, dz, B, H, A);
+                     c_now, c_prev, dz, B, H, A, dlen, step);
 }
 void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, const float* dCTX_dir_prev,
                        float* dx_out, float* dctx_prev_out, float* dh_rec, int B, int E, int H, int A,
-                       hipStream_t st) {
+                       const int* dlen, int step, hipStream_t st) {
   dim3 grid((E + H + A) / 16, (B + 15) / 16);
   // KB = 8 measured equal (5.68 vs 5.74 us at 128 rows, tools/dec_kernels_micro.py) at 96 instead
   // of 41 VGPRs, so this one keeps 4-step batches
   hipLaunchKernelGGL(dec_bwd_dz_kernel<4>, grid, dim3(256), 0, st, dz, Wbig, dX_dir, dCTX_dir_prev, dx_out,
-                     dctx_prev_out, dh_rec, B, E, H, A);
+                     dctx_prev_out, dh_rec, B, E, H, A, dlen, step);
 }

@@ -43,7 +43,8 @@ void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const fl
                           float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st);
 
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
-                         float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, hipStream_t st);
+                         float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, const int* dlen,
+                         int step, hipStream_t st);
 void launch_dec_cell_fwd_beam(const int* gidx, const int* latest, const float* XGtab, const bf16* ctxp,
                               const bf16* hprev, const float* cprev, const bf16* WcT, float* c_out, bf16* cb_out,
                               bf16* hb_out, int* step, int B, int H, int A, int V, int unk, hipStream_t st);
@@ -52,13 +53,14 @@ void launch_beam_sproj_xmerge(const bf16* cb, const bf16* hb, const bf16* WsT, c
                               const int* latest, float* x_out, int B, int H, int A, int E, int V, int unk,
                               hipStream_t st);
 void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out, int B, int H,
-                      int A, hipStream_t st);
+                      int A, const int* dlen, int step, hipStream_t st);
 void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,
-                         const float* c_prev, bf16* dz, int B, int H, int A, hipStream_t st);
+                         const float* c_prev, bf16* dz, int B, int H, int A, const int* dlen, int step,
+                         hipStream_t st);
 void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, const float* dCTX_dir_prev,
                        float* dx_out, float* dctx_prev_out, float* dh_rec, int B, int E, int H, int A,
-                       hipStream_t st);
+                       const int* dlen, int step, hipStream_t st);
 
 void launch_ptr_loss_bf16(const bf16* logits, const int* target, const float* rowg, const float* pgen,
                           const float* attn, const int* ext, const int* lens, float* loss_row, bf16* dlogits,

@@ -61,7 +61,8 @@ def test_pack_matches_engine_host_packing(tmp_path):
     exs = [Example(a, [s.strip() for s in abstract2sents(b)], vocab, hps)
            for a, b in binfmt.text_generator(binfmt.example_generator(pattern, True))]
     exs.sort(key=lambda e: e.enc_len)  # the worker's length bucketing
-    ref = pack_host_inputs(host_inputs(Batch(exs, hps, vocab, pad_enc_to=T), hps, D), input_layout(B, T, D)[0])
+    ref = pack_host_inputs(host_inputs(Batch(exs, hps, vocab, pad_enc_to=T), hps, D, sort_rows=True),
+                           input_layout(B, T, D)[0])
     assert bytes(pb.host_pack) == ref.tobytes()
 
 

@@ -103,7 +103,7 @@ def _worker(w: int, n: int, ring_name: str, data_path: str, vocab: Vocab, hps, s
             b = Batch(exs, hps, vocab, pad_enc_to=pad_enc_to)
             if b.enc_batch.shape != (B, T):
                 raise ValueError(f"batch shape {b.enc_batch.shape} != {(B, T)} (pad_enc_to must be max_enc_steps)")
-            buf = pack_host_inputs(host_inputs(b, hps, D), layout)
+            buf = pack_host_inputs(host_inputs(b, hps, D, sort_rows=True), layout)
             meta = json.dumps({"shape": [B, T], "tokens": b.num_tokens(), "padded": b.padded_tokens(),
                                "valid": int(b.valid.sum())}).encode()
             _push(ring, _HDR.pack(len(meta)) + meta + buf.tobytes())

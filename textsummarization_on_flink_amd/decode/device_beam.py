@@ -179,7 +179,7 @@ class DeviceBeamDecoder:
         R, T, H, A = self.R, self.T, eng.H, eng.A
         X = self.st[0]
         b["Cb2"].copy_(X["C"])
-        k.dec_sproj(b["Cb2"], X["H"], eng.pk["WsT"], self.p[ATT_B], b["s"], R, H, A)
+        k.dec_sproj(b["Cb2"], X["H"], eng.pk["WsT"], self.p[ATT_B], b["s"], R, H, A, None, 0)
         self._attention(None, X["ATT"], X["CTX"], X["CTXb"])
         X["COV"].zero_()
         b["gidx"].copy_(torch.arange(R, dtype=torch.int32, device=self.dev))
@@ -214,14 +214,14 @@ class DeviceBeamDecoder:
                       self.XGtab, self.Xtab, b["c"], b["h"], b["ctxs"], b["ctxs_bf"], Y["COV"] if cov else None,
                       b["XG"], b["x"], R, H, A, T, E, V, self.vocab.word2id(UNKNOWN_TOKEN), b["step"])
         k.dec_cell_fwd(b["XG"], b["ctxs_bf"], b["h"], b["c"], eng.pk["WcT2"], Y["C"], b["Cb2"], Y["H"], b["act"],
-                       R, H, A)
+                       R, H, A, None, 0)
         if hps.pointer_gen:
             # one launch: attention query s = [c, h] . W_s + b, and the x-merge for p_gen,
             # x = x0 + ctx*_{t-1} . W_in[E:] (x0 = emb . W_in[:E] + b_in gathered per token)
             k.linear2_pair(b["Cb2"], H, Y["H"], H, eng.pk["WsT"], p[ATT_B], None, b["s"], None, A,
                            b["ctxs_bf"], A, None, 0, eng.pk["WicT"], None, b["x"], b["x"], None, E, R)
         else:
-            k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
+            k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A, None, 0)
         self._attention(Y["COV"] if cov else None, Y["ATT"], Y["CTX"], b["ctx_bf"])
         pg = b["PG"] if hps.pointer_gen else None
         if hps.pointer_gen and not self.fused_vocab:
@@ -264,7 +264,7 @@ class DeviceBeamDecoder:
             k.beam_sproj_xmerge(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], X["CTXb"], eng.pk["WicT"],
                                 self.Xtab, b["gidx"], b["latest"], b["x"], R, H, A, E, V, unk)
         else:
-            k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A)
+            k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A, None, 0)
         k.attn_fwd_row_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], X["COV"] if cov else None,
                             X["ATT"] if cov else None, Y["COV"] if cov else None, b["gidx"], b["lens_att"], Y["ATT"],
                             Y["CTX"], Y["CTXb"], R, T, A, self.rep)

@@ -89,11 +89,16 @@ def mmf(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.mm(a, b, out_dtype=F32)
 
 
-def host_inputs(batch, hps, D: int) -> Dict[str, np.ndarray]:
+def host_inputs(batch, hps, D: int, sort_rows: bool = False) -> Dict[str, np.ndarray]:
     """The engine's per-batch inputs as host arrays (pure numpy: runs in loader worker
     processes too): token ids, lengths, the reversed-index map of the backward LSTM
     direction, extended-vocab ids, step-major decoder inputs / targets and the per-(step,
-    row) loss weights of the reference's loss averaging (``model.py:252-268``)."""
+    row) loss weights of the reference's loss averaging (``model.py:252-268``).
+
+    ``sort_rows``: the engine's rows are the batch's rows ordered by live decoder steps, longest
+    first (stable), so the steps a row skips past its summary form a suffix of the rows at every
+    decoder step and whole 16-row tiles of the decoder kernels go idle together.  The loss is a
+    sum over rows; ``row_src[b]`` is the batch row of engine row b."""
     T = batch.enc_batch.shape[1]
     lens = batch.enc_lens.astype(np.int64)
     if lens.min() < 1:
@@ -112,25 +117,29 @@ def host_inputs(batch, hps, D: int) -> Dict[str, np.ndarray]:
         wm = dm * valid[:, None]
         rowg = wm / wm.sum()
     gcl = hps.cov_loss_wt * dm * (valid / (np.maximum(dec_lens, 1) * nvalid))[:, None]
-    dec_t = np.ascontiguousarray(batch.dec_batch[:, :D].T).astype(np.int64)
-    sid, perm = emb_sort(batch.enc_batch, dec_t)
     # live decoder steps per row: 1 + the last step with a nonzero loss weight (0: none).  Steps
     # past it reach only masked loss terms (model.py:252-268), so their forward values and
     # gradients need not be computed (EngineConfig.skip_pad_steps)
     live = (rowg != 0) | (gcl != 0)  # [B, D]
     dlen = np.where(live.any(1), D - np.argmax(live[:, ::-1], 1), 0)
+    src = np.argsort(-dlen, kind="stable") if sort_rows else np.arange(len(dlen))
+    enc_batch, ext, rev = batch.enc_batch[src], batch.enc_batch_extend_vocab[src], rev[src]
+    enc_lens, rowg, gcl, dlen = batch.enc_lens[src], rowg[src], gcl[src], dlen[src]
+    dec_t = np.ascontiguousarray(batch.dec_batch[src, :D].T).astype(np.int64)
+    sid, perm = emb_sort(enc_batch, dec_t)
     return {
-        "enc_batch": batch.enc_batch.astype(np.int64),
-        "enc_lens": batch.enc_lens.astype(np.int32),
+        "enc_batch": enc_batch.astype(np.int64),
+        "enc_lens": enc_lens.astype(np.int32),
         "rev_idx": rev.astype(np.int64),
-        "ext": batch.enc_batch_extend_vocab.astype(np.int32),
+        "ext": ext.astype(np.int32),
         "dec_batch_t": dec_t,
-        "target_t": np.ascontiguousarray(batch.target_batch[:, :D].T).astype(np.int32),
+        "target_t": np.ascontiguousarray(batch.target_batch[src, :D].T).astype(np.int32),
         "rowg": np.ascontiguousarray(rowg.T).astype(np.float32),
         "gcl": np.ascontiguousarray(gcl.T).astype(np.float32),
         "emb_sid": sid,
         "emb_perm": perm,
         "dlen": dlen.astype(np.int32),
+        "row_src": src.astype(np.int32),
     }
 
 
@@ -165,7 +174,8 @@ def input_layout(B: int, T: int, D: int):
                          ("rev_idx", "BT", torch.long), ("ext", "BT", torch.int32),
                          ("dec_batch_t", "DB", torch.long), ("target_t", "DB", torch.int32),
                          ("rowg", "DB", F32), ("gcl", "DB", F32),
-                         ("emb_sid", "R", torch.int32), ("emb_perm", "R", torch.int32), ("dlen", "B", torch.int32)):
+                         ("emb_sid", "R", torch.int32), ("emb_perm", "R", torch.int32), ("dlen", "B", torch.int32),
+                         ("row_src", "B", torch.int32)):
         shp = shapes[sk]
         nb = int(np.prod(shp)) * np.dtype(_NP[dt]).itemsize
         layout.append((name, off, shp, dt, nb))
@@ -556,7 +566,7 @@ class HipPointerGenerator:
                 raise ValueError(f"host pack of {len(packed)} bytes, engine expects {hn.nbytes}")
             hn[:] = np.frombuffer(packed, dtype=np.uint8)
         else:
-            pack_host_inputs(host_inputs(batch, self.hps, self.D), self._in_layout, hn)
+            pack_host_inputs(host_inputs(batch, self.hps, self.D, sort_rows=self.skip_pad), self._in_layout, hn)
         cur = torch.cuda.current_stream()
         cs = self._copy_stream
         with torch.cuda.stream(cs):
@@ -634,10 +644,10 @@ class HipPointerGenerator:
             for t in range(D):
                 k.dec_cell_fwd(w["XG"][t][rs], w["CTXb"][t - 1][rs] if t > 0 else None, w["Hb"][t][rs],
                                w["Cst"][t][rs], self.pk["WcT2"], w["Cst"][t + 1][rs], w["Cb"][t + 1][rs],
-                               w["Hb"][t + 1][rs], w["ACT"][t][rs], Bg, H, A)
+                               w["Hb"][t + 1][rs], w["ACT"][t][rs], Bg, H, A, None, 0)
                 cov_in = w["COV"][t][rs] if (cov and t > 0) else None
                 k.dec_sproj(w["Cb"][t + 1][rs], w["Hb"][t + 1][rs], self.pk["WsT"], self.p[ATT_B], w["S"][t][rs], Bg,
-                            H, A)
+                            H, A, None, 0)
                 if self.row_attn:
                     k.attn_fwd_row(F[rs], enc_out[rs], w["S"][t][rs], v, wc, cov_in, lens[rs], w["ATT"][t][rs],
                                    w["COV"][t + 1][rs] if cov else None, w["covloss"][t][rs] if cov else None,
@@ -668,16 +678,17 @@ class HipPointerGenerator:
 
         def chain(r0, r1):
             Bg, rs = r1 - r0, slice(r0, r1)
+            dl = dlen[rs] if dlen is not None else None
             for t in range(D):
                 k.dec_cell_fwd(w["XG"][t][rs], w["GVb"][t - 1][rs] if t > 0 else None, w["Hb"][t][rs],
                                w["Cst"][t][rs], self.pk["KcT"], w["Cst"][t + 1][rs], w["Cb"][t + 1][rs],
-                               w["Hb"][t + 1][rs], w["ACT"][t][rs], Bg, H, E)
+                               w["Hb"][t + 1][rs], w["ACT"][t][rs], Bg, H, E, dl, t)
                 k.dec_sproj(w["Cb"][t + 1][rs], w["Hb"][t + 1][rs], self.pk["WsT"], self.p[ATT_B], w["S"][t][rs], Bg,
-                            H, A)
+                            H, A, dl, t)
                 k.attn_fwd_rowp(F[rs], G[rs], w["S"][t][rs], v, wc, w["COV"][t][rs] if (cov and t > 0) else None,
                                 lens[rs], w["ATT"][t][rs], w["COV"][t + 1][rs] if cov else None,
                                 w["covloss"][t][rs] if cov else None, w["GV"][t][rs], w["GVb"][t][rs], Bg, T, A,
-                                dlen[rs] if dlen is not None else None, t)
+                                dl, t)
 
         self._row_groups(chain)
         w["X"][0].copy_(w["xe"][0])
@@ -895,10 +906,10 @@ class HipPointerGenerator:
                                     dcov[t % 2][rs] if cov else None, Bg, T, A)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
-                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A)
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, None, 0)
                 k.dec_bwd_dz(w["DZ"][t][rs], self.pk["Wbig"], dX_dir[t][rs] if dX_dir is not None else None,
                              dCTX_dir[t - 1][rs] if t > 0 else None, w["DX"][t][rs],
-                             w["DCTX"][t - 1][rs] if t > 0 else None, w["dh_rec"][rs], Bg, E, H, A)
+                             w["DCTX"][t - 1][rs] if t > 0 else None, w["dh_rec"][rs], Bg, E, H, A, None, 0)
 
         self._row_groups(chain, self.split_bwd)
         self._backward_mid_rest(Hn, wg, run)
@@ -931,17 +942,18 @@ class HipPointerGenerator:
 
         def chain(r0, r1):
             Bg, rs = r1 - r0, slice(r0, r1)
+            dl = dlen[rs] if dlen is not None else None
             for t in reversed(range(D)):
                 k.attn_bwd_rowp(G[rs], F[rs], w["S"][t][rs], v, wc, w["COV"][t][rs] if (cov and t > 0) else None,
                                 w["ATT"][t][rs], w["DX"][t + 1][rs] if t < D - 1 else None, w["GV"][t][rs],
                                 Ga[t][rs], dcov[(t + 1) % 2][rs] if (cov and t < D - 1) else None,
                                 w["gcl"][t][rs] if cov else None, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
-                                dcov[t % 2][rs] if cov else None, Bg, T, A, dlen[rs] if dlen is not None else None, t)
+                                dcov[t % 2][rs] if cov else None, Bg, T, A, dl, t)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
-                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A)
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, dl, t)
                 k.dec_bwd_dz(w["DZ"][t][rs], Kc, dX_dir[t][rs] if dX_dir is not None else None, None,
-                             w["DX"][t][rs], None, w["dh_rec"][rs], Bg, E, H, 0)
+                             w["DX"][t][rs], None, w["dh_rec"][rs], Bg, E, H, 0, dl, t)
 
         self._row_groups(chain, self.split_bwd)
         w["DCTX"].copy_(dCTX_dir)

@@ -50,12 +50,12 @@ def main():
             dcc = r(B, H)
             res = {"H": H, "A": A, "rows": B,
                    "dec_cell_fwd_us": timed(lambda: k.dec_cell_fwd(XG, ctxp, hprev, cprev, WcT, c_out, cb, hb, act,
-                                                                   B, H, A)),
-                   "linear2_sproj_us": timed(lambda: k.dec_sproj(cb, hb, WsT, bs, s_out, B, H, A)),
-                   "dec_bwd_dz_us": timed(lambda: k.dec_bwd_dz(dz, Wbig, None, None, dx, dctx, dh, B, E, H, A))}
+                                                                   B, H, A, None, 0)),
+                   "linear2_sproj_us": timed(lambda: k.dec_sproj(cb, hb, WsT, bs, s_out, B, H, A, None, 0)),
+                   "dec_bwd_dz_us": timed(lambda: k.dec_bwd_dz(dz, Wbig, None, None, dx, dctx, dh, B, E, H, A, None, 0))}
             try:
                 res["dec_bwd_cell_us"] = timed(lambda: k.dec_bwd_cell(ds, Ws, None, dh, dh, dcc, act, c_out, cprev, dz,
-                                                                      B, H, A, None))
+                                                                      B, H, A, None, None, 0))
             except RuntimeError as e:  # noqa: BLE001
                 res["dec_bwd_cell_us"] = str(e)[:80]
             print(json.dumps(res), flush=True)
