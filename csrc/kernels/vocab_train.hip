@@ -114,7 +114,9 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     const float* __restrict__ alpha,  // [N]      pass 2
     bf16* __restrict__ dl,            // [N][V]   pass 2: dlogits
     float* __restrict__ dbias,        // [V]      pass 2 (nullable): += column sums of dlogits
-    int N, int V, int ldx) {
+    int N, int V, int ldx,
+    const int* __restrict__ dlen,     // [Bd]     nullable: row n = t Bd + b is live iff t < dlen[b]
+    int Bd) {
   constexpr int KS = H / 32;          // k-steps of 32
   constexpr int NI = vr_ni(H), VR_COLS = vr_cols(H);
   constexpr int XS = H + 8;           // padded LDS row (bank spread)
@@ -125,6 +127,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
   __shared__ float Pm[2][4][VR_ROWS], Ps[2][4][VR_ROWS];
   __shared__ int Tg[2][VR_ROWS];
   __shared__ float Ls[2][VR_ROWS], Al[2][VR_ROWS];
+  __shared__ int Lv[2][VR_ROWS];  // row live (a unit of 32 dead rows skips its MFMAs)
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int RB = (N + VR_ROWS - 1) / VR_ROWS, nt = (V + VR_COLS - 1) / VR_COLS;
   const long units = (long)RB * nt;
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     cacc = 0.f;
   };
   bf16x8 xr[CH];      // prefetched X chunks of the next unit
-  int tg_r = 0;
+  int tg_r = 0, lv_r = 1;
   float ls_r = 0.f, al_r = 0.f;
   auto fetch = [&](int u) {  // global -> registers (unit u's X rows, targets, row scalars)
     const int rb = (u % RB) * VR_ROWS;
@@ -162,6 +165,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     if (threadIdx.x < VR_ROWS) {
       const int row = min(rb + threadIdx.x, N - 1);
       tg_r = target[row];
+      lv_r = rb + (int)threadIdx.x < N && (!dlen || row / Bd < dlen[row % Bd]);
       if (GRAD) {
         ls_r = lse[row];
         al_r = alpha[row];
@@ -176,6 +180,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     }
     if (threadIdx.x < VR_ROWS) {
       Tg[buf][threadIdx.x] = tg_r;
+      Lv[buf][threadIdx.x] = lv_r;
       if (GRAD) {
         Ls[buf][threadIdx.x] = ls_r;
         Al[buf][threadIdx.x] = al_r;
@@ -216,20 +221,47 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
       cur_vt = vt;
     }
     if (u + 1 < u1) fetch(u + 1);
+    // 32 rows past their last loss-weighted decoder step (EngineConfig.skip_pad_steps): no MFMAs;
+    // pass 1 records an empty partial, pass 2 stores zero dlogits (block-uniform: LDS flags)
+    const bool live = __any(Lv[buf][c16] | Lv[buf][16 + c16]);
     f32x4 acc[NI][RJ];
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < RJ; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+    if (live) {
 #pragma unroll
-    for (int h = 0; h < KS; ++h)
+      for (int h = 0; h < KS; ++h)
 #pragma unroll
-      for (int j = 0; j < RJ; ++j) {
-        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&Xs[buf][(16 * j + c16) * XS + 32 * h + kof]);
+        for (int j = 0; j < RJ; ++j) {
+          const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&Xs[buf][(16 * j + c16) * XS + 32 * h + kof]);
 #pragma unroll
-        for (int i = 0; i < NI; ++i) acc[i][j] = mfma16(wa[h][i], xb, acc[i][j]);
+          for (int i = 0; i < NI; ++i) acc[i][j] = mfma16(wa[h][i], xb, acc[i][j]);
+        }
+    }
+    // (a dead unit of pass 2 whose columns straddle V takes the general epilogue: alpha = 0 there
+    // gives exact zeros)
+    const bool full_cols = (V % 4 == 0) && cw + 16 * NI <= V;
+    if (!live && (!GRAD || full_cols)) {
+      if constexpr (!GRAD) {
+        if (lane < 16) {
+#pragma unroll
+          for (int j = 0; j < RJ; ++j) {
+            Pm[buf][wid][16 * j + c16] = -INFINITY;
+            Ps[buf][wid][16 * j + c16] = 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < RJ; ++j) {
+          const int row = rb + 16 * j + c16;
+          if (row >= N) continue;
+          bf16* dst = dl + (size_t)row * V + cw + q4;
+#pragma unroll
+          for (int i = 0; i < NI; ++i) *reinterpret_cast<bf16x4*>(dst + 16 * i) = bf16x4{};
+        }
       }
-    if constexpr (!GRAD) {
+    } else if constexpr (!GRAD) {
 #pragma unroll
       for (int j = 0; j < RJ; ++j) {
         const int rr = 16 * j + c16, row = rb + rr;
@@ -421,10 +453,11 @@ static int vocab_train_grid(int N, int V, int H) {
 }
 
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
-                            float* zg, float* lse, float* pv, int N, int V, int H, hipStream_t st) {
+                            float* zg, float* lse, float* pv, int N, int V, int H, const int* dlen, int Bd,
+                            hipStream_t st) {
   const int grid = vocab_train_grid(N, V, H);
 #define VF(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
-                                  part, zg, nullptr, nullptr, nullptr, nullptr, N, V, ldx)
+                                  part, zg, nullptr, nullptr, nullptr, nullptr, N, V, ldx, dlen, Bd)
   if (H == 512) VF(512);
   else if (H == 256) VF(256);
   else VF(128);
@@ -435,10 +468,10 @@ void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float*
 
 void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
                             const float* lse, const float* alpha, bf16* dl, float* dbias, int N, int V, int H,
-                            hipStream_t st) {
+                            const int* dlen, int Bd, hipStream_t st) {
   const int grid = vocab_train_grid(N, V, H);
 #define VB(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
-                                  nullptr, nullptr, lse, alpha, dl, dbias, N, V, ldx)
+                                  nullptr, nullptr, lse, alpha, dl, dbias, N, V, ldx, dlen, Bd)
   if (H == 512) VB(512);
   else if (H == 256) VB(256);
   else VB(128);

@@ -721,8 +721,9 @@ class HipPointerGenerator:
             pg = w["pg"]
         if self.fused_vocab:
             k, ldx = self.k, H + 8  # outb is the first H columns of outb_ext
+            dlen = w["dlen"] if self.skip_pad else None  # 32-row blocks past their rows' last live step: no MFMAs
             k.vocab_train_fwd(w["outb_ext"], self.pk["owT"], p[OV], w["target_t"], w["vpart"], w["zg"], w["lse"],
-                              w["pv"], N, V, H, ldx)
+                              w["pv"], N, V, H, ldx, dlen, B)
             k.ptr_rowfin(w["pv"], w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None, w["ext"],
                          w["enc_lens"], w["loss_row"], w["alpha"] if need_grad else None,
                          w["dpre"] if (need_grad and hps.pointer_gen) else None,
@@ -730,7 +731,7 @@ class HipPointerGenerator:
             if need_grad:
                 w["dbias"].zero_()
                 k.vocab_train_bwd(w["outb_ext"], self.pk["owT"], p[OV], w["target_t"], w["lse"], w["alpha"],
-                                  w["dlogits"], None if self.det else w["dbias"], N, V, H, ldx)
+                                  w["dlogits"], None if self.det else w["dbias"], N, V, H, ldx, dlen, B)
                 if self.det:  # column sums of the bf16 dlogits in a fixed order
                     torch.sum(w["dlogits"], 0, dtype=F32, out=w["dbias"])
             return
