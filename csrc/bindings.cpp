@@ -498,7 +498,7 @@ int64_t vocab_train_tiles_op(int64_t V, int64_t H) { return vocab_train_tiles((i
 // X: [N][ldx] bf16 (the first H columns are the activations; ldx >= H, ldx % 8 == 0)
 void vocab_train_fwd(const Tensor& X, const Tensor& WT, const Tensor& bias, const Tensor& target, const Tensor& part,
                      const Tensor& zg, const Tensor& lse, const Tensor& pv, int64_t N, int64_t V, int64_t H,
-                     int64_t ldx, const OT& dlen, int64_t Bd) {
+                     int64_t ldx, const OT& vblk, const OT& vblk_n) {
   chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(target, I32, "target"); chk(part, F32, "part");
   chk(zg, F32, "zg"); chk(lse, F32, "lse"); chk(pv, F32, "pv");
   TORCH_CHECK(H == 128 || H == 256 || H == 512, "fused training vocab head: hidden size 128, 256 or 512");
@@ -506,26 +506,32 @@ void vocab_train_fwd(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
   numel_eq(X, N * ldx, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias"); numel_eq(target, N, "target");
   numel_eq(part, (int64_t)vocab_train_tiles((int)V, (int)H) * N * 2, "part"); numel_eq(zg, N, "zg"); numel_eq(lse, N, "lse");
   numel_eq(pv, N, "pv");
-  // dlen [Bd]: row n = t * Bd + b past its last live decoder step (t >= dlen[b]) is skipped
-  TORCH_CHECK(!dlen.has_value() || (Bd >= 1 && N % Bd == 0), "dlen needs N = D * Bd");
-  chko(dlen, I32, Bd, "dlen");
+  // vblk [ceil(N / 32)]: the live 32-row blocks first, *vblk_n of them (the host builds both)
+  const int64_t RB = (N + 31) / 32;
+  TORCH_CHECK(vblk.has_value() == vblk_n.has_value(), "vblk and vblk_n go together");
+  chko(vblk, I32, RB, "vblk"); chko(vblk_n, I32, 1, "vblk_n");
   launch_vocab_train_fwd(P<bf16>(X), (int)ldx, P<bf16>(WT), P<float>(bias), P<int>(target), P<float>(part), P<float>(zg),
-                         P<float>(lse), P<float>(pv), N, V, H, PO<int>(dlen), (int)std::max<int64_t>(Bd, 1), stream());
+                         P<float>(lse), P<float>(pv), N, V, H, PO<int>(vblk), PO<int>(vblk_n), stream());
 }
 
 void vocab_train_bwd(const Tensor& X, const Tensor& WT, const Tensor& bias, const Tensor& target, const Tensor& lse,
                      const Tensor& alpha, const Tensor& dl, const OT& dbias, int64_t N, int64_t V, int64_t H,
-                     int64_t ldx, const OT& dlen, int64_t Bd) {
+                     int64_t ldx, const OT& vblk, const OT& vblk_n, const OT& vlive, const OT& vstate) {
   chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(target, I32, "target"); chk(lse, F32, "lse");
   chk(alpha, F32, "alpha"); chk(dl, BF, "dl");
   TORCH_CHECK(H == 128 || H == 256 || H == 512, "fused training vocab head: hidden size 128, 256 or 512");
   TORCH_CHECK(N >= 1 && V >= 1 && ldx >= H && ldx % 8 == 0, "bad N/V/ldx");
   numel_eq(X, N * ldx, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias"); numel_eq(target, N, "target");
   numel_eq(lse, N, "lse"); numel_eq(alpha, N, "alpha"); numel_eq(dl, N * V, "dl"); chko(dbias, F32, V, "dbias");
-  TORCH_CHECK(!dlen.has_value() || (Bd >= 1 && N % Bd == 0), "dlen needs N = D * Bd");
-  chko(dlen, I32, Bd, "dlen");
+  const int64_t RB = (N + 31) / 32;
+  const bool has = vblk.has_value();
+  TORCH_CHECK(vblk_n.has_value() == has && vlive.has_value() == has && vstate.has_value() == has,
+              "vblk, vblk_n, vlive and vstate go together");
+  chko(vblk, I32, RB, "vblk"); chko(vblk_n, I32, 1, "vblk_n"); chko(vlive, I32, RB, "vlive");
+  chko(vstate, I32, RB, "vstate");
   launch_vocab_train_bwd(P<bf16>(X), (int)ldx, P<bf16>(WT), P<float>(bias), P<int>(target), P<float>(lse), P<float>(alpha),
-                         P<bf16>(dl), PO<float>(dbias), N, V, H, PO<int>(dlen), (int)std::max<int64_t>(Bd, 1), stream());
+                         P<bf16>(dl), PO<float>(dbias), N, V, H, PO<int>(vblk), PO<int>(vblk_n), PO<int>(vlive),
+                         PO<int>(vstate), stream());
 }
 
 void ptr_rowfin(const Tensor& pv, const Tensor& target, const Tensor& rowg, const OT& pgen, const OT& attn,

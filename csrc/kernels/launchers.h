@@ -133,11 +133,11 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
                        const BeamTail* bt = nullptr);
 int vocab_train_tiles(int V, int H);
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
-                            float* zg, float* lse, float* pv, int N, int V, int H, const int* dlen, int Bd,
+                            float* zg, float* lse, float* pv, int N, int V, int H, const int* vblk, const int* vblk_n,
                             hipStream_t st);
 void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
                             const float* lse, const float* alpha, bf16* dl, float* dbias, int N, int V, int H,
-                            const int* dlen, int Bd, hipStream_t st);
+                            const int* vblk, const int* vblk_n, const int* vlive, int* vstate, hipStream_t st);
 void launch_ptr_rowfin(const float* pv, const int* target, const float* rowg, const float* pgen, const float* attn,
                        const int* ext, const int* lens, float* loss_row, float* alpha, float* dpre, float* dA, int N,
                        int B, int T, hipStream_t st);

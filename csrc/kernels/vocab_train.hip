@@ -115,8 +115,8 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     bf16* __restrict__ dl,            // [N][V]   pass 2: dlogits
     float* __restrict__ dbias,        // [V]      pass 2 (nullable): += column sums of dlogits
     int N, int V, int ldx,
-    const int* __restrict__ dlen,     // [Bd]     nullable: row n = t Bd + b is live iff t < dlen[b]
-    int Bd) {
+    const int* __restrict__ vblk,     // nullable: the live 32-row blocks (EngineConfig.skip_pad_steps),
+    const int* __restrict__ vblk_n) { // *vblk_n of them; the units enumerate only those
   constexpr int KS = H / 32;          // k-steps of 32
   constexpr int NI = vr_ni(H), VR_COLS = vr_cols(H);
   constexpr int XS = H + 8;           // padded LDS row (bank spread)
@@ -127,10 +127,10 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
   __shared__ float Pm[2][4][VR_ROWS], Ps[2][4][VR_ROWS];
   __shared__ int Tg[2][VR_ROWS];
   __shared__ float Ls[2][VR_ROWS], Al[2][VR_ROWS];
-  __shared__ int Lv[2][VR_ROWS];  // row live (a unit of 32 dead rows skips its MFMAs)
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int RB = (N + VR_ROWS - 1) / VR_ROWS, nt = (V + VR_COLS - 1) / VR_COLS;
+  const int RB = vblk ? *vblk_n : (N + VR_ROWS - 1) / VR_ROWS, nt = (V + VR_COLS - 1) / VR_COLS;
   const long units = (long)RB * nt;
+  auto row0 = [&](int u) { return (vblk ? vblk[u % RB] : u % RB) * VR_ROWS; };  // unit u's first row
   const int u0 = (int)(units * blockIdx.x / gridDim.x), u1 = (int)(units * (blockIdx.x + 1) / gridDim.x);
   if (u0 >= u1) return;
   const int kof = 8 * (lane >> 4), c16 = lane & 15, q4 = 4 * (lane >> 4);
@@ -153,10 +153,10 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     cacc = 0.f;
   };
   bf16x8 xr[CH];      // prefetched X chunks of the next unit
-  int tg_r = 0, lv_r = 1;
+  int tg_r = 0;
   float ls_r = 0.f, al_r = 0.f;
   auto fetch = [&](int u) {  // global -> registers (unit u's X rows, targets, row scalars)
-    const int rb = (u % RB) * VR_ROWS;
+    const int rb = row0(u);
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = c * 256 + threadIdx.x, rr = idx / (H / 8), k8 = (idx % (H / 8)) * 8;
@@ -165,7 +165,6 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     if (threadIdx.x < VR_ROWS) {
       const int row = min(rb + threadIdx.x, N - 1);
       tg_r = target[row];
-      lv_r = rb + (int)threadIdx.x < N && (!dlen || row / Bd < dlen[row % Bd]);
       if (GRAD) {
         ls_r = lse[row];
         al_r = alpha[row];
@@ -180,7 +179,6 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     }
     if (threadIdx.x < VR_ROWS) {
       Tg[buf][threadIdx.x] = tg_r;
-      Lv[buf][threadIdx.x] = lv_r;
       if (GRAD) {
         Ls[buf][threadIdx.x] = ls_r;
         Al[buf][threadIdx.x] = al_r;
@@ -188,7 +186,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     }
   };
   auto merge_store = [&](int buf, int u) {  // pass 1: cross-wave (max, sum) of unit u -> part
-    const int vt = u / RB, rb = (u % RB) * VR_ROWS;
+    const int vt = u / RB, rb = row0(u);
     if (wid == 0 && lane < VR_ROWS && rb + lane < N) {
       float m = Pm[buf][0][lane], sm = Ps[buf][0][lane];
 #pragma unroll
@@ -201,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
   __syncthreads();
   for (int u = u0; u < u1; ++u) {
     const int buf = (u - u0) & 1;
-    const int vt = u / RB, rb = (u % RB) * VR_ROWS;
+    const int vt = u / RB, rb = row0(u);
     const int cw = vt * VR_COLS + 16 * NI * wid;  // this wave's first column
     if (vt != cur_vt) {  // new vocab tile: its A fragments and bias into registers
       if (GRAD && dbias && cur_vt >= 0) flush_bias(cur_vt);
@@ -221,47 +219,20 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
       cur_vt = vt;
     }
     if (u + 1 < u1) fetch(u + 1);
-    // 32 rows past their last loss-weighted decoder step (EngineConfig.skip_pad_steps): no MFMAs;
-    // pass 1 records an empty partial, pass 2 stores zero dlogits (block-uniform: LDS flags)
-    const bool live = __any(Lv[buf][c16] | Lv[buf][16 + c16]);
     f32x4 acc[NI][RJ];
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < RJ; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-    if (live) {
 #pragma unroll
-      for (int h = 0; h < KS; ++h)
+    for (int h = 0; h < KS; ++h)
 #pragma unroll
-        for (int j = 0; j < RJ; ++j) {
-          const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&Xs[buf][(16 * j + c16) * XS + 32 * h + kof]);
+      for (int j = 0; j < RJ; ++j) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&Xs[buf][(16 * j + c16) * XS + 32 * h + kof]);
 #pragma unroll
-          for (int i = 0; i < NI; ++i) acc[i][j] = mfma16(wa[h][i], xb, acc[i][j]);
-        }
-    }
-    // (a dead unit of pass 2 whose columns straddle V takes the general epilogue: alpha = 0 there
-    // gives exact zeros)
-    const bool full_cols = (V % 4 == 0) && cw + 16 * NI <= V;
-    if (!live && (!GRAD || full_cols)) {
-      if constexpr (!GRAD) {
-        if (lane < 16) {
-#pragma unroll
-          for (int j = 0; j < RJ; ++j) {
-            Pm[buf][wid][16 * j + c16] = -INFINITY;
-            Ps[buf][wid][16 * j + c16] = 0.f;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < RJ; ++j) {
-          const int row = rb + 16 * j + c16;
-          if (row >= N) continue;
-          bf16* dst = dl + (size_t)row * V + cw + q4;
-#pragma unroll
-          for (int i = 0; i < NI; ++i) *reinterpret_cast<bf16x4*>(dst + 16 * i) = bf16x4{};
-        }
+        for (int i = 0; i < NI; ++i) acc[i][j] = mfma16(wa[h][i], xb, acc[i][j]);
       }
-    } else if constexpr (!GRAD) {
+    if constexpr (!GRAD) {
 #pragma unroll
       for (int j = 0; j < RJ; ++j) {
         const int rr = 16 * j + c16, row = rb + rr;
@@ -381,6 +352,31 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
   if (GRAD && dbias) flush_bias(cur_vt);
 }
 
+// Rows past their last live decoder step are not enumerated by pass 2, so their dlogits keep what
+// an earlier batch wrote there.  Before pass 2, a 32-row block that is dead now but was written by
+// the previous pass 2 (state[b]) is zeroed -- the gradient GEMMs read every row -- and state[]
+// becomes this batch's liveness.  Consecutive batches have similar length profiles (rows sorted
+// by live steps), so few blocks change.
+__global__ __launch_bounds__(256) void vocab_zero_dead_kernel(bf16* __restrict__ dl, const int* __restrict__ vlive,
+                                                              int* __restrict__ state, int N, int V) {
+  const int b = blockIdx.x;
+  const int live = vlive[b];
+  if (!live && state[b]) {
+    const size_t r0 = (size_t)b * VR_ROWS, r1 = min((size_t)N, r0 + VR_ROWS);
+    bf16* p = dl + r0 * V;
+    const size_t n = (r1 - r0) * (size_t)V;
+    const size_t head = (16 - ((uintptr_t)p & 15)) & 15;  // bytes to 16-byte alignment
+    const size_t h = min(n, head / 2);
+    for (size_t i = threadIdx.x; i < h; i += 256) p[i] = f2bf(0.f);
+    typedef uint32_t u32x4z __attribute__((ext_vector_type(4)));
+    u32x4z* q = reinterpret_cast<u32x4z*>(p + h);
+    const size_t nv = (n - h) / 8;
+    for (size_t i = threadIdx.x; i < nv; i += 256) q[i] = u32x4z{0, 0, 0, 0};
+    for (size_t i = h + nv * 8 + threadIdx.x; i < n; i += 256) p[i] = f2bf(0.f);
+  }
+  if (threadIdx.x == 0) state[b] = live;
+}
+
 // lse and p_vocab(gold) per row: 32 rows x 8 tile slices per workgroup (slice j merges the
 // row's partials of tiles j, j + 8, ...: each warp-wide load is 32 consecutive rows' float2,
 // coalesced), the 8 slice partials merged through LDS.  N/32 workgroups instead of N/256 with a
@@ -453,11 +449,11 @@ static int vocab_train_grid(int N, int V, int H) {
 }
 
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
-                            float* zg, float* lse, float* pv, int N, int V, int H, const int* dlen, int Bd,
+                            float* zg, float* lse, float* pv, int N, int V, int H, const int* vblk, const int* vblk_n,
                             hipStream_t st) {
   const int grid = vocab_train_grid(N, V, H);
 #define VF(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
-                                  part, zg, nullptr, nullptr, nullptr, nullptr, N, V, ldx, dlen, Bd)
+                                  part, zg, nullptr, nullptr, nullptr, nullptr, N, V, ldx, vblk, vblk_n)
   if (H == 512) VF(512);
   else if (H == 256) VF(256);
   else VF(128);
@@ -468,10 +464,13 @@ void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float*
 
 void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
                             const float* lse, const float* alpha, bf16* dl, float* dbias, int N, int V, int H,
-                            const int* dlen, int Bd, hipStream_t st) {
+                            const int* vblk, const int* vblk_n, const int* vlive, int* vstate, hipStream_t st) {
   const int grid = vocab_train_grid(N, V, H);
+  if (vblk)
+    hipLaunchKernelGGL(vocab_zero_dead_kernel, dim3((N + VR_ROWS - 1) / VR_ROWS), dim3(256), 0, st, dl, vlive, vstate,
+                       N, V);
 #define VB(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
-                                  nullptr, nullptr, lse, alpha, dl, dbias, N, V, ldx, dlen, Bd)
+                                  nullptr, nullptr, lse, alpha, dl, dbias, N, V, ldx, vblk, vblk_n)
   if (H == 512) VB(512);
   else if (H == 256) VB(256);
   else VB(128);

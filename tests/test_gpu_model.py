@@ -188,32 +188,40 @@ def test_projected_context_matches_enc_out_path(monkeypatch, coverage, pointer_g
 
 @pytest.mark.parametrize("coverage,pointer_gen", [(True, True), (False, False)])
 def test_skip_pad_steps_same_loss_and_gradients(monkeypatch, coverage, pointer_gen):
-    """Skipping (row, step) pairs past a row's last loss-weighted decoder step (the projected
-    attention kernels exit, attn_bwd_feat stops at the row's length) leaves the loss, every
-    parameter gradient and the live steps' attention unchanged.  D = 40 decoder steps with
-    summaries of ~15-30 tokens: most rows have dead steps, some rows none."""
+    """Skipping (row, step) pairs past a row's last loss-weighted decoder step (rows sorted by live
+    steps; the projected attention kernels exit, decoder tiles and vocab-head blocks of dead rows
+    are not computed, attn_bwd_feat stops at the row's length) leaves the loss, every parameter
+    gradient and the live steps' attention unchanged.  D = 40 decoder steps with summaries of
+    ~15-30 tokens: most rows have dead steps.  Two batches in a row on the skipping engine: the
+    second batch's dead vocab blocks that the first batch wrote must read as zero dlogits."""
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
     hps, vocab, batch, params = _setup(coverage, pointer_gen, B=24, T=120, D=40, H=256, E=128)
+    corpus = SyntheticCorpus(vocab_size=2000, raw_vocab=8000, seed=5, art_mean=108, art_sd=48, sent_mean=4)
+    batch2 = make_batches(hps, vocab, corpus, 1, pad_enc_to=120)[0]
     monkeypatch.setenv("TSAMD_ROW_ATTN", "1")
-    got = []
+    got = {}
     for flag in ("0", "1"):
         monkeypatch.setenv("TSAMD_SKIP_PAD_STEPS", flag)
         params.enable_grad()
         eng = HipPointerGenerator(hps, vocab.size(), params, B=hps.batch_size, T=hps.max_enc_steps)
         assert eng.proj_attn and eng.skip_pad == (flag == "1")
-        eng.set_batch(batch)
-        out = eng.forward(need_grad=True)
-        eng.backward()
-        torch.cuda.synchronize()
-        got.append((out["total_loss"].detach().clone(), params.grad.clone(), eng.w["ATT"].clone()))
-    dlen, src = eng.w["dlen"].long(), eng.w["row_src"].long()  # the skipping engine's rows are sorted
-    assert bool((dlen[:-1] >= dlen[1:]).all()) and sorted(src.tolist()) == list(range(hps.batch_size))
-    live = torch.arange(eng.D, device="cuda")[:, None] < dlen[None, :]
-    assert int((dlen < eng.D).sum()) > 0 and int((dlen == 0).sum()) == 0
-    assert _rel(got[1][0], got[0][0]) < 1e-6
-    assert _rel(got[1][1], got[0][1]) < 1e-5, _rel(got[1][1], got[0][1])
-    assert _rel(got[1][2][live], got[0][2][:, src][live]) < 1e-6
-    assert float(got[1][2][~live].abs().max()) == 0.0
+        for bi, bt in enumerate((batch, batch2) if flag == "1" else (batch2, batch)):
+            eng.set_batch(bt)
+            out = eng.forward(need_grad=True)
+            eng.backward()
+            torch.cuda.synchronize()
+            got[(flag, id(bt))] = (out["total_loss"].detach().clone(), params.grad.clone(), eng.w["ATT"].clone(),
+                                  eng.w["dlen"].long().clone(), eng.w["row_src"].long().clone())
+    for bt in (batch, batch2):
+        l0, g0, a0, _, _ = got[("0", id(bt))]
+        l1, g1, a1, dlen, src = got[("1", id(bt))]
+        assert bool((dlen[:-1] >= dlen[1:]).all()) and sorted(src.tolist()) == list(range(hps.batch_size))
+        live = torch.arange(40, device="cuda")[:, None] < dlen[None, :]
+        assert int((dlen < 40).sum()) > 0 and int((dlen == 0).sum()) == 0
+        assert _rel(l1, l0) < 1e-6
+        assert _rel(g1, g0) < 1e-5, _rel(g1, g0)
+        assert _rel(a1[live], a0[:, src][live]) < 1e-6
+        assert float(a1[~live].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("layers,H", [(1, 256), (2, 128)])

@@ -127,6 +127,15 @@ def host_inputs(batch, hps, D: int, sort_rows: bool = False) -> Dict[str, np.nda
     enc_lens, rowg, gcl, dlen = batch.enc_lens[src], rowg[src], gcl[src], dlen[src]
     dec_t = np.ascontiguousarray(batch.dec_batch[src, :D].T).astype(np.int64)
     sid, perm = emb_sort(enc_batch, dec_t)
+    # the fused vocab head's 32-row blocks of the t-major [D * B] rows that hold a live row, listed
+    # first (vblk, vblk_n of them); vlive per block (the blocks pass 2 must keep zeroed)
+    nb = (D * len(dlen) + 31) // 32
+    lr = np.zeros(nb * 32, dtype=bool)
+    lr[:D * len(dlen)] = (np.arange(D)[:, None] < dlen[None, :]).reshape(-1)
+    vlive = lr.reshape(nb, 32).any(1)
+    vblk = np.zeros(nb, dtype=np.int32)
+    live_ids = np.nonzero(vlive)[0]
+    vblk[:len(live_ids)] = live_ids
     return {
         "enc_batch": enc_batch.astype(np.int64),
         "enc_lens": enc_lens.astype(np.int32),
@@ -140,6 +149,9 @@ def host_inputs(batch, hps, D: int, sort_rows: bool = False) -> Dict[str, np.nda
         "emb_perm": perm,
         "dlen": dlen.astype(np.int32),
         "row_src": src.astype(np.int32),
+        "vlive": vlive.astype(np.int32),
+        "vblk": vblk,
+        "vblk_n": np.array([len(live_ids)], dtype=np.int32),
     }
 
 
@@ -168,14 +180,15 @@ _NP = {torch.long: np.int64, torch.int32: np.int32, F32: np.float32}
 def input_layout(B: int, T: int, D: int):
     """Byte layout of the engine's input pack: [(name, offset, shape, torch dtype, nbytes)],
     total size (every array 256-byte aligned); the device copy is one buffer with views."""
-    shapes = {"BT": (B, T), "B": (B,), "DB": (D, B), "R": (B * T + D * B,)}
+    shapes = {"BT": (B, T), "B": (B,), "DB": (D, B), "R": (B * T + D * B,), "VB": ((D * B + 31) // 32,), "1": (1,)}
     layout, off = [], 0
     for name, sk, dt in (("enc_batch", "BT", torch.long), ("enc_lens", "B", torch.int32),
                          ("rev_idx", "BT", torch.long), ("ext", "BT", torch.int32),
                          ("dec_batch_t", "DB", torch.long), ("target_t", "DB", torch.int32),
                          ("rowg", "DB", F32), ("gcl", "DB", F32),
                          ("emb_sid", "R", torch.int32), ("emb_perm", "R", torch.int32), ("dlen", "B", torch.int32),
-                         ("row_src", "B", torch.int32)):
+                         ("row_src", "B", torch.int32), ("vlive", "VB", torch.int32), ("vblk", "VB", torch.int32),
+                         ("vblk_n", "1", torch.int32)):
         shp = shapes[sk]
         nb = int(np.prod(shp)) * np.dtype(_NP[dt]).itemsize
         layout.append((name, off, shp, dt, nb))
@@ -384,6 +397,7 @@ class HipPointerGenerator:
             for n in ("zg", "lse", "pv", "alpha"):
                 w[n] = z(N)
             w["dbias"] = z(V)  # output_projection/v gradient, column sums taken inside pass 2
+            w["vstate"] = z((N + 31) // 32, dt=torch.int32)  # dlogits blocks written by the last pass 2
         w["logits"] = z(D * B, V, dt=BF)
         # backward
         w["dlogits"] = w["logits"]
@@ -721,9 +735,10 @@ class HipPointerGenerator:
             pg = w["pg"]
         if self.fused_vocab:
             k, ldx = self.k, H + 8  # outb is the first H columns of outb_ext
-            dlen = w["dlen"] if self.skip_pad else None  # 32-row blocks past their rows' last live step: no MFMAs
+            # skip_pad: only the 32-row blocks holding a live row are enumerated (host-built list)
+            vb, vn = (w["vblk"], w["vblk_n"]) if self.skip_pad else (None, None)
             k.vocab_train_fwd(w["outb_ext"], self.pk["owT"], p[OV], w["target_t"], w["vpart"], w["zg"], w["lse"],
-                              w["pv"], N, V, H, ldx, dlen, B)
+                              w["pv"], N, V, H, ldx, vb, vn)
             k.ptr_rowfin(w["pv"], w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None, w["ext"],
                          w["enc_lens"], w["loss_row"], w["alpha"] if need_grad else None,
                          w["dpre"] if (need_grad and hps.pointer_gen) else None,
@@ -731,7 +746,8 @@ class HipPointerGenerator:
             if need_grad:
                 w["dbias"].zero_()
                 k.vocab_train_bwd(w["outb_ext"], self.pk["owT"], p[OV], w["target_t"], w["lse"], w["alpha"],
-                                  w["dlogits"], None if self.det else w["dbias"], N, V, H, ldx, dlen, B)
+                                  w["dlogits"], None if self.det else w["dbias"], N, V, H, ldx, vb, vn,
+                                  w["vlive"] if vb is not None else None, w["vstate"] if vb is not None else None)
                 if self.det:  # column sums of the bf16 dlogits in a fixed order
                     torch.sum(w["dlogits"], 0, dtype=F32, out=w["dbias"])
             return

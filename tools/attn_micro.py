@@ -96,11 +96,11 @@ def main():
     if eng.fused_vocab:
         ldx = H + 8
         res["vocab_fwd"] = timeit(lambda: k.vocab_train_fwd(w["outb_ext"], eng.pk["owT"], p[OV], w["target_t"],
-                                                            w["vpart"], w["zg"], w["lse"], w["pv"], N, V, H, ldx, None, 1),
+                                                            w["vpart"], w["zg"], w["lse"], w["pv"], N, V, H, ldx, None, None),
                                   it=10)
         res["vocab_bwd"] = timeit(lambda: k.vocab_train_bwd(w["outb_ext"], eng.pk["owT"], p[OV], w["target_t"],
                                                             w["lse"], w["alpha"], w["dlogits"], w.get("dbias"), N, V,
-                                                            H, ldx, None, 1), it=10)
+                                                            H, ldx, None, None, None, None), it=10)
     # output-projection weight gradient (K = N rows): [W|b] (M = H+1) vs W only vs split-K
     xe = w["outb_ext"]
     dst = torch.empty(H + 1, V, device="cuda")

@@ -53,8 +53,8 @@ def main():
     db = torch.zeros(V, device=dev)
     ref = None
     for rep in range(a.reps):
-        fwd = lambda: k.vocab_train_fwd(X, WT, bias, target, part, zg, lse, pv, N, V, H, ldx, None, 1)
-        bwd = lambda: k.vocab_train_bwd(X, WT, bias, target, lse, alpha, dl, db, N, V, H, ldx, None, 1)
+        fwd = lambda: k.vocab_train_fwd(X, WT, bias, target, part, zg, lse, pv, N, V, H, ldx, None, None)
+        bwd = lambda: k.vocab_train_bwd(X, WT, bias, target, lse, alpha, dl, db, N, V, H, ldx, None, None, None, None)
         r = {"rep": rep, "rows": N, "fwd_us": timed(fwd, a.iters), "bwd_us": timed(bwd, a.iters)}
         db.zero_()
         fwd()
