@@ -710,6 +710,12 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
 bool attn_row_supported(int A, int T) { return (A == 512 || A == 1024) && T >= 1 && T <= kRowMaxT; }
 bool attn_rowp_supported(int A, int T, int EG) { return attn_row_supported(A, T) && EG == kEG; }
 
+// waves per workgroup of the projected kernels: forward 16 / 8 (A = 512 / 1024) as row_waves();
+// backward 16 at A = 512 (128 VGPRs, 2 spilled: B = 256 17.47-17.51 -> 17.22 ms per step against
+// 12 waves, 17.75 with 8) and 8 at A = 1024 (4 equal, 12 spills 75; profiles/r3/ab/rowp_waves.txt)
+template <int NK>
+constexpr int rowp_bwd_waves() { return NK == 1 ? 16 : 8; }
+
 void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const float* v, const float* wc,
                           const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* gx,
                           bf16* gx_bf, int B, int T, int A, const int* dlen, int step, hipStream_t st) {
@@ -727,9 +733,8 @@ void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const fl
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
                           float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st) {
 #define LB(NK)                                                                                            \
-  hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, row_waves<NK, true>()>), dim3(B),                         \
-                     dim3(row_waves<NK, true>() * 64), 0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, \
-                     lens, de_out, ds, dcov_out, T, dlen, step)
+  hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, rowp_bwd_waves<NK>()>), dim3(B), dim3(rowp_bwd_waves<NK>() * 64), \
+                     0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, dlen, step)
   if (A == 512) LB(1);
   else LB(2);
 #undef LB
