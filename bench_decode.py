@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--no-pipeline", dest="pipelined", action="store_false",
                     help="decode batch by batch (host backtracking not overlapped with the next batch)")
     ap.add_argument("--vocab", type=int, default=50000)
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--layers", type=int, default=1, help="encoder bi-LSTM layers (config #5: 2)")
+    ap.add_argument("--enc", type=int, default=400, help="max encoder steps (config #5: 800)")
     args = ap.parse_args()
     import torch
     from textsummarization_on_flink_amd.config import HParams
@@ -34,7 +37,8 @@ def main():
     from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
     from textsummarization_on_flink_amd.models.params import build_params
 
-    hps = HParams(mode="decode", batch_size=args.articles, beam_size=args.beam, coverage=True, vocab_size=args.vocab)
+    hps = HParams(mode="decode", batch_size=args.articles, beam_size=args.beam, coverage=True, vocab_size=args.vocab,
+                  hidden_dim=args.hidden, enc_layers=args.layers, max_enc_steps=args.enc)
     corpus = SyntheticCorpus(vocab_size=args.vocab, seed=7)
     vocab = corpus.vocab(args.vocab)
     batches = make_batches(hps, vocab, corpus, args.batches + args.warmup, pad_enc_to=hps.max_enc_steps)
@@ -71,7 +75,8 @@ def main():
                       "ms_per_batch": round(1000 * el / args.batches, 2), "decode_steps_per_batch": steps / args.batches,
                       "ms_per_batch_min": round(1000 * min(per), 2),
                       "ms_per_batch_median": round(1000 * sorted(per)[len(per) // 2], 2),
-                      "config": {"model": "pointer-generator+coverage hidden=256 emb=128 enc=400 dec<=100 vocab=50000",
+                      "config": {"model": f"pointer-generator+coverage hidden={args.hidden} emb=128 enc={args.enc} "
+                                          f"dec<=100 vocab={args.vocab} enc_layers={args.layers}",
                                  "beam": args.beam, "articles_per_batch": args.articles,
                                  "rows": args.articles * args.beam, "graph": not args.no_graph,
                                  "pipelined": args.pipelined}}))
