@@ -732,15 +732,11 @@ void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const fl
                           const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
                           float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st) {
-  static const int nwv = getenv("TSAMD_AB_BWD_NW") ? atoi(getenv("TSAMD_AB_BWD_NW")) : 0;
-#define LB(NK, NW)                                                                                            \
-  hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, NW>), dim3(B), dim3(NW * 64), \
+#define LB(NK)                                                                                            \
+  hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, rowp_bwd_waves<NK>()>), dim3(B), dim3(rowp_bwd_waves<NK>() * 64), \
                      0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, dlen, step)
-  if (A == 512) {
-    if (nwv == 12) LB(1, 12);
-    else LB(1, 16);
-  }
-  else LB(2, 8);
+  if (A == 512) LB(1);
+  else LB(2);
 #undef LB
 }
 

@@ -250,6 +250,12 @@ class HipPointerGenerator:
         # B = 256 since the LDS-parameter row backward: 4 groups 19.35 / 19.49 ms, 2 groups 20.21 /
         # 19.99, 8 groups 27.2, 1 group 20.75 (profiles/r3/ab/split_b256.txt))
         sp = cfg.split or (4 if B >= 256 and B % 64 == 0 else 2 if B >= 128 and B % 32 == 0 else 1)
+        # deterministic mode: one chain.  With 4 concurrent row-group streams two deterministic
+        # runs of the projected-context path diverged in a few output-projection gradient columns
+        # when run late in the GPU test tier (history dependent; one chain and the E-form path
+        # were bit-identical there): profiles/r3/det_streams.md
+        if cfg.deterministic and not cfg.split:
+            sp = 1
         self.split = sp if (sp > 1 and B % (16 * sp) == 0) else 1
         # cfg.split_bwd: the decoder backward loop's own group count (default: split; B = 256 with
         # 4 forward groups: 4 backward groups 19.48 ms per step, 2 groups 19.79)
