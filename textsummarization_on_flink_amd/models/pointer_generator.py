@@ -249,7 +249,10 @@ class HipPointerGenerator:
         # per step, B = 1024 309.0 -> 301.1-301.9 ms; 8 groups 303.2 (profiles/r2/ab/split_groups.jsonl);
         # B = 256 since the LDS-parameter row backward: 4 groups 19.35 / 19.49 ms, 2 groups 20.21 /
         # 19.99, 8 groups 27.2, 1 group 20.75 (profiles/r3/ab/split_b256.txt))
-        sp = cfg.split or (4 if B >= 256 and B % 64 == 0 else 2 if B >= 128 and B % 32 == 0 else 1)
+        # With the projected attention and the rows sorted by live steps (B = 256: 2 groups 16.65-16.75 ms,
+        # 1 group 16.77, 3 groups 16.99, 4 groups 17.37-17.44; config #5 batch 1024: 2 = 4 = 204.4 ms, 8 206.6;
+        # profiles/r3/ab/split_sorted.txt)
+        sp = cfg.split or (2 if B >= 128 and B % 32 == 0 else 1)
         # deterministic mode: one chain.  With 4 concurrent row-group streams two deterministic
         # runs of the projected-context path diverged in a few output-projection gradient columns
         # when run late in the GPU test tier (history dependent; one chain and the E-form path
