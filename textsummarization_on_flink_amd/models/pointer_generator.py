@@ -252,7 +252,8 @@ class HipPointerGenerator:
         # With the projected attention and the rows sorted by live steps (B = 256: 2 groups 16.65-16.75 ms,
         # 1 group 16.77, 3 groups 16.99, 4 groups 17.37-17.44; config #5 batch 1024: 2 = 4 = 204.4 ms, 8 206.6;
         # profiles/r3/ab/split_sorted.txt)
-        sp = cfg.split or (2 if B >= 128 and B % 32 == 0 else 1)
+        # B = 128: 1 group 13.67 vs 2 groups 13.86 ms (profiles/r3/ab/small_batch.txt)
+        sp = cfg.split or (2 if B >= 256 and B % 32 == 0 else 1)
         # deterministic mode: one chain.  With 4 concurrent row-group streams two deterministic
         # runs of the projected-context path diverged in a few output-projection gradient columns
         # when run late in the GPU test tier (history dependent; one chain and the E-form path
@@ -347,10 +348,11 @@ class HipPointerGenerator:
         w["rs_cat"] = z(2, B, 2 * H, dt=BF)
         w["rs_dp"] = z(2, B, H, dt=BF)
         # row-resident attention (attention_row.hip: one workgroup per row and step, forward
-        # score + softmax + context in one launch) when the batch fills the CUs; else the
+        # score + softmax + context in one launch) from batch 64 (with the projected context and the
+        # skipped dead steps B = 64 12.02 -> 11.77 ms against the multi-block kernels); else the
         # multi-block-per-row kernels of attention.hip.  cfg.row_attn forces it on / off.
         self.row_attn = bool(self.k.attn_row_ok(A, T)) and (
-            cfg.row_attn if cfg.row_attn is not None else (B >= 128 or self.det))
+            cfg.row_attn if cfg.row_attn is not None else (B >= 64 or self.det))
         # backward: the row kernel too (its per-feature parameters in LDS: at A = 1024, 256 rows,
         # T = 800 it streams E and F at 5.2 TB/s, 162 us vs 206 us for the multi-block
         # attn_bwd_step -- tools/attn_micro_c5.py)
