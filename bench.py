@@ -219,6 +219,11 @@ def main(argv=None):
                 "loss": round(vals.get("total_loss", float("nan")), 4),
                 "graph": not args.no_graph,
                 "persistent_lstm": bool(tr.engine.persistent_lstm),
+                # projected-context attention and skipped dead decoder steps (loss and gradients
+                # unchanged; the metric counts non-pad tokens either way): README "Performance"
+                "proj_attn": bool(tr.engine.proj_attn),
+                "skip_pad_steps": bool(tr.engine.skip_pad),
+                "decoder_row_groups": int(tr.engine.split),
                 "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
                 "gpu_mem_gb": round(torch.cuda.get_device_properties(dev_id).total_memory / 2 ** 30, 1),
             },
