@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${OUTD:-pmc_attn}; mkdir -p $OUT
 export TMPDIR=/tmp
-R="attn_fwd_row|attn_bwd_row|attn_bwd_feat|attn_bwd_step4"
+R="${PMC_REGEX:-attn_fwd_row|attn_bwd_row|attn_bwd_feat|attn_bwd_step4}"
 p() {  # shape-tag pass counters...
   local n=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-include-regex "$R" -d $OUT/$n -o run --output-format csv -- python3 tools/attn_micro_c5.py > $OUT/$n.log 2>&1 || { tail -5 $OUT/$n.log; return 1; }

@@ -67,6 +67,17 @@ def main():
                                                          ctxb, MB, T, A, 1), NG)
         res["bwd_row"] = timeit(lambda i: k.attn_bwd_row(E[i], F[i], s, v, wc, cov, att, dctx, ctx, ga, dcn, gcl, lens,
                                                          de, ds, dco, MB, T, A), NG)
+    if k.attn_rowp_ok(A, T, 128):  # projected context: F and G = enc_out . W_in[E:] (128 wide)
+        Gp = (torch.randn(NG, MB, T, 128, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+        gx, gxb = torch.empty(MB, 128, device=dev), torch.empty(MB, 128, device=dev, dtype=torch.bfloat16)
+        dxp = torch.randn(MB, 128, device=dev, generator=g) * 0.1
+        res["fwd_rowp"] = timeit(lambda i: k.attn_fwd_rowp(F[i], Gp[i], s, v, wc, cov, lens, att, cov_out, covloss, gx,
+                                                           gxb, MB, T, A, None, 0), NG)
+        res["bwd_rowp"] = timeit(lambda i: k.attn_bwd_rowp(Gp[i], F[i], s, v, wc, cov, att, dxp, gx, ga, dcn, gcl, lens,
+                                                           de, ds, dco, MB, T, A, None, 0), NG)
+        gbp = MB * T * (A + 128) * 2 / 1e9  # F + G bytes per launch
+        for key in ("fwd_rowp", "bwd_rowp"):
+            res[key + "_GBs"] = round(gbp / (res[key] * 1e-6), 1)
     res["bwd_step"] = timeit(lambda i: (ds.zero_(), k.attn_bwd_step(E[i], F[i], s, v, wc, cov, att, dctx, ctx, ga, dcn,
                                                                     gcl, lens, de, ds, dco, MB, T, A)), NG)
     if os.environ.get("FEAT", "1") == "1":  # the post-loop dF / dv / dwc pass over D decoder steps
