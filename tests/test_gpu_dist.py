@@ -16,44 +16,51 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-B, T, D, V, STEPS = 8, 48, 12, 600, 3
+T, D, V, STEPS = 48, 12, 600, 3
+# (rows per rank, emb_dim, hidden_dim): the small model of the multi-block attention kernels, and
+# the projected-context row attention with the dead-step skipping (hidden 256, emb 128, 64 rows)
+SMALL, PROJ = (8, 64, 64), (64, 128, 256)
 
 
-def _hps(batch):
+def _hps(batch, dims=SMALL):
     from textsummarization_on_flink_amd.config import HParams
-    return HParams(batch_size=batch, max_enc_steps=T, max_dec_steps=D, vocab_size=V, emb_dim=64, hidden_dim=64,
-                   coverage=True, trunc_norm_init_std=0.05)
+    return HParams(batch_size=batch, max_enc_steps=T, max_dec_steps=D, vocab_size=V, emb_dim=dims[1],
+                   hidden_dim=dims[2], coverage=True, trunc_norm_init_std=0.05)
 
 
-def _examples():
+def _examples(dims=SMALL):
     from helpers import gpu_corpus
     from textsummarization_on_flink_amd.data.batch import Example
     from textsummarization_on_flink_amd.data.vocab import abstract2sents
     c = gpu_corpus(5)
     vocab = c.vocab()
-    hps = _hps(B)
+    B = dims[0]
+    hps = _hps(B, dims)
     return vocab, [Example(a, [x.strip() for x in abstract2sents(s)], vocab, hps) for a, s in c.examples(2 * B * STEPS)]
 
 
-def _batch(exs, rows, vocab):
+def _batch(exs, rows, vocab, dims=SMALL):
     from textsummarization_on_flink_amd.data.batch import Batch
-    return Batch([exs[i] for i in rows], _hps(len(rows)), vocab, pad_enc_to=T)
+    return Batch([exs[i] for i in rows], _hps(len(rows), dims), vocab, pad_enc_to=T)
 
 
-def _rank(rank, world, port, q, compress, exclusive):
+def _rank(rank, world, port, q, compress, exclusive, dims=SMALL):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
         from textsummarization_on_flink_amd.parallel.dist import init_from_env
         from textsummarization_on_flink_amd.train.trainer import GraphTrainer
         info = init_from_env(backend="gloo")
-        vocab, exs = _examples()
-        hps = _hps(B).replace(grad_compress=compress)
+        vocab, exs = _examples(dims)
+        B = dims[0]
+        hps = _hps(B, dims).replace(grad_compress=compress)
         tr = GraphTrainer(hps, vocab.size(), B=B, T=T, device="cuda:0", info=info)
+        if dims == PROJ:
+            assert tr.engine.proj_attn and tr.engine.skip_pad
         tr.lstm_exclusive = exclusive
         init = tr.params.flat.clone()
         for k in range(STEPS):
-            out = tr.step(_batch(exs, range(2 * B * k + B * rank, 2 * B * k + B * rank + B), vocab))
+            out = tr.step(_batch(exs, range(2 * B * k + B * rank, 2 * B * k + B * rank + B), vocab, dims))
         vals = tr.check_finite(out)
         q.put((rank, (tr.params.flat - init).cpu(), tr.params.flat.cpu(), vals["total_loss"]))
         torch.distributed.destroy_process_group()
@@ -69,12 +76,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("compress,exclusive,tol", [("none", False, 3e-2), ("bf16", True, 5e-2)])
-def test_graph_trainer_dp2_matches_dp1(compress, exclusive, tol):
+@pytest.mark.parametrize("compress,exclusive,tol,dims", [("none", False, 3e-2, SMALL), ("bf16", True, 5e-2, SMALL),
+                                                        ("none", False, 3e-2, PROJ)])
+def test_graph_trainer_dp2_matches_dp1(compress, exclusive, tol, dims):
+    """PROJ: each rank sorts its own rows by live decoder steps, DP=1 sorts the concatenation."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, compress, exclusive)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, compress, exclusive, dims)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -88,11 +97,12 @@ def test_graph_trainer_dp2_matches_dp1(compress, exclusive, tol):
     assert torch.equal(res[0][1], res[1][1]), "ranks diverged"
     # DP=1 on the concatenated batch (rows of both ranks), same init (same seed)
     from textsummarization_on_flink_amd.train.trainer import GraphTrainer
-    vocab, exs = _examples()
-    tr = GraphTrainer(_hps(2 * B), vocab.size(), B=2 * B, T=T, device="cuda:0")
+    vocab, exs = _examples(dims)
+    B = dims[0]
+    tr = GraphTrainer(_hps(2 * B, dims), vocab.size(), B=2 * B, T=T, device="cuda:0")
     init = tr.params.flat.clone()
     for k in range(STEPS):
-        tr.step(_batch(exs, range(2 * B * k, 2 * B * k + 2 * B), vocab))
+        tr.step(_batch(exs, range(2 * B * k, 2 * B * k + 2 * B), vocab, dims))
     tr.check_finite(tr.out)
     d1 = (tr.params.flat - init).cpu()
     d2 = res[0][0]
