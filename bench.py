@@ -66,6 +66,9 @@ def parse_args(argv=None):
     ap.add_argument("--decode-batches", type=int, default=10, help="timed beam-4 decode batches (0 = skip)")
     ap.add_argument("--decode-articles", type=int, default=64)
     ap.add_argument("--port", type=int, default=0, help="rendezvous port when launching ranks (0 = free port)")
+    ap.add_argument("--config5-steps", type=int, default=3,
+                    help="BASELINE config #5 (hidden 512, 2-layer encoder, enc 800, per-GPU batch 1024) timed train "
+                         "steps + 2 beam-4 decode batches, reported as config5_* fields (0 = skip)")
     return ap.parse_args(argv)
 
 
@@ -187,6 +190,14 @@ def main(argv=None):
     dec = None
     if args.decode_batches > 0:
         dec = bench_decode(args, info, D, torch, dev_id)
+    peak_gb = torch.cuda.max_memory_allocated() / 2 ** 30
+    eng_flags = {"persistent_lstm": bool(tr.engine.persistent_lstm), "proj_attn": bool(tr.engine.proj_attn),
+                 "skip_pad_steps": bool(tr.engine.skip_pad), "decoder_row_groups": int(tr.engine.split)}
+    c5 = None
+    if args.config5_steps > 0 and args.hidden != 512:
+        del tr, batches
+        torch.cuda.empty_cache()
+        c5 = bench_config5(args, info, D, torch, dev_id)
 
     if info.is_chief:
         rec = {
@@ -218,18 +229,17 @@ def main(argv=None):
                 "phase_ms_max_over_ranks": ph,
                 "loss": round(vals.get("total_loss", float("nan")), 4),
                 "graph": not args.no_graph,
-                "persistent_lstm": bool(tr.engine.persistent_lstm),
                 # projected-context attention and skipped dead decoder steps (loss and gradients
                 # unchanged; the metric counts non-pad tokens either way): README "Performance"
-                "proj_attn": bool(tr.engine.proj_attn),
-                "skip_pad_steps": bool(tr.engine.skip_pad),
-                "decoder_row_groups": int(tr.engine.split),
-                "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
+                **eng_flags,
+                "peak_mem_gb": round(peak_gb, 1),
                 "gpu_mem_gb": round(torch.cuda.get_device_properties(dev_id).total_memory / 2 ** 30, 1),
             },
         }
         if dec is not None:
             rec.update(dec)
+        if c5 is not None:
+            rec.update(c5)
         print(json.dumps(rec), flush=True)
     if info.enabled:
         torch.distributed.destroy_process_group()
@@ -257,12 +267,67 @@ def pick_batch(args, hps, vocab, corpus, info, D, torch, dev_id) -> int:
             tr.step(b)  # graph capture included: the peak allocation happens here
             torch.cuda.synchronize()
             del tr
-        except (torch.cuda.OutOfMemoryError, ValueError):
+        except torch.cuda.OutOfMemoryError as e:  # only "does not fit": any other error is real
+            print(f"--batch auto: batch {B} does not fit ({str(e).splitlines()[0][:120]})", file=sys.stderr)
             ok = 0.0
         torch.cuda.empty_cache()
         if D.all_reduce_scalar(ok, info, op="min", device=f"cuda:{dev_id}") > 0 or B == AUTO_BATCHES[-1]:
             return B
     return AUTO_BATCHES[-1]
+
+
+CONFIG5 = dict(hidden=512, layers=2, enc=800, batch=1024)  # BASELINE.json config #5 (run_summarization.py:62-66)
+
+
+def bench_config5(args, info, D, torch, dev_id):
+    """BASELINE config #5 on the same clock as the headline: hidden 512, 2-layer bi-LSTM encoder,
+    enc 800 -> dec 100, per-GPU batch 1024 (weak scaling), same timed region as the headline
+    (H2D, three graph replays, all-reduce, optimizer graph); then 2 batches of 64-article beam-4
+    decode at that size."""
+    import argparse as _ap
+    from textsummarization_on_flink_amd.config import HParams
+    from textsummarization_on_flink_amd.data.synthetic import SyntheticCorpus, make_batches
+    from textsummarization_on_flink_amd.train.trainer import GraphTrainer
+    c = CONFIG5
+    hps = HParams(batch_size=c["batch"], max_enc_steps=c["enc"], max_dec_steps=args.dec, vocab_size=args.vocab,
+                  hidden_dim=c["hidden"], emb_dim=args.emb, coverage=not args.no_coverage, pointer_gen=True,
+                  enc_layers=c["layers"], grad_compress=args.grad_compress)
+    corpus = SyntheticCorpus(vocab_size=args.vocab, seed=2000 + info.rank)
+    vocab = corpus.vocab(args.vocab)
+    batches = make_batches(hps, vocab, corpus, 2, pad_enc_to=c["enc"])
+    tr = GraphTrainer(hps, vocab.size(), B=c["batch"], T=c["enc"], device=f"cuda:{dev_id}", info=info,
+                      use_graph=not args.no_graph)
+    out = tr.step(batches[0])  # warm-up: graph capture
+    tr.check_finite(out)
+
+    def loop():
+        tokens = 0
+        o = None
+        for i in range(args.config5_steps):
+            b = batches[(i + 1) % 2]
+            o = tr.step(b)
+            tokens += b.num_tokens()
+        return o, tokens
+
+    (out, tokens), el = _timed(loop, info, D, torch)
+    tr.check_finite(out)
+    el_max = D.all_reduce_scalar(el, info, op="max", device=tr.device)
+    tok_all = D.all_reduce_scalar(float(tokens), info, op="sum", device=tr.device)
+    del tr, batches
+    torch.cuda.empty_cache()
+    rec = {"config5_tokens_per_sec": round(tok_all / el_max, 1),
+           "config5_ms_per_step": round(1000.0 * el_max / args.config5_steps, 3),
+           "config5_config": {"model": f"pointer-generator+coverage hidden={c['hidden']} emb={args.emb} "
+                                       f"enc={c['enc']} dec={args.dec} vocab={args.vocab} enc_layers={c['layers']}",
+                              "per_gpu_batch": c["batch"], "global_batch": c["batch"] * info.world,
+                              "steps": args.config5_steps, "warmup": 1}}
+    if args.decode_batches > 0:
+        a5 = _ap.Namespace(**{**vars(args), "hidden": c["hidden"], "layers": c["layers"], "enc": c["enc"],
+                              "decode_batches": 2})
+        d5 = bench_decode(a5, info, D, torch, dev_id)
+        rec["config5_beam4_summaries_per_sec"] = d5["beam4_summaries_per_sec"]
+        rec["config5_beam4_ms_per_batch"] = d5["beam4_ms_per_batch"]
+    return rec
 
 
 def bench_decode(args, info, D, torch, dev_id):

@@ -749,6 +749,35 @@ void attn_fwd_row_beam(const Tensor& F, const Tensor& E, const Tensor& s, const 
 }
 
 
+// beam-decode attention over one article's encoder rows for all its rep hypotheses (attention_beam.hip):
+// coverage as is (cov) or gathered from the parents (cov_src + a_src at gidx, kept in cov_keep)
+bool attn_beam_ok(int64_t A, int64_t T, int64_t rep) { return attn_beam_supported((int)A, (int)T, (int)rep); }
+int64_t attn_beam_chunks_op(int64_t Na, int64_t T) { return attn_beam_chunks((int)Na, (int)T); }
+void attn_beam(const Tensor& F, const Tensor& E, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
+               const OT& cov_src, const OT& a_src, const OT& cov_keep, const OT& gidx, const Tensor& lens,
+               const Tensor& e_buf, const Tensor& pm, const Tensor& pctx, const Tensor& a_out, const Tensor& ctx,
+               const OT& ctx_bf, int64_t R, int64_t T, int64_t A, int64_t rep, int64_t S) {
+  chk(F, BF, "F"); chk(E, BF, "E"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens");
+  chk(e_buf, F32, "e_buf"); chk(pm, F32, "pm"); chk(pctx, F32, "pctx"); chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
+  TORCH_CHECK(attn_beam_supported((int)A, (int)T, (int)rep) && R % rep == 0, "attn_beam: A = 512, rep = 4, T <= 4096");
+  TORCH_CHECK(S >= 1 && S <= 64, "attn_beam: 1 <= S <= 64 chunks");
+  const int64_t Na = R / rep;
+  numel_eq(F, Na * T * A, "F"); numel_eq(E, Na * T * A, "E"); numel_eq(s, R * A, "s"); numel_eq(v, A, "v");
+  numel_eq(lens, Na, "lens"); numel_eq(e_buf, R * T, "e_buf"); numel_eq(pm, R * S * 2, "pm");
+  numel_eq(pctx, R * S * A, "pctx"); numel_eq(a_out, R * T, "a_out"); numel_eq(ctx, R * A, "ctx");
+  chko(wc, F32, A, "wc"); chko(cov, F32, R * T, "cov"); chko(cov_src, F32, R * T, "cov_src");
+  chko(a_src, F32, R * T, "a_src"); chko(cov_keep, F32, R * T, "cov_keep"); chko(gidx, I32, R, "gidx");
+  chko(ctx_bf, BF, R * A, "ctx_bf");
+  const bool gather = PO<int>(gidx) != nullptr;
+  TORCH_CHECK(gather == (PO<float>(cov_src) != nullptr) && gather == (PO<float>(a_src) != nullptr) &&
+              gather == (PO<float>(cov_keep) != nullptr), "coverage gather: gidx, cov_src, a_src, cov_keep together");
+  TORCH_CHECK(!(gather && PO<float>(cov)), "cov (as is) and the coverage gather are exclusive");
+  launch_attn_beam(P<bf16>(F), P<bf16>(E), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), PO<float>(cov_src),
+                   PO<float>(a_src), PO<float>(cov_keep), PO<int>(gidx), P<int>(lens), P<float>(e_buf), P<float>(pm),
+                   P<float>(pctx), P<float>(a_out), P<float>(ctx), PO<bf16>(ctx_bf), (int)R, (int)T, (int)A, (int)rep,
+                   (int)S, stream());
+}
+
 // Advances step[0] by one (the last block to finish) when ctr (one zeroed uint32 scratch word)
 // is given; without ctr, beam_gather advanced it at the start of the decode step (t = step - 1).
 // att/att_hist/pg/pg_hist (optional): this step's attention rows and p_gen copied into row
@@ -933,5 +962,8 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("dec_cell_fwd_beam", &dec_cell_fwd_beam);
   m.def("beam_sproj_xmerge", &beam_sproj_xmerge);
   m.def("attn_fwd_row_beam", &attn_fwd_row_beam);
+  m.def("attn_beam_ok", &attn_beam_ok);
+  m.def("attn_beam_chunks", &attn_beam_chunks_op);
+  m.def("attn_beam", &attn_beam);
   m.def("pgen_bwd", &pgen_bwd);
 }

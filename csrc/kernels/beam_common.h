@@ -105,9 +105,9 @@ __device__ __forceinline__ void beam_article_tail(const BeamTail& bt, int a, flo
   }
   if (bt.att_hist) {
     const size_t th = (size_t)min(t, bt.max_dec - 1);
+    // (att was written by the previous launch; each row workgroup stores its own pg_hist entry)
     for (int i = lane; i < beam * bt.T; i += blockDim.x)
       bt.att_hist[(th * R + base) * bt.T + i] = bt.att[(size_t)base * bt.T + i];
-    if (bt.pg_hist && lane < beam) bt.pg_hist[th * R + base + lane] = bt.pg[base + lane];
   }
   if (is_done || t >= bt.max_dec) {
     if (lane < beam) bt.gidx[base + lane] = base + lane;

@@ -34,6 +34,14 @@ void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const flo
                          float* dcov_out, int B, int T, int A, hipStream_t st);
 
 bool attn_rowp_supported(int A, int T, int EG);
+// beam decode: one article's F / E read once for its rep = 4 hypotheses, positions split in S
+// chunks + a merge launch (attention_beam.hip)
+bool attn_beam_supported(int A, int T, int rep);
+int attn_beam_chunks(int Na, int T);
+void launch_attn_beam(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc, const float* cov,
+                      const float* cov_src, const float* a_src, float* cov_keep, const int* cg, const int* lens,
+                      float* e_buf, float* pm, float* pctx, float* a_out, float* ctx, bf16* ctx_bf, int R, int T,
+                      int A, int rep, int S, hipStream_t st);
 void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const float* v, const float* wc,
                           const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* gx,
                           bf16* gx_bf, int B, int T, int A, const int* dlen, int step, hipStream_t st);

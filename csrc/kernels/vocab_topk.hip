@@ -472,6 +472,12 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     out_lp[(size_t)r * K + tid] = __logf(pv_s[2][tid]);
   }
   if (bt.lp_sum) {  // uniform
+    // this row's own p_gen history entry (the article tail must not read the p_gen of the
+    // article's other rows: those are plain stores of other workgroups of this launch)
+    if (tid == 0 && bt.pg_hist) {
+      const size_t th = (size_t)min(*bt.step - 1, bt.max_dec - 1);
+      bt.pg_hist[th * ((size_t)bt.Na * beam) + r] = pg;
+    }
     if (tid < K) {  // this row's candidates as tagged granules (see beam_article_tail)
       const unsigned long long hi = ((unsigned long long)((unsigned)(*bt.step) & 0x7fffu) << 17) |
                                     (unsigned)(pi_s[2][tid] & 0x1ffff);

@@ -23,6 +23,7 @@
 #include <sys/stat.h>
 #include <thread>
 #include <unistd.h>
+#include <vector>
 
 namespace {
 
@@ -184,6 +185,128 @@ void ring_release(void* hp, int unlink) {
   close(r->fd);
   if (unlink) shm_unlink(r->name.c_str());
   delete r;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Ring pipes: native forwarding threads between rings (no Python, no GIL on the record path).
+//
+//   fanout: one source ring -> n destination rings; record k goes to dst[(k / group) % n], so
+//           with group = rows per batch every destination receives whole, consecutive batches
+//           (a stream worker's packer processes each build the batches of their own groups, and
+//           the trainer reads the packers' outputs round-robin: the serial batch order);
+//           end of stream at the source closes every destination.
+//   fanin:  n source rings -> one destination ring, each record forwarded the moment it lands
+//           (whichever source has one: emit-immediately, Issue-6); the destination is closed
+//           once every source is closed and drained (if close_dst).
+// Both poll with the rings' own backoff; ring_pipe_stop() makes them exit within ~50 ms.
+namespace {
+
+struct Pipe {
+  std::thread th;
+  std::atomic<int> stop{0};
+  std::atomic<int64_t> count{0};
+  std::atomic<int> err{0};  // 0 ok, -2 a destination was closed by its consumer, -4 source pop error
+};
+
+// blocking push that honours the stop flag; false when stopped or the destination closed
+bool pipe_push(Pipe* p, void* dst, const void* buf, uint32_t len) {
+  for (;;) {
+    int rc = ring_push(dst, buf, len, 50);
+    if (rc == 0) return true;
+    if (rc == -2 || rc == -3) {
+      p->err.store(rc, std::memory_order_relaxed);
+      return false;
+    }
+    if (p->stop.load(std::memory_order_relaxed)) return false;
+  }
+}
+
+// pop into a growable buffer: >= 0 length, -1 timeout, -2 closed and drained
+int64_t pipe_pop(void* src, std::string& buf, int64_t timeout_ms) {
+  for (;;) {
+    uint64_t need = 0;
+    int64_t n = ring_pop(src, &buf[0], buf.size(), timeout_ms, &need);
+    if (n != -3) return n;
+    buf.resize(size_t(need) * 2);
+  }
+}
+
+void fanout_main(Pipe* p, void* src, std::vector<void*> dsts, int64_t group) {
+  std::string buf(1 << 16, '\0');
+  const int64_t n = int64_t(dsts.size());
+  int64_t k = 0;
+  while (!p->stop.load(std::memory_order_relaxed)) {
+    int64_t len = pipe_pop(src, buf, 50);
+    if (len == -1) continue;
+    if (len < 0) break;  // end of stream
+    if (!pipe_push(p, dsts[size_t((k / group) % n)], buf.data(), uint32_t(len))) break;
+    ++k;
+    p->count.store(k, std::memory_order_relaxed);
+  }
+  for (void* d : dsts) ring_close_writer(d);
+}
+
+void fanin_main(Pipe* p, std::vector<void*> srcs, void* dst, int close_dst) {
+  std::string buf(1 << 16, '\0');
+  std::vector<char> live(srcs.size(), 1);
+  size_t nlive = srcs.size();
+  int64_t k = 0, idle_us = 1;
+  while (nlive && !p->stop.load(std::memory_order_relaxed)) {
+    bool any = false;
+    for (size_t i = 0; i < srcs.size(); ++i) {
+      if (!live[i]) continue;
+      int64_t len = pipe_pop(srcs[i], buf, 0);
+      if (len == -1) continue;
+      if (len < 0) {  // closed and drained
+        live[i] = 0;
+        --nlive;
+        continue;
+      }
+      any = true;
+      if (!pipe_push(p, dst, buf.data(), uint32_t(len))) { nlive = 0; break; }
+      p->count.store(++k, std::memory_order_relaxed);
+    }
+    if (any) {
+      idle_us = 1;
+    } else if (nlive) {
+      std::this_thread::sleep_for(std::chrono::microseconds(idle_us));
+      idle_us = idle_us < 500 ? idle_us * 2 : 500;
+    }
+  }
+  if (close_dst) ring_close_writer(dst);
+}
+
+}  // namespace
+
+extern "C" {
+
+void* ring_fanout_start(void* src, void** dsts, int n, int64_t group) {
+  if (!src || n < 1 || group < 1) return nullptr;
+  auto* p = new Pipe;
+  p->th = std::thread(fanout_main, p, src, std::vector<void*>(dsts, dsts + n), group);
+  return p;
+}
+
+void* ring_fanin_start(void** srcs, int n, void* dst, int close_dst) {
+  if (!dst || n < 1) return nullptr;
+  auto* p = new Pipe;
+  p->th = std::thread(fanin_main, p, std::vector<void*>(srcs, srcs + n), dst, close_dst);
+  return p;
+}
+
+int64_t ring_pipe_count(void* hp) { return static_cast<Pipe*>(hp)->count.load(); }
+void ring_pipe_stop(void* hp) { static_cast<Pipe*>(hp)->stop.store(1); }
+
+// join and free: records forwarded, or the (negative) error
+int64_t ring_pipe_join(void* hp) {
+  auto* p = static_cast<Pipe*>(hp);
+  if (p->th.joinable()) p->th.join();
+  const int e = p->err.load();
+  const int64_t c = p->count.load();
+  delete p;
+  return e ? int64_t(e) : c;
 }
 
 }  // extern "C"

@@ -94,6 +94,57 @@ def test_attn_fwd_row_matches_fp32(A, Na, rep):
         assert err < (1e-2 if name == "ctx_bf" else 2e-3), (name, err)
 
 
+@pytest.mark.parametrize("Na,T,S,gather", [(64, 400, 0, True), (16, 300, 0, False), (6, 300, 5, True),
+                                            (3, 37, 64, True)])
+def test_attn_beam_matches_fp32(Na, T, S, gather):
+    """attn_beam (attention_beam.hip: one article's F / E read once for its 4 hypotheses, the
+    positions split in S chunks + merge) against fp32: scores, softmax, context; coverage as is
+    or gathered from the parent rows (cov = cov_src[g] + a_src[g], kept in cov_keep).  S = 64 at
+    T = 37 leaves most chunks empty; lens of 1 and T."""
+    k = ops()
+    A, rep = 512, 4
+    B = Na * rep
+    S = S or int(k.attn_beam_chunks(Na, T))
+    gen = torch.Generator(device="cuda").manual_seed(Na * 7 + T)
+    dev = "cuda"
+
+    def r(*shape, s=1.0):
+        return torch.randn(*shape, generator=gen, device=dev) * s
+
+    lens = torch.randint(1, T + 1, (Na,), generator=gen, device=dev, dtype=torch.int32)
+    lens[0] = T
+    lens[-1] = 1
+    E, F = r(Na, T, A, s=0.5).bfloat16(), r(Na, T, A, s=0.5).bfloat16()
+    s, v, wc = r(B, A, s=0.3), r(A, s=0.1), r(A, s=0.5)
+    rl = lens.long().repeat_interleave(rep)
+    mask = torch.arange(T, device=dev)[None, :] < rl[:, None]
+    cov_src = torch.rand(B, T, generator=gen, device=dev) * mask
+    a_src = torch.rand(B, T, generator=gen, device=dev) * mask * 0.1
+    gidx = (torch.arange(B, device=dev) // rep * rep + torch.randint(0, rep, (B,), generator=gen, device=dev)).int()
+    cov = cov_src[gidx.long()] + a_src[gidx.long()] if gather else cov_src
+    e_buf, pm, pctx = torch.zeros(B, T, device=dev), torch.zeros(B, S, 2, device=dev), torch.zeros(B, S, A, device=dev)
+    a = torch.full((B, T), float("nan"), device=dev)
+    ctx, ctx_bf = torch.zeros(B, A, device=dev), torch.zeros(B, A, device=dev, dtype=torch.bfloat16)
+    keep = torch.zeros(B, T, device=dev)
+    if gather:
+        k.attn_beam(F, E, s, v, wc, None, cov_src, a_src, keep, gidx, lens, e_buf, pm, pctx, a, ctx, ctx_bf, B, T, A,
+                    rep, S)
+    else:
+        k.attn_beam(F, E, s, v, wc, cov_src, None, None, None, None, lens, e_buf, pm, pctx, a, ctx, ctx_bf, B, T, A,
+                    rep, S)
+    torch.cuda.synchronize()
+    Fr, Er = F.float().repeat_interleave(rep, 0), E.float().repeat_interleave(rep, 0)
+    e = torch.einsum("bta,a->bt", torch.tanh(Fr + s[:, None, :] + wc[None, None, :] * cov[:, :, None]), v)
+    a_ref = torch.softmax(e.masked_fill(~mask, float("-inf")), -1)
+    ctx_ref = torch.einsum("bt,bta->ba", a_ref, Er)
+    checks = [("a", a, a_ref), ("ctx", ctx, ctx_ref), ("ctx_bf", ctx_bf.float(), ctx_ref)]
+    if gather:
+        checks.append(("cov_keep", keep * mask, cov * mask))
+    for name, got, ref in checks:
+        err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        assert err < (1e-2 if name == "ctx_bf" else 2e-3), (name, err)
+
+
 @pytest.mark.parametrize("A", [512, 1024])
 def test_attn_bwd_row_matches_fp32(A):
     """attn_bwd_row (one workgroup per row) against the fp32 reference of the fused attention

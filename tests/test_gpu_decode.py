@@ -360,8 +360,12 @@ def test_fused_decode_step_equals_unfused(coverage, pointer_gen, H):
         assert d.fused_step
         d.fused_step = fused
         hy = d.decode(batch)
-        res.append(([h.tokens for h in hy], [h.avg_log_prob for h in hy], [np.stack(h.attn_dists) for h in hy]))
+        res.append(([h.tokens for h in hy], [h.avg_log_prob for h in hy], [np.stack(h.attn_dists) for h in hy],
+                    [np.array(h.p_gens, dtype=np.float64) if pointer_gen else None for h in hy]))
     assert res[0][0] == res[1][0]
     np.testing.assert_allclose(res[0][1], res[1][1], rtol=1e-6)
     for a, b in zip(res[0][2], res[1][2]):
         np.testing.assert_array_equal(a, b)
+    if pointer_gen:  # p_gen histories (each row workgroup stores its own entry in the fused step)
+        for a, b in zip(res[0][3], res[1][3]):
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)

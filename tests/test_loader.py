@@ -119,6 +119,9 @@ def test_dp_ranks_threaded_batcher_disjoint(tmp_path):
             got += [tuple(int(x) for x in b.enc_batch[r, :b.enc_lens[r]]) for r in range(int(b.valid.sum()))]
         bt.stop()
     assert sorted(got) == sorted(_ref_inputs(pattern, vocab, hps))
+    # without a shared seed each rank would shuffle the files differently: shards would overlap
+    with pytest.raises(ValueError, match="seed"):
+        Batcher(pattern, vocab, hps, single_pass=True, seed=None, rank=0, world=3)
 
 
 def test_crashed_worker_is_not_end_of_data(tmp_path, monkeypatch):

@@ -17,7 +17,7 @@ from __future__ import annotations
 import json
 from typing import Dict, List, Optional, Sequence, Union
 
-from ..data.example_proto import decode_example, encode_example
+from ..data.example_proto import decode_example, encode_example, string_row_encoder
 from .types import DataTypes, Row, TableSchema, coerce
 
 INPUT_TF_EXAMPLE_CONFIG = "input_tf_example_config"
@@ -35,6 +35,8 @@ class ExampleCoding:
         for t in self.types:
             if t in (DataTypes.FLOAT_16, DataTypes.UINT_8):
                 raise RuntimeError(f"Unsupported data type of {t}")
+        # all-STRING schemas (the streaming rows) take the precomputed fast path
+        self._fast = string_row_encoder(self.names) if all(t == DataTypes.STRING for t in self.types) else None
 
     def _fields(self, row) -> List:
         if isinstance(row, dict):
@@ -45,6 +47,8 @@ class ExampleCoding:
         vals = self._fields(row)
         if len(vals) != len(self.names):
             raise ValueError(f"row arity {len(vals)} != schema arity {len(self.names)}")
+        if self._fast is not None:
+            return self._fast(vals)
         feats = {}
         for n, t, v in zip(self.names, self.types, vals):
             if v is None:

@@ -89,6 +89,9 @@ class HParams:
     grad_compress: str = "none"    # DP gradient all-reduce wire format: none (fp32) | bf16
     loader_workers: int = -1       # GPU training input pipeline: N worker processes (0 = threaded Batcher,
                                    # -1 = min(8, CPUs - 2)); see data/loader.py
+    stream_packers: int = -1       # streaming (Flink-API) GPU workers: N packer processes parse rows into
+                                   # engine batches (0 = on the engine thread, -1 = min(12, CPUs - 3));
+                                   # see data/stream_pack.py
 
     # ------------------------------------------------------------------ helpers
     def replace(self, **kw) -> "HParams":

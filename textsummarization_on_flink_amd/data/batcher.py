@@ -65,6 +65,10 @@ class Batcher:
         fixes the shared file order)."""
         if not 0 <= rank < world:
             raise ValueError(f"rank {rank} outside world {world}")
+        if world > 1 and seed is None:
+            # the k % world record shards are disjoint only if every rank walks the same file
+            # order, which the shared seed fixes
+            raise ValueError("data-parallel Batcher (world > 1) needs a seed shared by every rank")
         self._shard = (rank, world)
         self._file_seed = seed
         self._data_path = data_path

@@ -70,6 +70,40 @@ def encode_example(features: Dict[str, object]) -> bytes:
     return _ld(1, entries)
 
 
+def _vi(n: int) -> bytes:
+    """Varint of a non-negative length (one- and two-byte fast paths)."""
+    if n < 128:
+        return bytes((n,))
+    if n < 16384:
+        return bytes(((n & 0x7F) | 0x80, n >> 7))
+    return _varint(n)
+
+
+def string_row_encoder(names):
+    """Encoder for rows whose features are all single strings (the streaming rows
+    ``uuid, article, reference`` / ``uuid, article, summary, reference``): byte-identical to
+    ``encode_example({name: [value]})`` with the constant key parts precomputed -- ~5x less
+    Python per row on the driver's hot path (one record per streamed row)."""
+    order = sorted(range(len(names)), key=lambda i: names[i])
+    keys = [(i, _ld(1, names[i].encode("utf-8"))) for i in order]
+
+    def encode(vals) -> bytes:
+        parts = []
+        for i, kb in keys:
+            v = vals[i]
+            if v is None:
+                continue
+            b = v if isinstance(v, (bytes, bytearray)) else str(v).encode("utf-8")
+            bl = b"\x0a" + _vi(len(b)) + b            # BytesList.value
+            ft = b"\x0a" + _vi(len(bl)) + bl          # Feature.bytes_list
+            ent = kb + b"\x12" + _vi(len(ft)) + ft    # map entry {key, value}
+            parts.append(b"\x0a" + _vi(len(ent)) + ent)
+        body = b"".join(parts)
+        return b"\x0a" + _vi(len(body)) + body
+
+    return encode
+
+
 def _skip(buf, pos, wt):
     if wt == 0:
         _, pos = _read_varint(buf, pos)

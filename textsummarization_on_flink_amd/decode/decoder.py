@@ -52,6 +52,22 @@ def split_sentences(decoded_words: List[str]) -> List[str]:
     return sents
 
 
+def decoded_words(ids: List[int], vocab, article_oovs) -> List[str]:
+    """Token ids after [START] -> words (in-article OOVs restored), cut at the first [STOP]."""
+    words = V.outputids2words([int(t) for t in ids], vocab, article_oovs)
+    if V.STOP_DECODING in words:
+        words = words[:words.index(V.STOP_DECODING)]
+    return words
+
+
+def flink_summary(ids: List[int], vocab, article_oovs, reference_sents, html_escape: bool = False):
+    """(summary, reference) of a result row (decode.py:159-185): sentences of the decoded words
+    joined with two spaces, reference sentences joined with one."""
+    dec = [make_html_safe(s, html_escape) for s in split_sentences(decoded_words(ids, vocab, article_oovs))]
+    refs = [make_html_safe(s, html_escape) for s in reference_sents]
+    return "  ".join(dec), " ".join(refs)
+
+
 def get_decode_dir_name(hps, ckpt_name: Optional[str]) -> str:
     dp = hps.data_path
     if "train" in dp:
@@ -109,11 +125,7 @@ class BeamSearchDecoder:
 
     # ------------------------------------------------------------------ per example
     def hyp_to_words(self, best, batch, row: int = 0) -> List[str]:
-        ids = [int(t) for t in best.tokens[1:]]
-        words = V.outputids2words(ids, self.vocab, batch.art_oovs[row] if self.hps.pointer_gen else None)
-        if V.STOP_DECODING in words:
-            words = words[:words.index(V.STOP_DECODING)]
-        return words
+        return decoded_words(best.tokens[1:], self.vocab, batch.art_oovs[row] if self.hps.pointer_gen else None)
 
     def handle(self, best, batch, row: int = 0, mode: str = "auto"):
         words = self.hyp_to_words(best, batch, row)
@@ -196,8 +208,8 @@ class BeamSearchDecoder:
         return None
 
     # ------------------------------------------------------------------ writers
-    def write_for_flink(self, uuid, article, decoded_words, reference_sents):
-        dec = [make_html_safe(s, self.html_escape) for s in split_sentences(decoded_words)]
+    def write_for_flink(self, uuid, article, words, reference_sents):
+        dec = [make_html_safe(s, self.html_escape) for s in split_sentences(words)]
         refs = [make_html_safe(s, self.html_escape) for s in reference_sents]
         self.writer.write_result(uuid, article, "  ".join(dec), " ".join(refs))
 

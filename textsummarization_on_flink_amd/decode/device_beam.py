@@ -63,6 +63,11 @@ class DeviceBeamDecoder:
         # it, else the multi-block kernels over the transposed features (EngineConfig.decode_row_attn)
         self.k = self.eng.k
         self.row_attn = self.eng.cfg.decode_row_attn and bool(self.k.attn_row_ok(self.eng.A, T))
+        # the article-level kernel (attention_beam.hip): each article's F / E read once for all its
+        # beam hypotheses, the positions split over S workgroups + a merge launch
+        self.beam_attn = self.row_attn and self.eng.cfg.decode_beam_attn and self.rep == self.beam and \
+            bool(self.k.attn_beam_ok(self.eng.A, T, self.rep))
+        self.S = int(self.k.attn_beam_chunks(self.Na, T)) if self.beam_attn else 0
         self.eng.keep_ft = not self.row_attn  # the multi-block score kernel reads transposed features
         self.dev = self.eng.dev
         # decode_batches: run batch n + 1's encoder on a side stream beside batch n's decode
@@ -120,6 +125,10 @@ class DeviceBeamDecoder:
         if self.keep_attn:
             b["ATT_hist"] = z(D, R, T)
             b["PG_hist"] = z(D, R)
+        if self.beam_attn:
+            b["e_buf"] = z(R, T)
+            b["pm"] = z(R, self.S, 2)
+            b["pctx"] = z(R, self.S, A)
         self.b = b
 
     def refresh_weights(self):
@@ -195,6 +204,10 @@ class DeviceBeamDecoder:
         was already accumulated into ``cov`` by beam_gather)."""
         k, b, eng = self.k, self.b, self.eng
         R, T, A = self.R, self.T, eng.A
+        if self.beam_attn:
+            k.attn_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], cov, None, None, None, None, b["lens_att"],
+                        b["e_buf"], b["pm"], b["pctx"], att_out, ctx_out, ctx_bf, R, T, A, self.rep, self.S)
+            return
         if self.row_attn:
             k.attn_fwd_row(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], cov, b["lens_att"], att_out, None,
                            None, ctx_out, ctx_bf, R, T, A, self.rep)
@@ -265,9 +278,15 @@ class DeviceBeamDecoder:
                                 self.Xtab, b["gidx"], b["latest"], b["x"], R, H, A, E, V, unk)
         else:
             k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A, None, 0)
-        k.attn_fwd_row_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], X["COV"] if cov else None,
-                            X["ATT"] if cov else None, Y["COV"] if cov else None, b["gidx"], b["lens_att"], Y["ATT"],
-                            Y["CTX"], Y["CTXb"], R, T, A, self.rep)
+        if self.beam_attn:
+            k.attn_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], None, X["COV"] if cov else None,
+                        X["ATT"] if cov else None, Y["COV"] if cov else None, b["gidx"] if cov else None,
+                        b["lens_att"], b["e_buf"], b["pm"], b["pctx"], Y["ATT"], Y["CTX"], Y["CTXb"], R, T, A,
+                        self.rep, self.S)
+        else:
+            k.attn_fwd_row_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], X["COV"] if cov else None,
+                                X["ATT"] if cov else None, Y["COV"] if cov else None, b["gidx"], b["lens_att"],
+                                Y["ATT"], Y["CTX"], Y["CTXb"], R, T, A, self.rep)
         k.linear2(Y["H"], H, Y["CTXb"], A, eng.pk["OUTmT"], p[OUT_B], None, None, b["outb"], R, H)
         ptr, hist = hps.pointer_gen, self.keep_attn
         k.vocab_topk_beam(b["outb"], self.owT, p[OV], Y["CTX"] if ptr else None, Y["C"] if ptr else None,
@@ -405,37 +424,64 @@ class DeviceBeamDecoder:
         ev.record()
         return {k: v.numpy() for k, v in pin.items()}, ev
 
+    FLUSH = object()  # a ``decode_batches`` input item: "no batch ready now, finish the pending one"
+
+    def _rows_ok(self, bt):
+        if bt.enc_batch.shape[0] != self.Na:
+            raise ValueError(f"batch has {bt.enc_batch.shape[0]} rows, engine expects {self.Na}")
+        return bt
+
+    @staticmethod
+    def _n_valid(bt) -> int:
+        nv = getattr(bt, "n_valid", None)  # a PackedBatch from a packer process
+        return int(nv) if nv is not None else int(bt.valid.sum())
+
     def decode_batches(self, batches):
         """Decode a sequence of Batches, yielding each batch's hypotheses, with the host work
         pipelined behind the GPU: a batch's result buffers are snapshotted into pinned memory
         (double-buffered) before the next batch's prologue, and backtracked on the host while
         the next batch's encoder and first decode chunk run.  Same results as ``decode`` per
-        batch; the last batch is finished after the loop."""
+        batch; the last batch is finished after the loop.
+
+        ``batches`` may yield ``FLUSH`` (a streaming source with nothing queued): the pending
+        batch is finished and yielded at once instead of waiting for the next batch (a result
+        must not lag behind the next request, Issue-6)."""
         pending, slot = None, 0
-
-        def rows_ok(bt):
-            if bt is not None and bt.enc_batch.shape[0] != self.Na:
-                raise ValueError(f"batch has {bt.enc_batch.shape[0]} rows, engine expects {self.Na}")
-            return bt
-
         it = iter(batches)
         ov = self.overlap_encoder
-        batch = rows_ok(next(it, None))
-        if batch is not None and ov:
-            self._encode_launch(batch)
-        # overlap_encoder: batch n + 1's encoder runs on a side stream beside batch n's decode steps
-        while batch is not None:
-            nxt = rows_ok(next(it, None))
+        batch, pre = None, False
+        while True:
+            if batch is None:
+                batch = next(it, None)
+                if batch is self.FLUSH:
+                    batch = None
+                    if pending is not None:
+                        yield self._finish(pending)
+                        pending = None
+                    continue
+                if batch is None:
+                    break
+                self._rows_ok(batch)
+                pre = False
+                if ov:
+                    self._encode_launch(batch)
+                    pre = True
+            # overlap_encoder: batch n + 1's encoder runs on a side stream beside batch n's decode steps
+            nxt = next(it, None) if ov else None
+            if nxt is self.FLUSH:
+                nxt = None  # polled again once this batch is queued
+            elif nxt is not None:
+                self._rows_ok(nxt)
             first = True
-            for _ in self.run_chunks(batch, pre_encoded=ov, next_batch=nxt if ov else None):
+            for _ in self.run_chunks(batch, pre_encoded=pre, next_batch=nxt):
                 if first and pending is not None:  # the GPU has this batch's work queued
                     yield self._finish(pending)
                     pending = None
                 first = False
             arrays, ev = self._snapshot(slot)
             slot ^= 1
-            pending = (arrays, ev, int(batch.valid.sum()), self.steps_run)
-            batch = nxt
+            pending = (arrays, ev, self._n_valid(batch), self.steps_run)
+            batch, pre = nxt, nxt is not None
         if pending is not None:
             yield self._finish(pending)
 
@@ -543,7 +589,7 @@ class DeviceBeamDecoder:
         if batch.enc_batch.shape[0] != self.Na:
             raise ValueError(f"batch has {batch.enc_batch.shape[0]} rows, engine expects {self.Na}")
         self.run(batch)
-        hyps = self.results(int(batch.valid.sum()))  # synchronises
+        hyps = self.results(self._n_valid(batch))  # synchronises
         self.eng.check_lstm_err()  # the encoder ran the persistent LSTM: never emit garbage summaries
         self._check_tail(int(self.b["tail_err"].item()))
         return hyps

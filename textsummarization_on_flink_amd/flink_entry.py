@@ -56,24 +56,99 @@ def _hps(context):
     return parse_hyperparam_string(context.properties.get(key, ""))
 
 
-def training_on_flink(context, hps, info: DistInfo):
+def _gpu() -> bool:
+    # device_count() does not initialise the GPU: packer processes are forked after this
+    return torch.cuda.device_count() > 0
+
+
+def _stream_packers(context, hps) -> int:
+    """Packer processes for this stream worker (0 = rows are parsed on the engine thread): GPU
+    workers with an input ring and a static-shape engine (``data/stream_pack.py``)."""
+    from textsummarization_on_flink_amd.data.stream_pack import default_packers
+    if not _gpu() or context._in is None or context.input_coding is None:
+        return 0
+    if hps.mode == "train" and not hps.pad_enc_to_max:
+        return 0
+    if hps.mode == "decode" and (max(1, hps.decode_batch) == 1 or context._out is None):
+        return 0
+    return default_packers(hps)
+
+
+def training_on_flink(context, hps, info: DistInfo, packer=None):
+    """Stream rows -> batches -> trainer.  With ``packer`` (a ``StreamTrainPacker`` forked
+    before the GPU was touched) the batches come pre-packed from its processes; the batch
+    sequence is the one ``FlinkTrainBatcher`` builds."""
     from textsummarization_on_flink_amd import cli
     from textsummarization_on_flink_amd.data.batcher import FlinkTrainBatcher
     from textsummarization_on_flink_amd.train.loop import setup_training
     vocab, hps = cli.default_setup(hps, info)
     if hps.mode != "train":
         raise ValueError("The 'mode' flag must be one of train/eval/decode")
-    pad = hps.max_enc_steps if torch.cuda.is_available() else None
-    batcher = SyncedBatcher(FlinkTrainBatcher(context.reader(), vocab, hps, pad_enc_to=pad), info)
-    setup_training(hps, vocab, batcher, info=info, metrics=cli.metrics_for(hps, info))
+    if packer is not None:
+        inner = packer
+    else:
+        pad = hps.max_enc_steps if (_gpu() and hps.pad_enc_to_max) else None
+        inner = FlinkTrainBatcher(context.reader(), vocab, hps, pad_enc_to=pad)
+    try:
+        setup_training(hps, vocab, SyncedBatcher(inner, info), info=info, metrics=cli.metrics_for(hps, info))
+    finally:
+        if packer is not None:
+            packer.stop()
 
 
-def inference_on_flink(context, hps):
+def _serve_packed(context, hps, vocab, pool):
+    """Streaming decode at engine speed: pre-packed batches from the packer processes ->
+    pipelined device beam search -> best token ids back to the packer that holds the batch's
+    strings (it writes the result rows; a native fanin forwards them to the output ring)."""
+    from collections import deque
+    import time
+    from textsummarization_on_flink_amd import cli
+    from textsummarization_on_flink_amd.decode.decoder import SECS_UNTIL_NEW_CKPT
+    from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
+    params, _, _ = cli.load_params_for_decode(hps, vocab, "cuda")
+    dev = DeviceBeamDecoder(hps, vocab, params, n_articles=hps.decode_batch, T=hps.max_enc_steps,
+                            use_graph=hps.graph, keep_attn=False)
+    fifo = deque()
+    t_load = time.time()
+
+    def batches():
+        nonlocal t_load
+        while True:
+            if not fifo and not hps.single_pass and time.time() - t_load > SECS_UNTIL_NEW_CKPT:
+                cli.load_params_into(hps, params)  # nothing in flight: reload (decode.py:155-157)
+                dev.refresh_weights()
+                t_load = time.time()
+            b = pool.poll(block=not fifo)
+            if b is pool.NOT_READY:
+                yield dev.FLUSH
+                continue
+            if b is None:
+                return
+            fifo.append(b)
+            yield b
+
+    n = 0
+    for hyps in dev.decode_batches(batches()):
+        b = fifo.popleft()
+        pool.send_results(b, [[int(t) for t in h.tokens[1:]] for h in hyps])
+        n += len(hyps)
+    pool.close()
+    log.info("stream decode: %d articles", n)
+    return n
+
+
+def inference_on_flink(context, hps, pool=None):
     from textsummarization_on_flink_amd import cli
     from textsummarization_on_flink_amd.data.batcher import FlinkInferenceBatcher
-    if torch.cuda.is_available():
+    if _gpu():
         torch.cuda.set_device(context.get_index() % torch.cuda.device_count())
     vocab, hps = cli.default_setup(hps)
+    if pool is not None:
+        try:
+            return _serve_packed(context, hps, vocab, pool)
+        except BaseException:
+            pool.stop()
+            raise
     writer = FlinkWriter(context)
     reader = context.reader()
     dec = cli.build_decoder(hps, vocab, lambda h, n, pad: FlinkInferenceBatcher(
@@ -82,17 +157,38 @@ def inference_on_flink(context, hps):
     dec.decode(with_rouge=False)
 
 
+def _fork_packers(context, hps):
+    """Fork the stream packer processes (before anything initialises the GPU)."""
+    from textsummarization_on_flink_amd.data.vocab import Vocab
+    n = _stream_packers(context, hps)
+    if not n:
+        return None
+    vocab = Vocab(hps.vocab_path, hps.vocab_size)
+    if hps.mode == "train":
+        from textsummarization_on_flink_amd.data.stream_pack import StreamTrainPacker
+        return StreamTrainPacker(context._in, context.input_coding, vocab, hps, n, hps.max_enc_steps)
+    from textsummarization_on_flink_amd.data.stream_pack import StreamDecodePacker
+    hd = hps.replace(batch_size=hps.beam_size)  # default_setup's decode-mode batch size
+    return StreamDecodePacker(context._in, context._out, context.input_coding, context.output_coding, vocab, hd, n,
+                              max(1, hps.decode_batch), hps.max_enc_steps, hps.stream_max_wait_ms / 1000.0)
+
+
 def main_on_flink(context):
     hps = _hps(context)
     if context.get_role_name() == "ps":
         raise ValueError("ps role is not supported (ps_num must be 0): gradients are all-reduced across workers")
-    if hps.mode == "train":
-        info = init_from_env(timeout_s=hps.dist_timeout_s)
-        training_on_flink(context, hps, info)
-    elif hps.mode == "decode":
-        inference_on_flink(context, hps)
-    else:
+    if hps.mode not in ("train", "decode"):
         raise ValueError("The 'mode' flag must be one of train/eval/decode")
+    packers = _fork_packers(context, hps)
+    try:
+        if hps.mode == "train":
+            info = init_from_env(timeout_s=hps.dist_timeout_s)
+            training_on_flink(context, hps, info, packers)
+        else:
+            inference_on_flink(context, hps, packers)
+    finally:
+        if packers is not None:
+            packers.stop()
 
 
 class AbstractFlinkWriter:

@@ -43,6 +43,11 @@ def lib():
             "ring_records_out": (u64, [vp]),
             "ring_capacity": (u64, [vp]),
             "ring_release": (None, [vp, i32]),
+            "ring_fanout_start": (vp, [vp, C.POINTER(vp), i32, i64]),
+            "ring_fanin_start": (vp, [C.POINTER(vp), i32, vp, i32]),
+            "ring_pipe_count": (i64, [vp]),
+            "ring_pipe_stop": (None, [vp]),
+            "ring_pipe_join": (i64, [vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

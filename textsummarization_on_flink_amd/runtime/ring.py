@@ -99,6 +99,56 @@ class RecordRing:
             pass
 
 
+class RingPipe:
+    """A native forwarding thread between rings (``shm_ring.cpp`` ring pipes; no GIL on the
+    record path).  ``fanout``: record k of ``src`` -> ``dsts[(k // group) % n]``, the
+    destinations closed at the source's end of stream.  ``fanin``: every record of any source
+    -> ``dst`` the moment it lands, ``dst`` closed once all sources are closed and drained."""
+
+    def __init__(self, handle, keep):
+        if not handle:
+            raise OSError("cannot start ring pipe")
+        self._h, self._keep = handle, keep  # keep the rings alive while the thread uses them
+
+    @classmethod
+    def fanout(cls, src: RecordRing, dsts, group: int = 1) -> "RingPipe":
+        arr = (C.c_void_p * len(dsts))(*[d._h for d in dsts])
+        return cls(lib().ring_fanout_start(src._h, arr, len(dsts), int(group)), (src, list(dsts)))
+
+    @classmethod
+    def fanin(cls, srcs, dst: RecordRing, close_dst: bool = True) -> "RingPipe":
+        arr = (C.c_void_p * len(srcs))(*[s._h for s in srcs])
+        return cls(lib().ring_fanin_start(arr, len(srcs), dst._h, int(close_dst)), (list(srcs), dst))
+
+    @property
+    def count(self) -> int:
+        return int(lib().ring_pipe_count(self._h)) if self._h else -1
+
+    def stop(self) -> None:
+        if self._h:
+            lib().ring_pipe_stop(self._h)
+
+    def join(self) -> int:
+        """Wait for the thread; records forwarded (raises if a destination was closed early)."""
+        if not self._h:
+            return 0
+        n = int(lib().ring_pipe_join(self._h))
+        self._h = None
+        if n == -2:
+            raise RingClosed("ring pipe: a destination ring was closed by its consumer")
+        if n < 0:
+            raise OSError(f"ring pipe failed: {n}")
+        return n
+
+    def __del__(self):
+        try:
+            if self._h:
+                self.stop()
+                lib().ring_pipe_join(self._h)
+        except Exception:
+            pass
+
+
 class RingDrainer(threading.Thread):
     """Consumer thread: pops records and calls ``on_record`` immediately (Issue-6 fix)."""
 
