@@ -38,6 +38,7 @@ bool attn_rowp_supported(int A, int T, int EG);
 // chunks + a merge launch (attention_beam.hip)
 bool attn_beam_supported(int A, int T, int rep);
 int attn_beam_chunks(int Na, int T);
+bool attn_beam_chunk_ok(int T, int S);
 void launch_attn_beam(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc, const float* cov,
                       const float* cov_src, const float* a_src, float* cov_keep, const int* cg, const int* lens,
                       float* e_buf, float* pm, float* pctx, float* a_out, float* ctx, bf16* ctx_bf, int R, int T,
@@ -135,10 +136,11 @@ struct PgIn {
   const float* ctx; const float* c; const bf16* h; const float* x; const float* w; const float* b; float* out;
   int A, H, E;
 };
+size_t vocab_topk_cand_floats(int R, int V, int H);
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
-                       int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st,
-                       const BeamTail* bt = nullptr);
+                       float* vcand, const unsigned* cmask, int R, int V, int H, int T, int K, int beam, PgIn pgi,
+                       hipStream_t st, const BeamTail* bt = nullptr);
 int vocab_train_tiles(int V, int H);
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
                             float* zg, float* lse, float* pv, int N, int V, int H, const int* vblk, const int* vblk_n,

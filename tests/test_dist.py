@@ -220,3 +220,57 @@ def test_lstm_error_on_one_rank_skips_the_step_on_all_ranks():
     for r in (0, 1):
         finite, g0, healthy_finite = res[r]
         assert not finite and g0 == 2.0 and healthy_finite
+
+
+@pytest.mark.parametrize("defer", [True, False])
+def test_bucket_issue_order_leaves_only_the_embedding(defer):
+    """GraphTrainer's replay order (train/trainer.py replay_phases / issue_plan) with a recording
+    reducer over the real flat-gradient layout of the bench model: every bucket except the
+    embedding's is issued before the last phase graph is queued, so at most the 25.6 MB embedding
+    gradient is all-reduced with nothing left to overlap; with the decoder weight gradients
+    deferred beside the encoder BPTT their bucket goes out right after that phase."""
+    from textsummarization_on_flink_amd.config import HParams
+    from textsummarization_on_flink_amd.models.params import FlatParams, param_specs
+    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
+    from textsummarization_on_flink_amd.parallel.dist import DistInfo, GradAllReducer
+    from textsummarization_on_flink_amd.train.trainer import BPTT_PHASE, issue_plan, replay_phases
+
+    hps = HParams(coverage=True)
+    specs = param_specs(hps, 50000)
+    offs, o = {}, 0
+    for sp in specs:
+        n = 1
+        for d in sp.shape:
+            n *= d
+        offs[sp.name] = o
+        o += n
+    bounds = [offs[nm] for nm in HipPointerGenerator.PHASE_FIRST_PARAM]
+    red = GradAllReducer(torch.zeros(o), DistInfo(0, 2, 0, "gloo"), bounds=bounds, average=False)
+    assert len(red.buckets) == 4
+    events = []
+
+    class G:
+        def __init__(self, i):
+            self.i = i
+
+        def replay(self):
+            events.append(("graph", self.i))
+
+    class Rec:
+        def bucket_ready(self, b):
+            events.append(("bucket", b))
+
+        def wait_issued(self):
+            events.append(("wait",))
+
+    replay_phases([G(i) for i in range(4)], Rec(), issue_plan(defer), BPTT_PHASE, lstm_exclusive=True)
+    issued_before_last = {e[1] for e in events[:events.index(("graph", 3))] if e[0] == "bucket"}
+    assert issued_before_last == {0, 1, 2}
+    assert events.index(("bucket", 0)) == events.index(("graph", 0)) + 1
+    assert events.index(("wait",)) == events.index(("graph", BPTT_PHASE)) - 1  # no RCCL beside the full-grid BPTT
+    if defer:
+        assert events.index(("bucket", 1)) == events.index(("graph", 2)) + 1
+    else:
+        assert events.index(("bucket", 1)) == events.index(("graph", 1)) + 1
+    left = sum(red.buckets[b].numel() * 4 for b in range(4) if b not in issued_before_last)
+    assert left == 50000 * 128 * 4 <= 26 * 2 ** 20  # the embedding only

@@ -803,10 +803,12 @@ class HipPointerGenerator:
         return out
 
     # ------------------------------------------------------------------ backward
-    # The backward runs in three phases so a data-parallel trainer can all-reduce each
+    # The backward runs in four phases so a data-parallel trainer can all-reduce each
     # phase's gradient bucket while the next phase computes (the flat gradient is laid out
-    # in this order: output_projection | decoder + attention | reduce_states + encoder + emb).
-    PHASE_FIRST_PARAM = (f"{DEC}/AttnOutputProjection/Linear/Matrix", f"{P}/reduce_final_st/w_reduce_c")
+    # in this order: output_projection | decoder + attention | reduce_states + encoder | emb).
+    # The embedding (25.6 MB at V = 50k) is its own last bucket, so the only all-reduce left
+    # after the last kernel is the embedding's.
+    PHASE_FIRST_PARAM = (f"{DEC}/AttnOutputProjection/Linear/Matrix", f"{P}/reduce_final_st/w_reduce_c", EMB)
 
     def phase_bounds(self):
         return [self.p.offsets[n][0] for n in self.PHASE_FIRST_PARAM]
@@ -815,6 +817,11 @@ class HipPointerGenerator:
         self.backward_head()
         self.backward_mid()
         self.backward_tail()
+
+    def backward_tail(self):
+        """reduce_states, encoder BPTT, encoder weights (bucket 2), embedding (bucket 3)."""
+        self.backward_tail_enc()
+        self.backward_tail_emb()
 
     def backward_head(self):
         """Vocab projection gradients (the 51 MB output_projection bucket)."""
@@ -1045,8 +1052,9 @@ class HipPointerGenerator:
         torch.addmm(dE2, dFb, self.pk["Wh"].t(), out_dtype=F32, out=dE2)
         self._dE = dE
 
-    def backward_tail(self):
-        """reduce_states, encoder BPTT, embedding (the last bucket)."""
+    def backward_tail_enc(self):
+        """reduce_states, encoder BPTT and weight gradients; joins the deferred decoder weight
+        gradients (buckets 1 and 2 are complete when this phase ends)."""
         k, w, p = self.k, self.w, self.p
         B, T, H = self.B, self.T, self.H
         g = p.g
@@ -1072,7 +1080,6 @@ class HipPointerGenerator:
         torch.mm(w["rs_cat"][1].t(), w["rs_dp"][1], out_dtype=F32, out=g(RH))
         # ---- encoder BPTT, top layer down
         d_in = dE
-        gemb = g(EMB)
         for layer in reversed(range(self.L)):
             st = self.enc[layer]
             din = st["din"]
@@ -1105,11 +1112,18 @@ class HipPointerGenerator:
             dx = st["dx"]
             k.from_step_frame(dxs, w["rev_idx"], dx, B, T, din)  # fw + reversed bw, batch frame
             d_in = dx
+        self._d_in = d_in
+        if late:
+            torch.cuda.current_stream().wait_stream(self._late_stream)  # the deferred weight gradients
+
+    def backward_tail_emb(self):
+        """Embedding gradient of the encoder and decoder token rows (the last bucket)."""
+        k, w, p = self.k, self.w, self.p
+        B, T = self.B, self.T
+        gemb, d_in = p.g(EMB), self._d_in
         # encoder + decoder token rows in id order (the order is sorted on the host with the
         # batch, emb_sort; one launch, embedding.hip): atomics only where the id changes, so
         # Zipf-hot tokens do not serialise
-        if late:
-            torch.cuda.current_stream().wait_stream(self._late_stream)  # d_emb_dec and the weight gradients
         if self.det:
             k.emb_grad_det(gemb, w["emb_sid"], w["emb_perm"], d_in.reshape(B * T, self.E), w["d_emb_dec"],
                            w["emb_pf"], w["emb_pl"])

@@ -49,6 +49,35 @@ def check_lstm_err(engine) -> None:
     engine.check_lstm_err()
 
 
+# phase graphs of a step: 0 forward + vocab backward, 1 decoder backward, 2 encoder backward
+# (+ the joined deferred decoder weight gradients), 3 embedding gradient; gradient buckets
+# (HipPointerGenerator.phase_bounds): 0 output projection, 1 decoder + attention, 2 reduce_states
+# + encoder, 3 embedding
+BPTT_PHASE = 2
+
+
+def issue_plan(defer_wgrad: bool):
+    """Buckets whose all-reduce is issued after each phase graph (the last bucket, the embedding,
+    is issued by the reducer call after the last graph).  With the decoder weight gradients
+    deferred beside the encoder BPTT, bucket 1 completes with phase 2."""
+    return [[0], [] if defer_wgrad else [1], [1, 2] if defer_wgrad else [2], []]
+
+
+def replay_phases(graphs, reducer, plan, bptt_phase: int, lstm_exclusive: bool, ev=None):
+    """Replay the phase graphs, issuing each bucket's all-reduce as soon as its phase has been
+    queued (RCCL runs it on its own stream behind that work) -- overlapped with the later phases.
+    ``lstm_exclusive``: the persistent BPTT fills the chip, so the device waits for the issued
+    all-reduces before that phase (no RCCL kernel shares the GPU with it)."""
+    for i, g in enumerate(graphs):
+        if i == bptt_phase and lstm_exclusive:
+            reducer.wait_issued()
+        g.replay()
+        if ev:
+            ev[i + 1].record()
+        for b in plan[i]:
+            reducer.bucket_ready(b)
+
+
 class GraphTrainer:
     def __init__(self, hps, vsize: int, B: int, T: int, device="cuda", info: Optional[DistInfo] = None,
                  params: Optional[FlatParams] = None, use_graph: bool = True, bucket_mb: float = 32.0):
@@ -66,7 +95,7 @@ class GraphTrainer:
         if self.info.enabled:
             broadcast_params(params.accum, self.info)
         self.engine = HipPointerGenerator(hps, vsize, params, B=B, T=T)
-        # buckets = backward phases: output_projection | decoder+attention | encoder+embedding;
+        # buckets = backward phases: output_projection | decoder+attention | encoder | embedding;
         # each is all-reduced while the following phase computes (RCCL over xGMI); the
         # 1/world average happens inside the optimizer kernel
         self.reducer = GradAllReducer(params.grad, self.info, bucket_mb=bucket_mb,
@@ -121,15 +150,17 @@ class GraphTrainer:
         self.engine.pack()
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        # three graphs (forward + vocab backward | decoder backward | encoder backward) so each
-        # gradient bucket's all-reduce overlaps the next phase
-        self.g_fb = [torch.cuda.CUDAGraph() for _ in range(3)]
+        # four graphs (forward + vocab backward | decoder backward | encoder backward |
+        # embedding gradient) so each gradient bucket's all-reduce overlaps the next phase
+        self.g_fb = [torch.cuda.CUDAGraph() for _ in range(4)]
         with torch.cuda.graph(self.g_fb[0], pool=pool):
             self.out = self._fwd_head()
         with torch.cuda.graph(self.g_fb[1], pool=pool):
             self.engine.backward_mid()
-        with torch.cuda.graph(self.g_fb[-1], pool=pool):
-            self.engine.backward_tail()
+        with torch.cuda.graph(self.g_fb[2], pool=pool):
+            self.engine.backward_tail_enc()
+        with torch.cuda.graph(self.g_fb[3], pool=pool):
+            self.engine.backward_tail_emb()
         self.g_opt = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_opt, pool=pool):
             self._opt()
@@ -145,16 +176,8 @@ class GraphTrainer:
             if ev:
                 ev[0].record()
             ng = len(self.g_fb)
-            for i, g in enumerate(self.g_fb):
-                if i == ng - 1 and self.lstm_exclusive:
-                    self.reducer.wait_issued()  # no RCCL kernel beside the full-grid persistent BPTT
-                g.replay()
-                if ev:
-                    ev[i + 1].record()
-                if i == 0:
-                    self.reducer.bucket_ready(0)
-                elif i == 1 and not self.engine.defer_wgrad:  # else bucket 1 completes beside the encoder BPTT
-                    self.reducer.bucket_ready(1)
+            replay_phases(self.g_fb, self.reducer, issue_plan(self.engine.defer_wgrad), BPTT_PHASE,
+                          self.lstm_exclusive, ev)
             self._maybe_poison()
             self.reducer()
             if ev:
@@ -178,11 +201,11 @@ class GraphTrainer:
 
     def phase_ms(self) -> Dict[str, float]:
         """Time of each phase of the last step (host-synchronising): forward + vocab backward,
-        decoder backward, encoder backward, exposed all-reduce wait, optimizer."""
+        decoder backward, encoder backward, embedding gradient, exposed all-reduce wait, optimizer."""
         if not self._ev:
             return {}
         self._ev[-1].synchronize()
-        names = ("ms_fwd_head", "ms_bwd_dec", "ms_bwd_enc", "ms_allreduce", "ms_optimizer")
+        names = ("ms_fwd_head", "ms_bwd_dec", "ms_bwd_enc", "ms_bwd_emb", "ms_allreduce", "ms_optimizer")
         return {n: self._ev[i].elapsed_time(self._ev[i + 1]) for i, n in enumerate(names)}
 
     def _maybe_poison(self):
