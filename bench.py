@@ -11,7 +11,7 @@ Weak scaling: the per-GPU batch is fixed, global batch = batch x N.
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 
 Multi-GPU: one process per GPU, torch.distributed over RCCL (backend "nccl"), gradients
-all-reduced in three buckets overlapped with the backward.  Either launch it with
+all-reduced in four buckets overlapped with the backward.  Either launch it with
 ``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` (RANK /
 WORLD_SIZE / MASTER_* come from the environment), or run ``python bench.py --gpus N``
 directly: without WORLD_SIZE in the environment this process starts the N rank processes
@@ -19,8 +19,8 @@ itself (torchrun-style env, rendezvous on 127.0.0.1) before anything touches the
 relays their output and exits with the worst exit code.  ``n_gpus`` in the JSON is the
 world size the process group reports.
 
-Timed region per step: H2D copy of the batch, forward + backward (three hipGraph
-replays), gradient all-reduce (RCCL), clip + Adagrad + weight repack (a fourth hipGraph)
+Timed region per step: H2D copy of the batch, forward + backward (four phase-graph
+replays), gradient all-reduce (RCCL), clip + Adagrad + weight repack (the optimizer hipGraph)
 -- the complete optimizer step; only synthetic text generation/tokenisation is done ahead
 of time (like a prefetching loader).  The W warmup steps include the graph captures.
 
@@ -29,6 +29,11 @@ every rank decodes ``--decode-batches`` batches of 64 articles x beam 4 (hipGrap
 device beam search, fresh random-init weights, encoder included, host backtracking
 included, tokenisation excluded); the value is the sum over ranks of completed summaries
 divided by the slowest rank's wall time.  ``--decode-batches 0`` skips it.
+
+Secondary (BASELINE config #5, ``config5_tokens_per_sec`` / ``config5_beam4_summaries_per_sec``):
+hidden 512, 2-layer encoder, enc 800, per-GPU batch 1024, ``--config5-steps`` timed steps after
+one warm-up (graph capture) step, the same timed region as the headline; then 2 beam-4 decode
+batches at that size.  ``--config5-steps 0`` skips it.
 """
 import argparse
 import json
@@ -197,7 +202,11 @@ def main(argv=None):
     if args.config5_steps > 0 and args.hidden != 512:
         del tr, batches
         torch.cuda.empty_cache()
-        c5 = bench_config5(args, info, D, torch, dev_id)
+        try:
+            c5 = bench_config5(args, info, D, torch, dev_id)
+        except torch.cuda.OutOfMemoryError as e:  # the headline line must still be printed
+            c5 = {"config5_error": str(e).splitlines()[0][:200]}
+            torch.cuda.empty_cache()
 
     if info.is_chief:
         rec = {

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--layers", type=int, default=1, help="encoder bi-LSTM layers (config #5: 2)")
     ap.add_argument("--enc", type=int, default=400, help="max encoder steps (config #5: 800)")
+    ap.add_argument("--unfused-step", action="store_true",
+                    help="A/B: the 8-launch decode step (separate beam_step) instead of the fused beam tail")
     args = ap.parse_args()
     import torch
     from textsummarization_on_flink_amd.config import HParams
@@ -45,6 +47,8 @@ def main():
     params = build_params(hps, vocab.size(), device="cuda")
     dec = DeviceBeamDecoder(hps, vocab, params, n_articles=args.articles, T=hps.max_enc_steps,
                             use_graph=not args.no_graph, keep_attn=False)
+    if args.unfused_step:
+        dec.fused_step = False
     for b in batches[:args.warmup]:
         dec.decode(b)
     torch.cuda.synchronize()
@@ -79,7 +83,7 @@ def main():
                                           f"dec<=100 vocab={args.vocab} enc_layers={args.layers}",
                                  "beam": args.beam, "articles_per_batch": args.articles,
                                  "rows": args.articles * args.beam, "graph": not args.no_graph,
-                                 "pipelined": args.pipelined}}))
+                                 "pipelined": args.pipelined, "fused_step": bool(dec.fused_step)}}))
 
 
 if __name__ == "__main__":

@@ -525,8 +525,9 @@ void vocab_train_bwd(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
   numel_eq(lse, N, "lse"); numel_eq(alpha, N, "alpha"); numel_eq(dl, N * V, "dl"); chko(dbias, F32, V, "dbias");
   const int64_t RB = (N + 31) / 32;
   const bool has = vblk.has_value();
-  TORCH_CHECK(vblk_n.has_value() == has && vlive.has_value() == has && vstate.has_value() == has,
-              "vblk, vblk_n, vlive and vstate go together");
+  // vblk + vblk_n alone: compacted dlogits (live block j -> rows 32 j ..); with vlive + vstate: in place
+  TORCH_CHECK(vblk_n.has_value() == has && vlive.has_value() == vstate.has_value() && (has || !vlive.has_value()),
+              "vblk and vblk_n go together, vlive and vstate go together (and need vblk)");
   chko(vblk, I32, RB, "vblk"); chko(vblk_n, I32, 1, "vblk_n"); chko(vlive, I32, RB, "vlive");
   chko(vstate, I32, RB, "vstate");
   launch_vocab_train_bwd(P<bf16>(X), (int)ldx, P<bf16>(WT), P<float>(bias), P<int>(target), P<float>(lse), P<float>(alpha),

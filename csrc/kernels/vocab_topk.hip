@@ -56,23 +56,26 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 // largest maxima (vocab_select), each of whose top-8 is in its list.  Copied words (ids of the
 // article's in-article tokens, a per-article bitmap) get their exact logit stored in place for
 // the pointer mixture.  Replaced storing every fp32 logit (51 MB per step at 256 x 50k).
+// bias of the lane's columns from the tile's LDS copy (bl = the wave's first column in it; -inf past V)
 template <int NI>
-__device__ __forceinline__ void vl_values(const f32x4 (&acc)[NI][4], int jr, const f32x2 (&bc)[NI][2],
+__device__ __forceinline__ void vl_values(const f32x4 (&acc)[NI][4], int jr, const float* bl, int lane,
                                           f32x2 (&x)[NI][2]) {
+  const int q4 = 4 * (lane >> 4);
 #pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      x[i][h] = f32x2{acc[i][jr][2 * h], acc[i][jr][2 * h + 1]} + bc[i][h];  // bc = -inf past V
+  for (int i = 0; i < NI; ++i) {
+    const float4 b4 = *reinterpret_cast<const float4*>(bl + 16 * i + q4);
+    x[i][0] = f32x2{acc[i][jr][0], acc[i][jr][1]} + f32x2{b4.x, b4.y};
+    x[i][1] = f32x2{acc[i][jr][2], acc[i][jr][3]} + f32x2{b4.z, b4.w};
+  }
 }
 
 // phase 1: (max, sum exp) of the row over the wave's 64 columns, and t_wave
 template <int NI>
-__device__ __forceinline__ void vl_stats(const f32x4 (&acc)[NI][4], int jr, const f32x2 (&bc)[NI][2], float* Pm,
-                                         float* Ps, float* Tw, int lane) {
+__device__ __forceinline__ void vl_stats(const f32x4 (&acc)[NI][4], int jr, const float* bl, float* Pm, float* Ps,
+                                         float* Tw, int lane) {
   constexpr float L2E = 1.4426950408889634f;
   f32x2 x[NI][2];
-  vl_values<NI>(acc, jr, bc, x);
+  vl_values<NI>(acc, jr, bl, lane, x);
   float m1 = -INFINITY, m2 = -INFINITY;  // the lane's two largest
 #pragma unroll
   for (int i = 0; i < NI; ++i)
@@ -107,24 +110,44 @@ __device__ __forceinline__ void vl_stats(const f32x4 (&acc)[NI][4], int jr, cons
 // phase 2: append the values >= t_tile to the (row, tile) candidate list; exact logits of the
 // article's copied words in place
 template <int NI>
-__device__ __forceinline__ void vl_emit(const f32x4 (&acc)[NI][4], int jr, const f32x2 (&bc)[NI][2], float tt,
-                                        int* cnt, float2* __restrict__ cand, float* __restrict__ logits,
-                                        const unsigned* cmrow, int row, int cw, int ct, int lane, int V) {
+__device__ __forceinline__ void vl_emit(const f32x4 (&acc)[NI][4], int jr, const float* bl, float tt, int* cnt,
+                                        float2* __restrict__ cand, float* __restrict__ logits, const unsigned* cmrow,
+                                        int row, int cw, int ct, int lane, int V) {
   f32x2 x[NI][2];
-  vl_values<NI>(acc, jr, bc, x);
+  vl_values<NI>(acc, jr, bl, lane, x);
   const int q4 = 4 * (lane >> 4);
+  // the lane's candidates: count, ONE LDS slot reservation, then the stores
+  unsigned sel = 0;
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int o4 = cw - ct + 16 * i + q4;  // column - tile start of the lane's 4 consecutive columns
-    const unsigned bits = cmrow ? cmrow[o4 >> 5] >> (o4 & 31) : 0u;
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float v = e & 1 ? x[i][e >> 1].y : x[i][e >> 1].x;
-      if (v >= tt) {
-        const int slot = atomicAdd(cnt, 1);
-        cand[slot] = make_float2(v, __int_as_float(o4 + e));
+      sel |= (unsigned)(v >= tt) << (4 * i + e);
+    }
+  if (sel) {
+    int slot = atomicAdd(cnt, __builtin_popcount(sel));
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if ((sel >> (4 * i + e)) & 1u) {
+          const float v = e & 1 ? x[i][e >> 1].y : x[i][e >> 1].x;
+          cand[slot++] = make_float2(v, __int_as_float(cw - ct + 16 * i + q4 + e));
+        }
+  }
+  if (cmrow) {  // copied words (a few per row and tile): their exact logits in place
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int o4 = cw - ct + 16 * i + q4;  // column - tile start of the lane's 4 consecutive columns
+      const unsigned bits = (cmrow[o4 >> 5] >> (o4 & 31)) & 15u;
+      if (bits) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = e & 1 ? x[i][e >> 1].y : x[i][e >> 1].x;
+          if (((bits >> e) & 1u) && ct + o4 + e < V) logits[(size_t)row * V + ct + o4 + e] = v;
+        }
       }
-      if (((bits >> e) & 1u) && ct + o4 + e < V) logits[(size_t)row * V + ct + o4 + e] = v;
     }
   }
 }
@@ -151,6 +174,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   __shared__ float Pm[4][BR], Ps[4][BR], Tw[4][VT_ROWS];
   __shared__ int cnt_s[BR];
   __shared__ unsigned cm_s[BR][VT_COLS / 32];  // each row's article's copied-word bits over this tile
+  __shared__ __attribute__((aligned(16))) float bias_s[VT_COLS];
   __shared__ __attribute__((aligned(16))) bf16 Xs[BR * (HMAX + 8)];  // X tile of the block
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // XCD-aware order: the RB row blocks of one vocab tile get block ids equal mod 8 (one XCD
@@ -182,16 +206,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   for (int h = 0; h < KS; ++h)
 #pragma unroll
     for (int i = 0; i < NI; ++i) wa[h][i] = ld8(arow[i] + min(32 * h, H - 32));
-  // bias of the lane's columns cw + 16 i + q4 + r, pairs (r = 2h, 2h + 1); -inf past V
-  const int q4 = 4 * (lane >> 4);
-  f32x2 bc[NI][2];
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int col = cw + 16 * i + q4 + 2 * h;
-      bc[i][h] = f32x2{col < V ? bias[col] : -INFINITY, col + 1 < V ? bias[col + 1] : -INFINITY};
-    }
+  // the tile's bias -> LDS (-inf past V)
+  for (int c = threadIdx.x; c < VT_COLS; c += 256) {
+    const int col = vt * VT_COLS + c;
+    bias_s[c] = col < V ? bias[col] : -INFINITY;
+  }
+  const float* bl = bias_s + (cw - vt * VT_COLS);
 #pragma unroll
   for (int u = 0; u < XPT; ++u) {
     const int c = threadIdx.x + 256 * u, rr = c / (H / 8), k8 = (c % (H / 8)) * 8;
@@ -227,7 +247,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     // phase 1: per-row statistics and the wave's candidate threshold
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr)
-      vl_stats<NI>(acc, jr, bc, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, Tw[wid], lane);
+      vl_stats<NI>(acc, jr, bl, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, Tw[wid], lane);
     __syncthreads();
     // phase 2: candidates >= t_tile = max of the 4 waves' thresholds, copied words in place
 #pragma unroll
@@ -235,7 +255,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
       const int rl = 16 * jr + c16, row = rbh + rl;
       const float tt = fmaxf(fmaxf(Tw[0][rl], Tw[1][rl]), fmaxf(Tw[2][rl], Tw[3][rl]));
       if (row < R)
-        vl_emit<NI>(acc, jr, bc, tt, &cnt_s[VT_ROWS * h2 + rl], cand + ((size_t)row * nt + vt) * VT_COLS, logits,
+        vl_emit<NI>(acc, jr, bl, tt, &cnt_s[VT_ROWS * h2 + rl], cand + ((size_t)row * nt + vt) * VT_COLS, logits,
                     cmask ? cm_s[VT_ROWS * h2 + rl] : nullptr, row, cw, vt * VT_COLS, lane, V);
     }
     __syncthreads();  // Tw reused by the next half

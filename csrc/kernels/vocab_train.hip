@@ -116,7 +116,8 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     float* __restrict__ dbias,        // [V]      pass 2 (nullable): += column sums of dlogits
     int N, int V, int ldx,
     const int* __restrict__ vblk,     // nullable: the live 32-row blocks (EngineConfig.skip_pad_steps),
-    const int* __restrict__ vblk_n) { // *vblk_n of them; the units enumerate only those
+    const int* __restrict__ vblk_n,   // *vblk_n of them; the units enumerate only those
+    int compact) {                    // pass 2: live block j's dlogits go to rows 32 j .. (compacted)
   constexpr int KS = H / 32;          // k-steps of 32
   constexpr int NI = vr_ni(H), VR_COLS = vr_cols(H);
   constexpr int XS = H + 8;           // padded LDS row (bank spread)
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
             cs[i][0] += d[i][0];
             cs[i][1] += d[i][1];
           }
-          bf16* dst = dl + (size_t)row * V + cw + q4;
+          bf16* dst = dl + (size_t)(compact ? (u % RB) * VR_ROWS + rr : row) * V + cw + q4;
           if (full) {
             // (plain stores: the 4 stores of a row's 128-byte line are merged in L2; non-temporal
             // stores went to HBM as 32-byte pieces, 1.31 -> 1.75 ms)
@@ -453,7 +454,7 @@ void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float*
                             hipStream_t st) {
   const int grid = vocab_train_grid(N, V, H);
 #define VF(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
-                                  part, zg, nullptr, nullptr, nullptr, nullptr, N, V, ldx, vblk, vblk_n)
+                                  part, zg, nullptr, nullptr, nullptr, nullptr, N, V, ldx, vblk, vblk_n, 0)
   if (H == 512) VF(512);
   else if (H == 256) VF(256);
   else VF(128);
@@ -466,11 +467,14 @@ void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float*
                             const float* lse, const float* alpha, bf16* dl, float* dbias, int N, int V, int H,
                             const int* vblk, const int* vblk_n, const int* vlive, int* vstate, hipStream_t st) {
   const int grid = vocab_train_grid(N, V, H);
-  if (vblk)
+  // with the live-block list: either the dead blocks an earlier pass wrote are zeroed (vlive /
+  // vstate; dlogits in place) or, without them, the live blocks' rows are written compacted
+  const int compact = vblk && !vlive;
+  if (vblk && vlive)
     hipLaunchKernelGGL(vocab_zero_dead_kernel, dim3((N + VR_ROWS - 1) / VR_ROWS), dim3(256), 0, st, dl, vlive, vstate,
                        N, V);
 #define VB(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
-                                  nullptr, nullptr, lse, alpha, dl, dbias, N, V, ldx, vblk, vblk_n)
+                                  nullptr, nullptr, lse, alpha, dl, dbias, N, V, ldx, vblk, vblk_n, compact)
   if (H == 512) VB(512);
   else if (H == 256) VB(256);
   else VB(128);

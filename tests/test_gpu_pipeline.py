@@ -51,3 +51,49 @@ def test_streaming_fit_then_transform_on_gpu(tmp_path):
     q = [Row(*[r[k] for k in FIELDS]) for r in c.rows(10, "q")]
     app.start_inference(js, CollectionSource(q), [sink], str(tmp_path), extra, echo=False)
     assert sorted(r[0] for r in sink.rows) == sorted(f"q-{i}" for i in range(10))
+
+
+def test_stream_fit_runs_at_engine_speed(tmp_path):
+    """Throughput of the streaming fit path (rows -> worker input ring -> native fanout -> stream
+    packer processes -> GraphTrainer) against the engine alone on the same batch shape: production
+    width (hidden 256, emb 128, enc 400 -> dec 100, coverage), vocab 5k, batch 64, 40 steps.  The
+    steady-state windows of the worker's metrics must reach 70% of the engine's tokens/s (the full
+    shape: tools/stream_throughput.py, profiles/r4/)."""
+    import json
+    import time
+
+    import torch
+
+    from textsummarization_on_flink_amd.config import HParams
+    from textsummarization_on_flink_amd.data.synthetic import SyntheticCorpus, make_batches
+    from textsummarization_on_flink_amd.train.trainer import GraphTrainer
+
+    V, B, steps = 5000, 64, 40
+    c = SyntheticCorpus(vocab_size=V, seed=3)
+    c.vocab(V).save(f"{tmp_path}/vocab")
+    # the engine alone
+    hps = HParams(batch_size=B, vocab_size=V, coverage=True)
+    batches = make_batches(hps, c.vocab(V), c, 4, pad_enc_to=400)
+    tr = GraphTrainer(hps, V, B=B, T=400)
+    for b in batches[:2]:
+        tr.step(b)
+    torch.cuda.synchronize()
+    t0, toks = time.time(), 0
+    for i in range(20):
+        tr.step(batches[i % 4])
+        toks += batches[i % 4].num_tokens()
+    torch.cuda.synchronize()
+    engine_tps = toks / (time.time() - t0)
+    del tr
+    torch.cuda.empty_cache()
+    # the streaming job
+    rows = [Row(*[r[k] for k in FIELDS]) for r in c.rows(B * steps)]
+    metrics = f"{tmp_path}/m.jsonl"
+    flags = [f"--vocab_size={V}", f"--batch_size={B}", "--num_steps=0", "--check_every=10", "--tensorboard=0",
+             f"--metrics_path={metrics}"]
+    app.start_training(CollectionSource(rows), str(tmp_path), flags, flags, echo=False)
+    win = [json.loads(x) for x in open(metrics)][1:]  # the first window holds the graph capture
+    stream_tps = sum(w["tokens_per_sec"] * w["step_ms"] * w["steps"] for w in win) / sum(
+        w["step_ms"] * w["steps"] for w in win)
+    assert sum(w["steps"] for w in win) >= 30
+    assert stream_tps >= 0.7 * engine_tps, (stream_tps, engine_tps)

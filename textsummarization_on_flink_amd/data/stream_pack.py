@@ -287,27 +287,49 @@ def _decode_packer(p: int, n: int, names: List[str], coding, out_coding, vocab, 
                         raise _Orphaned() from None
                     continue
                 return
-            if rec is None:
-                raise RuntimeError("decoder closed the result ring with examples pending")
-            meta, _ = _split_record(rec)
-            ents = [pending.pop(e) for e, _ids in meta["r"]]
-            for row in finish_rows(ents, [ids for _e, ids in meta["r"]], vocab, hps, bool(hps.html_escape)):
-                _push(rfin, out_coding.encode(dict(zip(fields, row))))
+            _finish(rec)
             if block:
                 return
 
+    def _try(ring, ms):
+        try:
+            return True, ring.pop(timeout_ms=ms)
+        except TimeoutError:
+            return False, None
+
+    def _finish(rec):
+        if rec is None:
+            raise RuntimeError("decoder closed the result ring with examples pending")
+        meta, _ = _split_record(rec)
+        ents = [pending.pop(e) for e, _ids in meta["r"]]
+        for row in finish_rows(ents, [ids for _e, ids in meta["r"]], vocab, hps, bool(hps.html_escape)):
+            _push(rfin, out_coding.encode(dict(zip(fields, row))))
+
     try:
         while in_open or pending:
-            drain_results(block=False)
             if not in_open:
                 drain_results(block=True)
                 continue
-            try:  # a short wait, so finished results are never held up behind an idle input
-                rec = rin.pop(timeout_ms=2)
-            except TimeoutError:
-                if not pending and os.getppid() != ppid:
-                    raise _Orphaned() from None
-                continue
+            if pending:
+                # results outstanding: check the result ring first and only peek at the input; an
+                # idle wait is on the result ring (its poll backoff stays < 1 ms), so a finished
+                # summary is written out within a fraction of a millisecond
+                got, rr = _try(rres, 0)
+                if got:
+                    _finish(rr)
+                    continue
+                got, rec = _try(rin, 0)
+                if not got:
+                    got, rr = _try(rres, 1)
+                    if got:
+                        _finish(rr)
+                    continue
+            else:
+                got, rec = _try(rin, 2)
+                if not got:
+                    if os.getppid() != ppid:
+                        raise _Orphaned() from None
+                    continue
             if rec is None:
                 in_open = False
                 rout.close()  # no more examples from this packer

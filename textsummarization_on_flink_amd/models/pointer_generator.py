@@ -133,7 +133,7 @@ def host_inputs(batch, hps, D: int, sort_rows: bool = False) -> Dict[str, np.nda
     lr = np.zeros(nb * 32, dtype=bool)
     lr[:D * len(dlen)] = (np.arange(D)[:, None] < dlen[None, :]).reshape(-1)
     vlive = lr.reshape(nb, 32).any(1)
-    vblk = np.zeros(nb, dtype=np.int32)
+    vblk = np.full(nb, nb, dtype=np.int32)  # past vblk_n: the dummy (all-zero) block nb of the compacted head
     live_ids = np.nonzero(vlive)[0]
     vblk[:len(live_ids)] = live_ids
     return {
@@ -280,6 +280,7 @@ class HipPointerGenerator:
         # in-stream copy costs ~15 us of DMA latency ahead of the step)
         layout, off = input_layout(B, T, D)
         self._in_layout = layout
+        self._in_off = {name: o for name, o, _, _, _ in layout}
         self._in_pack = torch.zeros(off, dtype=torch.uint8, device=self.dev)
         for name, o, shp, dt, nb in layout:
             w[name] = self._in_pack[o:o + nb].view(dt).view(shp)
@@ -370,6 +371,8 @@ class HipPointerGenerator:
         # (row, step) pairs past the row's last loss-weighted step are skipped by the projected
         # kernels (their outputs are written as zeros; loss and gradients are unchanged)
         self.skip_pad = self.proj_attn and cfg.skip_pad_steps
+        self.compact_vocab = self.skip_pad and cfg.fused_vocab_train and cfg.compact_vocab_grad and not cfg.deterministic \
+            and H in (128, 256, 512) and (D * B) % 32 == 0
         w["F"] = z(B, T, A, dt=BF)
         # transposed copy for the lanes-over-positions score kernel (not needed by the row
         # kernels; the beam decoder sets keep_ft to get it from _encoder_forward)
@@ -392,8 +395,12 @@ class HipPointerGenerator:
         w["e"] = z(B, T)
         w["covloss"] = z(D, B)
         # [outb | 1 | 0...]: the ones column makes the output-projection weight-gradient GEMM
-        # also produce the bias gradient (one read of dlogits instead of two)
-        w["outb_ext"] = z(D * B, H + 8, dt=BF)
+        # also produce the bias gradient (one read of dlogits instead of two).  One extra all-zero
+        # 32-row block after the D * B rows: the dummy block the compacted vocab head gathers for
+        # its padding (see backward_head)
+        nblk = (D * B + 31) // 32
+        w["outb_blk"] = z(nblk * 32 + 32, H + 8, dt=BF)
+        w["outb_ext"] = w["outb_blk"][:D * B]
         w["outb_ext"][:, H] = 1.0
         w["outb"] = w["outb_ext"][:, :H]
         w["pg"] = z(D, B)
@@ -412,6 +419,11 @@ class HipPointerGenerator:
         w["logits"] = z(D * B, V, dt=BF)
         # backward
         w["dlogits"] = w["logits"]
+        # compacted vocab head (skip_pad with the fused head, not deterministic mode): pass 2 writes the
+        # live 32-row blocks' dlogits to consecutive rows, and the two gradient GEMMs run over the
+        # live rows only, rounded up to one of a few block counts (one captured graph each)
+        self.vocab_buckets = sorted({max(1, -(-nblk * f // 8)) for f in (4, 5, 6, 7, 8)})
+        self.nbk = self.vocab_buckets[-1]
         w["dpre"] = z(D, B)
         w["dA"] = z(D, B, T)
         w["DCTX"] = z(D, B, A)
@@ -592,6 +604,10 @@ class HipPointerGenerator:
             hn[:] = np.frombuffer(packed, dtype=np.uint8)
         else:
             pack_host_inputs(host_inputs(batch, self.hps, self.D, sort_rows=self.skip_pad), self._in_layout, hn)
+        if self.compact_vocab:  # this batch's live vocab-head blocks -> the head's block-count bucket
+            o = self._in_off["vblk_n"]
+            nlive = int(np.frombuffer(hn, dtype=np.int32, count=1, offset=o)[0])
+            self.nbk = next(b for b in self.vocab_buckets if b >= nlive)
         cur = torch.cuda.current_stream()
         cs = self._copy_stream
         with torch.cuda.stream(cs):
@@ -756,9 +772,10 @@ class HipPointerGenerator:
                          w["dA"] if (need_grad and hps.pointer_gen) else None, N, B, T)
             if need_grad:
                 w["dbias"].zero_()
+                inplace = vb is not None and not self.compact_vocab  # else compacted (or every block)
                 k.vocab_train_bwd(w["outb_ext"], self.pk["owT"], p[OV], w["target_t"], w["lse"], w["alpha"],
                                   w["dlogits"], None if self.det else w["dbias"], N, V, H, ldx, vb, vn,
-                                  w["vlive"] if vb is not None else None, w["vstate"] if vb is not None else None)
+                                  w["vlive"] if inplace else None, w["vstate"] if inplace else None)
                 if self.det:  # column sums of the bf16 dlogits in a fixed order
                     torch.sum(w["dlogits"], 0, dtype=F32, out=w["dbias"])
             return
@@ -842,6 +859,8 @@ class HipPointerGenerator:
             o = p.offsets[OW][0]
             m, dst = H + 1, p.grad[o:o + (H + 1) * V].view(H + 1, V)
         N = self.D * self.B
+        if self.compact_vocab:
+            return self._backward_head_compact(g, dl, H, V, N)
 
         def dw():
             Sw = 4
@@ -860,6 +879,38 @@ class HipPointerGenerator:
         # dX = dlogits . W^T unsplit (split-K over vocab chunks measured slower at B = 256:
         # profiles/r2/ab/vocab_grad_split.jsonl)
         self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
+
+    def _backward_head_compact(self, g, dl, H, V, N):
+        """Vocab gradients over the live rows only: pass 2 wrote live block j's dlogits to rows
+        32 j .. 32 j + 31; the GEMMs run over nbk blocks (the batch's bucket, >= its live block count;
+        the padding gathers the all-zero dummy block nb of outb_ext, so the stale dlogits rows past the
+        live ones contribute exact zeros to dW) and dX is scattered back to the t-major rows (dead
+        rows: dlogits 0, so dX 0).  Same sums as the full GEMMs up to the split-K order."""
+        w = self.w
+        nbk, M = self.nbk, self.nbk * 32
+        nb = (N + 31) // 32
+        idx = w["vblk"][:nbk].long()
+        ob = w["outb_blk"].view(nb + 1, 32, H + 8)
+        if not hasattr(self, "_outb_c"):
+            self._outb_c = torch.zeros(nb * 32, H + 8, dtype=BF, device=self.dev)
+            self._dout_ext = torch.zeros(nb + 1, 32, H, dtype=F32, device=self.dev)
+        xc = self._outb_c[:M]
+        torch.index_select(ob, 0, idx, out=xc.view(nbk, 32, H + 8))
+        dlc = dl[:M]
+        g(OV).copy_(w["dbias"])
+        dst = g(OW)
+        Sw = 4 if M % 4 == 0 and (M // 4) * V < 2 ** 31 else 1
+        if Sw > 1:  # split K = M in 4 (one batched GEMM + a sum), as the full head
+            parts = torch.bmm(xc.view(Sw, M // Sw, H + 8)[:, :, :H].transpose(1, 2), dlc.view(Sw, M // Sw, V),
+                              out_dtype=F32)
+            torch.sum(parts, 0, out=dst)
+        else:
+            torch.mm(xc[:, :H].t(), dlc, out_dtype=F32, out=dst)
+        dxc = torch.mm(dlc, self.pk["ow"].t(), out_dtype=F32)  # [M, H]
+        de = self._dout_ext
+        de.zero_()
+        de.index_copy_(0, idx, dxc.view(nbk, 32, H))  # padding entries land in the dummy block nb
+        self._dout = de[:nb].view(nb * 32, H)[:N]
 
     def _cast_colsum(self, x, bias_grad):
         """bf16 copy of x [N, C] plus bias_grad += its column sums in one read of x (the

@@ -131,6 +131,17 @@ class GraphTrainer:
         self.engine.backward_head()
         return out
 
+    class _Phase0:
+        """Phase graph 0 = the forward graph + the vocab-gradient graph of the batch's live-block
+        bucket (HipPointerGenerator.compact_vocab: one head graph per block count)."""
+
+        def __init__(self, trainer):
+            self.t = trainer
+
+        def replay(self):
+            self.t.g_fwd.replay()
+            self.t.g_head[self.t.engine.nbk].replay()
+
     def _opt(self):
         self.engine.optimizer_step()
 
@@ -139,10 +150,17 @@ class GraphTrainer:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         snap = (self.params.flat.clone(), self.params.accum.clone())
+        eng = self.engine
+        buckets = eng.vocab_buckets if eng.compact_vocab else [eng.nbk]
         with torch.cuda.stream(s):
             for _ in range(2):
                 self._fb()
                 self._opt()
+            nbk = eng.nbk
+            for b in buckets:  # every head variant once before its capture
+                eng.nbk = b
+                eng.backward_head()
+            eng.nbk = nbk
         torch.cuda.current_stream().wait_stream(s)
         # undo the warm-up updates so capture does not change the model
         self.params.flat.copy_(snap[0])
@@ -152,15 +170,24 @@ class GraphTrainer:
         pool = torch.cuda.graph_pool_handle()
         # four graphs (forward + vocab backward | decoder backward | encoder backward |
         # embedding gradient) so each gradient bucket's all-reduce overlaps the next phase
-        self.g_fb = [torch.cuda.CUDAGraph() for _ in range(4)]
-        with torch.cuda.graph(self.g_fb[0], pool=pool):
-            self.out = self._fwd_head()
+        self.g_fb = [self._Phase0(self)] + [torch.cuda.CUDAGraph() for _ in range(3)]
+        self.g_fwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fwd, pool=pool):
+            self.out = self.engine.forward(need_grad=True)
+        nbk = eng.nbk
+        self.g_head = {}
+        for b in buckets:
+            eng.nbk = b
+            self.g_head[b] = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_head[b], pool=pool):
+                eng.backward_head()
+        eng.nbk = nbk
         with torch.cuda.graph(self.g_fb[1], pool=pool):
             self.engine.backward_mid()
         with torch.cuda.graph(self.g_fb[2], pool=pool):
-            self.engine.backward_tail_enc()
+            eng.backward_tail_enc()
         with torch.cuda.graph(self.g_fb[3], pool=pool):
-            self.engine.backward_tail_emb()
+            eng.backward_tail_emb()
         self.g_opt = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_opt, pool=pool):
             self._opt()
