@@ -679,6 +679,238 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
   }
 }
 
+// Backward with 32-row teams at H = 512 (batch > 256: batch 1024 in 2 launches instead of 4).
+// 16 waves per workgroup (4 per SIMD, 128 unified registers each).  Wave w produces the partial
+// dh of output units 32w .. 32w+31 (destined for slice w / 2) for all 32 rows: 2 x 2 MFMA
+// tiles.  Its W_hh B fragments are 2 column tiles x 8 k-chunks: tile 0 in registers (32 VGPRs),
+// tile 1 in LDS (16 waves x 8 KB = 128 KB, lane-contiguous 16-byte reads).  The cell update
+// covers 32 rows x 64 units at 2 rows per lane; hand-off protocol, tags and layouts are the
+// 16-row kernel's with 32-row slots.  (The earlier 32-row attempt -- 4 waves, all of W_hh in
+// registers -- spilled ~40 registers: profiles/r3/micro/lstm_rt2_bwd_rejected.log.)
+// base + a 32-bit byte offset: with a uniform base the access uses SGPR-base addressing and
+// one 32-bit offset register instead of a 64-bit address pair per access
+template <typename TT>
+__device__ __forceinline__ TT* boff(TT* p, unsigned bytes) {
+  return reinterpret_cast<TT*>(reinterpret_cast<char*>(const_cast<void*>(static_cast<const void*>(p))) + bytes);
+}
+__device__ __forceinline__ gu64* gboff(gu64* p, unsigned bytes) {
+  return reinterpret_cast<gu64*>(reinterpret_cast<__attribute__((address_space(1))) char*>(p) + bytes);
+}
+__device__ __forceinline__ const gu64* gboff(const gu64* p, unsigned bytes) {
+  return reinterpret_cast<const gu64*>(reinterpret_cast<const __attribute__((address_space(1))) char*>(p) + bytes);
+}
+
+#ifndef BWD32_PC
+#define BWD32_PC 2  // peers polled per chunk (4: 8 registers spill)
+#endif
+template <bool NT>
+__global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
+    bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
+    const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
+    const float* __restrict__ cs, const int* __restrict__ lens, gu64* xbuf, gu32* err,
+    float* __restrict__ dbias, int T, int B, int ntile, int tile0, int ntile_l) {
+  constexpr int H = 512, G4 = 4 * H, NC = H / 64, KS = 256 / 32, RT = 32, SLOT = RT * 64;
+  constexpr int TEAMX = 2 * NC * NC * SLOT, RPL = 2;
+  __shared__ __attribute__((aligned(16))) bf16x8 Wl[16 * KS * 64];  // [wave][kk][lane]
+  __shared__ __attribute__((aligned(16))) bf16 Ash[RT * 256];      // dz slice [32 rows][4 gates x 64 units]
+  __shared__ float Pown[RT * 64];                                  // own partial dh [32 rows][64 units]
+  int lt, c;
+  if (!team_of(NC, 2 * ntile_l, lt, c)) return;
+  const int d = lt / ntile_l, tile = tile0 + lt % ntile_l, r0 = tile * RT, team = d * ntile + tile;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int ul = (wid & 3) * 16 + (lane & 15);             // this lane's unit within the slice
+  const int row0 = (wid >> 2) * 8 + (lane >> 4) * RPL;     // its first row within the tile
+  const int u = c * 64 + ul;
+  const size_t BH = (size_t)B * H;
+  // B[k][n] = W_hh[v][gate col(k)], k = g*64 + unit-in-slice, n = output unit v = 32 wid + 16 t + (lane & 15)
+  bf16x8 Wr[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int k0 = kk * 32 + 8 * (lane >> 4), g = k0 / 64, ul0 = k0 % 64;
+    const int v = 32 * wid + (lane & 15);
+    Wr[kk] = ld8(Wn + ((size_t)d * H + v) * G4 + g * H + 64 * c + ul0);
+    Wl[(wid * KS + kk) * 64 + lane] = ld8(Wn + ((size_t)d * H + v + 16) * G4 + g * H + 64 * c + ul0);
+  }
+  int rc[RPL], ln[RPL];
+  bool rok[RPL];
+  float dcreg[RPL], dhf[RPL], cn[RPL];
+#pragma unroll
+  for (int i = 0; i < RPL; ++i) {
+    const int r = r0 + row0 + i;
+    rok[i] = r < B;
+    rc[i] = rok[i] ? r : B - 1;
+    ln[i] = rok[i] ? lens[r] : 0;
+    const size_t ri = (size_t)rc[i] * H + u;
+    dcreg[i] = dc_carry[(size_t)d * BH + ri];
+    dhf[i] = dh_fin[(size_t)d * BH + ri];
+    cn[i] = cs[((size_t)d * (T + 1) + T) * BH + ri];
+  }
+  gu64* xb = xbuf + (size_t)team * TEAMX;  // [parity][dest][src][32][64]
+  bool dead = false;
+  float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = T - 1; s >= 0; --s) {
+    int row0v = row0;
+    asm volatile("" : "+v"(row0v));
+    // uniform step bases + 32-bit per-lane byte offsets (saddr addressing: no 64-bit address
+    // pairs per row held across the step)
+    const float* dout_s = dout + ((size_t)d * T + s) * BH;
+    const float* acts_s = acts + ((size_t)d * T + s) * BH * 4;
+    const float* cs_s = cs + ((size_t)d * (T + 1) + s) * BH;
+    float dho[RPL], a4[RPL][4], cpv[RPL];
+    unsigned rio[RPL];  // rc * H + u, opaque per step (no loop-strength-reduced 64-bit pointers)
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      rio[i] = (unsigned)(rc[i] * H + u);
+      asm volatile("" : "+v"(rio[i]));
+    }
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      const unsigned ri = rio[i];
+      dho[i] = ld_f(boff(dout_s, ri * 4u), NT);
+      const f32x4 q = ld_f4(boff(acts_s, ri * 16u), NT);
+      a4[i][0] = q[0]; a4[i][1] = q[1]; a4[i][2] = q[2]; a4[i][3] = q[3];
+      cpv[i] = ld_f(boff(cs_s, ri * 4u), NT);
+    }
+    float rec[RPL];
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) rec[i] = 0.f;
+    if (s + 1 < T) {
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) rec[i] = Pown[(row0 + i) * 64 + ul];
+      constexpr int PC = BWD32_PC;
+      const gu64* src = xb + (size_t)((s + 1) & 1) * NC * NC * SLOT + (size_t)c * NC * SLOT;
+      const unsigned tag = (unsigned)(T - 1 - s);
+#pragma unroll
+      for (int p0 = 0; p0 < NC; p0 += PC) {
+        unsigned ready = 0;
+        unsigned long long x[PC][RPL];
+        constexpr unsigned allm = (1u << (RPL * PC)) - 1;
+        const unsigned need = (c >= p0 && c < p0 + PC) ? allm & ~(((1u << RPL) - 1) << (RPL * (c - p0))) : allm;
+        for (unsigned spins = 0;;) {
+          unsigned lo = (unsigned)(row0v * 64 + ul) * 8u;  // opaque per pass: not hoisted as address pairs
+          asm volatile("" : "+v"(lo));
+#pragma unroll
+          for (int q = 0; q < PC; ++q)
+#pragma unroll
+            for (int i = 0; i < RPL; ++i)
+              if (p0 + q != c && !((ready >> (q * RPL + i)) & 1))
+                x[q][i] = __hip_atomic_load(gboff(src + (p0 + q) * SLOT, lo + i * 512u), RLX_AGENT);
+#pragma unroll
+          for (int q = 0; q < PC; ++q)
+#pragma unroll
+            for (int i = 0; i < RPL; ++i) {
+              const int bit = q * RPL + i;
+              if (p0 + q != c && !((ready >> bit) & 1) && (unsigned)(x[q][i] >> 32) == tag) ready |= 1u << bit;
+            }
+          if (__all((ready & need) == need) || dead) break;
+          if (++spins > kSpinLimit / 4) {
+            if (lane == 0) __hip_atomic_store(err, 2u, RLX_AGENT);
+            dead = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(96);
+        }
+#pragma unroll
+        for (int q = 0; q < PC; ++q)
+#pragma unroll
+          for (int i = 0; i < RPL; ++i)
+            if (p0 + q != c) rec[i] += ((ready >> (q * RPL + i)) & 1) ? __uint_as_float((unsigned)x[q][i]) : 0.f;
+      }
+    }
+    // ---- cell backward -> dz (4 gates) for (the lane's rows, unit u)
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      float dzv[4];
+      if (s < ln[i]) {
+        const float dh = rec[i] + dho[i] + (s + 1 >= ln[i] ? dhf[i] : 0.f);
+        const float ig = a4[i][0], jg = a4[i][1], fg = a4[i][2], og = a4[i][3];
+        const float tc = ftanh(cn[i]);
+        const float dc = dcreg[i] + dh * og * (1.0f - tc * tc);
+        dzv[0] = dc * jg * ig * (1.0f - ig);
+        dzv[1] = dc * ig * (1.0f - jg * jg);
+        dzv[2] = dc * cpv[i] * fg * (1.0f - fg);
+        dzv[3] = dh * tc * og * (1.0f - og);
+        dcreg[i] = dc * fg;
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dzv[g] = 0.f;
+      }
+      cn[i] = cpv[i];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bacc[g] += dzv[g];
+      const int sb = swz<256>(row0 + i, ul);  // = swz(row, g * 64 + ul) - g * 64
+#pragma unroll
+      for (int g = 0; g < 4; ++g) Ash[sb + g * 64] = f2bf(dzv[g]);
+    }
+    auto store_dz = [&]() {
+#pragma unroll
+      for (int i = 0; i < RPL; ++i)
+        if (rok[i]) {
+          bf16* dz_s = dz + ((size_t)d * T + s) * B * G4;
+          const int sb = swz<256>(row0 + i, ul);
+          const unsigned o = (rio[i] + (unsigned)(rc[i] * 3 * H)) * 2u;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) st_b(boff(dz_s, o + g * H * 2u), Ash[sb + g * 64], NT);
+        }
+    };
+    if (s == 0) {
+      store_dz();
+      break;
+    }
+    __syncthreads();  // dz slice complete in LDS (and every lane has read Pown)
+    // ---- partial dh over this slice's gate columns, output units 32 wid .. +31, all 32 rows
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[rt][t] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const bf16x8 w1 = Wl[(wid * KS + kk) * 64 + lane];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Ash[swz<256>(rt * 16 + (lane & 15), kk * 32 + 8 * (lane >> 4))]);
+        acc[rt][0] = mfma16(a, Wr[kk], acc[rt][0]);
+        acc[rt][1] = mfma16(a, w1, acc[rt][1]);
+      }
+    }
+    // ---- publish: units 32 wid .. +31 are units (wid & 1) * 32 .. +31 of slice wid / 2
+    const int dw = wid >> 1, ub = (wid & 1) * 32 + (lane & 15);
+    if (dw == c) {
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Pown[(rt * 16 + (lane >> 4) * 4 + r) * 64 + ub + 16 * t] = acc[rt][t][r];
+    } else {
+      gu64* dst = xb + (size_t)(s & 1) * NC * NC * SLOT + ((size_t)dw * NC + c) * SLOT;
+      unsigned lo = (unsigned)((lane >> 4) * 4 * 64 + ub) * 8u;
+      asm volatile("" : "+v"(lo));
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            store_granule(gboff(dst, lo + (unsigned)((rt * 16 + r) * 64 + 16 * t) * 8u), (unsigned)(T - s),
+                          __float_as_uint(acc[rt][t][r]));
+    }
+    store_dz();
+    __syncthreads();  // Pown visible before the next step reads it; Ash free for rewriting
+  }
+#pragma unroll
+  for (int i = 0; i < RPL; ++i)
+    if (rok[i]) dc_carry[(size_t)d * BH + (size_t)rc[i] * H + u] = dcreg[i];
+  if (dbias) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float t = sum_x32(sum_x16(bacc[g]));  // lanes l, l^16, l^32, l^48: the wave's 4 row pairs
+      if ((lane >> 4) == 0) atomicAdd(dbias + (size_t)d * G4 + g * H + u, t);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------- launchers
 // Kernel variants (measured, tools/lstm_micro.py): the forward runs 4 waves per workgroup
 // (16 units per wave) up to H = 256 and 8 waves (8 units per wave) at H = 512, where the
@@ -713,6 +945,9 @@ int lstm_persistent_capacity(int H) {
                                                          256, 0) == hipSuccess;                                    \
     } else {                                                                                                       \
       ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[2], lstm_fwd_persistent_kernel<512, true, 2>, 256, 0) == hipSuccess; \
+      int o32 = 0;                                                                                                 \
+      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o32, lstm_bwd_persistent32_kernel<false>, 1024, 0) == hipSuccess; \
+      o[2] = min(o[2], o32);                                                                                      \
     }                                                                                                              \
   }
   OCC(64) OCC(128) OCC(256) OCC(512)
@@ -728,7 +963,18 @@ int lstm_persistent_capacity(int H) {
 // backward keeps 16: a 32-row BPTT (4 waves with two output slices each, 256 registers of W_hh,
 // inputs staged through LDS) still spilled ~40 registers and ran 36 us per step against 7.6 --
 // B = 1024: 29.1 vs 24.4 ms.
-static int lstm_rows(int H, int B, bool bwd) { return (!bwd && H == 512 && B > 256) ? 32 : 16; }
+// The backward runs 32-row teams at H = 512 above batch 256 too, with the 16-wave kernel
+// (lstm_bwd_persistent32_kernel; TSAMD_LSTM_BWD32=0 restores the 16-row BPTT).
+static bool lstm_bwd32() {
+  static const int on = [] {
+    const char* e = getenv("TSAMD_LSTM_BWD32");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+static int lstm_rows(int H, int B, bool bwd) {
+  return (H == 512 && B > 256 && (!bwd || lstm_bwd32())) ? 32 : 16;
+}
 
 // Row tiles per launch: the most whose grid (NC workgroups per (direction, tile) team,
 // teams dealt 8 at a time so members share an XCD) fits the resident capacity.  Teams are
@@ -763,8 +1009,8 @@ int lstm_persistent_launches(int H, int B) {
 
 size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {
   const int R = lstm_rows(H, B, bwd), ntile = (B + R - 1) / R, NC = H / 64;
-  // fwd: [team][parity][R rows][H/2 unit pairs]; bwd: [team][parity][dest][src][16][64]
-  return (size_t)2 * ntile * 2 * (bwd ? (size_t)NC * NC * 16 * 64 : (size_t)R * (H / 2));
+  // fwd: [team][parity][R rows][H/2 unit pairs]; bwd: [team][parity][dest][src][R][64]
+  return (size_t)2 * ntile * 2 * (bwd ? (size_t)NC * NC * R * 64 : (size_t)R * (H / 2));
 }
 
 void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
@@ -798,12 +1044,17 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, float* dbias, int T, int B, int H, hipStream_t st) {
-  const int ntile = (B + 15) / 16, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64;
+  const int R = lstm_rows(H, B, true), ntile = (B + R - 1) / R, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64;
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
   for (int t0 = 0; t0 < ntile; t0 += nl) {
     const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
+    if (R == 32) {
+      hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false>), dim3(grid), dim3(1024), 0, st, dz, Wn, dout, dh_fin,
+                         dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n);
+      continue;
+    }
 #define LAUNCH_B(HH, NTV)                                                                                                 \
   hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin,   \
                      dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)

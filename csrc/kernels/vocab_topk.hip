@@ -12,6 +12,7 @@
 //                       union copied ids).
 // Replaces a library GEMM + a separate per-element top-k pass over the logits.
 #include "common.h"
+#include <stdlib.h>
 #include "attn_common.h"  // f32x2 packed-FP32 helpers
 #include "beam_common.h"  // beam bookkeeping fused into the select kernel's tail
 #include "launchers.h"
@@ -112,7 +113,7 @@ __device__ __forceinline__ void vl_stats(const f32x4 (&acc)[NI][4], int jr, cons
 template <int NI>
 __device__ __forceinline__ void vl_emit(const f32x4 (&acc)[NI][4], int jr, const float* bl, float tt, int* cnt,
                                         float2* __restrict__ cand, float* __restrict__ logits, const unsigned* cmrow,
-                                        int row, int cw, int ct, int lane, int V) {
+                                        int row, int cw, int ct, int lane, int V, int mode) {
   f32x2 x[NI][2];
   vl_values<NI>(acc, jr, bl, lane, x);
   const int q4 = 4 * (lane >> 4);
@@ -125,8 +126,9 @@ __device__ __forceinline__ void vl_emit(const f32x4 (&acc)[NI][4], int jr, const
       const float v = e & 1 ? x[i][e >> 1].y : x[i][e >> 1].x;
       sel |= (unsigned)(v >= tt) << (4 * i + e);
     }
-  if (sel) {
+  if (sel && !(mode & 4)) {
     int slot = atomicAdd(cnt, __builtin_popcount(sel));
+    if (mode & 2) sel = 0;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -136,7 +138,7 @@ __device__ __forceinline__ void vl_emit(const f32x4 (&acc)[NI][4], int jr, const
           cand[slot++] = make_float2(v, __int_as_float(cw - ct + 16 * i + q4 + e));
         }
   }
-  if (cmrow) {  // copied words (a few per row and tile): their exact logits in place
+  if (cmrow && !(mode & 1)) {  // copied words (a few per row and tile): their exact logits in place
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int o4 = cw - ct + 16 * i + q4;  // column - tile start of the lane's 4 consecutive columns
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     float2* __restrict__ cand,      // [R][nt][VT_COLS] candidate (value, column in tile)
     int* __restrict__ ccnt,         // [R][nt] candidates per (row, tile)
     const unsigned* __restrict__ cmask,  // [R / beam][ceil(V / 32)] copied-word bitmap (nullptr: none)
-    int R, int V, int Hrt, int beam) {
+    int R, int V, int Hrt, int beam, int mode) {
   const int H = HFIX ? HMAX : Hrt;
   constexpr int BR = VT_ROWS * RH;  // rows per block
   constexpr int NI = vt_ni(HMAX), VT_COLS = vt_cols(HMAX), KS = HMAX / 32;
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
       const float tt = fmaxf(fmaxf(Tw[0][rl], Tw[1][rl]), fmaxf(Tw[2][rl], Tw[3][rl]));
       if (row < R)
         vl_emit<NI>(acc, jr, bl, tt, &cnt_s[VT_ROWS * h2 + rl], cand + ((size_t)row * nt + vt) * VT_COLS, logits,
-                    cmask ? cm_s[VT_ROWS * h2 + rl] : nullptr, row, cw, vt * VT_COLS, lane, V);
+                    cmask ? cm_s[VT_ROWS * h2 + rl] : nullptr, row, cw, vt * VT_COLS, lane, V, mode);
     }
     __syncthreads();  // Tw reused by the next half
   }
@@ -277,6 +279,16 @@ namespace {
 __device__ __forceinline__ int vhslot(int w) { return (int)(((unsigned)w * 2654435761u) >> 21) & (VM_HASH - 1); }
 
 }  // namespace
+
+// A/B instrumentation (TSAMD_VL_MODE, timing only -- results are wrong for mode != 0):
+// bit 0 skips the copied-word stores, bit 1 the candidate stores, bit 2 the slot reservation too
+static int vl_mode() {
+  static const int m = [] {
+    const char* e = getenv("TSAMD_VL_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
 
 #define VS_THREADS 1024  // 256 threads measured 16.6 us vs 14.0 at R = 256 (fewer loads in flight)
 #define VS_NONE 0x7fffffff  // sentinel id: (-inf, VS_NONE) never beats anything
@@ -600,11 +612,11 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
     const int RB = (R + VT_ROWS * 2 - 1) / (VT_ROWS * 2);
     // (HFIX at 256 spills 16 VGPRs: the constant split lets all 16 X chunks be hoisted in flight)
     hipLaunchKernelGGL((vocab_logits_kernel<2, 2, 256>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
-                       logits, part_ms, cand, ccnt, cmask, R, V, H, beam);
+                       logits, part_ms, cand, ccnt, cmask, R, V, H, beam, vl_mode());
   } else {
     const int RB = (R + VT_ROWS - 1) / VT_ROWS;
     hipLaunchKernelGGL((vocab_logits_kernel<2, 1, 512, true>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT,
-                       bias, logits, part_ms, cand, ccnt, cmask, R, V, H, beam);
+                       bias, logits, part_ms, cand, ccnt, cmask, R, V, H, beam, vl_mode());
   }
   hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, cand,
                      ccnt, out_ids, out_lp, V, T, K, beam, nt, tcols, pgi, bt ? *bt : none);

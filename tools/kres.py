@@ -14,7 +14,7 @@ def main():
     src, pat = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "")
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=fast",
            "-munsafe-fp-atomics", f"-I{ROOT}/csrc/kernels", "-c", src, "-o", "/tmp/kres.o",
-           "-Rpass-analysis=kernel-resource-usage"]
+           "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("KRES_FLAGS", "").split()
     out = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
     for line in out.splitlines():
