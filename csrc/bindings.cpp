@@ -586,18 +586,11 @@ void final_topk(const Tensor& logits, const Tensor& bias, const OT& pgen, const 
 }
 int64_t topk_parts(int64_t V) { return topk_split(V); }
 
-// the select kernel's candidate lists (+ counts) and the per-article copied-word bitmap (pointer mode)
-static void vcand_check(const Tensor& vcand, const OT& cmask, int64_t R, int64_t V, int64_t H, int64_t beam, bool ptr) {
-  chk(vcand, F32, "vcand");
-  numel_eq(vcand, (int64_t)vocab_topk_cand_floats((int)R, (int)V, (int)H), "vcand");
-  chko(cmask, I32, (R / beam) * ((V + 31) / 32), "cmask");
-  TORCH_CHECK(!ptr || PO<int>(cmask), "pointer mode needs the copied-word bitmap cmask");
-}
 // fused decode vocab head (vocab_topk.hip): MFMA logits + tile partials, select reads K tiles per row
 void vocab_topk(const Tensor& X, const Tensor& WT, const Tensor& bias, const OT& pgen, const OT& attn,
                 const Tensor& ext, const Tensor& lens, const Tensor& out_ids, const Tensor& out_lp,
-                const Tensor& logits, const Tensor& part_ms, const Tensor& vcand, const OT& cmask, int64_t R, int64_t V,
-                int64_t H, int64_t T, int64_t K, int64_t beam) {
+                const Tensor& logits, const Tensor& part_ms, int64_t R, int64_t V, int64_t H, int64_t T, int64_t K,
+                int64_t beam) {
   chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(ext, I32, "ext"); chk(lens, I32, "lens");
   chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp"); chk(logits, F32, "logits"); chk(part_ms, F32, "part_ms");
   const int64_t nt = vocab_topk_tiles((int)V, (int)H);
@@ -607,22 +600,19 @@ void vocab_topk(const Tensor& X, const Tensor& WT, const Tensor& bias, const OT&
   numel_eq(ext, (R / beam) * T, "ext"); numel_eq(lens, R / beam, "lens");
   numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
   numel_eq(logits, R * V, "logits"); numel_eq(part_ms, R * nt * 2, "part_ms");
-  vcand_check(vcand, cmask, R, V, H, beam, PO<float>(pgen) != nullptr);
-
   chko(pgen, F32, R, "pgen"); chko(attn, F32, R * T, "attn");
   TORCH_CHECK(!PO<float>(pgen) || PO<float>(attn), "pointer mode needs attn");
   launch_vocab_topk(P<bf16>(X), P<bf16>(WT), P<float>(bias), PO<float>(pgen), PO<float>(attn), P<int>(ext),
-                    P<int>(lens), P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), P<float>(vcand),
-                    (const unsigned*)PO<int>(cmask), R, V, H, T, K, beam, PgIn{}, stream());
+                    P<int>(lens), P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), R, V, H, T,
+                    K, beam, PgIn{}, stream());
 }
 // vocab_topk with p_gen = sigmoid([ctx, c, h, x] . w + b) computed inside the select kernel
 // (written to pg_out for the beam histories)
 void vocab_topk_pg(const Tensor& X, const Tensor& WT, const Tensor& bias, const Tensor& ctx, const Tensor& c,
                    const Tensor& h, const Tensor& x, const Tensor& pg_w, const Tensor& pg_b, const Tensor& pg_out,
                    const Tensor& attn, const Tensor& ext, const Tensor& lens, const Tensor& out_ids,
-                   const Tensor& out_lp, const Tensor& logits, const Tensor& part_ms, const Tensor& vcand,
-                   const OT& cmask, int64_t R, int64_t V, int64_t H, int64_t T, int64_t K, int64_t beam, int64_t A,
-                   int64_t E) {
+                   const Tensor& out_lp, const Tensor& logits, const Tensor& part_ms, int64_t R, int64_t V, int64_t H,
+                   int64_t T, int64_t K, int64_t beam, int64_t A, int64_t E) {
   chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(ext, I32, "ext"); chk(lens, I32, "lens");
   chk(out_ids, I32, "out_ids"); chk(out_lp, F32, "out_lp"); chk(logits, F32, "logits"); chk(part_ms, F32, "part_ms");
   chk(ctx, F32, "ctx"); chk(c, F32, "c"); chk(h, BF, "h"); chk(x, F32, "x"); chk(pg_w, F32, "pg_w");
@@ -633,19 +623,16 @@ void vocab_topk_pg(const Tensor& X, const Tensor& WT, const Tensor& bias, const 
   numel_eq(X, R * H, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias");
   numel_eq(ext, (R / beam) * T, "ext"); numel_eq(lens, R / beam, "lens");
   numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
-  numel_eq(logits, R * V, "logits"); numel_eq(part_ms, R * nt * 2, "part_ms");
-  vcand_check(vcand, cmask, R, V, H, beam, true);
- numel_eq(attn, R * T, "attn");
+  numel_eq(logits, R * V, "logits"); numel_eq(part_ms, R * nt * 2, "part_ms"); numel_eq(attn, R * T, "attn");
   numel_eq(ctx, R * A, "ctx"); numel_eq(c, R * H, "c"); numel_eq(h, R * H, "h"); numel_eq(x, R * E, "x");
   numel_eq(pg_w, A + 2 * H + E, "pg_w"); numel_eq(pg_b, 1, "pg_b"); numel_eq(pg_out, R, "pg_out");
   const PgIn pgi{P<float>(ctx), P<float>(c), P<bf16>(h), P<float>(x), P<float>(pg_w), P<float>(pg_b),
                  P<float>(pg_out), (int)A, (int)H, (int)E};
   launch_vocab_topk(P<bf16>(X), P<bf16>(WT), P<float>(bias), nullptr, P<float>(attn), P<int>(ext), P<int>(lens),
-                    P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), P<float>(vcand),
-                    (const unsigned*)PO<int>(cmask), R, V, H, T, K, beam, pgi, stream());
+                    P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), R, V, H, T, K, beam, pgi,
+                    stream());
 }
 int64_t vocab_topk_parts(int64_t V, int64_t H) { return vocab_topk_tiles((int)V, (int)H); }
-int64_t vocab_topk_cand_op(int64_t R, int64_t V, int64_t H) { return (int64_t)vocab_topk_cand_floats((int)R, (int)V, (int)H); }
 
 // One beam-decode step's head: vocab_topk (p_gen inside when the pointer inputs are given) with
 // the beam bookkeeping fused into the select kernel's per-article tail (replaces vocab_topk_pg +
@@ -653,7 +640,7 @@ int64_t vocab_topk_cand_op(int64_t R, int64_t V, int64_t H) { return (int64_t)vo
 void vocab_topk_beam(const Tensor& X, const Tensor& WT, const Tensor& bias, const OT& ctx, const OT& c, const OT& h,
                      const OT& x, const OT& pg_w, const OT& pg_b, const OT& pg_out, const OT& attn, const Tensor& ext,
                      const Tensor& lens, const Tensor& out_ids, const Tensor& out_lp, const Tensor& logits,
-                     const Tensor& part_ms, const Tensor& vcand, const OT& cmask, const Tensor& lp_sum, const Tensor& latest, const Tensor& gidx,
+                     const Tensor& part_ms, const Tensor& lp_sum, const Tensor& latest, const Tensor& gidx,
                      const Tensor& tok_hist, const Tensor& par_hist, const Tensor& done, const Tensor& res_count,
                      const Tensor& res_score, const Tensor& res_len, const Tensor& res_step, const Tensor& res_par,
                      const Tensor& step, const Tensor& art_ctr, const Tensor& gran, const Tensor& err,
@@ -668,9 +655,7 @@ void vocab_topk_beam(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
   numel_eq(X, R * H, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias");
   numel_eq(ext, Na * T, "ext"); numel_eq(lens, Na, "lens");
   numel_eq(out_ids, R * K, "out_ids"); numel_eq(out_lp, R * K, "out_lp");
-  numel_eq(logits, R * V, "logits"); numel_eq(part_ms, R * nt * 2, "part_ms");
-  vcand_check(vcand, cmask, R, V, H, beam, pg_w.has_value() && pg_w->defined());
- chko(attn, F32, R * T, "attn");
+  numel_eq(logits, R * V, "logits"); numel_eq(part_ms, R * nt * 2, "part_ms"); chko(attn, F32, R * T, "attn");
   const bool ptr = pg_w.has_value() && pg_w->defined();
   PgIn pgi{};
   if (ptr) {
@@ -701,8 +686,8 @@ void vocab_topk_beam(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
                     PO<float>(attn), PO<float>(att_hist), PO<float>(pg_out),
                     PO<float>(pg_hist), (int)T, (int)Na, (int)beam, (int)K, (int)stop_id, (int)min_dec, (int)max_dec};
   launch_vocab_topk(P<bf16>(X), P<bf16>(WT), P<float>(bias), nullptr, ptr ? PO<float>(attn) : nullptr, P<int>(ext),
-                    P<int>(lens), P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), P<float>(vcand),
-                    (const unsigned*)PO<int>(cmask), R, V, H, T, K, beam, pgi, stream(), &bt);
+                    P<int>(lens), P<int>(out_ids), P<float>(out_lp), P<float>(logits), P<float>(part_ms), R, V, H, T, K,
+                    beam, pgi, stream(), &bt);
 }
 
 // decoder cell of a beam-decode step with the parent / token gathers inside (dec_cell_fwd +
@@ -974,7 +959,6 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("pgen", &pgen);
   m.def("vocab_topk", &vocab_topk);
   m.def("vocab_topk_parts", &vocab_topk_parts);
-  m.def("vocab_topk_cand", &vocab_topk_cand_op);
   m.def("vocab_topk_beam", &vocab_topk_beam);
   m.def("dec_cell_fwd_beam", &dec_cell_fwd_beam);
   m.def("beam_sproj_xmerge", &beam_sproj_xmerge);

@@ -232,19 +232,5 @@ __device__ __forceinline__ float max_x16(float v) {
   const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
 }
-__device__ __forceinline__ float min_x32(float v) {
-  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fminf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-}
-__device__ __forceinline__ float min_x16(float v) {
-  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fminf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-}
-// median of three (v_med3_f32): with a >= b it is the second largest of {a, b, c}
-__device__ __forceinline__ float vmed3(float a, float b, float c) {
-  float r;
-  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
 
 #define HIP_LAUNCH_CHECK() (void)0

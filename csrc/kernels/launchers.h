@@ -136,11 +136,10 @@ struct PgIn {
   const float* ctx; const float* c; const bf16* h; const float* x; const float* w; const float* b; float* out;
   int A, H, E;
 };
-size_t vocab_topk_cand_floats(int R, int V, int H);
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
-                       float* vcand, const unsigned* cmask, int R, int V, int H, int T, int K, int beam, PgIn pgi,
-                       hipStream_t st, const BeamTail* bt = nullptr);
+                       int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st,
+                       const BeamTail* bt = nullptr);
 int vocab_train_tiles(int V, int H);
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
                             float* zg, float* lse, float* pv, int N, int V, int H, const int* vblk, const int* vblk_n,

@@ -700,10 +700,8 @@ __device__ __forceinline__ const gu64* gboff(const gu64* p, unsigned bytes) {
   return reinterpret_cast<const gu64*>(reinterpret_cast<const __attribute__((address_space(1))) char*>(p) + bytes);
 }
 
-#ifndef BWD32_PC
-#define BWD32_PC 2  // peers polled per chunk (4: 8 registers spill)
-#endif
-template <bool NT>
+// PC: peers polled per chunk (4: 8 registers spill); SL: s_sleep between poll passes
+template <bool NT, int PC = 2, int SL = 96>
 __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
@@ -777,7 +775,6 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
     if (s + 1 < T) {
 #pragma unroll
       for (int i = 0; i < RPL; ++i) rec[i] = Pown[(row0 + i) * 64 + ul];
-      constexpr int PC = BWD32_PC;
       const gu64* src = xb + (size_t)((s + 1) & 1) * NC * NC * SLOT + (size_t)c * NC * SLOT;
       const unsigned tag = (unsigned)(T - 1 - s);
 #pragma unroll
@@ -808,7 +805,7 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
             dead = true;
             break;
           }
-          __builtin_amdgcn_s_sleep(96);
+          __builtin_amdgcn_s_sleep(SL);
         }
 #pragma unroll
         for (int q = 0; q < PC; ++q)
@@ -972,6 +969,13 @@ static bool lstm_bwd32() {
   }();
   return on;
 }
+static int bwd32_variant() {
+  static const int v = [] {
+    const char* e = getenv("TSAMD_BWD32_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 static int lstm_rows(int H, int B, bool bwd) {
   return (H == 512 && B > 256 && (!bwd || lstm_bwd32())) ? 32 : 16;
 }
@@ -1051,8 +1055,17 @@ void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, con
   for (int t0 = 0; t0 < ntile; t0 += nl) {
     const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
     if (R == 32) {
-      hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false>), dim3(grid), dim3(1024), 0, st, dz, Wn, dout, dh_fin,
-                         dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n);
+#define LB32(PC, SL) hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false, PC, SL>), dim3(grid), dim3(1024), 0, st, dz, \
+                                        Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+      switch (bwd32_variant()) {  // A/B sweep (TSAMD_BWD32_VARIANT)
+        case 1: LB32(2, 24); break;
+        case 2: LB32(2, 48); break;
+        case 3: LB32(4, 96); break;
+        case 4: LB32(2, 8); break;
+        case 5: LB32(4, 24); break;
+        default: LB32(2, 96);
+      }
+#undef LB32
       continue;
     }
 #define LAUNCH_B(HH, NTV)                                                                                                 \

@@ -12,7 +12,6 @@
 //                       union copied ids).
 // Replaces a library GEMM + a separate per-element top-k pass over the logits.
 #include "common.h"
-#include <stdlib.h>
 #include "attn_common.h"  // f32x2 packed-FP32 helpers
 #include "beam_common.h"  // beam bookkeeping fused into the select kernel's tail
 #include "launchers.h"
@@ -46,51 +45,28 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 // to a plain logits GEMM (A = W^T fragments, B = X rows, as in vocab_train.hip), so
 // accumulator (i, jr, r) holds logit[row = rb + 16 jr + (lane & 15)][col = cw + 16 i + 4 q + r],
 // q = lane >> 4: every lane owns 16 columns of one row.  The row's (max, sum exp) over the
-// wave's 64 columns is 15 in-lane ops + 2 cross-lane steps (lanes l, l^16, l^32, l^48).
-//
-// No logit is stored in full.  Per (row, 256-column tile) the kernel keeps a candidate list
-// that provably holds the tile's top-8: each lane tracks its two largest values (v_max +
-// v_med3 per value), t_wave = min over the row's 4 lanes of their second largest is <= the
-// wave's 8th largest (8 distinct values are >= it), t_tile = max over the 4 waves is <= the
-// tile's 8th largest, and every value >= t_tile is appended (LDS slot counter, then one 8-byte
-// store of (value, column)).  The row's plain top-K (K <= 8) lies in the K tiles with the
-// largest maxima (vocab_select), each of whose top-8 is in its list.  Copied words (ids of the
-// article's in-article tokens, a per-article bitmap) get their exact logit stored in place for
-// the pointer mixture.  Replaced storing every fp32 logit (51 MB per step at 256 x 50k).
-// bias of the lane's columns from the tile's LDS copy (bl = the wave's first column in it; -inf past V)
-template <int NI>
-__device__ __forceinline__ void vl_values(const f32x4 (&acc)[NI][4], int jr, const float* bl, int lane,
-                                          f32x2 (&x)[NI][2]) {
-  const int q4 = 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const float4 b4 = *reinterpret_cast<const float4*>(bl + 16 * i + q4);
-    x[i][0] = f32x2{acc[i][jr][0], acc[i][jr][1]} + f32x2{b4.x, b4.y};
-    x[i][1] = f32x2{acc[i][jr][2], acc[i][jr][3]} + f32x2{b4.z, b4.w};
-  }
-}
-
-// phase 1: (max, sum exp) of the row over the wave's 64 columns, and t_wave
-template <int NI>
-__device__ __forceinline__ void vl_stats(const f32x4 (&acc)[NI][4], int jr, const float* bl, float* Pm, float* Ps,
-                                         float* Tw, int lane) {
+// wave's 64 columns is 15 in-lane ops + 2 cross-lane steps (lanes l, l^16, l^32, l^48), and the
+// lane's 4 consecutive columns per i are one 16-byte store (a row's 64 columns = one 256-byte
+// run over the 4 i and 4 q).  Replaced a [row = lane group] layout whose per-row reductions
+// took 16-lane DPP trees for each of the lane's 16 rows and an LDS staging pass for stores.
+template <bool FULL, int NI>
+__device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[NI][4], int jr, const f32x2 (&bc)[NI][2],
+                                            float* __restrict__ logits, float* Pm, float* Ps, int rb, int cw,
+                                            int lane, int R, int V) {
   constexpr float L2E = 1.4426950408889634f;
+  const int row = rb + 16 * jr + (lane & 15), q4 = 4 * (lane >> 4);
   f32x2 x[NI][2];
-  vl_values<NI>(acc, jr, bl, lane, x);
-  float m1 = -INFINITY, m2 = -INFINITY;  // the lane's two largest
+  float m = -INFINITY;
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      m2 = vmed3(m1, m2, x[i][h].x);
-      m1 = vmax2(m1, x[i][h].x);
-      m2 = vmed3(m1, m2, x[i][h].y);
-      m1 = vmax2(m1, x[i][h].y);
+      x[i][h] = f32x2{acc[i][jr][2 * h], acc[i][jr][2 * h + 1]} + bc[i][h];  // bc = -inf past V
+      m = vmax3(m, x[i][h].x, x[i][h].y);
     }
-  const float m = max_x32(max_x16(m1));
-  const float tw = min_x32(min_x16(m2));
+  m = max_x32(max_x16(m));
   f32x2 s2 = f32x2{0.f, 0.f};
-  if (m > -INFINITY) {
+  if (FULL || m > -INFINITY) {
     const f32x2 mb = f32x2{-m * L2E, -m * L2E};
 #pragma unroll
     for (int i = 0; i < NI; ++i)
@@ -104,57 +80,32 @@ __device__ __forceinline__ void vl_stats(const f32x4 (&acc)[NI][4], int jr, cons
   if (lane < 16) {
     Pm[16 * jr + lane] = m;
     Ps[16 * jr + lane] = sm;
-    Tw[16 * jr + lane] = tw;
   }
-}
-
-// phase 2: append the values >= t_tile to the (row, tile) candidate list; exact logits of the
-// article's copied words in place
-template <int NI>
-__device__ __forceinline__ void vl_emit(const f32x4 (&acc)[NI][4], int jr, const float* bl, float tt, int* cnt,
-                                        float2* __restrict__ cand, float* __restrict__ logits, const unsigned* cmrow,
-                                        int row, int cw, int ct, int lane, int V, int mode) {
-  f32x2 x[NI][2];
-  vl_values<NI>(acc, jr, bl, lane, x);
-  const int q4 = 4 * (lane >> 4);
-  // the lane's candidates: count, ONE LDS slot reservation, then the stores
-  unsigned sel = 0;
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float v = e & 1 ? x[i][e >> 1].y : x[i][e >> 1].x;
-      sel |= (unsigned)(v >= tt) << (4 * i + e);
-    }
-  if (sel && !(mode & 4)) {
-    int slot = atomicAdd(cnt, __builtin_popcount(sel));
-    if (mode & 2) sel = 0;
+  if (FULL) {
+    float* dst = logits + (size_t)row * V + cw + q4;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if ((sel >> (4 * i + e)) & 1u) {
-          const float v = e & 1 ? x[i][e >> 1].y : x[i][e >> 1].x;
-          cand[slot++] = make_float2(v, __int_as_float(cw - ct + 16 * i + q4 + e));
-        }
-  }
-  if (cmrow && !(mode & 1)) {  // copied words (a few per row and tile): their exact logits in place
+      *reinterpret_cast<float4*>(dst + 16 * i) = make_float4(x[i][0].x, x[i][0].y, x[i][1].x, x[i][1].y);
+  } else if (row < R) {
+    float* dst = logits + (size_t)row * V;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int o4 = cw - ct + 16 * i + q4;  // column - tile start of the lane's 4 consecutive columns
-      const unsigned bits = (cmrow[o4 >> 5] >> (o4 & 31)) & 15u;
-      if (bits) {
+      const int col = cw + 16 * i + q4;
+      const float xv[4] = {x[i][0].x, x[i][0].y, x[i][1].x, x[i][1].y};
+      if ((V & 3) == 0 && col + 4 <= V) {
+        *reinterpret_cast<float4*>(dst + col) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+      } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = e & 1 ? x[i][e >> 1].y : x[i][e >> 1].x;
-          if (((bits >> e) & 1u) && ct + o4 + e < V) logits[(size_t)row * V + ct + o4 + e] = v;
-        }
+        for (int e = 0; e < 4; ++e)
+          if (col + e < V) dst[col + e] = xv[e];
       }
     }
   }
 }
 
-// 2 workgroups per CU (<= 256 VGPRs): all 32 W^T fragments of a wave in flight at once.
+// 35 KB (RH = 1) / 70 KB (RH = 2) of LDS, 2 workgroups per CU (<= 256 VGPRs): all 32 W^T fragments
+// of a wave in flight at once.  (A 4-per-CU variant, 128
+// VGPRs, measured the same before this layout and spills with it.)
 // RH = 2: 128 rows per workgroup, the W^T fragments reused for two 64-row halves (half the
 // workgroups and W^T fetches: 392 tiles at R = 256 = one round), X tile 68 KB of LDS.
 // HFIX: H == HMAX, known at compile time (the X-staging row / chunk split by H / 8 is then a
@@ -164,19 +115,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     const bf16* __restrict__ X,     // [R][H]  output-projection activations (bf16)
     const bf16* __restrict__ WT,    // [V][H]  output_projection/w transposed ("Bt")
     const float* __restrict__ bias, // [V]
-    float* __restrict__ logits,     // [R][V]  fp32: only the copied words' entries are written
+    float* __restrict__ logits,     // [R][V]  fp32 (bias added)
     float* __restrict__ part_ms,    // [R][nt][2]  per tile (max, sum exp)
-    float2* __restrict__ cand,      // [R][nt][VT_COLS] candidate (value, column in tile)
-    int* __restrict__ ccnt,         // [R][nt] candidates per (row, tile)
-    const unsigned* __restrict__ cmask,  // [R / beam][ceil(V / 32)] copied-word bitmap (nullptr: none)
-    int R, int V, int Hrt, int beam, int mode) {
+    int R, int V, int Hrt) {
   const int H = HFIX ? HMAX : Hrt;
   constexpr int BR = VT_ROWS * RH;  // rows per block
   constexpr int NI = vt_ni(HMAX), VT_COLS = vt_cols(HMAX), KS = HMAX / 32;
-  __shared__ float Pm[4][BR], Ps[4][BR], Tw[4][VT_ROWS];
-  __shared__ int cnt_s[BR];
-  __shared__ unsigned cm_s[BR][VT_COLS / 32];  // each row's article's copied-word bits over this tile
-  __shared__ __attribute__((aligned(16))) float bias_s[VT_COLS];
+  __shared__ float Pm[4][BR], Ps[4][BR];
   __shared__ __attribute__((aligned(16))) bf16 Xs[BR * (HMAX + 8)];  // X tile of the block
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // XCD-aware order: the RB row blocks of one vocab tile get block ids equal mod 8 (one XCD
@@ -187,9 +132,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   if (vt >= nt) return;
   const int rb = (slot % RB) * BR;
   const int cw = vt * VT_COLS + 16 * NI * wid;  // this wave's first column
-  const int mwords = (V + 31) >> 5;
   // X rows of this block -> LDS once (shared by the 4 waves)
-  const int kof = 8 * (lane >> 4), c16 = lane & 15;
+  const int kof = 8 * (lane >> 4), c16 = lane & 15, q4 = 4 * (lane >> 4);
   constexpr int XPT = BR * HMAX / 8 / 256;  // 16-byte X chunks per thread (H <= HMAX)
   bf16x8 xr[XPT];
 #pragma unroll
@@ -208,23 +152,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   for (int h = 0; h < KS; ++h)
 #pragma unroll
     for (int i = 0; i < NI; ++i) wa[h][i] = ld8(arow[i] + min(32 * h, H - 32));
-  // the tile's bias -> LDS (-inf past V)
-  for (int c = threadIdx.x; c < VT_COLS; c += 256) {
-    const int col = vt * VT_COLS + c;
-    bias_s[c] = col < V ? bias[col] : -INFINITY;
-  }
-  const float* bl = bias_s + (cw - vt * VT_COLS);
+  // bias of the lane's columns cw + 16 i + q4 + r, pairs (r = 2h, 2h + 1); -inf past V
+  f32x2 bc[NI][2];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = cw + 16 * i + q4 + 2 * h;
+      bc[i][h] = f32x2{col < V ? bias[col] : -INFINITY, col + 1 < V ? bias[col + 1] : -INFINITY};
+    }
 #pragma unroll
   for (int u = 0; u < XPT; ++u) {
     const int c = threadIdx.x + 256 * u, rr = c / (H / 8), k8 = (c % (H / 8)) * 8;
     if (c < BR * (H / 8)) *reinterpret_cast<bf16x8*>(&Xs[rr * (H + 8) + k8]) = xr[u];
   }
-  for (int r = threadIdx.x; r < BR; r += 256) cnt_s[r] = 0;
-  if (cmask)
-    for (int u = threadIdx.x; u < BR * (VT_COLS / 32); u += 256) {
-      const int rr = u / (VT_COLS / 32), w = u % (VT_COLS / 32), gw = vt * (VT_COLS / 32) + w;
-      cm_s[rr][w] = (rb + rr < R && gw < mwords) ? cmask[(size_t)((rb + rr) / beam) * mwords + gw] : 0u;
-    }
   __syncthreads();
 #pragma unroll
   for (int h2 = 0; h2 < RH; ++h2) {
@@ -246,22 +187,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
         }
       }
     }
-    // phase 1: per-row statistics and the wave's candidate threshold
-#pragma unroll
-    for (int jr = 0; jr < 4; ++jr)
-      vl_stats<NI>(acc, jr, bl, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, Tw[wid], lane);
-    __syncthreads();
-    // phase 2: candidates >= t_tile = max of the 4 waves' thresholds, copied words in place
+    // ---- epilogue: + bias, store fp32, per-row (max, sum exp) over this wave's 64 columns.
+    // FULL (every tile but the last vocab tile / row block): no column or row guards.
+    const bool full = (vt + 1) * VT_COLS <= V && rbh + VT_ROWS <= R && (V & 3) == 0;
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
-      const int rl = 16 * jr + c16, row = rbh + rl;
-      const float tt = fmaxf(fmaxf(Tw[0][rl], Tw[1][rl]), fmaxf(Tw[2][rl], Tw[3][rl]));
-      if (row < R)
-        vl_emit<NI>(acc, jr, bl, tt, &cnt_s[VT_ROWS * h2 + rl], cand + ((size_t)row * nt + vt) * VT_COLS, logits,
-                    cmask ? cm_s[VT_ROWS * h2 + rl] : nullptr, row, cw, vt * VT_COLS, lane, V, mode);
+      if (full)
+        vl_epilogue<true, NI>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
+      else
+        vl_epilogue<false, NI>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
     }
-    __syncthreads();  // Tw reused by the next half
   }
+  __syncthreads();
   for (int rr = threadIdx.x; rr < BR; rr += 256) {
     const int row = rb + rr;
     float m = Pm[0][rr], sm = Ps[0][rr];
@@ -270,7 +207,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
     if (row < R) {
       part_ms[((size_t)row * nt + vt) * 2] = m;
       part_ms[((size_t)row * nt + vt) * 2 + 1] = sm;
-      ccnt[(size_t)row * nt + vt] = cnt_s[rr];
     }
   }
 }
@@ -279,16 +215,6 @@ namespace {
 __device__ __forceinline__ int vhslot(int w) { return (int)(((unsigned)w * 2654435761u) >> 21) & (VM_HASH - 1); }
 
 }  // namespace
-
-// A/B instrumentation (TSAMD_VL_MODE, timing only -- results are wrong for mode != 0):
-// bit 0 skips the copied-word stores, bit 1 the candidate stores, bit 2 the slot reservation too
-static int vl_mode() {
-  static const int m = [] {
-    const char* e = getenv("TSAMD_VL_MODE");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
 
 #define VS_THREADS 1024  // 256 threads measured 16.6 us vs 14.0 at R = 256 (fewer loads in flight)
 #define VS_NONE 0x7fffffff  // sentinel id: (-inf, VS_NONE) never beats anything
@@ -350,7 +276,6 @@ __device__ __forceinline__ void pad4(float* v, int* id, int n) {
 __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     const float* __restrict__ logits, const float* __restrict__ part_ms, const float* __restrict__ pgen,
     const float* __restrict__ attn, const int* __restrict__ ext, const int* __restrict__ lens,
-    const float2* __restrict__ cand, const int* __restrict__ ccnt,
     int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam, int nt, int tcols, PgIn pgi,
     BeamTail bt) {
   __shared__ float bt_cval[64];
@@ -364,7 +289,6 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   __shared__ float pv_s[3][VT_K];
   __shared__ int pi_s[3][VT_K];
   __shared__ int gkey[VT_K], gkey2[VT_K];
-  __shared__ int lcnt[VT_K];  // candidate-list lengths of the K selected tiles
   __shared__ int ncand, ncopy;
   const int r = blockIdx.x, tid = threadIdx.x;
   const int art = r / beam;
@@ -463,20 +387,16 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   __syncthreads();
   if (tid == 0) ncand = 0;
   const float tau = pv_s[0][K - 1];
-  // ---- round trip 2: the K selected tiles' candidate lists (vocab_logits: each holds its tile's
-  // top-8 and more) and the copied words' logits.  The first VS_CSPEC slots of every list are
-  // read speculatively with the counts; a longer list is finished in extra passes (rare).
-  constexpr int VS_CSPEC = VS_THREADS / VT_K;  // 128 slots per tile
-  int cn[1], cs[1];
-  float zs[1];
-  {
-    const int j = tid / VS_CSPEC, sl = tid % VS_CSPEC;
-    const int tq = j < K ? pi_s[0][j] : VS_NONE;
-    cn[0] = tq < nt ? ccnt[(size_t)r * nt + tq] : 0;
-    const float2 c = tq < nt ? cand[((size_t)r * nt + tq) * tcols + sl] : make_float2(-INFINITY, 0.f);
-    cs[0] = sl < cn[0] ? tq * tcols + __float_as_int(c.y) : V;
-    zs[0] = c.x;
-    if (sl == 0 && j < K) lcnt[j] = cn[0];
+  // ---- round trip 2: the K selected tiles' logits and the copied words' logits
+  constexpr int EPT = VT_K * 256 / VS_THREADS;  // tiles of <= 256 columns
+  float zs[EPT];
+  int cs[EPT];
+#pragma unroll
+  for (int u = 0; u < EPT; ++u) {
+    const int e = tid + u * VS_THREADS;
+    const int tq = e < K * tcols ? pi_s[0][e / tcols] : VS_NONE;
+    cs[u] = tq < nt ? tq * tcols + (e % tcols) : V;
+    zs[u] = cs[u] < V ? z[cs[u]] : -INFINITY;
   }
   int wk[SPT];
   float zk[SPT];
@@ -486,26 +406,13 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     zk[u] = (wk[u] >= 0 && wk[u] < V) ? z[wk[u]] : -INFINITY;
   }
   __syncthreads();  // ncand reset and the tile list read by everyone before the appends
-  if (cs[0] < V && zs[0] >= tau) {
-    const int slot = atomicAdd(&ncand, 1);
-    cv[slot] = zs[0];
-    ci[slot] = cs[0];
-  }
-  // lists longer than VS_CSPEC (a flat tile): the rest, one tile per pass
-  for (int j = 0; j < K; ++j) {
-    const int tq = pi_s[0][j];
-    if (tq >= nt) continue;  // uniform
-    const int n = lcnt[j];
-    for (int sl = VS_CSPEC + tid; sl < n; sl += VS_THREADS) {
-      const float2 c = cand[((size_t)r * nt + tq) * tcols + sl];
-      const int col = tq * tcols + __float_as_int(c.y);
-      if (col < V && c.x >= tau) {
-        const int slot = atomicAdd(&ncand, 1);
-        cv[slot] = c.x;
-        ci[slot] = col;
-      }
+#pragma unroll
+  for (int u = 0; u < EPT; ++u)
+    if (cs[u] < V && zs[u] >= tau) {
+      const int slot = atomicAdd(&ncand, 1);
+      cv[slot] = zs[u];
+      ci[slot] = cs[u];
     }
-  }
   __syncthreads();
   const int nc = ncand;
   pad4(cv, ci, nc);
@@ -591,18 +498,10 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
 
 int vocab_topk_tiles(int V, int H) { return (V + vt_cols(H) - 1) / vt_cols(H); }
 
-size_t vocab_topk_cand_floats(int R, int V, int H) {
-  const size_t nt = vocab_topk_tiles(V, H);
-  return (size_t)R * nt * vt_cols(H) * 2 + (size_t)R * nt;  // (value, column) slots, then the counts
-}
-
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
-                       float* vcand, const unsigned* cmask, int R, int V, int H, int T, int K, int beam, PgIn pgi,
-                       hipStream_t st, const BeamTail* bt) {
+                       int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st, const BeamTail* bt) {
   const int nt = vocab_topk_tiles(V, H), tcols = vt_cols(H);
-  float2* cand = reinterpret_cast<float2*>(vcand);
-  int* ccnt = reinterpret_cast<int*>(vcand + (size_t)R * nt * tcols * 2);
   const BeamTail none{};
   // default: 128-row workgroups (392 at R = 256, V = 50k: one round at 2 per CU; W^T fragments
   // fetched once per 128 rows): decode 5610 -> 5927 summaries/s at 64 articles, 6940 -> 7300 at
@@ -612,12 +511,12 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
     const int RB = (R + VT_ROWS * 2 - 1) / (VT_ROWS * 2);
     // (HFIX at 256 spills 16 VGPRs: the constant split lets all 16 X chunks be hoisted in flight)
     hipLaunchKernelGGL((vocab_logits_kernel<2, 2, 256>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
-                       logits, part_ms, cand, ccnt, cmask, R, V, H, beam, vl_mode());
+                       logits, part_ms, R, V, H);
   } else {
     const int RB = (R + VT_ROWS - 1) / VT_ROWS;
     hipLaunchKernelGGL((vocab_logits_kernel<2, 1, 512, true>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT,
-                       bias, logits, part_ms, cand, ccnt, cmask, R, V, H, beam, vl_mode());
+                       bias, logits, part_ms, R, V, H);
   }
-  hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, cand,
-                     ccnt, out_ids, out_lp, V, T, K, beam, nt, tcols, pgi, bt ? *bt : none);
+  hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
+                     out_lp, V, T, K, beam, nt, tcols, pgi, bt ? *bt : none);
 }

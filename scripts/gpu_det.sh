@@ -6,6 +6,6 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${OUTD:-det}; mkdir -p $OUT
 export TMPDIR=/tmp
-TSAMD_SPLIT=${SPLIT:-4} timeout -k 10 1000 python -u tools/det_seq_after_suite.py ${ARGS} > $OUT/det.log 2>&1; rc=$?
+DSQ_SPLIT=${SPLIT:-4} timeout -k 10 1000 python -u tools/det_seq_after_suite.py ${ARGS} > $OUT/det.log 2>&1; rc=$?
 grep -E "suite rc|step" $OUT/det.log | tail -8
 exit $rc

@@ -251,18 +251,12 @@ def test_pgen_matches_fp32():
     assert (pg - ref).abs().max().item() < 1e-4
 
 
-@pytest.mark.parametrize("pointer,V,H,flat", [(True, 3000, 128, False), (False, 3000, 128, False),
-                                              (True, 600, 64, False), (False, 600, 64, False),
-                                              (False, 50000, 256, False), (True, 50000, 256, False),
-                                              (True, 50000, 512, False), (False, 3000, 512, False),
-                                              (True, 3000, 256, True), (False, 1000, 512, True)])
-def test_fused_vocab_topk_matches_materialised_path(pointer, V, H, flat):
-    """vocab_topk (MFMA logits + per-tile (max, sum exp) partials and candidate lists holding each
-    tile's top-8, then a select that reads only the K best tiles' lists of each row) == the
-    library GEMM + final_topk path; V=600 has fewer vocab tiles than K.  flat: every logit equal
-    (X = 0, constant bias), so every list holds its whole tile -- past the select kernel's
-    speculative 128 slots.  Pointer mode: the copied words' exact logits are stored in place."""
-    from textsummarization_on_flink_amd.decode.device_beam import copy_bitmap
+@pytest.mark.parametrize("pointer,V,H", [(True, 3000, 128), (False, 3000, 128), (True, 600, 64), (False, 600, 64),
+                                         (False, 50000, 256), (True, 50000, 512), (False, 3000, 512)])
+def test_fused_vocab_topk_matches_materialised_path(pointer, V, H):
+    """vocab_topk (MFMA logits + per-tile (max, sum exp) partials, then a select that reads
+    only the K best tiles of each row) == the library GEMM + final_topk path; V=600 has
+    fewer vocab tiles than K."""
     from textsummarization_on_flink_amd.ops import ops
     k = ops()
     torch.manual_seed(5)
@@ -271,9 +265,6 @@ def test_fused_vocab_topk_matches_materialised_path(pointer, V, H, flat):
     X = (torch.randn(R, H, device="cuda")).bfloat16()
     W = (torch.randn(H, V, device="cuda") * 0.3).bfloat16()
     bias = torch.randn(V, device="cuda")
-    if flat:
-        X.zero_()
-        bias.fill_(0.25)
     lens = torch.randint(20, T + 1, (Na,), device="cuda", dtype=torch.int32)
     ext = torch.randint(0, V + 20, (Na, T), device="cuda", dtype=torch.int32)
     ext[:, :10] = ext[:, 10:20]
@@ -294,19 +285,11 @@ def test_fused_vocab_topk_matches_materialised_path(pointer, V, H, flat):
     nt = int(k.vocab_topk_parts(V, H))
     ids1 = torch.zeros(R, K, dtype=torch.int32, device="cuda")
     lp1 = torch.zeros(R, K, device="cuda")
-    lg = torch.full((R, V), float("nan"), device="cuda")
-    cm = copy_bitmap(ext, lens, V) if pointer else None
-    vc = torch.zeros(int(k.vocab_topk_cand(R, V, H)), device="cuda")
+    lg = torch.zeros(R, V, device="cuda")
     k.vocab_topk(X, W.t().contiguous(), bias, pg, attn, ext, lens, ids1, lp1, lg, torch.zeros(R, nt, 2, device="cuda"),
-                 vc, cm, R, V, H, T, K, beam)
+                 R, V, H, T, K, beam)
     torch.cuda.synchronize()
-    if pointer:  # exactly the copied in-vocabulary words' logits are stored
-        copied = torch.zeros(R, V, dtype=torch.bool, device="cuda")
-        for r in range(R):
-            ids = ext[r // beam, :lens[r // beam]].long()
-            copied[r, ids[ids < V]] = True
-        assert (lg[copied] - (logits + bias)[copied]).abs().max().item() < 1e-3
-        assert torch.isnan(lg[~copied]).all()
+    assert (lg - (logits + bias)).abs().max().item() < 1e-3
     bad = (ids0 != ids1).any(1).nonzero().flatten().tolist()
     assert not bad, (bad, ids0[bad[:2]].tolist(), ids1[bad[:2]].tolist(), lp0[bad[:2]].tolist(), lp1[bad[:2]].tolist())
     assert (lp0 - lp1).abs().max().item() < 1e-3

@@ -280,28 +280,42 @@ def test_config5_batch2048_graph_replays():
     assert all(math.isfinite(x) for x in losses) and losses[-1] < losses[0], losses
 
 
-@pytest.mark.parametrize("B", [64, 256])
-def test_deterministic_mode_bit_identical(monkeypatch, B):
+@pytest.mark.parametrize("B,split", [(64, "0"), (256, "1"), (256, "2"), (256, "4")])
+def test_deterministic_mode_bit_identical(monkeypatch, B, split):
     """TSAMD_DETERMINISTIC=1: no fp32 atomics in the step (fixed-order embedding / bias /
     attention-parameter reductions, row attention backward, inline weight gradients), so two
     trainings from the same init on the same batches end with bit-identical parameters and
-    Adagrad accumulators after 5 captured steps; and the result stays close to the default
-    (atomic) path."""
+    Adagrad accumulators after 5 captured steps -- with the decoder recurrences as ``split`` row
+    groups on parallel streams (0: the default), whose per-row arithmetic is the same on any
+    stream, so every split gives the single chain's bits; and the result stays close to the
+    default (atomic) path."""
     from textsummarization_on_flink_amd.train.trainer import GraphTrainer
     hps = _hps(B)
     vocab, batches = _batches(hps, 3, seed=17)
     res = {}
-    for mode, det in (("det1", "1"), ("det2", "1"), ("atomic", "0")):
+    runs = [("det1", "1", split), ("det2", "1", split), ("atomic", "0", "0")]
+    if split not in ("0", "1"):
+        runs.append(("chain", "1", "1"))
+    for mode, det, sp in runs:
         monkeypatch.setenv("TSAMD_DETERMINISTIC", det)
+        monkeypatch.setenv("TSAMD_SPLIT", sp)
         tr = GraphTrainer(hps, vocab.size(), B=B, T=T, device="cuda:0")
         assert tr.engine.det == (det == "1")
+        if sp != "0":
+            assert tr.engine.split == int(sp)
         for i in range(5):
             tr.check_finite(tr.step(batches[i % len(batches)]))
         res[mode] = (tr.params.flat.clone(), tr.params.accum.clone())
         offsets = tr.params.offsets
         del tr
         torch.cuda.empty_cache()
-    differ = [(n, int((res["det1"][1][o:o + c] != res["det2"][1][o:o + c]).sum()), c)
-              for n, (o, c) in offsets.items() if not torch.equal(res["det1"][1][o:o + c], res["det2"][1][o:o + c])]
-    assert torch.equal(res["det1"][0], res["det2"][0]) and torch.equal(res["det1"][1], res["det2"][1]), differ
+
+    def differ(a, b):
+        return [(n, int((res[a][1][o:o + c] != res[b][1][o:o + c]).sum()), c)
+                for n, (o, c) in offsets.items() if not torch.equal(res[a][1][o:o + c], res[b][1][o:o + c])]
+
+    for other in ("det2", "chain"):
+        if other in res:
+            assert torch.equal(res["det1"][0], res[other][0]) and torch.equal(res["det1"][1], res[other][1]), \
+                (other, differ("det1", other))
     assert _rel(res["det1"][0], res["atomic"][0]) < 1e-3

@@ -38,24 +38,6 @@ BF = torch.bfloat16
 F32 = torch.float32
 
 
-def copy_bitmap(ext: torch.Tensor, lens: torch.Tensor, V: int, out: torch.Tensor = None) -> torch.Tensor:
-    """[Na, ceil(V / 32)] int32 bitmap of the in-vocabulary ids among article a's first lens[a]
-    tokens (ext: [Na, T] extended ids): the words the pointer can copy, whose exact logits the
-    decode vocab head stores (vocab_topk.hip)."""
-    Na, T = ext.shape
-    nw = (V + 31) // 32
-    e = ext.long()
-    ok = (torch.arange(T, device=ext.device)[None, :] < lens[:, None].long()) & (e < V)
-    hit = torch.zeros(Na, nw * 32 + 1, dtype=torch.bool, device=ext.device)
-    hit.scatter_(1, torch.where(ok, e, nw * 32), ok)  # duplicates write the same True; misses go to the spare column
-    words = (hit[:, :nw * 32].view(Na, nw, 32).long() << torch.arange(32, device=ext.device)).sum(-1)
-    words = torch.where(words >= 2 ** 31, words - 2 ** 32, words).to(torch.int32)
-    if out is None:
-        return words.reshape(-1)
-    out.view(Na, nw).copy_(words)
-    return out
-
-
 class DeviceBeamDecoder:
     def __init__(self, hps, vocab, params, n_articles: int, T: int, use_graph: bool = True, chunk: int = 10,
                  keep_attn: bool = True):
@@ -130,10 +112,6 @@ class DeviceBeamDecoder:
         self.fused_vocab = self.eng.cfg.fused_vocab_decode and self.K <= 8 and (self.eng.H <= 256 or self.eng.H == 512)
         if self.fused_vocab:
             b["vpart_ms"] = z(R, int(self.k.vocab_topk_parts(V, H)), 2)
-            # per (row, vocab tile) candidate lists of the select kernel, and the per-article bitmap of
-            # the copied (in-article, in-vocabulary) word ids whose exact logits the logits kernel stores
-            b["vcand"] = z(int(self.k.vocab_topk_cand(R, V, H)))
-            b["cmask"] = z(Na * ((V + 31) // 32), dt=torch.int32)
         # fused step (5 + 1 launches): the parent / token gathers inside the cell, x-merge and
         # attention kernels, the beam bookkeeping in the vocab select kernel's tail
         self.fused_step = self.fused_vocab and self.row_attn and self.beam * self.K <= 64
@@ -200,14 +178,9 @@ class DeviceBeamDecoder:
         b["lens_att"].copy_(w["enc_lens"].repeat_interleave(r, 0) if r > 1 else w["enc_lens"])
         b["lens"].copy_(w["enc_lens"])
         b["ext"].copy_(w["ext"])
-        if self.fused_vocab and self.hps.pointer_gen:
-            self._copy_bitmap()
         X = self.st[0]
         X["C"].copy_(w["Cst"][0].repeat_interleave(beam, 0))
         X["H"].copy_(w["Hb"][0].repeat_interleave(beam, 0))
-
-    def _copy_bitmap(self):
-        copy_bitmap(self.b["ext"], self.b["lens"], self.V, out=self.b["cmask"])
 
     def _prologue(self):
         """Step-0 initial-state attention into state set 0, beam state reset."""
@@ -270,11 +243,11 @@ class DeviceBeamDecoder:
         if self.fused_vocab and hps.pointer_gen:
             # p_gen is computed inside the select kernel (into b["PG"] for the histories)
             k.vocab_topk_pg(b["outb"], self.owT, p[OV], Y["CTX"], Y["C"], Y["H"], b["x"], self.pg_w, p[PG_B], b["PG"],
-                            Y["ATT"], b["ext"], b["lens"], b["top_ids"], b["top_lp"], b["logits"], b["vpart_ms"],
-                            b["vcand"], b["cmask"], R, V, H, T, K, self.beam, A, E)
+                            Y["ATT"], b["ext"], b["lens"], b["top_ids"], b["top_lp"], b["logits"], b["vpart_ms"], R,
+                            V, H, T, K, self.beam, A, E)
         elif self.fused_vocab:
             k.vocab_topk(b["outb"], self.owT, p[OV], None, None, b["ext"], b["lens"], b["top_ids"], b["top_lp"],
-                         b["logits"], b["vpart_ms"], b["vcand"], None, R, V, H, T, K, self.beam)
+                         b["logits"], b["vpart_ms"], R, V, H, T, K, self.beam)
         else:
             torch.mm(b["outb"], eng.pk["ow"], out_dtype=F32, out=b["logits"])
             k.final_topk(b["logits"], p[OV], pg, Y["ATT"] if hps.pointer_gen else None, b["ext"], b["lens"],
@@ -319,8 +292,7 @@ class DeviceBeamDecoder:
         k.vocab_topk_beam(b["outb"], self.owT, p[OV], Y["CTX"] if ptr else None, Y["C"] if ptr else None,
                           Y["H"] if ptr else None, b["x"] if ptr else None, self.pg_w if ptr else None,
                           p[PG_B] if ptr else None, b["PG"] if ptr else None, Y["ATT"] if (ptr or hist) else None,
-                          b["ext"], b["lens"], b["top_ids"], b["top_lp"], b["logits"], b["vpart_ms"], b["vcand"],
-                          b["cmask"] if ptr else None, b["lp_sum"],
+                          b["ext"], b["lens"], b["top_ids"], b["top_lp"], b["logits"], b["vpart_ms"], b["lp_sum"],
                           b["latest"], b["gidx"], b["tok_hist"], b["par_hist"], b["done"], b["res_count"],
                           b["res_score"], b["res_len"], b["res_step"], b["res_par"], b["step"], b["art_ctr"],
                           b["gran"], b["tail_err"],

@@ -3,7 +3,7 @@ test_deterministic_mode_bit_identical -- train two deterministic-mode GraphTrain
 other (the first deleted before the second is built) and print, per step, which engine buffers and
 gradient slices differ (bit checksums).
 
-  python tools/det_seq_after_suite.py [--no-suite]
+  DSQ_SPLIT=4 python tools/det_seq_after_suite.py [--no-suite]
 """
 import json
 import os
@@ -60,6 +60,8 @@ def main():
         print("suite rc", rc, flush=True)
     import torch
     os.environ["TSAMD_DETERMINISTIC"] = "1"
+    if os.environ.get("DSQ_SPLIT"):  # row groups of the two deterministic trainers only (not the suite's)
+        os.environ["TSAMD_SPLIT"] = os.environ["DSQ_SPLIT"]
     from textsummarization_on_flink_amd.config import HParams
     from textsummarization_on_flink_amd.data.synthetic import SyntheticCorpus, make_batches
     from textsummarization_on_flink_amd.train.trainer import GraphTrainer

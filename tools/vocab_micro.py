@@ -37,12 +37,9 @@ def main():
     lg = torch.empty(R, V, device=dev)
     nt = int(k.vocab_topk_parts(V, H))
     pms = torch.empty(R, nt, 2, device=dev)
-    vc = torch.zeros(int(k.vocab_topk_cand(R, V, H)), device=dev)
-    from textsummarization_on_flink_amd.decode.device_beam import copy_bitmap
-    cm = copy_bitmap(ext, lens, V) if pg is not None else None
 
     def run():
-        k.vocab_topk(X, WT, bias, pg, attn, ext, lens, ids, lp, lg, pms, vc, cm, R, V, H, T, K, beam)
+        k.vocab_topk(X, WT, bias, pg, attn, ext, lens, ids, lp, lg, pms, R, V, H, T, K, beam)
 
     for _ in range(5):
         run()
