@@ -969,13 +969,6 @@ static bool lstm_bwd32() {
   }();
   return on;
 }
-static int bwd32_variant() {
-  static const int v = [] {
-    const char* e = getenv("TSAMD_BWD32_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
 static int lstm_rows(int H, int B, bool bwd) {
   return (H == 512 && B > 256 && (!bwd || lstm_bwd32())) ? 32 : 16;
 }
@@ -1057,14 +1050,7 @@ void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, con
     if (R == 32) {
 #define LB32(PC, SL) hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false, PC, SL>), dim3(grid), dim3(1024), 0, st, dz, \
                                         Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
-      switch (bwd32_variant()) {  // A/B sweep (TSAMD_BWD32_VARIANT)
-        case 1: LB32(2, 24); break;
-        case 2: LB32(2, 48); break;
-        case 3: LB32(4, 96); break;
-        case 4: LB32(2, 8); break;
-        case 5: LB32(4, 24); break;
-        default: LB32(2, 96);
-      }
+      LB32(2, 96);  // poll 2 peers per pass, s_sleep(96): profiles/r4/ab/bptt32.md
 #undef LB32
       continue;
     }

@@ -154,6 +154,7 @@ class ProcessBatcher:
         """``rank`` / ``world``: this process's data-parallel share of the records (the same
         ``seed`` on every rank: it fixes the shared file order)."""
         from ..runtime.ring import RecordRing
+        from ..utils.forking import fork_safe
         if workers < 1:
             raise ValueError("workers must be >= 1")
         if not 0 <= rank < world:
@@ -165,13 +166,14 @@ class ProcessBatcher:
         tag = _uuid.uuid4().hex[:10]
         ctx = mp.get_context("fork")
         self.rings, self.procs = [], []
-        for w in range(workers):
-            ring = RecordRing.create(f"/tsamd_ld_{tag}_{w}", ring_bytes)
-            p = ctx.Process(target=_worker, args=(w, workers, ring.name, data_path, vocab, hps, single_pass, seed,
-                                                  pad_enc_to, self.D, cache, rank, world), daemon=True)
-            p.start()
-            self.rings.append(ring)
-            self.procs.append(p)
+        with fork_safe():  # the children never collect the parent's (possibly GPU-owning) cycles
+            for w in range(workers):
+                ring = RecordRing.create(f"/tsamd_ld_{tag}_{w}", ring_bytes)
+                p = ctx.Process(target=_worker, args=(w, workers, ring.name, data_path, vocab, hps, single_pass, seed,
+                                                      pad_enc_to, self.D, cache, rank, world), daemon=True)
+                p.start()
+                self.rings.append(ring)
+                self.procs.append(p)
         self._live = list(range(workers))
         self._rr = 0
 

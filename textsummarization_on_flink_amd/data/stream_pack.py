@@ -96,6 +96,7 @@ class _Pool:
 
     def __init__(self, target, n: int, extra_rings: int, ring_bytes: int, args: tuple):
         from ..runtime.ring import RecordRing
+        from ..utils.forking import fork_safe
         if n < 1:
             raise ValueError("packers must be >= 1")
         tag = _uuid.uuid4().hex[:10]
@@ -103,10 +104,11 @@ class _Pool:
                       for p in range(n)]
         ctx = mp.get_context("fork")
         self.procs = []
-        for p in range(n):
-            pr = ctx.Process(target=target, args=(p, n, [r.name for r in self.rings[p]], *args), daemon=True)
-            pr.start()
-            self.procs.append(pr)
+        with fork_safe():  # the children never collect the parent's (possibly GPU-owning) cycles
+            for p in range(n):
+                pr = ctx.Process(target=target, args=(p, n, [r.name for r in self.rings[p]], *args), daemon=True)
+                pr.start()
+                self.procs.append(pr)
         self.pipes = []
 
     def check_alive(self, p: int) -> None:

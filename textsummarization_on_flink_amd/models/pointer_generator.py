@@ -253,13 +253,10 @@ class HipPointerGenerator:
         # 1 group 16.77, 3 groups 16.99, 4 groups 17.37-17.44; config #5 batch 1024: 2 = 4 = 204.4 ms, 8 206.6;
         # profiles/r3/ab/split_sorted.txt)
         # B = 128: 1 group 13.67 vs 2 groups 13.86 ms (profiles/r3/ab/small_batch.txt)
+        # Deterministic mode runs the same row groups: each row's arithmetic is the same on any
+        # stream, and test_deterministic_mode_bit_identical requires split 1 / 2 / 4 to give the
+        # single chain's bits (profiles/r4/det_streams.md: the round-3 one-chain override is gone)
         sp = cfg.split or (2 if B >= 256 and B % 32 == 0 else 1)
-        # deterministic mode: one chain.  With 4 concurrent row-group streams two deterministic
-        # runs of the projected-context path diverged in a few output-projection gradient columns
-        # when run late in the GPU test tier (history dependent; one chain and the E-form path
-        # were bit-identical there): profiles/r3/det_streams.md
-        if cfg.deterministic and not cfg.split:
-            sp = 1
         self.split = sp if (sp > 1 and B % (16 * sp) == 0) else 1
         # cfg.split_bwd: the decoder backward loop's own group count (default: split; B = 256 with
         # 4 forward groups: 4 backward groups 19.48 ms per step, 2 groups 19.79)
