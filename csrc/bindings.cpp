@@ -322,6 +322,15 @@ void cast_colsum(const Tensor& x, const Tensor& xb, const Tensor& colsum, int64_
   auto part = at::empty({(int64_t)cast_colsum_blocks((int)N, (int)C), C}, x.options());
   launch_cast_colsum(P<float>(x), P<bf16>(xb), P<float>(part), P<float>(colsum), (int)N, (int)C, stream());
 }
+// out[c] (= or += with acc) = sum_n x[n][c] in an order fixed by (N, C): x fp32 or bf16 [N][C]
+void colsum(const Tensor& x, const Tensor& out, int64_t N, int64_t C, bool acc) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && (x.scalar_type() == F32 || x.scalar_type() == BF),
+              "colsum: x must be a contiguous CUDA fp32 / bf16 tensor");
+  chk(out, F32, "out");
+  numel_eq(x, N * C, "x"); numel_eq(out, C, "out");
+  auto part = at::empty({(int64_t)colsum_det_chunks((int)N, (int)C), C}, out.options());
+  launch_colsum_det(x.data_ptr(), x.scalar_type() == BF, P<float>(part), P<float>(out), (int)N, (int)C, acc, stream());
+}
 
 // ---------------------------------------------------------------- reduce_states
 // cs / hs: the top encoder layer's step-frame states [2][T+1][B][H]; the kernels read rows T.
@@ -948,6 +957,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("transpose_bta", &transpose_bta);
   m.def("linear2_pair", &linear2_pair);
   m.def("cast_colsum", &cast_colsum);
+  m.def("colsum", &colsum);
   m.def("ptr_rowfin", &ptr_rowfin);
   m.def("clip_adagrad", &clip_adagrad);
   m.def("opt_parts", &opt_parts);

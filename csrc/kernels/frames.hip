@@ -165,3 +165,88 @@ void launch_cast_colsum(const float* x, bf16* xb, float* part, float* colsum, in
   hipLaunchKernelGGL(cast_colsum_kernel, dim3(G), dim3(256), 0, st, x, xb, part, N, C);
   hipLaunchKernelGGL(colsum_finish_kernel, dim3((C + 15) / 16), dim3(256), 0, st, part, colsum, G, C);
 }
+
+// Deterministic column sums out[c] (=, or += with acc) of a tall x [N][C] (fp32 or bf16):
+// the tall reductions of the backward (bias gradients: sum over tokens / decoder rows).
+// A torch sum(0) over ~10^5 rows splits each column over several workgroups and merges their
+// partials through a semaphore; on this device its results were not reproducible run to run
+// (profiles/r4/det_streams.md: the encoder LSTM bias gradient differed between two identical
+// deterministic-mode trainings while every weight gradient matched).  Here the order is fixed
+// by (N, C) alone: grid (column tiles of 256, G row chunks); wave w of a block sums rows
+// r0 + w, r0 + w + 4, ... of its chunk for 4 columns per lane, the 4 waves meet in LDS in wave
+// order, part[g][c] is stored, and colsum_det_finish adds the G partials in g order.
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void colsum_det_part_kernel(const T* __restrict__ x, float* __restrict__ part,
+                                                              int N, int C, int rpc) {
+  __shared__ float4 ps[4][64];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c0 = blockIdx.x * 256 + lane * 4;
+  const int r0 = blockIdx.y * rpc, r1 = min(N, r0 + rpc);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c0 < C) {
+    for (int r = r0 + wid; r < r1; r += 4) {
+      const T* p = x + (size_t)r * C + c0;
+      if constexpr (VEC) {  // C % 4 == 0: the lane's 4 columns in one load
+        if constexpr (sizeof(T) == 4) {
+          const float4 v = *reinterpret_cast<const float4*>(p);
+          s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+        } else {
+          const uint2 v = *reinterpret_cast<const uint2*>(p);
+          s[0] += __uint_as_float(v.x << 16); s[1] += __uint_as_float(v.x & 0xffff0000u);
+          s[2] += __uint_as_float(v.y << 16); s[3] += __uint_as_float(v.y & 0xffff0000u);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (c0 + j < C) s[j] += (float)p[j];
+      }
+    }
+  }
+  ps[wid][lane] = make_float4(s[0], s[1], s[2], s[3]);
+  __syncthreads();
+  if (wid == 0 && c0 < C) {
+    float4 t = ps[0][lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const float4 q = ps[w][lane];
+      t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
+    }
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+    float* dst = part + (size_t)blockIdx.y * C + c0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (c0 + j < C) dst[j] = tv[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_det_finish_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                                int G, int C, int acc) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += part[(size_t)g * C + c];
+  out[c] = acc ? out[c] + s : s;
+}
+
+// row chunks: about 2048 workgroups over the column tiles, at least 64 rows per chunk
+int colsum_det_chunks(int N, int C) {
+  const int nct = (C + 255) / 256;
+  int G = (2048 + nct - 1) / nct;
+  G = min(G, max(1, N / 64));
+  return max(1, G);
+}
+
+void launch_colsum_det(const void* x, bool bf, float* part, float* out, int N, int C, bool acc, hipStream_t st) {
+  if (N <= 0 || C <= 0) return;
+  const int G = colsum_det_chunks(N, C), rpc = (N + G - 1) / G;
+  const dim3 grid((C + 255) / 256, G);
+  const bool vec = C % 4 == 0;
+  if (bf) {
+    if (vec) hipLaunchKernelGGL((colsum_det_part_kernel<bf16, true>), grid, dim3(256), 0, st, (const bf16*)x, part, N, C, rpc);
+    else hipLaunchKernelGGL((colsum_det_part_kernel<bf16, false>), grid, dim3(256), 0, st, (const bf16*)x, part, N, C, rpc);
+  } else {
+    if (vec) hipLaunchKernelGGL((colsum_det_part_kernel<float, true>), grid, dim3(256), 0, st, (const float*)x, part, N, C, rpc);
+    else hipLaunchKernelGGL((colsum_det_part_kernel<float, false>), grid, dim3(256), 0, st, (const float*)x, part, N, C, rpc);
+  }
+  hipLaunchKernelGGL(colsum_det_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, out, G, C, acc ? 1 : 0);
+}

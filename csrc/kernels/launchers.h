@@ -170,6 +170,8 @@ void launch_from_step_frame(const float* in, const int64_t* rev, float* out, int
 void launch_transpose_bta(const bf16* in, bf16* out, int B, int T, int A, hipStream_t st);
 int cast_colsum_blocks(int N, int C);
 void launch_cast_colsum(const float* x, bf16* xb, float* part, float* colsum, int N, int C, hipStream_t st);
+int colsum_det_chunks(int N, int C);
+void launch_colsum_det(const void* x, bool bf, float* part, float* out, int N, int C, bool acc, hipStream_t st);
 void launch_emb_grad_sorted(float* gemb, const int* sid, const int* perm, const float* src0, int n0,
                             const float* src1, int n1, int E, int V, hipStream_t st);
 int emb_grad_det_chunks(int n);

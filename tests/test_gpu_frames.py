@@ -66,6 +66,30 @@ def test_cast_colsum(N, C):
     torch.testing.assert_close(cs.double(), ref, rtol=1e-5, atol=1e-4 * (N ** 0.5))
 
 
+@pytest.mark.parametrize("N,C,bf", [(25600, 1, False), (1, 3, False), (102400, 1024, True), (25600, 1024, True),
+                                    (25600, 50000, True), (999, 130, False), (256, 256, False), (37, 514, True)])
+def test_colsum_deterministic_matches_fp64(N, C, bf):
+    """colsum (frames.hip): column sums of a tall fp32 / bf16 matrix in an order fixed by (N, C) --
+    the deterministic replacement of torch sum(0) for the bias gradients -- vs an fp64 sum; two
+    runs give the same bits; acc adds onto the output."""
+    k = ops()
+    g = torch.Generator(device="cuda").manual_seed(N + C)
+    x = torch.randn(N, C, device="cuda", generator=g)
+    if bf:
+        x = x.bfloat16()
+    out = torch.empty(C, device="cuda")
+    k.colsum(x, out, N, C, False)
+    ref = x.double().sum(0)
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=2e-5 * (N ** 0.5))
+    again = torch.full((C,), 0.25, device="cuda")
+    for _ in range(3):
+        o2 = torch.empty(C, device="cuda")
+        k.colsum(x, o2, N, C, False)
+        assert torch.equal(o2.view(torch.int32), out.view(torch.int32))
+    k.colsum(x, again, N, C, True)
+    torch.testing.assert_close(again.double(), ref + 0.25, rtol=1e-5, atol=2e-5 * (N ** 0.5))
+
+
 @pytest.mark.parametrize("K,M,N,strided", [(1000, 128, 128, False), (25600, 256, 512, False), (3001, 128, 256, True),
                                            (130, 512, 128, True), (25600, 256, 5000, False), (3001, 256, 200, True)])
 def test_wgrad_tn_matches_fp32(K, M, N, strided):

@@ -774,7 +774,7 @@ class HipPointerGenerator:
                                   w["dlogits"], None if self.det else w["dbias"], N, V, H, ldx, vb, vn,
                                   w["vlive"] if inplace else None, w["vstate"] if inplace else None)
                 if self.det:  # column sums of the bf16 dlogits in a fixed order
-                    torch.sum(w["dlogits"], 0, dtype=F32, out=w["dbias"])
+                    k.colsum(w["dlogits"], w["dbias"], N, V, False)
             return
         torch.addmm(self.pk["ovb"], w["outb"], self.pk["ow"], out=w["logits"])
         self.k.ptr_loss(w["logits"], None, w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None,
@@ -918,7 +918,7 @@ class HipPointerGenerator:
             self.k.cast_colsum(x, xb, bias_grad, N, C)
         else:
             xb.copy_(x)
-            bias_grad.copy_(x.sum(0))
+            self.k.colsum(x, bias_grad, N, C, False)
         return xb
 
     def backward_mid(self):
@@ -957,7 +957,7 @@ class HipPointerGenerator:
             dC_dir, dX_dir = w["dC_dir"], w["dX_dir"]
             k.pgen_dirs(dpre, pm, dCTX_dir, dC_dir, dH_dir, dX_dir, None if self.det else g(PG_B).view(1), N, A, H, E)
             if self.det:
-                torch.sum(dpre, 0, keepdim=True, out=g(PG_B).view(1))
+                k.colsum(dpre, g(PG_B).view(1), N, 1, False)
         if self.proj_attn:
             return self._backward_mid_proj(dCTX_dir, dH_dir, dC_dir, dX_dir, Hn, wg, run)
         if dX_dir is not None and D > 1:  # p_gen path into ctx_{t-1} through x_t (hoisted out of the loop)
@@ -1068,7 +1068,7 @@ class HipPointerGenerator:
             gk = g(CELL_K)
             wg(gk[:E], w["Xb"].view(N, E), DZ)
             wg(gk[E:], w["Hb"][:D].reshape(N, H), DZ)
-            torch.sum(DZ, 0, dtype=F32, out=g(CELL_B))
+            k.colsum(DZ, g(CELL_B), N, 4 * H, False)
             gl = g(LIN_M)
             wg(gl[:E], emb_dec, DXb)
             gl[E:].zero_()
@@ -1084,9 +1084,9 @@ class HipPointerGenerator:
         w["dwc"].zero_()
         k.attn_bwd_feat(F, w["S"], v, wc, w["COV"][:D] if cov else None, w["DE"], lens, w["dF"], w["dv"],
                         w["dwc"] if cov else None, D, B, T, A, w["dlen"] if self.skip_pad else None)
-        g(VATT).copy_(w["dv"].sum(0).view_as(g(VATT)))
+        k.colsum(w["dv"], g(VATT).view(A), w["dv"].shape[0], A, False)
         if cov:
-            g(WCOV).view(A).copy_(w["dwc"].sum(0))
+            k.colsum(w["dwc"], g(WCOV).view(A), w["dwc"].shape[0], A, False)
         dFb = w["dF"].view(B * T, A)
         top = self.enc[-1]
         run(lambda: wg(g(WH).view(A, A), top["out"].view(B * T, A), dFb))
@@ -1123,7 +1123,7 @@ class HipPointerGenerator:
                  top["dc_carry"], top["dh_fin"], B, H)
         if self.det:  # bias gradients: relu'-masked row sums in a fixed order
             for pre, gsrc, dst in ((w["rs_pre"][0], w["dc_carry"], g(BRC)), (w["rs_pre"][1], w["dh_rec"], g(BRH))):
-                torch.sum(torch.where(pre > 0, gsrc, torch.zeros_like(gsrc)), 0, out=dst)
+                k.colsum(torch.where(pre > 0, gsrc, torch.zeros_like(gsrc)), dst, B, H, False)
         torch.mm(w["rs_cat"][0].t(), w["rs_dp"][0], out_dtype=F32, out=g(RC))
         torch.mm(w["rs_cat"][1].t(), w["rs_dp"][1], out_dtype=F32, out=g(RH))
         # ---- encoder BPTT, top layer down
@@ -1155,7 +1155,7 @@ class HipPointerGenerator:
                 if self.persistent_lstm and not self.det:
                     g(enc_b(layer, d)).copy_(w["lstm_db"][di])
                 else:
-                    g(enc_b(layer, d)).copy_(dzd.sum(0, dtype=F32))
+                    k.colsum(dzd, g(enc_b(layer, d)), T * B, 4 * H, False)
                 torch.mm(dzd, self.pk[f"enc{layer}_Kx{di}"].t(), out_dtype=F32, out=dxs[di])
             dx = st["dx"]
             k.from_step_frame(dxs, w["rev_idx"], dx, B, T, din)  # fw + reversed bw, batch frame
