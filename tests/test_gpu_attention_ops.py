@@ -235,10 +235,60 @@ def test_attn_bwd_rowp_matches_fp32(A, last):
     g = torch.full((B,), 0.7, device=dev)
     de, dcov = torch.full((B, T), float("nan"), device=dev), torch.full((B, T), float("nan"), device=dev)
     ds = torch.full((B, A), float("nan"), device=dev)
-    k.attn_bwd_rowp(G, F, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, None, 0)
+    k.attn_bwd_rowp(G, F, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, None, 0,
+                    None, None, None, None, 0)
     torch.cuda.synchronize()
     # the E-form reference with "E" = G and "dctx" = dx (zero at the last step)
     want = _reference(G, F, s, v, wc, cov, a, torch.zeros(B, EG, device=dev) if last else dx, Ga, dnext, g, lens)
     for name, got, ref in zip(("de", "ds", "dcov"), (de, ds, dcov), want):
         err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         assert err < 2e-3, (name, err)
+
+
+@pytest.mark.parametrize("A,H", [(512, 256), (1024, 512)])
+def test_attn_bwd_rowp_computes_dx_from_dz(A, H):
+    """The decoder backward in two launches: attn_bwd_rowp given dz_{t+1} computes
+    dx = dz_{t+1} . W_cell[:E]^T + dX_dir itself (stored to dx_out, dead rows zero) and gives the
+    gradients of the same kernel fed that dx."""
+    k = ops()
+    B, T, EG, G4 = 6, 300, 128, 4 * H
+    gen = torch.Generator(device="cuda").manual_seed(7 + A)
+    dev = "cuda"
+
+    def r(*shape, s=1.0):
+        return torch.randn(*shape, generator=gen, device=dev) * s
+
+    lens = torch.tensor([T, 1, 5, 129, 258, 300], dtype=torch.int32, device=dev)
+    mask = torch.arange(T, device=dev)[None, :] < lens[:, None].long()
+    G, F = r(B, T, EG, s=0.5).bfloat16(), r(B, T, A, s=0.5).bfloat16()
+    s, v, wc = r(B, A, s=0.3), r(A, s=0.1), r(A, s=0.1)
+    cov = torch.rand(B, T, generator=gen, device=dev) * mask
+    a = torch.softmax(r(B, T).masked_fill(~mask, float("-inf")), -1)
+    gv = torch.einsum("bt,bte->be", a, G.float())
+    dz = r(B, G4, s=0.1).bfloat16()
+    Kx = r(EG, G4, s=0.05).bfloat16()
+    dxdir = r(B, EG, s=0.01)
+    dlen = torch.tensor([9, 9, 2, 9, 9, 9], dtype=torch.int32, device=dev)  # row 2 is dead at step 4
+    dz[2] = 0
+    dxdir[2] = 0
+    Ga, dnext = r(B, T, s=0.1), r(B, T, s=0.1)
+    g = torch.full((B,), 0.7, device=dev)
+    dx_ref = dz.float() @ Kx.float().t() + dxdir
+    out = []
+    for fused in (False, True):
+        de, dcov = torch.full((B, T), float("nan"), device=dev), torch.full((B, T), float("nan"), device=dev)
+        ds = torch.full((B, A), float("nan"), device=dev)
+        dx_out = torch.full((B, EG), float("nan"), device=dev)
+        if fused:
+            k.attn_bwd_rowp(G, F, s, v, wc, cov, a, None, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, dlen, 4,
+                            dz, Kx, dxdir, dx_out, G4)
+        else:
+            k.attn_bwd_rowp(G, F, s, v, wc, cov, a, dx_ref, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, dlen, 4,
+                            None, None, None, None, 0)
+        torch.cuda.synchronize()
+        out.append((de, ds, dcov, dx_out))
+    err = float((out[1][3] - dx_ref).abs().max() / dx_ref.abs().max())
+    assert err < 1e-5, err
+    for name, got, ref in zip(("de", "ds", "dcov"), out[1][:3], out[0][:3]):
+        err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+        assert err < 1e-5, (name, err)

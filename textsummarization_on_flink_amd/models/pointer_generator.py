@@ -368,6 +368,7 @@ class HipPointerGenerator:
         # (row, step) pairs past the row's last loss-weighted step are skipped by the projected
         # kernels (their outputs are written as zeros; loss and gradients are unchanged)
         self.skip_pad = self.proj_attn and cfg.skip_pad_steps
+        self.dec_bwd_2l = self.proj_attn and cfg.dec_bwd_two_launch and 4 * H % 512 == 0 and 4 * H <= 2048
         self.compact_vocab = self.skip_pad and cfg.fused_vocab_train and cfg.compact_vocab_grad and not cfg.deterministic \
             and H in (128, 256, 512) and (D * B) % 32 == 0
         w["F"] = z(B, T, A, dt=BF)
@@ -955,9 +956,10 @@ class HipPointerGenerator:
                        g(PG_M).view(-1), N, A, H, E, self.det)
             # direct terms dCTX/dH += dp w_ctx/h, dC/dX = dp w_c/x and the bias gradient, one launch
             dC_dir, dX_dir = w["dC_dir"], w["dX_dir"]
-            k.pgen_dirs(dpre, pm, dCTX_dir, dC_dir, dH_dir, dX_dir, None if self.det else g(PG_B).view(1), N, A, H, E)
-            if self.det:
-                k.colsum(dpre, g(PG_B).view(1), N, 1, False)
+            # the p_gen bias gradient sum(dp) by colsum in both modes: pgen_dirs' one same-address atomic per
+            # workgroup (6400 at B = 256) serialised at L2 (95 us for a ~40 us kernel, round-3 kernel stats)
+            k.pgen_dirs(dpre, pm, dCTX_dir, dC_dir, dH_dir, dX_dir, None, N, A, H, E)
+            k.colsum(dpre, g(PG_B).view(1), N, 1, False)
         if self.proj_attn:
             return self._backward_mid_proj(dCTX_dir, dH_dir, dC_dir, dX_dir, Hn, wg, run)
         if dX_dir is not None and D > 1:  # p_gen path into ctx_{t-1} through x_t (hoisted out of the loop)
@@ -989,7 +991,7 @@ class HipPointerGenerator:
                                     dcov[t % 2][rs] if cov else None, Bg, T, A)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
-                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, None, 0)
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, None, 0, None, None)
                 k.dec_bwd_dz(w["DZ"][t][rs], self.pk["Wbig"], dX_dir[t][rs] if dX_dir is not None else None,
                              dCTX_dir[t - 1][rs] if t > 0 else None, w["DX"][t][rs],
                              w["DCTX"][t - 1][rs] if t > 0 else None, w["dh_rec"][rs], Bg, E, H, A, None, 0)
@@ -1022,23 +1024,39 @@ class HipPointerGenerator:
         dcov = w["dcov"]
         Kc = self.pk["Wbig"][:E + H]  # W_cell: [dx | dh] = dz . W_cell^T
         dlen = w["dlen"] if self.skip_pad else None
+        # two launches per step (cfg.dec_bwd_two_launch): dx_{t+1} = dz_{t+1} . W_cell[:E]^T (+ dX_dir) in
+        # the attention backward's prologue, dh_rec = dz_{t+1} . W_cell[E:]^T inside dec_bwd_cell; dx_0 and
+        # the final dh_rec after the loop.  Otherwise dec_bwd_dz produces both from dz_t at the end of
+        # every step.
+        two = self.dec_bwd_2l
+        Kx, Kh = Kc[:E], Kc[E:]  # views of W_cell^T rows: dx and dh_rec columns
 
         def chain(r0, r1):
             Bg, rs = r1 - r0, slice(r0, r1)
             dl = dlen[rs] if dlen is not None else None
             for t in reversed(range(D)):
+                nxt = t < D - 1
                 k.attn_bwd_rowp(G[rs], F[rs], w["S"][t][rs], v, wc, w["COV"][t][rs] if (cov and t > 0) else None,
-                                w["ATT"][t][rs], w["DX"][t + 1][rs] if t < D - 1 else None, w["GV"][t][rs],
-                                Ga[t][rs], dcov[(t + 1) % 2][rs] if (cov and t < D - 1) else None,
+                                w["ATT"][t][rs], w["DX"][t + 1][rs] if (nxt and not two) else None, w["GV"][t][rs],
+                                Ga[t][rs], dcov[(t + 1) % 2][rs] if (cov and nxt) else None,
                                 w["gcl"][t][rs] if cov else None, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
-                                dcov[t % 2][rs] if cov else None, Bg, T, A, dl, t)
+                                dcov[t % 2][rs] if cov else None, Bg, T, A, dl, t,
+                                w["DZ"][t + 1][rs] if (nxt and two) else None, Kx if two else None,
+                                dX_dir[t + 1][rs] if (nxt and two and dX_dir is not None) else None,
+                                w["DX"][t + 1][rs] if (nxt and two) else None, 4 * H)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
-                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, dl, t)
-                k.dec_bwd_dz(w["DZ"][t][rs], Kc, dX_dir[t][rs] if dX_dir is not None else None, None,
-                             w["DX"][t][rs], None, w["dh_rec"][rs], Bg, E, H, 0, dl, t)
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, dl, t,
+                               w["DZ"][t + 1][rs] if (nxt and two) else None, Kh if two else None)
+                if not two:
+                    k.dec_bwd_dz(w["DZ"][t][rs], Kc, dX_dir[t][rs] if dX_dir is not None else None, None,
+                                 w["DX"][t][rs], None, w["dh_rec"][rs], Bg, E, H, 0, dl, t)
 
         self._row_groups(chain, self.split_bwd)
+        if two:  # dx_0 and dh_rec = dz_0 . W_cell[E:]^T (the decoder's initial-state gradient, read by
+            # rs_bwd) over all rows in one launch; the loop produced dx_1 .. dx_{D-1}
+            k.dec_bwd_dz(w["DZ"][0], Kc, dX_dir[0] if dX_dir is not None else None, None, w["DX"][0], None,
+                         w["dh_rec"], B, E, H, 0, dlen, 0)
         w["DCTX"].copy_(dCTX_dir)
         if D > 1:
             dctx = w["DCTX"][:D - 1].view((D - 1) * B, A)
