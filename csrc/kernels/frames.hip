@@ -174,7 +174,7 @@ void launch_cast_colsum(const float* x, bf16* xb, float* part, float* colsum, in
 // deterministic-mode trainings while every weight gradient matched).  Here the order is fixed
 // by (N, C) alone: grid (column tiles of 256, G row chunks); wave w of a block sums rows
 // r0 + w, r0 + w + 4, ... of its chunk for 4 columns per lane, the 4 waves meet in LDS in wave
-// order, part[g][c] is stored, and colsum_det_finish adds the G partials in g order.
+// order, part[g][c] is stored, and colsum_det_finish adds the G partials in a fixed order.
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void colsum_det_part_kernel(const T* __restrict__ x, float* __restrict__ part,
                                                               int N, int C, int rpc) {
@@ -219,13 +219,27 @@ __global__ __launch_bounds__(256) void colsum_det_part_kernel(const T* __restric
   }
 }
 
+// out[c] (= or += acc) of the G partial rows: CPB columns x (256 / CPB) partial-row lanes per
+// block, every lane's loads independent (one round trip), then the lanes of a column summed in
+// lane order through LDS -- a fixed order for a given (G, C)
+template <int CPB>
 __global__ __launch_bounds__(256) void colsum_det_finish_kernel(const float* __restrict__ part, float* __restrict__ out,
                                                                 int G, int C, int acc) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  constexpr int GL = 256 / CPB;
+  __shared__ float red[GL][CPB + 1];
+  const int cl = threadIdx.x % CPB, gl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
   float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(size_t)g * C + c];
-  out[c] = acc ? out[c] + s : s;
+  if (c < C) {
+#pragma unroll 8
+    for (int g = gl; g < G; g += GL) s += part[(size_t)g * C + c];
+  }
+  red[gl][cl] = s;
+  __syncthreads();
+  if (gl == 0 && c < C) {
+    float t = 0.f;
+    for (int i = 0; i < GL; ++i) t += red[i][cl];
+    out[c] = acc ? out[c] + t : t;
+  }
 }
 
 // row chunks: about 2048 workgroups over the column tiles, at least 64 rows per chunk
@@ -248,5 +262,8 @@ void launch_colsum_det(const void* x, bool bf, float* part, float* out, int N, i
     if (vec) hipLaunchKernelGGL((colsum_det_part_kernel<float, true>), grid, dim3(256), 0, st, (const float*)x, part, N, C, rpc);
     else hipLaunchKernelGGL((colsum_det_part_kernel<float, false>), grid, dim3(256), 0, st, (const float*)x, part, N, C, rpc);
   }
-  hipLaunchKernelGGL(colsum_det_finish_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, out, G, C, acc ? 1 : 0);
+  if (C >= 64)
+    hipLaunchKernelGGL(colsum_det_finish_kernel<16>, dim3((C + 15) / 16), dim3(256), 0, st, part, out, G, C, acc ? 1 : 0);
+  else
+    hipLaunchKernelGGL(colsum_det_finish_kernel<1>, dim3(C), dim3(256), 0, st, part, out, G, C, acc ? 1 : 0);
 }

@@ -123,7 +123,7 @@ def test_stream_decode_packer_answers_every_row():
         # the pack is the one a Batch of these examples gives (padding rows, [START], first target)
         lens =[int(np.nonzero(enc[i] != 1)[0].max()) + 1 for i in range(b.n_valid)]
         mine = [by_ids[tuple(enc[i, :lens[i]].tolist())] for i in range(b.n_valid)]
-        ref = pack_host_inputs(host_inputs(Batch(mine, hb, vocab, pad_enc_to=T), hb, 1), layout)
+        ref = pack_host_inputs(host_inputs(Batch(mine, hb, vocab, pad_enc_to=T), hb, 1, need_grad=False), layout)
         assert bytes(b.host_pack) == ref.tobytes()
         # "decoded" summary of article i: its first three tokens, then [STOP]
         pool.send_results(b, [enc[i, :3].tolist() + [stop, 5] for i in range(b.n_valid)])

@@ -36,7 +36,7 @@ import os
 import struct
 import time
 import uuid as _uuid
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 from .batch import Batch
 from .batcher import IterRowReader, _StreamBatcher
@@ -263,6 +263,20 @@ def finish_rows(entries, results, vocab, hps, html_escape: bool = False):
 
 
 _EX = struct.Struct("<iii")  # example record: (example id, encoder length, first target id) + enc + ext ids
+_RES = struct.Struct("<i")   # result record: n, then n (example id, length) int32 pairs, then the ids
+
+
+def _results(rec) -> List[Tuple[int, List[int]]]:
+    """A result record -> [(example id, token ids)]."""
+    import numpy as np
+    n = _RES.unpack_from(rec, 0)[0]
+    head = np.frombuffer(rec, dtype=np.int32, count=2 * n, offset=_RES.size).reshape(n, 2)
+    body = np.frombuffer(rec, dtype=np.int32, offset=_RES.size + 8 * n).tolist()
+    out, o = [], 0
+    for e, L in head.tolist():
+        out.append((e, body[o:o + L]))
+        o += L
+    return out
 
 
 def _decode_packer(p: int, n: int, names: List[str], coding, out_coding, vocab, hps, T: int) -> None:
@@ -302,9 +316,9 @@ def _decode_packer(p: int, n: int, names: List[str], coding, out_coding, vocab, 
     def _finish(rec):
         if rec is None:
             raise RuntimeError("decoder closed the result ring with examples pending")
-        meta, _ = _split_record(rec)
-        ents = [pending.pop(e) for e, _ids in meta["r"]]
-        for row in finish_rows(ents, [ids for _e, ids in meta["r"]], vocab, hps, bool(hps.html_escape)):
+        res = _results(rec)
+        ents = [pending.pop(e) for e, _ids in res]
+        for row in finish_rows(ents, [ids for _e, ids in res], vocab, hps, bool(hps.html_escape)):
             _push(rfin, out_coding.encode(dict(zip(fields, row))))
 
     try:
@@ -473,16 +487,20 @@ class StreamDecodePacker:
                 time.sleep(0.0002)
                 self._gather(items, owners)
         rows = _DecodeRows(items, self.Na, self.T, self.pad_id, self.start_id)
-        buf = pack_host_inputs(host_inputs(rows, self.hb, 1), self.layout)
+        buf = pack_host_inputs(host_inputs(rows, self.hb, 1, need_grad=False), self.layout)
         return DecodePackedBatch(memoryview(buf), self.Na, self.T, owners)
 
     def send_results(self, batch: DecodePackedBatch, ids: List[List[int]]) -> None:
-        """Best-hypothesis token ids (after [START]) per valid row, routed to the packers."""
+        """Best-hypothesis token ids (after [START]) per valid row, routed to the packers: one
+        binary record per packer, (example id, length) int32 pairs then the ids (``_results``)."""
+        import numpy as np
         per = {}
         for (p, eid), t in zip(batch.owners, ids):
-            per.setdefault(p, []).append([eid, t])
+            per.setdefault(p, []).append((eid, t))
         for p, r in per.items():
-            _push(self.pool.rings[p][2], _meta_record({"r": r}))
+            head = np.array([(e, len(t)) for e, t in r], dtype=np.int32).reshape(-1)
+            body = np.concatenate([np.asarray(t, dtype=np.int32) for _e, t in r]) if r else np.zeros(0, np.int32)
+            _push(self.pool.rings[p][2], _RES.pack(len(r)) + head.tobytes() + body.tobytes())
 
     def close(self) -> None:
         """After the last result: end the result rings, let the packers flush, join the fanin."""

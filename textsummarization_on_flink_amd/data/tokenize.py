@@ -36,16 +36,23 @@ def word_tokenize(text: str, ptb_brackets: bool = False) -> List[str]:
     text = re.sub(r'(?<=[\s(\[{<])"', " `` ", text)
     text = text.replace('"', " '' ")
     out: List[str] = []
+    append = out.append
     for tok in _TOKEN_RE.findall(text):
-        m = _CONTRACTION.match(tok)
-        if m and len(m.group(1)) > 0 and tok.lower() not in ("can't",):
-            out.extend([m.group(1), m.group(2)])
-        elif tok.lower() == "can't":
-            out.extend([tok[:2], tok[2:]])
+        if "'" in tok:  # every contraction suffix holds an apostrophe: the regex only runs on those
+            low = tok.lower()
+            m = _CONTRACTION.match(tok)
+            if m and len(m.group(1)) > 0 and low != "can't":
+                out.extend([m.group(1), m.group(2)])
+            elif low == "can't":
+                out.extend([tok[:2], tok[2:]])
+            elif ptb_brackets and tok in _BRACKETS:
+                append(_BRACKETS[tok])
+            else:
+                append(tok)
         elif ptb_brackets and tok in _BRACKETS:
-            out.append(_BRACKETS[tok])
+            append(_BRACKETS[tok])
         else:
-            out.append(tok)
+            append(tok)
     return out
 
 

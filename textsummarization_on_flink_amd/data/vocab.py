@@ -129,10 +129,13 @@ def outputids2words(id_list: Sequence[int], vocab: Vocab, article_oovs: Optional
     """Map ids (incl. temporary OOV ids) back to words (``data.py:196-219``)."""
     words = []
     V = vocab.size()
+    table = vocab._id_to_word
     for i in id_list:
         i = int(i)
-        if i < V:
-            words.append(vocab.id2word(i))
+        if 0 <= i < V:
+            words.append(table[i])
+        elif i < 0:
+            raise ValueError(f"Id not found in vocab: {i}")
         else:
             if article_oovs is None:
                 raise ValueError("model produced a word ID that isn't in the vocabulary (baseline mode)")

@@ -450,6 +450,7 @@ class DeviceBeamDecoder:
         it = iter(batches)
         ov = self.overlap_encoder
         batch, pre = None, False
+        done_src = False  # the source ended while prefetching
         while True:
             if batch is None:
                 batch = next(it, None)
@@ -472,16 +473,30 @@ class DeviceBeamDecoder:
                 nxt = None  # polled again once this batch is queued
             elif nxt is not None:
                 self._rows_ok(nxt)
-            first = True
+            first, fetched = True, ov
             for _ in self.run_chunks(batch, pre_encoded=pre, next_batch=nxt):
                 if first and pending is not None:  # the GPU has this batch's work queued
                     yield self._finish(pending)
                     pending = None
                 first = False
+                if not fetched and self.steps_run >= self.maxD:
+                    # the last chunk is queued (and the one before it may still run): take the next
+                    # batch now, so forming and packing it overlaps the GPU instead of following it
+                    # (a streaming source forms it from the requests that arrived meanwhile)
+                    fetched = True
+                    nxt = next(it, None)
+                    if nxt is self.FLUSH:
+                        nxt = None  # nothing ready: polled again once this batch is done
+                    elif nxt is not None:
+                        self._rows_ok(nxt)
+                    else:
+                        done_src = True
             arrays, ev = self._snapshot(slot)
             slot ^= 1
             pending = (arrays, ev, self._n_valid(batch), self.steps_run)
-            batch, pre = nxt, nxt is not None
+            batch, pre = nxt, (nxt is not None and ov)
+            if batch is None and done_src:
+                break
         if pending is not None:
             yield self._finish(pending)
 

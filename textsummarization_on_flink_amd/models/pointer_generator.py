@@ -89,7 +89,7 @@ def mmf(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return torch.mm(a, b, out_dtype=F32)
 
 
-def host_inputs(batch, hps, D: int, sort_rows: bool = False) -> Dict[str, np.ndarray]:
+def host_inputs(batch, hps, D: int, sort_rows: bool = False, need_grad: bool = True) -> Dict[str, np.ndarray]:
     """The engine's per-batch inputs as host arrays (pure numpy: runs in loader worker
     processes too): token ids, lengths, the reversed-index map of the backward LSTM
     direction, extended-vocab ids, step-major decoder inputs / targets and the per-(step,
@@ -98,7 +98,10 @@ def host_inputs(batch, hps, D: int, sort_rows: bool = False) -> Dict[str, np.nda
     ``sort_rows``: the engine's rows are the batch's rows ordered by live decoder steps, longest
     first (stable), so the steps a row skips past its summary form a suffix of the rows at every
     decoder step and whole 16-row tiles of the decoder kernels go idle together.  The loss is a
-    sum over rows; ``row_src[b]`` is the batch row of engine row b."""
+    sum over rows; ``row_src[b]`` is the batch row of engine row b.
+
+    ``need_grad`` False (decode / eval packs): the embedding-gradient id order is not computed
+    (zeros; no backward reads it) -- the largest host cost of a serving batch."""
     T = batch.enc_batch.shape[1]
     lens = batch.enc_lens.astype(np.int64)
     if lens.min() < 1:
@@ -126,7 +129,10 @@ def host_inputs(batch, hps, D: int, sort_rows: bool = False) -> Dict[str, np.nda
     enc_batch, ext, rev = batch.enc_batch[src], batch.enc_batch_extend_vocab[src], rev[src]
     enc_lens, rowg, gcl, dlen = batch.enc_lens[src], rowg[src], gcl[src], dlen[src]
     dec_t = np.ascontiguousarray(batch.dec_batch[src, :D].T).astype(np.int64)
-    sid, perm = emb_sort(enc_batch, dec_t)
+    if need_grad:
+        sid, perm = emb_sort(enc_batch, dec_t)
+    else:
+        sid = perm = np.zeros(enc_batch.size + dec_t.size, dtype=np.int32)
     # the fused vocab head's 32-row blocks of the t-major [D * B] rows that hold a live row, listed
     # first (vblk, vblk_n of them); vlive per block (the blocks pass 2 must keep zeroed)
     nb = (D * len(dlen) + 31) // 32
@@ -601,7 +607,8 @@ class HipPointerGenerator:
                 raise ValueError(f"host pack of {len(packed)} bytes, engine expects {hn.nbytes}")
             hn[:] = np.frombuffer(packed, dtype=np.uint8)
         else:
-            pack_host_inputs(host_inputs(batch, self.hps, self.D, sort_rows=self.skip_pad), self._in_layout, hn)
+            pack_host_inputs(host_inputs(batch, self.hps, self.D, sort_rows=self.skip_pad,
+                                         need_grad=getattr(self.hps, "mode", "train") != "decode"), self._in_layout, hn)
         if self.compact_vocab:  # this batch's live vocab-head blocks -> the head's block-count bucket
             o = self._in_off["vblk_n"]
             nlive = int(np.frombuffer(hn, dtype=np.int32, count=1, offset=o)[0])
