@@ -306,6 +306,7 @@ def bench_config5(args, info, D, torch, dev_id):
     batches = make_batches(hps, vocab, corpus, 2, pad_enc_to=c["enc"])
     tr = GraphTrainer(hps, vocab.size(), B=c["batch"], T=c["enc"], device=f"cuda:{dev_id}", info=info,
                       use_graph=not args.no_graph)
+    n_warm = len(batches)
     for b in batches:  # warm-up: graph capture, then a replay of each batch (each live-row bucket's head graph)
         out = tr.step(b)
     tr.check_finite(out)
@@ -330,7 +331,7 @@ def bench_config5(args, info, D, torch, dev_id):
            "config5_config": {"model": f"pointer-generator+coverage hidden={c['hidden']} emb={args.emb} "
                                        f"enc={c['enc']} dec={args.dec} vocab={args.vocab} enc_layers={c['layers']}",
                               "per_gpu_batch": c["batch"], "global_batch": c["batch"] * info.world,
-                              "steps": args.config5_steps, "warmup": len(batches)}}
+                              "steps": args.config5_steps, "warmup": n_warm}}
     if args.decode_batches > 0:
         a5 = _ap.Namespace(**{**vars(args), "hidden": c["hidden"], "layers": c["layers"], "enc": c["enc"],
                               "decode_batches": 4})

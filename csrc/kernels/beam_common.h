@@ -20,54 +20,71 @@ __device__ __forceinline__ void beam_step_body(
   const int norig = t == 0 ? 1 : beam;
   const int ncand = norig * K;
   if (lane >= ncand) tot = -INFINITY;
-  if (lane < ncand) {
-    cval[lane] = tot;
-    cid[lane] = tid_cand;
-  }
-  // stable rank: descending total, ties keep candidate order
+  // stable rank: descending total, ties keep candidate order (readlane: a uniform lane index,
+  // no LDS permute per candidate)
   int rank = 0;
   for (int q = 0; q < ncand; ++q) {
-    const float v = __shfl(tot, q, 64);
+    const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tot), q));
     if (v > tot || (v == tot && q < lane)) ++rank;
   }
-  if (lane < ncand) srt[rank] = lane;
+  if (lane < ncand) {  // rank-ordered candidate table: value, token, parent
+    cval[rank] = tot;
+    cid[rank] = tid_cand;
+    srt[rank] = lane / K;
+  }
+  __shared__ float nlp[BEAM_CAND_MAX];
+  __shared__ int ntok[BEAM_CAND_MAX], npar[BEAM_CAND_MAX];
+  __shared__ int nh_s, nres_s;
   __syncthreads();
-  if (lane == 0) {
-    int nres = nres0, nh = 0;
-    float new_lp[BEAM_CAND_MAX];
-    int new_tok[BEAM_CAND_MAX], new_par[BEAM_CAND_MAX];
-    for (int q = 0; q < ncand; ++q) {
-      const int cnd = srt[q];
-      const int i = cnd / K, tok = cid[cnd];
-      const float v = cval[cnd];
-      if (tok == stop_id) {
-        if (t >= min_dec && nres < beam) {
-          res_score[a * beam + nres] = v / (float)(t + 2);
-          res_len[a * beam + nres] = t + 2;
-          res_step[a * beam + nres] = t;
-          res_par[a * beam + nres] = i;
-          ++nres;
-        }
-      } else if (nh < beam) {
-        new_lp[nh] = v;
-        new_tok[nh] = tok;
-        new_par[nh] = i;
-        ++nh;
-      }
-      if (nh == beam || nres == beam) break;
+  // The reference walks the ranked candidates in order: a STOP (from step min_dec on) becomes a
+  // result, any other token a new hypothesis, until beam of either (beam_search.py:120-150).
+  // Here every rank position decides at once: with the exclusive counts of results / hypotheses
+  // ranked before it (ballot + popcount), position q is reached iff both counts are still below
+  // beam, and its slot is that count.
+  if (lane < 64) {
+    const bool act = lane < ncand;
+    const int tok = act ? cid[lane] : 0;
+    const bool is_res = act && tok == stop_id && t >= min_dec;
+    const bool is_hyp = act && tok != stop_id;
+    const unsigned long long below = (1ull << lane) - 1ull;  // lanes < this one (lane <= 63)
+    const unsigned long long mres = __ballot(is_res), mhyp = __ballot(is_hyp);
+    const int ns = __popcll(mres & below), nn = __popcll(mhyp & below);
+    const bool reached = act && nn < beam && nres0 + ns < beam;
+    const float v = act ? cval[lane] : 0.f;
+    const int par = act ? srt[lane] : 0;
+    if (reached && is_res) {
+      const int slot = a * beam + nres0 + ns;
+      res_score[slot] = v / (float)(t + 2);
+      res_len[slot] = t + 2;
+      res_step[slot] = t;
+      res_par[slot] = par;
     }
-    res_count[a] = nres;
-    if (nres >= beam) done[a] = 1;
-    for (int k = 0; k < beam; ++k) {
-      const int kk = k < nh ? k : (nh > 0 ? nh - 1 : 0);
-      const int par = nh > 0 ? new_par[kk] : 0;
-      lp_sum[base + k] = nh > 0 ? new_lp[kk] : -INFINITY;
-      latest[base + k] = nh > 0 ? new_tok[kk] : stop_id;
-      gidx[base + k] = base + par;
-      tok_hist[(size_t)t * Na * beam + base + k] = nh > 0 ? new_tok[kk] : stop_id;
-      par_hist[(size_t)t * Na * beam + base + k] = par;
+    if (reached && is_hyp) {
+      nlp[nn] = v;
+      ntok[nn] = tok;
+      npar[nn] = par;
+    }
+    const unsigned long long mreach = __ballot(reached);
+    if (lane == 0) {
+      const int nres = nres0 + __popcll(mres & mreach);
+      nh_s = __popcll(mhyp & mreach);
+      nres_s = nres;
+      res_count[a] = nres;
+      if (nres >= beam) done[a] = 1;
     }
   }
+  __syncthreads();
+  if (lane < beam) {
+    const int nh = nh_s, k = lane;
+    const int kk = k < nh ? k : (nh > 0 ? nh - 1 : 0);
+    const int par = nh > 0 ? npar[kk] : 0;
+    lp_sum[base + k] = nh > 0 ? nlp[kk] : -INFINITY;
+    latest[base + k] = nh > 0 ? ntok[kk] : stop_id;
+    gidx[base + k] = base + par;
+    tok_hist[(size_t)t * Na * beam + base + k] = nh > 0 ? ntok[kk] : stop_id;
+    par_hist[(size_t)t * Na * beam + base + k] = par;
+  }
+  (void)nres_s;
 }
 
 

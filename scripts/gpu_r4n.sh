@@ -1,6 +1,7 @@
 #!/bin/bash
 # round-4: the whole GPU tier after the serving-path changes (next batch prefetched during the
 # current batch's last chunk, decode packs without the embedding sort, binary result records;
+# beam bookkeeping ranked and selected in parallel (ballot prefix counts);
 # colsum finish), then decode / stream throughput / latency
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
