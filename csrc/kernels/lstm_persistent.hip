@@ -463,7 +463,7 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
 // (its own partial stays in LDS): per step a lane reads 4 x (NC-1) granules instead of 32.
 // NW = 4 or 8 waves: the cell update covers the tile's 16 rows x 64 units with RPL = 16 / NW
 // rows per lane (4 or 2); waves < NC run the partial GEMM (at H = 512, NC = 8: all 8 waves).
-template <int H, int NW, bool NT, bool EARLY = false>
+template <int H, int NW, bool NT>
 __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
@@ -636,7 +636,6 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
       store_dz();  // own-lane LDS values: no barrier needed
       break;
     }
-    if constexpr (EARLY) store_dz();  // in flight during the barrier / MFMA / publish
     __syncthreads();  // dz slice complete in LDS (and every lane has read Pown)
     // ---- partial dh over this slice's gate columns, for units 64*wid .. +63
     if (wid < NC) {
@@ -665,7 +664,7 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
                         __float_as_uint(acc[t][r]));
     }
     }
-    if constexpr (!EARLY) store_dz();
+    store_dz();
     __syncthreads();  // Pown visible before the next step reads it; Ash free for rewriting
   }
 #pragma unroll
@@ -702,7 +701,7 @@ __device__ __forceinline__ const gu64* gboff(const gu64* p, unsigned bytes) {
 }
 
 // PC: peers polled per chunk (4: 8 registers spill); SL: s_sleep between poll passes
-template <bool NT, int PC = 2, int SL = 96, bool EARLY = false>
+template <bool NT, int PC = 2, int SL = 96>
 __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
@@ -855,7 +854,6 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
       store_dz();
       break;
     }
-    if constexpr (EARLY) store_dz();  // own-lane LDS values: in flight during the barrier / MFMA / publish
     __syncthreads();  // dz slice complete in LDS (and every lane has read Pown)
     // ---- partial dh over this slice's gate columns, output units 32 wid .. +31, all 32 rows
     f32x4 acc[2][2];
@@ -895,7 +893,7 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
             store_granule(gboff(dst, lo + (unsigned)((rt * 16 + r) * 64 + 16 * t) * 8u), (unsigned)(T - s),
                           __float_as_uint(acc[rt][t][r]));
     }
-    if constexpr (!EARLY) store_dz();
+    store_dz();
     __syncthreads();  // Pown visible before the next step reads it; Ash free for rewriting
   }
 #pragma unroll
@@ -968,15 +966,6 @@ static bool lstm_bwd32() {
   static const int on = [] {
     const char* e = getenv("TSAMD_LSTM_BWD32");
     return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on;
-}
-// A/B switch (TSAMD_LSTM_EARLY_DZ=1): the BPTT's dz stores issued right after the cell update
-// instead of after the hand-off publish
-static bool bwd_early_dz() {
-  static const bool on = [] {
-    const char* e = getenv("TSAMD_LSTM_EARLY_DZ");
-    return e && e[0] == '1';
   }();
   return on;
 }
@@ -1061,20 +1050,13 @@ void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, con
     if (R == 32) {
 #define LB32(PC, SL) hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false, PC, SL>), dim3(grid), dim3(1024), 0, st, dz, \
                                         Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
-      if (bwd_early_dz()) hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false, 2, 96, true>), dim3(grid), dim3(1024), 0,
-                                             st, dz, Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B,
-                                             ntile, t0, n);
-      else LB32(2, 96);  // poll 2 peers per pass, s_sleep(96): profiles/r4/ab/bptt32.md
+      LB32(2, 96);  // poll 2 peers per pass, s_sleep(96): profiles/r4/ab/bptt32.md
 #undef LB32
       continue;
     }
 #define LAUNCH_B(HH, NTV)                                                                                                 \
-  if (bwd_early_dz())                                                                                                \
-    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV, true>), dim3(grid), dim3(512), 0, st, dz, Wn, dout,   \
-                       dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n);                          \
-  else                                                                                                               \
-    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin, \
-                       dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+  hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin,   \
+                     dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
     if (H == 64) LAUNCH_B(64, false);
     else if (H == 128) LAUNCH_B(128, false);
     else if (H == 256) LAUNCH_B(256, false);
