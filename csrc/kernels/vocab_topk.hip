@@ -12,6 +12,7 @@
 //                       union copied ids).
 // Replaces a library GEMM + a separate per-element top-k pass over the logits.
 #include "common.h"
+#include <stdlib.h>
 #include "attn_common.h"  // f32x2 packed-FP32 helpers
 #include "beam_common.h"  // beam bookkeeping fused into the select kernel's tail
 #include "launchers.h"
@@ -49,7 +50,7 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 // lane's 4 consecutive columns per i are one 16-byte store (a row's 64 columns = one 256-byte
 // run over the 4 i and 4 q).  Replaced a [row = lane group] layout whose per-row reductions
 // took 16-lane DPP trees for each of the lane's 16 rows and an LDS staging pass for stores.
-template <bool FULL, int NI>
+template <bool FULL, int NI, bool NTS = false>
 __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[NI][4], int jr, const f32x2 (&bc)[NI][2],
                                             float* __restrict__ logits, float* Pm, float* Ps, int rb, int cw,
                                             int lane, int R, int V) {
@@ -85,7 +86,11 @@ __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[NI][4], int jr, c
     float* dst = logits + (size_t)row * V + cw + q4;
 #pragma unroll
     for (int i = 0; i < NI; ++i)
-      *reinterpret_cast<float4*>(dst + 16 * i) = make_float4(x[i][0].x, x[i][0].y, x[i][1].x, x[i][1].y);
+      if constexpr (NTS)
+        __builtin_nontemporal_store(f32x4{x[i][0].x, x[i][0].y, x[i][1].x, x[i][1].y},
+                                    reinterpret_cast<f32x4*>(dst + 16 * i));
+      else
+        *reinterpret_cast<float4*>(dst + 16 * i) = make_float4(x[i][0].x, x[i][0].y, x[i][1].x, x[i][1].y);
   } else if (row < R) {
     float* dst = logits + (size_t)row * V;
 #pragma unroll
@@ -110,7 +115,10 @@ __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[NI][4], int jr, c
 // workgroups and W^T fetches: 392 tiles at R = 256 = one round), X tile 68 KB of LDS.
 // HFIX: H == HMAX, known at compile time (the X-staging row / chunk split by H / 8 is then a
 // shift instead of an integer division per 16-byte chunk)
-template <int OCC, int RH, int HMAX, bool HFIX = false>
+// NTS: the logits stores are non-temporal -- the select kernel re-reads only the K best tiles
+// and the copied words of each row, so 51 MB per step (R = 256) need not displace L2 lines:
+// 25.1 -> 23.6 us, decode 6092-6102 -> 6143-6155 summaries/s (profiles/r4/ab/decode_logits_nt.md)
+template <int OCC, int RH, int HMAX, bool HFIX = false, bool NTS = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void vocab_logits_kernel(
     const bf16* __restrict__ X,     // [R][H]  output-projection activations (bf16)
     const bf16* __restrict__ WT,    // [V][H]  output_projection/w transposed ("Bt")
@@ -193,7 +201,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
       if (full)
-        vl_epilogue<true, NI>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
+        vl_epilogue<true, NI, NTS>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
       else
         vl_epilogue<false, NI>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
     }
