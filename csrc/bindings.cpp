@@ -494,9 +494,11 @@ void wgrad_tn(const Tensor& a, const Tensor& b, const Tensor& out) {
 
 // weight repack (pack.hip): jobs [nj][13] int64 on the device (see the kernel for the layout)
 int64_t pack_max_jobs_op() { return pack_max_jobs(); }
+int64_t pack_job_cols_op() { return pack_job_cols(); }
+// total: the number of workgroups (sum of the jobs' block counts, pack.hip)
 void pack_cast(const Tensor& jobs, int64_t total) {
   TORCH_CHECK(jobs.is_cuda() && jobs.scalar_type() == at::kLong && jobs.is_contiguous() && jobs.dim() == 2 &&
-              jobs.size(1) == 13, "pack_cast: jobs [nj][13] int64 on the GPU");
+              jobs.size(1) == pack_job_cols(), "pack_cast: jobs [nj][", pack_job_cols(), "] int64 on the GPU");
   TORCH_CHECK(jobs.size(0) >= 1 && jobs.size(0) <= pack_max_jobs(), "pack_cast: 1..", pack_max_jobs(), " jobs");
   launch_pack_cast(P<long>(jobs), (int)jobs.size(0), (long)total, stream());
 }
@@ -954,6 +956,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("pgen_dirs", &pgen_dirs);
   m.def("pack_cast", &pack_cast);
   m.def("pack_max_jobs", &pack_max_jobs_op);
+  m.def("pack_job_cols", &pack_job_cols_op);
   m.def("debug_enabled", &debug_enabled);
   m.def("debug_status", &debug_status);
   m.def("debug_clear", &debug_clear);

@@ -193,6 +193,7 @@ void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out,
 
 // weight repack as one launch over a job table (pack.hip)
 int pack_max_jobs();
+int pack_job_cols();
 void launch_pack_cast(const long* jobs, int nj, long total, hipStream_t st);
 
 // p_gen gradient into the decoder inputs' direct terms + bias gradient (decoder.hip)

@@ -224,16 +224,19 @@ def test_skip_pad_steps_same_loss_and_gradients(monkeypatch, coverage, pointer_g
         assert float(a1[~live].abs().max()) == 0.0
 
 
-@pytest.mark.parametrize("layers,H", [(1, 256), (2, 128)])
-def test_fast_pack_matches_torch_pack(layers, H):
-    """pack() after the first call = one pack_cast launch over the job table (pack.hip): every
-    bf16 / fp32 layout bit-identical to the torch cast / transpose / cat path."""
+@pytest.mark.parametrize("layers,H,V", [(1, 256, 2000), (2, 128, 2000), (1, 256, 50000)])
+def test_fast_pack_matches_torch_pack(layers, H, V):
+    """pack() after the first call = one pack_cast launch over the job table (pack.hip: contiguous
+    copies, 64 x 64 transposes, generic strided jobs): every bf16 / fp32 layout bit-identical to
+    the torch cast / transpose / cat path (V = 50k: the bench's 12.8M-element vocab transpose)."""
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
-    hps = HParams(batch_size=16, max_enc_steps=32, max_dec_steps=6, vocab_size=2000, emb_dim=128, hidden_dim=H,
+    hps = HParams(batch_size=16, max_enc_steps=32, max_dec_steps=6, vocab_size=V, emb_dim=128, hidden_dim=H,
                   coverage=True, pointer_gen=True, enc_layers=layers)
-    params = build_params(hps, 2000, device="cuda", seed=2).enable_grad()
-    eng = HipPointerGenerator(hps, 2000, params, B=16, T=32, D=6)
+    params = build_params(hps, V, device="cuda", seed=2).enable_grad()
+    eng = HipPointerGenerator(hps, V, params, B=16, T=32, D=6)
     assert eng._pack_jobs is not None
+    kinds = eng._pack_jobs[:, 12].tolist()
+    assert 1 in kinds and 2 in kinds and 0 in kinds, kinds
     params.flat.add_(torch.randn_like(params.flat) * 0.01)  # new master weights
     eng.pack()  # fast path
     torch.cuda.synchronize()

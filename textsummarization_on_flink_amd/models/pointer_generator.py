@@ -511,9 +511,12 @@ class HipPointerGenerator:
         return pairs
 
     def _build_pack_jobs(self):
+        """The pack_cast job table (pack.hip): per layout its kind -- contiguous copy (2048
+        elements per workgroup), transpose of a contiguous matrix (64 x 64 tiles) or generic
+        strided (256) -- and its first workgroup."""
         E = self.E
         self._wcomb = torch.mm(self.p[LIN_M][E:], self.p[CELL_K][:E])
-        rows, off = [], 0
+        rows, blk = [], 0
         for dst, src in self._pack_job_pairs():
             assert dst.shape == src.shape and src.dtype == F32 and dst.dtype in (BF, F32) and dst.dim() <= 3, \
                 (dst.shape, src.shape)
@@ -521,12 +524,19 @@ class HipPointerGenerator:
             ss = [0] * (3 - src.dim()) + list(src.stride())
             ts = [0] * (3 - dst.dim()) + list(dst.stride())
             n = dst.numel()
-            rows.append([src.data_ptr(), dst.data_ptr(), *shape, *ss, *ts, off, int(dst.dtype == F32)])
-            off += n
-        if len(rows) > int(self.k.pack_max_jobs()):
+            if dst.is_contiguous() and src.is_contiguous() and src.data_ptr() % 32 == 0 and dst.data_ptr() % 16 == 0:
+                kind, nblk = 1, -(-n // 2048)
+            elif (dst.dim() == 2 and dst.is_contiguous() and src.stride() == (1, src.shape[0])):
+                R, C = dst.shape  # src = the transpose view of a contiguous [C][R] matrix
+                kind, nblk = 2, -(-R // 64) * -(-C // 64)
+            else:
+                kind, nblk = 0, -(-n // 256)
+            rows.append([src.data_ptr(), dst.data_ptr(), *shape, *ss, *ts, blk, kind, int(dst.dtype == F32), n, 0])
+            blk += nblk
+        if len(rows) > int(self.k.pack_max_jobs()) or len(rows[0]) != int(self.k.pack_job_cols()):
             return  # keep the torch path
         self._pack_jobs = torch.tensor(rows, dtype=torch.long, device=self.dev)
-        self._pack_total = off
+        self._pack_total = blk
 
     def _pack_torch(self):
         p, E, H, A = self.p, self.E, self.H, self.A
