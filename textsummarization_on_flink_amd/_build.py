@@ -97,17 +97,19 @@ def build_kernels(verbose=False, jobs=8, debug=False):
         if _newer([src] + hdrs, obj):
             jobsl.append([HIPCC, *common, "-c", src, "-o", obj])
     tflags, tld = _torch_flags()
-    bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(bdir, "bindings.o")
-    objs.append(bobj)
-    if _newer([bsrc] + hdrs, bobj):
-        jobsl.append([HIPCC, "-O2", "-std=c++17", "-fPIC", f"-I{kdir}", *tflags, "-c", bsrc, "-o", bobj])
+    for host in ("bindings.cpp", "blt_gemm.cpp"):  # torch op registrations (blt_gemm: hipBLASLt calls)
+        bsrc = os.path.join(CSRC, host)
+        bobj = os.path.join(bdir, host.replace(".cpp", ".o"))
+        objs.append(bobj)
+        if _newer([bsrc] + hdrs, bobj):
+            jobsl.append([HIPCC, "-O2", "-std=c++17", "-fPIC", f"-I{kdir}", *tflags, "-c", bsrc, "-o", bobj])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobsl))
     so = os.path.join(PKG_DIR, "_C_debug.so" if debug else "_C.so")
     if jobsl or not os.path.exists(so):
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + (["-fgpu-rdc"] if debug else [])
-        _run([*link, *objs, "-o", so, *tld], verbose)
+        # -lhipblaslt resolves to torch's own copy (its lib dir comes first in tld): one instance
+        _run([*link, *objs, "-o", so, *tld, "-lhipblaslt"], verbose)
     return so
 
 

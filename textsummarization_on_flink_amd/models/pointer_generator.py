@@ -13,7 +13,8 @@ Where the work goes:
     materialises the [N, V+O] final distribution;
   * every hoistable GEMM (input projections for all T, W_h features, p_gen / output
     projections for all D, vocab projection, all weight gradients) -> one big bf16 GEMM
-    each (hipBLASLt through torch.mm, fp32 accumulate/output);
+    each (hipBLASLt, the fastest candidate per shape: ``gemm`` / csrc/blt_gemm.cpp; fp32
+    accumulate/output);
   * clip + Adagrad -> fused kernel over the flat parameter buffer (``optim.hip``).
 
 Reference semantics: ``model.py:76-305``, ``attention_decoder.py:27-180``.
@@ -21,6 +22,7 @@ Reference semantics: ``model.py:76-305``, ``attention_decoder.py:27-180``.
 from __future__ import annotations
 
 
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -57,9 +59,38 @@ def enc_b(layer, d):
     return f"{enc_prefix(layer)}/bidirectional_rnn/{d}/lstm_cell/bias"
 
 
-def mm_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None):
-    """out = a . b (+ bias), fp32 accumulate, written straight into ``out`` (fp32 or bf16)
-    -- no temporary, no separate bias pass (hipBLASLt bias epilogue)."""
+# TSAMD_BLT=0: library GEMMs through torch.mm (hipBLASLt's first heuristic pick) instead of
+# blt_mm (csrc/blt_gemm.cpp: hipBLASLt called directly, the fastest of its candidates per shape)
+BLT = os.environ.get("TSAMD_BLT", "1") != "0"
+# the long-K weight gradients (encoder, vocab dW) through blt_mm too (default: split-K batched GEMM)
+BLT_WGRAD = BLT and os.environ.get("TSAMD_BLT_WGRAD", "0") == "1"
+BLT_VDW = BLT and os.environ.get("TSAMD_BLT_VOCAB_DW", "0") == "1"
+
+
+def _stored(x: torch.Tensor):
+    """(row-contiguous tensor holding x's elements, whether x is its transpose)."""
+    if x.stride(-1) == 1:
+        return x, False
+    if x.dim() == 2 and x.stride(0) == 1:
+        return x.t(), True
+    return x.contiguous(), False
+
+
+def gemm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float = 0.0,
+         bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = beta * out + a . b (+ bias[N]): bf16 operands, fp32 accumulate, fp32 or bf16 ``out``
+    written in place (row slices of bigger buffers included).  Transposed views of stored
+    operands are passed as (storage, transpose flag), never copied."""
+    if BLT and out.is_cuda and a.dtype == BF and b.dtype == BF:
+        sa, ta = _stored(a)
+        sb, tb = _stored(b)
+        _ops().blt_mm(sa, sb, out, ta, tb, float(beta), bias)
+        return out
+    if beta != 0.0:
+        assert bias is None
+        if out.dtype == F32 and a.dtype == BF:
+            return torch.addmm(out, a, b, out_dtype=F32, out=out)
+        return out.addmm_(a, b, beta=beta)
     if out.dtype == F32 and a.dtype == BF:
         if bias is None:
             return torch.mm(a, b, out_dtype=F32, out=out)
@@ -69,12 +100,21 @@ def mm_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, bias: Optional[
     return torch.addmm(bias.to(out.dtype), a, b, out=out)
 
 
+def mm_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None):
+    """out = a . b (+ bias), fp32 accumulate, written straight into ``out`` (fp32 or bf16)
+    -- no temporary, no separate bias pass (hipBLASLt bias epilogue)."""
+    return gemm(out, a, b, 0.0, bias)
+
+
 def wgrad_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
     """out[M,N] = a[K,M]^T . b[K,N] for weight gradients: K (= rows: tokens or decoder steps
-    x batch) is long and M x N is a handful of output tiles, which a plain GEMM runs on a
-    few CUs.  Split K into S chunks as one batched GEMM (S x the tiles, fp32 partials) and
-    sum the partials: 3-5x faster on MI355X for K = 25.6k-102k (tools/wgrad_micro.py)."""
+    x batch) is long and M x N is a handful of output tiles.  blt_mm picks among hipBLASLt's
+    stream-K / split-K solutions per shape.  The torch path (TSAMD_BLT=0) splits K into S
+    chunks as one batched GEMM (S x the tiles, fp32 partials) and sums the partials: 3-5x
+    faster than torch.mm's pick for K = 25.6k-102k (tools/wgrad_micro.py)."""
     K = a.shape[0]
+    if a.is_cuda and BLT_WGRAD and a.dtype == BF:
+        return gemm(out, a.t(), b)
     if a.is_cuda:
         for S in ((32, 16, 8) if K >= 65536 else (16, 8)):
             if K % S == 0 and K // S >= 256:
@@ -86,6 +126,8 @@ def wgrad_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
 
 def mmf(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """bf16 x bf16 -> fp32 GEMM (fp32 accumulate), hipBLASLt."""
+    if BLT and a.is_cuda:
+        return gemm(torch.empty(a.shape[0], b.shape[1], device=a.device, dtype=F32), a, b)
     return torch.mm(a, b, out_dtype=F32)
 
 
@@ -766,8 +808,8 @@ class HipPointerGenerator:
         ctxb = w["CTXb"].view(N, A)
         # out = [h, ctx] . W_o + b: bias-epilogue GEMM, second GEMM accumulating (beta = 1)
         out = w["out_f32"]
-        torch.addmm(p[OUT_B], Hn, self.pk["OUTm"][:H], out_dtype=F32, out=out)
-        torch.addmm(out, ctxb, self.pk["OUTm"][H:], out_dtype=F32, out=out)
+        gemm(out, Hn, self.pk["OUTm"][:H], 0.0, p[OUT_B])
+        gemm(out, ctxb, self.pk["OUTm"][H:], 1.0)
         w["outb"].copy_(out)
         pg = None
         if hps.pointer_gen:
@@ -794,7 +836,7 @@ class HipPointerGenerator:
                 if self.det:  # column sums of the bf16 dlogits in a fixed order
                     k.colsum(w["dlogits"], w["dbias"], N, V, False)
             return
-        torch.addmm(self.pk["ovb"], w["outb"], self.pk["ow"], out=w["logits"])
+        gemm(w["logits"], w["outb"], self.pk["ow"], 0.0, self.pk["ovb"])
         self.k.ptr_loss(w["logits"], None, w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None,
                         w["ext"], w["enc_lens"], w["loss_row"], w["dlogits"] if need_grad else None,
                         w["dpre"] if (need_grad and hps.pointer_gen) else None,
@@ -883,17 +925,17 @@ class HipPointerGenerator:
             # elements: the library's strided-batched path is not trusted past 32-bit strides
             while Sw > 1 and (N // Sw) * V >= 2 ** 31 and N % (2 * Sw) == 0:
                 Sw *= 2
-            if m == H and Sw > 1 and N % Sw == 0 and (N // Sw) * V < 2 ** 31:
+            if not BLT_VDW and m == H and Sw > 1 and N % Sw == 0 and (N // Sw) * V < 2 ** 31:
                 # split K = N in Sw = 4 (one batched GEMM + a sum): 0.82 -> 0.74 ms at B = 256
                 xe = w["outb_ext"].view(Sw, N // Sw, H + 8)[:, :, :H]
                 parts = torch.bmm(xe.transpose(1, 2), dl.view(Sw, N // Sw, V), out_dtype=F32)
                 torch.sum(parts, 0, out=dst)
             else:
-                torch.mm(w["outb_ext"][:, :m].t(), dl, out_dtype=F32, out=dst)
+                gemm(dst, w["outb_ext"][:, :m].t(), dl)
         dw()
         # dX = dlogits . W^T unsplit (split-K over vocab chunks measured slower at B = 256:
         # profiles/r2/ab/vocab_grad_split.jsonl)
-        self._dout = torch.mm(dl, self.pk["ow"].t(), out_dtype=F32)  # [N,H]
+        self._dout = mmf(dl, self.pk["ow"].t())  # [N,H]
 
     def _backward_head_compact(self, g, dl, H, V, N):
         """Vocab gradients over the live rows only: pass 2 wrote live block j's dlogits to rows
@@ -914,14 +956,14 @@ class HipPointerGenerator:
         dlc = dl[:M]
         g(OV).copy_(w["dbias"])
         dst = g(OW)
-        Sw = 4 if M % 4 == 0 and (M // 4) * V < 2 ** 31 else 1
+        Sw = 4 if not BLT_VDW and M % 4 == 0 and (M // 4) * V < 2 ** 31 else 1
         if Sw > 1:  # split K = M in 4 (one batched GEMM + a sum), as the full head
             parts = torch.bmm(xc.view(Sw, M // Sw, H + 8)[:, :, :H].transpose(1, 2), dlc.view(Sw, M // Sw, V),
                               out_dtype=F32)
             torch.sum(parts, 0, out=dst)
         else:
-            torch.mm(xc[:, :H].t(), dlc, out_dtype=F32, out=dst)
-        dxc = torch.mm(dlc, self.pk["ow"].t(), out_dtype=F32)  # [M, H]
+            gemm(dst, xc[:, :H].t(), dlc)
+        dxc = mmf(dlc, self.pk["ow"].t())  # [M, H]
         de = self._dout_ext
         de.zero_()
         de.index_copy_(0, idx, dxc.view(nbk, 32, H))  # padding entries land in the dummy block nb
@@ -980,7 +1022,7 @@ class HipPointerGenerator:
         if self.proj_attn:
             return self._backward_mid_proj(dCTX_dir, dH_dir, dC_dir, dX_dir, Hn, wg, run)
         if dX_dir is not None and D > 1:  # p_gen path into ctx_{t-1} through x_t (hoisted out of the loop)
-            dCTX_dir[:D - 1].view((D - 1) * B, A).addmm_(dX_dir[1:].view((D - 1) * B, E), p[LIN_M][E:].t())
+            gemm(dCTX_dir[:D - 1].view((D - 1) * B, A), dX_dir[1:].view((D - 1) * B, E), p[LIN_M][E:].t(), 1.0)
         # ---- decoder reverse loop
         enc_out, lens, F = self.enc[-1]["out"], w["enc_lens"], w["F"]
         v, wc = self.f32["v"], self.f32["wc"]
@@ -1079,7 +1121,7 @@ class HipPointerGenerator:
             dctx = w["DCTX"][:D - 1].view((D - 1) * B, A)
             dxb = w["DXb"][1:].view((D - 1) * B, E)
             dxb.copy_(w["DX"][1:].view((D - 1) * B, E))
-            torch.addmm(dctx, dxb, self.pk["WicT"], out_dtype=F32, out=dctx)
+            gemm(dctx, dxb, self.pk["WicT"], 1.0)
         self._backward_mid_rest(Hn, wg, run)
 
     def _backward_mid_rest(self, Hn, wg, run):
@@ -1096,7 +1138,7 @@ class HipPointerGenerator:
         emb_dec = self._emb_dec
 
         DXb = self._cast_colsum(w["DX"].view(N, E), g(LIN_B))
-        torch.mm(DXb, self.pk["lin_emb"].t(), out_dtype=F32, out=w["d_emb_dec"])  # [N,E] (embedding gradient)
+        gemm(w["d_emb_dec"], DXb, self.pk["lin_emb"].t())  # [N,E] (embedding gradient)
 
         def dec_wgrad():
             DZ = w["DZ"].view(N, 4 * H)
@@ -1132,7 +1174,7 @@ class HipPointerGenerator:
         w["DCTXb"].copy_(w["DCTX"])
         torch.bmm(w["ATTb"].permute(1, 2, 0), w["DCTXb"].permute(1, 0, 2), out_dtype=F32, out=dE)
         dE2 = dE.view(B * T, A)
-        torch.addmm(dE2, dFb, self.pk["Wh"].t(), out_dtype=F32, out=dE2)
+        gemm(dE2, dFb, self.pk["Wh"].t(), 1.0)
         self._dE = dE
 
     def backward_tail_enc(self):
@@ -1159,8 +1201,8 @@ class HipPointerGenerator:
         if self.det:  # bias gradients: relu'-masked row sums in a fixed order
             for pre, gsrc, dst in ((w["rs_pre"][0], w["dc_carry"], g(BRC)), (w["rs_pre"][1], w["dh_rec"], g(BRH))):
                 k.colsum(torch.where(pre > 0, gsrc, torch.zeros_like(gsrc)), dst, B, H, False)
-        torch.mm(w["rs_cat"][0].t(), w["rs_dp"][0], out_dtype=F32, out=g(RC))
-        torch.mm(w["rs_cat"][1].t(), w["rs_dp"][1], out_dtype=F32, out=g(RH))
+        gemm(g(RC), w["rs_cat"][0].t(), w["rs_dp"][0])
+        gemm(g(RH), w["rs_cat"][1].t(), w["rs_dp"][1])
         # ---- encoder BPTT, top layer down
         d_in = dE
         for layer in reversed(range(self.L)):
@@ -1191,7 +1233,7 @@ class HipPointerGenerator:
                     g(enc_b(layer, d)).copy_(w["lstm_db"][di])
                 else:
                     k.colsum(dzd, g(enc_b(layer, d)), T * B, 4 * H, False)
-                torch.mm(dzd, self.pk[f"enc{layer}_Kx{di}"].t(), out_dtype=F32, out=dxs[di])
+                gemm(dxs[di], dzd, self.pk[f"enc{layer}_Kx{di}"].t())
             dx = st["dx"]
             k.from_step_frame(dxs, w["rev_idx"], dx, B, T, din)  # fw + reversed bw, batch frame
             d_in = dx
