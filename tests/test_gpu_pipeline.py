@@ -97,3 +97,79 @@ def test_stream_fit_runs_at_engine_speed(tmp_path):
         w["step_ms"] * w["steps"] for w in win)
     assert sum(w["steps"] for w in win) >= 30
     assert stream_tps >= 0.7 * engine_tps, (stream_tps, engine_tps)
+
+
+def test_stream_transform_runs_at_engine_speed(tmp_path):
+    """Throughput of the streaming transform path (rows -> worker input ring -> stream packer
+    processes -> demand-formed decode batches -> DeviceBeamDecoder -> binary result records ->
+    sink) against the decoder alone on the same shape: hidden 256, enc 400, dec 100, beam 4,
+    vocab 5k, 16-article batches.  Summaries/s over the timed rows must reach 70% of the
+    decoder's (the full shape: tools/stream_throughput.py, profiles/r4/stream.md)."""
+    import os
+    import threading
+    import time
+
+    import torch
+
+    from textsummarization_on_flink_amd.api.io import CallbackSink, Source
+    from textsummarization_on_flink_amd.config import HParams
+    from textsummarization_on_flink_amd.data.synthetic import SyntheticCorpus, make_batches
+    from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
+    from textsummarization_on_flink_amd.models.params import build_params
+
+    V, NA, warm, timed = 5000, 16, 32, 320
+    c = SyntheticCorpus(vocab_size=V, seed=5)
+    c.vocab(V).save(f"{tmp_path}/vocab")
+    # the decoder alone
+    hps = HParams(mode="decode", batch_size=NA, beam_size=4, coverage=True, vocab_size=V)
+    params = build_params(hps, V, device="cuda", seed=1)
+    batches = make_batches(hps, c.vocab(V), c, 1 + timed // NA, pad_enc_to=hps.max_enc_steps)
+    dec = DeviceBeamDecoder(hps, c.vocab(V), params, n_articles=NA, T=hps.max_enc_steps, keep_attn=False)
+    dec.decode(batches[0])
+    torch.cuda.synchronize()
+    t0, n = time.perf_counter(), 0
+    for hyps in dec.decode_batches(batches[1:]):
+        n += len(hyps)
+    torch.cuda.synchronize()
+    engine_sps = n / (time.perf_counter() - t0)
+    del dec
+    torch.cuda.empty_cache()
+    # the streaming job, from a random-init checkpoint
+    train_dir = os.path.join(tmp_path, "log", "pretrained_model", "train")
+    os.makedirs(train_dir)
+    ckpt.Saver(train_dir).save(build_params(HParams(vocab_size=V, coverage=True), V, device="cpu", seed=1), 0)
+    rows = c.rows(warm + timed, "q")
+    warm_ids = {r["uuid"] for r in rows[:warm]}
+
+    class Gated(Source):
+        def __init__(self):
+            self.warm = threading.Event()
+            self.t_start = None
+
+        def field_names(self):
+            return list(FIELDS)
+
+        def __iter__(self):
+            for i, r in enumerate(rows):
+                if i == warm:
+                    self.warm.wait(600)
+                    self.t_start = time.time()
+                yield Row(r["uuid"], r["article"], "", r["reference"])
+
+    src, lock, got = Gated(), threading.Lock(), {"warm": 0, "timed": 0, "t_last": None}
+
+    def on_row(row):
+        with lock:
+            if row[0] in warm_ids:
+                got["warm"] += 1
+                if got["warm"] == warm:
+                    src.warm.set()
+            else:
+                got["timed"] += 1
+                got["t_last"] = time.time()
+
+    flags = [f"--vocab_size={V}", "--coverage=1", f"--decode_batch={NA}", "--stream_max_wait_ms=0"]
+    app.start_inference(None, src, [CallbackSink(on_row)], str(tmp_path), flags, echo=False)
+    assert got["timed"] == timed
+    stream_sps = timed / (got["t_last"] - src.t_start)
+    assert stream_sps >= 0.7 * engine_sps, (stream_sps, engine_sps)
