@@ -222,7 +222,9 @@ void blt_mm(const Tensor& a, const Tensor& b, const Tensor& out, bool ta, bool t
     BLT_CK(hipblasLtMatmulPreferenceCreate(&pref));
     uint64_t w64 = wsb;
     BLT_CK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &w64, sizeof(w64)));
-    const bool tune = !cap && env_int("TSAMD_BLT_TUNE", 1) != 0;
+    // deterministic mode: the library's first fitting pick, so a run's GEMMs do not depend on
+    // another run's timings (bit-reproducible across processes, not only within one)
+    const bool tune = !cap && env_int("TSAMD_BLT_TUNE", 1) != 0 && env_int("TSAMD_DETERMINISTIC", 0) == 0;
     const int want = tune ? std::max(1, env_int("TSAMD_BLT_CANDIDATES", 24)) : 8;
     std::vector<hipblasLtMatmulHeuristicResult_t> hr(want);
     int got = 0;
