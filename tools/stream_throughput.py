@@ -64,6 +64,36 @@ def run_fit(a, root, corpus):
     return rec
 
 
+def engine_decode(root, corpus, na, n_batches=12):
+    """The decoder alone (bench_decode.py's loop) with the checkpoint the streaming job served --
+    a random-init one, or the one the fit just trained, whose decode differs -- on synthetic
+    batches of the same shape: the fair denominator for the streaming transform."""
+    import torch
+    from textsummarization_on_flink_amd.config import HParams
+    from textsummarization_on_flink_amd.data.synthetic import make_batches
+    from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
+    from textsummarization_on_flink_amd.models.params import build_params
+    from textsummarization_on_flink_amd.train import checkpoint as ckpt
+    hps = HParams(mode="decode", batch_size=na, beam_size=4, coverage=True, vocab_size=50000)
+    params = build_params(hps, 50000, device="cuda")
+    ckpt.restore(ckpt.latest_checkpoint(os.path.join(root, "log", "pretrained_model", "train")), params,
+                 load_adagrad=False, strict=False)
+    vocab = corpus.vocab(50000)
+    batches = make_batches(hps, vocab, corpus, n_batches + 1, pad_enc_to=hps.max_enc_steps)
+    dec = DeviceBeamDecoder(hps, vocab, params, n_articles=na, T=hps.max_enc_steps, keep_attn=False)
+    dec.decode(batches[0])
+    torch.cuda.synchronize()
+    t0, n, steps = time.perf_counter(), 0, 0
+    for hyps in dec.decode_batches(batches[1:]):
+        n += len(hyps)
+        steps += dec.finished_steps
+    torch.cuda.synchronize()
+    sps = round(n / (time.perf_counter() - t0), 1)
+    del dec, params
+    torch.cuda.empty_cache()
+    return sps, round(steps / n_batches, 1)
+
+
 def run_transform(a, root, corpus):
     from textsummarization_on_flink_amd.api import app
     from textsummarization_on_flink_amd.api.io import CallbackSink, Source
@@ -106,7 +136,10 @@ def run_transform(a, root, corpus):
     app.start_inference(None, src, [CallbackSink(on_row)], root, extra, echo=False)
     wall = time.time() - t0
     el = got["t_last"] - src.t_start
+    eng_sps, eng_steps = engine_decode(root, corpus, a.decode_batch)
     rec = {"metric": "stream_transform_summaries_per_sec", "value": round(got["timed"] / el, 1),
+           "engine_same_ckpt_summaries_per_sec": eng_sps, "engine_decode_steps_per_batch": eng_steps,
+           "ratio_vs_engine": round(got["timed"] / el / eng_sps, 3),
            "unit": "summaries/s", "rows": a.transform_rows, "answered": got["timed"], "timed_s": round(el, 2),
            "decode_batch": a.decode_batch, "beam": 4, "wall_s": round(wall, 1), "packers": a.packers,
            "config": "H=256 E=128 V=50k enc400 dec100 beam4 coverage, synthetic rows, random init"}
