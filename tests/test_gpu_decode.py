@@ -251,12 +251,17 @@ def test_pgen_matches_fp32():
     assert (pg - ref).abs().max().item() < 1e-4
 
 
-@pytest.mark.parametrize("pointer,V,H", [(True, 3000, 128), (False, 3000, 128), (True, 600, 64), (False, 600, 64),
-                                         (False, 50000, 256), (True, 50000, 512), (False, 3000, 512)])
-def test_fused_vocab_topk_matches_materialised_path(pointer, V, H):
+@pytest.mark.parametrize("pointer,V,H,bias_kind", [
+    (True, 3000, 128, "rand"), (False, 3000, 128, "rand"), (True, 600, 64, "rand"), (False, 600, 64, "rand"),
+    (False, 50000, 256, "rand"), (True, 50000, 512, "rand"), (False, 3000, 512, "rand"),
+    (True, 50000, 256, "zipf"), (False, 50000, 256, "zipf"), (True, 3000, 128, "flat")])
+def test_fused_vocab_topk_matches_materialised_path(pointer, V, H, bias_kind):
     """vocab_topk (MFMA logits + per-tile (max, sum exp) partials, then a select that reads
     only the K best tiles of each row) == the library GEMM + final_topk path; V=600 has
-    fewer vocab tiles than K."""
+    fewer vocab tiles than K.  bias_kind "zipf": a trained model's frequency-shaped output
+    bias over a frequency-sorted vocabulary (the best tiles are full of entries above the
+    tile bound: the select's group-maxima bound prunes them); "flat": every logit equal
+    (ties broken by id)."""
     from textsummarization_on_flink_amd.ops import ops
     k = ops()
     torch.manual_seed(5)
@@ -265,6 +270,12 @@ def test_fused_vocab_topk_matches_materialised_path(pointer, V, H):
     X = (torch.randn(R, H, device="cuda")).bfloat16()
     W = (torch.randn(H, V, device="cuda") * 0.3).bfloat16()
     bias = torch.randn(V, device="cuda")
+    if bias_kind == "zipf":
+        W = (W.float() * 0.05).bfloat16()
+        bias = -1.5 * torch.log1p(torch.arange(V, device="cuda", dtype=torch.float32)) + 0.05 * bias
+    elif bias_kind == "flat":
+        W = torch.zeros_like(W)
+        bias = torch.full((V,), 0.25, device="cuda")
     lens = torch.randint(20, T + 1, (Na,), device="cuda", dtype=torch.int32)
     ext = torch.randint(0, V + 20, (Na, T), device="cuda", dtype=torch.int32)
     ext[:, :10] = ext[:, 10:20]
