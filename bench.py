@@ -198,6 +198,10 @@ def main(argv=None):
     peak_gb = torch.cuda.max_memory_allocated() / 2 ** 30
     eng_flags = {"persistent_lstm": bool(tr.engine.persistent_lstm), "proj_attn": bool(tr.engine.proj_attn),
                  "skip_pad_steps": bool(tr.engine.skip_pad), "decoder_row_groups": int(tr.engine.split)}
+    from textsummarization_on_flink_amd.models import pointer_generator as _pg
+    if _pg.BLT:  # library GEMMs through blt_mm: GEMM shapes seen / given a timed candidate search
+        st = tr.engine.k.blt_stats()
+        eng_flags["blt_mm"] = {"keys": int(st[0]), "tuned": int(st[1])}
     c5 = None
     if args.config5_steps > 0 and args.hidden != 512:
         del tr, batches
