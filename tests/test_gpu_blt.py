@@ -7,6 +7,7 @@ import torch
 
 from textsummarization_on_flink_amd.models.pointer_generator import gemm
 from textsummarization_on_flink_amd.ops import ops
+from textsummarization_on_flink_amd.utils.graphs import capture_guard
 
 pytestmark = pytest.mark.gpu
 
@@ -84,7 +85,7 @@ def test_blt_under_graph_capture_replays():
     torch.cuda.current_stream().wait_stream(s)
     gr = torch.cuda.CUDAGraph()
     c = (torch.randn(333, 200, device="cuda", generator=g) * 0.1).to(BF)
-    with torch.cuda.graph(gr):
+    with capture_guard(), torch.cuda.graph(gr):
         gemm(out, c, b, 1.0)
     out.zero_()
     gr.replay()
@@ -102,7 +103,7 @@ def test_blt_long_k_wgrad_captured_on_a_fresh_stream():
     b = (torch.randn(K, N, device="cuda", generator=g) * 0.1).to(BF)
     out = torch.zeros(M, N, device="cuda", dtype=F32)
     gr = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gr, stream=torch.cuda.Stream()):
+    with capture_guard(), torch.cuda.graph(gr, stream=torch.cuda.Stream()):
         gemm(out, a.t(), b)
     gr.replay()
     torch.cuda.synchronize()

@@ -264,13 +264,15 @@ def test_deferred_weight_gradients_match_inline(monkeypatch):
         torch.cuda.synchronize()
         eager = params.grad.clone()
         g = [torch.cuda.CUDAGraph() for _ in range(3)]
-        with torch.cuda.graph(g[0]):
-            eng.forward(need_grad=True)
-            eng.backward_head()
-        with torch.cuda.graph(g[1]):
-            eng.backward_mid()
-        with torch.cuda.graph(g[2]):
-            eng.backward_tail()
+        from textsummarization_on_flink_amd.utils.graphs import capture_guard
+        with capture_guard():
+            with torch.cuda.graph(g[0]):
+                eng.forward(need_grad=True)
+                eng.backward_head()
+            with torch.cuda.graph(g[1]):
+                eng.backward_mid()
+            with torch.cuda.graph(g[2]):
+                eng.backward_tail()
         for x in g:
             x.replay()
         torch.cuda.synchronize()

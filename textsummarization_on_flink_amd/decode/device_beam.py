@@ -32,6 +32,7 @@ from ..data.vocab import START_DECODING, STOP_DECODING, UNKNOWN_TOKEN
 from ..models.pointer_generator import (ATT_B, CELL_B, CELL_K, EMB, LIN_B, LIN_M, OUT_B, OV, PG_B, PG_M,
                                         HipPointerGenerator, mmf)
 from ..models.engine_config import EngineConfig
+from ..utils.graphs import capture_guard
 from .beam_search import Hypothesis
 
 BF = torch.bfloat16
@@ -317,7 +318,7 @@ class DeviceBeamDecoder:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with capture_guard(), torch.cuda.graph(self.graph):
             self._graph_steps()
         torch.cuda.synchronize()
         self._captured_now = True  # the warm-up consumed the encoded state: re-encode once

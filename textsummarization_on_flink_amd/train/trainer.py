@@ -26,6 +26,7 @@ from __future__ import annotations
 import logging
 import math
 import time
+import weakref
 from typing import Callable, Dict, Optional
 
 import torch
@@ -33,6 +34,7 @@ import torch
 from ..models.params import FlatParams, build_params
 from ..models.pointer_generator import HipPointerGenerator, LstmHandoffError  # noqa: F401
 from ..parallel.dist import DistInfo, GradAllReducer, broadcast_params
+from ..utils.graphs import capture_guard
 
 log = logging.getLogger(__name__)
 
@@ -136,7 +138,7 @@ class GraphTrainer:
         bucket (HipPointerGenerator.compact_vocab: one head graph per block count)."""
 
         def __init__(self, trainer):
-            self.t = trainer
+            self.t = weakref.proxy(trainer)  # no trainer <-> phase cycle: trainers free by refcount
 
         def replay(self):
             self.t.g_fwd.replay()
@@ -167,30 +169,31 @@ class GraphTrainer:
         self.params.accum.copy_(snap[1])
         self.engine.pack()
         torch.cuda.synchronize()
-        pool = torch.cuda.graph_pool_handle()
-        # four graphs (forward + vocab backward | decoder backward | encoder backward |
-        # embedding gradient) so each gradient bucket's all-reduce overlaps the next phase
-        self.g_fb = [self._Phase0(self)] + [torch.cuda.CUDAGraph() for _ in range(3)]
-        self.g_fwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fwd, pool=pool):
-            self.out = self.engine.forward(need_grad=True)
-        nbk = eng.nbk
-        self.g_head = {}
-        for b in buckets:
-            eng.nbk = b
-            self.g_head[b] = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_head[b], pool=pool):
-                eng.backward_head()
-        eng.nbk = nbk
-        with torch.cuda.graph(self.g_fb[1], pool=pool):
-            self.engine.backward_mid()
-        with torch.cuda.graph(self.g_fb[2], pool=pool):
-            eng.backward_tail_enc()
-        with torch.cuda.graph(self.g_fb[3], pool=pool):
-            eng.backward_tail_emb()
-        self.g_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_opt, pool=pool):
-            self._opt()
+        with capture_guard():  # no cyclic GC (and its HIP-calling destructors) inside the captures
+            pool = torch.cuda.graph_pool_handle()
+            # four graphs (forward + vocab backward | decoder backward | encoder backward |
+            # embedding gradient) so each gradient bucket's all-reduce overlaps the next phase
+            self.g_fb = [self._Phase0(self)] + [torch.cuda.CUDAGraph() for _ in range(3)]
+            self.g_fwd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_fwd, pool=pool):
+                self.out = self.engine.forward(need_grad=True)
+            nbk = eng.nbk
+            self.g_head = {}
+            for b in buckets:
+                eng.nbk = b
+                self.g_head[b] = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g_head[b], pool=pool):
+                    eng.backward_head()
+            eng.nbk = nbk
+            with torch.cuda.graph(self.g_fb[1], pool=pool):
+                self.engine.backward_mid()
+            with torch.cuda.graph(self.g_fb[2], pool=pool):
+                eng.backward_tail_enc()
+            with torch.cuda.graph(self.g_fb[3], pool=pool):
+                eng.backward_tail_emb()
+            self.g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_opt, pool=pool):
+                self._opt()
         torch.cuda.synchronize()
 
     # ------------------------------------------------------------------ step

@@ -56,11 +56,13 @@ def main():
             fn()
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
-    for _, fn in phases:
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=pool):
-            fn()
-        graphs.append(g)
+    from textsummarization_on_flink_amd.utils.graphs import capture_guard
+    with capture_guard():
+        for _, fn in phases:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                fn()
+            graphs.append(g)
     torch.cuda.synchronize()
     res = {"batch": a.batch, "hidden": a.hidden, "enc": a.enc, "layers": a.layers}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
