@@ -149,6 +149,7 @@ struct L2Args {
   const int* dlen = nullptr; int step = 0;  // training: skip tiles of rows past their last live step
 };
 
+template <int KB>
 __device__ __forceinline__ void linear2_body(const L2Args& p, int B, int n0, int r0, float* red) {
   if (tile_dead(p.dlen, p.step, r0, B)) return;  // (nothing reads a dead row's s)
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -162,7 +163,7 @@ __device__ __forceinline__ void linear2_body(const L2Args& p, int B, int n0, int
   const int nst = K / 32;
   const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
   f32x4 acc[1] = {f32x4{0, 0, 0, 0}};
-  kslice_mma<1>([&](int k) { return k < K1 ? ld8(r1 + k) : ld8(r2 + k); },
+  kslice_mma<1, KB>([&](int k) { return k < K1 ? ld8(r1 + k) : ld8(r2 + k); },
                 [&](int, int k) { return ld8(brow + k); }, k0, k1, acc);
   float o[1];
   ksplit_reduce<1>(acc, red, o);
@@ -179,22 +180,24 @@ __device__ __forceinline__ void linear2_body(const L2Args& p, int B, int n0, int
   if (p.outb) p.outb[ix] = f2bf(v);
 }
 
+template <int KB>
 __global__ __launch_bounds__(256) void linear2_kernel(L2Args p, int B) {
   __shared__ float red[4 * 256];
   int tx, ty;
   xcd_tile(tx, ty);
-  linear2_body(p, B, tx * 16, ty * 16, red);
+  linear2_body<KB>(p, B, tx * 16, ty * 16, red);
 }
 
 // Two independent linear2 problems on the same rows in one launch (blockIdx.z picks the
 // problem; column tiles past a problem's N exit): the beam-decode step pairs the attention
 // query projection with the x-merge of the previous context, saving a kernel boundary.
+template <int KB>
 __global__ __launch_bounds__(256) void linear2_pair_kernel(L2Args p0, L2Args p1, int B) {
   __shared__ float red[4 * 256];
   const L2Args& p = blockIdx.z ? p1 : p0;
   const int n0 = blockIdx.x * 16;
   if (n0 >= p.N) return;  // uniform per block, before any barrier
-  linear2_body(p, B, n0, blockIdx.y * 16, red);
+  linear2_body<KB>(p, B, n0, blockIdx.y * 16, red);
 }
 
 // p_gen = sigmoid([ctx, c, h, x] . w + b), one wave per row (reference attention_decoder.py:164-168).
@@ -420,6 +423,23 @@ void launch_dec_cell_fwd_beam(const int* gidx, const int* latest, const float* X
                      hb_out, nullptr, B, H, A, BeamGather{gidx, latest, XGtab, V, unk, step}, nullptr, 0);
 }
 // the beam-decode pair: s = [cb, hb] . WsT^T + bs, and x = Xtab[token] + ctx_parent . WicT^T
+// k-steps per load batch of linear2: a wave's whole K / 4 slice in one batch (one L2 round trip)
+// when it is at most 8 k-steps (the output projection's K = H + A = 768 at hidden 256: 6; the
+// query projection's K = 2H = 1024 at hidden 512: 8), else batches of 4
+static int l2_kb(int K) {
+  static const bool off = getenv("TSAMD_L2_KB") && atoi(getenv("TSAMD_L2_KB")) == 0;  // A/B: batches of 4
+  if (off) return 4;
+  const int ks = (K / 32 + 3) / 4;
+  return ks <= 4 ? 4 : ks <= 6 ? 6 : ks <= 8 ? 8 : 4;
+}
+#define L2_LAUNCH(KERN, K, GRID, ST, ...)                                                          \
+  do {                                                                                           \
+    const int kb_ = l2_kb(K);                                                                    \
+    if (kb_ == 6) hipLaunchKernelGGL(KERN<6>, GRID, dim3(256), 0, ST, __VA_ARGS__);              \
+    else if (kb_ == 8) hipLaunchKernelGGL(KERN<8>, GRID, dim3(256), 0, ST, __VA_ARGS__);         \
+    else hipLaunchKernelGGL(KERN<4>, GRID, dim3(256), 0, ST, __VA_ARGS__);                       \
+  } while (0)
+
 void launch_beam_sproj_xmerge(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out,
                               const bf16* ctx_src, const bf16* WicT, const float* Xtab, const int* gidx,
                               const int* latest, float* x_out, int B, int H, int A, int E, int V, int unk,
@@ -431,13 +451,13 @@ void launch_beam_sproj_xmerge(const bf16* cb, const bf16* hb, const bf16* WsT, c
   p1.gtok = latest;
   p1.V = V;
   p1.unk = unk;
-  hipLaunchKernelGGL(linear2_pair_kernel, grid, dim3(256), 0, st, p0, p1, B);
+  L2_LAUNCH(linear2_pair_kernel, H + H > A ? H + H : A, grid, st, p0, p1, B);
 }
 void launch_linear2(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
                     const float* add, float* out, bf16* outb, int B, int N, hipStream_t st) {
   dim3 grid(N / 16, (B + 15) / 16);
   const L2Args p{a1, K1, a2, K2, Wt, bias, add, out, outb, N};
-  hipLaunchKernelGGL(linear2_kernel, grid, dim3(256), 0, st, p, B);
+  L2_LAUNCH(linear2_kernel, K1 + K2, grid, st, p, B);
 }
 void launch_linear2_pair(const bf16* a1, int K1, const bf16* a2, int K2, const bf16* Wt, const float* bias,
                          const float* add, float* out, bf16* outb, int N, const bf16* c1, int L1, const bf16* c2,
@@ -446,7 +466,7 @@ void launch_linear2_pair(const bf16* a1, int K1, const bf16* a2, int K2, const b
   dim3 grid((N > M ? N : M) / 16, (B + 15) / 16, 2);
   const L2Args p0{a1, K1, a2, K2, Wt, bias, add, out, outb, N};
   const L2Args p1{c1, L1, c2, L2, Vt, vbias, vadd, vout, voutb, M};
-  hipLaunchKernelGGL(linear2_pair_kernel, grid, dim3(256), 0, st, p0, p1, B);
+  L2_LAUNCH(linear2_pair_kernel, K1 + K2 > L1 + L2 ? K1 + K2 : L1 + L2, grid, st, p0, p1, B);
 }
 void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const float* bs, float* s_out, int B, int H,
                       int A, const int* dlen, int step, hipStream_t st) {
@@ -454,7 +474,7 @@ void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const flo
   L2Args p{cb, H, hb, H, WsT, bs, nullptr, s_out, nullptr, A};
   p.dlen = dlen;
   p.step = step;
-  hipLaunchKernelGGL(linear2_kernel, grid, dim3(256), 0, st, p, B);
+  L2_LAUNCH(linear2_kernel, H + H, grid, st, p, B);
 }
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
                      int N, int A, int H, int E, bool det, hipStream_t st) {
