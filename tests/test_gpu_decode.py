@@ -184,7 +184,8 @@ def test_pipelined_decode_batches_equal_batch_by_batch(overlap):
 
 
 @pytest.mark.parametrize("B,K1,K2,N,use_add", [(20, 256, 512, 256, False), (37, 512, 0, 128, True),
-                                               (64, 256, 256, 512, False)])
+                                               (64, 256, 256, 512, False), (33, 512, 512, 256, True),
+                                               (16, 1024, 1024, 128, False)])
 def test_linear2_matches_fp32(B, K1, K2, N, use_add):
     from textsummarization_on_flink_amd.ops import ops
     k = ops()
