@@ -68,6 +68,7 @@ struct State {
   std::map<Key, Pick> picks;
   std::map<hipStream_t, void*> ws;
   std::vector<void*> spare;  // allocated eagerly, handed to streams first seen inside a capture
+  bool spares_made = false;
   int64_t tuned = 0, calls = 0;
 };
 
@@ -178,7 +179,8 @@ void blt_mm(const Tensor& a, const Tensor& b, const Tensor& out, bool ta, bool t
   std::lock_guard<std::mutex> g(S.mu);
   if (!S.handle) BLT_CK(hipblasLtCreate(&S.handle));
   const bool cap = capturing(s);
-  if (!cap && S.spare.empty() && S.ws.empty()) {
+  if (!cap && !S.spares_made) {
+    S.spares_made = true;
     // spare workspaces for the capture streams (torch.cuda.graph captures on a stream of its
     // own): no allocation can happen inside a capture, and a solution that needs a workspace
     // must never get a null one
