@@ -291,6 +291,14 @@ void emb_grad_det(const Tensor& gemb, const Tensor& sid, const Tensor& perm, con
 
 // ---------------------------------------------------------------- frames (frames.hip)
 // out[2][T][B][W] from src rows: (ids? ids[b,tt] : b*T+tt), tt = t | rev[b,t]; columns d*doff..
+void step_frame_hop(const Tensor& in, const Tensor& rev, const Tensor& out, int64_t B, int64_t T, int64_t H) {
+  chk(in, F32, "in"); chk(out, F32, "out");
+  TORCH_CHECK(H % 4 == 0 && B > 0 && T > 0, "step_frame_hop: H % 4 == 0");
+  TORCH_CHECK(rev.scalar_type() == at::kLong && rev.is_contiguous() && rev.numel() == B * T, "rev [B,T] int64");
+  numel_eq(in, 2 * T * B * 2 * H, "in"); numel_eq(out, 2 * T * B * H, "out");
+  launch_step_frame_hop(P<float>(in), rev.data_ptr<int64_t>(), P<float>(out), (int)B, (int)T, (int)H, stream());
+}
+
 void to_step_frame(const Tensor& src, const OT& ids, const Tensor& rev, const Tensor& out, int64_t B, int64_t T,
                    int64_t W, int64_t doff) {
   TORCH_CHECK(src.is_cuda() && src.is_contiguous() && out.is_contiguous() && src.scalar_type() == out.scalar_type(),
@@ -973,6 +981,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("linear2_pair", &linear2_pair);
   m.def("cast_colsum", &cast_colsum);
   m.def("colsum", &colsum);
+  m.def("step_frame_hop", &step_frame_hop);
   m.def("ptr_rowfin", &ptr_rowfin);
   m.def("clip_adagrad", &clip_adagrad);
   m.def("opt_parts", &opt_parts);

@@ -48,6 +48,32 @@ __global__ __launch_bounds__(256) void from_step_frame_kernel(const float* __res
   }
 }
 
+// Between two stacked encoder layers in the BPTT: the upper layer's input gradients (step frame,
+// in[dir][t][b][2H]) straight into the lower layer's output-gradient step frame out[d][t][b][H] --
+// from_step_frame then to_step_frame (doff = H) in one pass, without the batch-frame dx between
+// them (2 x T x B x 2H fp32 of traffic less per layer boundary; the same two fp32 operands added):
+//   out[0][t][b] = in[0][t][b][0:H]    + in[1][rev(b,t)][b][0:H]
+//   out[1][t][b] = in[0][rev(b,t)][b][H:2H] + in[1][t][b][H:2H]        (rev is an involution)
+__global__ __launch_bounds__(256) void step_frame_hop_kernel(const float* __restrict__ in, const int64_t* __restrict__ rev,
+                                                             float* __restrict__ out, int B, int T, int H) {
+  const int cpr = H / 4;
+  const long n = 2L * T * B * cpr;
+  const size_t plane = (size_t)T * B * 2 * H;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % cpr);
+    const long row = i / cpr;  // (d, t, b)
+    const int b = (int)(row % B);
+    const int t = (int)((row / B) % T);
+    const int d = (int)(row / ((long)B * T));
+    const int rt = (int)DCHECK_IDX(rev[(size_t)b * T + t], 0, T, CHK_FRAME_REV);
+    const int t0 = d == 0 ? t : rt, t1 = d == 0 ? rt : t;
+    const size_t col = (size_t)d * H + 4 * c;
+    const float4 x = *reinterpret_cast<const float4*>(in + ((size_t)t0 * B + b) * 2 * H + col);
+    const float4 y = *reinterpret_cast<const float4*>(in + plane + ((size_t)t1 * B + b) * 2 * H + col);
+    *reinterpret_cast<float4*>(out + (size_t)row * H + 4 * c) = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+  }
+}
+
 // bf16 [B][T][A] -> [B][A][T] through a 64 x 64 LDS tile (8-byte loads and stores)
 __global__ __launch_bounds__(256) void transpose_bta_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int T,
                                                             int A) {
@@ -98,6 +124,11 @@ void launch_to_step_frame(const void* src, int es, const int64_t* ids, const int
 void launch_from_step_frame(const float* in, const int64_t* rev, float* out, int B, int T, int W, hipStream_t st) {
   const long n = (long)B * T * (W / 4);
   hipLaunchKernelGGL(from_step_frame_kernel, dim3(grid_for(n)), dim3(256), 0, st, in, rev, out, B, T, W);
+}
+
+void launch_step_frame_hop(const float* in, const int64_t* rev, float* out, int B, int T, int H, hipStream_t st) {
+  const long n = 2L * T * B * (H / 4);
+  hipLaunchKernelGGL(step_frame_hop_kernel, dim3(grid_for(n)), dim3(256), 0, st, in, rev, out, B, T, H);
 }
 
 void launch_transpose_bta(const bf16* in, bf16* out, int B, int T, int A, hipStream_t st) {

@@ -111,3 +111,23 @@ def test_wgrad_tn_matches_fp32(K, M, N, strided):
     assert err < 1e-4, err
     if strided:  # nothing written outside the slice
         assert float(big[:, :pad].abs().max()) == 0 and float(big[:, pad + N:].abs().max()) == 0
+
+
+@pytest.mark.parametrize("B,T,H", [(5, 7, 16), (16, 33, 64)])
+def test_step_frame_hop_equals_from_then_to_step_frame(B, T, H):
+    """step_frame_hop (upper layer's step-frame input gradients straight into the lower layer's
+    output-gradient step frame) == from_step_frame followed by to_step_frame (doff = H), bit for bit."""
+    k = ops()
+    g = torch.Generator().manual_seed(B * T + H)
+    lens = torch.randint(1, T + 1, (B,), generator=g)
+    lens[0] = T
+    rev = _rev(lens, T).cuda()
+    dxs = torch.randn(2, T * B, 2 * H, generator=g).cuda()
+    dx = torch.empty(B, T, 2 * H, device="cuda")
+    k.from_step_frame(dxs, rev, dx, B, T, 2 * H)
+    ref = torch.empty(B, T, 2 * H, device="cuda")  # [2][T][B][H] in the engine's dout buffer
+    k.to_step_frame(dx, None, rev, ref, B, T, H, H)
+    out = torch.full((B, T, 2 * H), float("nan"), device="cuda")
+    k.step_frame_hop(dxs, rev, out, B, T, H)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

@@ -357,7 +357,9 @@ class HipPointerGenerator:
                 "dh_fin": z(2, B, H),
                 "dc_carry": z(2, B, H),
                 "dxs": z(2, T * B, din),
-                "dx": z(B, T, din),
+                # batch-frame input gradient: the embedding gradient's source (layer 0 only; above it
+                # step_frame_hop feeds the layer below directly)
+                "dx": z(B, T, din) if layer == 0 else None,
             })
         # persistent weight-resident recurrence (lstm_persistent.hip) when the shape allows
         # it; cfg.persistent_lstm = False forces the per-step kernels
@@ -1208,8 +1210,10 @@ class HipPointerGenerator:
         for layer in reversed(range(self.L)):
             st = self.enc[layer]
             din = st["din"]
-            # dL/dh_out in step frame: fw as is, bw reversed within each length
-            k.to_step_frame(d_in, None, w["rev_idx"], st["dout"], B, T, H, H)
+            # dL/dh_out in step frame: fw as is, bw reversed within each length (below the top layer
+            # the previous iteration's step_frame_hop wrote it straight from the upper layer's dxs)
+            if layer == self.L - 1:
+                k.to_step_frame(d_in, None, w["rev_idx"], st["dout"], B, T, H, H)
             if layer != self.L - 1:  # the top layer's seeds came from rs_bwd
                 st["dh_fin"].zero_()
                 st["dc_carry"].zero_()
@@ -1234,6 +1238,9 @@ class HipPointerGenerator:
                 else:
                     k.colsum(dzd, g(enc_b(layer, d)), T * B, 4 * H, False)
                 gemm(dxs[di], dzd, self.pk[f"enc{layer}_Kx{di}"].t())
+            if layer > 0:  # the layer below's output-gradient step frame, without the batch-frame dx
+                k.step_frame_hop(dxs, w["rev_idx"], self.enc[layer - 1]["dout"], B, T, H)
+                continue
             dx = st["dx"]
             k.from_step_frame(dxs, w["rev_idx"], dx, B, T, din)  # fw + reversed bw, batch frame
             d_in = dx
