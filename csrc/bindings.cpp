@@ -194,8 +194,7 @@ void attn_fwd_rowp(const Tensor& F, const Tensor& G, const Tensor& s, const Tens
 void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                    const Tensor& a, const OT& dx, const Tensor& gv, const OT& Ga, const OT& dcov_next, const OT& gcl,
                    const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out, int64_t B, int64_t T,
-                   int64_t A, const OT& dlen, int64_t step, const OT& dzn, const OT& Kx, const OT& dxdir,
-                   const OT& dx_out, int64_t G4) {
+                   int64_t A, const OT& dlen, int64_t step) {
   chk(G, BF, "G"); chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(gv, F32, "gv");
   chk(lens, I32, "lens"); chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
   const int64_t EG = gv.numel() / std::max<int64_t>(B, 1);
@@ -207,16 +206,9 @@ void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tens
   chko(dx, F32, B * EG, "dx"); chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(Ga, F32, B * T, "Ga");
   chko(dcov_next, F32, B * T, "dcov_next"); chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
   chko(dlen, I32, B, "dlen");
-  // dzn: dx = dz_{t+1} . Kx^T (+ dxdir) computed in the kernel (stored to dx_out) instead of read from dx
-  const bool fused = PO<bf16>(dzn) != nullptr;
-  TORCH_CHECK(!fused || (G4 % 512 == 0 && G4 <= 2048 && !PO<float>(dx) && PO<bf16>(Kx) && PO<float>(dx_out)),
-              "attn_bwd_rowp: dzn needs Kx and dx_out, no dx, 4H a multiple of 512 up to 2048");
-  chko(dzn, BF, B * G4, "dzn"); chko(Kx, BF, EG * G4, "Kx"); chko(dxdir, F32, B * EG, "dxdir");
-  chko(dx_out, F32, B * EG, "dx_out");
   launch_attn_bwd_rowp(P<bf16>(G), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
                        PO<float>(dx), P<float>(gv), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl), P<int>(lens),
-                       P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, PO<int>(dlen), (int)step, stream(),
-                       PO<bf16>(dzn), PO<bf16>(Kx), PO<float>(dxdir), PO<float>(dx_out), (int)G4);
+                       P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, PO<int>(dlen), (int)step, stream());
 }
 
 void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
@@ -424,8 +416,7 @@ void dec_sproj(const Tensor& cb, const Tensor& hb, const Tensor& WsT, const Tens
 
 void dec_bwd_cell(const Tensor& ds, const Tensor& Ws, const OT& dC_dir, const OT& dH_dir, const Tensor& dh_rec,
                   const Tensor& dc_carry, const Tensor& act, const Tensor& c_now, const Tensor& c_prev,
-                  const Tensor& dz, int64_t B, int64_t H, int64_t A, const OT& dlen, int64_t step, const OT& dzn,
-                  const OT& Kh) {
+                  const Tensor& dz, int64_t B, int64_t H, int64_t A, const OT& dlen, int64_t step) {
   chk(ds, F32, "ds"); chk(Ws, BF, "Ws"); chk(dh_rec, F32, "dh_rec"); chk(dc_carry, F32, "dc_carry");
   chk(act, F32, "act"); chk(c_now, F32, "c_now"); chk(c_prev, F32, "c_prev"); chk(dz, BF, "dz");
   TORCH_CHECK(H % 16 == 0 && A % 32 == 0, "bad dims");
@@ -433,12 +424,9 @@ void dec_bwd_cell(const Tensor& ds, const Tensor& Ws, const OT& dC_dir, const OT
   chko(dH_dir, F32, B * H, "dH_dir"); numel_eq(dh_rec, B * H, "dh_rec"); numel_eq(dc_carry, B * H, "dc_carry");
   numel_eq(act, B * 4 * H, "act"); numel_eq(c_now, B * H, "c_now"); numel_eq(c_prev, B * H, "c_prev");
   numel_eq(dz, B * 4 * H, "dz"); chko(dlen, I32, B, "dlen");
-  // dzn: dh_rec = dz_{t+1} . Kh^T computed in the kernel (Kh: W_cell[E:] as [H][4H]) instead of read
-  chko(dzn, BF, B * 4 * H, "dzn"); chko(Kh, BF, H * 4 * H, "Kh");
-  TORCH_CHECK(!PO<bf16>(dzn) || PO<bf16>(Kh), "dec_bwd_cell: dzn needs Kh");
   launch_dec_bwd_cell(P<float>(ds), P<bf16>(Ws), PO<float>(dC_dir), PO<float>(dH_dir), P<float>(dh_rec),
                       P<float>(dc_carry), P<float>(act), P<float>(c_now), P<float>(c_prev), P<bf16>(dz), B, H, A,
-                      PO<int>(dlen), (int)step, stream(), PO<bf16>(dzn), PO<bf16>(Kh));
+                      PO<int>(dlen), (int)step, stream());
 }
 
 void dec_bwd_dz(const Tensor& dz, const Tensor& Wbig, const OT& dX_dir, const OT& dCTX_dir_prev, const Tensor& dx_out,
@@ -781,35 +769,6 @@ void attn_fwd_row_beam(const Tensor& F, const Tensor& E, const Tensor& s, const 
 }
 
 
-// beam-decode attention over one article's encoder rows for all its rep hypotheses (attention_beam.hip):
-// coverage as is (cov) or gathered from the parents (cov_src + a_src at gidx, kept in cov_keep)
-bool attn_beam_ok(int64_t A, int64_t T, int64_t rep) { return attn_beam_supported((int)A, (int)T, (int)rep); }
-int64_t attn_beam_chunks_op(int64_t Na, int64_t T) { return attn_beam_chunks((int)Na, (int)T); }
-void attn_beam(const Tensor& F, const Tensor& E, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
-               const OT& cov_src, const OT& a_src, const OT& cov_keep, const OT& gidx, const Tensor& lens,
-               const Tensor& e_buf, const Tensor& pm, const Tensor& pctx, const Tensor& a_out, const Tensor& ctx,
-               const OT& ctx_bf, int64_t R, int64_t T, int64_t A, int64_t rep, int64_t S) {
-  chk(F, BF, "F"); chk(E, BF, "E"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens");
-  chk(e_buf, F32, "e_buf"); chk(pm, F32, "pm"); chk(pctx, F32, "pctx"); chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
-  TORCH_CHECK(attn_beam_supported((int)A, (int)T, (int)rep) && R % rep == 0, "attn_beam: A = 512, rep = 4, T <= 4096");
-  TORCH_CHECK(attn_beam_chunk_ok((int)T, (int)S), "attn_beam: 1 <= S <= 64 chunks of <= 512 positions");
-  const int64_t Na = R / rep;
-  numel_eq(F, Na * T * A, "F"); numel_eq(E, Na * T * A, "E"); numel_eq(s, R * A, "s"); numel_eq(v, A, "v");
-  numel_eq(lens, Na, "lens"); numel_eq(e_buf, R * T, "e_buf"); numel_eq(pm, R * S * 2, "pm");
-  numel_eq(pctx, R * S * A, "pctx"); numel_eq(a_out, R * T, "a_out"); numel_eq(ctx, R * A, "ctx");
-  chko(wc, F32, A, "wc"); chko(cov, F32, R * T, "cov"); chko(cov_src, F32, R * T, "cov_src");
-  chko(a_src, F32, R * T, "a_src"); chko(cov_keep, F32, R * T, "cov_keep"); chko(gidx, I32, R, "gidx");
-  chko(ctx_bf, BF, R * A, "ctx_bf");
-  const bool gather = PO<int>(gidx) != nullptr;
-  TORCH_CHECK(gather == (PO<float>(cov_src) != nullptr) && gather == (PO<float>(a_src) != nullptr) &&
-              gather == (PO<float>(cov_keep) != nullptr), "coverage gather: gidx, cov_src, a_src, cov_keep together");
-  TORCH_CHECK(!(gather && PO<float>(cov)), "cov (as is) and the coverage gather are exclusive");
-  launch_attn_beam(P<bf16>(F), P<bf16>(E), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), PO<float>(cov_src),
-                   PO<float>(a_src), PO<float>(cov_keep), PO<int>(gidx), P<int>(lens), P<float>(e_buf), P<float>(pm),
-                   P<float>(pctx), P<float>(a_out), P<float>(ctx), PO<bf16>(ctx_bf), (int)R, (int)T, (int)A, (int)rep,
-                   (int)S, stream());
-}
-
 // Advances step[0] by one (the last block to finish) when ctr (one zeroed uint32 scratch word)
 // is given; without ctr, beam_gather advanced it at the start of the decode step (t = step - 1).
 // att/att_hist/pg/pg_hist (optional): this step's attention rows and p_gen copied into row
@@ -997,8 +956,5 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("dec_cell_fwd_beam", &dec_cell_fwd_beam);
   m.def("beam_sproj_xmerge", &beam_sproj_xmerge);
   m.def("attn_fwd_row_beam", &attn_fwd_row_beam);
-  m.def("attn_beam_ok", &attn_beam_ok);
-  m.def("attn_beam_chunks", &attn_beam_chunks_op);
-  m.def("attn_beam", &attn_beam);
   m.def("pgen_bwd", &pgen_bwd);
 }

@@ -543,14 +543,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
 }
 
 // backward: da_i = r_i + dx . G_i (r_i already holds the output-projection / p_gen part of
-// dctx . E_i), S = sum_j a_j r_j + dx . g_t; the rest as attn_bwd_row.  dx == nullptr and
-// dzn == nullptr: last step.
-// dzn set (the decoder backward in two launches per step): dx = dx_{t+1} is computed here,
-//   dx = dz_{t+1} . W_cell[:E]^T + dX_dir_{t+1}   (Kx: W_cell[:E] as [E][4H], K = G4 = 4H),
-// and stored to dx_out for the weight gradients after the loop -- the work of the retired
-// dec_bwd_dz launch's first E columns.  Wave w takes outputs w, w + NW, ...; each lane holds
-// G4 / 64 elements of the dz row and the output is a wave reduction.  Kx (256 KB at H = 256)
-// streams from L2; the first position group's F / G rows are already in flight.
+// dctx . E_i), S = sum_j a_j r_j + dx . g_t; the rest as attn_bwd_row.  dx == nullptr:
+// last step.
 template <int NK, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     const bf16* __restrict__ G, const bf16* __restrict__ F, const float* __restrict__ s,
@@ -558,13 +552,11 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     const float* __restrict__ a, const float* __restrict__ dx, const float* __restrict__ gv,
     const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
     const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
-    float* __restrict__ dcov_out, int T, const int* __restrict__ dlen, int step, const bf16* __restrict__ dzn,
-    const bf16* __restrict__ Kx, const float* __restrict__ dxdir, float* __restrict__ dx_out, int G4) {
+    float* __restrict__ dcov_out, int T, const int* __restrict__ dlen, int step) {
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float part[NW][A];
   __shared__ float red[NW];
   __shared__ f32x2 prm[3 * NK * 4 * 64];
-  __shared__ float dxs[kEG];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
@@ -576,8 +568,6 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
       if (dcov_out) dcov_out[rb + i] = 0.f;
     }
     for (int k = tid; k < A; k += NT) ds[(size_t)b * A + k] = 0.f;
-    if (dzn)  // dz_{t+1} and dX_dir_{t+1} of a dead row are zero too
-      for (int k = tid; k < kEG; k += NT) dx_out[(size_t)b * kEG + k] = 0.f;
     return;
   }
   const float g = gcl ? gcl[b] : 0.f;
@@ -621,42 +611,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     }
   }
   auto par = [&](int which, int kb, int jp) -> f32x2 { return prm[((which * NK + kb) * 4 + jp) * 64 + lane]; };
-  if (dzn) {  // dx_{t+1} = dz_{t+1} . W_cell[:E]^T + dX_dir_{t+1} -> LDS (and dx_out)
-    const bf16* zr = dzn + (size_t)b * G4;
-    bf16x8 zf[4];  // G4 <= 2048: the lane's 8-element chunks lane*8 + 512 j
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (512 * j < G4) zf[j] = ld8(zr + 512 * j + lane * 8);
-    for (int e0 = wid; e0 < kEG; e0 += 2 * NW) {  // two outputs per pass: both rows' loads in flight
-      const int e1 = e0 + NW;
-      float d0 = 0.f, d1 = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (512 * j >= G4) continue;
-        const bf16x8 w0 = ld8(Kx + (size_t)e0 * G4 + 512 * j + lane * 8);
-        const bf16x8 w1 = ld8(Kx + (size_t)min(e1, kEG - 1) * G4 + 512 * j + lane * 8);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          d0 = fmaf(bf2f(zf[j][q]), bf2f(w0[q]), d0);
-          d1 = fmaf(bf2f(zf[j][q]), bf2f(w1[q]), d1);
-        }
-      }
-      d0 = sum_x32(sum_x16(dpp_sum16(d0)));
-      d1 = sum_x32(sum_x16(dpp_sum16(d1)));
-      if (lane == 0) {
-        const float x0 = d0 + (dxdir ? dxdir[(size_t)b * kEG + e0] : 0.f);
-        dxs[e0] = x0;
-        dx_out[(size_t)b * kEG + e0] = x0;
-        if (e1 < kEG) {
-          const float x1 = d1 + (dxdir ? dxdir[(size_t)b * kEG + e1] : 0.f);
-          dxs[e1] = x1;
-          dx_out[(size_t)b * kEG + e1] = x1;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  const float* dxp = dzn ? dxs : (dx ? dx + (size_t)b * kEG : nullptr);
+  const float* dxp = dx ? dx + (size_t)b * kEG : nullptr;
   // the lane's 8 features of dx (position-independent)
   f32x2 dx2[4];
 #pragma unroll
@@ -777,12 +732,10 @@ void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const fl
 void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st,
-                          const bf16* dzn, const bf16* Kx, const float* dxdir, float* dx_out, int G4) {
+                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st) {
 #define LB(NK)                                                                                            \
   hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, rowp_bwd_waves<NK>()>), dim3(B), dim3(rowp_bwd_waves<NK>() * 64), \
-                     0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, dlen, step, \
-                     dzn, Kx, dxdir, dx_out, G4)
+                     0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, dlen, step)
   if (A == 512) LB(1);
   else LB(2);
 #undef LB

@@ -279,19 +279,14 @@ __global__ __launch_bounds__(256) void pgen_dirs_kernel(const float* __restrict_
 //   cell backward -> dz_t (bf16), dc_carry <- dc_total * f
 // ds (fp32 [B][A]) was accumulated by attn_bwd_step's blocks with atomics, or stored by
 // attn_bwd_row.
-// dzn set (the decoder backward in two launches per step): dh_rec = dz_{t+1} . W_cell[E:]^T is
-// computed here instead of read (Kh: W_cell[E:] as [H][4H]) -- the same 16 x 16 tiles, K split
-// over the 4 waves and LDS reduce as the retired dec_bwd_dz launch's dh_rec columns, so the
-// values are bit-identical to it.
 __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
     const float* __restrict__ ds,
     const bf16* __restrict__ Ws,                                               // Ws: [2H][A] (TF Matrix)
     const float* __restrict__ dC_dir, const float* __restrict__ dH_dir,       // [B][H] (nullable)
     const float* __restrict__ dh_rec, float* __restrict__ dc_carry,            // [B][H]
     const float* __restrict__ act, const float* __restrict__ c_now, const float* __restrict__ c_prev,
-    bf16* __restrict__ dz, int B, int H, int A, const int* __restrict__ dlen, int step,
-    const bf16* __restrict__ dzn, const bf16* __restrict__ Kh) {
-  __shared__ float red[4 * 3 * 256];
+    bf16* __restrict__ dz, int B, int H, int A, const int* __restrict__ dlen, int step) {
+  __shared__ float red[4 * 2 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int tx, ty;
   xcd_tile(tx, ty);
@@ -308,7 +303,7 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
   const size_t ri = (size_t)(rok ? r : 0) * H + u;
   float dh0, dc0, a4[4], cn, cpv;
   {
-    dh0 = (dzn ? 0.f : dh_rec[ri]) + (dH_dir ? dH_dir[ri] : 0.f);
+    dh0 = dh_rec[ri] + (dH_dir ? dH_dir[ri] : 0.f);
     dc0 = dc_carry[ri] + (dC_dir ? dC_dir[ri] : 0.f);
     const float* ap = act + (size_t)(rok ? r : 0) * 4 * H;
 #pragma unroll
@@ -326,24 +321,10 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
   f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
   kslice_mma<2>([&](int k) { return ld8f(arow + k); },
                 [&](int j, int k) { return ld8((j == 0 ? bc : bh) + k); }, k0, k1, acc);
-  float o[3] = {0.f, 0.f, 0.f};  // ds . W_s[0:H]^T, ds . W_s[H:2H]^T, dh_rec
-  if (dzn) {  // block-uniform
-    const int G = 4 * H, gst = G / 32;
-    const int g0 = (wid * gst / 4) * 32, g1 = ((wid + 1) * gst / 4) * 32;
-    const bf16* zrow = dzn + (size_t)ar * G + kof;
-    const bf16* krow = Kh + (size_t)(u0 + (lane & 15)) * G + kof;
-    f32x4 accz[1] = {f32x4{0, 0, 0, 0}};
-    kslice_mma<1, 4>([&](int k) { return ld8(zrow + k); }, [&](int, int k) { return ld8(krow + k); }, g0, g1, accz);
-    const f32x4 acc3[3] = {acc[0], acc[1], accz[0]};
-    ksplit_reduce<3>(acc3, red, o);
-  } else {
-    float o2[2];
-    ksplit_reduce<2>(acc, red, o2);
-    o[0] = o2[0];
-    o[1] = o2[1];
-  }
+  float o[2];  // ds . W_s[0:H]^T, ds . W_s[H:2H]^T
+  ksplit_reduce<2>(acc, red, o);
   if (!rok) return;
-  const float dh = dh0 + o[2] + o[1];
+  const float dh = dh0 + o[1];
   float dc = dc0 + o[0];
   const float ig = a4[0], jg = a4[1], fg = a4[2], og = a4[3];
   const float tc = ftanh(cn);
@@ -496,10 +477,10 @@ void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x
 void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,
                          const float* c_prev, bf16* dz, int B, int H, int A, const int* dlen, int step,
-                         hipStream_t st, const bf16* dzn, const bf16* Kh) {
+                         hipStream_t st) {
   dim3 grid(H / 16, (B + 15) / 16);
   hipLaunchKernelGGL(dec_bwd_cell_kernel, grid, dim3(256), 0, st, ds, Ws, dC_dir, dH_dir, dh_rec, dc_carry, act,
-                     c_now, c_prev, dz, B, H, A, dlen, step, dzn, Kh);
+                     c_now, c_prev, dz, B, H, A, dlen, step);
 }
 void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, const float* dCTX_dir_prev,
                        float* dx_out, float* dctx_prev_out, float* dh_rec, int B, int E, int H, int A,

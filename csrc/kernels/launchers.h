@@ -34,24 +34,13 @@ void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const flo
                          float* dcov_out, int B, int T, int A, hipStream_t st);
 
 bool attn_rowp_supported(int A, int T, int EG);
-// beam decode: one article's F / E read once for its rep = 4 hypotheses, positions split in S
-// chunks + a merge launch (attention_beam.hip)
-bool attn_beam_supported(int A, int T, int rep);
-int attn_beam_chunks(int Na, int T);
-bool attn_beam_chunk_ok(int T, int S);
-void launch_attn_beam(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc, const float* cov,
-                      const float* cov_src, const float* a_src, float* cov_keep, const int* cg, const int* lens,
-                      float* e_buf, float* pm, float* pctx, float* a_out, float* ctx, bf16* ctx_bf, int R, int T,
-                      int A, int rep, int S, hipStream_t st);
 void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const float* v, const float* wc,
                           const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* gx,
                           bf16* gx_bf, int B, int T, int A, const int* dlen, int step, hipStream_t st);
 void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st,
-                          const bf16* dzn = nullptr, const bf16* Kx = nullptr, const float* dxdir = nullptr,
-                          float* dx_out = nullptr, int G4 = 0);
+                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st);
 
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, const int* dlen,
@@ -68,8 +57,7 @@ void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const flo
 void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, const float* dH_dir,
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,
                          const float* c_prev, bf16* dz, int B, int H, int A, const int* dlen, int step,
-                         hipStream_t st,
-                         const bf16* dzn = nullptr, const bf16* Kh = nullptr);
+                         hipStream_t st);
 void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, const float* dCTX_dir_prev,
                        float* dx_out, float* dctx_prev_out, float* dh_rec, int B, int E, int H, int A,
                        const int* dlen, int step, hipStream_t st);

@@ -221,29 +221,6 @@ def test_row_split_streams_match_single_chain(monkeypatch, split):
     assert _rel(got[1][2], got[0][2]) < 1e-4
 
 
-@pytest.mark.parametrize("B,H", [(256, 256), (128, 512)])
-def test_decoder_backward_two_launches_matches_three(monkeypatch, B, H):
-    """TSAMD_DEC_BWD_2L: the projected-context decoder backward with dx_{t+1} computed in the
-    attention backward's prologue and dh_rec inside dec_bwd_cell (2 launches per step) gives the
-    gradients of the 3-launch loop (dec_bwd_dz after every step)."""
-    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
-    hps = _hps(B, trunc_norm_init_std=0.05).replace(max_dec_steps=24, hidden_dim=H)
-    vocab, (batch,) = _batches(hps, 1, seed=16)
-    got = []
-    for two in ("0", "1"):
-        monkeypatch.setenv("TSAMD_DEC_BWD_2L", two)
-        params = build_params(hps, vocab.size(), device="cuda", seed=7).enable_grad()
-        eng = HipPointerGenerator(hps, vocab.size(), params, B=B, T=T, D=24)
-        assert eng.proj_attn and eng.dec_bwd_2l == (two == "1")
-        eng.set_batch(batch)
-        out = eng.forward(need_grad=True)
-        eng.backward()
-        torch.cuda.synchronize()
-        got.append((float(out["total_loss"]), params.grad.clone()))
-    assert got[0][0] == got[1][0]
-    assert _rel(got[1][1], got[0][1]) < 1e-4, _rel(got[1][1], got[0][1])
-
-
 def test_deferred_weight_gradients_match_inline(monkeypatch):
     """The decoder-side weight gradients deferred onto a side stream beside the encoder BPTT
     (TSAMD_DEFER_WGRAD, default on) give

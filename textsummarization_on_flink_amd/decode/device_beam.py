@@ -64,11 +64,6 @@ class DeviceBeamDecoder:
         # it, else the multi-block kernels over the transposed features (EngineConfig.decode_row_attn)
         self.k = self.eng.k
         self.row_attn = self.eng.cfg.decode_row_attn and bool(self.k.attn_row_ok(self.eng.A, T))
-        # the article-level kernel (attention_beam.hip): each article's F / E read once for all its
-        # beam hypotheses, the positions split over S workgroups + a merge launch
-        self.beam_attn = self.row_attn and self.eng.cfg.decode_beam_attn and self.rep == self.beam and \
-            bool(self.k.attn_beam_ok(self.eng.A, T, self.rep))
-        self.S = int(self.k.attn_beam_chunks(self.Na, T)) if self.beam_attn else 0
         self.eng.keep_ft = not self.row_attn  # the multi-block score kernel reads transposed features
         self.dev = self.eng.dev
         # decode_batches: run batch n + 1's encoder on a side stream beside batch n's decode
@@ -126,10 +121,6 @@ class DeviceBeamDecoder:
         if self.keep_attn:
             b["ATT_hist"] = z(D, R, T)
             b["PG_hist"] = z(D, R)
-        if self.beam_attn:
-            b["e_buf"] = z(R, T)
-            b["pm"] = z(R, self.S, 2)
-            b["pctx"] = z(R, self.S, A)
         self.b = b
 
     def refresh_weights(self):
@@ -205,10 +196,6 @@ class DeviceBeamDecoder:
         was already accumulated into ``cov`` by beam_gather)."""
         k, b, eng = self.k, self.b, self.eng
         R, T, A = self.R, self.T, eng.A
-        if self.beam_attn:
-            k.attn_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], cov, None, None, None, None, b["lens_att"],
-                        b["e_buf"], b["pm"], b["pctx"], att_out, ctx_out, ctx_bf, R, T, A, self.rep, self.S)
-            return
         if self.row_attn:
             k.attn_fwd_row(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], cov, b["lens_att"], att_out, None,
                            None, ctx_out, ctx_bf, R, T, A, self.rep)
@@ -279,15 +266,9 @@ class DeviceBeamDecoder:
                                 self.Xtab, b["gidx"], b["latest"], b["x"], R, H, A, E, V, unk)
         else:
             k.dec_sproj(b["Cb2"], Y["H"], eng.pk["WsT"], p[ATT_B], b["s"], R, H, A, None, 0)
-        if self.beam_attn:
-            k.attn_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], None, X["COV"] if cov else None,
-                        X["ATT"] if cov else None, Y["COV"] if cov else None, b["gidx"] if cov else None,
-                        b["lens_att"], b["e_buf"], b["pm"], b["pctx"], Y["ATT"], Y["CTX"], Y["CTXb"], R, T, A,
-                        self.rep, self.S)
-        else:
-            k.attn_fwd_row_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], X["COV"] if cov else None,
-                                X["ATT"] if cov else None, Y["COV"] if cov else None, b["gidx"], b["lens_att"],
-                                Y["ATT"], Y["CTX"], Y["CTXb"], R, T, A, self.rep)
+        k.attn_fwd_row_beam(b["F"], b["E"], b["s"], eng.f32["v"], eng.f32["wc"], X["COV"] if cov else None,
+                            X["ATT"] if cov else None, Y["COV"] if cov else None, b["gidx"], b["lens_att"],
+                            Y["ATT"], Y["CTX"], Y["CTXb"], R, T, A, self.rep)
         k.linear2(Y["H"], H, Y["CTXb"], A, eng.pk["OUTmT"], p[OUT_B], None, None, b["outb"], R, H)
         ptr, hist = hps.pointer_gen, self.keep_attn
         k.vocab_topk_beam(b["outb"], self.owT, p[OV], Y["CTX"] if ptr else None, Y["C"] if ptr else None,

@@ -16,9 +16,7 @@ engine is built); code can also pass a config explicitly.
 | TSAMD_PROJ_ATTN           | proj_attn          | 1: training row attention streams G = enc_out . W_in[E:] (emb_dim wide) instead of enc_out; 0: enc_out |
 | TSAMD_SKIP_PAD_STEPS      | skip_pad_steps     | 1: the projected-context attention kernels skip (row, step) pairs past the row's last loss-weighted decoder step; 0: compute them |
 | TSAMD_DEC_ROW_ATTN        | decode_row_attn    | 1: beam-decode attention through the row kernel; 0: score + softmax kernels |
-| TSAMD_DEC_BEAM_ATTN       | decode_beam_attn   | 0 (measured slower, profiles/r4/ab/decode_attn_beam.txt); 1: beam-decode attention reads each article's F / E once for its 4 hypotheses (attention_beam.hip, A = 512); 0: per-hypothesis row kernel |
 | TSAMD_COMPACT_VOCAB_GRAD  | compact_vocab_grad | 1: with skip_pad_steps, the vocab-head dlogits of the live 32-row blocks are written compacted and the two gradient GEMMs run over those rows only (bucketed block counts); 0: every row |
-| TSAMD_DEC_BWD_2L          | dec_bwd_two_launch | 0 (measured slower, profiles/r4/ab/dec_bwd_two_launch.md); 1: with proj_attn, the decoder backward runs 2 launches per step and row group (dx_{t+1} in the attention backward's prologue, dh_rec inside dec_bwd_cell; no dec_bwd_dz); 0: 3 launches |
 | TSAMD_DEFER_WGRAD         | defer_wgrad        | 1: decoder-side weight gradients beside the encoder BPTT (B >= 256); 0: inline |
 | TSAMD_DETERMINISTIC       | deterministic      | 0; 1: fixed-order reductions instead of fp32 atomics (bit-reproducible steps) |
 | TSAMD_KERNEL_DEBUG        | (ops loader)       | 0; 1: the bounds-checked kernel library ``_C_debug.so`` |
@@ -51,9 +49,7 @@ class EngineConfig:
     proj_attn: bool = True
     skip_pad_steps: bool = True
     decode_row_attn: bool = True
-    decode_beam_attn: bool = False
     compact_vocab_grad: bool = True
-    dec_bwd_two_launch: bool = False
     defer_wgrad: bool = True
     deterministic: bool = False
 
@@ -70,9 +66,7 @@ class EngineConfig:
             proj_attn=_flag(env, "TSAMD_PROJ_ATTN", True),
             skip_pad_steps=_flag(env, "TSAMD_SKIP_PAD_STEPS", True),
             decode_row_attn=_flag(env, "TSAMD_DEC_ROW_ATTN", True),
-            decode_beam_attn=_flag(env, "TSAMD_DEC_BEAM_ATTN", False),
             compact_vocab_grad=_flag(env, "TSAMD_COMPACT_VOCAB_GRAD", True),
-            dec_bwd_two_launch=_flag(env, "TSAMD_DEC_BWD_2L", False),
             defer_wgrad=_flag(env, "TSAMD_DEFER_WGRAD", True),
             deterministic=_flag(env, "TSAMD_DETERMINISTIC", False),
         )

@@ -418,7 +418,6 @@ class HipPointerGenerator:
         # (row, step) pairs past the row's last loss-weighted step are skipped by the projected
         # kernels (their outputs are written as zeros; loss and gradients are unchanged)
         self.skip_pad = self.proj_attn and cfg.skip_pad_steps
-        self.dec_bwd_2l = self.proj_attn and cfg.dec_bwd_two_launch and 4 * H % 512 == 0 and 4 * H <= 2048
         self.compact_vocab = self.skip_pad and cfg.fused_vocab_train and cfg.compact_vocab_grad and not cfg.deterministic \
             and H in (128, 256, 512) and (D * B) % 32 == 0
         w["F"] = z(B, T, A, dt=BF)
@@ -1052,7 +1051,7 @@ class HipPointerGenerator:
                                     dcov[t % 2][rs] if cov else None, Bg, T, A)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
-                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, None, 0, None, None)
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, None, 0)
                 k.dec_bwd_dz(w["DZ"][t][rs], self.pk["Wbig"], dX_dir[t][rs] if dX_dir is not None else None,
                              dCTX_dir[t - 1][rs] if t > 0 else None, w["DX"][t][rs],
                              w["DCTX"][t - 1][rs] if t > 0 else None, w["dh_rec"][rs], Bg, E, H, A, None, 0)
@@ -1085,12 +1084,9 @@ class HipPointerGenerator:
         dcov = w["dcov"]
         Kc = self.pk["Wbig"][:E + H]  # W_cell: [dx | dh] = dz . W_cell^T
         dlen = w["dlen"] if self.skip_pad else None
-        # two launches per step (cfg.dec_bwd_two_launch): dx_{t+1} = dz_{t+1} . W_cell[:E]^T (+ dX_dir) in
-        # the attention backward's prologue, dh_rec = dz_{t+1} . W_cell[E:]^T inside dec_bwd_cell; dx_0 and
-        # the final dh_rec after the loop.  Otherwise dec_bwd_dz produces both from dz_t at the end of
-        # every step.
-        two = self.dec_bwd_2l
-        Kx, Kh = Kc[:E], Kc[E:]  # views of W_cell^T rows: dx and dh_rec columns
+        # dec_bwd_dz produces dx_t and dh_rec = dz_t . W_cell[E:]^T at the end of every step (the
+        # 2-launch variant with dx in the attention backward's prologue measured slower:
+        # profiles/r4/ab/dec_bwd_two_launch.md)
 
         def chain(r0, r1):
             Bg, rs = r1 - r0, slice(r0, r1)
@@ -1098,26 +1094,17 @@ class HipPointerGenerator:
             for t in reversed(range(D)):
                 nxt = t < D - 1
                 k.attn_bwd_rowp(G[rs], F[rs], w["S"][t][rs], v, wc, w["COV"][t][rs] if (cov and t > 0) else None,
-                                w["ATT"][t][rs], w["DX"][t + 1][rs] if (nxt and not two) else None, w["GV"][t][rs],
+                                w["ATT"][t][rs], w["DX"][t + 1][rs] if nxt else None, w["GV"][t][rs],
                                 Ga[t][rs], dcov[(t + 1) % 2][rs] if (cov and nxt) else None,
                                 w["gcl"][t][rs] if cov else None, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
-                                dcov[t % 2][rs] if cov else None, Bg, T, A, dl, t,
-                                w["DZ"][t + 1][rs] if (nxt and two) else None, Kx if two else None,
-                                dX_dir[t + 1][rs] if (nxt and two and dX_dir is not None) else None,
-                                w["DX"][t + 1][rs] if (nxt and two) else None, 4 * H)
+                                dcov[t % 2][rs] if cov else None, Bg, T, A, dl, t)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
-                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, dl, t,
-                               w["DZ"][t + 1][rs] if (nxt and two) else None, Kh if two else None)
-                if not two:
-                    k.dec_bwd_dz(w["DZ"][t][rs], Kc, dX_dir[t][rs] if dX_dir is not None else None, None,
-                                 w["DX"][t][rs], None, w["dh_rec"][rs], Bg, E, H, 0, dl, t)
+                               w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, dl, t)
+                k.dec_bwd_dz(w["DZ"][t][rs], Kc, dX_dir[t][rs] if dX_dir is not None else None, None,
+                             w["DX"][t][rs], None, w["dh_rec"][rs], Bg, E, H, 0, dl, t)
 
         self._row_groups(chain, self.split_bwd)
-        if two:  # dx_0 and dh_rec = dz_0 . W_cell[E:]^T (the decoder's initial-state gradient, read by
-            # rs_bwd) over all rows in one launch; the loop produced dx_1 .. dx_{D-1}
-            k.dec_bwd_dz(w["DZ"][0], Kc, dX_dir[0] if dX_dir is not None else None, None, w["DX"][0], None,
-                         w["dh_rec"], B, E, H, 0, dlen, 0)
         w["DCTX"].copy_(dCTX_dir)
         if D > 1:
             dctx = w["DCTX"][:D - 1].view((D - 1) * B, A)

@@ -55,7 +55,7 @@ def main():
                    "dec_bwd_dz_us": timed(lambda: k.dec_bwd_dz(dz, Wbig, None, None, dx, dctx, dh, B, E, H, A, None, 0))}
             try:
                 res["dec_bwd_cell_us"] = timed(lambda: k.dec_bwd_cell(ds, Ws, None, dh, dh, dcc, act, c_out, cprev, dz,
-                                                                      B, H, A, None, 0, None, None))
+                                                                      B, H, A, None, 0))
             except RuntimeError as e:  # noqa: BLE001
                 res["dec_bwd_cell_us"] = str(e)[:80]
             print(json.dumps(res), flush=True)
