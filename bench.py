@@ -31,9 +31,11 @@ included, tokenisation excluded); the value is the sum over ranks of completed s
 divided by the slowest rank's wall time.  ``--decode-batches 0`` skips it.
 
 Secondary (BASELINE config #5, ``config5_tokens_per_sec`` / ``config5_beam4_summaries_per_sec``):
-hidden 512, 2-layer encoder, enc 800, per-GPU batch 1024, ``--config5-steps`` timed steps after
-two warm-up steps (graph capture + one replay of the other batch), the same timed region as the
-headline; then 4 beam-4 decode batches at that size.  ``--config5-steps 0`` skips it.
+hidden 512, 2-layer encoder, enc 800, per-GPU batch sized for the GPU's HBM (the largest of
+2048 / 1024 / 512 whose captured step fits EVERY rank, agreed before any gradient collective;
+``config5_peak_mem_gb`` reports the footprint), ``--config5-steps`` timed steps after two warm-up
+steps (graph capture + one replay of the other batch), the same timed region as the headline;
+then 4 beam-4 decode batches at that size.  ``--config5-steps 0`` skips it.
 """
 import argparse
 import json
@@ -87,11 +89,13 @@ def _free_port() -> int:
 def launch_ranks(n: int, argv, port: int = 0) -> int:
     """Start ``n`` rank processes of this script (one per GPU) and wait for them.  Runs
     before anything initialises the GPU in this process (torch is not even imported)."""
+    from textsummarization_on_flink_amd.parallel.rccl_env import rccl_env  # torch-free
     port = port or _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        rccl_env(env)  # RCCL's CU cap before the rank touches the GPU (parallel/rccl_env.py)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
     rc = 0
     try:
@@ -206,11 +210,9 @@ def main(argv=None):
     if args.config5_steps > 0 and args.hidden != 512:
         del tr, batches
         torch.cuda.empty_cache()
-        try:
-            c5 = bench_config5(args, info, D, torch, dev_id)
-        except torch.cuda.OutOfMemoryError as e:  # the headline line must still be printed
-            c5 = {"config5_error": str(e).splitlines()[0][:200]}
-            torch.cuda.empty_cache()
+        # no rank-local OOM handling here: bench_config5 agrees on a batch that fits every rank
+        # before any collective (a rank that skipped alone would leave its peers in an all-reduce)
+        c5 = bench_config5(args, info, D, torch, dev_id)
 
     if info.is_chief:
         rec = {
@@ -262,58 +264,111 @@ def main(argv=None):
 AUTO_BATCHES = (2048, 1024, 512, 256, 128)
 
 
+def _oom_type():
+    import torch
+    return torch.cuda.OutOfMemoryError
+
+
+def agree_largest(cands, trial, info, D, device):
+    """Rank-agreed capacity search: ``trial(c)`` runs rank-locally (no collectives inside) for
+    each candidate, largest first; a ``torch.cuda.OutOfMemoryError`` (and only that: any other
+    error is real) marks it as not fitting on this rank.  The ranks all-reduce MIN of their
+    success flags after each trial, so every rank returns the same ``(c, trial result)`` -- or
+    ``(None, None)`` when no candidate fits everywhere -- before any gradient collective runs.
+    A rank never skips or falls back on its own."""
+    oom = _oom_type()
+    for c in cands:
+        res, ok = None, 1.0
+        try:
+            res = trial(c)
+        except oom as e:
+            print(f"capacity search: {c} does not fit ({str(e).splitlines()[0][:120]})", file=sys.stderr)
+            ok = 0.0
+        _empty_cache()
+        if D.all_reduce_scalar(ok, info, op="min", device=device) > 0:
+            return c, res
+        res = None
+        _empty_cache()
+    return None, None
+
+
+def _empty_cache():
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+
+
 def pick_batch(args, hps, vocab, corpus, info, D, torch, dev_id) -> int:
     """``--batch auto``: the largest per-GPU batch whose captured training step fits EVERY
-    rank's memory.  Each candidate is tried rank-locally (a trainer without collectives, one
-    captured step) and kept only if it fit on all ranks (all-reduce MIN of the success flag),
-    so the ranks agree before any gradient collective runs."""
+    rank's memory (``agree_largest``: a trainer without collectives, one captured step per
+    candidate); the smallest candidate if none does."""
     from textsummarization_on_flink_amd.data.synthetic import make_batches
     from textsummarization_on_flink_amd.parallel.dist import DistInfo
     from textsummarization_on_flink_amd.train.trainer import GraphTrainer
-    for B in AUTO_BATCHES:
+
+    def trial(B):
         h = hps.replace(batch_size=B)
-        ok = 1.0
-        try:
-            b = make_batches(h, vocab, corpus, 1, pad_enc_to=args.enc)[0]
-            tr = GraphTrainer(h, vocab.size(), B=B, T=args.enc, device=f"cuda:{dev_id}", info=DistInfo(),
-                              use_graph=not args.no_graph)
-            tr.step(b)  # graph capture included: the peak allocation happens here
-            torch.cuda.synchronize()
-            del tr
-        except torch.cuda.OutOfMemoryError as e:  # only "does not fit": any other error is real
-            print(f"--batch auto: batch {B} does not fit ({str(e).splitlines()[0][:120]})", file=sys.stderr)
-            ok = 0.0
-        torch.cuda.empty_cache()
-        if D.all_reduce_scalar(ok, info, op="min", device=f"cuda:{dev_id}") > 0 or B == AUTO_BATCHES[-1]:
-            return B
-    return AUTO_BATCHES[-1]
+        b = make_batches(h, vocab, corpus, 1, pad_enc_to=args.enc)[0]
+        tr = GraphTrainer(h, vocab.size(), B=B, T=args.enc, device=f"cuda:{dev_id}", info=DistInfo(),
+                          use_graph=not args.no_graph)
+        tr.step(b)  # graph capture included: the peak allocation happens here
+        torch.cuda.synchronize()
+        return None
+
+    B, _ = agree_largest(AUTO_BATCHES, trial, info, D, f"cuda:{dev_id}")
+    return B if B is not None else AUTO_BATCHES[-1]
 
 
-CONFIG5 = dict(hidden=512, layers=2, enc=800, batch=1024)  # BASELINE.json config #5 (run_summarization.py:62-66)
+CONFIG5 = dict(hidden=512, layers=2, enc=800)  # BASELINE.json config #5 (run_summarization.py:62-66)
+CONFIG5_BATCHES = (2048, 1024, 512)            # "batch sized for 288 GB HBM": the largest that fits
 
 
 def bench_config5(args, info, D, torch, dev_id):
     """BASELINE config #5 on the same clock as the headline: hidden 512, 2-layer bi-LSTM encoder,
-    enc 800 -> dec 100, per-GPU batch 1024 (weak scaling), same timed region as the headline
-    (H2D, three graph replays, all-reduce, optimizer graph); then 2 batches of 64-article beam-4
-    decode at that size."""
+    enc 800 -> dec 100, the largest per-GPU batch of CONFIG5_BATCHES whose captured step fits every
+    rank (weak scaling), same timed region as the headline (H2D, phase-graph replays, all-reduce,
+    optimizer graph); then 4 batches of 64-article beam-4 decode at that size.
+
+    The batch is found by ``agree_largest`` before any collective: each rank captures a trainer
+    without collectives at the candidate size (its two warm-up steps); on one rank that trainer is
+    the timed one, on several ranks the data-parallel trainer is built at the agreed size."""
     import argparse as _ap
     from textsummarization_on_flink_amd.config import HParams
     from textsummarization_on_flink_amd.data.synthetic import SyntheticCorpus, make_batches
+    from textsummarization_on_flink_amd.parallel.dist import DistInfo
     from textsummarization_on_flink_amd.train.trainer import GraphTrainer
     c = CONFIG5
-    hps = HParams(batch_size=c["batch"], max_enc_steps=c["enc"], max_dec_steps=args.dec, vocab_size=args.vocab,
-                  hidden_dim=c["hidden"], emb_dim=args.emb, coverage=not args.no_coverage, pointer_gen=True,
-                  enc_layers=c["layers"], grad_compress=args.grad_compress)
+    hps = HParams(batch_size=CONFIG5_BATCHES[0], max_enc_steps=c["enc"], max_dec_steps=args.dec,
+                  vocab_size=args.vocab, hidden_dim=c["hidden"], emb_dim=args.emb, coverage=not args.no_coverage,
+                  pointer_gen=True, enc_layers=c["layers"], grad_compress=args.grad_compress)
     corpus = SyntheticCorpus(vocab_size=args.vocab, seed=2000 + info.rank)
     vocab = corpus.vocab(args.vocab)
-    batches = make_batches(hps, vocab, corpus, 2, pad_enc_to=c["enc"])
-    tr = GraphTrainer(hps, vocab.size(), B=c["batch"], T=c["enc"], device=f"cuda:{dev_id}", info=info,
-                      use_graph=not args.no_graph)
+    dev = f"cuda:{dev_id}"
+    torch.cuda.reset_peak_memory_stats(dev_id)
+
+    def warm(tr, batches):
+        out = None
+        for b in batches:  # warm-up: graph capture, then a replay of each batch (each live-row bucket's head graph)
+            out = tr.step(b)
+        tr.check_finite(out)
+
+    def trial(B):
+        h = hps.replace(batch_size=B)
+        batches = make_batches(h, vocab, corpus, 2, pad_enc_to=c["enc"])
+        tr = GraphTrainer(h, vocab.size(), B=B, T=c["enc"], device=dev, info=DistInfo(), use_graph=not args.no_graph)
+        warm(tr, batches)
+        torch.cuda.synchronize()
+        return (tr if not info.enabled else None), batches
+
+    B, got = agree_largest(CONFIG5_BATCHES, trial, info, D, dev)
+    if B is None:
+        return {"config5_error": f"no per-GPU batch of {CONFIG5_BATCHES} fits every rank"}
+    tr, batches = got
+    if tr is None:  # data parallel: the trial trainer had no collectives
+        tr = GraphTrainer(hps.replace(batch_size=B), vocab.size(), B=B, T=c["enc"], device=dev, info=info,
+                          use_graph=not args.no_graph)
+        warm(tr, batches)
     n_warm = len(batches)
-    for b in batches:  # warm-up: graph capture, then a replay of each batch (each live-row bucket's head graph)
-        out = tr.step(b)
-    tr.check_finite(out)
 
     def loop():
         tokens = 0
@@ -328,13 +383,16 @@ def bench_config5(args, info, D, torch, dev_id):
     tr.check_finite(out)
     el_max = D.all_reduce_scalar(el, info, op="max", device=tr.device)
     tok_all = D.all_reduce_scalar(float(tokens), info, op="sum", device=tr.device)
+    peak = D.all_reduce_scalar(torch.cuda.max_memory_allocated(dev_id) / 2 ** 30, info, op="max", device=tr.device)
     del tr, batches
     torch.cuda.empty_cache()
     rec = {"config5_tokens_per_sec": round(tok_all / el_max, 1),
            "config5_ms_per_step": round(1000.0 * el_max / args.config5_steps, 3),
+           "config5_peak_mem_gb": round(peak, 1),
            "config5_config": {"model": f"pointer-generator+coverage hidden={c['hidden']} emb={args.emb} "
                                        f"enc={c['enc']} dec={args.dec} vocab={args.vocab} enc_layers={c['layers']}",
-                              "per_gpu_batch": c["batch"], "global_batch": c["batch"] * info.world,
+                              "per_gpu_batch": B, "global_batch": B * info.world,
+                              "batch_sizing": f"largest of {list(CONFIG5_BATCHES)} whose step fits every rank",
                               "steps": args.config5_steps, "warmup": n_warm}}
     if args.decode_batches > 0:
         a5 = _ap.Namespace(**{**vars(args), "hidden": c["hidden"], "layers": c["layers"], "enc": c["enc"],

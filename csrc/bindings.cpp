@@ -511,6 +511,28 @@ Tensor debug_status() {
 }
 void debug_clear() { tsamd_debug_clear(); }
 
+// ---------------------------------------------------------------- probes (probes.hip)
+int64_t cu_hold_max_lds_op() { return cu_hold_max_lds(); }
+void cu_hold(const Tensor& times, int64_t grid, double ms, int64_t lds_bytes) {
+  chk(times, at::kLong, "times");
+  numel_eq(times, 2 * grid, "times");
+  TORCH_CHECK(grid >= 1 && grid <= 4096 && ms > 0 && ms <= 2000, "cu_hold: 1..4096 workgroups for at most 2 s");
+  TORCH_CHECK(lds_bytes >= 0 && lds_bytes <= cu_hold_max_lds(), "cu_hold: lds_bytes above the CU's LDS");
+  launch_cu_hold((int)grid, (unsigned long long)(ms * 1e5), P<long long>(times), (int)lds_bytes, stream());
+}
+void tanh_eval(const Tensor& x, const Tensor& t, const Tensor& s2, int64_t mode) {
+  chk(x, F32, "x"); chk(t, F32, "t"); chk(s2, F32, "s2");
+  numel_eq(t, x.numel(), "t"); numel_eq(s2, x.numel(), "s2");
+  TORCH_CHECK(mode == 0 || mode == 1, "tanh_eval: mode 0 (exp + rcp) or 1 (rational)");
+  launch_tanh_eval(P<float>(x), P<float>(t), P<float>(s2), (int)x.numel(), (int)mode, stream());
+}
+void tanh_tput(const Tensor& in, const Tensor& out, int64_t iters, int64_t mode) {
+  chk(in, F32, "in"); chk(out, F32, "out");
+  TORCH_CHECK(in.numel() >= 1024 && out.numel() % 256 == 0 && out.numel() > 0, "tanh_tput: in >= 1024, out % 256");
+  TORCH_CHECK((mode == 0 || mode == 1) && iters >= 1, "tanh_tput: mode 0 / 1");
+  launch_tanh_tput(P<float>(in), P<float>(out), (int)out.numel(), (int)iters, (int)mode, stream());
+}
+
 // fused training vocab head (vocab_train.hip): logits never materialised
 int64_t vocab_train_tiles_op(int64_t V, int64_t H) { return vocab_train_tiles((int)V, (int)H); }
 
@@ -927,6 +949,10 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("debug_enabled", &debug_enabled);
   m.def("debug_status", &debug_status);
   m.def("debug_clear", &debug_clear);
+  m.def("cu_hold_max_lds", &cu_hold_max_lds_op);
+  m.def("cu_hold", &cu_hold);
+  m.def("tanh_eval", &tanh_eval);
+  m.def("tanh_tput", &tanh_tput);
   m.def("vocab_train_tiles", &vocab_train_tiles_op);
   m.def("vocab_train_fwd", &vocab_train_fwd);
   m.def("vocab_train_bwd", &vocab_train_bwd);

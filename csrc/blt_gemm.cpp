@@ -18,7 +18,11 @@
 // allocated on the first eager call on that stream; a stream first seen inside a capture (the
 // capture stream of torch.cuda.graph) takes one of the spares allocated on the first call.  No
 // solution ever runs with a workspace smaller than it reports needing (a null workspace under
-// capture faulted the GPU in round 4: profiles/r4/ab/blt_gemm.md).
+// capture faulted the GPU in round 4: profiles/r4/ab/blt_gemm.md).  Workspaces come from torch's
+// caching allocator (an allocation failure is torch.cuda.OutOfMemoryError, which `--batch auto`
+// steps down from) and are never freed: captured graphs keep their pointers.  At most
+// TSAMD_BLT_MAX_WS (16) streams get one; later streams run workspace-free solutions (the key
+// records which), so the footprint is bounded whatever the stream pool hands out.
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -48,8 +52,8 @@ struct Key {
   bool ta, tb;
   int64_t M, N, K, lda, ldb, ldc;
   int out_bf16, beta_nz, bias_kind;  // bias_kind: 0 none, 1 fp32, 2 bf16
-  bool ws;
-  auto tie() const { return std::tie(ta, tb, M, N, K, lda, ldb, ldc, out_bf16, beta_nz, bias_kind, ws); }
+  bool ws, det;                      // det: deterministic mode (first fitting pick, never timed)
+  auto tie() const { return std::tie(ta, tb, M, N, K, lda, ldb, ldc, out_bf16, beta_nz, bias_kind, ws, det); }
   bool operator<(const Key& o) const { return tie() < o.tie(); }
 };
 
@@ -67,7 +71,8 @@ struct State {
   hipblasLtHandle_t handle = nullptr;
   std::map<Key, Pick> picks;
   std::map<hipStream_t, void*> ws;
-  std::vector<void*> spare;  // allocated eagerly, handed to streams first seen inside a capture
+  std::vector<Tensor> owned;  // every workspace (torch caching allocator), kept for the process
+  std::vector<void*> spare;   // allocated eagerly, handed to streams first seen inside a capture
   bool spares_made = false;
   int64_t tuned = 0, calls = 0;
 };
@@ -86,6 +91,11 @@ bool capturing(hipStream_t s) {
 int env_int(const char* n, int d) {
   const char* v = std::getenv(n);
   return v && *v ? std::atoi(v) : d;
+}
+
+void* new_workspace(State& S, const Tensor& like) {
+  S.owned.push_back(at::empty({(int64_t)kWorkspace}, like.options().dtype(at::kByte)));
+  return S.owned.back().data_ptr();
 }
 
 struct Desc {
@@ -184,26 +194,24 @@ void blt_mm(const Tensor& a, const Tensor& b, const Tensor& out, bool ta, bool t
     // spare workspaces for the capture streams (torch.cuda.graph captures on a stream of its
     // own): no allocation can happen inside a capture, and a solution that needs a workspace
     // must never get a null one
-    for (int i = 0; i < std::max(0, env_int("TSAMD_BLT_SPARE_WS", 4)); ++i) {
-      void* w = nullptr;
-      BLT_CK(hipMalloc(&w, kWorkspace));
-      S.spare.push_back(w);
-    }
+    for (int i = 0; i < std::max(0, env_int("TSAMD_BLT_SPARE_WS", 4)); ++i) S.spare.push_back(new_workspace(S, out));
   }
   void* ws = nullptr;
   auto wit = S.ws.find(s);
   if (wit != S.ws.end()) {
     ws = wit->second;
-  } else if (!cap) {
-    BLT_CK(hipMalloc(&ws, kWorkspace));
+  } else if (!cap && (int)S.ws.size() < env_int("TSAMD_BLT_MAX_WS", 16)) {
+    ws = new_workspace(S, out);
     S.ws[s] = ws;
-  } else if (!S.spare.empty()) {
+  } else if (cap && !S.spare.empty()) {
     ws = S.spare.back();
     S.spare.pop_back();
     S.ws[s] = ws;
   }
   const size_t wsb = ws ? kWorkspace : 0;
-  Key k{ta, tb, M, N, K, lds(a), lds(b), lds(out), out.scalar_type() == at::kBFloat16, beta != 0.0, bias_kind, ws != nullptr};
+  const bool det = env_int("TSAMD_DETERMINISTIC", 0) != 0;
+  Key k{ta, tb, M, N, K, lds(a), lds(b), lds(out), out.scalar_type() == at::kBFloat16, beta != 0.0, bias_kind, ws != nullptr,
+        det};
   const void* bias_ptr = bias_kind ? bias->data_ptr() : nullptr;
   Desc d;
   make_desc(d, k, bias_ptr);
@@ -226,7 +234,7 @@ void blt_mm(const Tensor& a, const Tensor& b, const Tensor& out, bool ta, bool t
     BLT_CK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &w64, sizeof(w64)));
     // deterministic mode: the library's first fitting pick, so a run's GEMMs do not depend on
     // another run's timings (bit-reproducible across processes, not only within one)
-    const bool tune = !cap && env_int("TSAMD_BLT_TUNE", 1) != 0 && env_int("TSAMD_DETERMINISTIC", 0) == 0;
+    const bool tune = !cap && env_int("TSAMD_BLT_TUNE", 1) != 0 && !det;
     const int want = tune ? std::max(1, env_int("TSAMD_BLT_CANDIDATES", 24)) : 8;
     std::vector<hipblasLtMatmulHeuristicResult_t> hr(want);
     int got = 0;

@@ -188,3 +188,9 @@ void launch_pack_cast(const long* jobs, int nj, long total, hipStream_t st);
 // p_gen gradient into the decoder inputs' direct terms + bias gradient (decoder.hip)
 void launch_pgen_dirs(const float* dpre, const float* w, float* dctx, float* dc, float* dh, float* dx, float* gb,
                       int N, int A, int H, int E, hipStream_t st);
+
+// probes.hip: CU hold (RCCL co-residency stand-in), device tanh accuracy / issue-rate probes
+int cu_hold_max_lds();
+void launch_cu_hold(int grid, unsigned long long ticks, long long* times, int lds_bytes, hipStream_t st);
+void launch_tanh_eval(const float* x, float* t, float* s2, int n, int mode, hipStream_t st);
+void launch_tanh_tput(const float* in, float* out, int threads, int iters, int mode, hipStream_t st);

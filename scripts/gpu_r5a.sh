@@ -1,0 +1,12 @@
+#!/bin/bash
+# round-5 check: new probes + co-residency test first, the GPU tier, smoke, tanh probe, bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/${OUTD:-r5a}; mkdir -p $OUT
+export TMPDIR=/tmp
+step() { local n=$1; shift; echo "== $n"; timeout -k 10 ${T:-300} "$@" > $OUT/$n.log 2>&1; local rc=$?; tail -${TL:-3} $OUT/$n.log; return $rc; }
+step new python -u -m pytest tests/test_gpu_probes.py tests/test_gpu_production.py -q -x --timeout 200 --timeout-method thread -k "probe or tanh or held" &&
+TL=1 step tanh python -u tools/tanh_probe.py &&
+T=900 step tier python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread &&
+step smoke python -u -c "import __graft_entry__ as g; g.smoke()" &&
+T=600 TL=1 step bench python -u bench.py

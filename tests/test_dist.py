@@ -274,3 +274,70 @@ def test_bucket_issue_order_leaves_only_the_embedding(defer):
         assert events.index(("bucket", 1)) == events.index(("graph", 1)) + 1
     left = sum(red.buckets[b].numel() * 4 for b in range(4) if b not in issued_before_last)
     assert left == 50000 * 128 * 4 <= 26 * 2 ** 20  # the embedding only
+
+
+class _ListBatcher:
+    def __init__(self, n):
+        self.items = list(range(n))
+
+    def next_batch(self):
+        return self.items.pop(0) if self.items else None
+
+
+def _synced_worker(rank, world, port, q, lengths, window):
+    info = _init(rank, world, port)
+    from textsummarization_on_flink_amd.parallel.dist import SyncedBatcher
+    sb = SyncedBatcher(_ListBatcher(lengths[rank]), info, window=window)
+    got = []
+    while True:
+        b = sb.next_batch()
+        if b is None:
+            break
+        got.append(b)
+    sb.close()
+    q.put((rank, got, sb.collectives))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("lengths,window", [((23, 17), 5), ((10, 10), 5), ((3, 40), 4), ((0, 7), 3)])
+def test_synced_batcher_stops_every_rank_at_the_same_step(lengths, window):
+    """Stream-fed DP (flink_entry.training_on_flink): streams that end unevenly across ranks stop
+    every rank after the same number of batches (the shortest stream's), with ONE blocking host
+    collective per window of batches -- not one per batch (no per-step host sync)."""
+    res = _spawn(_synced_worker, 2, lengths, window)
+    n = min(lengths)
+    for r in range(2):
+        got, coll = res[r]
+        assert got == list(range(n)), (r, got)
+        assert coll <= n // window + 1, (r, coll)
+
+
+def _agree_worker(rank, world, port, q, fits_on_rank1):
+    info = _init(rank, world, port)
+    import sys as _sys
+    _sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from textsummarization_on_flink_amd.parallel import dist as D
+
+    def trial(c):
+        if rank == 1 and c > fits_on_rank1:  # an OOM on one rank only
+            raise torch.cuda.OutOfMemoryError(f"HIP out of memory (injected, batch {c})")
+        return f"trainer-{c}"
+
+    got = bench.agree_largest((2048, 1024, 512), trial, info, D, "cpu")
+    # a collective after the search: every rank must reach it (no rank left behind in a trial)
+    total = D.all_reduce_scalar(1.0, info, op="sum", device="cpu")
+    q.put((rank, got, total))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("fits_on_rank1,want", [(1024, 1024), (2048, 2048), (0, None)])
+def test_capacity_search_agrees_when_one_rank_runs_out_of_memory(fits_on_rank1, want):
+    """bench.py's config #5 batch sizing: an OOM injected on rank 1 only makes EVERY rank step down
+    to the same batch (or all skip when nothing fits), then both reach the next collective: no
+    rank-local skip that would leave its peer blocked in an all-reduce."""
+    res = _spawn(_agree_worker, 2, fits_on_rank1)
+    for r in range(2):
+        (c, trial_result), total = res[r]
+        assert c == want and total == 2.0
+        assert trial_result == (None if want is None else f"trainer-{want}")

@@ -165,8 +165,8 @@ def test_device_beam_graph_equals_eager_and_tracks_oracle(coverage, pointer_gen)
         assert len(hg[0].attn_dists) == len(hg[0].tokens) - 1
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_pipelined_decode_batches_equal_batch_by_batch(overlap):
+@pytest.mark.parametrize("overlap,flush", [(False, False), (True, False), (True, True)])
+def test_pipelined_decode_batches_equal_batch_by_batch(overlap, flush):
     """decode_batches (results snapshotted to pinned memory, backtracked while the next batch
     runs; overlap: the next batch's encoder on a side stream beside the decode steps) ==
     decode() batch by batch: same summaries in the same order."""
@@ -179,7 +179,10 @@ def test_pipelined_decode_batches_equal_batch_by_batch(overlap):
     d = DeviceBeamDecoder(hps, vocab, params, n_articles=hps.batch_size, T=hps.max_enc_steps, use_graph=True)
     seq = [[h.tokens for h in d.decode(b)] for b in batches]
     d.overlap_encoder = overlap
-    piped = [[h.tokens for h in hy] for hy in d.decode_batches(batches)]
+    # flush: a streaming source with nothing queued between batches (FLUSH from the encoder
+    # look-ahead, then a batch from the last-chunk poll, which was not pre-encoded)
+    src = [x for b in batches for x in (b, d.FLUSH)] if flush else batches
+    piped = [[h.tokens for h in hy] for hy in d.decode_batches(src)]
     assert piped == seq
 
 

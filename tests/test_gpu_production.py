@@ -337,3 +337,49 @@ def test_deterministic_mode_bit_identical(monkeypatch, B, split):
                     print(other, *d, flush=True)
             assert same, other
     assert _rel(res["det1"][0].view(torch.float32), res["atomic"][0].view(torch.float32)) < 1e-3
+
+
+def test_bptt_phase_beside_cus_held_like_rccl(monkeypatch):
+    """The data-parallel co-residency guard (train/trainer.py): RCCL collective kernels hold at most
+    RCCL_MAX_CHANNELS CUs (one workgroup per channel, capped in every rank's environment), and a
+    persistent-LSTM grid that leaves that many CUs free may run beside in-flight all-reduces.
+    Here a kernel holds exactly LSTM_RCCL_RESERVE_CUS CUs (one workgroup per CU through its whole-LDS
+    request, spinning on the clock) while the captured B = 256 step replays, encoder BPTT included:
+    no hand-off timeout (lstm_err 0) and gradients bit-equal to the solo step (deterministic mode)."""
+    from textsummarization_on_flink_amd.ops import ops
+    from textsummarization_on_flink_amd.parallel.rccl_env import RCCL_MAX_CHANNELS
+    from textsummarization_on_flink_amd.train.trainer import LSTM_RCCL_RESERVE_CUS, GraphTrainer
+    k = ops()
+    monkeypatch.setenv("TSAMD_DETERMINISTIC", "1")
+    B = 256
+    hps = _hps(B)
+    vocab, (batch,) = _batches(hps, 1, seed=21)
+    tr = GraphTrainer(hps, vocab.size(), B=B, T=T, device="cuda:0")
+    eng = tr.engine
+    reserve = max(LSTM_RCCL_RESERVE_CUS, RCCL_MAX_CHANNELS)
+    grid, cap = int(k.lstm_persistent_grid(eng.H, B)), int(k.lstm_persistent_capacity(eng.H))
+    assert eng.persistent_lstm and 0 < grid <= cap - reserve  # the shape the DP trainer lets RCCL overlap
+    snap = (tr.params.flat.clone(), tr.params.accum.clone())
+    tr.check_finite(tr.step(batch))  # capture + one step
+
+    def step(hold: bool):
+        tr.params.flat.copy_(snap[0])
+        tr.params.accum.copy_(snap[1])
+        eng.pack()
+        times = torch.zeros(2 * reserve, dtype=torch.long, device="cuda")
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        if hold:
+            with torch.cuda.stream(side):  # held for 300 ms: the whole step (~20 ms) runs beside it
+                k.cu_hold(times, reserve, 300.0, int(k.cu_hold_max_lds()))
+        tr.step(batch)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        return tr.params.grad.clone().view(torch.int32), int(eng.w["lstm_err"].item()), times.cpu()
+
+    g_solo, err_solo, _ = step(False)
+    g_held, err_held, times = step(True)
+    assert err_solo == 0 and err_held == 0
+    t0, t1 = times[0::2], times[1::2]
+    assert int(t0.max()) < int(t1.min())  # every holding workgroup was resident at once
+    assert torch.equal(g_solo, g_held)

@@ -99,6 +99,7 @@ def test_stream_decode_packer_answers_every_row():
     hps = HParams(mode="decode", batch_size=4, beam_size=4, max_enc_steps=T, max_dec_steps=10, vocab_size=2000,
                   coverage=True)
     rows = corpus.rows(23, "q")
+    rows[5]["uuid"] = ""  # an empty uuid is written back as is (the serial writer's rule)
     cin, cout = ExampleCoding(IN_COLS, [DataTypes.STRING] * 3), ExampleCoding(OUT_COLS, [DataTypes.STRING] * 4)
     rin, rout = _ring("din"), _ring("dout")
     pool = StreamDecodePacker(rin, rout, cin, cout, vocab, hps, packers=2, n_articles=Na, T=T, max_wait_s=0.0)
@@ -140,3 +141,25 @@ def test_stream_decode_packer_answers_every_row():
         assert o["summary"] == summary and o["reference"] == reference and o["article"] == r["article"]
     for x in (rin, rout):
         x.release()
+
+
+def test_stream_train_packer_raises_when_its_feed_fails():
+    """A row larger than a packer ring stops the native fanout, which closes every packer input:
+    the consumer must see an error, not a normal end of stream on truncated input."""
+    corpus = SyntheticCorpus(vocab_size=2000, raw_vocab=6000, seed=4, art_mean=80, art_sd=30)
+    vocab = corpus.vocab(2000)
+    hps = HParams(batch_size=8, max_enc_steps=64, max_dec_steps=12, vocab_size=2000, coverage=True)
+    rows = corpus.rows(40)
+    rows[20]["article"] = " ".join(["word"] * 40000)  # ~200 KB: does not fit a 64 KB packer ring
+    coding = ExampleCoding(IN_COLS, [DataTypes.STRING] * 3)
+    rin = _ring("in")
+    sp = StreamTrainPacker(rin, coding, vocab, hps, 2, pad_enc_to=64, ring_bytes=1 << 16)
+    for r in rows:
+        rin.push(coding.encode(r))
+    rin.close()
+    n = 0
+    with pytest.raises(RuntimeError, match="fanout"):
+        while sp.next_batch() is not None:
+            n += 1
+    sp.stop()
+    assert n <= 3  # the batches before the failed row at most

@@ -230,6 +230,8 @@ class WorkerJob:
                         "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
                         "PYTHONPATH": REPO_ROOT + os.pathsep + env.get("PYTHONPATH", "")})
             env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            from ..parallel.rccl_env import rccl_env
+            rccl_env(env)  # RCCL's CU cap, before the worker initialises anything
             self.procs.append(subprocess.Popen([py, "-m", "textsummarization_on_flink_amd.api.worker", sp], env=env,
                                                cwd=os.getcwd()))
             if rout is not None:

@@ -138,14 +138,29 @@ class _Pool:
                 raise RuntimeError(f"stream packer {p} failed: {meta['error']}")
             return meta, payload
 
+    def check_feed(self) -> None:
+        """At a consumer's end of stream: the input fanout (``pipes[0]``) must have ended at its
+        source's end of stream.  A fanout that stopped on an error (a row larger than a packer
+        ring, a packer ring closed early) also closes every packer input ring, which the packers
+        cannot tell from a normal end -- so the error is raised here instead of the stream
+        ending 'successfully' on truncated input."""
+        if not self.pipes or self.pipes[0] is None:
+            return
+        fan, self.pipes[0] = self.pipes[0], None
+        try:
+            fan.join()
+        except Exception as e:  # noqa: BLE001
+            raise RuntimeError(f"stream input fanout failed: {e!r}") from e
+
     def stop(self):
-        for pipe in self.pipes:
+        pipes = [p for p in self.pipes if p is not None]
+        for pipe in pipes:
             pipe.stop()
-        for pipe in self.pipes:
+        for pipe in pipes:
             try:
                 pipe.join()
-            except Exception:  # noqa: BLE001
-                pass
+            except Exception as e:  # noqa: BLE001 -- cleanup (also on error paths): logged, not raised
+                log.warning("stream pipe ended with %r", e)
         self.pipes = []
         for rs in self.rings:
             for r in rs:
@@ -236,8 +251,9 @@ class StreamTrainPacker:
             return None
         p = self.k % len(self.pool.procs)
         got = self.pool.pop(p)
-        if got is None:  # packer p had no group k: the stream ended
+        if got is None:  # packer p had no group k: the stream ended (or its feed failed: raises)
             self.done = True
+            self.pool.check_feed()
             return None
         meta, payload = got
         self.k += 1
@@ -351,7 +367,8 @@ def _decode_packer(p: int, n: int, names: List[str], coding, out_coding, vocab, 
                 rout.close()  # no more examples from this packer
                 continue
             ex = sb._example(coding.decode_dict(rec))
-            pending[eid] = (ex.uuid if ex.uuid else "uuid-%d-%d" % (p, eid), ex.original_article,
+            # the serial writer's rule (decoder.py handle): only a missing uuid gets a synthetic one
+            pending[eid] = (ex.uuid if ex.uuid is not None else "uuid-%d-%d" % (p, eid), ex.original_article,
                             ex.original_abstract_sents, ex.article_oovs)
             enc = np.asarray(ex.enc_input, dtype=np.int32)
             ext = np.asarray(ex.enc_input_extend_vocab, dtype=np.int32)
@@ -468,6 +485,7 @@ class StreamDecodePacker:
         self._gather(items, owners)
         if not items:
             if not self._live:
+                self.pool.check_feed()
                 return None
             if not block:
                 return self.NOT_READY
@@ -480,6 +498,7 @@ class StreamDecodePacker:
                         self.pool.check_alive(p)
                 self._gather(items, owners)
             if not items:
+                self.pool.check_feed()
                 return None
         if self.max_wait_s > 0 and len(items) < self.Na:
             deadline = time.time() + self.max_wait_s

@@ -451,11 +451,13 @@ class DeviceBeamDecoder:
                     pre = True
             # overlap_encoder: batch n + 1's encoder runs on a side stream beside batch n's decode steps
             nxt = next(it, None) if ov else None
-            if nxt is self.FLUSH:
-                nxt = None  # polled again once this batch is queued
+            flushed = nxt is self.FLUSH
+            if flushed:
+                nxt = None  # nothing ready: polled again while this batch's last chunk runs
             elif nxt is not None:
                 self._rows_ok(nxt)
-            first, fetched = True, ov
+            nxt_pre = nxt is not None  # run_chunks launches its encoder beside this batch's steps
+            first, fetched = True, ov and not flushed
             for _ in self.run_chunks(batch, pre_encoded=pre, next_batch=nxt):
                 if first and pending is not None:  # the GPU has this batch's work queued
                     yield self._finish(pending)
@@ -466,7 +468,7 @@ class DeviceBeamDecoder:
                     # batch now, so forming and packing it overlaps the GPU instead of following it
                     # (a streaming source forms it from the requests that arrived meanwhile)
                     fetched = True
-                    nxt = next(it, None)
+                    nxt, nxt_pre = next(it, None), False
                     if nxt is self.FLUSH:
                         nxt = None  # nothing ready: polled again once this batch is done
                     elif nxt is not None:
@@ -476,7 +478,7 @@ class DeviceBeamDecoder:
             arrays, ev = self._snapshot(slot)
             slot ^= 1
             pending = (arrays, ev, self._n_valid(batch), self.steps_run)
-            batch, pre = nxt, (nxt is not None and ov)
+            batch, pre = nxt, (nxt is not None and nxt_pre)
             if batch is None and done_src:
                 break
         if pending is not None:

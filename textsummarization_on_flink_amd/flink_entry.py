@@ -15,7 +15,7 @@ import logging
 import torch
 
 from textsummarization_on_flink_amd.config import parse_hyperparam_string
-from textsummarization_on_flink_amd.parallel.dist import DistInfo, all_reduce_scalar, init_from_env
+from textsummarization_on_flink_amd.parallel.dist import DistInfo, SyncedBatcher, init_from_env
 
 log = logging.getLogger("flink_entry")
 DEFAULT_KEY = "TF_Hyperparameter"
@@ -33,22 +33,6 @@ class FlinkWriter:
 
     def close(self):
         self._w.close()
-
-
-class SyncedBatcher:
-    """DP lock-step: every rank gets a batch or all stop (avoids a collective hang when
-    the row stream ends unevenly across workers)."""
-
-    def __init__(self, inner, info: DistInfo):
-        self.inner, self.info = inner, info
-
-    def next_batch(self):
-        b = self.inner.next_batch()
-        if self.info.enabled:
-            have = all_reduce_scalar(0.0 if b is None else 1.0, self.info)
-            if have < self.info.world:
-                return None
-        return b
 
 
 def _hps(context):
@@ -89,9 +73,12 @@ def training_on_flink(context, hps, info: DistInfo, packer=None):
     else:
         pad = hps.max_enc_steps if (_gpu() and hps.pad_enc_to_max) else None
         inner = FlinkTrainBatcher(context.reader(), vocab, hps, pad_enc_to=pad)
+    # lock-step end of stream: one host-side agreement per check window (never a per-step sync)
+    synced = SyncedBatcher(inner, info, window=max(1, int(hps.check_every)))
     try:
-        setup_training(hps, vocab, SyncedBatcher(inner, info), info=info, metrics=cli.metrics_for(hps, info))
+        setup_training(hps, vocab, synced, info=info, metrics=cli.metrics_for(hps, info))
     finally:
+        synced.close()
         if packer is not None:
             packer.stop()
 

@@ -20,13 +20,19 @@ summaries) -- fixing the reference's every-worker-is-chief defect (SURVEY 2.9 it
 """
 from __future__ import annotations
 
+import collections
 import datetime
 import os
+import queue
+import threading
 from dataclasses import dataclass
 from typing import List, Optional
 
 import torch
 import torch.distributed as dist
+
+
+from .rccl_env import RCCL_MAX_CHANNELS, rccl_cu_reserve, rccl_env  # noqa: F401  (torch-free)
 
 
 @dataclass
@@ -57,6 +63,7 @@ def init_from_env(backend: Optional[str] = None, timeout_s: int = 600, ps_num: i
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    rccl_env()  # before the first communicator initialises (torchrun-launched ranks)
     if backend == "nccl":
         torch.cuda.set_device(local)
     if not dist.is_initialized():
@@ -184,3 +191,106 @@ def barrier(info: DistInfo, device=None):
             dist.barrier(device_ids=[info.local_rank])
         else:
             dist.barrier()
+
+
+_CPU_GROUPS = {}
+
+
+def cpu_group(info: DistInfo):
+    """A gloo process group over every rank for host-side agreement (collectives on CPU tensors
+    that never wait on the GPU stream); the default group when that is gloo already.  Created
+    once per process: every rank must reach the first call."""
+    if not info.enabled:
+        return None
+    if info.backend == "gloo":
+        return None
+    key = (info.world, info.backend)
+    if key not in _CPU_GROUPS:
+        _CPU_GROUPS[key] = dist.new_group(backend="gloo")
+    return _CPU_GROUPS[key]
+
+
+class SyncedBatcher:
+    """Data-parallel lock-step over streams that end unevenly across ranks (reference: every
+    worker reads its own Flink partition, ``run_summarization.py:402-426`` / ``train.py:92-120``;
+    with synchronous all-reduce, a rank that runs out first would leave the others blocked in a
+    gradient collective).
+
+    Agreement once per window of ``window`` batches instead of once per batch: a prefetch thread
+    pulls the inner batcher's batches ahead (host-side packs), and at each window boundary the
+    ranks all-reduce MIN over how many batches they hold for the next window (at most
+    ``window``) on a CPU gloo group -- one blocking host collective per window that never waits
+    on the GPU stream (the GPU trainer enqueues steps without host syncs).  Every rank then
+    serves exactly the agreed count; a count below ``window`` means some rank's stream ended,
+    and every rank stops after those batches: all ranks stop at the same step."""
+
+    _END = object()
+
+    def __init__(self, inner, info: DistInfo, window: int = 10, group=None):
+        self.inner, self.info = inner, info
+        self.window = max(1, int(window))
+        self.collectives = 0  # blocking host collectives issued (one per window)
+        self._buf = collections.deque()
+        self._allowed = 0
+        self._final = False
+        self._src_done = False
+        self._stop = threading.Event()
+        self._thread = None
+        if info.enabled:
+            self._group = group if group is not None else cpu_group(info)
+            self._q: "queue.Queue" = queue.Queue(maxsize=2 * self.window)
+            self._thread = threading.Thread(target=self._pump, name="synced-batcher", daemon=True)
+            self._thread.start()
+
+    def _pump(self):
+        try:
+            while not self._stop.is_set():
+                b = self.inner.next_batch()
+                self._put(self._END if b is None else b)
+                if b is None:
+                    return
+        except BaseException as e:  # noqa: BLE001 -- re-raised on the consumer thread
+            self._put(e)
+
+    def _put(self, item):
+        while not self._stop.is_set():
+            try:
+                self._q.put(item, timeout=0.2)
+                return
+            except queue.Full:
+                continue
+
+    def _fill(self) -> int:
+        """Batches held for the next window: blocks until ``window`` are buffered or the local
+        stream ended (the prefetch thread normally has them ready)."""
+        while len(self._buf) < self.window and not self._src_done:
+            item = self._q.get()
+            if item is self._END:
+                self._src_done = True
+            elif isinstance(item, BaseException):
+                raise item
+            else:
+                self._buf.append(item)
+        return min(len(self._buf), self.window)
+
+    def next_batch(self):
+        if not self.info.enabled:
+            return self.inner.next_batch()
+        if self._allowed == 0:
+            if self._final:
+                return None
+            have = self._fill()
+            t = torch.tensor([float(have)], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._group)
+            self.collectives += 1
+            self._allowed = int(t.item())
+            self._final = self._allowed < self.window
+            if self._allowed == 0:
+                return None
+        self._allowed -= 1
+        return self._buf.popleft()
+
+    def close(self):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5)

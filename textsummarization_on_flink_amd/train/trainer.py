@@ -33,7 +33,7 @@ import torch
 
 from ..models.params import FlatParams, build_params
 from ..models.pointer_generator import HipPointerGenerator, LstmHandoffError  # noqa: F401
-from ..parallel.dist import DistInfo, GradAllReducer, broadcast_params
+from ..parallel.dist import DistInfo, GradAllReducer, broadcast_params, rccl_cu_reserve
 from ..utils.graphs import capture_guard
 
 log = logging.getLogger(__name__)
@@ -43,7 +43,8 @@ class NonFiniteLossError(RuntimeError):
     pass
 
 
-# CUs kept free of persistent-LSTM workgroups before RCCL kernels may overlap the launch
+# CUs kept free of persistent-LSTM workgroups before RCCL kernels may overlap the launch: RCCL's
+# channel cap (parallel/dist.py RCCL_MAX_CHANNELS, applied to every rank's environment)
 LSTM_RCCL_RESERVE_CUS = 64
 
 
@@ -110,7 +111,7 @@ class GraphTrainer:
         if self.info.enabled and eng.persistent_lstm:
             grid = int(eng.k.lstm_persistent_grid(eng.H, eng.B))
             cap = int(eng.k.lstm_persistent_capacity(eng.H))
-            self.lstm_exclusive = grid > cap - LSTM_RCCL_RESERVE_CUS
+            self.lstm_exclusive = grid > cap - max(LSTM_RCCL_RESERVE_CUS, rccl_cu_reserve())
         self.use_graph = use_graph
         self.g_fb = None
         self.g_opt = None
