@@ -511,6 +511,40 @@ Tensor debug_status() {
 }
 void debug_clear() { tsamd_debug_clear(); }
 
+// ---------------------------------------------------------------- hand-written MFMA GEMM (gemm_mfma.hip)
+// out[M, N] (+)= A[arow(m), :K] . Bt[N, K]^T (+ bias): A rows plain (ids / rev absent) or gathered
+// through the encoder step frame (rev [B][T] int64, direction dir; ids [B][T] int64 optional: A is
+// then the embedding table) -- every operand row-contiguous with its own leading dimension
+bool gemm_bt_ok(int64_t M, int64_t N, int64_t K) { return gemm_bt_supported((int)M, (int)N, (int)K, N % 256 == 0 ? 256 : 128); }
+void gemm_bt(const Tensor& A, const Tensor& Bt, const Tensor& out, double beta, const OT& bias, const OT& ids,
+             const OT& rev, int64_t B, int64_t T, int64_t dir) {
+  TORCH_CHECK(A.is_cuda() && A.dim() == 2 && A.scalar_type() == BF && A.stride(1) == 1, "gemm_bt: A [rows, K] bf16");
+  TORCH_CHECK(Bt.is_cuda() && Bt.dim() == 2 && Bt.scalar_type() == BF && Bt.stride(1) == 1, "gemm_bt: Bt [N, K] bf16");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.stride(1) == 1 && (out.scalar_type() == F32 || out.scalar_type() == BF),
+              "gemm_bt: out [M, N] fp32 / bf16");
+  const int64_t M = out.size(0), N = out.size(1), K = Bt.size(1);
+  TORCH_CHECK(Bt.size(0) == N && A.size(1) >= K, "gemm_bt: shape mismatch A ", A.sizes(), " Bt ", Bt.sizes(), " out ", out.sizes());
+  TORCH_CHECK(gemm_bt_ok(M, N, K), "gemm_bt: N % 128 == 0 and K % 64 == 0 (got N ", N, " K ", K, ")");
+  TORCH_CHECK(A.stride(0) % 8 == 0 && Bt.stride(0) % 8 == 0 && out.stride(0) % 8 == 0 &&
+              reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(Bt.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "gemm_bt: 16-byte aligned rows");
+  const bool obf = out.scalar_type() == BF;
+  TORCH_CHECK(beta == 0.0 || (beta == 1.0 && !obf), "gemm_bt: beta 0, or 1 with an fp32 out");
+  chko(bias, F32, N, "bias");
+  const bool frame = PO<int64_t>(rev) != nullptr;
+  if (frame) {
+    chk(*rev, at::kLong, "rev"); numel_eq(*rev, B * T, "rev");
+    TORCH_CHECK(M == B * T && (dir == 0 || dir == 1), "gemm_bt: step frame needs M = T * B and dir 0 / 1");
+    if (PO<int64_t>(ids)) { chk(*ids, at::kLong, "ids"); numel_eq(*ids, B * T, "ids"); }
+    else TORCH_CHECK(A.size(0) == B * T, "gemm_bt: batch-frame A needs B * T rows");
+  } else {
+    TORCH_CHECK(A.size(0) >= M && !PO<int64_t>(ids), "gemm_bt: plain A needs M rows");
+  }
+  launch_gemm_bt(P<bf16>(A), A.stride(0), P<bf16>(Bt), Bt.stride(0), out.data_ptr(), out.stride(0), obf, beta != 0.0,
+                 PO<float>(bias), (int)M, (int)N, (int)K, frame ? 1 : 0, PO<int64_t>(ids), PO<int64_t>(rev), A.size(0),
+                 (int)B, (int)T, (int)dir, stream());
+}
+
 // ---------------------------------------------------------------- probes (probes.hip)
 int64_t cu_hold_max_lds_op() { return cu_hold_max_lds(); }
 void cu_hold(const Tensor& times, int64_t grid, double ms, int64_t lds_bytes) {
@@ -949,6 +983,8 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("debug_enabled", &debug_enabled);
   m.def("debug_status", &debug_status);
   m.def("debug_clear", &debug_clear);
+  m.def("gemm_bt_ok", &gemm_bt_ok);
+  m.def("gemm_bt", &gemm_bt);
   m.def("cu_hold_max_lds", &cu_hold_max_lds_op);
   m.def("cu_hold", &cu_hold);
   m.def("tanh_eval", &tanh_eval);

@@ -194,3 +194,9 @@ int cu_hold_max_lds();
 void launch_cu_hold(int grid, unsigned long long ticks, long long* times, int lds_bytes, hipStream_t st);
 void launch_tanh_eval(const float* x, float* t, float* s2, int n, int mode, hipStream_t st);
 void launch_tanh_tput(const float* in, float* out, int threads, int iters, int mode, hipStream_t st);
+
+// gemm_mfma.hip: C (+)= A[arow(m)] . Bt^T (+ bias); amode 0 plain rows, 1 step-frame gather
+bool gemm_bt_supported(int M, int N, int K, int BN);
+void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, long ldc, bool out_bf16, bool beta,
+                    const float* bias, int M, int N, int K, int amode, const int64_t* ids, const int64_t* rev,
+                    long nsrc, int B, int T, int dir, hipStream_t st);

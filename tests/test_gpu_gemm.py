@@ -1,0 +1,68 @@
+"""Hand-written MFMA GEMM (csrc/kernels/gemm_mfma.hip) against an fp32 PyTorch matmul of the same
+bf16 operands: plain rows (fp32 / bf16 out, bias, beta = 1 accumulate, partial row tiles, 128-wide
+column tiles) and the encoder step-frame gather of its A rows (the embedding table by token id,
+or the layer below's batch-frame output; the bw direction reversed within each length) -- the
+rows to_step_frame used to write for the library GEMM."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _k():
+    from textsummarization_on_flink_amd.ops import ops
+    return ops()
+
+
+def _close(got, ref, tol=2e-3):
+    err = float((got.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+    assert err < tol, err
+
+
+@pytest.mark.parametrize("M,N,K,out_bf16,bias,beta", [(1000, 512, 256, False, True, False),
+                                                      (256, 256, 64, False, False, False),
+                                                      (777, 384, 128, True, True, False),
+                                                      (4096, 2048, 1024, False, False, True),
+                                                      (300, 128, 192, True, False, False)])
+def test_gemm_bt_plain_matches_fp32(M, N, K, out_bf16, bias, beta):
+    k = _k()
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    Bt = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g) if bias else None
+    c0 = torch.randn(M, N, device="cuda", generator=g)
+    out = c0.clone() if beta else torch.full((M, N), float("nan"), device="cuda",
+                                             dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    k.gemm_bt(A, Bt, out, 1.0 if beta else 0.0, b, None, None, 0, 0, 0)
+    torch.cuda.synchronize()
+    ref = A.float() @ Bt.float().t() + (b if bias else 0) + (c0 if beta else 0)
+    _close(out, ref, 1e-2 if out_bf16 else 2e-3)
+
+
+@pytest.mark.parametrize("ids", [True, False])
+@pytest.mark.parametrize("direction", [0, 1])
+def test_gemm_bt_step_frame_gather_matches_to_step_frame(ids, direction):
+    """out[(t, b)] = src[row(b, tt)] . W with tt = t (fw) or rev[b][t] (bw) -- bit-identical to the
+    library path's to_step_frame + GEMM operands (same bf16 rows), equal to fp32 within rounding."""
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    B, T, K, N, V = 48, 37, 128, 512, 3000
+    g = torch.Generator(device="cuda").manual_seed(11 + direction)
+    lens = torch.randint(1, T + 1, (B,), generator=g, device="cuda")
+    t = torch.arange(T, device="cuda")
+    rev = torch.where(t[None, :] < lens[:, None], lens[:, None] - 1 - t[None, :], t[None, :]).long().contiguous()
+    if ids:
+        src = torch.randn(V, K, device="cuda", generator=g).bfloat16()
+        tok = torch.randint(0, V, (B, T), generator=g, device="cuda").long()
+    else:
+        src = torch.randn(B * T, K, device="cuda", generator=g).bfloat16()
+        tok = None
+    W = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
+    out = torch.full((T * B, N), float("nan"), device="cuda")
+    k.gemm_bt(src, W, out, 0.0, None, tok, rev, B, T, direction)
+    torch.cuda.synchronize()
+    tt = t[None, :].expand(B, T) if direction == 0 else rev
+    rows = tok.gather(1, tt) if ids else torch.arange(B, device="cuda")[:, None] * T + tt
+    A = src[rows.t().reshape(-1)]  # step frame: m = t * B + b
+    ref = A.float() @ W.float().t()
+    _close(out, ref)

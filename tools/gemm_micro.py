@@ -1,43 +1,68 @@
-"""Timing of the output-projection gradient variants (dW = outb^T . dl, db = colsum(dl))."""
+"""Hand-written MFMA GEMM (gemm_bt) vs hipBLASLt (blt_mm, the fastest of its candidates) on the
+engine's activation-GEMM shapes; HIP-event times of graph-captured repeats, random bf16 data.
+
+  python tools/gemm_micro.py [--reps 10]
+"""
+import argparse
 import json
-import torch
+import os
+import sys
 
-F32, BF = torch.float32, torch.bfloat16
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-
-def t(fn, it=20):
-    for _ in range(3):
-        fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(); s.record()
-    for _ in range(it):
-        fn()
-    e.record(); torch.cuda.synchronize()
-    return round(s.elapsed_time(e) * 1e3 / it, 1)
+SHAPES = [  # name, M, N, K, out dtype
+    ("c5_gx_l1", 819200, 2048, 1024, "f32"), ("c5_gx_l0", 819200, 2048, 128, "f32"),
+    ("c5_F", 819200, 1024, 1024, "bf16"), ("c5_dx_l1", 819200, 1024, 2048, "f32"),
+    ("b256_gx", 102400, 1024, 128, "f32"), ("b256_F", 102400, 512, 512, "bf16"),
+    ("sq4096", 4096, 4096, 4096, "f32"), ("sq8192", 8192, 8192, 8192, "bf16"),
+]
 
 
-N, H, V = 25600, 256, 50000
-dl = (torch.randn(N, V, device="cuda") * 1e-3).to(BF)
-ob = torch.zeros(N, H + 8, device="cuda", dtype=BF)
-ob[:, :H] = torch.randn(N, H, device="cuda").to(BF)
-ob[:, H] = 1
-grad = torch.zeros((H + 1) * V, device="cuda")
-buf = torch.zeros(V, H + 8, device="cuda")
-buf2 = torch.zeros(H + 64, V, device="cuda")
-ob64 = torch.zeros(N, H + 64, device="cuda", dtype=BF)
-W = torch.randn(H, V, device="cuda").to(BF)
-bias = torch.randn(V, device="cuda").to(BF)
-lg = torch.empty(N, V, device="cuda", dtype=BF)
-r = {
-    "dW_M256": t(lambda: torch.mm(ob[:, :H].t(), dl, out_dtype=F32, out=grad[:H * V].view(H, V))),
-    "db_sum": t(lambda: grad[H * V:].copy_(dl.sum(0, dtype=F32))),
-    "dWb_M257": t(lambda: torch.mm(ob[:, :H + 1].t(), dl, out_dtype=F32, out=grad.view(H + 1, V))),
-    "dWbT_N264": t(lambda: torch.mm(dl.t(), ob, out_dtype=F32, out=buf)),
-    "dWbT_N264_plus_copy": t(lambda: (torch.mm(dl.t(), ob, out_dtype=F32, out=buf),
-                                      grad.view(H + 1, V).copy_(buf[:, :H + 1].t()))),
-    "dWb_M320": t(lambda: torch.mm(ob64.t(), dl, out_dtype=F32, out=buf2)),
-    "dX": t(lambda: torch.mm(dl, W.t(), out_dtype=F32)),
-    "logits_addmm_bf16": t(lambda: torch.addmm(bias, ob[:, :H], W, out=lg)),
-    "logits_mm_fp32": t(lambda: torch.mm(ob[:, :H], W, out_dtype=F32)),
-}
-print(json.dumps(r))
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    import torch
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    torch.manual_seed(0)
+    for name, M, N, K, od in SHAPES:
+        if a.only and a.only not in name:
+            continue
+        A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+        Bt = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+        out = torch.empty(M, N, device="cuda", dtype=torch.float32 if od == "f32" else torch.bfloat16)
+        res = {"shape": name, "M": M, "N": N, "K": K, "out": od}
+        runs = {"gemm_bt": lambda: k.gemm_bt(A, Bt, out, 0.0, None, None, None, 0, 0, 0),
+                "blt_mm": lambda: k.blt_mm(A, Bt, out, False, True, 0.0, None)}
+        ref = None
+        for tag, fn in runs.items():
+            fn()
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = out.float().clone() if M * N <= 1 << 26 else out[:4096].float().clone()
+            else:
+                cmp = out.float() if M * N <= 1 << 26 else out[:4096].float()
+                res["max_rel_diff"] = float((cmp - ref).abs().max() / ref.abs().max())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(a.reps):
+                    fn()
+            g.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            e1.synchronize()
+            us = e0.elapsed_time(e1) * 1000 / a.reps
+            res[f"{tag}_us"] = round(us, 1)
+            res[f"{tag}_TF"] = round(2.0 * M * N * K / us / 1e6, 1)
+        print(json.dumps(res), flush=True)
+        del A, Bt, out
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
