@@ -11,7 +11,7 @@ step gemmt python -u -m pytest tests/test_gpu_gemm.py -q -x --timeout 120 --time
 TL=8 step gemm python -u tools/gemm_micro.py &&
 T=900 step tier python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread &&
 step smoke python -u -c "import __graft_entry__ as g; g.smoke()" &&
-T=600 TL=1 step bench python -u bench.py
+T=600 TL=1 step bench python -u bench.py &&
 step trace rocprofv3 --kernel-trace -d $OUT/tr -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --decode-batches 0 --config5-steps 0 &&
 python scripts/kwin.py $OUT/tr/run_kernel_trace.csv 1 40 > $OUT/kwin_b256.txt &&
 python scripts/loop_tl.py $OUT/tr/run_kernel_trace.csv attn_bwd_rowp 60 30 > $OUT/tl_bwd.txt &&
