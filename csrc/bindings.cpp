@@ -517,7 +517,7 @@ void debug_clear() { tsamd_debug_clear(); }
 // then the embedding table) -- every operand row-contiguous with its own leading dimension
 bool gemm_bt_ok(int64_t M, int64_t N, int64_t K) { return gemm_bt_supported((int)M, (int)N, (int)K, N % 256 == 0 ? 256 : 128); }
 void gemm_bt(const Tensor& A, const Tensor& Bt, const Tensor& out, double beta, const OT& bias, const OT& ids,
-             const OT& rev, int64_t B, int64_t T, int64_t dir) {
+             const OT& rev, int64_t B, int64_t T, int64_t dir, const OT& xsf) {
   TORCH_CHECK(A.is_cuda() && A.dim() == 2 && A.scalar_type() == BF && A.stride(1) == 1, "gemm_bt: A [rows, K] bf16");
   TORCH_CHECK(Bt.is_cuda() && Bt.dim() == 2 && Bt.scalar_type() == BF && Bt.stride(1) == 1, "gemm_bt: Bt [N, K] bf16");
   TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.stride(1) == 1 && (out.scalar_type() == F32 || out.scalar_type() == BF),
@@ -537,11 +537,12 @@ void gemm_bt(const Tensor& A, const Tensor& Bt, const Tensor& out, double beta, 
     TORCH_CHECK(M == B * T && (dir == 0 || dir == 1), "gemm_bt: step frame needs M = T * B and dir 0 / 1");
     if (PO<int64_t>(ids)) { chk(*ids, at::kLong, "ids"); numel_eq(*ids, B * T, "ids"); }
     else TORCH_CHECK(A.size(0) == B * T, "gemm_bt: batch-frame A needs B * T rows");
+    chko(xsf, BF, M * K, "xsf");
   } else {
-    TORCH_CHECK(A.size(0) >= M && !PO<int64_t>(ids), "gemm_bt: plain A needs M rows");
+    TORCH_CHECK(A.size(0) >= M && !PO<int64_t>(ids) && !PO<bf16>(xsf), "gemm_bt: plain A needs M rows (no xsf)");
   }
   launch_gemm_bt(P<bf16>(A), A.stride(0), P<bf16>(Bt), Bt.stride(0), out.data_ptr(), out.stride(0), obf, beta != 0.0,
-                 PO<float>(bias), (int)M, (int)N, (int)K, frame ? 1 : 0, PO<int64_t>(ids), PO<int64_t>(rev), A.size(0),
+                 PO<float>(bias), (int)M, (int)N, (int)K, frame ? 1 : 0, PO<int64_t>(ids), PO<int64_t>(rev), PO<bf16>(xsf), A.size(0),
                  (int)B, (int)T, (int)dir, stream());
 }
 

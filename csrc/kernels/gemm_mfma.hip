@@ -10,7 +10,9 @@
 //            direction reversed within each length);  arow = ids ? ids[b][tt] (embedding table
 //            rows: layer 0 reads the token embeddings straight from the table) : b * T + tt
 //            (the layer below's batch-frame output) -- what to_step_frame wrote and the library
-//            GEMM re-read.
+//            GEMM re-read.  With xsf set the gathered rows are also stored there ([M][K], the
+//            step-frame copy the weight gradient reads later): the N-tile workgroups of an M tile
+//            each store an interleaved 1/ntn of its rows from the landed LDS stage.
 //
 // Geometry (cdna_hip_programming.md s5): 256 x BN x 64 tiles, 8 waves as 2 (M) x 4 (N), each wave
 // 128 x BN/4 of v_mfma_f32_16x16x32_bf16 accumulators.  Both operand tiles are staged global -> LDS
@@ -37,6 +39,7 @@ struct GemmP {
   const float* bias;
   const int64_t* ids;  // AMODE 1: token ids [B][T] (nullable)
   const int64_t* rev;  // AMODE 1: [B][T] reversed position of (b, t)
+  bf16* xsf;           // AMODE 1, nullable: the gathered A rows [M][K]
   long lda, ldb, ldc, nsrc;
   int M, N, K, B, T, dir;
 };
@@ -125,6 +128,15 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
     if (kt + 1 < nk) stage_load(s ^ 1, kt + 1);
     const char* As = smem + s * STAGE;
     const char* Bs = As + A_BYTES;
+    if (AMODE == 1 && p.xsf) {  // this workgroup's share of the landed A tile -> the step-frame copy
+      const int nrows = (BM - tn + ntn - 1) / ntn;
+      for (int pc = tid; pc < nrows * 8; pc += GM_THREADS) {
+        const int r = (pc >> 3) * ntn + tn, c = pc & 7, m = m0 + r;
+        if (m < p.M)
+          *reinterpret_cast<bf16x8*>(p.xsf + (size_t)m * p.K + kt * BK + c * 8) =
+              *reinterpret_cast<const bf16x8*>(As + r * (BK * 2) + ((c ^ (r & 7)) * 16));
+      }
+    }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       const int chunk = kb * 4 + fq;
@@ -198,8 +210,8 @@ size_t gemm_bt_lds(int BN) { return 2 * (size_t)(GM_BM * GM_BK * 2 + BN * GM_BK 
 
 void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, long ldc, bool out_bf16, bool beta,
                     const float* bias, int M, int N, int K, int amode, const int64_t* ids, const int64_t* rev,
-                    long nsrc, int B, int T, int dir, hipStream_t st) {
-  GemmP p{A, Bt, C, bias, ids, rev, lda, ldb, ldc, nsrc, M, N, K, B, T, dir};
+                    bf16* xsf, long nsrc, int B, int T, int dir, hipStream_t st) {
+  GemmP p{A, Bt, C, bias, ids, rev, xsf, lda, ldb, ldc, nsrc, M, N, K, B, T, dir};
   const int BN = N % 256 == 0 ? 256 : 128;
   const int grid = ((M + GM_BM - 1) / GM_BM) * (N / BN);
   const size_t lds = gemm_bt_lds(BN);

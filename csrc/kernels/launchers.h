@@ -199,4 +199,4 @@ void launch_tanh_tput(const float* in, float* out, int threads, int iters, int m
 bool gemm_bt_supported(int M, int N, int K, int BN);
 void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, long ldc, bool out_bf16, bool beta,
                     const float* bias, int M, int N, int K, int amode, const int64_t* ids, const int64_t* rev,
-                    long nsrc, int B, int T, int dir, hipStream_t st);
+                    bf16* xsf, long nsrc, int B, int T, int dir, hipStream_t st);

@@ -33,7 +33,7 @@ def test_gemm_bt_plain_matches_fp32(M, N, K, out_bf16, bias, beta):
     c0 = torch.randn(M, N, device="cuda", generator=g)
     out = c0.clone() if beta else torch.full((M, N), float("nan"), device="cuda",
                                              dtype=torch.bfloat16 if out_bf16 else torch.float32)
-    k.gemm_bt(A, Bt, out, 1.0 if beta else 0.0, b, None, None, 0, 0, 0)
+    k.gemm_bt(A, Bt, out, 1.0 if beta else 0.0, b, None, None, 0, 0, 0, None)
     torch.cuda.synchronize()
     ref = A.float() @ Bt.float().t() + (b if bias else 0) + (c0 if beta else 0)
     _close(out, ref, 1e-2 if out_bf16 else 2e-3)
@@ -59,10 +59,12 @@ def test_gemm_bt_step_frame_gather_matches_to_step_frame(ids, direction):
         tok = None
     W = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
     out = torch.full((T * B, N), float("nan"), device="cuda")
-    k.gemm_bt(src, W, out, 0.0, None, tok, rev, B, T, direction)
+    xsf = torch.full((T * B, K), float("nan"), device="cuda").bfloat16()
+    k.gemm_bt(src, W, out, 0.0, None, tok, rev, B, T, direction, xsf)
     torch.cuda.synchronize()
     tt = t[None, :].expand(B, T) if direction == 0 else rev
     rows = tok.gather(1, tt) if ids else torch.arange(B, device="cuda")[:, None] * T + tt
     A = src[rows.t().reshape(-1)]  # step frame: m = t * B + b
     ref = A.float() @ W.float().t()
     _close(out, ref)
+    assert torch.equal(xsf, A)  # the step-frame copy of the gathered rows (what to_step_frame wrote)

@@ -138,7 +138,7 @@ class DeviceBeamDecoder:
     # ------------------------------------------------------------------ per-chunk phases
     def _encode(self, batch):
         self.eng.set_batch(batch)
-        self.eng._encoder_forward()
+        self.eng._encoder_forward(need_grad=False)
         self._encode_copy()
 
     def _encode_launch(self, batch):
@@ -153,7 +153,7 @@ class DeviceBeamDecoder:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             self.eng.set_batch(batch)
-            self.eng._encoder_forward()
+            self.eng._encoder_forward(need_grad=False)
         self._enc_ev = torch.cuda.Event()
         self._enc_ev.record(s)
 

@@ -67,6 +67,78 @@ BLT_WGRAD = BLT and os.environ.get("TSAMD_BLT_WGRAD", "0") == "1"
 BLT_VDW = BLT and os.environ.get("TSAMD_BLT_VOCAB_DW", "0") == "1"
 
 
+# TSAMD_GEMM_BT: the hand-written MFMA GEMM (csrc/kernels/gemm_mfma.hip) for the activation GEMMs
+# whose weight operand has a [N][K] twin: "auto" (default) times it against blt_mm once per shape
+# on the first eager call (a row subset, scratch output) and keeps the faster -- hipBLASLt stays only
+# where the hand-written kernel measures slower; "1" always where eligible (deterministic mode
+# too: no timing-dependent choice); "0" never
+GEMM_BT = os.environ.get("TSAMD_GEMM_BT", "auto")
+_BT_PICK: Dict[tuple, bool] = {}
+_BT_TIMES: Dict[tuple, tuple] = {}
+# the step-frame gather path replaces to_step_frame + the GEMM: kept while the gather GEMM is at
+# most this much slower than the library GEMM alone (the layout pass it saves costs ~25-40 % of it)
+FRAME_SLACK = 1.25
+
+
+def _aligned(t: torch.Tensor) -> bool:
+    return t.stride(-1) == 1 and (t.dim() < 2 or t.stride(0) % 8 == 0) and t.data_ptr() % 16 == 0
+
+
+def _bt_ok(out, sa, ta, Bt, beta, bias) -> bool:
+    return (GEMM_BT != "0" and Bt is not None and not ta and Bt.dtype == BF and out.is_cuda and _aligned(sa)
+            and _aligned(Bt) and _aligned(out) and beta in (0.0, 1.0) and not (beta and out.dtype == BF)
+            and (bias is None or (bias.dtype == F32 and bias.is_contiguous()))
+            and bool(_ops().gemm_bt_ok(out.shape[0], out.shape[1], Bt.shape[1])) and sa.shape[1] == Bt.shape[1])
+
+
+def _deterministic() -> bool:
+    return os.environ.get("TSAMD_DETERMINISTIC", "0") not in ("", "0")
+
+
+def _time_us(fn, reps: int = 3) -> float:
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / reps
+
+
+def _bt_timed(out, sa, Bt, beta, bias, sb, tb):
+    """(gemm_bt us, blt_mm us) of this shape on a row subset (<= 131072 rows) into scratch."""
+    key = (tuple(out.shape), out.dtype, sa.shape[1], beta != 0.0, bias is not None, sa.stride(0), Bt.stride(0))
+    if key not in _BT_TIMES:
+        m = min(out.shape[0], 131072)
+        a, o = sa[:m], torch.empty(m, out.shape[1], dtype=out.dtype, device=out.device)
+        k = _ops()
+        t_bt = _time_us(lambda: k.gemm_bt(a, Bt, o, float(beta), bias, None, None, 0, 0, 0, None))
+        t_blt = _time_us(lambda: k.blt_mm(a, sb, o, False, tb, float(beta), bias))
+        _BT_TIMES[key] = (t_bt, t_blt)
+    return _BT_TIMES[key]
+
+
+def _use_bt(out, sa, ta, Bt, beta, bias, sb, tb, slack: float = 1.0) -> bool:
+    if not _bt_ok(out, sa, ta, Bt, beta, bias):
+        return False
+    if GEMM_BT == "1" or _deterministic():
+        return True
+    key = (tuple(out.shape), out.dtype, sa.shape[1], beta != 0.0, bias is not None, sa.stride(0), Bt.stride(0), slack)
+    if key not in _BT_PICK:
+        if torch.cuda.is_current_stream_capturing():
+            return False  # first seen inside a capture: no timing possible, keep the library GEMM
+        t_bt, t_blt = _bt_timed(out, sa, Bt, beta, bias, sb, tb)
+        _BT_PICK[key] = t_bt <= slack * t_blt
+    return _BT_PICK[key]
+
+
+def gemm_bt_stats() -> Dict[str, object]:
+    """Shapes seen by the hand-written-GEMM dispatch and the ones it took, with their timings."""
+    return {"shapes": len(_BT_PICK), "gemm_bt": int(sum(_BT_PICK.values())),
+            "timed_us": {f"{k[0][0]}x{k[0][1]}x{k[2]}": [round(v[0], 1), round(v[1], 1)] for k, v in _BT_TIMES.items()}}
+
+
 def _stored(x: torch.Tensor):
     """(row-contiguous tensor holding x's elements, whether x is its transpose)."""
     if x.stride(-1) == 1:
@@ -77,13 +149,19 @@ def _stored(x: torch.Tensor):
 
 
 def gemm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float = 0.0,
-         bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+         bias: Optional[torch.Tensor] = None, bt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = beta * out + a . b (+ bias[N]): bf16 operands, fp32 accumulate, fp32 or bf16 ``out``
     written in place (row slices of bigger buffers included).  Transposed views of stored
-    operands are passed as (storage, transpose flag), never copied."""
+    operands are passed as (storage, transpose flag), never copied.  ``bt``: a row-major [N][K]
+    twin of ``b`` (a packed weight layout) -- with it, or when ``b`` is itself the transpose of a
+    row-major [N][K] matrix, the hand-written MFMA GEMM is eligible (TSAMD_GEMM_BT)."""
     if BLT and out.is_cuda and a.dtype == BF and b.dtype == BF:
         sa, ta = _stored(a)
         sb, tb = _stored(b)
+        Bt = sb if tb else bt
+        if _use_bt(out, sa, ta, Bt, beta, bias, sb, tb):
+            _ops().gemm_bt(sa, Bt, out, float(beta), bias, None, None, 0, 0, 0, None)
+            return out
         _ops().blt_mm(sa, sb, out, ta, tb, float(beta), bias)
         return out
     if beta != 0.0:
@@ -100,10 +178,11 @@ def gemm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float = 0.0,
     return torch.addmm(bias.to(out.dtype), a, b, out=out)
 
 
-def mm_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None):
+def mm_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
+            bt: Optional[torch.Tensor] = None):
     """out = a . b (+ bias), fp32 accumulate, written straight into ``out`` (fp32 or bf16)
-    -- no temporary, no separate bias pass (hipBLASLt bias epilogue)."""
-    return gemm(out, a, b, 0.0, bias)
+    -- no temporary, no separate bias pass (GEMM bias epilogue)."""
+    return gemm(out, a, b, 0.0, bias, bt)
 
 
 def wgrad_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
@@ -542,9 +621,11 @@ class HipPointerGenerator:
                 Kd = p[enc_k(layer, d)]
                 pairs += [(pk[f"enc{layer}_Kx{di}"], Kd[:din]),
                           (pk[f"enc{layer}_Kxi{di}"].view(din, H, 4), Kd[:din].view(din, 4, H).permute(0, 2, 1)),
+                          (pk[f"enc{layer}_KxiT{di}"].view(H, 4, din), Kd[:din].view(din, 4, H).permute(2, 1, 0)),
                           (pk[f"enc{layer}_Wn"][di], Kd[din:]), (pk[f"enc{layer}_Wt"][di], Kd[din:].t()),
                           (f32[f"enc{layer}_b"][di], p[enc_b(layer, d)])]
-        pairs += [(pk["Wh"], p[WH].reshape(A, A)), (pk["RC"], p[RC]), (pk["RH"], p[RH]), (pk["RCt"], p[RC].t()),
+        pairs += [(pk["Wh"], p[WH].reshape(A, A)), (pk["WhT"], p[WH].reshape(A, A).t()), (pk["lin_embT"], M[:E].t()),
+                  (pk["RC"], p[RC]), (pk["RH"], p[RH]), (pk["RCt"], p[RC].t()),
                   (pk["RHt"], p[RH].t()), (pk["lin_emb"], M[:E]), (pk["Wic"], M[E:]), (pk["WicT"], M[E:].t()),
                   (pk["cell_x"], K[:E]), (pk["KcT"], K.t()), (pk["WcT2"][:, :A], W.t()), (pk["WcT2"][:, A:], K[E:].t()),
                   (pk["Wbig"][:E + H], K), (pk["Wbig"][E + H:], W), (pk["Ws"], p[ATT_M]), (pk["WsT"], p[ATT_M].t()),
@@ -601,16 +682,20 @@ class HipPointerGenerator:
                 # forward copy with gate-interleaved columns (u*4 + g): the x.W_x GEMM then
                 # writes gx as [T][B][H][4], one 16-byte load per (row, unit) in the recurrence
                 put(f"enc{layer}_Kxi{di}", K[:din].reshape(din, 4, self.H).transpose(1, 2).reshape(din, 4 * self.H))
+                # its [4H][din] twin: the "Bt" operand of the hand-written gather GEMM (gemm_mfma.hip)
+                put(f"enc{layer}_KxiT{di}", K[:din].reshape(din, 4, self.H).permute(2, 1, 0).reshape(4 * self.H, din))
             Kh = torch.stack([p[enc_k(layer, d)][din:] for d in ("fw", "bw")])  # [2][H][4H]
             put(f"enc{layer}_Wn", Kh)
             put(f"enc{layer}_Wt", Kh.transpose(1, 2))
         put("Wh", p[WH].reshape(A, A))
+        put("WhT", p[WH].reshape(A, A).t())
         put("RC", p[RC])
         put("RH", p[RH])
         put("RCt", p[RC].t())  # [H][2H]: "Bt" operand of the fused reduce_states forward
         put("RHt", p[RH].t())
         M = p[LIN_M]
         put("lin_emb", M[:E])
+        put("lin_embT", M[:E].t())
         put("Wic", M[E:])
         put("WicT", M[E:].t())
         K = p[CELL_K]
@@ -683,21 +768,42 @@ class HipPointerGenerator:
         self._in_i = i ^ 1
 
     # ------------------------------------------------------------------ forward
-    def _encoder_forward(self):
+    def _frame_gemm_bt(self, layer: int) -> bool:
+        """The input projection of encoder layer ``layer`` through the hand-written gather GEMM
+        (its A rows read through the step frame: no to_step_frame pass) -- by TSAMD_GEMM_BT, timed
+        once per shape against the library GEMM alone (``FRAME_SLACK``: the gather path also saves
+        the layout pass)."""
+        st = self.enc[layer]
+        din, TB, G = st["din"], self.T * self.B, 4 * self.H
+        Bt, xs = self.pk[f"enc{layer}_KxiT0"], st["x_sf"][0].view(TB, din)
+        return _use_bt(st["gx"][0].view(TB, G), xs, False, Bt, 0.0, None, self.pk[f"enc{layer}_Kxi0"], False,
+                       slack=FRAME_SLACK)
+
+    def _encoder_forward(self, need_grad: bool = True):
         k, w, B, T, H, A = self.k, self.w, self.B, self.T, self.H, self.A
         lens, rev = w["enc_lens"], w["rev_idx"]
         x = None
         for layer, st in enumerate(self.enc):
             din = st["din"]
             xs = st["x_sf"]
-            # step-frame inputs [2][T][B][din] (bw reversed within each length) in one gather
-            # launch: layer 0 straight from the embedding table by token id (frames.hip)
-            if x is None:
-                k.to_step_frame(self.pk["emb"], w["enc_batch"], rev, xs, B, T, din, 0)
+            if self._frame_gemm_bt(layer):
+                # x.W_x with the A rows gathered through the step frame inside the GEMM (layer 0
+                # straight from the embedding table by token id); the gathered rows are also
+                # stored to x_sf for the weight gradient (need_grad only)
+                src = self.pk["emb"] if x is None else x.view(B * T, din)
+                ids = w["enc_batch"] if x is None else None
+                for di in range(2):
+                    k.gemm_bt(src, self.pk[f"enc{layer}_KxiT{di}"], st["gx"][di].view(T * B, 4 * H), 0.0, None, ids,
+                              rev, B, T, di, xs[di].view(T * B, din) if need_grad else None)
             else:
-                k.to_step_frame(x, None, rev, xs, B, T, din, 0)
-            for di in range(2):  # x.W_x, bias added in the recurrence kernel
-                mm_into(st["gx"][di].view(T * B, 4 * H), xs[di].view(T * B, din), self.pk[f"enc{layer}_Kxi{di}"])
+                # step-frame inputs [2][T][B][din] (bw reversed within each length) in one gather
+                # launch: layer 0 straight from the embedding table by token id (frames.hip)
+                if x is None:
+                    k.to_step_frame(self.pk["emb"], w["enc_batch"], rev, xs, B, T, din, 0)
+                else:
+                    k.to_step_frame(x, None, rev, xs, B, T, din, 0)
+                for di in range(2):  # x.W_x, bias added in the recurrence kernel
+                    mm_into(st["gx"][di].view(T * B, 4 * H), xs[di].view(T * B, din), self.pk[f"enc{layer}_Kxi{di}"])
             st["hs"][:, 0].zero_()
             st["cs"][:, 0].zero_()
             st["out"].zero_()
@@ -715,9 +821,9 @@ class HipPointerGenerator:
         # state, one launch (reduce_states.hip) reading the encoder's final states in place
         k.rs_fwd(top["cs"], top["hs"], T, self.pk["RCt"], self.pk["RHt"], self.p[BRC], self.p[BRH], w["rs_pre"][0],
                  w["rs_pre"][1], w["Cst"][0], w["Cb"][0], w["Hb"][0], w["rs_cat"][0], w["rs_cat"][1], B, H)
-        mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["Wh"])
+        mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["Wh"], bt=self.pk["WhT"])
         if self.proj_attn:
-            mm_into(w["Genc"].view(B * T, self.E), top["out"].view(B * T, A), self.pk["Wic"])
+            mm_into(w["Genc"].view(B * T, self.E), top["out"].view(B * T, A), self.pk["Wic"], bt=self.pk["WicT"])
         if self.keep_ft:
             if w["Ft"] is None:
                 w["Ft"] = torch.empty(B, A, T, dtype=BF, device=self.dev)
@@ -729,8 +835,8 @@ class HipPointerGenerator:
         cov = hps.coverage
         emb_dec = self.pk["emb"][w["dec_batch_t"]].view(D * B, E)
         xe = w["xe"].view(D * B, E)
-        mm_into(xe, emb_dec, self.pk["lin_emb"], self.p[LIN_B])
-        mm_into(w["XG"].view(D * B, 4 * H), xe.to(BF), self.pk["cell_x"], self.p[CELL_B])
+        mm_into(xe, emb_dec, self.pk["lin_emb"], self.p[LIN_B], bt=self.pk["lin_embT"])
+        mm_into(w["XG"].view(D * B, 4 * H), xe.to(BF), self.pk["cell_x"], self.p[CELL_B], bt=self.pk["KcT"][:, :E])
         self._emb_dec = emb_dec
         enc_out, lens, Ft, F = self.enc[-1]["out"], w["enc_lens"], w["Ft"], w["F"]
         v, wc = self.f32["v"], self.f32["wc"]
@@ -809,8 +915,8 @@ class HipPointerGenerator:
         ctxb = w["CTXb"].view(N, A)
         # out = [h, ctx] . W_o + b: bias-epilogue GEMM, second GEMM accumulating (beta = 1)
         out = w["out_f32"]
-        gemm(out, Hn, self.pk["OUTm"][:H], 0.0, p[OUT_B])
-        gemm(out, ctxb, self.pk["OUTm"][H:], 1.0)
+        gemm(out, Hn, self.pk["OUTm"][:H], 0.0, p[OUT_B], bt=self.pk["OUTmT"][:, :H])
+        gemm(out, ctxb, self.pk["OUTm"][H:], 1.0, bt=self.pk["OUTmT"][:, H:])
         w["outb"].copy_(out)
         pg = None
         if hps.pointer_gen:
@@ -860,7 +966,7 @@ class HipPointerGenerator:
             cur.wait_stream(st)
 
     def forward(self, need_grad: bool = False):
-        self._encoder_forward()
+        self._encoder_forward(need_grad)
         self._decoder_forward()
         self._head_forward(need_grad)
         return self.losses()
@@ -1110,7 +1216,7 @@ class HipPointerGenerator:
             dctx = w["DCTX"][:D - 1].view((D - 1) * B, A)
             dxb = w["DXb"][1:].view((D - 1) * B, E)
             dxb.copy_(w["DX"][1:].view((D - 1) * B, E))
-            gemm(dctx, dxb, self.pk["WicT"], 1.0)
+            gemm(dctx, dxb, self.pk["WicT"], 1.0, bt=self.pk["Wic"])
         self._backward_mid_rest(Hn, wg, run)
 
     def _backward_mid_rest(self, Hn, wg, run):

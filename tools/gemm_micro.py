@@ -34,7 +34,7 @@ def main():
         Bt = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
         out = torch.empty(M, N, device="cuda", dtype=torch.float32 if od == "f32" else torch.bfloat16)
         res = {"shape": name, "M": M, "N": N, "K": K, "out": od}
-        runs = {"gemm_bt": lambda: k.gemm_bt(A, Bt, out, 0.0, None, None, None, 0, 0, 0),
+        runs = {"gemm_bt": lambda: k.gemm_bt(A, Bt, out, 0.0, None, None, None, 0, 0, 0, None),
                 "blt_mm": lambda: k.blt_mm(A, Bt, out, False, True, 0.0, None)}
         ref = None
         for tag, fn in runs.items():
