@@ -17,3 +17,7 @@ python scripts/kwin.py $OUT/tr/run_kernel_trace.csv 1 40 > $OUT/kwin_b256.txt &&
 python scripts/loop_tl.py $OUT/tr/run_kernel_trace.csv attn_bwd_rowp 60 30 > $OUT/tl_bwd.txt &&
 python scripts/loop_tl.py $OUT/tr/run_kernel_trace.csv attn_fwd_rowp 60 30 > $OUT/tl_fwd.txt &&
 rm -rf $OUT/tr && echo done
+for v in 1 0 1 0; do
+  TSAMD_VL_STORE=$v T=120 step vl$v rocprofv3 --kernel-trace --stats -d $OUT/v$v -o run --output-format csv -- python3 tools/vocab_micro.py || exit 1
+  python scripts/kstats.py $OUT/v$v/run_kernel_stats.csv 1 3 | sed -n 2,3p
+done
