@@ -20,9 +20,10 @@
 // solution ever runs with a workspace smaller than it reports needing (a null workspace under
 // capture faulted the GPU in round 4: profiles/r4/ab/blt_gemm.md).  Workspaces come from torch's
 // caching allocator (an allocation failure is torch.cuda.OutOfMemoryError, which `--batch auto`
-// steps down from) and are never freed: captured graphs keep their pointers.  At most
-// TSAMD_BLT_MAX_WS (16) streams get one; later streams run workspace-free solutions (the key
-// records which), so the footprint is bounded whatever the stream pool hands out.
+// steps down from) and are never freed: captured graphs keep their pointers.  The count is bounded
+// by torch's stream pool (32 streams per priority and device, recycled round-robin, so the same
+// handles come back); TSAMD_BLT_MAX_WS (72) caps it regardless, later streams then running only
+// workspace-free solutions (the key records which).
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
@@ -200,7 +201,7 @@ void blt_mm(const Tensor& a, const Tensor& b, const Tensor& out, bool ta, bool t
   auto wit = S.ws.find(s);
   if (wit != S.ws.end()) {
     ws = wit->second;
-  } else if (!cap && (int)S.ws.size() < env_int("TSAMD_BLT_MAX_WS", 16)) {
+  } else if (!cap && (int)S.ws.size() < env_int("TSAMD_BLT_MAX_WS", 72)) {
     ws = new_workspace(S, out);
     S.ws[s] = ws;
   } else if (cap && !S.spare.empty()) {

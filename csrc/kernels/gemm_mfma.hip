@@ -139,8 +139,10 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
     }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+      // every fragment of this 32-deep k block first (one LDS round trip), then its MFMAs at raised
+      // priority: the other wave of the SIMD issues its reads under them
       const int chunk = kb * 4 + fq;
-      bf16x8 bfrag[NI];
+      bf16x8 bfrag[NI], afrag[MI];
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int row = wc * WN + j * 16 + fr;
@@ -149,10 +151,14 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int row = wr * 128 + i * 16 + fr;
-        const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(As + row * (BK * 2) + ((chunk ^ (row & 7)) * 16));
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(afrag, bfrag[j], acc[i][j]);
+        afrag[i] = *reinterpret_cast<const bf16x8*>(As + row * (BK * 2) + ((chunk ^ (row & 7)) * 16));
       }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(afrag[i], bfrag[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -165,6 +171,7 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
   constexpr int RPP = 64 / LPR;          // rows per pass
   float bv[RUN];
   const int col = n0 + wc * WN + (lane % LPR) * RUN;
+  const bool full = m0 + BM <= p.M;
 #pragma unroll
   for (int e = 0; e < RUN; ++e) bv[e] = p.bias ? p.bias[col + e] : 0.f;
 #pragma unroll
@@ -177,24 +184,32 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) ep[(ii * 16 + fq * 4 + rr) * WN + j * 16 + fr] = acc[2 * slab + ii][j][rr];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's slab writes done (wave-private)
+    // all passes' row runs first (distinct registers: a store's data registers are not reused
+    // before it drains), then the stores; full tiles need no row guard
+    float4 v[32 / RPP];
+#pragma unroll
+    for (int pass = 0; pass < 32 / RPP; ++pass)
+      v[pass] = *reinterpret_cast<const float4*>(ep + (pass * RPP + lane / LPR) * WN + (lane % LPR) * RUN);
+    const int mb = m0 + wr * 128 + slab * 32 + lane / LPR;
+    if (BETA) {
+#pragma unroll
+      for (int pass = 0; pass < 32 / RPP; ++pass) {
+        const int m = min(mb + pass * RPP, p.M - 1);
+        const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.C) + (size_t)m * p.ldc + col);
+        v[pass].x += c.x; v[pass].y += c.y; v[pass].z += c.z; v[pass].w += c.w;
+      }
+    }
 #pragma unroll
     for (int pass = 0; pass < 32 / RPP; ++pass) {
-      const int lrow = pass * RPP + lane / LPR;
-      const int m = m0 + wr * 128 + slab * 32 + lrow;
-      const float4 v = *reinterpret_cast<const float4*>(ep + lrow * WN + (lane % LPR) * RUN);
-      float o[RUN] = {v.x + bv[0], v.y + bv[1], v.z + bv[2], v.w + bv[3]};
-      if (m < p.M) {
+      const int m = mb + pass * RPP;
+      if (full || m < p.M) {
+        const float o0 = v[pass].x + bv[0], o1 = v[pass].y + bv[1], o2 = v[pass].z + bv[2], o3 = v[pass].w + bv[3];
         if (OUT == 1) {
           typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          bf16x4 h{f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3])};
-          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.C) + (size_t)m * p.ldc + col) = h;
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.C) + (size_t)m * p.ldc + col) =
+              bf16x4{f2bf(o0), f2bf(o1), f2bf(o2), f2bf(o3)};
         } else {
-          float* dst = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + col;
-          if (BETA) {
-            const float4 c = *reinterpret_cast<const float4*>(dst);
-            o[0] += c.x; o[1] += c.y; o[2] += c.z; o[3] += c.w;
-          }
-          *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + col) = make_float4(o0, o1, o2, o3);
         }
       }
     }

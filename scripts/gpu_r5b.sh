@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 5: GEMM v2 micro + tests, the deterministic test, bench, timeline trace
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/${OUTD:-r5b}; mkdir -p $OUT
+export TMPDIR=/tmp
+step() { local n=$1; shift; echo "== $n"; timeout -k 10 ${T:-300} "$@" > $OUT/$n.log 2>&1; local rc=$?; tail -${TL:-3} $OUT/$n.log; return $rc; }
+step gemmt python -u -m pytest tests/test_gpu_gemm.py -q -x --timeout 120 --timeout-method thread &&
+TL=8 step gemm python -u tools/gemm_micro.py &&
+step det python -u -m pytest tests/test_gpu_production.py -q -x --timeout 300 --timeout-method thread -k "deterministic or oracle or held" &&
+T=600 TL=1 step bench python -u bench.py &&
+step trace rocprofv3 --kernel-trace -d $OUT/tr -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --decode-batches 0 --config5-steps 0 &&
+python scripts/kwin.py $OUT/tr/run_kernel_trace.csv 1 40 > $OUT/kwin_b256.txt &&
+python scripts/loop_tl.py $OUT/tr/run_kernel_trace.csv attn_bwd_rowp 60 30 > $OUT/tl_bwd.txt &&
+python scripts/loop_tl.py $OUT/tr/run_kernel_trace.csv attn_fwd_rowp 60 30 > $OUT/tl_fwd.txt &&
+rm -rf $OUT/tr && echo done
