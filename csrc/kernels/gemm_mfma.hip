@@ -171,7 +171,12 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
   constexpr int RPP = 64 / LPR;          // rows per pass
   float bv[RUN];
   const int col = n0 + wc * WN + (lane % LPR) * RUN;
-  const bool full = m0 + BM <= p.M;
+  constexpr int ES = OUT == 1 ? 2 : 4;  // output element bytes
+  // buffer resource over this workgroup's output rows [m0, min(M, m0 + BM)): stores past M drop
+  const long rows = min((long)BM, (long)p.M - m0);
+  const __amdgpu_buffer_rsrc_t crsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<char*>(p.C) + (size_t)m0 * p.ldc * ES, 0, (int)(rows * p.ldc * ES), 0x00020000);
+  const int voff = (int)(((size_t)(wr * 128 + lane / LPR) * p.ldc + col) * ES);
 #pragma unroll
   for (int e = 0; e < RUN; ++e) bv[e] = p.bias ? p.bias[col + e] : 0.f;
 #pragma unroll
@@ -184,33 +189,31 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) ep[(ii * 16 + fq * 4 + rr) * WN + j * 16 + fr] = acc[2 * slab + ii][j][rr];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's slab writes done (wave-private)
-    // all passes' row runs first (distinct registers: a store's data registers are not reused
-    // before it drains), then the stores; full tiles need no row guard
+    // all passes' row runs first, then buffer stores: one VGPR offset for every pass (the pass
+    // and slab offsets are SGPR soffsets), distinct data registers, and rows past M dropped by
+    // the resource's range check instead of branches
     float4 v[32 / RPP];
 #pragma unroll
     for (int pass = 0; pass < 32 / RPP; ++pass)
       v[pass] = *reinterpret_cast<const float4*>(ep + (pass * RPP + lane / LPR) * WN + (lane % LPR) * RUN);
-    const int mb = m0 + wr * 128 + slab * 32 + lane / LPR;
-    if (BETA) {
-#pragma unroll
-      for (int pass = 0; pass < 32 / RPP; ++pass) {
-        const int m = min(mb + pass * RPP, p.M - 1);
-        const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p.C) + (size_t)m * p.ldc + col);
-        v[pass].x += c.x; v[pass].y += c.y; v[pass].z += c.z; v[pass].w += c.w;
-      }
-    }
 #pragma unroll
     for (int pass = 0; pass < 32 / RPP; ++pass) {
-      const int m = mb + pass * RPP;
-      if (full || m < p.M) {
-        const float o0 = v[pass].x + bv[0], o1 = v[pass].y + bv[1], o2 = v[pass].z + bv[2], o3 = v[pass].w + bv[3];
-        if (OUT == 1) {
-          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.C) + (size_t)m * p.ldc + col) =
-              bf16x4{f2bf(o0), f2bf(o1), f2bf(o2), f2bf(o3)};
-        } else {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + col) = make_float4(o0, o1, o2, o3);
-        }
+      const int soff = (int)(((size_t)(slab * 32 + pass * RPP) * p.ldc) * ES);
+      if (BETA) {
+        const auto c = __builtin_amdgcn_raw_buffer_load_b128(crsrc, voff, soff, 0);
+        v[pass].x += __uint_as_float(c[0]); v[pass].y += __uint_as_float(c[1]);
+        v[pass].z += __uint_as_float(c[2]); v[pass].w += __uint_as_float(c[3]);
+      }
+      const float o0 = v[pass].x + bv[0], o1 = v[pass].y + bv[1], o2 = v[pass].z + bv[2], o3 = v[pass].w + bv[3];
+      if (OUT == 1) {
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+        const bf16x4 h{f2bf(o0), f2bf(o1), f2bf(o2), f2bf(o3)};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, h), crsrc, voff, soff, 0);
+      } else {
+        typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4v{__float_as_uint(o0), __float_as_uint(o1), __float_as_uint(o2), __float_as_uint(o3)}, crsrc, voff, soff, 0);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab read before the next slab's writes
