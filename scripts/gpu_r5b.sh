@@ -9,6 +9,7 @@ step() { local n=$1; shift; echo "== $n"; timeout -k 10 ${T:-300} "$@" > $OUT/$n
 step gemmt python -u -m pytest tests/test_gpu_gemm.py -q -x --timeout 120 --timeout-method thread || exit 1
 step dect python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_decode_parity.py -q -x --timeout 300 --timeout-method thread || exit 1
 TL=8 step gemm python -u tools/gemm_micro.py || exit 1
+TL=12 step wgrad python -u tools/wgrad_tn_micro.py || exit 1
 step det python -u -m pytest tests/test_gpu_production.py -q -x --timeout 300 --timeout-method thread -k "deterministic or oracle or held" || exit 1
 for v in 1 0; do
   TSAMD_VS_ART=$v T=120 step vs$v rocprofv3 --kernel-trace --stats -d $OUT/vs$v -o run --output-format csv -- python3 tools/vocab_micro.py || exit 1

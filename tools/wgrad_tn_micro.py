@@ -34,7 +34,10 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(0)
     shapes = [("out_proj_h", 25600, 256, 256), ("out_proj_ctx", 25600, 512, 256), ("cell_x", 25600, 128, 1024),
               ("cell_h", 25600, 256, 1024), ("lin_ctx", 25344, 512, 128), ("att_c", 25600, 256, 512),
-              ("W_h", 102400, 512, 512)]
+              ("W_h", 102400, 512, 512),
+              # encoder weight gradients x^T.dz / h^T.dz: B = 256 (K = T.B = 102400) and config #5 (819200)
+              ("enc_x_b256", 102400, 128, 1024), ("enc_h_b256", 102400, 256, 1024),
+              ("enc_x_l0_c5", 819200, 128, 2048), ("enc_x_l1_c5", 819200, 1024, 2048), ("enc_h_c5", 819200, 512, 2048)]
     for name, K, M, N in shapes:
         a = (torch.randn(K, M, device="cuda", generator=g) * 0.1).bfloat16()
         b = (torch.randn(K, N, device="cuda", generator=g) * 0.1).bfloat16()
