@@ -516,312 +516,6 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   }
 }
 
-// ------------------------------------------------------------------ article select (default)
-// The select kernel above spends most of its ~20 us in block barriers of a 1024-thread workgroup per
-// row (a dozen phases) and the cross-workgroup hand-off of its beam tail.  Here ONE WAVE handles a
-// row and the workgroup is one article's `beam` rows: every phase is a wave-level step (ballot /
-// mbcnt compaction, DPP / shuffle reductions, LDS broadcast rank counting) with no barrier, and the
-// article's beam bookkeeping runs right after one workgroup barrier -- no arrival counter, no
-// granule polling.  Same candidate logic and the same exact result as vocab_select_kernel:
-//   lse from the tile partials; the tiles at or above the minimum of K disjoint group maxima hold
-//   the plain top-K tiles; their logits at or above tau2 hold the plain top-K; plain top-K (copied
-//   words masked) + copied words at or above thr hold the final top-K of the pointer mixture.
-// Limits (else the block kernel): nt <= 64 VA_TPL tiles, K * tcols <= 64 VA_EPL, T <= 64 VA_PPL.
-#define VA_TPL 8
-#define VA_EPL 32
-#define VA_PPL 16
-#define VA_HASH 2048
-#define VA_CAND (64 * VA_EPL + 8)
-
-namespace {
-__device__ __forceinline__ void wsync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-__device__ __forceinline__ float wmax(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wmin(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ int mbcnt(unsigned long long m) {
-  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
-// minimum over the K groups {lanes j : j % K == g} of the group maxima of the lanes' values x: the
-// groups are disjoint, so it is <= the K-th largest value held (as in vocab_select_kernel)
-__device__ __forceinline__ float group_bound(float x, int K, float* tmp, int lane) {
-  tmp[lane] = x;
-  wsync();
-  float g = INFINITY;
-  if (lane < K) {
-    g = -INFINITY;
-    for (int j = lane; j < 64; j += K) g = fmaxf(g, tmp[j]);
-  }
-  wsync();
-  return wmin(g);
-}
-// append the entries with pred to (cv, ci) at n (wave-uniform), returns the new n
-__device__ __forceinline__ int wappend(bool pred, float v, int id, float* cv, int* ci, int n) {
-  const unsigned long long m = __ballot(pred);
-  if (pred) {
-    const int pos = n + mbcnt(m);
-    cv[pos] = v;
-    ci[pos] = id;
-  }
-  return n + __popcll(m);
-}
-// top-K of n entries of (cv, ci) by (value desc, id asc) into (ov, oi)[0..K) (pre-filled -inf/NONE)
-__device__ __forceinline__ void wrank(const float* cv, const int* ci, int n, int K, float* ov, int* oi, int lane) {
-  if (lane < 4) {  // pad to a multiple of 4 for the float4 reads
-    const_cast<float*>(cv)[n + lane] = -INFINITY;
-    const_cast<int*>(ci)[n + lane] = VS_NONE;
-  }
-  if (lane < VT_K) {
-    ov[lane] = -INFINITY;
-    oi[lane] = VS_NONE;
-  }
-  wsync();
-  const int n4 = (n + 3) & ~3;
-  for (int i = lane; i < n; i += 64) {
-    const float x = cv[i];
-    const int xi = ci[i];
-    int rank = 0;
-    for (int j = 0; j < n4; j += 4) {
-      const float4 a = *reinterpret_cast<const float4*>(cv + j);
-      const int4 b = *reinterpret_cast<const int4*>(ci + j);
-      rank += beats(a.x, b.x, x, xi) + beats(a.y, b.y, x, xi) + beats(a.z, b.z, x, xi) + beats(a.w, b.w, x, xi);
-    }
-    if (rank < K) {
-      ov[rank] = x;
-      oi[rank] = xi;
-    }
-  }
-  wsync();
-}
-}  // namespace
-
-__global__ __launch_bounds__(256) void vocab_select_art_kernel(
-    const float* __restrict__ logits, const float* __restrict__ part_ms, const float* __restrict__ pgen,
-    const float* __restrict__ attn, const int* __restrict__ ext, const int* __restrict__ lens,
-    int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam, int nt, int tcols, PgIn pgi,
-    BeamTail bt) {
-  extern __shared__ __attribute__((aligned(16))) char va_smem[];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int art = blockIdx.x, r = art * beam + w;
-  // per-wave LDS: candidates, copy-word hash, scratch
-  constexpr size_t WAVE_BYTES = 2 * VA_CAND * 4 + 2 * VA_HASH * 4 + 64 * 4 + 3 * 2 * VT_K * 4 + 16;
-  char* wb = va_smem + (size_t)w * WAVE_BYTES;
-  float* cv = reinterpret_cast<float*>(wb);
-  int* ci = reinterpret_cast<int*>(cv + VA_CAND);
-  int* hkey = ci + VA_CAND;
-  float* hmass = reinterpret_cast<float*>(hkey + VA_HASH);
-  float* tmp = hmass + VA_HASH;
-  float* pv0 = tmp + 64;
-  int* pi0 = reinterpret_cast<int*>(pv0 + VT_K);
-  float* pv1 = reinterpret_cast<float*>(pi0 + VT_K);
-  int* pi1 = reinterpret_cast<int*>(pv1 + VT_K);
-  float* pv2 = reinterpret_cast<float*>(pi1 + VT_K);
-  int* pi2 = reinterpret_cast<int*>(pv2 + VT_K);
-  // beam tail tables (after the waves' regions)
-  float* bt_cval = reinterpret_cast<float*>(va_smem + (size_t)beam * WAVE_BYTES);
-  int* bt_cid = reinterpret_cast<int*>(bt_cval + 64);
-  int* bt_srt = bt_cid + 64;
-  float* cand_lp = reinterpret_cast<float*>(bt_srt + 64);
-  int* cand_id = reinterpret_cast<int*>(cand_lp + 64);
-
-  const float* z = logits + (size_t)r * V;
-  const bool ptr = pgen || pgi.w;
-  // ---- round trip 1: tile partials, the p_gen inputs, copy ids and attention
-  float2 pm[VA_TPL];
-#pragma unroll
-  for (int u = 0; u < VA_TPL; ++u) {
-    const int q = lane + 64 * u;
-    pm[u] = q < nt ? *reinterpret_cast<const float2*>(part_ms + ((size_t)r * nt + q) * 2) : make_float2(-INFINITY, 0.f);
-  }
-  const int len = ptr ? (int)DCHECK_IDX(lens[art], 0, T + 1, CHK_LOSS_LEN) : 0;
-  int ew[VA_PPL];
-  float ea[VA_PPL];
-#pragma unroll
-  for (int u = 0; u < VA_PPL; ++u) {
-    const int i = lane + 64 * u;
-    ew[u] = i < len ? ext[(size_t)art * T + i] : -1;
-    ea[u] = i < len ? attn[(size_t)r * T + i] : 0.f;
-  }
-  float pg = pgen ? pgen[r] : 1.0f;
-  if (pgi.w) {
-    const int A = pgi.A, H = pgi.H;
-    float pgd = 0.f;
-    for (int i = lane; i < A + 2 * H + pgi.E; i += 64) {
-      const float x = i < A ? pgi.ctx[(size_t)r * A + i]
-                    : i < A + H ? pgi.c[(size_t)r * H + i - A]
-                    : i < A + 2 * H ? bf2f(pgi.h[(size_t)r * H + i - A - H])
-                    : pgi.x[(size_t)r * pgi.E + i - A - 2 * H];
-      pgd += x * pgi.w[i];
-    }
-    pg = fsigmoid(wave_sum(pgd) + pgi.b[0]);
-    if (lane == 0 && pgi.out) pgi.out[r] = pg;
-  }
-  // ---- copy mass per extended-vocab word (wave-private LDS hash)
-  for (int i = lane; i < VA_HASH; i += 64) {
-    hkey[i] = -1;
-    hmass[i] = 0.f;
-  }
-  wsync();
-#pragma unroll
-  for (int u = 0; u < VA_PPL; ++u) {
-    const int wd = ew[u];
-    if (wd < 0) continue;
-    int h = vhslot(wd);
-    for (int probe = 0; probe < VA_HASH; ++probe) {
-      const int prev = atomicCAS(&hkey[h], -1, wd);
-      if (prev == -1 || prev == wd) {
-        atomicAdd(&hmass[h], ea[u]);
-        break;
-      }
-      h = (h + 1) & (VA_HASH - 1);
-    }
-  }
-  // ---- log-sum-exp of the row from the tile partials
-  float m = -INFINITY;
-#pragma unroll
-  for (int u = 0; u < VA_TPL; ++u) m = fmaxf(m, pm[u].x);
-  const float M = wmax(m);
-  float sacc = 0.f;
-#pragma unroll
-  for (int u = 0; u < VA_TPL; ++u)
-    if (pm[u].x > -INFINITY) sacc += pm[u].y * fexp(pm[u].x - M);
-  const float lse = M + __logf(wave_sum(sacc));
-  // ---- the K best tiles (tile maxima at or above the group bound, then exact ranks)
-  const float gmin = group_bound(m, K, tmp, lane);
-  int n = 0;
-#pragma unroll
-  for (int u = 0; u < VA_TPL; ++u) {
-    const int q = lane + 64 * u;
-    n = wappend(q < nt && pm[u].x >= gmin, pm[u].x, q, cv, ci, n);
-  }
-  wrank(cv, ci, n, K, pv0, pi0, lane);
-  const float tau = pv0[K - 1];
-  // ---- round trip 2: the K tiles' logits and the copied words' logits
-  float zs[VA_EPL];
-  int cs[VA_EPL];
-#pragma unroll
-  for (int u = 0; u < VA_EPL; ++u) {
-    const int e = lane + 64 * u;
-    const int tq = e < K * tcols ? pi0[e / tcols] : VS_NONE;
-    cs[u] = tq < nt ? tq * tcols + (e % tcols) : V;
-    zs[u] = cs[u] < V ? z[cs[u]] : -INFINITY;
-  }
-  // distinct copied words -> this wave's lanes (word j at lane j % 64, slot j / 64), via the
-  // candidate buffer (free until the entries below are appended)
-  wsync();  // hash inserts complete
-  int nw = 0;
-  for (int i0 = 0; i0 < VA_HASH; i0 += 64) {
-    const int key = hkey[i0 + lane];
-    nw = wappend(key >= 0, hmass[i0 + lane], key, cv, ci, nw);
-  }
-  wsync();
-  int wk[VA_PPL];
-  float wm[VA_PPL], zk[VA_PPL];
-#pragma unroll
-  for (int u = 0; u < VA_PPL; ++u) {
-    const int j = lane + 64 * u;
-    wk[u] = j < nw ? ci[j] : -1;
-    wm[u] = j < nw ? cv[j] : 0.f;
-  }
-#pragma unroll
-  for (int u = 0; u < VA_PPL; ++u) zk[u] = (wk[u] >= 0 && wk[u] < V) ? z[wk[u]] : -INFINITY;
-  wsync();  // the word list is read: the candidate buffer is free
-  // ---- plain top-K: entries at or above max(tau, the entries' group bound)
-  float lmax = -INFINITY;
-#pragma unroll
-  for (int u = 0; u < VA_EPL; ++u) lmax = fmaxf(lmax, zs[u]);
-  const float tau2 = fmaxf(group_bound(lmax, K, tmp, lane), tau);
-  n = 0;
-#pragma unroll
-  for (int u = 0; u < VA_EPL; ++u) n = wappend(cs[u] < V && zs[u] >= tau2, zs[u], cs[u], cv, ci, n);
-  wrank(cv, ci, n, K, pv1, pi1, lane);
-  // ---- final candidates: plain top-K (copied words masked: their exact entry follows) U copied words
-  float theta = INFINITY;
-  if (lane < K) {
-    const int wd = pi1[lane];
-    bool incopy = false;
-    if (len > 0 && wd != VS_NONE) {
-      int h = vhslot(wd);
-      for (int probe = 0; probe < VA_HASH; ++probe) {
-        const int kk = hkey[h];
-        if (kk == -1) break;
-        if (kk == wd) { incopy = true; break; }
-        h = (h + 1) & (VA_HASH - 1);
-      }
-    }
-    const float plain = wd == VS_NONE ? -INFINITY : pg * fexp(pv1[lane] - lse);
-    theta = plain;
-    cv[lane] = incopy ? -INFINITY : plain;
-    ci[lane] = wd;
-  }
-  theta = wmin(theta);
-  float fin[VA_PPL];
-  float fmx = -INFINITY;
-#pragma unroll
-  for (int u = 0; u < VA_PPL; ++u) {
-    const float pvv = (wk[u] >= 0 && wk[u] < V) ? fexp(zk[u] - lse) : 0.f;
-    fin[u] = wk[u] < 0 ? -INFINITY : pg * pvv + (1.0f - pg) * wm[u];
-    if (fin[u] >= theta) fmx = fmaxf(fmx, fin[u]);
-  }
-  const float thr = fmaxf(group_bound(fmx, K, tmp, lane), theta);
-  n = K;
-#pragma unroll
-  for (int u = 0; u < VA_PPL; ++u) n = wappend(wk[u] >= 0 && fin[u] >= thr, fin[u], wk[u], cv, ci, n);
-  wrank(cv, ci, n, K, pv2, pi2, lane);
-  if (lane < K) {
-    out_ids[(size_t)r * K + lane] = pi2[lane];
-    out_lp[(size_t)r * K + lane] = __logf(pv2[lane]);
-  }
-  if (!bt.lp_sum) return;  // uniform over the grid
-  // ---- beam bookkeeping of the article (beam_common.h) after one workgroup barrier
-  if (lane == 0 && bt.pg_hist) {
-    const size_t th = (size_t)min(*bt.step - 1, bt.max_dec - 1);
-    bt.pg_hist[th * ((size_t)bt.Na * beam) + r] = pg;
-  }
-  if (lane < K) {
-    cand_id[w * K + lane] = pi2[lane];
-    cand_lp[w * K + lane] = __logf(pv2[lane]);
-  }
-  __syncthreads();
-  const int tid = threadIdx.x, base = art * beam;
-  const int t = *bt.step - 1;
-  const int is_done = bt.done[art], nres0 = bt.res_count[art];
-  float tot = -INFINITY;
-  int tid_cand = 0;
-  if (tid < beam * K) {
-    tot = bt.lp_sum[base + tid / K] + cand_lp[tid];
-    tid_cand = cand_id[tid];
-  }
-  if (bt.att_hist) {
-    const size_t th = (size_t)min(t, bt.max_dec - 1);
-    const size_t R = (size_t)bt.Na * beam;
-    for (int i = tid; i < beam * bt.T; i += blockDim.x)
-      bt.att_hist[(th * R + base) * bt.T + i] = bt.att[(size_t)base * bt.T + i];
-  }
-  if (is_done || t >= bt.max_dec) {
-    if (tid < beam) bt.gidx[base + tid] = base + tid;
-  } else {
-    beam_step_body(nullptr, nullptr, bt.lp_sum, bt.latest, bt.gidx, bt.tok_hist, bt.par_hist, bt.done, bt.res_count,
-                   bt.res_score, bt.res_len, bt.res_step, bt.res_par, bt_cval, bt_cid, bt_srt, art, tid, t, base,
-                   beam, K, bt.stop_id, bt.min_dec, tot, tid_cand, nres0, bt.Na);
-  }
-}
-
-static size_t va_lds(int beam) {
-  const size_t wave = 2 * VA_CAND * 4 + 2 * VA_HASH * 4 + 64 * 4 + 3 * 2 * VT_K * 4 + 16;
-  return beam * wave + 5 * 64 * 4;
-}
-
 int vocab_topk_tiles(int V, int H) { return (V + vt_cols(H) - 1) / vt_cols(H); }
 
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
@@ -847,17 +541,6 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
     const int RB = (R + VT_ROWS - 1) / VT_ROWS;
     hipLaunchKernelGGL((vocab_logits_kernel<2, 1, 512, true>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT,
                        bias, logits, part_ms, R, V, H);
-  }
-  // the article select (one wave per row, one workgroup per article) where its limits allow;
-  // TSAMD_VS_ART=0: the block-per-row kernel (A/B)
-  static const bool art_sel = !getenv("TSAMD_VS_ART") || atoi(getenv("TSAMD_VS_ART")) != 0;
-  const size_t lds = va_lds(beam);
-  if (art_sel && R % beam == 0 && beam * 64 <= 256 && K <= VT_K && nt <= 64 * VA_TPL && K * tcols <= 64 * VA_EPL &&
-      T <= 64 * VA_PPL && lds <= 160 * 1024) {
-    (void)hipFuncSetAttribute((const void*)vocab_select_art_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(vocab_select_art_kernel, dim3(R / beam), dim3(64 * beam), lds, st, logits, part_ms, pgen, attn,
-                       ext, lens, out_ids, out_lp, V, T, K, beam, nt, tcols, pgi, bt ? *bt : none);
-    return;
   }
   hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
                      out_lp, V, T, K, beam, nt, tcols, pgi, bt ? *bt : none);
