@@ -194,7 +194,7 @@ void attn_fwd_rowp(const Tensor& F, const Tensor& G, const Tensor& s, const Tens
 void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                    const Tensor& a, const OT& dx, const Tensor& gv, const OT& Ga, const OT& dcov_next, const OT& gcl,
                    const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out, int64_t B, int64_t T,
-                   int64_t A, const OT& dlen, int64_t step, int64_t parts) {
+                   int64_t A, const OT& dlen, int64_t step) {
   chk(G, BF, "G"); chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(gv, F32, "gv");
   chk(lens, I32, "lens"); chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
   const int64_t EG = gv.numel() / std::max<int64_t>(B, 1);
@@ -206,12 +206,9 @@ void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tens
   chko(dx, F32, B * EG, "dx"); chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(Ga, F32, B * T, "Ga");
   chko(dcov_next, F32, B * T, "dcov_next"); chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
   chko(dlen, I32, B, "dlen");
-  // parts > 1: ds is accumulated with atomics and must be zero on entry (dead rows store zeros)
-  TORCH_CHECK(parts == 1 || parts == 2 || parts == 4, "attn_bwd_rowp: parts 1, 2 or 4");
   launch_attn_bwd_rowp(P<bf16>(G), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
                        PO<float>(dx), P<float>(gv), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl), P<int>(lens),
-                       P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, PO<int>(dlen), (int)step, stream(),
-                       (int)parts);
+                       P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, PO<int>(dlen), (int)step, stream());
 }
 
 void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,

@@ -545,12 +545,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
 // backward: da_i = r_i + dx . G_i (r_i already holds the output-projection / p_gen part of
 // dctx . E_i), S = sum_j a_j r_j + dx . g_t; the rest as attn_bwd_row.  dx == nullptr:
 // last step.
-// parts > 1: the grid is parts x B workgroups, workgroup (part p, row b) takes the p-th contiguous
-// share of the row's 4-position groups (S needs no merge: every part sums the cheap a.r pre-loop
-// over all positions), so a row's latency is split over `parts` CUs -- the decoder steps late in a
-// batch have few live rows, and one CU per row left most of the chip idle there.  The parts' ds
-// contributions are added into the pre-zeroed ds with fp32 atomics: with 2 parts, 0 + x + y is
-// the same float in either order, so the result stays deterministic.
 template <int NK, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     const bf16* __restrict__ G, const bf16* __restrict__ F, const float* __restrict__ s,
@@ -558,19 +552,17 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     const float* __restrict__ a, const float* __restrict__ dx, const float* __restrict__ gv,
     const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
     const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
-    float* __restrict__ dcov_out, int T, const int* __restrict__ dlen, int step, int parts) {
+    float* __restrict__ dcov_out, int T, const int* __restrict__ dlen, int step) {
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float part[NW][A];
   __shared__ float red[NW];
   __shared__ f32x2 prm[3 * NK * 4 * 64];
-  const int nrow = gridDim.x / parts;
-  const int b = blockIdx.x % nrow, pp = blockIdx.x / nrow;
+  const int b = blockIdx.x;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int len = (int)DCHECK_IDX(lens[b], 1, T + 1, CHK_ATTN_LEN);
   const size_t rb = (size_t)b * T;
   if (dlen && step >= dlen[b]) {
     // past the row's last loss-weighted step every gradient is exactly zero (block-uniform exit)
-    if (pp != 0) return;
     for (int i = tid; i < T; i += NT) {
       de_out[rb + i] = 0.f;
       if (dcov_out) dcov_out[rb + i] = 0.f;
@@ -582,7 +574,6 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
   const bf16* Gb = G + (size_t)b * T * kEG + (lane & 15) * 8;
   const bf16* Fb = F + (size_t)b * T * A;
   const int ngrp = (len + 3) >> 2;
-  const int gbeg = pp * ngrp / parts, gend = (pp + 1) * ngrp / parts;  // this part's groups
   const int qm = lane >> 4;
   const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
   struct Scal {
@@ -602,7 +593,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     x.dn = dcov_next ? dcov_next[ix] : 0.f;
     x.r = (Ga ? Ga[ix] : 0.f) + x.dn + ((gcl && x.a <= x.c) ? g : 0.f);
   };
-  if (gbeg + wid < gend) load(gbeg + wid, fA, gA, xA);
+  if (wid < ngrp) load(wid, fA, gA, xA);
   f32x2 acc[NK][4];
 #pragma unroll
   for (int kb = 0; kb < NK; ++kb) {
@@ -687,21 +678,20 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
       }
     }
   };
-  for (int gi = gbeg + wid; gi < gend;) {
+  for (int gi = wid; gi < ngrp;) {
     const int g1 = gi + NW;
-    if (g1 < gend) load(g1, fB, gB, xB);
+    if (g1 < ngrp) load(g1, fB, gB, xB);
     compute(gi, fA, gA, xA);
-    if (g1 >= gend) break;
+    if (g1 >= ngrp) break;
     const int g2 = g1 + NW;
-    if (g2 < gend) load(g2, fA, gA, xA);
+    if (g2 < ngrp) load(g2, fA, gA, xA);
     compute(g1, fB, gB, xB);
     gi = g2;
   }
-  if (pp == 0)
-    for (int p = 4 * ngrp + tid; p < T; p += NT) {
-      de_out[rb + p] = 0.f;
-      if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
-    }
+  for (int p = 4 * ngrp + tid; p < T; p += NT) {
+    de_out[rb + p] = 0.f;
+    if (dcov_out) dcov_out[rb + p] = dcov_next ? dcov_next[rb + p] : 0.f;
+  }
 #pragma unroll
   for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
@@ -713,10 +703,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     float x = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) x += part[w][k];
-    if (parts == 1)
-      ds[(size_t)b * A + k] = 4.f * v[k] * x;
-    else
-      atomicAdd(ds + (size_t)b * A + k, 4.f * v[k] * x);
+    ds[(size_t)b * A + k] = 4.f * v[k] * x;
   }
 }
 
@@ -745,11 +732,10 @@ void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const fl
 void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st, int parts) {
+                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st) {
 #define LB(NK)                                                                                            \
-  hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, rowp_bwd_waves<NK>()>), dim3(B * parts),                  \
-                     dim3(rowp_bwd_waves<NK>() * 64), 0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, lens, \
-                     de_out, ds, dcov_out, T, dlen, step, parts)
+  hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, rowp_bwd_waves<NK>()>), dim3(B), dim3(rowp_bwd_waves<NK>() * 64), \
+                     0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, dlen, step)
   if (A == 512) LB(1);
   else LB(2);
 #undef LB

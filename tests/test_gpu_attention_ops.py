@@ -160,12 +160,10 @@ def test_attn_fwd_rowp_matches_fp32(A):
 
 @pytest.mark.parametrize("A", [512, 1024])
 @pytest.mark.parametrize("last", [False, True])
-@pytest.mark.parametrize("parts", [1, 2, 4])
-def test_attn_bwd_rowp_matches_fp32(A, last, parts):
+def test_attn_bwd_rowp_matches_fp32(A, last):
     """attn_bwd_rowp: the backward step with da_i = r_i + dx . G_i (dx = None: the last decoder
     step) against the fp32 reference, which is the E-form with dctx . E_i = dx . G_i when
-    G = E . W and dctx = W . dx.  parts > 1: each row's positions split over that many
-    workgroups, ds added into a zeroed buffer."""
+    G = E . W and dctx = W . dx."""
     k = ops()
     B, T, EG = 6, 300, 128
     gen = torch.Generator(device="cuda").manual_seed(91 + A)
@@ -185,8 +183,8 @@ def test_attn_bwd_rowp_matches_fp32(A, last, parts):
     Ga, dnext = r(B, T, s=0.1), r(B, T, s=0.1)
     g = torch.full((B,), 0.7, device=dev)
     de, dcov = torch.full((B, T), float("nan"), device=dev), torch.full((B, T), float("nan"), device=dev)
-    ds = torch.full((B, A), float("nan"), device=dev) if parts == 1 else torch.zeros(B, A, device=dev)
-    k.attn_bwd_rowp(G, F, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, None, 0, parts)
+    ds = torch.full((B, A), float("nan"), device=dev)
+    k.attn_bwd_rowp(G, F, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, None, 0)
     torch.cuda.synchronize()
     # the E-form reference with "E" = G and "dctx" = dx (zero at the last step)
     want = _reference(G, F, s, v, wc, cov, a, torch.zeros(B, EG, device=dev) if last else dx, Ga, dnext, g, lens)

@@ -16,7 +16,6 @@ engine is built); code can also pass a config explicitly.
 | TSAMD_PROJ_ATTN           | proj_attn          | 1: training row attention streams G = enc_out . W_in[E:] (emb_dim wide) instead of enc_out; 0: enc_out |
 | TSAMD_SKIP_PAD_STEPS      | skip_pad_steps     | 1: the projected-context attention kernels skip (row, step) pairs past the row's last loss-weighted decoder step; 0: compute them |
 | TSAMD_DEC_ROW_ATTN        | decode_row_attn    | 1: beam-decode attention through the row kernel; 0: score + softmax kernels |
-| TSAMD_ATTN_PARTS          | attn_parts         | 2: workgroups per row of the projected attention backward (the row's positions split over CUs, ds added with atomics); 1: one per row; 4 |
 | TSAMD_COMPACT_VOCAB_GRAD  | compact_vocab_grad | 1: with skip_pad_steps, the vocab-head dlogits of the live 32-row blocks are written compacted and the two gradient GEMMs run over those rows only (bucketed block counts); 0: every row |
 | TSAMD_DEFER_WGRAD         | defer_wgrad        | 1: decoder-side weight gradients beside the encoder BPTT (B >= 256); 0: inline |
 | TSAMD_DETERMINISTIC       | deterministic      | 0; 1: fixed-order reductions instead of fp32 atomics (bit-reproducible steps) |
@@ -51,7 +50,6 @@ class EngineConfig:
     skip_pad_steps: bool = True
     decode_row_attn: bool = True
     compact_vocab_grad: bool = True
-    attn_parts: int = 2
     defer_wgrad: bool = True
     deterministic: bool = False
 
@@ -69,7 +67,6 @@ class EngineConfig:
             skip_pad_steps=_flag(env, "TSAMD_SKIP_PAD_STEPS", True),
             decode_row_attn=_flag(env, "TSAMD_DEC_ROW_ATTN", True),
             compact_vocab_grad=_flag(env, "TSAMD_COMPACT_VOCAB_GRAD", True),
-            attn_parts=int(env.get("TSAMD_ATTN_PARTS", "2") or 2),
             defer_wgrad=_flag(env, "TSAMD_DEFER_WGRAD", True),
             deterministic=_flag(env, "TSAMD_DETERMINISTIC", False),
         )

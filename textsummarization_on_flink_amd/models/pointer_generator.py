@@ -497,9 +497,6 @@ class HipPointerGenerator:
         # (row, step) pairs past the row's last loss-weighted step are skipped by the projected
         # kernels (their outputs are written as zeros; loss and gradients are unchanged)
         self.skip_pad = self.proj_attn and cfg.skip_pad_steps
-        # workgroups per row of the projected attention backward (positions split over CUs); 2 at
-        # most in deterministic mode (two fp32 adds onto zero commute exactly)
-        self.attn_parts = max(1, min(cfg.attn_parts, 2 if cfg.deterministic else 4))
         self.compact_vocab = self.skip_pad and cfg.fused_vocab_train and cfg.compact_vocab_grad and not cfg.deterministic \
             and H in (128, 256, 512) and (D * B) % 32 == 0
         w["F"] = z(B, T, A, dt=BF)
@@ -1190,8 +1187,6 @@ class HipPointerGenerator:
             Ga.copy_(da.transpose(0, 1))
         w["dh_rec"].zero_()
         w["dc_carry"].zero_()
-        if self.attn_parts > 1:  # the position-split attention backward adds its parts into ds
-            w["DS"].zero_()
         dcov = w["dcov"]
         Kc = self.pk["Wbig"][:E + H]  # W_cell: [dx | dh] = dz . W_cell^T
         dlen = w["dlen"] if self.skip_pad else None
@@ -1208,7 +1203,7 @@ class HipPointerGenerator:
                                 w["ATT"][t][rs], w["DX"][t + 1][rs] if nxt else None, w["GV"][t][rs],
                                 Ga[t][rs], dcov[(t + 1) % 2][rs] if (cov and nxt) else None,
                                 w["gcl"][t][rs] if cov else None, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
-                                dcov[t % 2][rs] if cov else None, Bg, T, A, dl, t, self.attn_parts)
+                                dcov[t % 2][rs] if cov else None, Bg, T, A, dl, t)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
                                w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, dl, t)
