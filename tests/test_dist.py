@@ -222,8 +222,8 @@ def test_lstm_error_on_one_rank_skips_the_step_on_all_ranks():
         assert not finite and g0 == 2.0 and healthy_finite
 
 
-@pytest.mark.parametrize("defer,vdw", [(True, False), (False, False), (True, True)])
-def test_bucket_issue_order_leaves_only_the_embedding(defer, vdw):
+@pytest.mark.parametrize("defer", [True, False])
+def test_bucket_issue_order_leaves_only_the_embedding(defer):
     """GraphTrainer's replay order (train/trainer.py replay_phases / issue_plan) with a recording
     reducer over the real flat-gradient layout of the bench model: every bucket except the
     embedding's is issued before the last phase graph is queued, so at most the 25.6 MB embedding
@@ -263,12 +263,10 @@ def test_bucket_issue_order_leaves_only_the_embedding(defer, vdw):
         def wait_issued(self):
             events.append(("wait",))
 
-    replay_phases([G(i) for i in range(4)], Rec(), issue_plan(defer, vdw), BPTT_PHASE, lstm_exclusive=True)
+    replay_phases([G(i) for i in range(4)], Rec(), issue_plan(defer), BPTT_PHASE, lstm_exclusive=True)
     issued_before_last = {e[1] for e in events[:events.index(("graph", 3))] if e[0] == "bucket"}
     assert issued_before_last == {0, 1, 2}
-    # bucket 0 (output projection) right after the phase that completes it: the head graph, or the
-    # decoder-backward graph when the vocab dW runs beside the decoder backward loop
-    assert events.index(("bucket", 0)) == events.index(("graph", 1 if vdw else 0)) + 1
+    assert events.index(("bucket", 0)) == events.index(("graph", 0)) + 1
     assert events.index(("wait",)) == events.index(("graph", BPTT_PHASE)) - 1  # no RCCL beside the full-grid BPTT
     if defer:
         assert events.index(("bucket", 1)) == events.index(("graph", 2)) + 1

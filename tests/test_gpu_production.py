@@ -221,42 +221,6 @@ def test_row_split_streams_match_single_chain(monkeypatch, split):
     assert _rel(got[1][2], got[0][2]) < 1e-4
 
 
-def test_vocab_dw_beside_the_decoder_loop_matches(monkeypatch):
-    """TSAMD_VDW_LOOP: the vocab dW through wgrad_tn on a side stream beside the decoder backward
-    loop gives the gradients of the head-phase split-K GEMM (eager and through the phase graphs)."""
-    from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
-    from textsummarization_on_flink_amd.utils.graphs import capture_guard
-    B = 256
-    hps = _hps(B, trunc_norm_init_std=0.05).replace(max_dec_steps=24)
-    vocab, (batch,) = _batches(hps, 1, seed=19)
-    got = []
-    for on in ("0", "1"):
-        monkeypatch.setenv("TSAMD_VDW_LOOP", on)
-        params = build_params(hps, vocab.size(), device="cuda", seed=8).enable_grad()
-        eng = HipPointerGenerator(hps, vocab.size(), params, B=B, T=T, D=24)
-        assert eng.vdw_loop == (on == "1")
-        eng.set_batch(batch)
-        eng.forward(need_grad=True)
-        eng.backward()
-        torch.cuda.synchronize()
-        eager = params.grad.clone()
-        g = [torch.cuda.CUDAGraph() for _ in range(3)]
-        with capture_guard():
-            with torch.cuda.graph(g[0]):
-                eng.forward(need_grad=True)
-                eng.backward_head()
-            with torch.cuda.graph(g[1]):
-                eng.backward_mid()
-            with torch.cuda.graph(g[2]):
-                eng.backward_tail()
-        for x in g:
-            x.replay()
-        torch.cuda.synchronize()
-        got.append((eager, params.grad.clone()))
-    for a, b in ((got[0][0], got[1][0]), (got[0][0], got[1][1])):
-        assert _rel(b, a) < 1e-5, _rel(b, a)
-
-
 def test_deferred_weight_gradients_match_inline(monkeypatch):
     """The decoder-side weight gradients deferred onto a side stream beside the encoder BPTT
     (TSAMD_DEFER_WGRAD, default on) give

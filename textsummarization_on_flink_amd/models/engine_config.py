@@ -17,7 +17,6 @@ engine is built); code can also pass a config explicitly.
 | TSAMD_SKIP_PAD_STEPS      | skip_pad_steps     | 1: the projected-context attention kernels skip (row, step) pairs past the row's last loss-weighted decoder step; 0: compute them |
 | TSAMD_DEC_ROW_ATTN        | decode_row_attn    | 1: beam-decode attention through the row kernel; 0: score + softmax kernels |
 | TSAMD_COMPACT_VOCAB_GRAD  | compact_vocab_grad | 1: with skip_pad_steps, the vocab-head dlogits of the live 32-row blocks are written compacted and the two gradient GEMMs run over those rows only (bucketed block counts); 0: every row |
-| TSAMD_VDW_LOOP            | vdw_loop           | 0: vocab dW in the head phase (split-K batched GEMM); 1: through wgrad_tn on a side stream beside the decoder backward loop |
 | TSAMD_DEFER_WGRAD         | defer_wgrad        | 1: decoder-side weight gradients beside the encoder BPTT (B >= 256); 0: inline |
 | TSAMD_DETERMINISTIC       | deterministic      | 0; 1: fixed-order reductions instead of fp32 atomics (bit-reproducible steps) |
 | TSAMD_KERNEL_DEBUG        | (ops loader)       | 0; 1: the bounds-checked kernel library ``_C_debug.so`` |
@@ -52,7 +51,6 @@ class EngineConfig:
     decode_row_attn: bool = True
     compact_vocab_grad: bool = True
     defer_wgrad: bool = True
-    vdw_loop: bool = False
     deterministic: bool = False
 
     @classmethod
@@ -70,7 +68,6 @@ class EngineConfig:
             decode_row_attn=_flag(env, "TSAMD_DEC_ROW_ATTN", True),
             compact_vocab_grad=_flag(env, "TSAMD_COMPACT_VOCAB_GRAD", True),
             defer_wgrad=_flag(env, "TSAMD_DEFER_WGRAD", True),
-            vdw_loop=_flag(env, "TSAMD_VDW_LOOP", False),
             deterministic=_flag(env, "TSAMD_DETERMINISTIC", False),
         )
         return replace(cfg, **overrides) if overrides else cfg

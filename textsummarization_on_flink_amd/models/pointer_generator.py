@@ -470,14 +470,6 @@ class HipPointerGenerator:
             not self.persistent_lstm or
             int(self.k.lstm_persistent_grid(H, B)) <= int(self.k.lstm_persistent_capacity(H)) - 64))
         self._late_stream = torch.cuda.Stream(self.dev) if self.defer_wgrad else None
-        # vocab dW = X^T . dlogits beside the decoder backward loop (cfg.vdw_loop): the loop is
-        # latency-bound and leaves most of the chip idle; the GEMM goes through wgrad_tn (custom,
-        # no inter-workgroup waits: safe beside the loop's kernels and library GEMMs), so bucket 0
-        # (output projection) completes with phase 1 instead of phase 0.  Not in deterministic mode
-        # (fp32 atomics).
-        self.vdw_loop = bool(cfg.vdw_loop and not self.det and H % 128 == 0)
-        self._vdw = None
-        self._vdw_stream = torch.cuda.Stream(self.dev) if self.vdw_loop else None
         # reduce_states: pre-activations [c; h], bf16 [fw, bw] inputs and bf16 dp (wgrad operands)
         w["rs_pre"] = z(2, B, H)
         w["rs_cat"] = z(2, B, 2 * H, dt=BF)
@@ -1071,14 +1063,6 @@ class HipPointerGenerator:
         dlc = dl[:M]
         g(OV).copy_(w["dbias"])
         dst = g(OW)
-        if self.vdw_loop:  # launched beside the decoder backward loop (backward_mid)
-            self._vdw = lambda: self.k.wgrad_tn(xc[:, :H], dlc, dst)
-            dxc = mmf(dlc, self.pk["ow"].t())  # [M, H]
-            de = self._dout_ext
-            de.zero_()
-            de.index_copy_(0, idx, dxc.view(nbk, 32, H))
-            self._dout = de[:nb].view(nb * 32, H)[:N]
-            return
         Sw = 4 if not BLT_VDW and M % 4 == 0 and (M // 4) * V < 2 ** 31 else 1
         if Sw > 1:  # split K = M in 4 (one batched GEMM + a sum), as the full head
             parts = torch.bmm(xc.view(Sw, M // Sw, H + 8)[:, :, :H].transpose(1, 2), dlc.view(Sw, M // Sw, V),
@@ -1112,11 +1096,6 @@ class HipPointerGenerator:
         g = p.g
         cov = hps.coverage
         dout = self._dout
-        vdw, self._vdw = self._vdw, None
-        if vdw is not None:  # vocab dW beside this phase (joined at its end)
-            self._vdw_stream.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self._vdw_stream):
-                vdw()
         # ---- output projection [h, ctx]
         Hn = w["Hb"][1:].reshape(N, H)
         ctxb = w["CTXb"].view(N, A)
@@ -1292,8 +1271,6 @@ class HipPointerGenerator:
         dE2 = dE.view(B * T, A)
         gemm(dE2, dFb, self.pk["Wh"].t(), 1.0)
         self._dE = dE
-        if self._vdw_stream is not None:  # the vocab dW launched beside this phase
-            torch.cuda.current_stream().wait_stream(self._vdw_stream)
 
     def backward_tail_enc(self):
         """reduce_states, encoder BPTT and weight gradients; joins the deferred decoder weight

@@ -59,14 +59,11 @@ def check_lstm_err(engine) -> None:
 BPTT_PHASE = 2
 
 
-def issue_plan(defer_wgrad: bool, vdw_loop: bool = False):
+def issue_plan(defer_wgrad: bool):
     """Buckets whose all-reduce is issued after each phase graph (the last bucket, the embedding,
     is issued by the reducer call after the last graph).  With the decoder weight gradients
-    deferred beside the encoder BPTT, bucket 1 completes with phase 2; with the vocab dW beside the
-    decoder backward loop, bucket 0 completes with phase 1."""
-    p0 = [] if vdw_loop else [0]
-    p1 = ([0] if vdw_loop else []) + ([] if defer_wgrad else [1])
-    return [p0, p1, [1, 2] if defer_wgrad else [2], []]
+    deferred beside the encoder BPTT, bucket 1 completes with phase 2."""
+    return [[0], [] if defer_wgrad else [1], [1, 2] if defer_wgrad else [2], []]
 
 
 def replay_phases(graphs, reducer, plan, bptt_phase: int, lstm_exclusive: bool, ev=None):
@@ -210,7 +207,7 @@ class GraphTrainer:
             if ev:
                 ev[0].record()
             ng = len(self.g_fb)
-            replay_phases(self.g_fb, self.reducer, issue_plan(self.engine.defer_wgrad, self.engine.vdw_loop), BPTT_PHASE,
+            replay_phases(self.g_fb, self.reducer, issue_plan(self.engine.defer_wgrad), BPTT_PHASE,
                           self.lstm_exclusive, ev)
             self._maybe_poison()
             self.reducer()
