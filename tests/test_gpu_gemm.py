@@ -31,12 +31,19 @@ def test_gemm_bt_plain_matches_fp32(M, N, K, out_bf16, bias, beta):
     Bt = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).bfloat16()
     b = torch.randn(N, device="cuda", generator=g) if bias else None
     c0 = torch.randn(M, N, device="cuda", generator=g)
-    out = c0.clone() if beta else torch.full((M, N), float("nan"), device="cuda",
-                                             dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    # the output is the head of a taller buffer: the rows after M must keep their sentinel (the
+    # epilogue's row-range guard covers every store of a partial row tile)
+    full = torch.full((M + 256, N), 12345.0, device="cuda", dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    out = full[:M]
+    if beta:
+        out.copy_(c0)
+    else:
+        out.fill_(float("nan"))
     k.gemm_bt(A, Bt, out, 1.0 if beta else 0.0, b, None, None, 0, 0, 0, None)
     torch.cuda.synchronize()
     ref = A.float() @ Bt.float().t() + (b if bias else 0) + (c0 if beta else 0)
     _close(out, ref, 1e-2 if out_bf16 else 2e-3)
+    assert bool((full[M:] == 12345.0).all())
 
 
 @pytest.mark.parametrize("ids", [True, False])
