@@ -546,6 +546,30 @@ void gemm_bt(const Tensor& A, const Tensor& Bt, const Tensor& out, double beta, 
                  (int)B, (int)T, (int)dir, stream());
 }
 
+// AMODE 2 (gemm_mfma.hip): out[m] = [dz[0] row | dz[1] row] . Bt^T, the rows of each k-half read at
+// step t or rev[b][t] (mode bits 0 / 1), m = t * B + b or b * T + t (mode bit 2)
+void gemm_bt_merge(const Tensor& dz, const Tensor& Bt, const Tensor& out, const Tensor& rev, int64_t B, int64_t T,
+                   int64_t mode) {
+  TORCH_CHECK(dz.is_cuda() && dz.scalar_type() == BF && dz.is_contiguous() && dz.numel() % (2 * B * T) == 0,
+              "gemm_bt_merge: dz [2][T][B][Kh] bf16, contiguous");
+  const int64_t Kh = dz.numel() / (2 * B * T);
+  TORCH_CHECK(Bt.is_cuda() && Bt.dim() == 2 && Bt.scalar_type() == BF && Bt.stride(1) == 1 && Bt.size(1) == 2 * Kh,
+              "gemm_bt_merge: Bt [N, 2 Kh] bf16");
+  chk(out, F32, "out");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == B * T && out.size(1) == Bt.size(0) && out.stride(1) == 1,
+              "gemm_bt_merge: out [T * B, N] fp32");
+  chk(rev, at::kLong, "rev");
+  numel_eq(rev, B * T, "rev");
+  TORCH_CHECK(mode >= 0 && mode <= 7, "gemm_bt_merge: mode bits 0-2");
+  const int64_t M = B * T, N = Bt.size(0), K = 2 * Kh;
+  TORCH_CHECK(Kh % 64 == 0 && gemm_bt_ok(M, N, K), "gemm_bt_merge: Kh % 64 == 0 and N % 128 == 0");
+  TORCH_CHECK(Bt.stride(0) % 8 == 0 && out.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(dz.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(Bt.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "gemm_bt_merge: 16-byte aligned rows");
+  launch_gemm_bt(P<bf16>(dz), Kh, P<bf16>(Bt), Bt.stride(0), out.data_ptr(), out.stride(0), false, false, nullptr,
+                 (int)M, (int)N, (int)K, 2, nullptr, P<int64_t>(rev), nullptr, 0, (int)B, (int)T, (int)mode, stream());
+}
+
 // ---------------------------------------------------------------- probes (probes.hip)
 int64_t cu_hold_max_lds_op() { return cu_hold_max_lds(); }
 void cu_hold(const Tensor& times, int64_t grid, double ms, int64_t lds_bytes) {
@@ -986,6 +1010,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("debug_clear", &debug_clear);
   m.def("gemm_bt_ok", &gemm_bt_ok);
   m.def("gemm_bt", &gemm_bt);
+  m.def("gemm_bt_merge", &gemm_bt_merge);
   m.def("cu_hold_max_lds", &cu_hold_max_lds_op);
   m.def("cu_hold", &cu_hold);
   m.def("tanh_eval", &tanh_eval);

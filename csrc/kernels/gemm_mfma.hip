@@ -13,6 +13,11 @@
 //            GEMM re-read.  With xsf set the gathered rows are also stored there ([M][K], the
 //            step-frame copy the weight gradient reads later): the N-tile workgroups of an M tile
 //            each store an interleaved 1/ntn of its rows from the landed LDS stage.
+//   AMODE 2  two-direction merge (the encoder input-gradient GEMM): K = 2 Kh, A = the BPTT's dz
+//            [2][T][B][Kh] (step frame); output row m = (t, b) -- step frame t * B + b, or batch
+//            frame b * T + t with dir bit 2 -- and k-half h reads dz[h] at step t, or at rev[b][t]
+//            with dir bit h.  One GEMM over [dz_fw | dz_bw] . [Kx_fw ; Kx_bw] replaces the two
+//            per-direction GEMMs and the from_step_frame / step_frame_hop pass that added them.
 //
 // Geometry (cdna_hip_programming.md s5): 256 x BN x 64 tiles, 8 waves as 2 (M) x 4 (N), each wave
 // 128 x BN/4 of v_mfma_f32_16x16x32_bf16 accumulators.  Both operand tiles are staged global -> LDS
@@ -52,6 +57,20 @@ __device__ __forceinline__ const bf16* a_row(const GemmP& p, int m, int AMODE) {
   const int tt = p.dir == 0 ? t : (int)DCHECK_IDX(p.rev[(size_t)b * p.T + t], 0, p.T, CHK_FRAME_REV);
   const long src = p.ids ? DCHECK_IDX(p.ids[(size_t)b * p.T + tt], 0, p.nsrc, CHK_FRAME_ID) : (long)b * p.T + tt;
   return p.A + (size_t)src * p.lda;
+}
+
+__device__ __forceinline__ const bf16* a_row2(const GemmP& p, int m, int h) {
+  m = min(m, p.M - 1);
+  int t, b;
+  if (p.dir & 4) {
+    b = m / p.T;
+    t = m - b * p.T;
+  } else {
+    t = m / p.B;
+    b = m - t * p.B;
+  }
+  const int tt = (p.dir >> h) & 1 ? (int)DCHECK_IDX(p.rev[(size_t)b * p.T + t], 0, p.T, CHK_FRAME_REV) : t;
+  return p.A + (((size_t)h * p.T + tt) * p.B + b) * p.lda;
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -150,11 +169,18 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
   // loads row (piece row0 + l / 8), k-chunk (l % 8) ^ (row & 7) of the current K tile
   const int lr = lane >> 3, lc = lane & 7;
   const bf16* asrc[A_PER_WAVE];
+  const bf16* asrc1[AMODE == 2 ? A_PER_WAVE : 1];  // AMODE 2: the second k-half's rows
 #pragma unroll
   for (int i = 0; i < A_PER_WAVE; ++i) {
     const int row = (wid * A_PER_WAVE + i) * 8 + lr;
-    asrc[i] = a_row(p, m0 + row, AMODE) + ((lc ^ (row & 7)) * 8);
+    if constexpr (AMODE == 2) {
+      asrc[i] = a_row2(p, m0 + row, 0) + ((lc ^ (row & 7)) * 8);
+      asrc1[i] = a_row2(p, m0 + row, 1) + ((lc ^ (row & 7)) * 8);
+    } else {
+      asrc[i] = a_row(p, m0 + row, AMODE) + ((lc ^ (row & 7)) * 8);
+    }
   }
+  const int nkh = p.K / (2 * BK);  // AMODE 2: k tiles per half
   const bf16* bsrc[B_PER_WAVE];
 #pragma unroll
   for (int i = 0; i < B_PER_WAVE; ++i) {
@@ -164,9 +190,11 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
   auto stage_load = [&](int s, int kt) {
     char* base = smem + s * STAGE;
 #pragma unroll
-    for (int i = 0; i < A_PER_WAVE; ++i)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[i] + kt * BK),
-                                       (lds_ptr_t)(base + ((wid * A_PER_WAVE + i) * 8) * (BK * 2)), 16, 0, 0);
+    for (int i = 0; i < A_PER_WAVE; ++i) {
+      const bf16* src = (AMODE == 2 && kt >= nkh) ? asrc1[AMODE == 2 ? i : 0] + (kt - nkh) * BK : asrc[i] + kt * BK;
+      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(base + ((wid * A_PER_WAVE + i) * 8) * (BK * 2)), 16, 0,
+                                       0);
+    }
 #pragma unroll
     for (int i = 0; i < B_PER_WAVE; ++i)
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[i] + kt * BK),
@@ -351,6 +379,11 @@ void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, 
   else GL(AM, BNN, 0, false);
   // TSAMD_GEMM_V=4: the 4-stage BK = 32 pipeline (no step-frame copy-out yet: xsf calls stay on v3)
   static const int ver = getenv("TSAMD_GEMM_V") ? atoi(getenv("TSAMD_GEMM_V")) : 3;
+  if (amode == 2) {  // merge: fp32 out, no beta
+    if (BN == 256) GL(2, 256, 0, false);
+    else GL(2, 128, 0, false);
+    return;
+  }
   if (ver == 4 && !xsf) {
     const size_t lds4 = 4 * (size_t)(GM_BM * 64 + BN * 64);
 #define GL4(AM, BNN, O, BE)                                                                                   \

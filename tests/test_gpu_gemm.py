@@ -75,3 +75,32 @@ def test_gemm_bt_step_frame_gather_matches_to_step_frame(ids, direction):
     ref = A.float() @ W.float().t()
     _close(out, ref)
     assert torch.equal(xsf, A)  # the step-frame copy of the gathered rows (what to_step_frame wrote)
+
+
+@pytest.mark.parametrize("mode", [6, 2, 1])
+def test_gemm_bt_merge_matches_two_direction_sum(mode):
+    """AMODE 2: out[m] = [dz_fw row | dz_bw row] . [Kx_fw ; Kx_bw], the row of half h read at step t or
+    rev[b][t] (mode bit h), m = t * B + b or b * T + t (bit 2) -- the per-direction GEMMs plus
+    from_step_frame (mode 6) / step_frame_hop's two outputs (modes 2, 1) it replaces."""
+    k = _k()
+    B, T, Kh, N = 40, 29, 256, 128
+    g = torch.Generator(device="cuda").manual_seed(100 + mode)
+    lens = torch.randint(1, T + 1, (B,), generator=g, device="cuda")
+    t = torch.arange(T, device="cuda")
+    rev = torch.where(t[None, :] < lens[:, None], lens[:, None] - 1 - t[None, :], t[None, :]).long().contiguous()
+    dz = torch.randn(2, T, B, Kh, device="cuda", generator=g).bfloat16()
+    Bt = (torch.randn(N, 2 * Kh, device="cuda", generator=g) * Kh ** -0.5).bfloat16()
+    full = torch.full((T * B + 64, N), 12345.0, device="cuda")
+    out = full[:T * B]
+    k.gemm_bt_merge(dz, Bt, out, rev, B, T, mode)
+    torch.cuda.synchronize()
+    bb = torch.arange(B, device="cuda")[:, None].expand(B, T)
+    tt = t[None, :].expand(B, T)
+    t0 = rev if mode & 1 else tt
+    t1 = rev if mode & 2 else tt
+    A = torch.cat([dz[0][t0, bb], dz[1][t1, bb]], -1)  # [B][T][2 Kh]: rows of output (b, t)
+    ref = A.float() @ Bt.float().t()
+    if not mode & 4:
+        ref = ref.transpose(0, 1)  # step frame: m = t * B + b
+    _close(out.view(ref.shape), ref)
+    assert bool((full[T * B:] == 12345.0).all())
