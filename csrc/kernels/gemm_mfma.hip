@@ -32,7 +32,6 @@
 // run on one XCD and read the block from its L2.
 #include "common.h"
 #include "launchers.h"
-#include <stdlib.h>
 
 namespace {
 
@@ -257,103 +256,6 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
   gemm_epilogue<BN, OUT, BETA>(p, acc, smem, m0, n0, wr, wc, wid, lane);
 }
 
-// ---- deeper pipeline: 4 LDS stages of BK = 32 (32 KB each at BN = 256), three K tiles in flight
-// while one is multiplied; the wait before each barrier is COUNTED (vmcnt of the stages still
-// allowed in flight, never 0 in the loop) and the barrier is a raw s_barrier (no fence, so the
-// in-flight LDS-DMA is not drained, cdna_hip_programming.md s5 "Pipelining across barriers").
-// The buffer refilled in iteration k is the one multiplied in k - 1: every wave has passed the
-// barrier of k, so its fragment reads of k - 1 (waited before their MFMAs) are complete.  LDS row =
-// 64 bytes (4 chunks of 8 bf16); chunk c of row r sits in slot c ^ ((r >> 2) & 3), so the 16 rows of
-// a fragment read (4 per 256-byte bank row) spread over the 4 slots.
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int AMODE, int BN, int OUT, bool BETA>
-__global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt4_kernel(GemmP p) {
-  constexpr int BM = GM_BM, BK = 32, NS = 4;
-  constexpr int WN = BN / 4, NI = WN / 16, MI = 128 / 16;
-  constexpr int ROWB = BK * 2;  // 64-byte LDS rows
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_PER_WAVE = BM / 16 / 8;  // glds pieces (16 rows of 64 B) per wave: 2
-  constexpr int B_PER_WAVE = BN / 16 / 8;  // 2 (BN 256) / 1 (BN 128)
-  constexpr int PER_STAGE = A_PER_WAVE + B_PER_WAVE;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int wr = wid >> 2, wc = wid & 3;
-  const int ntn = p.N / BN, ntm = (p.M + BM - 1) / BM, nwg = ntn * ntm;
-  const int id = blockIdx.x, xcd = id & 7, q = nwg >> 3, r8 = nwg & 7;
-  const int lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (id >> 3);
-  const int tm = lin / ntn, tn = lin - tm * ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int lr = lane >> 2, lc = lane & 3;  // piece: 16 rows x 4 chunks
-  const bf16* asrc[A_PER_WAVE];
-#pragma unroll
-  for (int i = 0; i < A_PER_WAVE; ++i) {
-    const int row = (wid * A_PER_WAVE + i) * 16 + lr;
-    asrc[i] = a_row(p, m0 + row, AMODE) + ((lc ^ ((row >> 2) & 3)) * 8);
-  }
-  const bf16* bsrc[B_PER_WAVE];
-#pragma unroll
-  for (int i = 0; i < B_PER_WAVE; ++i) {
-    const int row = (wid * B_PER_WAVE + i) * 16 + lr;
-    bsrc[i] = p.Bt + (size_t)(n0 + row) * p.ldb + ((lc ^ ((row >> 2) & 3)) * 8);
-  }
-  auto stage_load = [&](int s, int kt) {
-    char* base = smem + s * STAGE;
-#pragma unroll
-    for (int i = 0; i < A_PER_WAVE; ++i)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(asrc[i] + kt * BK),
-                                       (lds_ptr_t)(base + ((wid * A_PER_WAVE + i) * 16) * ROWB), 16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < B_PER_WAVE; ++i)
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[i] + kt * BK),
-                                       (lds_ptr_t)(base + A_BYTES + ((wid * B_PER_WAVE + i) * 16) * ROWB), 16, 0, 0);
-  };
-  f32x4 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = p.K / BK;
-  const int fr = lane & 15, fq = lane >> 4;
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) stage_load(s, s);
-  for (int kt = 0; kt < nk; ++kt) {
-    // stage kt landed for this wave: at most the stages after it (up to 2) stay in flight
-    const int after = min(NS - 2, nk - 1 - kt);
-    if (after >= 2) vm_wait<2 * PER_STAGE>();
-    else if (after == 1) vm_wait<PER_STAGE>();
-    else vm_wait<0>();
-    __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nk) stage_load((kt + NS - 1) % NS, kt + NS - 1);
-    const char* As = smem + (kt % NS) * STAGE;
-    const char* Bs = As + A_BYTES;
-    bf16x8 bfrag[NI], afrag[MI];
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int row = wc * WN + j * 16 + fr;
-      bfrag[j] = *reinterpret_cast<const bf16x8*>(Bs + row * ROWB + ((fq ^ ((row >> 2) & 3)) * 16));
-    }
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int row = wr * 128 + i * 16 + fr;
-      afrag[i] = *reinterpret_cast<const bf16x8*>(As + row * ROWB + ((fq ^ ((row >> 2) & 3)) * 16));
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(afrag[i], bfrag[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  __syncthreads();  // every wave's last fragment reads done before the epilogue reuses LDS
-  gemm_epilogue<BN, OUT, BETA>(p, acc, smem, m0, n0, wr, wc, wid, lane);
-}
-
 bool gemm_bt_supported(int M, int N, int K, int BN) {
   return M >= 1 && K >= 64 && K % 64 == 0 && (BN == 256 || BN == 128) && N % BN == 0;
 }
@@ -377,32 +279,9 @@ void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, 
   if (out_bf16) GL(AM, BNN, 1, false);  \
   else if (beta) GL(AM, BNN, 0, true);  \
   else GL(AM, BNN, 0, false);
-  // TSAMD_GEMM_V=4: the 4-stage BK = 32 pipeline (no step-frame copy-out yet: xsf calls stay on v3)
-  static const int ver = getenv("TSAMD_GEMM_V") ? atoi(getenv("TSAMD_GEMM_V")) : 3;
   if (amode == 2) {  // merge: fp32 out, no beta
     if (BN == 256) GL(2, 256, 0, false);
     else GL(2, 128, 0, false);
-    return;
-  }
-  if (ver == 4 && !xsf) {
-    const size_t lds4 = 4 * (size_t)(GM_BM * 64 + BN * 64);
-#define GL4(AM, BNN, O, BE)                                                                                   \
-  do {                                                                                                        \
-    auto kfn = gemm_bt4_kernel<AM, BNN, O, BE>;                                                               \
-    (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4);     \
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(GM_THREADS), lds4, st, p);                                       \
-  } while (0)
-#define GL4_OUT(AM, BNN)                 \
-  if (out_bf16) GL4(AM, BNN, 1, false);  \
-  else if (beta) GL4(AM, BNN, 0, true);  \
-  else GL4(AM, BNN, 0, false);
-    if (amode == 0) {
-      if (BN == 256) { GL4_OUT(0, 256) } else { GL4_OUT(0, 128) }
-    } else {
-      if (BN == 256) { GL4_OUT(1, 256) } else { GL4_OUT(1, 128) }
-    }
-#undef GL4_OUT
-#undef GL4
     return;
   }
   if (amode == 0) {
