@@ -91,7 +91,8 @@ void lstm_fwd_persistent(const Tensor& gx, const Tensor& bias, const Tensor& Wt,
 
 void lstm_bwd_persistent(const Tensor& dz, const Tensor& Wn, const Tensor& dout, const Tensor& dh_fin,
                          const Tensor& dc_carry, const Tensor& acts, const Tensor& cs, const Tensor& lens,
-                         const Tensor& xbuf, const Tensor& err, const OT& dbias, int64_t T, int64_t B, int64_t H) {
+                         const Tensor& xbuf, const Tensor& err, const OT& dbias, int64_t T, int64_t B, int64_t H,
+                         bool dout_batch_frame) {
   chk(dz, BF, "dz"); chk(Wn, BF, "Wn"); chk(dout, F32, "dout"); chk(dh_fin, F32, "dh_fin");
   chko(dbias, F32, 2 * 4 * H, "dbias");
   chk(dc_carry, F32, "dc_carry"); chk(acts, F32, "acts"); chk(cs, F32, "cs"); chk(lens, I32, "lens");
@@ -105,7 +106,7 @@ void lstm_bwd_persistent(const Tensor& dz, const Tensor& Wn, const Tensor& dout,
   numel_eq(err, 1, "err");
   launch_lstm_bwd_persistent(P<bf16>(dz), P<bf16>(Wn), P<float>(dout), P<float>(dh_fin), P<float>(dc_carry),
                              P<float>(acts), P<float>(cs), P<int>(lens), (unsigned long long*)xbuf.data_ptr(),
-                             (unsigned*)err.data_ptr(), PO<float>(dbias), T, B, H, stream());
+                             (unsigned*)err.data_ptr(), PO<float>(dbias), T, B, H, dout_batch_frame, stream());
 }
 
 // ---------------------------------------------------------------- attention

@@ -107,7 +107,7 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
                                 int H, hipStream_t st);
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
-                                unsigned* err, float* dbias, int T, int B, int H, hipStream_t st);
+                                unsigned* err, float* dbias, int T, int B, int H, bool dout_bf, hipStream_t st);
 int vocab_topk_tiles(int V, int H);
 
 

@@ -95,6 +95,13 @@ __device__ __forceinline__ void st_b(bf16* p, bf16 v, bool nt) {
   if (nt) __builtin_nontemporal_store(__builtin_bit_cast(unsigned short, v), reinterpret_cast<unsigned short*>(p));
   else *p = v;
 }
+// dL/dh_out of (direction d, step s, row r of length len, unit u) in the BATCH frame: the
+// encoder-output gradient [B][T][2H] itself, read at position s (fw) or len - 1 - s (bw; steps past
+// the length are dead and read position s) -- no to_step_frame pass before the top layer's BPTT
+__device__ __forceinline__ size_t dout_bf_idx(int d, int s, int r, int len, int u, int T, int H) {
+  const int t = (d == 0 || s >= len) ? s : len - 1 - s;
+  return ((size_t)r * T + t) * 2 * H + (size_t)d * H + u;
+}
 __device__ __forceinline__ f32x4 ld_f4(const float* p, bool nt) {
   if (nt) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
   return *reinterpret_cast<const f32x4*>(p);
@@ -490,7 +497,7 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
 // (its own partial stays in LDS): per step a lane reads 4 x (NC-1) granules instead of 32.
 // NW = 4 or 8 waves: the cell update covers the tile's 16 rows x 64 units with RPL = 16 / NW
 // rows per lane (4 or 2); waves < NC run the partial GEMM (at H = 512, NC = 8: all 8 waves).
-template <int H, int NW, bool NT>
+template <int H, int NW, bool NT, bool DBF = false>
 __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
@@ -556,12 +563,12 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
     for (int i = 0; i < RPL; ++i) {
       const size_t ri = (size_t)rc[i] * H + u;
       if constexpr (NT) {
-        dho[i] = ld_f(dout + ((size_t)d * T + s) * BH + ri, true);
+        dho[i] = ld_f(dout + (DBF ? dout_bf_idx(d, s, rc[i], ln[i], u, T, H) : ((size_t)d * T + s) * BH + ri), true);
         const f32x4 q = ld_f4(acts + ((((size_t)d * T + s) * B + rc[i]) * H + u) * 4, true);
         a4[i][0] = q[0]; a4[i][1] = q[1]; a4[i][2] = q[2]; a4[i][3] = q[3];
         cpv[i] = ld_f(cs + ((size_t)d * (T + 1) + s) * BH + ri, true);
       } else {
-        dho[i] = dout[((size_t)d * T + s) * BH + ri];
+        dho[i] = dout[DBF ? dout_bf_idx(d, s, rc[i], ln[i], u, T, H) : ((size_t)d * T + s) * BH + ri];
         const float4 q = *reinterpret_cast<const float4*>(acts + ((((size_t)d * T + s) * B + rc[i]) * H + u) * 4);
         a4[i][0] = q.x; a4[i][1] = q.y; a4[i][2] = q.z; a4[i][3] = q.w;
         cpv[i] = cs[((size_t)d * (T + 1) + s) * BH + ri];
@@ -728,7 +735,7 @@ __device__ __forceinline__ const gu64* gboff(const gu64* p, unsigned bytes) {
 }
 
 // PC: peers polled per chunk (4: 8 registers spill); SL: s_sleep between poll passes
-template <bool NT, int PC = 2, int SL = 96>
+template <bool NT, int PC = 2, int SL = 96, bool DBF = false>
 __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
@@ -778,7 +785,8 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
     asm volatile("" : "+v"(row0v));
     // uniform step bases + 32-bit per-lane byte offsets (saddr addressing: no 64-bit address
     // pairs per row held across the step)
-    const float* dout_s = dout + ((size_t)d * T + s) * BH;
+    // (DBF: the batch-frame gradient's direction half; rows and positions per lane below)
+    const float* dout_s = DBF ? dout + d * H : dout + ((size_t)d * T + s) * BH;
     const float* acts_s = acts + ((size_t)d * T + s) * BH * 4;
     const float* cs_s = cs + ((size_t)d * (T + 1) + s) * BH;
     float dho[RPL], a4[RPL][4], cpv[RPL];
@@ -791,7 +799,13 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
 #pragma unroll
     for (int i = 0; i < RPL; ++i) {
       const unsigned ri = rio[i];
-      dho[i] = ld_f(boff(dout_s, ri * 4u), NT);
+      if constexpr (DBF) {  // batch-frame row (rc * T + position), opaque: no hoisted 64-bit offsets
+        // (the row from the opaque rio = rc * H + u: no extra live register per row)
+        const unsigned rt = (ri / H) * (unsigned)T + (unsigned)((d == 0 || s >= ln[i]) ? s : ln[i] - 1 - s);
+        dho[i] = ld_f(boff(dout_s, (unsigned)u * 4u) + (size_t)rt * (2 * H), NT);
+      } else {
+        dho[i] = ld_f(boff(dout_s, ri * 4u), NT);
+      }
       const f32x4 q = ld_f4(boff(acts_s, ri * 16u), NT);
       a4[i][0] = q[0]; a4[i][1] = q[1]; a4[i][2] = q[2]; a4[i][3] = q[3];
       cpv[i] = ld_f(boff(cs_s, ri * 4u), NT);
@@ -1082,7 +1096,7 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
 
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
-                                unsigned* err, float* dbias, int T, int B, int H, hipStream_t st) {
+                                unsigned* err, float* dbias, int T, int B, int H, bool dout_bf, hipStream_t st) {
   const int R = lstm_rows(H, B, true), ntile = (B + R - 1) / R, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64;
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
@@ -1090,15 +1104,21 @@ void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, con
   for (int t0 = 0; t0 < ntile; t0 += nl) {
     const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
     if (R == 32) {
-#define LB32(PC, SL) hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false, PC, SL>), dim3(grid), dim3(1024), 0, st, dz, \
-                                        Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
-      LB32(2, 96);  // poll 2 peers per pass, s_sleep(96): profiles/r4/ab/bptt32.md
+#define LB32(PC, SL, DB) hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false, PC, SL, DB>), dim3(grid), dim3(1024), 0, st, \
+                                            dz, Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+      // poll 2 peers per pass, s_sleep(96): profiles/r4/ab/bptt32.md
+      if (dout_bf) LB32(2, 96, true);
+      else LB32(2, 96, false);
 #undef LB32
       continue;
     }
 #define LAUNCH_B(HH, NTV)                                                                                                 \
-  hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin,   \
-                     dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+  if (dout_bf)                                                                                                        \
+    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV, true>), dim3(grid), dim3(512), 0, st, dz, Wn, dout,  \
+                       dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n);                          \
+  else                                                                                                                \
+    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin, \
+                       dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
     if (H == 64) LAUNCH_B(64, false);
     else if (H == 128) LAUNCH_B(128, false);
     else if (H == 256) LAUNCH_B(256, false);

@@ -63,7 +63,20 @@ def test_persistent_matches_step_kernels(H, B, T):
         else:
             xb = torch.zeros(int(k.lstm_persistent_xbuf(H, B, True)), device="cuda", dtype=torch.long)
             db = torch.full((2, 4 * H), 0.25, device="cuda")  # accumulates onto what is there
-            k.lstm_bwd_persistent(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, xb, err, db, T, B, H)
+            dcc0 = dcc.clone()
+            k.lstm_bwd_persistent(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, xb, err, db, T, B, H, False)
+            # the same gradient in the BATCH frame ([B][T][2H], bw half at the reversed position), read
+            # by the kernel directly (what the top layer's to_step_frame pass used to rebuild): same bits
+            t = torch.arange(T, device="cuda")
+            ln = lens.long()[:, None]
+            rev = torch.where(t[None, :] < ln, ln - 1 - t[None, :], t[None, :])
+            dE = torch.cat([dout[0].transpose(0, 1),
+                            dout[1].transpose(0, 1)[torch.arange(B, device="cuda")[:, None], rev]], -1).contiguous()
+            dz2 = torch.zeros_like(dz)
+            xb.zero_()
+            k.lstm_bwd_persistent(dz2, Wn, dE, dh_fin, dcc0, acts, cs, lens, xb, err, None, T, B, H, True)
+            torch.cuda.synchronize()
+            assert torch.equal(dz2, dz) and torch.equal(dcc0, dcc)
         torch.cuda.synchronize()
         assert int(err.item()) == 0
         if mode != "step":
@@ -142,7 +155,7 @@ def test_persistent_lstm_with_concurrent_kernels():
                 for _ in range(30):
                     a @ a
         xb.zero_()
-        k.lstm_bwd_persistent(dz, Wn, dout, dhf, dcc, acts, cs, lens, xb, err, None, T, B, H)
+        k.lstm_bwd_persistent(dz, Wn, dout, dhf, dcc, acts, cs, lens, xb, err, None, T, B, H, False)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         return out.clone(), dz.clone()
@@ -185,7 +198,7 @@ def test_persistent_lstm_stress_full_grid(H, B):
         dcc.zero_()
         dhf.zero_()
         xb.zero_()
-        k.lstm_bwd_persistent(dz, Wn, dout, dhf, dcc, acts, cs, lens, xb, err, None, T, B, H)
+        k.lstm_bwd_persistent(dz, Wn, dout, dhf, dcc, acts, cs, lens, xb, err, None, T, B, H, False)
         if ref is None:
             ref = (out.clone(), dz.clone(), dcc.clone())
         elif it % 8 == 0 or it == 39:

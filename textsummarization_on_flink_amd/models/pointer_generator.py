@@ -1316,7 +1316,9 @@ class HipPointerGenerator:
             din = st["din"]
             # dL/dh_out in step frame: fw as is, bw reversed within each length (below the top layer
             # the previous iteration's step_frame_hop wrote it straight from the upper layer's dxs)
-            if layer == self.L - 1:
+            # (the persistent BPTT reads the top layer's gradient in the batch frame itself: no pass)
+            top_bf = layer == self.L - 1 and self.persistent_lstm
+            if layer == self.L - 1 and not top_bf:
                 k.to_step_frame(d_in, None, w["rev_idx"], st["dout"], B, T, H, H)
             if layer != self.L - 1:  # the top layer's seeds came from rs_bwd
                 st["dh_fin"].zero_()
@@ -1324,9 +1326,9 @@ class HipPointerGenerator:
             if self.persistent_lstm:
                 w["lstm_xb"].zero_()
                 w["lstm_db"].zero_()
-                k.lstm_bwd_persistent(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"], st["dc_carry"],
-                                      st["acts"], st["cs"], lens, w["lstm_xb"], w["lstm_err"],
-                                      None if self.det else w["lstm_db"], T, B, H)
+                k.lstm_bwd_persistent(st["dz"], self.pk[f"enc{layer}_Wn"], d_in if top_bf else st["dout"], st["dh_fin"],
+                                      st["dc_carry"], st["acts"], st["cs"], lens, w["lstm_xb"], w["lstm_err"],
+                                      None if self.det else w["lstm_db"], T, B, H, top_bf)
             else:
                 for s in reversed(range(T)):
                     k.lstm_enc_bwd_step(st["dz"], self.pk[f"enc{layer}_Wn"], st["dout"], st["dh_fin"],

@@ -55,7 +55,7 @@ def main():
 
         def bwd():
             xb.zero_()
-            k.lstm_bwd_persistent(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, xb, err, db, T, B, H)
+            k.lstm_bwd_persistent(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, xb, err, db, T, B, H, False)
 
         tf, tb = timeit(fwd), timeit(bwd)
         print(json.dumps({"H": H, "B": B, "T": T, "nw": "auto",
