@@ -135,20 +135,12 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     bf16* __restrict__ hs, float* __restrict__ cs, float* __restrict__ acts, bf16* __restrict__ out,
     const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile, int tile0, int ntile_l) {
   constexpr int KS = H / 32, NC = H / 64, HP = H / 2, R = 16 * RT, G = R * HP, NPL = G / 256;
-  // granules per lane per sweep (chunks keep x[] at 16 VGPRs; 32 at RT = 4, where the gates are
-  // dead during the sweep)
-  constexpr int CH = NPL < 8 ? NPL : 8;
+  constexpr int CH = NPL < 8 ? NPL : 8;  // granules per lane per sweep (chunks keep x[] at 16 VGPRs)
   constexpr int NR = 4 * RT;             // rows per lane
   static_assert(NPL % CH == 0, "sweep chunks");
-  // h tile: double-buffered by step parity up to RT = 2; ONE buffer at RT = 4 (64 KB), which is
-  // safe without a barrier: a wave writes a row chunk of step s + 1 only after its sweep saw
-  // every unit of those rows published, including the units of this workgroup's other waves,
-  // and each wave publishes only after its step-s MFMAs consumed their Ash fragments.
-  constexpr int NAB = RT > 2 ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) bf16 Ash[NAB][R * H];
-  // RT = 2: the step's gate activations wait here (not in registers) until the hand-off is out;
-  // RT = 4 keeps them in registers (the LDS holds the h tile and the staged x.W_x: 128 KB)
-  __shared__ __attribute__((aligned(16))) float Gsh[RT == 2 ? 256 * NR * 4 : 4];
+  __shared__ __attribute__((aligned(16))) bf16 Ash[2][R * H];
+  // RT = 2: the step's gate activations wait here (not in registers) until the hand-off is out
+  __shared__ __attribute__((aligned(16))) float Gsh[RT > 1 ? 256 * NR * 4 : 4];
   int lt, c;
   if (!team_of(NC, 2 * ntile_l, lt, c)) return;
   const int d = lt / ntile_l, tile = tile0 + lt % ntile_l, r0 = tile * R, team = d * ntile + tile;
@@ -168,18 +160,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // rc / ln: recomputed / read from LDS (lnsh) rather than held in 2 x NR registers
   __shared__ int lnsh[R];
   if (threadIdx.x < R) lnsh[threadIdx.x] = r0 + (int)threadIdx.x < B ? lens[r0 + threadIdx.x] : 0;
-  // RT = 4: the lane's first row is re-made opaque at every step (an empty asm "changes" it), so
-  // the 16 rows' address offsets are recomputed where they are used instead of being hoisted out
-  // of the step loop as 16 live 64-bit addresses per stream (which spilled the kernel)
-  int lrow = r0 + (lane >> 4) * 4;
-  auto rowof = [&](int j) { return lrow + (j >> 2) * 16 + (j & 3); };
-  float creg[NR], hreg_r[RT > 2 ? 1 : NR];
-  // RT = 4: h (bf16-exact floats, live across steps for rows past their length) in LDS, 16 KB
-  __shared__ float Hsh[RT > 2 ? 256 * NR : 1];
-  auto HR = [&](int j) -> float& {
-    if constexpr (RT > 2) return Hsh[j * 256 + threadIdx.x];
-    else return hreg_r[j];
-  };
+  auto rowof = [&](int j) { return r0 + (j >> 2) * 16 + (lane >> 4) * 4 + (j & 3); };
+  float creg[NR], hreg[NR];
   const bf16* hs0 = hs + (size_t)d * (T + 1) * BH;
   const float* cs0 = cs + (size_t)d * (T + 1) * BH;
 #pragma unroll
@@ -187,7 +169,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     const int r = rowof(j);
     const int rr = r < B ? r : B - 1;
     creg[j] = cs0[(size_t)rr * H + u];
-    HR(j) = bf2f(hs0[(size_t)rr * H + u]);
+    hreg[j] = bf2f(hs0[(size_t)rr * H + u]);
   }
   gu64* xb = xbuf + (size_t)team * 2 * G;
   bool dead = false;
@@ -213,8 +195,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   };
   load_gz(0);
   for (int s = 0; s < T; ++s) {
-    const int buf = NAB == 1 ? 0 : s & 1;
-    if constexpr (RT > 2) asm volatile("" : "+v"(lrow));
+    const int buf = s & 1;
     // RT = 1: the next step's x.W_x is requested now and the current one kept in gz; RT = 2
     // (no registers for two copies): requested after this step's cell update consumed gzn
     float gz[RT > 1 ? 1 : NR][4];
@@ -288,14 +269,12 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         z[3] = fsigmoid(acc[rt][3][i] + x[3] + gb[3]);
         const float cc = z[2] * creg[j] + z[0] * z[1];
         creg[j] = cc;
-        HR(j) = bf2f(f2bf(z[3] * ftanh(cc)));
-        if constexpr (RT == 2)
+        hreg[j] = bf2f(f2bf(z[3] * ftanh(cc)));
+        if constexpr (RT > 1)
           *reinterpret_cast<float4*>(&Gsh[(j * 256 + threadIdx.x) * 4]) = make_float4(z[0], z[1], z[2], z[3]);
-        else if constexpr (RT > 2)  // in place of the x.W_x just consumed (this lane's own slot)
-          *reinterpret_cast<float4*>(&Gxsh[((wid * NR + j) * 64 + lane) * 4]) = make_float4(z[0], z[1], z[2], z[3]);
       }
     }
-    if constexpr (RT == 2) {
+    if constexpr (RT > 1) {
       if (s + 1 < T) load_gz(s + 1);
     }
     // ---- publish h_{s+1}: unit pairs (u, u+1) of adjacent lanes -> one granule
@@ -303,10 +282,10 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       gu64* dst = xb + (size_t)((s + 1) & 1) * G;
 #pragma unroll
       for (int j = 0; j < NR; ++j) {
-        const float hn = __shfl_xor(HR(j), 1, 64);
+        const float hn = __shfl_xor(hreg[j], 1, 64);
         if (!(lane & 1))
           store_granule(dst + ((j >> 2) * 16 + (lane >> 4) * 4 + (j & 3)) * HP + u / 2, (unsigned)(s + 1),
-                        pack_bf2(HR(j), hn));
+                        pack_bf2(hreg[j], hn));
       }
     }
     float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
@@ -316,25 +295,19 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       const int r = rowof(j), lj = lnsh[r - r0];
       if (s < lj) {
         if constexpr (RT > 1) {
-          const float4 z = RT == 2 ? *reinterpret_cast<const float4*>(&Gsh[(j * 256 + threadIdx.x) * 4])
-                                   : *reinterpret_cast<const float4*>(&Gxsh[((wid * NR + j) * 64 + lane) * 4]);
+          const float4 z = *reinterpret_cast<const float4*>(&Gsh[(j * 256 + threadIdx.x) * 4]);
           st_f4(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4, z.x, z.y, z.z, z.w, NT);
         } else {
           st_f4(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4, ga[j][0], ga[j][1], ga[j][2], ga[j][3],
                 NT);  // one 16-byte store per (row, unit)
         }
         const int t = d == 0 ? s : lj - 1 - s;
-        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(HR(j)), NT);
+        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(hreg[j]), NT);
       }
       if (r < B) {
         st_f(cnext + (size_t)r * H + u, creg[j], NT);
-        st_b(hnext + (size_t)r * H + u, f2bf(HR(j)), NT);
+        st_b(hnext + (size_t)r * H + u, f2bf(hreg[j]), NT);
       }
-    }
-    // RT = 4: the gates left the slots, so the next step's x.W_x can land there (in flight
-    // during the next sweep)
-    if constexpr (RT > 2) {
-      if (s + 1 < T) load_gz(s + 1);
     }
   }
 }
@@ -983,9 +956,7 @@ int lstm_persistent_capacity(int H) {
                                                          256, 0) == hipSuccess;                                    \
     } else {                                                                                                       \
       ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[2], lstm_fwd_persistent_kernel<512, true, 2>, 256, 0) == hipSuccess; \
-      int o32 = 0, o64 = 0;                                                                                        \
-      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o64, lstm_fwd_persistent_kernel<512, true, 4>, 256, 0) == hipSuccess; \
-      o[2] = min(o[2], o64);                                                                                      \
+      int o32 = 0;                                                                                                 \
       ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o32, lstm_bwd_persistent32_kernel<false>, 1024, 0) == hipSuccess; \
       o[2] = min(o[2], o32);                                                                                      \
     }                                                                                                              \
@@ -1012,17 +983,7 @@ static bool lstm_bwd32() {
   }();
   return on;
 }
-// The forward runs 64-row teams (RT = 4, one h buffer, gates in registers) above batch 512:
-// batch 1024 in ONE launch instead of 2 (TSAMD_LSTM_FWD64=0 keeps 32-row teams).
-static bool lstm_fwd64() {
-  static const int on = [] {
-    const char* e = getenv("TSAMD_LSTM_FWD64");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on;
-}
 static int lstm_rows(int H, int B, bool bwd) {
-  if (H == 512 && !bwd && B > 512 && lstm_fwd64()) return 64;
   return (H == 512 && B > 256 && (!bwd || lstm_bwd32())) ? 32 : 16;
 }
 
@@ -1067,7 +1028,7 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
                                 int H, hipStream_t st) {
   const int R = lstm_rows(H, B, false), ntile = (B + R - 1) / R, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64;
-  const int nw = R >= 32 ? 4 : lstm_nw(H);
+  const int nw = R == 32 ? 4 : lstm_nw(H);
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
@@ -1077,9 +1038,6 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
   if (nw == 8)                                                                                                  \
     hipLaunchKernelGGL((lstm_fwd_persistent8_kernel<HH, NTV>), dim3(grid), dim3(512), 0, st, gx, bias, Wt, hs, cs, \
                        acts, out, lens, xb, e, T, B, ntile, t0, n);                                             \
-  else if (R == 64)                                                                                             \
-    hipLaunchKernelGGL((lstm_fwd_persistent_kernel<512, NTV, 4>), dim3(grid), dim3(256), 0, st, gx, bias, Wt, hs, \
-                       cs, acts, out, lens, xb, e, T, B, ntile, t0, n);                                         \
   else if (R == 32)                                                                                             \
     hipLaunchKernelGGL((lstm_fwd_persistent_kernel<512, NTV, 2>), dim3(grid), dim3(256), 0, st, gx, bias, Wt, hs, \
                        cs, acts, out, lens, xb, e, T, B, ntile, t0, n);                                         \

@@ -75,9 +75,13 @@ BLT_VDW = BLT and os.environ.get("TSAMD_BLT_VOCAB_DW", "0") == "1"
 GEMM_BT = os.environ.get("TSAMD_GEMM_BT", "auto")
 _BT_PICK: Dict[tuple, bool] = {}
 _BT_TIMES: Dict[tuple, tuple] = {}
-# TSAMD_DX_MERGE=0: the encoder input gradients as two per-direction GEMMs + from_step_frame /
-# step_frame_hop (default: one hand-written GEMM per output over [dz_fw | dz_bw], rows gathered
-# through the reversed index, written in the frame the consumer reads -- gemm_mfma.hip AMODE 2)
+# TSAMD_DX_MERGE=0: the input gradients of an upper encoder layer as two per-direction GEMMs +
+# step_frame_hop (default: one hand-written GEMM per output direction over [dz_fw | dz_bw], rows
+# gathered through the reversed index, written straight into the lower layer's step frame --
+# gemm_mfma.hip AMODE 2).  Config #5 at batch 2048: same step time (391.8 vs 391.9 ms), 14 GB less
+# memory (no per-direction dxs).  Layer 0 keeps the library GEMMs + from_step_frame: its merged
+# GEMM (N = E = 128, one 128-column tile) measured 0.1 ms slower at batch 256
+# (profiles/r5/dx_merge.md).
 DX_MERGE = os.environ.get("TSAMD_DX_MERGE", "1") != "0"
 # the step-frame gather path replaces to_step_frame + the GEMM: kept while the gather GEMM is at
 # most this much slower than the library GEMM alone (the layout pass it saves costs ~25-40 % of it)
@@ -423,10 +427,9 @@ class HipPointerGenerator:
         self._in_used = [None, None]   # staging copy i consumed (its D2D copy into the inputs finished)
         self._copy_stream = torch.cuda.Stream(self.dev)
         self._in_i = 0
-        # encoder input gradients through the merged hand-written GEMM (no per-direction dxs)
-        self.dx_merge = (DX_MERGE and BLT and GEMM_BT != "0" and self.dev.type == "cuda"
-                         and hasattr(self.k, "gemm_bt_merge") and bool(self.k.gemm_bt_ok(T * B, E, 8 * H))
-                         and (L == 1 or bool(self.k.gemm_bt_ok(T * B, H, 8 * H))))
+        # upper encoder layers' input gradients through the merged hand-written GEMM (no dxs)
+        self.dx_merge = (DX_MERGE and L > 1 and BLT and GEMM_BT != "0" and self.dev.type == "cuda"
+                         and hasattr(self.k, "gemm_bt_merge") and bool(self.k.gemm_bt_ok(T * B, H, 8 * H)))
         # encoder, per layer
         self.enc = []
         for layer in range(L):
@@ -443,7 +446,7 @@ class HipPointerGenerator:
                 "dout": z(B, T, A),
                 "dh_fin": z(2, B, H),
                 "dc_carry": z(2, B, H),
-                "dxs": None if self.dx_merge else z(2, T * B, din),
+                "dxs": None if (self.dx_merge and layer > 0) else z(2, T * B, din),
                 # batch-frame input gradient: the embedding gradient's source (layer 0 only; above it
                 # step_frame_hop feeds the layer below directly)
                 "dx": z(B, T, din) if layer == 0 else None,
@@ -631,8 +634,9 @@ class HipPointerGenerator:
                           (pk[f"enc{layer}_Kxi{di}"].view(din, H, 4), Kd[:din].view(din, 4, H).permute(0, 2, 1)),
                           (pk[f"enc{layer}_KxiT{di}"].view(H, 4, din), Kd[:din].view(din, 4, H).permute(2, 1, 0)),
                           (pk[f"enc{layer}_Wn"][di], Kd[din:]), (pk[f"enc{layer}_Wt"][di], Kd[din:].t()),
-                          (f32[f"enc{layer}_b"][di], p[enc_b(layer, d)]),
-                          (pk[f"enc{layer}_Kx01"][:, di * 4 * H:(di + 1) * 4 * H], Kd[:din])]
+                          (f32[f"enc{layer}_b"][di], p[enc_b(layer, d)])]
+                if layer > 0:
+                    pairs.append((pk[f"enc{layer}_Kx01"][:, di * 4 * H:(di + 1) * 4 * H], Kd[:din]))
         pairs += [(pk["Wh"], p[WH].reshape(A, A)), (pk["WhT"], p[WH].reshape(A, A).t()), (pk["lin_embT"], M[:E].t()),
                   (pk["RC"], p[RC]), (pk["RH"], p[RH]), (pk["RCt"], p[RC].t()),
                   (pk["RHt"], p[RH].t()), (pk["lin_emb"], M[:E]), (pk["Wic"], M[E:]), (pk["WicT"], M[E:].t()),
@@ -693,8 +697,8 @@ class HipPointerGenerator:
                 put(f"enc{layer}_Kxi{di}", K[:din].reshape(din, 4, self.H).transpose(1, 2).reshape(din, 4 * self.H))
                 # its [4H][din] twin: the "Bt" operand of the hand-written gather GEMM (gemm_mfma.hip)
                 put(f"enc{layer}_KxiT{di}", K[:din].reshape(din, 4, self.H).permute(2, 1, 0).reshape(4 * self.H, din))
-            # [Kx_fw | Kx_bw] ([din][8H]): the "Bt" operand of the merged input-gradient GEMM
-            put(f"enc{layer}_Kx01", torch.cat([p[enc_k(layer, d)][:din] for d in ("fw", "bw")], 1))
+            if layer > 0:  # [Kx_fw | Kx_bw] ([din][8H]): the "Bt" operand of the merged input-gradient GEMM
+                put(f"enc{layer}_Kx01", torch.cat([p[enc_k(layer, d)][:din] for d in ("fw", "bw")], 1))
             Kh = torch.stack([p[enc_k(layer, d)][din:] for d in ("fw", "bw")])  # [2][H][4H]
             put(f"enc{layer}_Wn", Kh)
             put(f"enc{layer}_Wt", Kh.transpose(1, 2))
@@ -1335,6 +1339,7 @@ class HipPointerGenerator:
                                         st["dc_carry"], st["acts"], st["cs"], lens, s, T, B, H)
             dxs = st["dxs"]  # [2][T*B][din]: both directions' input gradients, step frame
             rev = w["rev_idx"]
+            merge = self.dx_merge and layer > 0
             for di, d in enumerate(("fw", "bw")):
                 dzd = st["dz"][di].view(T * B, 4 * H)
                 gkd = g(enc_k(layer, d))
@@ -1344,22 +1349,19 @@ class HipPointerGenerator:
                     g(enc_b(layer, d)).copy_(w["lstm_db"][di])
                 else:
                     k.colsum(dzd, g(enc_b(layer, d)), T * B, 4 * H, False)
-                if not self.dx_merge:
+                if not merge:
                     gemm(dxs[di], dzd, self.pk[f"enc{layer}_Kx{di}"].t())
-            Km = self.pk[f"enc{layer}_Kx01"]
             if layer > 0:  # the layer below's output-gradient step frame, without the batch-frame dx
                 lo = self.enc[layer - 1]["dout"].view(2, T * B, H)
-                if self.dx_merge:  # fw units: [dz_fw(t) | dz_bw(rev)]; bw units: [dz_fw(rev) | dz_bw(t)]
+                if merge:  # fw units: [dz_fw(t) | dz_bw(rev)]; bw units: [dz_fw(rev) | dz_bw(t)]
+                    Km = self.pk[f"enc{layer}_Kx01"]
                     k.gemm_bt_merge(st["dz"], Km[:H], lo[0], rev, B, T, 2)
                     k.gemm_bt_merge(st["dz"], Km[H:], lo[1], rev, B, T, 1)
                 else:
                     k.step_frame_hop(dxs, rev, lo, B, T, H)
                 continue
             dx = st["dx"]
-            if self.dx_merge:  # batch frame: dx[b][t] = dz_fw(t) . Kx_fw + dz_bw(rev(b, t)) . Kx_bw
-                k.gemm_bt_merge(st["dz"], Km, dx.view(B * T, din), rev, B, T, 6)
-            else:
-                k.from_step_frame(dxs, rev, dx, B, T, din)  # fw + reversed bw, batch frame
+            k.from_step_frame(dxs, rev, dx, B, T, din)  # fw + reversed bw, batch frame
             d_in = dx
         self._d_in = d_in
         if late:
