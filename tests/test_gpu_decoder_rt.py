@@ -1,0 +1,106 @@
+"""Large-batch decoder step kernels (decoder.hip *_rt_kernel: 64 rows per block, the weight slice
+fetched once per 64 rows; used from 512 rows per launch) against the 16-row kernels: the same rows
+computed in launches below 512 rows (two launches over the row prefix / suffix) must give the same
+bits -- same K split, same summation order, same per-row epilogues, dead row tiles included."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+H, A, E = 512, 1024, 128
+B1, CUT = 640, 496  # B1 >= 512: the RT kernels; 496 and 144 rows: the 16-row kernels
+
+
+def _k():
+    from textsummarization_on_flink_amd.ops import ops
+    return ops()
+
+
+def _g(seed):
+    return torch.Generator(device="cuda").manual_seed(seed)
+
+
+def _r(g, *shape, sc=1.0, dt=torch.float32):
+    return (torch.randn(*shape, device="cuda", generator=g) * sc).to(dt)
+
+
+def _dlen(g, step):
+    # rows sorted by live steps (as the engine sorts them): the tail tiles are dead at `step`
+    d = torch.randint(0, 30, (B1,), device="cuda", generator=g).sort(descending=True).values
+    d[:CUT // 2] = max(int(d[0]), step + 1)
+    return d.int().contiguous()
+
+
+def _split(run):
+    """run(lo, hi) on rows [lo, hi) of every tensor: full B1 in one launch vs [0, CUT) + [CUT, B1)."""
+    full = run(0, B1)
+    parts = [run(0, CUT), run(CUT, B1)]
+    for i, f in enumerate(full):
+        assert torch.equal(f[:CUT], parts[0][i]), i
+        assert torch.equal(f[CUT:], parts[1][i]), i
+
+
+@pytest.mark.parametrize("step", [0, 12])
+def test_dec_cell_fwd_rt_matches_16_row(step):
+    k, g = _k(), _g(1 + step)
+    XG, ctx, hp, cp = _r(g, B1, 4 * H), _r(g, B1, A, dt=torch.bfloat16), _r(g, B1, H, dt=torch.bfloat16), _r(g, B1, H)
+    WcT = _r(g, 4 * H, A + H, sc=(A + H) ** -0.5, dt=torch.bfloat16)
+    dlen = _dlen(g, step)
+
+    def run(lo, hi):
+        n = hi - lo
+        outs = [torch.full((n, H), float("nan"), device="cuda"), torch.zeros(n, H, device="cuda", dtype=torch.bfloat16),
+                torch.zeros(n, H, device="cuda", dtype=torch.bfloat16), torch.full((n, 4 * H), float("nan"), device="cuda")]
+        k.dec_cell_fwd(XG[lo:hi], ctx[lo:hi], hp[lo:hi], cp[lo:hi], WcT, *outs, n, H, A, dlen[lo:hi], step)
+        torch.cuda.synchronize()
+        return outs
+    _split(run)
+
+
+def test_dec_sproj_rt_matches_16_row():
+    k, g = _k(), _g(3)
+    cb, hb = _r(g, B1, H, dt=torch.bfloat16), _r(g, B1, H, dt=torch.bfloat16)
+    WsT, bs = _r(g, A, 2 * H, sc=(2 * H) ** -0.5, dt=torch.bfloat16), _r(g, A)
+    dlen = _dlen(g, 7)
+
+    def run(lo, hi):
+        s = torch.full((hi - lo, A), 7.0, device="cuda")  # dead rows keep what was there
+        k.dec_sproj(cb[lo:hi], hb[lo:hi], WsT, bs, s, hi - lo, H, A, dlen[lo:hi], 7)
+        torch.cuda.synchronize()
+        return [s]
+    _split(run)
+
+
+def test_dec_bwd_cell_rt_matches_16_row():
+    k, g = _k(), _g(5)
+    ds, Ws = _r(g, B1, A), _r(g, 2 * H, A, sc=A ** -0.5, dt=torch.bfloat16)
+    dC, dH, dh_rec, dc0 = _r(g, B1, H), _r(g, B1, H), _r(g, B1, H), _r(g, B1, H)
+    act = torch.rand(B1, 4 * H, device="cuda", generator=g)
+    c_now, c_prev = _r(g, B1, H), _r(g, B1, H)
+    dlen = _dlen(g, 9)
+
+    def run(lo, hi):
+        dc = dc0[lo:hi].clone()
+        dz = torch.full((hi - lo, 4 * H), 3.0, device="cuda", dtype=torch.bfloat16)
+        k.dec_bwd_cell(ds[lo:hi], Ws, dC[lo:hi], dH[lo:hi], dh_rec[lo:hi], dc, act[lo:hi], c_now[lo:hi], c_prev[lo:hi],
+                       dz, hi - lo, H, A, dlen[lo:hi], 9)
+        torch.cuda.synchronize()
+        return [dz, dc]
+    _split(run)
+
+
+def test_dec_bwd_dz_rt_matches_16_row():
+    k, g = _k(), _g(7)
+    dz = _r(g, B1, 4 * H, dt=torch.bfloat16)
+    Wbig = _r(g, E + H + A, 4 * H, sc=(4 * H) ** -0.5, dt=torch.bfloat16)
+    dX, dC = _r(g, B1, E), _r(g, B1, A)
+    dlen = _dlen(g, 11)
+
+    def run(lo, hi):
+        n = hi - lo
+        outs = [torch.full((n, E), 5.0, device="cuda"), torch.full((n, A), 5.0, device="cuda"),
+                torch.full((n, H), 5.0, device="cuda")]
+        k.dec_bwd_dz(dz[lo:hi], Wbig, dX[lo:hi], dC[lo:hi], outs[0], outs[1], outs[2], n, E, H, A, dlen[lo:hi], 11)
+        torch.cuda.synchronize()
+        return outs
+    _split(run)
