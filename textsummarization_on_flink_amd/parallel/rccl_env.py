@@ -7,8 +7,8 @@ import os
 # initialises -- the bench launcher, the worker runtime and ``init_from_env`` all apply
 # ``rccl_env``), so in-flight all-reduces hold at most this many CUs.  The persistent encoder LSTM
 # needs all its workgroups resident: a launch grid leaving at least this many CUs free may share
-# the GPU with RCCL (train/trainer.py; tests/test_gpu_lstm.py holds exactly this many CUs with a
-# spinning kernel during the captured BPTT phase).  An 86 MB fp32 gradient all-reduce at 8 ranks
+# the GPU with RCCL (train/trainer.py; tests/test_gpu_production.py holds exactly this many CUs with
+# a spinning kernel during the captured BPTT phase).  An 86 MB fp32 gradient all-reduce at 8 ranks
 # moves 2 x 7/8 x 86 MB = 150 MB per rank; 64 channels spread it over all 7 xGMI links
 # (~0.2-0.4 ms at 50-100 GB/s per link and direction), more channels do not add link bandwidth.
 RCCL_MAX_CHANNELS = 64
