@@ -405,6 +405,10 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
     const float* __restrict__ dh_rec, float* __restrict__ dc_carry,            // [B][H]
     const float* __restrict__ act, const float* __restrict__ c_now, const float* __restrict__ c_prev,
     bf16* __restrict__ dz, int B, int H, int A, const int* __restrict__ dlen, int step) {
+  // no FMA contraction in the cell backward (here and in dec_bwd_cell_rt_kernel): the 64-row
+  // variant's compiler packs some products across its row tiles, and only uncontracted products
+  // round the same both ways (bit-identical results, tests/test_gpu_decoder_rt.py)
+#pragma clang fp contract(off)
   __shared__ float red[4 * 2 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int tx, ty;
@@ -464,6 +468,7 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_rt_kernel(
     const float* __restrict__ dH_dir, const float* __restrict__ dh_rec, float* __restrict__ dc_carry,
     const float* __restrict__ act, const float* __restrict__ c_now, const float* __restrict__ c_prev,
     bf16* __restrict__ dz, int B, int H, int A, const int* __restrict__ dlen, int step) {
+#pragma clang fp contract(off)  // as in dec_bwd_cell_kernel
   __shared__ float red[4 * RT * 2 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int tx, ty;
