@@ -36,8 +36,14 @@ def _split(run):
     full = run(0, B1)
     parts = [run(0, CUT), run(CUT, B1)]
     for i, f in enumerate(full):
-        assert torch.equal(f[:CUT], parts[0][i]), i
-        assert torch.equal(f[CUT:], parts[1][i]), i
+        for got, ref, off in ((f[:CUT], parts[0][i], 0), (f[CUT:], parts[1][i], CUT)):
+            if not torch.equal(got, ref):
+                bad = (got != ref) & ~(torch.isnan(got) & torch.isnan(ref))
+                rows = bad.any(1).nonzero().flatten()
+                cols = bad.any(0).nonzero().flatten()
+                d = (got.float() - ref.float()).abs()[bad]
+                raise AssertionError(f"output {i}: {int(bad.sum())} elements differ, rows {(rows + off).tolist()[:20]}, "
+                                     f"cols {cols.tolist()[:20]}, max |diff| {float(d.max()) if d.numel() else 0}")
 
 
 @pytest.mark.parametrize("step", [0, 12])
