@@ -143,38 +143,6 @@ __device__ __forceinline__ void kslice_mma(FA a, FB b, int k0, int k1, f32x4 (&a
   }
 }
 
-// kslice_mma over RT row tiles that share the Bt fragments (large-batch decoder steps: the weight
-// slice is fetched once per 16 RT rows instead of once per 16 rows).  a(rt, k): this lane's A
-// pointer for row tile rt; row tiles with live[rt] == false (block-uniform) load nothing and keep
-// zero accumulators.
-template <int RT, int NB, int KB, typename FA, typename FB>
-__device__ __forceinline__ void kslice_mma_rt(FA a, FB b, int k0, int k1, const bool (&live)[RT], f32x4 (&acc)[RT][NB]) {
-  for (int k = k0; k < k1; k += 32 * KB) {
-    bf16x8 af[RT][KB];
-    bf16x8 bfr[NB][KB];
-#pragma unroll
-    for (int i = 0; i < KB; ++i) {
-      const int kk = k + 32 * i;
-      const int kc = kk < k1 ? kk : k0;
-#pragma unroll
-      for (int j = 0; j < NB; ++j) bfr[j][i] = b(j, kc);
-#pragma unroll
-      for (int t = 0; t < RT; ++t)
-        if (live[t]) af[t][i] = a(t, kc);
-    }
-#pragma unroll
-    for (int i = 0; i < KB; ++i) {
-      if (k + 32 * i < k1) {
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-          if (live[t])
-#pragma unroll
-            for (int j = 0; j < NB; ++j) acc[t][j] = mfma16(af[t][i], bfr[j][i], acc[t][j]);
-      }
-    }
-  }
-}
-
 // Sum NB tiles across the 4 waves of a 256-thread block.  red: >= 4*NB*256 floats of LDS.
 // Afterwards wave w owns accumulator register r = w of every tile: lane l holds the
 // full sum for C[row = (l>>4)*4 + w][col = l&15] of tile j in out[j].

@@ -134,83 +134,6 @@ __global__ __launch_bounds__(256) void dec_cell_fwd_kernel(
   }
 }
 
-// ---- large-batch training variants (rows per launch >= 512, config #5's 1024-row groups): a block
-// covers RT = 4 row tiles (64 rows) and fetches its weight slice once for all of them -- the 16-row
-// kernels re-read the slice for every 16 rows (2 MB per CU per call from L2 at 1024 rows: dec_cell_fwd
-// 51.8 us, linear2 46.0, dec_bwd_dz 43.1, dec_bwd_cell 42.9 at config #5).  Same math, same per-row
-// epilogues, same K split over the 4 waves and the same summation order (bit-identical results).
-template <int RT>
-__device__ __forceinline__ bool rt_live(const int* dlen, int step, int r0, int B, bool (&live)[RT]) {
-  bool any = false;
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    live[t] = r0 + 16 * t < B && !tile_dead(dlen, step, r0 + 16 * t, B);
-    any |= live[t];
-  }
-  return any;
-}
-
-template <int KB, int RT>
-__global__ __launch_bounds__(256) void dec_cell_fwd_rt_kernel(
-    const float* __restrict__ XG, const bf16* __restrict__ ctxp, const bf16* __restrict__ hprev,
-    const float* __restrict__ cprev, const bf16* __restrict__ WcT, float* __restrict__ c_out,
-    bf16* __restrict__ cb_out, bf16* __restrict__ hb_out, float* __restrict__ act, int B, int H, int A,
-    const int* __restrict__ dlen, int step) {
-  __shared__ float red[4 * RT * 4 * 256];
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int tx, ty;
-  xcd_tile(tx, ty);
-  const int u0 = tx * 16, r0 = ty * 16 * RT;
-  const int G = 4 * H, K = A + H, u = u0 + (lane & 15);
-  bool live[RT];
-  rt_live<RT>(dlen, step, r0, B, live);
-  const int kof = 8 * (lane >> 4);
-  const bf16* crow[RT];
-  const bf16* hrow[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int ar = min(r0 + 16 * t + (lane & 15), B - 1);
-    crow[t] = ctxp ? ctxp + (size_t)ar * A + kof : nullptr;
-    hrow[t] = hprev + (size_t)ar * H + kof - A;
-  }
-  const bf16* W = WcT + (size_t)(u0 + (lane & 15)) * K + kof;
-  const int kbeg = ctxp ? 0 : A;
-  const int nst = (K - kbeg) / 32;
-  const int k0 = kbeg + (wid * nst / 4) * 32, k1 = kbeg + ((wid + 1) * nst / 4) * 32;
-  f32x4 acc[RT][4];
-#pragma unroll
-  for (int t = 0; t < RT; ++t)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) acc[t][g] = f32x4{0, 0, 0, 0};
-  kslice_mma_rt<RT, 4, KB>([&](int t, int k) { return k < A ? ld8(crow[t] + k) : ld8(hrow[t] + k); },
-                           [&](int g, int k) { return ld8(W + (size_t)g * H * K + k); }, k0, k1, live, acc);
-  float z[RT][4];
-  ksplit_reduce<RT * 4>(reinterpret_cast<const f32x4(&)[RT * 4]>(acc), red, reinterpret_cast<float(&)[RT * 4]>(z));
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int r = r0 + 16 * t + (lane >> 4) * 4 + wid;
-    if (r >= B) continue;
-    const size_t ri = (size_t)r * H + u;
-    float* a4 = act ? act + (size_t)r * G : nullptr;
-    if (!live[t]) {  // finite zeros: the head reads every row's state
-      c_out[ri] = 0.f;
-      cb_out[ri] = f2bf(0.f);
-      hb_out[ri] = f2bf(0.f);
-      if (a4) { a4[u] = 0.f; a4[H + u] = 0.f; a4[2 * H + u] = 0.f; a4[3 * H + u] = 0.f; }
-      continue;
-    }
-    const float* xr = XG + (size_t)r * G;
-    const float ig = fsigmoid(z[t][0] + xr[u]), jg = ftanh(z[t][1] + xr[H + u]);
-    const float fg = fsigmoid(z[t][2] + xr[2 * H + u] + 1.0f), og = fsigmoid(z[t][3] + xr[3 * H + u]);
-    const float c = fg * cprev[ri] + ig * jg;
-    const float h = og * ftanh(c);
-    c_out[ri] = c;
-    cb_out[ri] = f2bf(c);
-    hb_out[ri] = f2bf(h);
-    if (a4) { a4[u] = ig; a4[H + u] = jg; a4[2 * H + u] = fg; a4[3 * H + u] = og; }
-  }
-}
-
 // Generic small-M linear on two concatenated bf16 inputs (the shape of every per-step
 // projection of the decoder: s = [c,h].W_s + b, out = [h,ctx].W_o + b, x = x0 + ctx.W_in[E:]):
 //   out[r][n] = sum_{k<K1} a1[r][k] Wt[n][k] + sum_{k<K2} a2[r][k] Wt[n][K1+k] + bias[n] + add[r][n]
@@ -263,48 +186,6 @@ __global__ __launch_bounds__(256) void linear2_kernel(L2Args p, int B) {
   int tx, ty;
   xcd_tile(tx, ty);
   linear2_body<KB>(p, B, tx * 16, ty * 16, red);
-}
-
-// linear2 over RT row tiles per block (training, no beam gathers)
-template <int KB, int RT>
-__global__ __launch_bounds__(256) void linear2_rt_kernel(L2Args p, int B) {
-  __shared__ float red[4 * RT * 256];
-  int tx, ty;
-  xcd_tile(tx, ty);
-  const int n0 = tx * 16, r0 = ty * 16 * RT;
-  bool live[RT];
-  if (!rt_live<RT>(p.dlen, p.step, r0, B, live)) return;  // (nothing reads a dead row's s)
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int kof = 8 * (lane >> 4);
-  const int K1 = p.K1, K = p.K1 + p.K2, N = p.N;
-  const bf16* r1[RT];
-  const bf16* r2[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int ar = min(r0 + 16 * t + (lane & 15), B - 1);
-    r1[t] = p.a1 + (size_t)ar * K1 + kof;
-    r2[t] = p.a2 ? p.a2 + (size_t)ar * p.K2 + kof - K1 : nullptr;
-  }
-  const bf16* brow = p.Wt + (size_t)(n0 + (lane & 15)) * K + kof;
-  const int nst = K / 32;
-  const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
-  f32x4 acc[RT][1];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) acc[t][0] = f32x4{0, 0, 0, 0};
-  kslice_mma_rt<RT, 1, KB>([&](int t, int k) { return k < K1 ? ld8(r1[t] + k) : ld8(r2[t] + k); },
-                           [&](int, int k) { return ld8(brow + k); }, k0, k1, live, acc);
-  float o[RT];
-  ksplit_reduce<RT>(reinterpret_cast<const f32x4(&)[RT]>(acc), red, o);
-  const int n = n0 + (lane & 15);
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int r = r0 + 16 * t + (lane >> 4) * 4 + wid;
-    if (!live[t] || r >= B) continue;
-    const size_t ix = (size_t)r * N + n;
-    const float v = o[t] + (p.bias ? p.bias[n] : 0.f) + (p.add ? p.add[ix] : 0.f);
-    if (p.out) p.out[ix] = v;
-    if (p.outb) p.outb[ix] = f2bf(v);
-  }
 }
 
 // Two independent linear2 problems on the same rows in one launch (blockIdx.z picks the
@@ -405,10 +286,6 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
     const float* __restrict__ dh_rec, float* __restrict__ dc_carry,            // [B][H]
     const float* __restrict__ act, const float* __restrict__ c_now, const float* __restrict__ c_prev,
     bf16* __restrict__ dz, int B, int H, int A, const int* __restrict__ dlen, int step) {
-  // no FMA contraction in the cell backward (here and in dec_bwd_cell_rt_kernel): the 64-row
-  // variant's compiler packs some products across its row tiles, and only uncontracted products
-  // round the same both ways (bit-identical results, tests/test_gpu_decoder_rt.py)
-#pragma clang fp contract(off)
   __shared__ float red[4 * 2 * 256];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int tx, ty;
@@ -461,61 +338,6 @@ __global__ __launch_bounds__(256) void dec_bwd_cell_kernel(
   dzr[u] = f2bf(dzi); dzr[H + u] = f2bf(dzj); dzr[2 * H + u] = f2bf(dzf); dzr[3 * H + u] = f2bf(dzo);
 }
 
-// dec_bwd_cell over RT row tiles per block
-template <int RT>
-__global__ __launch_bounds__(256) void dec_bwd_cell_rt_kernel(
-    const float* __restrict__ ds, const bf16* __restrict__ Ws, const float* __restrict__ dC_dir,
-    const float* __restrict__ dH_dir, const float* __restrict__ dh_rec, float* __restrict__ dc_carry,
-    const float* __restrict__ act, const float* __restrict__ c_now, const float* __restrict__ c_prev,
-    bf16* __restrict__ dz, int B, int H, int A, const int* __restrict__ dlen, int step) {
-#pragma clang fp contract(off)  // as in dec_bwd_cell_kernel
-  __shared__ float red[4 * RT * 2 * 256];
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int tx, ty;
-  xcd_tile(tx, ty);
-  const int u0 = tx * 16, r0 = ty * 16 * RT, u = u0 + (lane & 15);
-  bool live[RT];
-  rt_live<RT>(dlen, step, r0, B, live);
-  const int kof = 8 * (lane >> 4);
-  const float* arow[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) arow[t] = ds + (size_t)min(r0 + 16 * t + (lane & 15), B - 1) * A + kof;
-  const bf16* bc = Ws + (size_t)(u0 + (lane & 15)) * A + kof;
-  const bf16* bh = Ws + (size_t)(H + u0 + (lane & 15)) * A + kof;
-  const int nst = A / 32;
-  const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
-  f32x4 acc[RT][2];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) acc[t][0] = acc[t][1] = f32x4{0, 0, 0, 0};
-  kslice_mma_rt<RT, 2, 2>([&](int t, int k) { return ld8f(arow[t] + k); },
-                          [&](int j, int k) { return ld8((j == 0 ? bc : bh) + k); }, k0, k1, live, acc);
-  float o[RT][2];  // ds . W_s[0:H]^T, ds . W_s[H:2H]^T
-  ksplit_reduce<RT * 2>(reinterpret_cast<const f32x4(&)[RT * 2]>(acc), red, reinterpret_cast<float(&)[RT * 2]>(o));
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int r = r0 + 16 * t + (lane >> 4) * 4 + wid;
-    if (r >= B) continue;
-    bf16* dzr = dz + (size_t)r * 4 * H;
-    if (!live[t]) {  // dz = 0 (read by the weight-gradient GEMMs); dc_carry stays 0
-      dzr[u] = f2bf(0.f); dzr[H + u] = f2bf(0.f); dzr[2 * H + u] = f2bf(0.f); dzr[3 * H + u] = f2bf(0.f);
-      continue;
-    }
-    const size_t ri = (size_t)r * H + u;
-    const float* ap = act + (size_t)r * 4 * H;
-    const float dh = dh_rec[ri] + (dH_dir ? dH_dir[ri] : 0.f) + o[t][1];
-    float dc = dc_carry[ri] + (dC_dir ? dC_dir[ri] : 0.f) + o[t][0];
-    const float ig = ap[u], jg = ap[H + u], fg = ap[2 * H + u], og = ap[3 * H + u];
-    const float tc = ftanh(c_now[ri]);
-    dc += dh * og * (1.0f - tc * tc);
-    const float dzo = dh * tc * og * (1.0f - og);
-    const float dzi = dc * jg * ig * (1.0f - ig);
-    const float dzj = dc * ig * (1.0f - jg * jg);
-    const float dzf = dc * c_prev[ri] * fg * (1.0f - fg);
-    dc_carry[ri] = dc * fg;
-    dzr[u] = f2bf(dzi); dzr[H + u] = f2bf(dzj); dzr[2 * H + u] = f2bf(dzf); dzr[3 * H + u] = f2bf(dzo);
-  }
-}
-
 // [dx_t | dh_{t-1} | dctx_{t-1}] = dz_t . Wbig^T, Wbig = [W_cell ; W_comb]: [E+H+A][4H].
 // grid ((E+H+A)/16, ceil(B/16)).  KB: k-steps per load batch (see the launcher).
 template <int KB>
@@ -564,70 +386,12 @@ __global__ __launch_bounds__(256) void dec_bwd_dz_kernel(
   }
 }
 
-// dec_bwd_dz over RT row tiles per block
-template <int KB, int RT>
-__global__ __launch_bounds__(256) void dec_bwd_dz_rt_kernel(
-    const bf16* __restrict__ dz, const bf16* __restrict__ Wbig, const float* __restrict__ dX_dir,
-    const float* __restrict__ dCTX_dir_prev, float* __restrict__ dx_out, float* __restrict__ dctx_prev_out,
-    float* __restrict__ dh_rec, int B, int E, int H, int A, const int* __restrict__ dlen, int step) {
-  __shared__ float red[4 * RT * 256];
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int tx, ty;
-  xcd_tile(tx, ty);
-  const int n0 = tx * 16, r0 = ty * 16 * RT;
-  if (n0 >= E + H && !dctx_prev_out) return;  // uniform per block
-  bool live[RT];
-  rt_live<RT>(dlen, step, r0, B, live);
-  const int G = 4 * H;
-  const int kof = 8 * (lane >> 4);
-  const bf16* arow[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) arow[t] = dz + (size_t)min(r0 + 16 * t + (lane & 15), B - 1) * G + kof;
-  const bf16* brow = Wbig + (size_t)(n0 + (lane & 15)) * G + kof;
-  const int nst = G / 32;
-  const int k0 = (wid * nst / 4) * 32, k1 = ((wid + 1) * nst / 4) * 32;
-  f32x4 acc[RT][1];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) acc[t][0] = f32x4{0, 0, 0, 0};
-  kslice_mma_rt<RT, 1, KB>([&](int t, int k) { return ld8(arow[t] + k); }, [&](int, int k) { return ld8(brow + k); }, k0,
-                           k1, live, acc);
-  float o[RT];
-  ksplit_reduce<RT>(reinterpret_cast<const f32x4(&)[RT]>(acc), red, o);
-  const int n = n0 + (lane & 15);
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int r = r0 + 16 * t + (lane >> 4) * 4 + wid;
-    if (r >= B) continue;
-    const float v = live[t] ? o[t] : 0.f;  // every output is an exact zero past the last live step
-    if (n < E) {
-      dx_out[(size_t)r * E + n] = v + (live[t] && dX_dir ? dX_dir[(size_t)r * E + n] : 0.f);
-    } else if (n < E + H) {
-      dh_rec[(size_t)r * H + n - E] = v;
-    } else {
-      const int a = n - E - H;
-      dctx_prev_out[(size_t)r * A + a] = v + (live[t] && dCTX_dir_prev ? dCTX_dir_prev[(size_t)r * A + a] : 0.f);
-    }
-  }
-}
-
-// Large-batch variants from this many rows per launch (TSAMD_DEC_RT=0: never)
-static bool dec_rt(int B) {
-  static const int on = getenv("TSAMD_DEC_RT") ? atoi(getenv("TSAMD_DEC_RT")) : 1;
-  return on && B >= 512;
-}
-constexpr int DEC_RT = 4;
-
 // dec_cell_fwd with 6-step load batches: 7.67 -> 6.79 us per call at hidden 256 / 128 rows (one
 // L2 round trip instead of two with 4-step batches), equal at hidden 512; B = 256 train
 // 19.71-19.77 -> 19.63-19.67 ms (profiles/r2/ab/dec_cell_kb.jsonl)
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, const int* dlen,
                          int step, hipStream_t st) {
-  if (dec_rt(B)) {
-    hipLaunchKernelGGL((dec_cell_fwd_rt_kernel<2, DEC_RT>), dim3(H / 16, (B + 16 * DEC_RT - 1) / (16 * DEC_RT)),
-                       dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out, hb_out, act, B, H, A, dlen, step);
-    return;
-  }
   dim3 grid(H / 16, (B + 15) / 16);
   hipLaunchKernelGGL(dec_cell_fwd_kernel<6>, grid, dim3(256), 0, st, XG, ctxp, hprev, cprev, WcT, c_out, cb_out,
                      hb_out, act, B, H, A, BeamGather{nullptr, nullptr, nullptr, 0, 0, nullptr}, dlen, step);
@@ -691,11 +455,6 @@ void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const flo
   L2Args p{cb, H, hb, H, WsT, bs, nullptr, s_out, nullptr, A};
   p.dlen = dlen;
   p.step = step;
-  if (dec_rt(B)) {
-    hipLaunchKernelGGL((linear2_rt_kernel<4, DEC_RT>), dim3(A / 16, (B + 16 * DEC_RT - 1) / (16 * DEC_RT)), dim3(256), 0,
-                       st, p, B);
-    return;
-  }
   L2_LAUNCH(linear2_kernel, H + H, grid, st, p, B);
 }
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
@@ -719,11 +478,6 @@ void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, c
                          const float* dh_rec, float* dc_carry, const float* act, const float* c_now,
                          const float* c_prev, bf16* dz, int B, int H, int A, const int* dlen, int step,
                          hipStream_t st) {
-  if (dec_rt(B)) {
-    hipLaunchKernelGGL(dec_bwd_cell_rt_kernel<DEC_RT>, dim3(H / 16, (B + 16 * DEC_RT - 1) / (16 * DEC_RT)), dim3(256), 0,
-                       st, ds, Ws, dC_dir, dH_dir, dh_rec, dc_carry, act, c_now, c_prev, dz, B, H, A, dlen, step);
-    return;
-  }
   dim3 grid(H / 16, (B + 15) / 16);
   hipLaunchKernelGGL(dec_bwd_cell_kernel, grid, dim3(256), 0, st, ds, Ws, dC_dir, dH_dir, dh_rec, dc_carry, act,
                      c_now, c_prev, dz, B, H, A, dlen, step);
@@ -731,12 +485,6 @@ void launch_dec_bwd_cell(const float* ds, const bf16* Ws, const float* dC_dir, c
 void launch_dec_bwd_dz(const bf16* dz, const bf16* Wbig, const float* dX_dir, const float* dCTX_dir_prev,
                        float* dx_out, float* dctx_prev_out, float* dh_rec, int B, int E, int H, int A,
                        const int* dlen, int step, hipStream_t st) {
-  if (dec_rt(B)) {
-    hipLaunchKernelGGL((dec_bwd_dz_rt_kernel<4, DEC_RT>), dim3((E + H + A) / 16, (B + 16 * DEC_RT - 1) / (16 * DEC_RT)),
-                       dim3(256), 0, st, dz, Wbig, dX_dir, dCTX_dir_prev, dx_out, dctx_prev_out, dh_rec, B, E, H, A, dlen,
-                       step);
-    return;
-  }
   dim3 grid((E + H + A) / 16, (B + 15) / 16);
   // KB = 8 measured equal (5.68 vs 5.74 us at 128 rows, tools/dec_kernels_micro.py) at 96 instead
   // of 41 VGPRs, so this one keeps 4-step batches

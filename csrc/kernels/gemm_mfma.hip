@@ -32,7 +32,6 @@
 // run on one XCD and read the block from its L2.
 #include "common.h"
 #include "launchers.h"
-#include <stdlib.h>
 
 namespace {
 
@@ -74,12 +73,6 @@ __device__ __forceinline__ const bf16* a_row2(const GemmP& p, int m, int h) {
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-template <int N>
-__device__ __forceinline__ void vm_wait_a() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
 }  // namespace
@@ -146,11 +139,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmP& p, const f32x4 (&acc)
 }
 
 // BN: 256 or 128 output columns per workgroup; OUT: 0 fp32, 1 bf16; BETA: C += (fp32 only)
-// P3: the A operand (streamed from HBM) three K tiles deep, B (the L2-resident weight) two: A of
-// tile k + 2 and B of tile k + 1 are in flight while tile k is multiplied, and the wait at the end
-// of a K step is COUNTED (vmcnt = one A tile's loads: A of k + 2 stays in flight across the raw
-// barrier).  160 KB of LDS at BN = 256.  Without P3: both operands two deep, vmcnt(0) + barrier.
-template <int AMODE, int BN, int OUT, bool BETA, bool P3 = false>
+template <int AMODE, int BN, int OUT, bool BETA>
 __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
   constexpr int BM = GM_BM, BK = GM_BK;
   constexpr int WN = BN / 4;           // columns per wave
@@ -197,24 +186,18 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
     const int row = (wid * B_PER_WAVE + i) * 8 + lr;
     bsrc[i] = p.Bt + (size_t)(n0 + row) * p.ldb + ((lc ^ (row & 7)) * 8);
   }
-  // LDS: P3 -> [A0][A1][A2][B0][B1]; else [A0][B0][A1][B1] (stage s = A_s, B_s)
-  auto a_buf = [&](int s) { return smem + (P3 ? s * A_BYTES : s * STAGE); };
-  auto b_buf = [&](int s) { return smem + (P3 ? 3 * A_BYTES + s * B_BYTES : s * STAGE + A_BYTES); };
-  auto load_a = [&](int s, int kt) {
-    char* base = a_buf(s);
+  auto stage_load = [&](int s, int kt) {
+    char* base = smem + s * STAGE;
 #pragma unroll
     for (int i = 0; i < A_PER_WAVE; ++i) {
       const bf16* src = (AMODE == 2 && kt >= nkh) ? asrc1[AMODE == 2 ? i : 0] + (kt - nkh) * BK : asrc[i] + kt * BK;
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(base + ((wid * A_PER_WAVE + i) * 8) * (BK * 2)), 16, 0,
                                        0);
     }
-  };
-  auto load_b = [&](int s, int kt) {
-    char* base = b_buf(s);
 #pragma unroll
     for (int i = 0; i < B_PER_WAVE; ++i)
       __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[i] + kt * BK),
-                                       (lds_ptr_t)(base + ((wid * B_PER_WAVE + i) * 8) * (BK * 2)), 16, 0, 0);
+                                       (lds_ptr_t)(base + A_BYTES + ((wid * B_PER_WAVE + i) * 8) * (BK * 2)), 16, 0, 0);
   };
 
   f32x4 acc[MI][NI];
@@ -226,22 +209,14 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
   const int nk = p.K / BK;
   // fragment read offsets: lane reads row (l & 15) of a subtile, k-chunk kb * 4 + (l >> 4)
   const int fr = lane & 15, fq = lane >> 4;
-  load_a(0, 0);
-  load_b(0, 0);
-  if (P3 && nk > 1) {
-    load_a(1, 1);
-    vm_wait_a<A_PER_WAVE>();  // tile 0 landed, A of tile 1 in flight
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  stage_load(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int s = kt & 1;
-    const char* As = P3 ? a_buf(kt % 3) : a_buf(s);
-    const char* Bs = b_buf(s);
+    if (kt + 1 < nk) stage_load(s ^ 1, kt + 1);
+    const char* As = smem + s * STAGE;
+    const char* Bs = As + A_BYTES;
     if (AMODE == 1 && p.xsf) {  // this workgroup's share of the landed A tile -> the step-frame copy
       const int nrows = (BM - tn + ntn - 1) / ntn;
       for (int pc = tid; pc < nrows * 8; pc += GM_THREADS) {
@@ -249,17 +224,6 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
         if (m < p.M)
           *reinterpret_cast<bf16x8*>(p.xsf + (size_t)m * p.K + kt * BK + c * 8) =
               *reinterpret_cast<const bf16x8*>(As + r * (BK * 2) + ((c ^ (r & 7)) * 16));
-      }
-    }
-    // next loads (after the copy-out's stores: the counted wait below keeps only the newest A
-    // tile's loads outstanding, and older stores must not be among them)
-    if constexpr (P3) {
-      if (kt + 1 < nk) load_b(s ^ 1, kt + 1);
-      if (kt + 2 < nk) load_a((kt + 2) % 3, kt + 2);
-    } else {
-      if (kt + 1 < nk) {
-        load_a(s ^ 1, kt + 1);
-        load_b(s ^ 1, kt + 1);
       }
     }
 #pragma unroll
@@ -285,20 +249,9 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
         for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(afrag[i], bfrag[j], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
-    if constexpr (P3) {
-      // A and B of tile k + 1 landed (A of k + 2 may stay in flight); every wave's fragment
-      // reads of tile k are done (their MFMAs consumed them), so the next step may refill its buffers
-      if (kt + 2 < nk) vm_wait_a<A_PER_WAVE>();
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
-  if constexpr (P3) __syncthreads();  // (drained above) the epilogue reuses the stage LDS
 
   gemm_epilogue<BN, OUT, BETA>(p, acc, smem, m0, n0, wr, wc, wid, lane);
 }
@@ -307,10 +260,7 @@ bool gemm_bt_supported(int M, int N, int K, int BN) {
   return M >= 1 && K >= 64 && K % 64 == 0 && (BN == 256 || BN == 128) && N % BN == 0;
 }
 
-size_t gemm_bt_lds(int BN, bool p3) {
-  return p3 ? 3 * (size_t)(GM_BM * GM_BK * 2) + 2 * (size_t)(BN * GM_BK * 2)
-            : 2 * (size_t)(GM_BM * GM_BK * 2 + BN * GM_BK * 2);
-}
+size_t gemm_bt_lds(int BN) { return 2 * (size_t)(GM_BM * GM_BK * 2 + BN * GM_BK * 2); }
 
 void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, long ldc, bool out_bf16, bool beta,
                     const float* bias, int M, int N, int K, int amode, const int64_t* ids, const int64_t* rev,
@@ -318,26 +268,20 @@ void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, 
   GemmP p{A, Bt, C, bias, ids, rev, xsf, lda, ldb, ldc, nsrc, M, N, K, B, T, dir};
   const int BN = N % 256 == 0 ? 256 : 128;
   const int grid = ((M + GM_BM - 1) / GM_BM) * (N / BN);
-  // TSAMD_GEMM_V=5: the three-deep A pipeline (P3) for the A/B
-  static const int ver = getenv("TSAMD_GEMM_V") ? atoi(getenv("TSAMD_GEMM_V")) : 3;
-  const bool p3 = ver == 5;
-  const size_t lds = gemm_bt_lds(BN, p3);
-#define GLP(AM, BNN, O, BE, PP)                                                                               \
+  const size_t lds = gemm_bt_lds(BN);
+#define GL(AM, BNN, O, BE)                                                                                    \
   do {                                                                                                        \
-    auto kfn = gemm_bt_kernel<AM, BNN, O, BE, PP>;                                                            \
+    auto kfn = gemm_bt_kernel<AM, BNN, O, BE>;                                                                \
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);      \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(GM_THREADS), lds, st, p);                                        \
   } while (0)
-#define GL(AM, BNN, O, BE)          \
-  if (p3) GLP(AM, BNN, O, BE, true); \
-  else GLP(AM, BNN, O, BE, false);
-#define GL_OUT(AM, BNN)                   \
-  if (out_bf16) { GL(AM, BNN, 1, false) } \
-  else if (beta) { GL(AM, BNN, 0, true) } \
-  else { GL(AM, BNN, 0, false) }
+#define GL_OUT(AM, BNN)                 \
+  if (out_bf16) GL(AM, BNN, 1, false);  \
+  else if (beta) GL(AM, BNN, 0, true);  \
+  else GL(AM, BNN, 0, false);
   if (amode == 2) {  // merge: fp32 out, no beta
-    if (BN == 256) { GL(2, 256, 0, false) }
-    else { GL(2, 128, 0, false) }
+    if (BN == 256) GL(2, 256, 0, false);
+    else GL(2, 128, 0, false);
     return;
   }
   if (amode == 0) {
@@ -347,5 +291,4 @@ void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, 
   }
 #undef GL_OUT
 #undef GL
-#undef GLP
 }

@@ -531,14 +531,7 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
     const int RB = (R + VT_ROWS * 2 - 1) / (VT_ROWS * 2);
     // (HFIX at 256 spills 16 VGPRs: the constant split lets all 16 X chunks be hoisted in flight)
     static const bool store = !getenv("TSAMD_VL_STORE") || atoi(getenv("TSAMD_VL_STORE")) != 0;
-    // TSAMD_VL_RH=4: 256-row workgroups, one per CU (196 at V = 50k): every W^T tile fetched once
-    // and the X tile (135 KB of LDS) read by one workgroup per CU instead of two
-    static const int rh = getenv("TSAMD_VL_RH") ? atoi(getenv("TSAMD_VL_RH")) : 2;
-    if (rh == 4 && store) {
-      const int RB4 = (R + VT_ROWS * 4 - 1) / (VT_ROWS * 4);
-      hipLaunchKernelGGL((vocab_logits_kernel<1, 4, 256>), dim3(8 * RB4 * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
-                         logits, part_ms, R, V, H);
-    } else if (store)
+    if (store)
       hipLaunchKernelGGL((vocab_logits_kernel<2, 2, 256>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
                          logits, part_ms, R, V, H);
     else

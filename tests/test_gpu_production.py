@@ -100,9 +100,8 @@ def test_config5_shape_matches_fp32_oracle(B):
     the fp32 oracle, D = 20 decoder steps: B = 8 runs the multi-block attention kernels, B >= 128
     the row-resident forward and backward at A = 1024 (2 / 4 row groups); all use the fused
     H = 512 vocab head; B = 128 the 8-wave persistent LSTM forward and 16-row BPTT, B = 512 the 32-row-team ones,
-    B = 1024 two launches of them and the 64-row-block decoder step kernels (512 rows per row group).
-    The upper layer's input gradients go through the merged two-direction GEMM (gemm_bt_merge)
-    straight into the lower layer's step frame."""
+    B = 1024 two launches of them.  The upper layer's input gradients go through the merged
+    two-direction GEMM (gemm_bt_merge) straight into the lower layer's step frame."""
     hps = HParams(batch_size=B, max_enc_steps=800, max_dec_steps=20, vocab_size=V, coverage=True, pointer_gen=True,
                   hidden_dim=512, emb_dim=128, enc_layers=2, trunc_norm_init_std=0.05)
     kinds = _oracle_check(hps, B, 800, 20, seed=21)
