@@ -612,12 +612,14 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
   }
   auto par = [&](int which, int kb, int jp) -> f32x2 { return prm[((which * NK + kb) * 4 + jp) * 64 + lane]; };
   const float* dxp = dx ? dx + (size_t)b * kEG : nullptr;
-  // the lane's 8 features of dx (position-independent)
-  f32x2 dx2[4];
-#pragma unroll
-  for (int jp = 0; jp < 4; ++jp) {
-    const float2 d = dxp ? *reinterpret_cast<const float2*>(dxp + (lane & 15) * 8 + 2 * jp) : make_float2(0.f, 0.f);
-    dx2[jp] = f32x2{d.x, d.y};
+  // dx (position-independent; lane l uses features (l & 15) * 8 .. + 8) in LDS, not in 8 VGPRs:
+  // with it in registers the 16-wave kernel spilled 3 VGPRs inside the position loop (21.5 vs
+  // 20.1 us per call at B = 256)
+  __shared__ f32x2 dxl[4 * 16];
+  if (tid < 64) {
+    const int c = tid & 15, jp = tid >> 4;
+    const float2 d = dxp ? *reinterpret_cast<const float2*>(dxp + c * 8 + 2 * jp) : make_float2(0.f, 0.f);
+    dxl[jp * 16 + c] = f32x2{d.x, d.y};
   }
   float S = 0.f;
   for (int i = tid; i < len; i += NT) {
@@ -633,7 +635,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
   auto compute = [&](int grp, const Rows<NK>& f, const u32x4& gq, const Scal& x) {
     f32x2 d2 = f32x2{0.f, 0.f};
 #pragma unroll
-    for (int jp = 0; jp < 4; ++jp) d2 = fma2(bf2pair(gq[jp]), dx2[jp], d2);
+    for (int jp = 0; jp < 4; ++jp) d2 = fma2(bf2pair(gq[jp]), dxl[jp * 16 + (lane & 15)], d2);
     const float dot = dpp_sum16(d2.x + d2.y);
     const int p = 4 * grp + qm;
     const float de_q = p < len ? x.a * (x.r + dot - S) : 0.f;
