@@ -301,8 +301,11 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
           st_f4(acts + ((((size_t)d * T + s) * B + r) * H + u) * 4, ga[j][0], ga[j][1], ga[j][2], ga[j][3],
                 NT);  // one 16-byte store per (row, unit)
         }
-        const int t = d == 0 ? s : lj - 1 - s;
-        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(hreg[j]), NT);
+      }
+      if (r < B) {  // h at its position; positions past the length get zeros (no fill of out)
+        const bool live = s < lj;
+        const int t = (d == 0 || !live) ? s : lj - 1 - s;
+        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(live ? hreg[j] : 0.f), NT);
       }
       if (r < B) {
         st_f(cnext + (size_t)r * H + u, creg[j], NT);
@@ -385,8 +388,11 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
       const int r = rc[i];
       if (ss < ln[i]) {
         st_f4(acts + ((((size_t)d * T + ss) * B + r) * H + u) * 4, ga[i][0], ga[i][1], ga[i][2], ga[i][3], NT);
-        const int t = d == 0 ? ss : ln[i] - 1 - ss;
-        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(hreg[i]), NT);
+      }
+      if (rok[i]) {  // h at its position; positions past the length get zeros (no fill of out)
+        const bool live = ss < ln[i];
+        const int t = (d == 0 || !live) ? ss : ln[i] - 1 - ss;
+        st_b(out + ((size_t)r * T + t) * 2 * H + d * H + u, f2bf(live ? hreg[i] : 0.f), NT);
       }
       if (rok[i]) {
         st_f(cnext + (size_t)r * H + u, creg[i], NT);

@@ -41,7 +41,8 @@ def test_persistent_matches_step_kernels(H, B, T):
     for mode in ("step", "persistent"):
         hs, cs = hs0.clone(), cs0.clone()
         acts = torch.zeros(2, T, B, 4 * H, device="cuda")
-        out = torch.zeros(B, T, 2 * H, device="cuda", dtype=torch.bfloat16)
+        # the persistent kernels write every position of out (zeros past the length): start from NaN
+        out = torch.full((B, T, 2 * H), 0.0 if mode == "step" else float("nan"), device="cuda", dtype=torch.bfloat16)
         err = torch.zeros(1, device="cuda", dtype=torch.int32)
         if mode == "step":
             for s in range(T):

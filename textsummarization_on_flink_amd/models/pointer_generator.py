@@ -821,7 +821,8 @@ class HipPointerGenerator:
                     mm_into(st["gx"][di].view(T * B, 4 * H), xs[di].view(T * B, din), self.pk[f"enc{layer}_Kxi{di}"])
             st["hs"][:, 0].zero_()
             st["cs"][:, 0].zero_()
-            st["out"].zero_()
+            if not self.persistent_lstm:  # (the persistent kernels write zeros past each length)
+                st["out"].zero_()
             if self.persistent_lstm:
                 w["lstm_xf"].zero_()  # hand-off tags must start at 0 every launch
                 k.lstm_fwd_persistent(st["gx"], self.f32[f"enc{layer}_b"], self.pk[f"enc{layer}_Wt"], st["hs"], st["cs"], st["acts"], st["out"],
