@@ -441,10 +441,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
   // r-form (see rsig2): with r = 1/(1 + 2^y),
   //   dF  = 4 v sum_t de r(1-r),  dv = sum_t de - 2 sum_t de r,  dwc = 4 v sum_t de cov r(1-r)
   f32x2 w2[4], accv[4], accw[4];
-  float sum_de = 0.f;
-  // v is read again where it is needed (after the step loop), not held in 8 VGPRs across it:
-  // with them the kernel spilled 16 VGPRs at its 128-register cap, one reload inside the loop
-  auto vk = [&](int j) { return kok && k0 + j < A ? v[k0 + j] : 0.f; };
+  float vk[8], sum_de = 0.f;
 #pragma unroll
   for (int jp = 0; jp < 4; ++jp) {
     float wv[2];
@@ -452,6 +449,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
     for (int h = 0; h < 2; ++h) {
       const int j = 2 * jp + h;
       const bool ok = kok && k0 + j < A;
+      vk[j] = ok ? v[k0 + j] : 0.f;
       wv[h] = (ok && wc) ? wc[k0 + j] : 0.f;
     }
     w2[jp] = f32x2{wv[0], wv[1]} * K2LOG2E;
@@ -506,7 +504,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
       if (p0 + q < T) {  // bf16 straight into the GEMM operand; zeros past len
         bf16x8 o8;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o8[j] = f2bf(q < np ? 4.0f * vk(j) * acc[q][j >> 1][j & 1] : 0.f);
+        for (int j = 0; j < 8; ++j) o8[j] = f2bf(q < np ? 4.0f * vk[j] * acc[q][j >> 1][j & 1] : 0.f);
         *reinterpret_cast<bf16x8*>(dF + ((size_t)b * T + p0 + q) * A + k0) = o8;
       }
     }
@@ -518,7 +516,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     adv[j] = sum_de - 2.0f * accv[j >> 1][j & 1];
-    adw[j] = 4.0f * vk(j) * accw[j >> 1][j & 1];
+    adw[j] = 4.0f * vk[j] * accw[j >> 1][j & 1];
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
