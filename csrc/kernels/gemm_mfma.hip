@@ -32,7 +32,6 @@
 // run on one XCD and read the block from its L2.
 #include "common.h"
 #include "launchers.h"
-#include <stdlib.h>
 
 namespace {
 
@@ -74,12 +73,6 @@ __device__ __forceinline__ const bf16* a_row2(const GemmP& p, int m, int h) {
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-template <int N>
-__device__ __forceinline__ void vm_wait_n() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
 }  // namespace
@@ -263,135 +256,6 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
   gemm_epilogue<BN, OUT, BETA>(p, acc, smem, m0, n0, wr, wc, wid, lane);
 }
 
-// ---- staggered schedule (TSAMD_GEMM_V=6 A/B): K in 32-deep slots, a ring of 5 slots (160 KB at
-// BN = 256), slot p + 3 loaded while slot p is multiplied.  The two wave groups (waves 0-3: output
-// rows 0-127, waves 4-7: rows 128-255) run one barrier apart -- group 1 executes one extra barrier
-// first -- so on every SIMD one group's MFMA cluster overlaps the other group's fragment reads and
-// load issue.  Each phase: [issue loads, fragment reads] barrier [MFMAs, counted wait] barrier.
-// Group g loads its own A rows; group 0 (the leader) loads all of B.  Hazards (barrier k of group 0
-// pairs with barrier k + 1 of group 1):
-//   RAW  a wave reads slot p only after a barrier that follows the wait retiring the loads of p: its
-//        own A (waited before its previous phase's second barrier) and group 0's B (waited by
-//        group 0 before its B2(p - 1), which precedes the barrier group 1 passed);
-//   WAR  slot p + 3 goes to the ring position of slot p - 2, whose last reads (group 1, phase p - 2)
-//        were retired by lgkmcnt before group 1's B2(p - 2), paired with group 0's B1(p - 1).
-template <int AMODE, int BN, int OUT, bool BETA>
-__global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt6_kernel(GemmP p) {
-  constexpr int BM = GM_BM, BK = 32, NSLOT = 5;
-  constexpr int WN = BN / 4, NI = WN / 16, MI = 128 / 16;
-  constexpr int ROWB = BK * 2;  // 64-byte LDS rows
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, SLOT = A_BYTES + B_BYTES;
-  constexpr int A_PW = 128 / 16 / 4;  // glds pieces (16 rows) per wave for its group's A half: 2
-  constexpr int B_PW = BN / 16 / 4;   // group 0's waves for B: 4 (BN 256) / 2 (BN 128)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int wr = wid >> 2, wc = wid & 3, gw = wid & 3;  // group, column quarter, wave in group
-  const int ntn = p.N / BN, ntm = (p.M + BM - 1) / BM, nwg = ntn * ntm;
-  const int id = blockIdx.x, xcd = id & 7, q = nwg >> 3, r8 = nwg & 7;
-  const int lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (id >> 3);
-  const int tm = lin / ntn, tn = lin - tm * ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int lr = lane >> 2, lc = lane & 3;  // piece: 16 rows x 4 chunks of 16 bytes
-  const bf16* asrc[A_PW];
-  const bf16* asrc1[AMODE == 2 ? A_PW : 1];
-#pragma unroll
-  for (int i = 0; i < A_PW; ++i) {
-    const int row = wr * 128 + (gw * A_PW + i) * 16 + lr;
-    const int sw = (lc ^ ((row >> 2) & 3)) * 8;
-    if constexpr (AMODE == 2) {
-      asrc[i] = a_row2(p, m0 + row, 0) + sw;
-      asrc1[i] = a_row2(p, m0 + row, 1) + sw;
-    } else {
-      asrc[i] = a_row(p, m0 + row, AMODE) + sw;
-    }
-  }
-  const int nkh = p.K / (2 * BK);
-  const bf16* bsrc[B_PW];
-#pragma unroll
-  for (int i = 0; i < B_PW; ++i) {
-    const int row = (gw * B_PW + i) * 16 + lr;
-    bsrc[i] = p.Bt + (size_t)(n0 + row) * p.ldb + ((lc ^ ((row >> 2) & 3)) * 8);
-  }
-  auto load_slot = [&](int kt) {  // this wave's share of slot kt
-    char* base = smem + (kt % NSLOT) * SLOT;
-#pragma unroll
-    for (int i = 0; i < A_PW; ++i) {
-      const bf16* src = (AMODE == 2 && kt >= nkh) ? asrc1[AMODE == 2 ? i : 0] + (kt - nkh) * BK : asrc[i] + kt * BK;
-      __builtin_amdgcn_global_load_lds((gbl_ptr_t)src,
-                                       (lds_ptr_t)(base + (wr * 128 + (gw * A_PW + i) * 16) * ROWB), 16, 0, 0);
-    }
-    if (wr == 0) {
-#pragma unroll
-      for (int i = 0; i < B_PW; ++i)
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(bsrc[i] + kt * BK),
-                                         (lds_ptr_t)(base + A_BYTES + ((gw * B_PW + i) * 16) * ROWB), 16, 0, 0);
-    }
-  };
-  // counted wait: at most `after` slots newer than the one needed may stay in flight
-  auto wait_slots = [&](int after) {
-    if (wr == 0) {
-      if (after >= 2) vm_wait_n<2 * (A_PW + B_PW)>();
-      else if (after == 1) vm_wait_n<A_PW + B_PW>();
-      else vm_wait_n<0>();
-    } else {
-      if (after >= 2) vm_wait_n<2 * A_PW>();
-      else if (after == 1) vm_wait_n<A_PW>();
-      else vm_wait_n<0>();
-    }
-  };
-  auto barrier = [&]() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  f32x4 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = p.K / BK;
-  const int fr = lane & 15, fq = lane >> 4;
-  // prologue: slots 0, 1, 2 in flight; slot 0 retired; group 1 then takes one extra barrier
-#pragma unroll
-  for (int s = 0; s < 3; ++s)
-    if (s < nk) load_slot(s);
-  wait_slots(min(2, nk - 1));
-  barrier();
-  if (wr == 1) barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    // ---- segment A: next loads, this slot's fragments
-    if (kt + 3 < nk) load_slot(kt + 3);
-    const char* As = smem + (kt % NSLOT) * SLOT;
-    const char* Bs = As + A_BYTES;
-    bf16x8 bfrag[NI], afrag[MI];
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int row = wc * WN + j * 16 + fr;
-      bfrag[j] = *reinterpret_cast<const bf16x8*>(Bs + row * ROWB + ((fq ^ ((row >> 2) & 3)) * 16));
-    }
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int row = wr * 128 + i * 16 + fr;
-      afrag[i] = *reinterpret_cast<const bf16x8*>(As + row * ROWB + ((fq ^ ((row >> 2) & 3)) * 16));
-    }
-    barrier();
-    // ---- segment B: MFMAs, then retire the next slot's loads
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(afrag[i], bfrag[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    if (kt + 1 < nk) wait_slots(min(2, nk - 2 - kt));
-    barrier();
-  }
-  if (wr == 0) barrier();  // group 0 takes the barrier group 1 took first: counts match again
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // the epilogue reuses the ring
-  gemm_epilogue<BN, OUT, BETA>(p, acc, smem, m0, n0, wr, wc, wid, lane);
-}
-
 bool gemm_bt_supported(int M, int N, int K, int BN) {
   return M >= 1 && K >= 64 && K % 64 == 0 && (BN == 256 || BN == 128) && N % BN == 0;
 }
@@ -415,32 +279,6 @@ void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, 
   if (out_bf16) GL(AM, BNN, 1, false);  \
   else if (beta) GL(AM, BNN, 0, true);  \
   else GL(AM, BNN, 0, false);
-  // TSAMD_GEMM_V=6: the staggered 5-slot schedule (gemm_bt6_kernel; no step-frame copy-out: xsf
-  // calls stay on the two-stage kernel)
-  static const int ver = getenv("TSAMD_GEMM_V") ? atoi(getenv("TSAMD_GEMM_V")) : 3;
-  if (ver == 6 && !xsf) {
-    const size_t lds6 = 5 * (size_t)(GM_BM * 64 + BN * 64);
-#define GL6(AM, BNN, O, BE)                                                                                   \
-  do {                                                                                                        \
-    auto kfn = gemm_bt6_kernel<AM, BNN, O, BE>;                                                               \
-    (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds6);     \
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(GM_THREADS), lds6, st, p);                                       \
-  } while (0)
-#define GL6_OUT(AM, BNN)                    \
-  if (out_bf16) { GL6(AM, BNN, 1, false); } \
-  else if (beta) { GL6(AM, BNN, 0, true); } \
-  else { GL6(AM, BNN, 0, false); }
-    if (amode == 2) {
-      if (BN == 256) { GL6(2, 256, 0, false); } else { GL6(2, 128, 0, false); }
-    } else if (amode == 0) {
-      if (BN == 256) { GL6_OUT(0, 256) } else { GL6_OUT(0, 128) }
-    } else {
-      if (BN == 256) { GL6_OUT(1, 256) } else { GL6_OUT(1, 128) }
-    }
-#undef GL6_OUT
-#undef GL6
-    return;
-  }
   if (amode == 2) {  // merge: fp32 out, no beta
     if (BN == 256) GL(2, 256, 0, false);
     else GL(2, 128, 0, false);
