@@ -89,6 +89,28 @@ void lstm_fwd_persistent(const Tensor& gx, const Tensor& bias, const Tensor& Wt,
                              stream());
 }
 
+// the input projection of encoder layer 0 inside the recurrence: xsf = step-frame inputs
+// [2][T][B][128] (bf16), Wx0 / Wx1 = W_x^T of each direction [4H][128] (row u * 4 + g)
+bool lstm_persistent_fx_ok_op(int64_t H, int64_t B, int64_t E) { return lstm_persistent_fx_ok((int)H, (int)B, (int)E); }
+void lstm_fwd_persistent_fx(const Tensor& xsf, const Tensor& Wx0, const Tensor& Wx1, const Tensor& bias,
+                            const Tensor& Wt, const Tensor& hs, const Tensor& cs, const Tensor& acts, const Tensor& out,
+                            const Tensor& lens, const Tensor& xbuf, const Tensor& err, int64_t T, int64_t B, int64_t H) {
+  chk(xsf, BF, "xsf"); chk(Wx0, BF, "Wx0"); chk(Wx1, BF, "Wx1");
+  chk(bias, F32, "bias"); numel_eq(bias, 2 * 4 * H, "bias"); chk(Wt, BF, "Wt"); chk(hs, BF, "hs"); chk(cs, F32, "cs");
+  chk(acts, F32, "acts"); chk(out, BF, "out"); chk(lens, I32, "lens"); chk(xbuf, at::kLong, "xbuf"); chk(err, I32, "err");
+  TORCH_CHECK(lstm_persistent_fx_ok((int)H, (int)B, 128), "persistent LSTM with the input projection: unsupported H/B");
+  TORCH_CHECK(T >= 1 && T < (1 << 30), "bad T");
+  numel_eq(xsf, 2 * T * B * 128, "xsf"); numel_eq(Wx0, 4 * H * 128, "Wx0"); numel_eq(Wx1, 4 * H * 128, "Wx1");
+  numel_eq(Wt, 2 * 4 * H * H, "Wt");
+  numel_eq(hs, 2 * (T + 1) * B * H, "hs"); numel_eq(cs, 2 * (T + 1) * B * H, "cs");
+  numel_eq(acts, 2 * T * B * 4 * H, "acts"); numel_eq(out, B * T * 2 * H, "out"); numel_eq(lens, B, "lens");
+  TORCH_CHECK(xbuf.numel() >= (int64_t)lstm_persistent_xbuf_elems((int)H, (int)B, false), "xbuf too small");
+  numel_eq(err, 1, "err");
+  launch_lstm_fwd_persistent(nullptr, P<float>(bias), P<bf16>(Wt), P<bf16>(hs), P<float>(cs), P<float>(acts), P<bf16>(out),
+                             P<int>(lens), (unsigned long long*)xbuf.data_ptr(), (unsigned*)err.data_ptr(), T, B, H,
+                             stream(), P<bf16>(xsf), P<bf16>(Wx0), P<bf16>(Wx1));
+}
+
 void lstm_bwd_persistent(const Tensor& dz, const Tensor& Wn, const Tensor& dout, const Tensor& dh_fin,
                          const Tensor& dc_carry, const Tensor& acts, const Tensor& cs, const Tensor& lens,
                          const Tensor& xbuf, const Tensor& err, const OT& dbias, int64_t T, int64_t B, int64_t H,
@@ -984,6 +1006,8 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("rs_bwd", &rs_bwd);
   m.def("lstm_persistent_xbuf", &lstm_persistent_xbuf_op);
   m.def("lstm_fwd_persistent", &lstm_fwd_persistent);
+  m.def("lstm_fwd_persistent_fx", &lstm_fwd_persistent_fx);
+  m.def("lstm_persistent_fx_ok", &lstm_persistent_fx_ok_op);
   m.def("lstm_bwd_persistent", &lstm_bwd_persistent);
   m.def("attn_score", &attn_score);
   m.def("attn_softmax_ctx", &attn_softmax_ctx);

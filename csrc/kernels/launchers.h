@@ -104,7 +104,9 @@ int lstm_persistent_launches(int H, int B);
 size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd);
 void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
-                                int H, hipStream_t st);
+                                int H, hipStream_t st, const bf16* xsf = nullptr, const bf16* Wx0 = nullptr,
+                                const bf16* Wx1 = nullptr);
+bool lstm_persistent_fx_ok(int H, int B, int E);
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, float* dbias, int T, int B, int H, bool dout_bf, hipStream_t st);

@@ -129,18 +129,35 @@ __device__ __forceinline__ bool team_of(int NC, int nteams, int& team, int& c) {
 // 2 launches instead of 4).  At H = 512 the 4 waves x 16 units x 4 gates need 256 VGPRs of
 // W_hh B fragments per lane: launch bounds (256, 1) leave one wave per SIMD and the 512
 // unified registers (arch + acc) for them.
-template <int H, bool NT, int RT = 1>
+//
+// FX (layer 0, E = 128): the input projection x.W_x is computed HERE instead of by a GEMM
+// writing gx (fp32 [2][T][B][4H]: 13.4 GB per direction at config #5 batch 2048, 420 MB at
+// the bench shape).  The step-frame inputs xsf [2][T][B][128] (bf16, one gather launch) are
+// read a step ahead; the x MFMAs of step s run before the step's hand-off sweep, i.e. in the
+// shadow of the wait for the team's h_s, not on the recurrence's critical path.  W_x
+// fragments: registers at RT = 1 (64 VGPRs), LDS at RT = 2 (64 KB; registers are full), where
+// x is staged into LDS by global_load_lds (XOR-swizzled 16-byte chunks) and the x part of
+// the gates waits in Gsh (the slots the cell update overwrites with the activations) --
+// Ash is single-buffered there to make room: a wave only rewrites Ash after its sweep saw
+// h_{s+1} of every wave of the team, each published after that wave's MFMAs read Ash.
+template <int H, bool NT, int RT = 1, bool FX = false>
 __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     const float* __restrict__ gx, const float* __restrict__ bias, const bf16* __restrict__ Wt,
     bf16* __restrict__ hs, float* __restrict__ cs, float* __restrict__ acts, bf16* __restrict__ out,
-    const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile, int tile0, int ntile_l) {
+    const int* __restrict__ lens, gu64* xbuf, gu32* err, int T, int B, int ntile, int tile0, int ntile_l,
+    const bf16* __restrict__ xsf, const bf16* __restrict__ Wx0, const bf16* __restrict__ Wx1) {
   constexpr int KS = H / 32, NC = H / 64, HP = H / 2, R = 16 * RT, G = R * HP, NPL = G / 256;
   constexpr int CH = NPL < 8 ? NPL : 8;  // granules per lane per sweep (chunks keep x[] at 16 VGPRs)
   constexpr int NR = 4 * RT;             // rows per lane
+  constexpr int KE = 128, KSX = KE / 32; // FX: input width, its 32-deep MFMA steps
+  constexpr bool FXL = FX && RT > 1;     // FX with W_x / x in LDS
   static_assert(NPL % CH == 0, "sweep chunks");
-  __shared__ __attribute__((aligned(16))) bf16 Ash[2][R * H];
+  __shared__ __attribute__((aligned(16))) bf16 Ash[FXL ? 1 : 2][R * H];
   // RT = 2: the step's gate activations wait here (not in registers) until the hand-off is out
   __shared__ __attribute__((aligned(16))) float Gsh[RT > 1 ? 256 * NR * 4 : 4];
+  // FXL: x rows of steps s / s + 1 [2][R][128] and this workgroup's W_x fragments [wave][gate][kk][lane]
+  __shared__ __attribute__((aligned(16))) bf16 Xsh[FXL ? 2 * R * KE : 8];
+  __shared__ __attribute__((aligned(16))) bf16x8 Wxs[FXL ? 4 * 4 * KSX * 64 : 1];
   int lt, c;
   if (!team_of(NC, 2 * ntile_l, lt, c)) return;
   const int d = lt / ntile_l, tile = tile0 + lt % ntile_l, r0 = tile * R, team = d * ntile + tile;
@@ -173,12 +190,46 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   }
   gu64* xb = xbuf + (size_t)team * 2 * G;
   bool dead = false;
+  // FX: W_x B fragments of this lane's unit (row u * 4 + g of W_x^T [4H][128])
+  bf16x8 Wxf[FX && !FXL ? 4 : 1][FX && !FXL ? KSX : 1];
+  if constexpr (FX) {
+    const bf16* Wx = d ? Wx1 : Wx0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int kk = 0; kk < KSX; ++kk) {
+        const bf16x8 wv = ld8(Wx + (size_t)(u * 4 + g) * KE + kk * 32 + 8 * (lane >> 4));
+        if constexpr (FXL) Wxs[((wid * 4 + g) * KSX + kk) * 64 + lane] = wv;  // read back by this wave only
+        else Wxf[g][kk] = wv;
+      }
+  }
+  // FX: x rows of step st (tile rows, clamped to the batch) -- RT = 1 as A fragments in
+  // registers (xan), RT = 2 into Xsh[st & 1] (wave w stages rows 8w .. 8w + 7, 1 KB per instruction)
+  bf16x8 xan[FX && !FXL ? KSX : 1];
+  auto load_x = [&](int st) {
+    if constexpr (FXL) {
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int row = (wid * 2 + q) * 4 + (ln >> 4), cg = (ln & 15) ^ (row & 7);
+        const bf16* src = xsf + (((size_t)d * T + st) * B + min(r0 + row, B - 1)) * KE + cg * 8;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)&Xsh[(st & 1) * R * KE + (wid * 2 + q) * 512],
+                                         16, 0, 0);
+      }
+    } else {
+      const bf16* src = xsf + (((size_t)d * T + st) * B + min(r0 + (lane & 15), B - 1)) * KE + 8 * (lane >> 4);
+#pragma unroll
+      for (int kk = 0; kk < KSX; ++kk) xan[kk] = ld8(src + kk * 32);
+    }
+  };
   // gate pre-activations x.W_x of step s + 1 are loaded during step s (off the recurrence's
   // critical path: an HBM round trip per step otherwise)
   // RT = 1: in registers (gzn); RT = 2: straight into LDS (Gxsh, one global_load_lds_dwordx4
   // per row and lane: lane-linear 1 KB per wave instruction), no VGPRs
-  float gzn[RT > 1 ? 1 : NR][4];
-  __shared__ __attribute__((aligned(16))) float Gxsh[RT > 1 ? 4 * NR * 64 * 4 : 4];
+  float gzn[RT > 1 || FX ? 1 : NR][4];
+  __shared__ __attribute__((aligned(16))) float Gxsh[RT > 1 && !FX ? 4 * NR * 64 * 4 : 4];
   auto load_gz = [&](int st) {
     const float* gxs = gx + ((size_t)d * T + st) * B * G4;
 #pragma unroll
@@ -193,13 +244,53 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       }
     }
   };
-  load_gz(0);
+  if constexpr (FX) load_x(0);
+  else load_gz(0);
   for (int s = 0; s < T; ++s) {
-    const int buf = s & 1;
+    const int buf = FXL ? 0 : s & 1;
+    f32x4 acc[RT][4];
+    // FX: the x part of the gates, before the sweep (the wait for h_s hides it)
+    if constexpr (FX && !FXL) {
+      bf16x8 xa[KSX];
+#pragma unroll
+      for (int kk = 0; kk < KSX; ++kk) xa[kk] = xan[kk];
+      if (s + 1 < T) load_x(s + 1);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        acc[0][g] = f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int kk = 0; kk < KSX; ++kk) acc[0][g] = mfma16(xa[kk], Wxf[g][kk], acc[0][g]);
+      }
+    } else if constexpr (FXL) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's Xsh pieces of step s landed
+      __syncthreads();                      // ... and every wave's
+      const bf16* xs = &Xsh[(s & 1) * R * KE];
+      // opaque per step: keeps the loop-invariant W_x fragment reads in the loop (hoisted, they
+      // would hold 64 VGPRs for the whole launch and spill)
+      // (and the lane's Xsh offsets: recomputed per step, not held)
+      int wb = wid * 4 * KSX * 64 + lane, ln = lane;
+      asm volatile("" : "+v"(wb), "+v"(ln));
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int row = rt * 16 + (ln & 15);
+        bf16x8 xa[KSX];
+#pragma unroll
+        for (int kk = 0; kk < KSX; ++kk)
+          xa[kk] = *reinterpret_cast<const bf16x8*>(&xs[row * KE + (((kk * 4 + (ln >> 4)) ^ (row & 7)) << 3)]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 xz = f32x4{0, 0, 0, 0};
+#pragma unroll
+          for (int kk = 0; kk < KSX; ++kk) xz = mfma16(xa[kk], Wxs[wb + (g * KSX + kk) * 64], xz);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) Gsh[((rt * 4 + i) * 256 + threadIdx.x) * 4 + g] = xz[i];
+        }
+      }
+    }
     // RT = 1: the next step's x.W_x is requested now and the current one kept in gz; RT = 2
     // (no registers for two copies): requested after this step's cell update consumed gzn
-    float gz[RT > 1 ? 1 : NR][4];
-    if constexpr (RT == 1) {
+    float gz[RT > 1 || FX ? 1 : NR][4];
+    if constexpr (RT == 1 && !FX) {
 #pragma unroll
       for (int j = 0; j < NR; ++j)
 #pragma unroll
@@ -228,13 +319,14 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       }
     }
     __syncthreads();
-    if constexpr (RT > 1) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's Gxsh landed
+    if constexpr (RT > 1 && !FX) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's Gxsh landed
     // ---- z = h_s . W_hh for this wave's 16 units x 4 gates (B operands in registers)
-    f32x4 acc[RT][4];
+    if constexpr (!(FX && !FXL)) {
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) acc[rt][g] = f32x4{0, 0, 0, 0};
+        for (int g = 0; g < 4; ++g) acc[rt][g] = f32x4{0, 0, 0, 0};
+    }
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
@@ -255,7 +347,12 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       if (s < lnsh[rowof(j) - r0]) {
         float* z = ga[RT > 1 ? 0 : j];
         float xv[4];
-        if constexpr (RT > 1) {
+        if constexpr (FX && !FXL) {
+          xv[0] = xv[1] = xv[2] = xv[3] = 0.f;  // already in acc
+        } else if constexpr (FXL) {
+          const float4 q = *reinterpret_cast<const float4*>(&Gsh[(j * 256 + threadIdx.x) * 4]);
+          xv[0] = q.x; xv[1] = q.y; xv[2] = q.z; xv[3] = q.w;
+        } else if constexpr (RT > 1) {
           const float4 q = *reinterpret_cast<const float4*>(&Gxsh[((wid * NR + j) * 64 + lane) * 4]);
           xv[0] = q.x; xv[1] = q.y; xv[2] = q.z; xv[3] = q.w;
         } else {
@@ -274,7 +371,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
           *reinterpret_cast<float4*>(&Gsh[(j * 256 + threadIdx.x) * 4]) = make_float4(z[0], z[1], z[2], z[3]);
       }
     }
-    if constexpr (RT > 1) {
+    if constexpr (FXL) {
+      if (s + 1 < T) load_x(s + 1);
+    } else if constexpr (RT > 1 && !FX) {
       if (s + 1 < T) load_gz(s + 1);
     }
     // ---- publish h_{s+1}: unit pairs (u, u+1) of adjacent lanes -> one granule
@@ -290,9 +389,13 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     }
     float* cnext = cs + ((size_t)d * (T + 1) + s + 1) * BH;
     bf16* hnext = hs + ((size_t)d * (T + 1) + s + 1) * BH;
+    // FXL: the rows' store addresses recomputed per step from an opaque lane (held for the
+    // launch they spill, and the reloads wait behind the step's outstanding stores)
+    int sl = lane;
+    if constexpr (FXL) asm volatile("" : "+v"(sl));
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
-      const int r = rowof(j), lj = lnsh[r - r0];
+      const int r = r0 + (j >> 2) * 16 + (sl >> 4) * 4 + (j & 3), lj = lnsh[r - r0];
       if (s < lj) {
         if constexpr (RT > 1) {
           const float4 z = *reinterpret_cast<const float4*>(&Gsh[(j * 256 + threadIdx.x) * 4]);
@@ -960,8 +1063,15 @@ int lstm_persistent_capacity(int H) {
     if (HH <= 256) {                                                                                               \
       ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[3], lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), true>, \
                                                          256, 0) == hipSuccess;                                    \
+      int ofx = 0;                                                                                                 \
+      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                          \
+                &ofx, lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), true, 1, true>, 256, 0) == hipSuccess;    \
+      o[3] = min(o[3], ofx);                                                                                       \
     } else {                                                                                                       \
       ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o[2], lstm_fwd_persistent_kernel<512, true, 2>, 256, 0) == hipSuccess; \
+      int ofx = 0;                                                                                                 \
+      ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&ofx, lstm_fwd_persistent_kernel<512, true, 2, true>, 256, 0) == hipSuccess; \
+      o[2] = min(o[2], ofx);                                                                                       \
       int o32 = 0;                                                                                                 \
       ok &= hipOccupancyMaxActiveBlocksPerMultiprocessor(&o32, lstm_bwd_persistent32_kernel<false>, 1024, 0) == hipSuccess; \
       o[2] = min(o[2], o32);                                                                                      \
@@ -1030,31 +1140,44 @@ size_t lstm_persistent_xbuf_elems(int H, int B, bool bwd) {
   return (size_t)2 * ntile * 2 * (bwd ? (size_t)NC * NC * R * 64 : (size_t)R * (H / 2));
 }
 
+// FX (the input projection inside the recurrence, E = 128): the 4-wave kernels only -- the
+// 8-wave H = 512 kernel (batch <= 256) has no registers or LDS left for W_x
+bool lstm_persistent_fx_ok(int H, int B, int E) {
+  return E == 128 && lstm_persistent_grid(H, B) > 0 && (lstm_rows(H, B, false) == 32 || lstm_nw(H) == 4);
+}
+
 void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* Wt, bf16* hs, float* cs, float* acts,
                                 bf16* out, const int* lens, unsigned long long* xbuf, unsigned* err, int T, int B,
-                                int H, hipStream_t st) {
+                                int H, hipStream_t st, const bf16* xsf, const bf16* Wx0, const bf16* Wx1) {
   const int R = lstm_rows(H, B, false), ntile = (B + R - 1) / R, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64;
   const int nw = R == 32 ? 4 : lstm_nw(H);
   if (nl <= 0) return;
+  const bool fx = xsf != nullptr;
+  if (fx && nw != 4) return;  // the binding checks lstm_persistent_fx_ok first
   gu64* xb = (gu64*)xbuf;
   gu32* e = (gu32*)err;
   for (int t0 = 0; t0 < ntile; t0 += nl) {
     const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
+#define ARGS gx, bias, Wt, hs, cs, acts, out, lens, xb, e, T, B, ntile, t0, n, xsf, Wx0, Wx1
 #define LAUNCH_F(HH, NTV)                                                                                            \
-  if (nw == 8)                                                                                                  \
+  if (fx && R == 32)                                                                                            \
+    hipLaunchKernelGGL((lstm_fwd_persistent_kernel<512, NTV, 2, true>), dim3(grid), dim3(256), 0, st, ARGS);    \
+  else if (fx)                                                                                                  \
+    hipLaunchKernelGGL((lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), NTV, 1, true>), dim3(grid), dim3(256), \
+                       0, st, ARGS);                                                                            \
+  else if (nw == 8)                                                                                             \
     hipLaunchKernelGGL((lstm_fwd_persistent8_kernel<HH, NTV>), dim3(grid), dim3(512), 0, st, gx, bias, Wt, hs, cs, \
                        acts, out, lens, xb, e, T, B, ntile, t0, n);                                             \
   else if (R == 32)                                                                                             \
-    hipLaunchKernelGGL((lstm_fwd_persistent_kernel<512, NTV, 2>), dim3(grid), dim3(256), 0, st, gx, bias, Wt, hs, \
-                       cs, acts, out, lens, xb, e, T, B, ntile, t0, n);                                         \
+    hipLaunchKernelGGL((lstm_fwd_persistent_kernel<512, NTV, 2>), dim3(grid), dim3(256), 0, st, ARGS);          \
   else                                                                                                          \
-    hipLaunchKernelGGL((lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), NTV>), dim3(grid), dim3(256), 0, st, \
-                       gx, bias, Wt, hs, cs, acts, out, lens, xb, e, T, B, ntile, t0, n)
+    hipLaunchKernelGGL((lstm_fwd_persistent_kernel<(HH <= 256 ? HH : 256), NTV>), dim3(grid), dim3(256), 0, st, ARGS)
     if (H == 64) LAUNCH_F(64, true);
     else if (H == 128) LAUNCH_F(128, true);
     else if (H == 256) LAUNCH_F(256, true);
     else LAUNCH_F(512, true);
 #undef LAUNCH_F
+#undef ARGS
   }
 }
 

@@ -208,3 +208,45 @@ def test_persistent_lstm_stress_full_grid(H, B):
     torch.cuda.synchronize()
     assert int(err.item()) == 0
     assert torch.equal(out, ref[0]) and torch.equal(dz, ref[1])
+
+
+# The input projection inside the recurrence (FX, encoder layer 0, E = 128) against the same
+# recurrence fed gx = x . W_x from an fp32 matmul: 4-wave H <= 256 kernels (W_x in registers),
+# the H = 512 32-row-team kernel (W_x / x staged in LDS, single-buffered h tile), several
+# launches over row-tile ranges (256, 600), and a partial last tile (512, 300).
+@pytest.mark.parametrize("H,B,T", [(64, 16, 9), (128, 37, 20), (256, 64, 33), (256, 600, 7), (512, 300, 9),
+                                   (512, 512, 40)])
+def test_persistent_input_projection_matches_gx_path(H, B, T):
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    E = 128
+    assert bool(k.lstm_persistent_fx_ok(H, B, E))
+    g, r, lens, _, Wt, _, hs0, cs0 = _setup(H, B, T, 11 + H + B)
+    xsf = r(2, T, B, E, sc=0.5).bfloat16()
+    WxT = r(2, 4 * H, E, sc=1.0 / E ** 0.5).bfloat16()           # [d][u * 4 + g][E]
+    bias = torch.randn(2, 4 * H, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5)) * 0.2
+    gx = torch.stack([xsf[d].float().reshape(T * B, E) @ WxT[d].float().t() for d in range(2)]).view(2, T, B, 4 * H)
+    res = {}
+    for mode in ("gx", "fx"):
+        hs, cs = hs0.clone(), cs0.clone()
+        acts = torch.full((2, T, B, 4 * H), float("nan"), device="cuda")
+        out = torch.full((B, T, 2 * H), float("nan"), device="cuda", dtype=torch.bfloat16)
+        err = torch.zeros(1, device="cuda", dtype=torch.int32)
+        xf = torch.zeros(int(k.lstm_persistent_xbuf(H, B, False)), device="cuda", dtype=torch.long)
+        if mode == "gx":
+            k.lstm_fwd_persistent(gx, bias, Wt, hs, cs, acts, out, lens, xf, err, T, B, H)
+        else:
+            k.lstm_fwd_persistent_fx(xsf, WxT[0].contiguous(), WxT[1].contiguous(), bias, Wt, hs, cs, acts, out, lens,
+                                     xf, err, T, B, H)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        res[mode] = (hs, cs, acts, out)
+    t = torch.arange(T, device="cuda")
+    live = (t[None, :] < lens.long()[:, None]).t()                # [T][B]
+    for name, a, b in zip(("hs", "cs"), res["gx"][:2], res["fx"][:2]):
+        torch.testing.assert_close(b.float(), a.float(), rtol=2e-2, atol=2e-2, msg=name)
+    ag, af = res["gx"][2], res["fx"][2]
+    m = live[None, :, :, None].expand_as(ag)
+    torch.testing.assert_close(af[m], ag[m], rtol=1e-2, atol=1e-2)
+    assert not torch.isnan(res["fx"][3]).any()                    # every out position written
+    torch.testing.assert_close(res["fx"][3].float(), res["gx"][3].float(), rtol=2e-2, atol=2e-2)

@@ -83,6 +83,11 @@ _BT_TIMES: Dict[tuple, tuple] = {}
 # GEMM (N = E = 128, one 128-column tile) measured 0.1 ms slower at batch 256
 # (profiles/r5/dx_merge.md).
 DX_MERGE = os.environ.get("TSAMD_DX_MERGE", "1") != "0"
+# TSAMD_LSTM_FX=0: encoder layer 0's input projection x.W_x as a GEMM writing gx (fp32
+# [2][T][B][4H]) before the persistent recurrence.  Default: inside the recurrence
+# (lstm_persistent.hip FX): the step-frame inputs (bf16, E = 128) are gathered once and each
+# step's x MFMAs run in the shadow of the hand-off wait -- no gx GEMM, no gx buffer.
+LSTM_FX = os.environ.get("TSAMD_LSTM_FX", "1") != "0"
 # the step-frame gather path replaces to_step_frame + the GEMM: kept while the gather GEMM is at
 # most this much slower than the library GEMM alone (the layout pass it saves costs ~25-40 % of it)
 FRAME_SLACK = 1.25
@@ -430,6 +435,9 @@ class HipPointerGenerator:
         # upper encoder layers' input gradients through the merged hand-written GEMM (no dxs)
         self.dx_merge = (DX_MERGE and L > 1 and BLT and GEMM_BT != "0" and self.dev.type == "cuda"
                          and hasattr(self.k, "gemm_bt_merge") and bool(self.k.gemm_bt_ok(T * B, H, 8 * H)))
+        # layer 0's input projection inside the persistent recurrence (no gx)
+        self.lstm_fx = (LSTM_FX and self.cfg.persistent_lstm and self.dev.type == "cuda"
+                        and hasattr(self.k, "lstm_persistent_fx_ok") and bool(self.k.lstm_persistent_fx_ok(H, B, E)))
         # encoder, per layer
         self.enc = []
         for layer in range(L):
@@ -437,7 +445,7 @@ class HipPointerGenerator:
             self.enc.append({
                 "din": din,
                 "x_sf": z(2, T, B, din, dt=BF),          # step-frame inputs (bw reversed)
-                "gx": z(2, T, B, 4 * H),                 # [2][T][B][H][4 gates]
+                "gx": None if (self.lstm_fx and layer == 0) else z(2, T, B, 4 * H),  # [2][T][B][H][4 gates]
                 "hs": z(2, T + 1, B, H, dt=BF),
                 "cs": z(2, T + 1, B, H),
                 "acts": z(2, T, B, 4 * H),               # [2][T][B][H][4 gates]
@@ -801,6 +809,17 @@ class HipPointerGenerator:
         for layer, st in enumerate(self.enc):
             din = st["din"]
             xs = st["x_sf"]
+            if self.lstm_fx and layer == 0:
+                # x.W_x inside the recurrence: only the step-frame gather of the embeddings here
+                k.to_step_frame(self.pk["emb"], w["enc_batch"], rev, xs, B, T, din, 0)
+                st["hs"][:, 0].zero_()
+                st["cs"][:, 0].zero_()
+                w["lstm_xf"].zero_()  # hand-off tags must start at 0 every launch
+                k.lstm_fwd_persistent_fx(xs, self.pk["enc0_KxiT0"], self.pk["enc0_KxiT1"], self.f32["enc0_b"],
+                                         self.pk["enc0_Wt"], st["hs"], st["cs"], st["acts"], st["out"], lens,
+                                         w["lstm_xf"], w["lstm_err"], T, B, H)
+                x = st["out"]
+                continue
             if self._frame_gemm_bt(layer):
                 # x.W_x with the A rows gathered through the step frame inside the GEMM (layer 0
                 # straight from the embedding table by token id); the gathered rows are also
