@@ -100,9 +100,9 @@ __global__ __launch_bounds__(SW * 64) void attn_score_kernel(
       *reinterpret_cast<float4*>(sk + 4) = *reinterpret_cast<const float4*>(sb + k + 4);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        // y = 2 log2(e) (F + s_k + w_k cov) for both positions at once
+        // y = 2 log2(e) (F + s_k + w_k cov) for both positions at once (F stored pre-scaled)
         const f32x2 base = fma2(splat2(wk[i] * K2LOG2E), cc[q], splat2(sk[i] * K2LOG2E));
-        const f32x2 y = fma2(bf2pair(raw[i]), splat2(K2LOG2E), base);
+        const f32x2 y = fadd_bf2(raw[i], base);
         acc[q] = fma2(splat2(vk[i]), rsig2(y), acc[q]);
       }
     }
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
       for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
         for (int jp = 0; jp < 4; ++jp) {
-          const f32x2 y = fma2(bf2pair(fr[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          const f32x2 y = fadd_bf2(fr[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
           const f32x2 r = rsig2(y);
           const f32x2 qv = fma2(-r, r, r);
           acc[kb][jp] = fma2(qv, splat2(de), acc[kb][jp]);
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
       const u32x4 fw = __builtin_bit_cast(u32x4, ld8(F + ((size_t)b * T + p) * A + k0));
 #pragma unroll
       for (int jp = 0; jp < 4; ++jp) {
-        fs[q][jp] = bf2pair(fw[jp]) * K2LOG2E;  // pre-scaled features
+        fs[q][jp] = bf2pair(fw[jp]);  // F is stored pre-scaled (attn_common.h)
         acc[q][jp] = f32x2{0.f, 0.f};
       }
     }

@@ -126,7 +126,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
       for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
         for (int jp = 0; jp < 4; ++jp) {
-          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
           d2 = fma2(v2[kb][jp], rsig2(y), d2);
         }
       pd[q] = vsum - 2.0f * (d2.x + d2.y);
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
         const f32x2 ps = par(0, kb, jp), pw = par(1, kb, jp), pv = par(2, kb, jp);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(pw, splat2(cq[q]), ps));
+          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(pw, splat2(cq[q]), ps));
           const f32x2 r = rsig2(y);
           const f32x2 qv = fma2(-r, r, r);
           acc[kb][jp] = fma2(qv, splat2(deq[q]), acc[kb][jp]);
@@ -470,7 +470,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
       for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
         for (int jp = 0; jp < 4; ++jp) {
-          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
           d2 = fma2(v2[kb][jp], rsig2(y), d2);
         }
       pd[q] = vsum - 2.0f * (d2.x + d2.y);
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
         const f32x2 ps = par(0, kb, jp), pw = par(1, kb, jp), pv = par(2, kb, jp);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x2 y = fma2(bf2pair(f.x[kb][q][jp]), splat2(K2LOG2E), fma2(pw, splat2(cq[q]), ps));
+          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(pw, splat2(cq[q]), ps));
           const f32x2 r = rsig2(y);
           const f32x2 qv = fma2(-r, r, r);
           acc[kb][jp] = fma2(qv, splat2(deq[q]), acc[kb][jp]);

@@ -17,6 +17,17 @@ __device__ __forceinline__ f32x2 rsig2(f32x2 y) {
   return f32x2{__builtin_amdgcn_rcpf(ex.x), __builtin_amdgcn_rcpf(ex.y)};
 }
 __device__ __forceinline__ f32x2 bf2pair(uint32_t r) { return f32x2{__uint_as_float(r << 16), __uint_as_float(r & 0xffff0000u)}; }
+// The attention features F = enc_out . W_h are STORED pre-scaled by 2 log2(e) (the engine's
+// F GEMM runs on W_h * K2LOG2E, pack.hip), so a score argument is y = F + t with t = 2 log2(e)
+// (s + w cov) -- per feature pair two v_dot2_f32_bf16 against (1, 0) / (0, 1): the bf16 -> f32
+// unpack and the add in ONE op per element instead of shift / and + packed FMA (12.4 vs 16.8
+// cycles per pair, tools/micro/dot2_probe.cpp; the products are exact, one rounding of F + t).
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 fadd_bf2(uint32_t r, f32x2 t) {
+  const bf16x2_t x = __builtin_bit_cast(bf16x2_t, r);
+  return f32x2{__builtin_amdgcn_fdot2_f32_bf16(x, __builtin_bit_cast(bf16x2_t, 0x00003f80u), t.x, false),
+               __builtin_amdgcn_fdot2_f32_bf16(x, __builtin_bit_cast(bf16x2_t, 0x3f800000u), t.y, false)};
+}
 
 __device__ __forceinline__ float rdlane(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));

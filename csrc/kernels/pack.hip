@@ -10,7 +10,8 @@
 #define PACK_COLS 16  // int64 per job row
 
 // Job row (PACK_COLS int64): src, dst, d0, d1, d2, src strides s0..s2, dst strides t0..t2
-// (elements), first block, kind, dst dtype (0 bf16, 1 fp32), element count.  Kinds (host-classified):
+// (elements), first block, kind, dst dtype (0 bf16, 1 fp32), element count, scale (the bits of an
+// fp32 factor applied before the cast in the low 32 bits; 0 = 1.0).  Kinds (host-classified):
 //   0 generic strided copy: 256 elements per block, one per thread (index math per element);
 //   1 contiguous src and dst: 2048 elements per block, 8 per thread (two 16-byte loads, one
 //     16-byte bf16 store);
@@ -35,13 +36,16 @@ __global__ __launch_bounds__(256) void pack_cast_kernel(const long* __restrict__
   const long jb = blk - start[lo];
   const int kind = (int)J[12], f32o = (int)J[13];
   const long n = J[14];
+  const float sc = J[15] ? __int_as_float((int)J[15]) : 1.f;
   const float* src = reinterpret_cast<const float*>(J[0]);
   if (kind == 1) {
     const long e0 = jb * 2048 + (long)threadIdx.x * 8;
     if (e0 >= n) return;
     if (e0 + 8 <= n) {
-      const float4 a = *reinterpret_cast<const float4*>(src + e0);
-      const float4 b = *reinterpret_cast<const float4*>(src + e0 + 4);
+      float4 a = *reinterpret_cast<const float4*>(src + e0);
+      float4 b = *reinterpret_cast<const float4*>(src + e0 + 4);
+      a.x *= sc; a.y *= sc; a.z *= sc; a.w *= sc;
+      b.x *= sc; b.y *= sc; b.z *= sc; b.w *= sc;
       if (f32o) {
         float* d = reinterpret_cast<float*>(J[1]) + e0;
         *reinterpret_cast<float4*>(d) = a;
@@ -54,8 +58,8 @@ __global__ __launch_bounds__(256) void pack_cast_kernel(const long* __restrict__
       }
     } else {
       for (long e = e0; e < n; ++e) {
-        if (f32o) reinterpret_cast<float*>(J[1])[e] = src[e];
-        else reinterpret_cast<bf16*>(J[1])[e] = f2bf(src[e]);
+        if (f32o) reinterpret_cast<float*>(J[1])[e] = src[e] * sc;
+        else reinterpret_cast<bf16*>(J[1])[e] = f2bf(src[e] * sc);
       }
     }
     return;
@@ -73,7 +77,7 @@ __global__ __launch_bounds__(256) void pack_cast_kernel(const long* __restrict__
     for (int k = ty; k < 64; k += 4) {  // dst row i0 + k, cols c0 + tx: coalesced
       const long i = i0 + k, c = c0 + tx;
       if (i < R && c < C) {
-        const float v = tile[tx][k];
+        const float v = tile[tx][k] * sc;
         if (f32o) reinterpret_cast<float*>(J[1])[i * C + c] = v;
         else reinterpret_cast<bf16*>(J[1])[i * C + c] = f2bf(v);
       }
@@ -84,7 +88,7 @@ __global__ __launch_bounds__(256) void pack_cast_kernel(const long* __restrict__
   if (li >= n) return;
   const unsigned d1 = (unsigned)J[3], d2 = (unsigned)J[4];
   const unsigned ul = (unsigned)li, i2 = ul % d2, r = ul / d2, i1 = r % d1, i0 = r / d1;
-  const float v = src[i0 * J[5] + i1 * J[6] + i2 * J[7]];
+  const float v = src[i0 * J[5] + i1 * J[6] + i2 * J[7]] * sc;
   const long o = i0 * J[8] + i1 * J[9] + i2 * J[10];
   if (f32o) reinterpret_cast<float*>(J[1])[o] = v;
   else reinterpret_cast<bf16*>(J[1])[o] = f2bf(v);

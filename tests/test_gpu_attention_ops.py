@@ -5,7 +5,9 @@ few, and T leave fully masked blocks and masked tail groups.
 
 Reference semantics (attention_decoder.py:79-129, model.py:463-480 of the reference): scores
 e_i = v . tanh(F_i + s + w_c cov_i), a = masked softmax(e), ctx = sum_i a_i E_i, coverage loss
-sum_i min(a_i, cov_i), cov_{t+1} = cov_t + a_t.
+sum_i min(a_i, cov_i), cov_{t+1} = cov_t + a_t.  The kernels read F stored multiplied by 2 log2(e)
+(the engine's F GEMM runs on W_h * 2 log2(e)): each test passes that operand and checks against the
+reference on the same values divided back.
 """
 import pytest
 import torch
@@ -13,6 +15,15 @@ import torch
 from textsummarization_on_flink_amd.ops import ops
 
 pytestmark = pytest.mark.gpu
+
+KF = 2.8853900817779268  # 2 log2(e): the kernels read F stored pre-scaled by it (attn_common.h)
+
+
+def _scaled(F):
+    """(kernel operand, reference features) of bf16 features F: the operand is F * 2 log2(e)
+    rounded to bf16, the reference its exact value divided back."""
+    Fk = (F.float() * KF).bfloat16()
+    return Fk, Fk.float() / KF
 
 
 def _reference(E, F, s, v, wc, cov, a, dctx, Ga, dnext, g, lens):
@@ -51,9 +62,10 @@ def test_attn_bwd_step_matches_fp32(A):
     dctx, Ga, dnext = r(B, A, s=0.1), r(B, T, s=0.1), r(B, T, s=0.1)
     g = torch.full((B,), 0.7, device=dev)
     de, ds, dcov = torch.zeros(B, T, device=dev), torch.zeros(B, A, device=dev), torch.zeros(B, T, device=dev)
-    k.attn_bwd_step(E, F, s, v, wc, cov, a, dctx, ctx, Ga, dnext, g, lens, de, ds, dcov, B, T, A)
+    Fk, Fr = _scaled(F)
+    k.attn_bwd_step(E, Fk, s, v, wc, cov, a, dctx, ctx, Ga, dnext, g, lens, de, ds, dcov, B, T, A)
     torch.cuda.synchronize()
-    want = _reference(E, F, s, v, wc, cov, a, dctx, Ga, dnext, g, lens)
+    want = _reference(E, Fr, s, v, wc, cov, a, dctx, Ga, dnext, g, lens)
     for name, got, ref in zip(("de", "ds", "dcov"), (de, ds, dcov), want):
         err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         assert err < 2e-3, (name, err)
@@ -81,9 +93,10 @@ def test_attn_fwd_row_matches_fp32(A, Na, rep):
     cov = torch.rand(B, T, generator=gen, device=dev) * mask
     a, cov_out, cl = torch.zeros(B, T, device=dev), torch.zeros(B, T, device=dev), torch.zeros(B, device=dev)
     ctx, ctx_bf = torch.zeros(B, A, device=dev), torch.zeros(B, A, device=dev, dtype=torch.bfloat16)
-    k.attn_fwd_row(F, E, s, v, wc, cov, lens, a, cov_out, cl, ctx, ctx_bf, B, T, A, rep)
+    Fk, Fr = _scaled(F)
+    k.attn_fwd_row(Fk, E, s, v, wc, cov, lens, a, cov_out, cl, ctx, ctx_bf, B, T, A, rep)
     torch.cuda.synchronize()
-    Fr, Er = F.float().repeat_interleave(rep, 0), E.float().repeat_interleave(rep, 0)
+    Fr, Er = Fr.repeat_interleave(rep, 0), E.float().repeat_interleave(rep, 0)
     e = torch.einsum("bta,a->bt", torch.tanh(Fr + s[:, None, :] + wc[None, None, :] * cov[:, :, None]), v)
     a_ref = torch.softmax(e.masked_fill(~mask, float("-inf")), -1)
     ctx_ref = torch.einsum("bt,bta->ba", a_ref, Er)
@@ -117,10 +130,11 @@ def test_attn_bwd_row_matches_fp32(A):
     g = torch.full((B,), 0.7, device=dev)
     de, dcov = torch.full((B, T), float("nan"), device=dev), torch.full((B, T), float("nan"), device=dev)
     ds = torch.full((B, A), float("nan"), device=dev)
-    k.attn_bwd_row(E, F, s, v, wc, cov, a, dctx, ctx, Ga, dnext, g, lens, de, ds, dcov, B, T, A)
+    Fk, Fr = _scaled(F)
+    k.attn_bwd_row(E, Fk, s, v, wc, cov, a, dctx, ctx, Ga, dnext, g, lens, de, ds, dcov, B, T, A)
     torch.cuda.synchronize()
     got_ds = ds
-    want = _reference(E, F, s, v, wc, cov, a, dctx, Ga, dnext, g, lens)
+    want = _reference(E, Fr, s, v, wc, cov, a, dctx, Ga, dnext, g, lens)
     for name, got, ref in zip(("de", "ds", "dcov"), (de, got_ds, dcov), want):
         err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         assert err < 2e-3, (name, err)
@@ -146,9 +160,10 @@ def test_attn_fwd_rowp_matches_fp32(A):
     a, cov_out, cl = (torch.full((B, T), float("nan"), device=dev), torch.zeros(B, T, device=dev),
                       torch.zeros(B, device=dev))
     gx, gxb = torch.zeros(B, EG, device=dev), torch.zeros(B, EG, device=dev, dtype=torch.bfloat16)
-    k.attn_fwd_rowp(F, G, s, v, wc, cov, lens, a, cov_out, cl, gx, gxb, B, T, A, None, 0)
+    Fk, Fr = _scaled(F)
+    k.attn_fwd_rowp(Fk, G, s, v, wc, cov, lens, a, cov_out, cl, gx, gxb, B, T, A, None, 0)
     torch.cuda.synchronize()
-    e = torch.einsum("bta,a->bt", torch.tanh(F.float() + s[:, None, :] + wc[None, None, :] * cov[:, :, None]), v)
+    e = torch.einsum("bta,a->bt", torch.tanh(Fr + s[:, None, :] + wc[None, None, :] * cov[:, :, None]), v)
     a_ref = torch.softmax(e.masked_fill(~mask, float("-inf")), -1)
     g_ref = torch.einsum("bt,bte->be", a_ref, G.float())
     checks = (("a", a, a_ref), ("g", gx, g_ref), ("cov_out", cov_out, cov + a_ref),
@@ -184,10 +199,11 @@ def test_attn_bwd_rowp_matches_fp32(A, last):
     g = torch.full((B,), 0.7, device=dev)
     de, dcov = torch.full((B, T), float("nan"), device=dev), torch.full((B, T), float("nan"), device=dev)
     ds = torch.full((B, A), float("nan"), device=dev)
-    k.attn_bwd_rowp(G, F, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, None, 0)
+    Fk, Fr = _scaled(F)
+    k.attn_bwd_rowp(G, Fk, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, None, 0)
     torch.cuda.synchronize()
     # the E-form reference with "E" = G and "dctx" = dx (zero at the last step)
-    want = _reference(G, F, s, v, wc, cov, a, torch.zeros(B, EG, device=dev) if last else dx, Ga, dnext, g, lens)
+    want = _reference(G, Fr, s, v, wc, cov, a, torch.zeros(B, EG, device=dev) if last else dx, Ga, dnext, g, lens)
     for name, got, ref in zip(("de", "ds", "dcov"), (de, ds, dcov), want):
         err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         assert err < 2e-3, (name, err)

@@ -88,6 +88,9 @@ DX_MERGE = os.environ.get("TSAMD_DX_MERGE", "1") != "0"
 # (lstm_persistent.hip FX): the step-frame inputs (bf16, E = 128) are gathered once and each
 # step's x MFMAs run in the shadow of the hand-off wait -- no gx GEMM, no gx buffer.
 LSTM_FX = os.environ.get("TSAMD_LSTM_FX", "1") != "0"
+# 2 log2(e): the attention features F = enc_out . W_h are stored multiplied by it (the kernels'
+# tanh argument is 2^(K u); attn_common.h fadd_bf2)
+K2LOG2E = 2.8853900817779268
 # the step-frame gather path replaces to_step_frame + the GEMM: kept while the gather GEMM is at
 # most this much slower than the library GEMM alone (the layout pass it saves costs ~25-40 % of it)
 FRAME_SLACK = 1.25
@@ -630,7 +633,7 @@ class HipPointerGenerator:
             self._build_pack_jobs()
 
     def _pack_job_pairs(self):
-        """(destination view, fp32 source view) of every layout pack() maintains."""
+        """(destination view, fp32 source view[, scale]) of every layout pack() maintains."""
         p, E, H, A, pk, f32 = self.p, self.E, self.H, self.A, self.pk, self.f32
         M, K, W = p[LIN_M], p[CELL_K], self._wcomb
         pairs = [(pk["emb"], p[EMB])]
@@ -645,7 +648,9 @@ class HipPointerGenerator:
                           (f32[f"enc{layer}_b"][di], p[enc_b(layer, d)])]
                 if layer > 0:
                     pairs.append((pk[f"enc{layer}_Kx01"][:, di * 4 * H:(di + 1) * 4 * H], Kd[:din]))
-        pairs += [(pk["Wh"], p[WH].reshape(A, A)), (pk["WhT"], p[WH].reshape(A, A).t()), (pk["lin_embT"], M[:E].t()),
+        pairs += [(pk["Wh"], p[WH].reshape(A, A)),
+                  (pk["WhK"], p[WH].reshape(A, A), K2LOG2E), (pk["WhKT"], p[WH].reshape(A, A).t(), K2LOG2E),
+                  (pk["lin_embT"], M[:E].t()),
                   (pk["RC"], p[RC]), (pk["RH"], p[RH]), (pk["RCt"], p[RC].t()),
                   (pk["RHt"], p[RH].t()), (pk["lin_emb"], M[:E]), (pk["Wic"], M[E:]), (pk["WicT"], M[E:].t()),
                   (pk["cell_x"], K[:E]), (pk["KcT"], K.t()), (pk["WcT2"][:, :A], W.t()), (pk["WcT2"][:, A:], K[E:].t()),
@@ -662,7 +667,7 @@ class HipPointerGenerator:
         E = self.E
         self._wcomb = torch.mm(self.p[LIN_M][E:], self.p[CELL_K][:E])
         rows, blk = [], 0
-        for dst, src in self._pack_job_pairs():
+        for dst, src, *scale in self._pack_job_pairs():
             assert dst.shape == src.shape and src.dtype == F32 and dst.dtype in (BF, F32) and dst.dim() <= 3, \
                 (dst.shape, src.shape)
             shape = [1] * (3 - dst.dim()) + list(dst.shape)
@@ -676,7 +681,8 @@ class HipPointerGenerator:
                 kind, nblk = 2, -(-R // 64) * -(-C // 64)
             else:
                 kind, nblk = 0, -(-n // 256)
-            rows.append([src.data_ptr(), dst.data_ptr(), *shape, *ss, *ts, blk, kind, int(dst.dtype == F32), n, 0])
+            sc = int(np.array(scale[0], dtype=np.float32).view(np.int32)) if scale else 0  # fp32 bits, 0 = 1.0
+            rows.append([src.data_ptr(), dst.data_ptr(), *shape, *ss, *ts, blk, kind, int(dst.dtype == F32), n, sc])
             blk += nblk
         if len(rows) > int(self.k.pack_max_jobs()) or len(rows[0]) != int(self.k.pack_job_cols()):
             return  # keep the torch path
@@ -711,7 +717,10 @@ class HipPointerGenerator:
             put(f"enc{layer}_Wn", Kh)
             put(f"enc{layer}_Wt", Kh.transpose(1, 2))
         put("Wh", p[WH].reshape(A, A))
-        put("WhT", p[WH].reshape(A, A).t())
+        # W_h * 2 log2(e): the F GEMM's operand -- F is stored pre-scaled for the attention
+        # kernels' score arguments (attn_common.h fadd_bf2); Wh / WhT stay for dE = dF . W_h^T
+        put("WhK", p[WH].reshape(A, A) * K2LOG2E)
+        put("WhKT", p[WH].reshape(A, A).t() * K2LOG2E)
         put("RC", p[RC])
         put("RH", p[RH])
         put("RCt", p[RC].t())  # [H][2H]: "Bt" operand of the fused reduce_states forward
@@ -856,7 +865,8 @@ class HipPointerGenerator:
         # state, one launch (reduce_states.hip) reading the encoder's final states in place
         k.rs_fwd(top["cs"], top["hs"], T, self.pk["RCt"], self.pk["RHt"], self.p[BRC], self.p[BRH], w["rs_pre"][0],
                  w["rs_pre"][1], w["Cst"][0], w["Cb"][0], w["Hb"][0], w["rs_cat"][0], w["rs_cat"][1], B, H)
-        mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["Wh"], bt=self.pk["WhT"])
+        # F = enc_out . W_h * 2 log2(e) (stored pre-scaled: attn_common.h)
+        mm_into(w["F"].view(B * T, A), top["out"].view(B * T, A), self.pk["WhK"], bt=self.pk["WhKT"])
         if self.proj_attn:
             mm_into(w["Genc"].view(B * T, self.E), top["out"].view(B * T, A), self.pk["Wic"], bt=self.pk["WicT"])
         if self.keep_ft:
