@@ -38,6 +38,7 @@ __global__ __launch_bounds__(SW * 64) void attn_score_kernel(
     const bf16* __restrict__ Ft, const float* __restrict__ s, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov, const int* __restrict__ lens,
     float* __restrict__ e, int T, int A, int xcd) {
+  const Dot2Sel dsel = dot2_sel();  // F pair selectors for fadd_bf2
   __shared__ float red[SW][REP][SCORE_POS];
   // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs, so consecutive
   // ids would put the position chunks of one Ft row on different XCDs.  A row is T*2 bytes
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(SW * 64) void attn_score_kernel(
       for (int i = 0; i < 8; ++i) {
         // y = 2 log2(e) (F + s_k + w_k cov) for both positions at once (F stored pre-scaled)
         const f32x2 base = fma2(splat2(wk[i] * K2LOG2E), cc[q], splat2(sk[i] * K2LOG2E));
-        const f32x2 y = fadd_bf2(raw[i], base);
+        const f32x2 y = fadd_bf2(raw[i], base, dsel);
         acc[q] = fma2(splat2(vk[i]), rsig2(y), acc[q]);
       }
     }
@@ -247,6 +248,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
     const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
     const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
     float* __restrict__ dcov_out, int T, int A) {
+  const Dot2Sel dsel = dot2_sel();  // F pair selectors for fadd_bf2
   constexpr int PW = 4 * NG4;  // positions per wave
   constexpr int PB = 4 * PW;   // positions per block
   static_assert(PW == 32 || PW == 16 || PW == 64, "lane -> position map needs a power of two <= 64");
@@ -375,7 +377,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
       for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
         for (int jp = 0; jp < 4; ++jp) {
-          const f32x2 y = fadd_bf2(fr[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          const f32x2 y = fadd_bf2(fr[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]), dsel);
           const f32x2 r = rsig2(y);
           const f32x2 qv = fma2(-r, r, r);
           acc[kb][jp] = fma2(qv, splat2(de), acc[kb][jp]);

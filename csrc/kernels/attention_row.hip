@@ -65,6 +65,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
     float* __restrict__ covloss, float* __restrict__ ctx, bf16* __restrict__ ctx_bf, int T, int rep, int xper,
     const int* __restrict__ cg, const float* __restrict__ asrc, float* __restrict__ cov_keep) {
+  const Dot2Sel dsel = dot2_sel();  // F pair selectors for fadd_bf2
   // cg set (beam decode): the coverage of hypothesis row b is its parent's coverage plus the
   // parent's last attention, cov = cov[g] + asrc[g] with g = cg[b] (the gather of the former
   // beam_gather kernel); cov_keep receives it for the next step
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
       for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
         for (int jp = 0; jp < 4; ++jp) {
-          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]), dsel);
           d2 = fma2(v2[kb][jp], rsig2(y), d2);
         }
       pd[q] = vsum - 2.0f * (d2.x + d2.y);
@@ -223,6 +224,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
     const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
     const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
     float* __restrict__ dcov_out, int T) {
+  const Dot2Sel dsel = dot2_sel();  // F pair selectors for fadd_bf2
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float part[NW][A];
   __shared__ float red[NW];
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_row_kernel(
         const f32x2 ps = par(0, kb, jp), pw = par(1, kb, jp), pv = par(2, kb, jp);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(pw, splat2(cq[q]), ps));
+          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(pw, splat2(cq[q]), ps), dsel);
           const f32x2 r = rsig2(y);
           const f32x2 qv = fma2(-r, r, r);
           acc[kb][jp] = fma2(qv, splat2(deq[q]), acc[kb][jp]);
@@ -402,6 +404,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
     const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
     float* __restrict__ covloss, float* __restrict__ gx, bf16* __restrict__ gx_bf, int T,
     const int* __restrict__ dlen, int step) {
+  const Dot2Sel dsel = dot2_sel();  // F pair selectors for fadd_bf2
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float es[kRowMaxT];
   __shared__ float part[NW][4][kEG];
@@ -470,7 +473,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
       for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
         for (int jp = 0; jp < 4; ++jp) {
-          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]));
+          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]), dsel);
           d2 = fma2(v2[kb][jp], rsig2(y), d2);
         }
       pd[q] = vsum - 2.0f * (d2.x + d2.y);
@@ -553,6 +556,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
     const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
     float* __restrict__ dcov_out, int T, const int* __restrict__ dlen, int step) {
+  const Dot2Sel dsel = dot2_sel();  // F pair selectors for fadd_bf2
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float part[NW][A];
   __shared__ float red[NW];
@@ -655,7 +659,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
         const f32x2 ps = par(0, kb, jp), pw = par(1, kb, jp), pv = par(2, kb, jp);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(pw, splat2(cq[q]), ps));
+          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(pw, splat2(cq[q]), ps), dsel);
           const f32x2 r = rsig2(y);
           const f32x2 qv = fma2(-r, r, r);
           acc[kb][jp] = fma2(qv, splat2(deq[q]), acc[kb][jp]);

@@ -23,10 +23,21 @@ __device__ __forceinline__ f32x2 bf2pair(uint32_t r) { return f32x2{__uint_as_fl
 // unpack and the add in ONE op per element instead of shift / and + packed FMA (12.4 vs 16.8
 // cycles per pair, tools/micro/dot2_probe.cpp; the products are exact, one rounding of F + t).
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 fadd_bf2(uint32_t r, f32x2 t) {
+// The (1, 0) / (0, 1) selectors live in SGPRs made opaque once per kernel (dot2_sel()): left as
+// constants, the compiler encodes (1, 0) as the inline constant 1.0, which the hardware does not
+// expand to a bf16 1.0 in the low half (test_gpu_attention_ops failed with it).
+struct Dot2Sel {
+  uint32_t lo, hi;
+};
+__device__ __forceinline__ Dot2Sel dot2_sel() {
+  uint32_t lo = 0x00003f80u, hi = 0x3f800000u;
+  asm volatile("" : "+s"(lo), "+s"(hi));
+  return Dot2Sel{lo, hi};
+}
+__device__ __forceinline__ f32x2 fadd_bf2(uint32_t r, f32x2 t, Dot2Sel sel) {
   const bf16x2_t x = __builtin_bit_cast(bf16x2_t, r);
-  return f32x2{__builtin_amdgcn_fdot2_f32_bf16(x, __builtin_bit_cast(bf16x2_t, 0x00003f80u), t.x, false),
-               __builtin_amdgcn_fdot2_f32_bf16(x, __builtin_bit_cast(bf16x2_t, 0x3f800000u), t.y, false)};
+  return f32x2{__builtin_amdgcn_fdot2_f32_bf16(x, __builtin_bit_cast(bf16x2_t, sel.lo), t.x, false),
+               __builtin_amdgcn_fdot2_f32_bf16(x, __builtin_bit_cast(bf16x2_t, sel.hi), t.y, false)};
 }
 
 __device__ __forceinline__ float rdlane(float x, int l) {
