@@ -9,7 +9,7 @@ engine is built); code can also pass a config explicitly.
 |---------------------------|--------------------|-------------------|
 | TSAMD_LSTM_PERSISTENT     | persistent_lstm    | 1: one persistent weight-resident launch per bi-LSTM pass; 0: per-step kernels |
 | TSAMD_ROW_ATTN            | row_attn           | auto (B >= 64): one workgroup per row; 0 / 1 force |
-| TSAMD_SPLIT               | split              | auto (2 groups from B = 256): decoder row groups on parallel streams |
+| TSAMD_SPLIT               | split              | auto (2 groups from B = 256, 4 from B = 1024): decoder row groups on parallel streams |
 | TSAMD_SPLIT_BWD           | split_bwd          | auto (= split): row groups of the decoder backward loop |
 | TSAMD_FUSED_VOCAB_TRAIN   | fused_vocab_train  | 1: training vocab head with the logits only in MFMA accumulators; 0: library GEMM + ptr_loss |
 | TSAMD_FUSED_VOCAB         | fused_vocab_decode | 1: decode vocab head + top-k fused; 0: GEMM + final_topk |

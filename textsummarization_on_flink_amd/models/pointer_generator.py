@@ -399,7 +399,10 @@ class HipPointerGenerator:
         # Deterministic mode runs the same row groups: each row's arithmetic is the same on any
         # stream, and test_deterministic_mode_bit_identical requires split 1 / 2 / 4 to give the
         # single chain's bits (profiles/r4/det_streams.md: the round-3 one-chain override is gone)
-        sp = cfg.split or (2 if B >= 256 and B % 32 == 0 else 1)
+        # Round 5 (projected attention with dot2 scores, FX encoder): 4 groups from B = 1024 --
+        # config #5 batch 2048 366.2-367.7 ms vs 368.9-369.7 with 2 groups (8: 368.3; 8 forward / 4
+        # backward 366.4), batch 1024 188.7 vs 191.0 ms (profiles/r5/runs/r5t*)
+        sp = cfg.split or (4 if B >= 1024 and B % 64 == 0 else 2 if B >= 256 and B % 32 == 0 else 1)
         self.split = sp if (sp > 1 and B % (16 * sp) == 0) else 1
         # cfg.split_bwd: the decoder backward loop's own group count (default: split; B = 256 with
         # 4 forward groups: 4 backward groups 19.48 ms per step, 2 groups 19.79)
