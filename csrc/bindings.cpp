@@ -217,7 +217,7 @@ void attn_fwd_rowp(const Tensor& F, const Tensor& G, const Tensor& s, const Tens
 void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                    const Tensor& a, const OT& dx, const Tensor& gv, const OT& Ga, const OT& dcov_next, const OT& gcl,
                    const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out, int64_t B, int64_t T,
-                   int64_t A, const OT& dlen, int64_t step, const OT& vacc, const OT& wacc) {
+                   int64_t A, const OT& dlen, int64_t step) {
   chk(G, BF, "G"); chk(F, BF, "F"); chk(s, F32, "s"); chk(v, F32, "v"); chk(a, F32, "a"); chk(gv, F32, "gv");
   chk(lens, I32, "lens"); chk(de_out, F32, "de_out"); chk(ds, F32, "ds");
   const int64_t EG = gv.numel() / std::max<int64_t>(B, 1);
@@ -229,14 +229,9 @@ void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tens
   chko(dx, F32, B * EG, "dx"); chko(wc, F32, A, "wc"); chko(cov, F32, B * T, "cov"); chko(Ga, F32, B * T, "Ga");
   chko(dcov_next, F32, B * T, "dcov_next"); chko(gcl, F32, B, "gcl"); chko(dcov_out, F32, B * T, "dcov_out");
   chko(dlen, I32, B, "dlen");
-  // vacc / wacc: per-row [B][A] accumulators of the v / w_c gradients (A = 1024 only; wacc needs vacc)
-  chko(vacc, F32, B * A, "vacc"); chko(wacc, F32, B * A, "wacc");
-  TORCH_CHECK((!vacc.has_value() || A == 1024) && (!wacc.has_value() || vacc.has_value()),
-              "attn_bwd_rowp: vacc / wacc at A = 1024 only (wacc with vacc)");
   launch_attn_bwd_rowp(P<bf16>(G), P<bf16>(F), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<float>(a),
                        PO<float>(dx), P<float>(gv), PO<float>(Ga), PO<float>(dcov_next), PO<float>(gcl), P<int>(lens),
-                       P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, PO<int>(dlen), (int)step, stream(),
-                       PO<float>(vacc), PO<float>(wacc));
+                       P<float>(de_out), P<float>(ds), PO<float>(dcov_out), B, T, A, PO<int>(dlen), (int)step, stream());
 }
 
 void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
@@ -257,25 +252,22 @@ void attn_bwd_step(const Tensor& E, const Tensor& F, const Tensor& s, const Tens
 }
 
 void attn_bwd_feat(const Tensor& F, const Tensor& S_all, const Tensor& v, const OT& wc, const OT& cov_all,
-                   const Tensor& de_all, const Tensor& lens, const Tensor& dF, const OT& dv, const OT& dwc,
+                   const Tensor& de_all, const Tensor& lens, const Tensor& dF, const Tensor& dv, const OT& dwc,
                    int64_t D, int64_t B, int64_t T, int64_t A, const OT& dlen) {
   chk(F, BF, "F"); chk(S_all, F32, "S_all"); chk(v, F32, "v"); chk(de_all, F32, "de_all"); chk(lens, I32, "lens");
-  chk(dF, BF, "dF");
+  chk(dF, BF, "dF"); chk(dv, F32, "dv");
   TORCH_CHECK(A % 64 == 0, "bad A");
   numel_eq(F, B * T * A, "F"); numel_eq(S_all, D * B * A, "S_all"); numel_eq(de_all, D * B * T, "de_all");
   // dv / dwc: [nslot][A] partial rows (nslot a power of two; the caller sums them).  With nslot >=
-  // the number of workgroups every slot has one writer (deterministic mode).  dv absent: dF only
-  // (the row backward accumulated dv / dwc, attn_bwd_rowp vacc / wacc)
-  const int64_t nslot = dv.has_value() ? dv->numel() / A : 1;
-  if (dv.has_value()) chk(*dv, F32, "dv");
-  TORCH_CHECK(nslot >= 1 && nslot <= (1 << 20) && (nslot & (nslot - 1)) == 0 && (!dv.has_value() || dv->numel() == nslot * A),
+  // the number of workgroups every slot has one writer (deterministic mode)
+  const int64_t nslot = dv.numel() / A;
+  TORCH_CHECK(nslot >= 1 && nslot <= (1 << 20) && (nslot & (nslot - 1)) == 0 && dv.numel() == nslot * A,
               "dv: [nslot, A] with nslot a power of two");
-  TORCH_CHECK(dv.has_value() || !dwc.has_value(), "attn_bwd_feat: dwc needs dv");
   numel_eq(dF, B * T * A, "dF");
   chko(wc, F32, A, "wc"); chko(cov_all, F32, D * B * T, "cov_all"); chko(dwc, F32, nslot * A, "dwc");
   chko(dlen, I32, B, "dlen");
   launch_attn_bwd_feat(P<bf16>(F), P<float>(S_all), P<float>(v), PO<float>(wc), PO<float>(cov_all), P<float>(de_all),
-                       P<int>(lens), P<bf16>(dF), PO<float>(dv), PO<float>(dwc), D, B, T, A, (int)nslot, stream(),
+                       P<int>(lens), P<bf16>(dF), P<float>(dv), PO<float>(dwc), D, B, T, A, (int)nslot, stream(),
                        PO<int>(dlen));
 }
 

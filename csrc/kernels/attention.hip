@@ -425,8 +425,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_step4_kernel(
 // dF[b,i,k] = sum_t de[t,b,i] v_k sech2(u_tik); dv_k = sum de tanh(u); dwc_k = sum de v_k sech2 cov.
 // Lanes on features (8 per lane), each wave keeps 4 positions x 8 features of dF in
 // registers across all D steps; de / cov are wave-uniform scalar loads.
-// VWO = false: dv / dwc were accumulated by the row backward (attn_bwd_rowp VW): dF only.
-template <int NPW, int OCC, bool VWO = true>
+template <int NPW, int OCC>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
     const bf16* __restrict__ F, const float* __restrict__ S_all, const float* __restrict__ v,
     const float* __restrict__ wc, const float* __restrict__ cov_all, const float* __restrict__ de_all,
@@ -496,10 +495,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
             const f32x2 r = rsig2(y);
             const f32x2 qv = fma2(-r, r, r);
             acc[q][jp] = fma2(qv, splat2(de), acc[q][jp]);
-            if constexpr (VWO) {
-              accv[jp] = fma2(r, splat2(de), accv[jp]);
-              accw[jp] = fma2(qv, splat2(dec), accw[jp]);
-            }
+            accv[jp] = fma2(r, splat2(de), accv[jp]);
+            accw[jp] = fma2(qv, splat2(dec), accw[jp]);
           }
         }
       }
@@ -518,7 +515,6 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_feat_kernel(
     for (int q = 0; q < NPW; ++q)
       if (p0 + q < T) *reinterpret_cast<bf16x8*>(dF + ((size_t)b * T + p0 + q) * A + k0) = zero8();
   }
-  if constexpr (!VWO) return;  // (block-uniform: no barrier below is skipped by part of the block)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     adv[j] = sum_de - 2.0f * accv[j >> 1][j & 1];
@@ -591,10 +587,6 @@ void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, con
   // vs 1.64 ms uncapped at 3 waves/SIMD and 1.65 ms with 2 positions per wave (B = 256,
   // T = 400, D = 100)
   dim3 grid((T + 15) / 16, B, (A + 511) / 512);
-  if (dv)
-    hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 4>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens,
-                       dF, dv, dwc, D, B, T, A, nslot, dlen);
-  else  // dv / dwc accumulated by attn_bwd_rowp (VW): dF only
-    hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 4, false>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all,
-                       lens, dF, nullptr, nullptr, D, B, T, A, 1, dlen);
+  hipLaunchKernelGGL((attn_bwd_feat_kernel<4, 4>), grid, dim3(256), 0, st, F, S_all, v, wc, cov_all, de_all, lens, dF,
+                     dv, dwc, D, B, T, A, nslot, dlen);
 }

@@ -548,22 +548,14 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
 // backward: da_i = r_i + dx . G_i (r_i already holds the output-projection / p_gen part of
 // dctx . E_i), S = sum_j a_j r_j + dx . g_t; the rest as attn_bwd_row.  dx == nullptr:
 // last step.
-// VW: the v and w_c gradients of this step, dv_k = sum_i de_i tanh(u_ik) and
-// dwc_k = 4 v_k sum_i de_i cov_i r(1 - r), added to per-row accumulators vacc / wacc [B][A]
-// (this row's workgroup is their only writer in a launch; the step launches of a row group are
-// stream-ordered) -- two packed FMAs per element here, where the loop streams F at the HBM rate
-// (A = 1024), instead of in attn_bwd_feat, which is VALU-bound (profiles/r5/vw_rowp.md).  The
-// per-lane sums live in LDS (thread-private slots, one read-modify-write per group of 4
-// positions): in registers they spilled the double-buffered rows (57 VGPRs at A = 1024).
-template <int NK, int NW, bool VW = false>
+template <int NK, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     const bf16* __restrict__ G, const bf16* __restrict__ F, const float* __restrict__ s,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
     const float* __restrict__ a, const float* __restrict__ dx, const float* __restrict__ gv,
     const float* __restrict__ Ga, const float* __restrict__ dcov_next, const float* __restrict__ gcl,
     const int* __restrict__ lens, float* __restrict__ de_out, float* __restrict__ ds,
-    float* __restrict__ dcov_out, int T, const int* __restrict__ dlen, int step, float* __restrict__ vacc,
-    float* __restrict__ wacc) {
+    float* __restrict__ dcov_out, int T, const int* __restrict__ dlen, int step) {
   const Dot2Sel dsel = dot2_sel();  // F pair selectors for fadd_bf2
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float part[NW][A];
@@ -607,16 +599,12 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
   };
   if (wid < ngrp) load(wid, fA, gA, xA);
   f32x2 acc[NK][4];
-  __shared__ f32x2 vws[VW ? 2 * NK * 4 * NT : 1];  // VW: [v / w][kb][jp][thread]
-  auto vw = [&](int which, int kb, int jp) -> f32x2& { return vws[((which * NK + kb) * 4 + jp) * NT + tid]; };
-  float sde = 0.f;  // VW: sum of this wave's de (wave-uniform)
 #pragma unroll
   for (int kb = 0; kb < NK; ++kb) {
     const int k0 = kb * 512 + lane * 8;
 #pragma unroll
     for (int jp = 0; jp < 4; ++jp) {
       acc[kb][jp] = f32x2{0.f, 0.f};
-      if constexpr (VW) vw(0, kb, jp) = vw(1, kb, jp) = f32x2{0.f, 0.f};
       if (wid != 0) continue;
       const float2 sv = *reinterpret_cast<const float2*>(s + (size_t)b * A + k0 + 2 * jp);
       const float2 vv = *reinterpret_cast<const float2*>(v + k0 + 2 * jp);
@@ -662,19 +650,13 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
       cq[q] = rdlane(x.c, 16 * q);
     }
     f32x2 dc2[4];
-    float dcq[VW ? 4 : 1];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      dc2[q] = f32x2{0.f, 0.f};
-      if constexpr (VW) dcq[q] = deq[q] * cq[q];
-    }
-    if constexpr (VW) sde += (deq[0] + deq[1]) + (deq[2] + deq[3]);
+    for (int q = 0; q < 4; ++q) dc2[q] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
       for (int jp = 0; jp < 4; ++jp) {
         const f32x2 ps = par(0, kb, jp), pw = par(1, kb, jp), pv = par(2, kb, jp);
-        f32x2 tv = f32x2{0.f, 0.f}, tw = f32x2{0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(pw, splat2(cq[q]), ps), dsel);
@@ -682,14 +664,6 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
           const f32x2 qv = fma2(-r, r, r);
           acc[kb][jp] = fma2(qv, splat2(deq[q]), acc[kb][jp]);
           dc2[q] = fma2(qv, pv, dc2[q]);
-          if constexpr (VW) {
-            tv = fma2(r, splat2(deq[q]), tv);
-            tw = fma2(qv, splat2(dcq[q]), tw);
-          }
-        }
-        if constexpr (VW) {
-          vw(0, kb, jp) += tv;
-          vw(1, kb, jp) += tw;
         }
       }
     float dcv[4];
@@ -737,36 +711,6 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_rowp_kernel(
     for (int w = 0; w < NW; ++w) x += part[w][k];
     ds[(size_t)b * A + k] = 4.f * v[k] * x;
   }
-  if constexpr (VW) {
-    // dv_k += sum_i de_i - 2 sum_i de_i r_ik;  dwc_k += 4 v_k sum_i de_i cov_i r(1 - r)
-    const float sd = block_sum<NT>(lane == 0 ? sde : 0.f, red);  // (its barriers also end the reads of part)
-#pragma unroll
-    for (int kb = 0; kb < NK; ++kb)
-#pragma unroll
-      for (int jp = 0; jp < 4; ++jp)
-        *reinterpret_cast<float2*>(&part[wid][kb * 512 + lane * 8 + 2 * jp]) = make_float2(vw(0, kb, jp).x, vw(0, kb, jp).y);
-    __syncthreads();
-    for (int k = tid; k < A; k += NT) {
-      float x = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) x += part[w][k];
-      vacc[(size_t)b * A + k] += sd - 2.f * x;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kb = 0; kb < NK; ++kb)
-#pragma unroll
-      for (int jp = 0; jp < 4; ++jp)
-        *reinterpret_cast<float2*>(&part[wid][kb * 512 + lane * 8 + 2 * jp]) = make_float2(vw(1, kb, jp).x, vw(1, kb, jp).y);
-    __syncthreads();
-    if (wacc)
-      for (int k = tid; k < A; k += NT) {
-        float x = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) x += part[w][k];
-        wacc[(size_t)b * A + k] += 4.f * v[k] * x;
-      }
-  }
 }
 
 // ------------------------------------------------------------------------------ launchers
@@ -794,18 +738,12 @@ void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const fl
 void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st,
-                          float* vacc, float* wacc) {
-#define LB(NK, VW)                                                                                        \
-  hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, rowp_bwd_waves<NK>(), VW>), dim3(B), dim3(rowp_bwd_waves<NK>() * 64), \
-                     0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, dlen, step, \
-                     vacc, wacc)
-  if (A == 512) {
-    LB(1, false);  // (the binding admits vacc at A = 1024 only: at A = 512 the row backward is not HBM-bound)
-  } else {
-    if (vacc) LB(2, true);
-    else LB(2, false);
-  }
+                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st) {
+#define LB(NK)                                                                                            \
+  hipLaunchKernelGGL((attn_bwd_rowp_kernel<NK, rowp_bwd_waves<NK>()>), dim3(B), dim3(rowp_bwd_waves<NK>() * 64), \
+                     0, st, G, F, s, v, wc, cov, a, dx, gv, Ga, dcov_next, gcl, lens, de_out, ds, dcov_out, T, dlen, step)
+  if (A == 512) LB(1);
+  else LB(2);
 #undef LB
 }
 

@@ -40,8 +40,7 @@ void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const fl
 void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
-                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st,
-                          float* vacc = nullptr, float* wacc = nullptr);
+                          float* dcov_out, int B, int T, int A, const int* dlen, int step, hipStream_t st);
 
 void launch_dec_cell_fwd(const float* XG, const bf16* ctxp, const bf16* hprev, const float* cprev, const bf16* WcT,
                          float* c_out, bf16* cb_out, bf16* hb_out, float* act, int B, int H, int A, const int* dlen,

@@ -200,22 +200,10 @@ def test_attn_bwd_rowp_matches_fp32(A, last):
     de, dcov = torch.full((B, T), float("nan"), device=dev), torch.full((B, T), float("nan"), device=dev)
     ds = torch.full((B, A), float("nan"), device=dev)
     Fk, Fr = _scaled(F)
-    # A = 1024: the v / w_c gradients accumulated onto per-row buffers (VW), which hold earlier steps' sums
-    vacc = r(B, A, s=0.1) if A == 1024 else None
-    wacc = r(B, A, s=0.1) if A == 1024 else None
-    vacc0, wacc0 = (vacc.clone(), wacc.clone()) if A == 1024 else (None, None)
-    k.attn_bwd_rowp(G, Fk, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, None, 0, vacc, wacc)
+    k.attn_bwd_rowp(G, Fk, s, v, wc, cov, a, dx, gv, Ga, dnext, g, lens, de, ds, dcov, B, T, A, None, 0)
     torch.cuda.synchronize()
     # the E-form reference with "E" = G and "dctx" = dx (zero at the last step)
     want = _reference(G, Fr, s, v, wc, cov, a, torch.zeros(B, EG, device=dev) if last else dx, Ga, dnext, g, lens)
     for name, got, ref in zip(("de", "ds", "dcov"), (de, ds, dcov), want):
         err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
         assert err < 2e-3, (name, err)
-    if A == 1024:
-        u = Fr + s[:, None, :] + wc[None, None, :] * cov[:, :, None]
-        th = torch.tanh(u)
-        dv_ref = vacc0 + torch.einsum("bt,bta->ba", want[0], th)
-        dwc_ref = wacc0 + torch.einsum("bt,bta->ba", want[0] * cov, 1 - th ** 2) * v[None, :]
-        for name, got, ref in (("dv", vacc, dv_ref), ("dwc", wacc, dwc_ref)):
-            err = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
-            assert err < 2e-3, (name, err)

@@ -91,10 +91,6 @@ LSTM_FX = os.environ.get("TSAMD_LSTM_FX", "1") != "0"
 # 2 log2(e): the attention features F = enc_out . W_h are stored multiplied by it (the kernels'
 # tanh argument is 2^(K u); attn_common.h fadd_bf2)
 K2LOG2E = 2.8853900817779268
-# TSAMD_VW_ROWP=0: the attention v / w_c gradients in attn_bwd_feat.  Default at A = 1024: in the
-# projected row backward (attn_bwd_rowp VW: per-row accumulators over the reverse loop, HBM-bound
-# there), so attn_bwd_feat (VALU-bound) only computes dF (profiles/r5/vw_rowp.md)
-VW_ROWP = os.environ.get("TSAMD_VW_ROWP", "1") != "0"
 # the step-frame gather path replaces to_step_frame + the GEMM: kept while the gather GEMM is at
 # most this much slower than the library GEMM alone (the layout pass it saves costs ~25-40 % of it)
 FRAME_SLACK = 1.25
@@ -517,10 +513,6 @@ class HipPointerGenerator:
         # G = enc_out . W_in[E:] ([B, T, E]) instead of F and enc_out; ctx of all steps is one batched
         # GEMM after the loop, the output-projection / p_gen part of dctx . E_i one before the backward
         self.proj_attn = self.row_attn and cfg.proj_attn and bool(self.k.attn_rowp_ok(A, T, E))
-        self.vw_rowp = VW_ROWP and self.proj_attn and A == 1024
-        if self.vw_rowp:  # per-row v / w_c gradient accumulators of the reverse loop
-            w["vacc"] = z(B, A)
-            w["wacc"] = z(B, A)
         if self.proj_attn:
             w["Genc"] = z(B, T, E, dt=BF)
             w["GV"] = z(D, B, E)         # g_t = sum_i a_ti G_i = ctx_t . W_in[E:]
@@ -1243,13 +1235,6 @@ class HipPointerGenerator:
             Ga.copy_(da.transpose(0, 1))
         w["dh_rec"].zero_()
         w["dc_carry"].zero_()
-        vacc = wacc = None
-        if self.vw_rowp:
-            vacc = w["vacc"]
-            vacc.zero_()
-            if cov:
-                wacc = w["wacc"]
-                wacc.zero_()
         dcov = w["dcov"]
         Kc = self.pk["Wbig"][:E + H]  # W_cell: [dx | dh] = dz . W_cell^T
         dlen = w["dlen"] if self.skip_pad else None
@@ -1266,8 +1251,7 @@ class HipPointerGenerator:
                                 w["ATT"][t][rs], w["DX"][t + 1][rs] if nxt else None, w["GV"][t][rs],
                                 Ga[t][rs], dcov[(t + 1) % 2][rs] if (cov and nxt) else None,
                                 w["gcl"][t][rs] if cov else None, lens[rs], w["DE"][t][rs], w["DS"][t][rs],
-                                dcov[t % 2][rs] if cov else None, Bg, T, A, dl, t,
-                                vacc[rs] if vacc is not None else None, wacc[rs] if wacc is not None else None)
+                                dcov[t % 2][rs] if cov else None, Bg, T, A, dl, t)
                 k.dec_bwd_cell(w["DS"][t][rs], self.pk["Ws"], dC_dir[t][rs] if dC_dir is not None else None,
                                dH_dir[t][rs], w["dh_rec"][rs], w["dc_carry"][rs], w["ACT"][t][rs], w["Cst"][t + 1][rs],
                                w["Cst"][t][rs], w["DZ"][t][rs], Bg, H, A, dl, t)
@@ -1316,20 +1300,13 @@ class HipPointerGenerator:
             wg(gs[H:], Hn, DSb)
         run(dec_wgrad)
         # ---- attention feature gradients (tanh recomputed once over all steps)
-        if self.vw_rowp:  # dv / dwc came out of the reverse loop (attn_bwd_rowp VW): dF only here
-            k.attn_bwd_feat(F, w["S"], v, wc, w["COV"][:D] if cov else None, w["DE"], lens, w["dF"], None, None,
-                            D, B, T, A, w["dlen"] if self.skip_pad else None)
-            k.colsum(w["vacc"], g(VATT).view(A), B, A, False)
-            if cov:
-                k.colsum(w["wacc"], g(WCOV).view(A), B, A, False)
-        else:
-            w["dv"].zero_()
-            w["dwc"].zero_()
-            k.attn_bwd_feat(F, w["S"], v, wc, w["COV"][:D] if cov else None, w["DE"], lens, w["dF"], w["dv"],
-                            w["dwc"] if cov else None, D, B, T, A, w["dlen"] if self.skip_pad else None)
-            k.colsum(w["dv"], g(VATT).view(A), w["dv"].shape[0], A, False)
-            if cov:
-                k.colsum(w["dwc"], g(WCOV).view(A), w["dwc"].shape[0], A, False)
+        w["dv"].zero_()
+        w["dwc"].zero_()
+        k.attn_bwd_feat(F, w["S"], v, wc, w["COV"][:D] if cov else None, w["DE"], lens, w["dF"], w["dv"],
+                        w["dwc"] if cov else None, D, B, T, A, w["dlen"] if self.skip_pad else None)
+        k.colsum(w["dv"], g(VATT).view(A), w["dv"].shape[0], A, False)
+        if cov:
+            k.colsum(w["dwc"], g(WCOV).view(A), w["dwc"].shape[0], A, False)
         dFb = w["dF"].view(B * T, A)
         top = self.enc[-1]
         run(lambda: wg(g(WH).view(A, A), top["out"].view(B * T, A), dFb))

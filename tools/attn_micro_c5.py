@@ -74,7 +74,7 @@ def main():
         res["fwd_rowp"] = timeit(lambda i: k.attn_fwd_rowp(F[i], Gp[i], s, v, wc, cov, lens, att, cov_out, covloss, gx,
                                                            gxb, MB, T, A, None, 0), NG)
         res["bwd_rowp"] = timeit(lambda i: k.attn_bwd_rowp(Gp[i], F[i], s, v, wc, cov, att, dxp, gx, ga, dcn, gcl, lens,
-                                                           de, ds, dco, MB, T, A, None, 0, None, None), NG)
+                                                           de, ds, dco, MB, T, A, None, 0), NG)
         gbp = MB * T * (A + 128) * 2 / 1e9  # F + G bytes per launch
         for key in ("fwd_rowp", "bwd_rowp"):
             res[key + "_GBs"] = round(gbp / (res[key] * 1e-6), 1)
