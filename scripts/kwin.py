@@ -1,7 +1,8 @@
 """Per-kernel ms/step over the last N training steps of a rocprofv3 kernel_trace.csv (the
 dispatches after the (N+1)-th last optimizer kernel up to the last one), so one-off work before
 them (graph capture warm-up, blt_mm's candidate timing) is left out.
-usage: kwin.py <kernel_trace.csv> <N> [top, default 40] [marker substring, default adagrad_kernel]"""
+usage: kwin.py <kernel_trace.csv> <N> [top, default 40] [marker substring, default adagrad_kernel] [skip]
+(skip: leave out the last `skip` steps, e.g. bench.py's phase-timed diagnostic steps)"""
 import csv
 import sys
 
@@ -10,7 +11,8 @@ n = int(sys.argv[2])
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
 mark = sys.argv[4] if len(sys.argv) > 4 else "adagrad_kernel"
 idx = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"]]
-win = rows[idx[-n - 1] + 1: idx[-1] + 1]
+sk = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+win = rows[idx[-n - 1 - sk] + 1: idx[-1 - sk] + 1]
 t0, t1 = int(win[0]["Start_Timestamp"]), int(win[-1]["End_Timestamp"])
 agg = {}
 for r in win:
