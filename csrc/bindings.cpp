@@ -200,9 +200,10 @@ void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tenso
 bool attn_rowp_ok(int64_t A, int64_t T, int64_t EG) { return attn_rowp_supported((int)A, (int)T, (int)EG); }
 void attn_fwd_rowp(const Tensor& F, const Tensor& G, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                    const Tensor& lens, const Tensor& a_out, const OT& cov_out, const OT& covloss, const Tensor& gx,
-                   const Tensor& gx_bf, int64_t B, int64_t T, int64_t A, const OT& dlen, int64_t step) {
+                   const Tensor& gx_bf, int64_t B, int64_t T, int64_t A, const OT& dlen, int64_t step,
+                   const OT& a_bf) {
   chk(F, BF, "F"); chk(G, BF, "G"); chk(s, F32, "s"); chk(v, F32, "v"); chk(lens, I32, "lens");
-  chk(a_out, F32, "a_out"); chk(gx, F32, "gx"); chk(gx_bf, BF, "gx_bf");
+  chk(a_out, F32, "a_out"); chk(gx, F32, "gx"); chk(gx_bf, BF, "gx_bf"); chko(a_bf, BF, B * T, "a_bf");
   const int64_t EG = gx.numel() / std::max<int64_t>(B, 1);
   TORCH_CHECK(attn_rowp_supported((int)A, (int)T, (int)EG), "projected row attention needs A in {512, 1024}, "
               "T <= 2048 and a 128-wide projection");
@@ -212,7 +213,7 @@ void attn_fwd_rowp(const Tensor& F, const Tensor& G, const Tensor& s, const Tens
   chko(covloss, F32, B, "covloss"); chko(dlen, I32, B, "dlen");
   launch_attn_fwd_rowp(P<bf16>(F), P<bf16>(G), P<float>(s), P<float>(v), PO<float>(wc), PO<float>(cov), P<int>(lens),
                        P<float>(a_out), PO<float>(cov_out), PO<float>(covloss), P<float>(gx), P<bf16>(gx_bf), B, T, A,
-                       PO<int>(dlen), (int)step, stream());
+                       PO<int>(dlen), (int)step, stream(), PO<bf16>(a_bf));
 }
 void attn_bwd_rowp(const Tensor& G, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                    const Tensor& a, const OT& dx, const Tensor& gv, const OT& Ga, const OT& dcov_next, const OT& gcl,
@@ -345,6 +346,14 @@ void transpose_bta(const Tensor& in, const Tensor& out, int64_t B, int64_t T, in
   TORCH_CHECK(A % 64 == 0, "A % 64");
   numel_eq(in, B * T * A, "in"); numel_eq(out, B * T * A, "out");
   launch_transpose_bta(P<bf16>(in), P<bf16>(out), (int)B, (int)T, (int)A, stream());
+}
+// fp32 [P][Q][R] -> [Q][P][R] fp32 (out) and bf16 (outb), either nullable, one pass
+void tr01(const Tensor& in, const OT& out, const OT& outb, int64_t P, int64_t Q, int64_t R) {
+  chk(in, F32, "in");
+  TORCH_CHECK(R % 4 == 0 && P >= 1 && Q >= 1, "tr01: R % 4 == 0");
+  numel_eq(in, P * Q * R, "in");
+  chko(out, F32, P * Q * R, "out"); chko(outb, BF, P * Q * R, "outb");
+  launch_tr01(P<float>(in), PO<float>(out), PO<bf16>(outb), (int)P, (int)Q, (int)R, stream());
 }
 void cast_colsum(const Tensor& x, const Tensor& xb, const Tensor& colsum, int64_t N, int64_t C) {
   chk(x, F32, "x"); chk(xb, BF, "xb"); chk(colsum, F32, "colsum");
@@ -1050,6 +1059,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("to_step_frame", &to_step_frame);
   m.def("from_step_frame", &from_step_frame);
   m.def("transpose_bta", &transpose_bta);
+  m.def("tr01", &tr01);
   m.def("linear2_pair", &linear2_pair);
   m.def("cast_colsum", &cast_colsum);
   m.def("colsum", &colsum);

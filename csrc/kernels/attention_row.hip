@@ -403,7 +403,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
     const int* __restrict__ lens, float* __restrict__ a_out, float* __restrict__ cov_out,
     float* __restrict__ covloss, float* __restrict__ gx, bf16* __restrict__ gx_bf, int T,
-    const int* __restrict__ dlen, int step) {
+    const int* __restrict__ dlen, int step, bf16* __restrict__ a_bf) {
   const Dot2Sel dsel = dot2_sel();  // F pair selectors for fadd_bf2
   constexpr int A = 512 * NK, NT = NW * 64;
   __shared__ float es[kRowMaxT];
@@ -418,6 +418,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
     // computes reaches the loss, so write zeros (a, g, coverage loss) and carry the coverage
     for (int i = tid; i < T; i += NT) {
       a_out[rb + i] = 0.f;
+      if (a_bf) a_bf[rb + i] = f2bf(0.f);
       if (cov_out) cov_out[rb + i] = cov ? cov[rb + i] : 0.f;
     }
     for (int k = tid; k < kEG; k += NT) {
@@ -533,6 +534,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_rowp_kernel(
   for (int i = tid; i < T; i += NT) {
     const float a = i < len ? fexp(es[i] - m) * invL : 0.f;
     a_out[rb + i] = a;
+    if (a_bf) a_bf[rb + i] = f2bf(a);  // the bf16 operand of the post-loop ctx GEMM (no cast pass)
     if (cov_out) {
       const float c = cov ? cov[rb + i] : 0.f;
       cov_out[rb + i] = c + a;
@@ -725,11 +727,11 @@ constexpr int rowp_bwd_waves() { return NK == 1 ? 16 : 8; }
 
 void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const float* v, const float* wc,
                           const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* gx,
-                          bf16* gx_bf, int B, int T, int A, const int* dlen, int step, hipStream_t st) {
+                          bf16* gx_bf, int B, int T, int A, const int* dlen, int step, hipStream_t st, bf16* a_bf) {
 #define LF(NK)                                                                                            \
   hipLaunchKernelGGL((attn_fwd_rowp_kernel<NK, row_waves<NK, false>()>), dim3(B),                        \
                      dim3(row_waves<NK, false>() * 64), 0, st, F, G, s, v, wc, cov, lens, a_out, cov_out, covloss, \
-                     gx, gx_bf, T, dlen, step)
+                     gx, gx_bf, T, dlen, step, a_bf)
   if (A == 512) LF(1);
   else LF(2);
 #undef LF

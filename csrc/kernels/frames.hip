@@ -74,6 +74,24 @@ __global__ __launch_bounds__(256) void step_frame_hop_kernel(const float* __rest
   }
 }
 
+// fp32 [P][Q][R] -> [Q][P][R] (out, nullable) and its bf16 twin (outb, nullable) in one pass: the
+// step-major ctx of all decoder steps from the batched a . enc_out GEMM ([B][D][A]), which took a
+// strided torch copy plus a bf16 cast (two more passes over D x B x A) before
+__global__ __launch_bounds__(256) void tr01_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                   bf16* __restrict__ outb, int P, int Q, int R4) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // float4 index in the OUTPUT [Q][P][R4]
+  if (i >= (size_t)P * Q * R4) return;
+  const int r = (int)(i % R4);
+  const size_t qp = i / R4;
+  const int pp = (int)(qp % P), q = (int)(qp / P);
+  const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in) + ((size_t)pp * Q + q) * R4 + r);
+  if (out) reinterpret_cast<f32x4*>(out)[i] = x;
+  if (outb) {
+    bf16 o[4] = {f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+    *reinterpret_cast<uint2*>(outb + 4 * i) = *reinterpret_cast<const uint2*>(o);
+  }
+}
+
 // bf16 [B][T][A] -> [B][A][T] through a 64 x 64 LDS tile (8-byte loads and stores)
 __global__ __launch_bounds__(256) void transpose_bta_kernel(const bf16* __restrict__ in, bf16* __restrict__ out, int T,
                                                             int A) {
@@ -297,4 +315,10 @@ void launch_colsum_det(const void* x, bool bf, float* part, float* out, int N, i
     hipLaunchKernelGGL(colsum_det_finish_kernel<16>, dim3((C + 15) / 16), dim3(256), 0, st, part, out, G, C, acc ? 1 : 0);
   else
     hipLaunchKernelGGL(colsum_det_finish_kernel<1>, dim3(C), dim3(256), 0, st, part, out, G, C, acc ? 1 : 0);
+}
+
+void launch_tr01(const float* in, float* out, bf16* outb, int P, int Q, int R, hipStream_t st) {
+  const size_t n = (size_t)P * Q * (R / 4);
+  if (n == 0) return;
+  hipLaunchKernelGGL(tr01_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, out, outb, P, Q, R / 4);
 }

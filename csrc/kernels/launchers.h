@@ -36,7 +36,8 @@ void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const flo
 bool attn_rowp_supported(int A, int T, int EG);
 void launch_attn_fwd_rowp(const bf16* F, const bf16* G, const float* s, const float* v, const float* wc,
                           const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* gx,
-                          bf16* gx_bf, int B, int T, int A, const int* dlen, int step, hipStream_t st);
+                          bf16* gx_bf, int B, int T, int A, const int* dlen, int step, hipStream_t st,
+                          bf16* a_bf = nullptr);
 void launch_attn_bwd_rowp(const bf16* G, const bf16* F, const float* s, const float* v, const float* wc,
                           const float* cov, const float* a, const float* dx, const float* gv, const float* Ga,
                           const float* dcov_next, const float* gcl, const int* lens, float* de_out, float* ds,
@@ -162,6 +163,7 @@ void launch_to_step_frame(const void* src, int es, const int64_t* ids, const int
 void launch_from_step_frame(const float* in, const int64_t* rev, float* out, int B, int T, int W, hipStream_t st);
 void launch_step_frame_hop(const float* in, const int64_t* rev, float* out, int B, int T, int H, hipStream_t st);
 void launch_transpose_bta(const bf16* in, bf16* out, int B, int T, int A, hipStream_t st);
+void launch_tr01(const float* in, float* out, bf16* outb, int P, int Q, int R, hipStream_t st);
 int cast_colsum_blocks(int N, int C);
 void launch_cast_colsum(const float* x, bf16* xb, float* part, float* colsum, int N, int C, hipStream_t st);
 int colsum_det_chunks(int N, int C);

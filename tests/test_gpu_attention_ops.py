@@ -161,11 +161,13 @@ def test_attn_fwd_rowp_matches_fp32(A):
                       torch.zeros(B, device=dev))
     gx, gxb = torch.zeros(B, EG, device=dev), torch.zeros(B, EG, device=dev, dtype=torch.bfloat16)
     Fk, Fr = _scaled(F)
-    k.attn_fwd_rowp(Fk, G, s, v, wc, cov, lens, a, cov_out, cl, gx, gxb, B, T, A, None, 0)
+    ab = torch.full((B, T), float("nan"), device=dev, dtype=torch.bfloat16)
+    k.attn_fwd_rowp(Fk, G, s, v, wc, cov, lens, a, cov_out, cl, gx, gxb, B, T, A, None, 0, ab)
     torch.cuda.synchronize()
     e = torch.einsum("bta,a->bt", torch.tanh(Fr + s[:, None, :] + wc[None, None, :] * cov[:, :, None]), v)
     a_ref = torch.softmax(e.masked_fill(~mask, float("-inf")), -1)
     g_ref = torch.einsum("bt,bte->be", a_ref, G.float())
+    assert torch.equal(ab, a.bfloat16())  # the bf16 twin of a, written by the same kernel
     checks = (("a", a, a_ref), ("g", gx, g_ref), ("cov_out", cov_out, cov + a_ref),
               ("covloss", cl, torch.minimum(a_ref, cov).sum(1)), ("g_bf", gxb.float(), g_ref))
     for name, got, ref in checks:

@@ -941,19 +941,19 @@ class HipPointerGenerator:
                 k.attn_fwd_rowp(F[rs], G[rs], w["S"][t][rs], v, wc, w["COV"][t][rs] if (cov and t > 0) else None,
                                 lens[rs], w["ATT"][t][rs], w["COV"][t + 1][rs] if cov else None,
                                 w["covloss"][t][rs] if cov else None, w["GV"][t][rs], w["GVb"][t][rs], Bg, T, A,
-                                dl, t)
+                                dl, t, w["ATTb"][t][rs])
 
         self._row_groups(chain)
         w["X"][0].copy_(w["xe"][0])
         if D > 1:
             torch.add(w["xe"][1:], w["GV"][:D - 1], out=w["X"][1:])
         w["Xb"].copy_(w["X"])
-        # ctx_t = a_t . enc_out for every step: [B][D, T] x [B][T, A] (bf16 a, fp32 accumulate)
-        w["ATTb"].copy_(w["ATT"])
+        # ctx_t = a_t . enc_out for every step: [B][D, T] x [B][T, A] (bf16 a -- written by the
+        # attention kernel next to the fp32 a -- fp32 accumulate), then [B][D][A] -> CTX [D][B][A]
+        # and its bf16 twin in one pass (tr01)
         ctx = w["bd_tmp"][:B * D * A].view(B, D, A)
         torch.bmm(w["ATTb"].permute(1, 0, 2), enc_out, out_dtype=F32, out=ctx)
-        w["CTX"].copy_(ctx.transpose(0, 1))
-        w["CTXb"].copy_(w["CTX"])
+        self.k.tr01(ctx, w["CTX"], w["CTXb"], B, D, A)
 
     def _head_forward(self, need_grad: bool):
         w, hps, p = self.w, self.hps, self.p

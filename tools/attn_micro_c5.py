@@ -72,7 +72,7 @@ def main():
         gx, gxb = torch.empty(MB, 128, device=dev), torch.empty(MB, 128, device=dev, dtype=torch.bfloat16)
         dxp = torch.randn(MB, 128, device=dev, generator=g) * 0.1
         res["fwd_rowp"] = timeit(lambda i: k.attn_fwd_rowp(F[i], Gp[i], s, v, wc, cov, lens, att, cov_out, covloss, gx,
-                                                           gxb, MB, T, A, None, 0), NG)
+                                                           gxb, MB, T, A, None, 0, None), NG)
         res["bwd_rowp"] = timeit(lambda i: k.attn_bwd_rowp(Gp[i], F[i], s, v, wc, cov, att, dxp, gx, ga, dcn, gcl, lens,
                                                            de, ds, dco, MB, T, A, None, 0), NG)
         gbp = MB * T * (A + 128) * 2 / 1e9  # F + G bytes per launch
