@@ -348,12 +348,13 @@ void transpose_bta(const Tensor& in, const Tensor& out, int64_t B, int64_t T, in
   launch_transpose_bta(P<bf16>(in), P<bf16>(out), (int)B, (int)T, (int)A, stream());
 }
 // fp32 [P][Q][R] -> [Q][P][R] fp32 (out) and bf16 (outb), either nullable, one pass
-void tr01(const Tensor& in, const OT& out, const OT& outb, int64_t np_, int64_t nq, int64_t nr) {
+void tr01(const Tensor& in, const OT& out, const OT& outb, int64_t np_, int64_t nq, int64_t nr, bool acc) {
   chk(in, F32, "in");
   TORCH_CHECK(nr % 4 == 0 && np_ >= 1 && nq >= 1, "tr01: R % 4 == 0");
+  TORCH_CHECK(!acc || (out.has_value() && !outb.has_value()), "tr01: acc adds into out (no bf16 twin)");
   numel_eq(in, np_ * nq * nr, "in");
   chko(out, F32, np_ * nq * nr, "out"); chko(outb, BF, np_ * nq * nr, "outb");
-  launch_tr01(P<float>(in), PO<float>(out), PO<bf16>(outb), (int)np_, (int)nq, (int)nr, stream());
+  launch_tr01(P<float>(in), PO<float>(out), PO<bf16>(outb), (int)np_, (int)nq, (int)nr, acc, stream());
 }
 void cast_colsum(const Tensor& x, const Tensor& xb, const Tensor& colsum, int64_t N, int64_t C) {
   chk(x, F32, "x"); chk(xb, BF, "xb"); chk(colsum, F32, "colsum");

@@ -74,18 +74,23 @@ __global__ __launch_bounds__(256) void step_frame_hop_kernel(const float* __rest
   }
 }
 
-// fp32 [P][Q][R] -> [Q][P][R] (out, nullable) and its bf16 twin (outb, nullable) in one pass: the
-// step-major ctx of all decoder steps from the batched a . enc_out GEMM ([B][D][A]), which took a
-// strided torch copy plus a bf16 cast (two more passes over D x B x A) before
+// fp32 [P][Q][R] -> [Q][P][R] (out, nullable; acc: added to it) and its bf16 twin (outb, nullable)
+// in one pass: the step-major ctx of all decoder steps from the batched a . enc_out GEMM
+// ([B][D][A]), and the attention-weight gradient's dctx . E_i part added into dA ([B][D][T]),
+// which took strided torch copies / adds plus a bf16 cast before
 __global__ __launch_bounds__(256) void tr01_kernel(const float* __restrict__ in, float* __restrict__ out,
-                                                   bf16* __restrict__ outb, int P, int Q, int R4) {
+                                                   bf16* __restrict__ outb, int P, int Q, int R4, bool acc) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // float4 index in the OUTPUT [Q][P][R4]
   if (i >= (size_t)P * Q * R4) return;
   const int r = (int)(i % R4);
   const size_t qp = i / R4;
   const int pp = (int)(qp % P), q = (int)(qp / P);
   const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in) + ((size_t)pp * Q + q) * R4 + r);
-  if (out) reinterpret_cast<f32x4*>(out)[i] = x;
+  if (out) {
+    f32x4 y = x;
+    if (acc) y += reinterpret_cast<const f32x4*>(out)[i];
+    reinterpret_cast<f32x4*>(out)[i] = y;
+  }
   if (outb) {
     bf16 o[4] = {f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
     *reinterpret_cast<uint2*>(outb + 4 * i) = *reinterpret_cast<const uint2*>(o);
@@ -317,8 +322,9 @@ void launch_colsum_det(const void* x, bool bf, float* part, float* out, int N, i
     hipLaunchKernelGGL(colsum_det_finish_kernel<1>, dim3(C), dim3(256), 0, st, part, out, G, C, acc ? 1 : 0);
 }
 
-void launch_tr01(const float* in, float* out, bf16* outb, int P, int Q, int R, hipStream_t st) {
+void launch_tr01(const float* in, float* out, bf16* outb, int P, int Q, int R, bool acc, hipStream_t st) {
   const size_t n = (size_t)P * Q * (R / 4);
   if (n == 0) return;
-  hipLaunchKernelGGL(tr01_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, out, outb, P, Q, R / 4);
+  hipLaunchKernelGGL(tr01_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, out, outb, P, Q, R / 4,
+                     acc);
 }

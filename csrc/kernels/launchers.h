@@ -163,7 +163,7 @@ void launch_to_step_frame(const void* src, int es, const int64_t* ids, const int
 void launch_from_step_frame(const float* in, const int64_t* rev, float* out, int B, int T, int W, hipStream_t st);
 void launch_step_frame_hop(const float* in, const int64_t* rev, float* out, int B, int T, int H, hipStream_t st);
 void launch_transpose_bta(const bf16* in, bf16* out, int B, int T, int A, hipStream_t st);
-void launch_tr01(const float* in, float* out, bf16* outb, int P, int Q, int R, hipStream_t st);
+void launch_tr01(const float* in, float* out, bf16* outb, int P, int Q, int R, bool acc, hipStream_t st);
 int cast_colsum_blocks(int N, int C);
 void launch_cast_colsum(const float* x, bf16* xb, float* part, float* colsum, int N, int C, hipStream_t st);
 int colsum_det_chunks(int N, int C);

@@ -953,7 +953,7 @@ class HipPointerGenerator:
         # and its bf16 twin in one pass (tr01)
         ctx = w["bd_tmp"][:B * D * A].view(B, D, A)
         torch.bmm(w["ATTb"].permute(1, 0, 2), enc_out, out_dtype=F32, out=ctx)
-        self.k.tr01(ctx, w["CTX"], w["CTXb"], B, D, A)
+        self.k.tr01(ctx, w["CTX"], w["CTXb"], B, D, A, False)
 
     def _head_forward(self, need_grad: bool):
         w, hps, p = self.w, self.hps, self.p
@@ -1228,8 +1228,10 @@ class HipPointerGenerator:
         w["DCTXb"].copy_(dCTX_dir)
         da = w["bd_tmp"][:B * D * T].view(B, D, T)
         torch.bmm(w["DCTXb"].permute(1, 0, 2), enc_out.transpose(1, 2), out_dtype=F32, out=da)
-        Ga = w["dA"]
-        if hps.pointer_gen:
+        Ga = w["dA"]  # [D][B][T] (+)= da^T, one vectorised pass (tr01; T % 4 == 0)
+        if T % 4 == 0:
+            k.tr01(da, Ga, None, B, D, T, bool(hps.pointer_gen))
+        elif hps.pointer_gen:
             Ga.add_(da.transpose(0, 1))
         else:
             Ga.copy_(da.transpose(0, 1))
