@@ -131,3 +131,23 @@ def test_step_frame_hop_equals_from_then_to_step_frame(B, T, H):
     k.step_frame_hop(dxs, rev, out, B, T, H)
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("P,Q,R", [(6, 5, 512), (3, 7, 12), (256, 100, 400)])
+def test_tr01_transposes_casts_and_accumulates(P, Q, R):
+    """tr01: fp32 [P][Q][R] -> [Q][P][R] (copy or accumulate) and the bf16 twin in one pass."""
+    from textsummarization_on_flink_amd.ops import ops
+    k = ops()
+    g = torch.Generator(device="cuda").manual_seed(P + Q + R)
+    x = torch.randn(P, Q, R, device="cuda", generator=g)
+    out = torch.full((Q, P, R), float("nan"), device="cuda")
+    outb = torch.full((Q, P, R), float("nan"), device="cuda", dtype=torch.bfloat16)
+    k.tr01(x, out, outb, P, Q, R, False)
+    torch.cuda.synchronize()
+    assert torch.equal(out, x.transpose(0, 1))
+    assert torch.equal(outb, x.transpose(0, 1).bfloat16())
+    base = torch.randn(Q, P, R, device="cuda", generator=g)
+    acc = base.clone()
+    k.tr01(x, acc, None, P, Q, R, True)
+    torch.cuda.synchronize()
+    assert torch.equal(acc, base + x.transpose(0, 1))
