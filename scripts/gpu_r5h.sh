@@ -1,18 +1,13 @@
 #!/bin/bash
-# round 5: 64-row-block decoder step kernels (TSAMD_DEC_RT) and 256-row decode vocab_logits
-# (TSAMD_VL_RH): bit-identity tests, oracle at config #5 B = 1024, config #5 A/B, decode A/B.
+# round 5: A/B of the tr01 / in-kernel bf16 a glue removal at config #5 (TSAMD_TR01_AB=0: the torch passes)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/${OUTD:-r5h}; mkdir -p $OUT
+OUT=gpurun_out/r5h; mkdir -p $OUT
 export TMPDIR=/tmp
-step() { local n=$1; shift; echo "== $n"; timeout -k 10 ${T:-300} "$@" > $OUT/$n.log 2>&1; local rc=$?; tail -${TL:-3} $OUT/$n.log; return $rc; }
-step rt python -u -m pytest tests/test_gpu_decoder_rt.py -q -x --timeout 120 --timeout-method thread || exit 1
-T=600 step orc python -u -m pytest tests/test_gpu_production.py -q -x --timeout 300 --timeout-method thread -k "config5_shape" || exit 1
-TSAMD_VL_RH=4 step dect4 python -u -m pytest tests/test_gpu_decode.py -q -x --timeout 300 --timeout-method thread -k "topk or vocab" || exit 1
-T=500 TL=1 step c1 python -u bench.py --steps 1 --warmup 1 --decode-batches 0 --config5-steps 3 || exit 1
-TSAMD_DEC_RT=0 T=500 TL=1 step c0 python -u bench.py --steps 1 --warmup 1 --decode-batches 0 --config5-steps 3 || exit 1
-TL=1 step d2 python -u bench_decode.py --batches 10 || exit 1
-TSAMD_VL_RH=4 TL=1 step d4 python -u bench_decode.py --batches 10 || exit 1
-TL=1 step d2b python -u bench_decode.py --batches 10 || exit 1
-TSAMD_VL_RH=4 TL=1 step d4b python -u bench_decode.py --batches 10 || exit 1
+C5="--hidden 512 --enc 800 --layers 2 --batch 2048 --steps 10 --warmup 2 --decode-batches 0 --config5-steps 0"
+step() { local n=$1; shift; echo "== $n"; timeout -k 10 ${T:-300} "$@" > $OUT/$n.log 2>&1; local rc=$?; grep -o '"ms_per_step": [0-9.]*' $OUT/$n.log; return $rc; }
+step new1 python -u bench.py $C5 || exit 1
+step old1 env TSAMD_TR01_AB=0 python -u bench.py $C5 || exit 1
+step new2 python -u bench.py $C5 || exit 1
+step old2 env TSAMD_TR01_AB=0 python -u bench.py $C5 || exit 1
 echo done
