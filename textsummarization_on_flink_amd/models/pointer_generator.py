@@ -1159,7 +1159,11 @@ class HipPointerGenerator:
             wg(g(OUT_M)[H:], ctxb, doutb)
         run(out_proj_wgrad)
         dH_dir = mmf(doutb, self.pk["OUTm"][:H].t()).view(D, B, H)
-        dCTX_dir = mmf(doutb, self.pk["OUTm"][H:].t()).view(D, B, A)
+        if self.proj_attn:  # DCTX itself: the loop adds nothing per step, the post-loop GEMM accumulates into it
+            mm_into(w["DCTX"].view(N, A), doutb, self.pk["OUTm"][H:].t())
+            dCTX_dir = w["DCTX"]
+        else:
+            dCTX_dir = mmf(doutb, self.pk["OUTm"][H:].t()).view(D, B, A)
         dC_dir = None
         dX_dir = None
         if hps.pointer_gen:
@@ -1261,7 +1265,8 @@ class HipPointerGenerator:
                              w["DX"][t][rs], None, w["dh_rec"][rs], Bg, E, H, 0, dl, t)
 
         self._row_groups(chain, self.split_bwd)
-        w["DCTX"].copy_(dCTX_dir)
+        if dCTX_dir is not w["DCTX"]:
+            w["DCTX"].copy_(dCTX_dir)
         if D > 1:
             dctx = w["DCTX"][:D - 1].view((D - 1) * B, A)
             dxb = w["DXb"][1:].view((D - 1) * B, E)
