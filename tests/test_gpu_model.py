@@ -219,7 +219,10 @@ def test_skip_pad_steps_same_loss_and_gradients(monkeypatch, coverage, pointer_g
         live = torch.arange(40, device="cuda")[:, None] < dlen[None, :]
         assert int((dlen < 40).sum()) > 0 and int((dlen == 0).sum()) == 0
         assert _rel(l1, l0) < 1e-6
-        assert _rel(g1, g0) < 1e-5, _rel(g1, g0)
+        # fp32 reassociation only: the rows are in another order, and the library GEMM picks (timed per
+        # shape, process-wide) can be stream-K kernels whose partial-sum order varies run to run --
+        # 0.6-1.4e-5 across runs of the full GPU tier (1.4e-5 once with a 1e-5 bound)
+        assert _rel(g1, g0) < 3e-5, _rel(g1, g0)
         assert _rel(a1[live], a0[:, src][live]) < 1e-6
         assert float(a1[~live].abs().max()) == 0.0
 
