@@ -50,7 +50,7 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
 // lane's 4 consecutive columns per i are one 16-byte store (a row's 64 columns = one 256-byte
 // run over the 4 i and 4 q).  Replaced a [row = lane group] layout whose per-row reductions
 // took 16-lane DPP trees for each of the lane's 16 rows and an LDS staging pass for stores.
-template <bool FULL, int NI, bool NTS = false, bool STORE = true>
+template <bool FULL, int NI, bool NTS = false>
 __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[NI][4], int jr, const f32x2 (&bc)[NI][2],
                                             float* __restrict__ logits, float* Pm, float* Ps, int rb, int cw,
                                             int lane, int R, int V) {
@@ -82,7 +82,6 @@ __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[NI][4], int jr, c
     Pm[16 * jr + lane] = m;
     Ps[16 * jr + lane] = sm;
   }
-  if (!STORE) return;  // timing knob only (TSAMD_VL_STORE=0: no logits, wrong results)
   if (FULL) {
     float* dst = logits + (size_t)row * V + cw + q4;
 #pragma unroll
@@ -119,7 +118,7 @@ __device__ __forceinline__ void vl_epilogue(const f32x4 (&acc)[NI][4], int jr, c
 // NTS: the logits stores are non-temporal -- the select kernel re-reads only the K best tiles
 // and the copied words of each row, so 51 MB per step (R = 256) need not displace L2 lines:
 // 25.1 -> 23.6 us, decode 6092-6102 -> 6143-6155 summaries/s (profiles/r4/ab/decode_logits_nt.md)
-template <int OCC, int RH, int HMAX, bool HFIX = false, bool NTS = true, bool STORE = true>
+template <int OCC, int RH, int HMAX, bool HFIX = false, bool NTS = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) void vocab_logits_kernel(
     const bf16* __restrict__ X,     // [R][H]  output-projection activations (bf16)
     const bf16* __restrict__ WT,    // [V][H]  output_projection/w transposed ("Bt")
@@ -202,7 +201,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
       if (full)
-        vl_epilogue<true, NI, NTS, STORE>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
+        vl_epilogue<true, NI, NTS>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
       else
         vl_epilogue<false, NI>(acc, jr, bc, logits, Pm[wid] + VT_ROWS * h2, Ps[wid] + VT_ROWS * h2, rbh, cw, lane, R, V);
     }
@@ -530,13 +529,8 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
   if (H <= 256) {
     const int RB = (R + VT_ROWS * 2 - 1) / (VT_ROWS * 2);
     // (HFIX at 256 spills 16 VGPRs: the constant split lets all 16 X chunks be hoisted in flight)
-    static const bool store = !getenv("TSAMD_VL_STORE") || atoi(getenv("TSAMD_VL_STORE")) != 0;
-    if (store)
-      hipLaunchKernelGGL((vocab_logits_kernel<2, 2, 256>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
-                         logits, part_ms, R, V, H);
-    else
-      hipLaunchKernelGGL((vocab_logits_kernel<2, 2, 256, false, true, false>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0,
-                         st, X, WT, bias, logits, part_ms, R, V, H);
+    hipLaunchKernelGGL((vocab_logits_kernel<2, 2, 256>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT, bias,
+                       logits, part_ms, R, V, H);
   } else {
     const int RB = (R + VT_ROWS - 1) / VT_ROWS;
     hipLaunchKernelGGL((vocab_logits_kernel<2, 1, 512, true>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT,
