@@ -408,8 +408,6 @@ void launch_dec_cell_fwd_beam(const int* gidx, const int* latest, const float* X
 // when it is at most 8 k-steps (the output projection's K = H + A = 768 at hidden 256: 6; the
 // query projection's K = 2H = 1024 at hidden 512: 8), else batches of 4
 static int l2_kb(int K) {
-  static const bool off = getenv("TSAMD_L2_KB") && atoi(getenv("TSAMD_L2_KB")) == 0;  // A/B: batches of 4
-  if (off) return 4;
   const int ks = (K / 32 + 3) / 4;
   return ks <= 4 ? 4 : ks <= 6 ? 6 : ks <= 8 ? 8 : 4;
 }
