@@ -758,7 +758,12 @@ void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const flo
 #define LF(NK)                                                                                                 \
   hipLaunchKernelGGL((attn_fwd_row_kernel<NK, row_waves<NK, false>()>), dim3(B), dim3(row_waves<NK, false>() * 64), \
                      0, st, F, E, s, v, wc, cov, lens, a_out, cov_out, covloss, ctx, ctx_bf, T, rep, xper, cg, asrc, cov_keep)
-  if (A == 512) LF(1);
+  // beam decode at A = 512: 12 waves per workgroup (bench_decode 6093 / 6137 vs 6061 / 6105 summaries/s with 16,
+  // 5945 / 5984 with 8: profiles/r5/runs/r5aw)
+  if (A == 512 && rep > 1)
+    hipLaunchKernelGGL((attn_fwd_row_kernel<1, 12>), dim3(B), dim3(12 * 64), 0, st, F, E, s, v, wc, cov, lens, a_out,
+                       cov_out, covloss, ctx, ctx_bf, T, rep, xper, cg, asrc, cov_keep);
+  else if (A == 512) LF(1);
   else LF(2);
 #undef LF
 }
