@@ -766,6 +766,21 @@ void vocab_topk_pg(const Tensor& X, const Tensor& WT, const Tensor& bias, const 
                     stream());
 }
 int64_t vocab_topk_parts(int64_t V, int64_t H) { return vocab_topk_tiles((int)V, (int)H); }
+// attribution: per-phase s_memtime stamps of the decode select kernel into buf ([R][16] int64), or off
+void vocab_select_stamps(const OT& buf) {
+  set_vocab_select_stamps(buf.has_value() && buf->defined() ? (unsigned long long*)buf->data_ptr() : nullptr);
+}
+// attribution probe of the span logits kernel (H = 256; tools/vocab_span_probe.py)
+void vocab_span_probe(const Tensor& X, const Tensor& WT, const Tensor& bias, const Tensor& logits, const Tensor& part_ms,
+                      int64_t R, int64_t V, int64_t probe) {
+  chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(logits, F32, "logits"); chk(part_ms, F32, "part_ms");
+  numel_eq(X, R * 256, "X"); numel_eq(WT, V * 256, "WT"); numel_eq(bias, V, "bias");
+  // (the span-major store probe writes [NW][R][32] floats)
+  TORCH_CHECK(logits.numel() >= std::max(R * V, R * 32 * (int64_t)vocab_topk_tiles((int)V, 256)), "logits too small");
+  numel_eq(part_ms, R * vocab_topk_tiles((int)V, 256) * 2, "part_ms");
+  launch_vocab_span_probe(P<bf16>(X), P<bf16>(WT), P<float>(bias), P<float>(logits), P<float>(part_ms), (int)R, (int)V,
+                          (int)probe, stream());
+}
 
 // One beam-decode step's head: vocab_topk (p_gen inside when the pointer inputs are given) with
 // the beam bookkeeping fused into the select kernel's per-article tail (replaces vocab_topk_pg +
@@ -1076,6 +1091,8 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("pgen", &pgen);
   m.def("vocab_topk", &vocab_topk);
   m.def("vocab_topk_parts", &vocab_topk_parts);
+  m.def("vocab_span_probe", &vocab_span_probe);
+  m.def("vocab_select_stamps", &vocab_select_stamps);
   m.def("vocab_topk_beam", &vocab_topk_beam);
   m.def("dec_cell_fwd_beam", &dec_cell_fwd_beam);
   m.def("beam_sproj_xmerge", &beam_sproj_xmerge);

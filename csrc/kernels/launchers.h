@@ -112,6 +112,9 @@ void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, con
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
                                 unsigned* err, float* dbias, int T, int B, int H, bool dout_bf, hipStream_t st);
 int vocab_topk_tiles(int V, int H);
+void set_vocab_select_stamps(unsigned long long* buf);
+void launch_vocab_span_probe(const bf16* X, const bf16* WT, const float* bias, float* logits, float* part_ms, int R, int V,
+                             int probe, hipStream_t st);
 
 
 // Beam bookkeeping fused into the vocab select kernel (the last row workgroup of each article

@@ -13,6 +13,7 @@
 // Replaces a library GEMM + a separate per-element top-k pass over the logits.
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 #include "attn_common.h"  // f32x2 packed-FP32 helpers
 #include "beam_common.h"  // beam bookkeeping fused into the select kernel's tail
 #include "launchers.h"
@@ -219,6 +220,264 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Column-span logits kernel (H = 128 / 256 / 512): every W^T byte is fetched by ONE wave.
+//
+// The tile kernel above re-reads W^T once per row block and X once per workgroup: at R = 256,
+// V = 50k, H = 256 that is 392 x (128 KB of W^T + 64 KB of X) = 75 MB pulled into the CUs for
+// 25.6 MB of unique data, ~384 KB per CU.  A prologue burst of every CU sustains ~11 B/cycle/CU
+// (MI355X_MICROARCH.md, "prologue HBM burst"), so the fetch alone is ~15 us of its 20.8 us
+// no-store time (profiles/r6/decode_vocab_span.md).
+//
+// Here the grid is one workgroup per CU (G = 256 for V = 50k), 8 waves, and wave q of the grid
+// owns the 16-column tiles [q nt16 / NW, (q + 1) nt16 / NW) (1 or 2 tiles; NW = 8 G): it holds
+// their W^T fragments in registers for the whole launch and multiplies them against ALL rows of
+// X, which the workgroup stages into LDS once (R x H bf16: 128 KB at R = 256, H = 256; rows
+// beyond what fits run as further chunks).  Per CU that is ~100 KB of W^T (HBM) + 128 KB of X
+// (L2): 58 MB chip-wide instead of 75 MB, with the W^T part read exactly once.
+//
+// LDS image of X: row r's 16-byte chunk c sits at chunk slot c ^ (r & 15) of its 2H-byte row (no
+// padding, glds-fillable): the B-fragment read (rows 16 jr + (l & 15), chunk 4 h + (l >> 4)) hits
+// 16 distinct 16-byte bank slots in each of ds_read_b128's four 16-lane groups.
+//
+// Same MFMA sequence as the tile kernel (acc from zero, k-steps ascending, + bias): the logits are
+// bit-identical to it.  Partials: one (max, sum exp) per (row, wave), laid out [G][R][8] so a
+// workgroup's 8 waves write 64 contiguous bytes per row; the select kernel maps partial q back
+// to its column span (vp_span).
+#define VP_WAVES 8
+#define VP_THREADS (64 * VP_WAVES)
+#define VP_NI 2                 // 16-column tiles per wave, at most
+#define VP_LDS (144 * 1024)     // X chunk bytes
+#define VP_CUS 256
+
+__host__ __device__ inline int vp_groups(int V) {
+  const int nt16 = (V + 15) / 16;
+  const int g = nt16 > VP_CUS * VP_WAVES * VP_NI ? (nt16 + VP_WAVES * VP_NI - 1) / (VP_WAVES * VP_NI) : VP_CUS;
+  return min(g, (nt16 + VP_WAVES - 1) / VP_WAVES);
+}
+__host__ __device__ inline bool vp_supported(int H) { return H == 128 || H == 256 || H == 512; }
+// TSAMD_VL_TILE=1: the tile kernel above (A/B switch)
+static inline bool vp_use(int H) {
+  static const bool tile = getenv("TSAMD_VL_TILE") && getenv("TSAMD_VL_TILE")[0] == '1';
+  return vp_supported(H) && !tile;
+}
+// first 16-column tile of partial q (q in [0, NW]; NW = 8 * vp_groups(V))
+__device__ __forceinline__ int vp_lo(int q, int nt16, int NW) { return (int)(((long)q * nt16) / NW); }
+
+// s_barrier with release / acquire fences on LDS only: the workgroup-wide __syncthreads fence
+// also waits for every global load and store in flight (vmcnt(0)), which would end the overlap
+// of the X staging and the logits stores with the MFMAs
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// PROBE (attribution builds only, vocab_span_probe): bit 0 no logits stores, bit 1 no epilogue
+// math (partials from the raw row max), bit 2 no MFMAs (loads + epilogue only)
+//
+// Pipeline: X is staged in sub-chunks of SUBR rows through registers (global_load_dwordx4 ->
+// ds_write_b128), VP_LOOK sub-chunks ahead of the one being multiplied, so the compiler counts
+// every wait exactly (loads, stores and the staging are all visible to it; an LDS-DMA fill is
+// not counted by it and turns the wait for the W^T registers into vmcnt(0)); each CU starts its
+// 1 KB pieces at a different offset; the epilogue of a group runs its row tiles side by side
+// (max, cross-lane steps, exp sums, stores), not one dependent chain per tile.
+#define VP_LOOK 2
+template <int H, int PROBE = 0>
+__global__ __launch_bounds__(VP_THREADS, 1) void vocab_logits_span_kernel(
+    const bf16* __restrict__ X, const bf16* __restrict__ WT, const float* __restrict__ bias,
+    float* __restrict__ logits, float* __restrict__ part_ms, int R, int V) {
+  constexpr float L2E = 1.4426950408889634f;
+  constexpr int KS = H / 32, RB = 2 * H;             // k-steps, LDS row bytes
+  constexpr int SUBR = H >= 512 ? 32 : 64, NJ = SUBR / 16;
+  constexpr int RS = VP_LDS / RB / SUBR * SUBR;      // rows per X chunk
+  constexpr int PS = SUBR * RB / 1024;               // 1 KB pieces per sub-chunk (a multiple of 8)
+  constexpr int PPW = PS / VP_WAVES;                 // pieces per wave per sub-chunk
+  constexpr int MAXSUB = RS / SUBR;
+  extern __shared__ __attribute__((aligned(16))) char Xs[];
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int nt16 = (V + 15) >> 4, NW = gridDim.x * VP_WAVES, q = blockIdx.x * VP_WAVES + wid;
+  const int lo = vp_lo(q, nt16, NW), ni = vp_lo(q + 1, nt16, NW) - lo;
+  const int cw = 16 * lo;  // this wave's first column
+  const int c16 = lane & 15, qd = lane >> 4, kof = 8 * qd;
+  const int rot = (blockIdx.x >> 3) % PS;  // piece rotation of this CU (blockIdx % 8 = XCD)
+  // the wave's W^T fragments: loaded once, before the first X chunk's LDS fill
+  bf16x8 wa[KS][VP_NI];
+#pragma unroll
+  for (int i = 0; i < VP_NI; ++i) {
+    const bf16* arow = WT + (size_t)min(cw + 16 * i + c16, V - 1) * H + kof;
+#pragma unroll
+    for (int h = 0; h < KS; ++h) wa[h][i] = i < ni ? ld8(arow + 32 * h) : bf16x8{};
+  }
+  f32x2 bc[VP_NI][2];
+#pragma unroll
+  for (int i = 0; i < VP_NI; ++i)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int col = cw + 16 * i + 4 * qd + 2 * hh;
+      const bool ok = i < ni;
+      bc[i][hh] = f32x2{ok && col < V ? bias[col] : -INFINITY, ok && col + 1 < V ? bias[col + 1] : -INFINITY};
+    }
+  const bool colfull = (V & 3) == 0 && cw + 16 * ni <= V;
+
+  // sub-chunk s of the chunk at r0: piece j of this wave -> registers, then -> its LDS slot
+  auto issue = [&](int r0, int s, bf16x8 (&st)[PPW]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int pc = s * PS + (wid + VP_WAVES * j + rot) % PS;
+      const int b = pc * 1024 + lane * 16, rr = b / RB, slot = (b % RB) >> 4;
+      st[j] = ld8(X + (size_t)min(r0 + rr, R - 1) * H + ((slot ^ (rr & 15)) << 3));
+    }
+  };
+  auto land = [&](int s, const bf16x8 (&st)[PPW]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int pc = s * PS + (wid + VP_WAVES * j + rot) % PS;
+      *reinterpret_cast<bf16x8*>(Xs + pc * 1024 + lane * 16) = st[j];
+    }
+  };
+  // the multiply + epilogue of sub-chunk s (row tiles 4 s .. of the chunk at r0)
+  auto compute = [&](int r0, int s, int nrt) __attribute__((always_inline)) {
+    const int jg = NJ * s, nj = min(NJ, nrt - jg);
+    f32x4 acc[VP_NI][NJ];
+#pragma unroll
+    for (int i = 0; i < VP_NI; ++i)
+#pragma unroll
+      for (int jr = 0; jr < NJ; ++jr) acc[i][jr] = f32x4{0, 0, 0, 0};
+    // per k-step: the group's NJ fragments first (one LDS round trip), then its MFMAs; the next
+    // k-step's fragments are read under them (xn), so no MFMA waits on a single read
+    auto frag = [&](int h, int jr) __attribute__((always_inline)) {
+      const int rr = 16 * (jg + min(jr, nj - 1)) + c16;
+      return *reinterpret_cast<const bf16x8*>(Xs + rr * RB + (((4 * h + qd) ^ (rr & 15)) << 4));
+    };
+    bf16x8 xb[NJ];
+#pragma unroll
+    for (int jr = 0; jr < NJ; ++jr) xb[jr] = frag(0, jr);
+#pragma unroll
+    for (int h = 0; h < KS; ++h) {
+      bf16x8 xn[NJ];
+      if (h + 1 < KS) {
+#pragma unroll
+        for (int jr = 0; jr < NJ; ++jr) xn[jr] = frag(h + 1, jr);
+      }
+#pragma unroll
+      for (int jr = 0; jr < NJ; ++jr) {
+        if (PROBE & 4) {
+          acc[0][jr][0] += (float)xb[jr][0];
+        } else {
+          acc[0][jr] = mfma16(wa[h][0], xb[jr], acc[0][jr]);
+          if (ni > 1) acc[1][jr] = mfma16(wa[h][1], xb[jr], acc[1][jr]);
+        }
+      }
+      if (h + 1 < KS) {
+#pragma unroll
+        for (int jr = 0; jr < NJ; ++jr) xb[jr] = xn[jr];
+      }
+    }
+    f32x2 x[NJ][VP_NI][2];
+    float m[NJ], sm[NJ];
+#pragma unroll
+    for (int jr = 0; jr < NJ; ++jr) {
+      m[jr] = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < VP_NI; ++i)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          x[jr][i][hh] = f32x2{acc[i][jr][2 * hh], acc[i][jr][2 * hh + 1]} + bc[i][hh];  // -inf past V / ni
+          m[jr] = vmax3(m[jr], x[jr][i][hh].x, x[jr][i][hh].y);
+        }
+    }
+    if (!(PROBE & 2)) {
+#pragma unroll
+      for (int jr = 0; jr < NJ; ++jr) m[jr] = max_x16(m[jr]);
+#pragma unroll
+      for (int jr = 0; jr < NJ; ++jr) m[jr] = max_x32(m[jr]);
+      f32x2 s2[NJ];
+#pragma unroll
+      for (int jr = 0; jr < NJ; ++jr) {
+        s2[jr] = f32x2{0.f, 0.f};
+        const f32x2 mb = f32x2{-m[jr] * L2E, -m[jr] * L2E};
+#pragma unroll
+        for (int i = 0; i < VP_NI; ++i)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const f32x2 t = __builtin_elementwise_fma(x[jr][i][hh], f32x2{L2E, L2E}, mb);
+            s2[jr] += f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};  // exp(-inf) = 0
+          }
+      }
+#pragma unroll
+      for (int jr = 0; jr < NJ; ++jr) sm[jr] = sum_x16(s2[jr].x + s2[jr].y);
+#pragma unroll
+      for (int jr = 0; jr < NJ; ++jr) sm[jr] = sum_x32(sm[jr]);
+    } else {
+#pragma unroll
+      for (int jr = 0; jr < NJ; ++jr) sm[jr] = 0.f;
+    }
+#pragma unroll
+    for (int jr = 0; jr < NJ; ++jr) {
+      if (jr >= nj) break;
+      const int row = r0 + 16 * (jg + jr) + c16;
+      if (row >= R) break;
+      if (lane < 16)
+        *reinterpret_cast<float2*>(part_ms + (((size_t)blockIdx.x * R + row) * VP_WAVES + wid) * 2) =
+            make_float2(m[jr], sm[jr]);
+      if (PROBE & 1) continue;
+      float* dst = logits + (size_t)row * V;
+#pragma unroll
+      for (int i = 0; i < VP_NI; ++i) {
+        if (i >= ni) break;
+        const int col = cw + 16 * i + 4 * qd;
+        if (PROBE & 8) {  // plain (temporal) stores
+          *reinterpret_cast<f32x4*>(dst + col) = f32x4{x[jr][i][0].x, x[jr][i][0].y, x[jr][i][1].x, x[jr][i][1].y};
+        } else if (PROBE & 16) {  // span-major [NW][R][32]: a row's span is one 128-byte line
+          f32x4* d = reinterpret_cast<f32x4*>(logits + (((size_t)q * R + row) * 32) + 8 * qd + 4 * i);
+          __builtin_nontemporal_store(f32x4{x[jr][i][0].x, x[jr][i][0].y, x[jr][i][1].x, x[jr][i][1].y}, d);
+        } else if (PROBE & 32) {  // bf16 logits (half the bytes)
+          typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+          const unsigned a = (unsigned)__builtin_bit_cast(unsigned short, f2bf(x[jr][i][0].x)) |
+                             ((unsigned)__builtin_bit_cast(unsigned short, f2bf(x[jr][i][0].y)) << 16);
+          const unsigned b = (unsigned)__builtin_bit_cast(unsigned short, f2bf(x[jr][i][1].x)) |
+                             ((unsigned)__builtin_bit_cast(unsigned short, f2bf(x[jr][i][1].y)) << 16);
+          __builtin_nontemporal_store(u32x2v{a, b}, reinterpret_cast<u32x2v*>(reinterpret_cast<bf16*>(logits) + (size_t)row * V + col));
+        } else if (colfull) {
+          __builtin_nontemporal_store(f32x4{x[jr][i][0].x, x[jr][i][0].y, x[jr][i][1].x, x[jr][i][1].y},
+                                      reinterpret_cast<f32x4*>(dst + col));
+        } else {
+          const float xv[4] = {x[jr][i][0].x, x[jr][i][0].y, x[jr][i][1].x, x[jr][i][1].y};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < V) dst[col + e] = xv[e];
+        }
+      }
+    }
+  };
+  // one X chunk (rows [r0, r0 + RS)).  FULL: all MAXSUB sub-chunks hold rows (no run-time guard
+  // around a load, so the compiler's wait counts stay exact); otherwise sub-chunks past the
+  // chunk's rows are neither loaded nor multiplied
+  auto chunk = [&](const int r0, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+    const int nrt = (min(RS, R - r0) + 15) >> 4;  // 16-row tiles of this chunk
+    const int nsub = FULL ? MAXSUB : (nrt + NJ - 1) / NJ;
+    if (r0 > 0) lds_barrier();  // the previous chunk's fragment reads are done
+    bf16x8 st[VP_LOOK][PPW];
+#pragma unroll
+    for (int s = 0; s < VP_LOOK && s < MAXSUB; ++s)
+      if (FULL || s < nsub) issue(r0, s, st[s]);
+#pragma unroll
+    for (int s = 0; s < MAXSUB; ++s) {
+      if (FULL || s < nsub) {
+        land(s, st[s % VP_LOOK]);
+        lds_barrier();
+        if (s + VP_LOOK < MAXSUB && (FULL || s + VP_LOOK < nsub)) issue(r0, s + VP_LOOK, st[s % VP_LOOK]);
+        if (ni > 0) compute(r0, s, nrt);
+      }
+    }
+  };
+  int r0 = 0;
+  for (; r0 + RS <= R; r0 += RS) chunk(r0, std::integral_constant<bool, true>{});
+  if (r0 < R) chunk(r0, std::integral_constant<bool, false>{});
+}
+
 namespace {
 __device__ __forceinline__ int vhslot(int w) { return (int)(((unsigned)w * 2654435761u) >> 21) & (VM_HASH - 1); }
 
@@ -281,11 +540,21 @@ __device__ __forceinline__ void pad4(float* v, int* id, int n) {
 // BeamTail (bt.lp_sum set): the last of an article's ``beam`` row workgroups to finish (one
 // arrival counter per article) then runs that article's beam bookkeeping (beam_common.h) --
 // one kernel boundary less per decode step than a separate beam_step launch.
+// attribution builds (tools/vocab_select_stamps.py): thread 0 of each row stamps s_memtime at the
+// phase boundaries into vs_stamps[row][16] (a buffer only the tool reads)
+__device__ unsigned long long* vs_stamps = nullptr;
+#define VS_ST(k)                                                                       \
+  do {                                                                                 \
+    if constexpr (STAMP) {                                                             \
+      if (tid == 0) vs_stamps[(size_t)r * 16 + (k)] = __builtin_amdgcn_s_memtime();    \
+    }                                                                                  \
+  } while (0)
+template <bool STAMP = false>
 __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     const float* __restrict__ logits, const float* __restrict__ part_ms, const float* __restrict__ pgen,
     const float* __restrict__ attn, const int* __restrict__ ext, const int* __restrict__ lens,
     int* __restrict__ out_ids, float* __restrict__ out_lp, int V, int T, int K, int beam, int nt, int tcols, PgIn pgi,
-    BeamTail bt) {
+    BeamTail bt, int span) {  // span: partials of vocab_logits_span_kernel (nt = NW waves, [G][R][8], vp_lo columns)
   __shared__ float bt_cval[64];
   __shared__ int bt_cid[64], bt_srt[64];
   __shared__ int bt_last;
@@ -301,6 +570,7 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   const int r = blockIdx.x, tid = threadIdx.x;
   const int art = r / beam;
   const float* z = logits + (size_t)r * V;
+  VS_ST(0);
   constexpr int PPT = VM_CAND / VS_THREADS;  // tile partials per thread (nt <= 4096)
   constexpr int TPT = 2048 / VS_THREADS;     // source positions per thread (T <= 2048)
   constexpr int SPT = VM_HASH / VS_THREADS;  // hash slots per thread
@@ -323,7 +593,14 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
 #pragma unroll
   for (int u = 0; u < PPT; ++u) {
     const int q = tid + u * VS_THREADS;
-    pm[u] = q < nt ? *reinterpret_cast<const float2*>(part_ms + ((size_t)r * nt + q) * 2) : make_float2(-INFINITY, 0.f);
+    if (span) {  // empty spans (V < 16 NW) hold no partial
+      const int nt16 = (V + 15) >> 4;
+      pm[u] = q < nt && vp_lo(q + 1, nt16, nt) > vp_lo(q, nt16, nt)
+                  ? *reinterpret_cast<const float2*>(part_ms + (((size_t)(q >> 3) * gridDim.x + r) * VP_WAVES + (q & 7)) * 2)
+                  : make_float2(-INFINITY, 0.f);
+    } else {
+      pm[u] = q < nt ? *reinterpret_cast<const float2*>(part_ms + ((size_t)r * nt + q) * 2) : make_float2(-INFINITY, 0.f);
+    }
   }
   int ew[TPT];
   float ea[TPT];
@@ -345,6 +622,7 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     if (tid == 0 && pgi.out) pgi.out[r] = pg;
   }
   __syncthreads();  // hash cleared before the inserts below (and red free for block_max)
+  VS_ST(1);
   // pointer copy mass per extended-vocab word (LDS hash)
 #pragma unroll
   for (int u = 0; u < TPT; ++u) {
@@ -361,7 +639,9 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     }
   }
   // log-sum-exp of the row from the partials
+  VS_ST(2);
   const float M = block_max<VS_THREADS>(m, red);
+  VS_ST(3);
   float s = 0.f;
 #pragma unroll
   for (int u = 0; u < PPT; ++u)
@@ -374,6 +654,7 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
     if (q < nt) atomicMax(&gkey[q % K], okey(pm[u].x));
   }
   const float lse = M + __logf(block_sum<VS_THREADS>(s, red));  // (its syncs also close the hash inserts)
+  VS_ST(4);
   float gmin = INFINITY;
   for (int g = 0; g < K; ++g) gmin = fminf(gmin, okey_inv(gkey[g]));
 #pragma unroll
@@ -391,8 +672,10 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   __syncthreads();
   // the K tiles with the largest maxima hold the plain top-K (value desc, index asc): an
   // element of any other tile is <= its tile max <= tau, and each selected tile max beats it
+  VS_ST(5);
   rank_select(cv, ci, (ntile + 3) & ~3, K, pv_s[0], pi_s[0]);
   __syncthreads();
+  VS_ST(6);
   if (tid == 0) ncand = 0;
   const float tau = pv_s[0][K - 1];
   // ---- round trip 2: the K selected tiles' logits and the copied words' logits
@@ -403,7 +686,13 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   for (int u = 0; u < EPT; ++u) {
     const int e = tid + u * VS_THREADS;
     const int tq = e < K * tcols ? pi_s[0][e / tcols] : VS_NONE;
-    cs[u] = tq < nt ? tq * tcols + (e % tcols) : V;
+    if (span) {  // tile tq = columns [16 vp_lo(tq), 16 vp_lo(tq + 1)), tcols = 16 VP_NI
+      const int nt16 = (V + 15) >> 4;
+      const int c = tq < nt ? 16 * vp_lo(tq, nt16, nt) + (e % tcols) : V;
+      cs[u] = tq < nt && c < 16 * vp_lo(tq + 1, nt16, nt) ? c : V;
+    } else {
+      cs[u] = tq < nt ? tq * tcols + (e % tcols) : V;
+    }
     zs[u] = cs[u] < V ? z[cs[u]] : -INFINITY;
   }
   int wk[SPT];
@@ -422,6 +711,7 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   for (int u = 0; u < EPT; ++u)
     if (cs[u] < V) atomicMax(&gkey3[(tid + u * VS_THREADS) % K], okey(zs[u]));
   __syncthreads();  // ncand reset, the tile list and the group maxima read by everyone before the appends
+  VS_ST(7);
   float tau2 = INFINITY;
   for (int g = 0; g < K; ++g) tau2 = fminf(tau2, okey_inv(gkey3[g]));
   tau2 = fmaxf(tau2, tau);
@@ -436,8 +726,10 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   const int nc = ncand;
   pad4(cv, ci, nc);
   __syncthreads();
+  VS_ST(8);
   rank_select(cv, ci, (nc + 3) & ~3, K, pv_s[1], pi_s[1]);  // plain top-K
   __syncthreads();
+  VS_ST(9);
   // final candidates: plain top-K (copied words masked: their entry below is exact) U copied words
   if (tid < K) {
     const int w = pi_s[1][tid];
@@ -484,8 +776,10 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   const int nf = K + ncopy;
   pad4(cv, ci, nf);
   __syncthreads();
+  VS_ST(10);
   rank_select(cv, ci, (nf + 3) & ~3, K, pv_s[2], pi_s[2]);
   __syncthreads();
+  VS_ST(11);
   if (tid < K) {
     out_ids[(size_t)r * K + tid] = pi_s[2][tid];
     out_lp[(size_t)r * K + tid] = __logf(pv_s[2][tid]);
@@ -513,15 +807,71 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
       beam_article_tail(bt, art, bt_cval, bt_cid, bt_srt);
     }
   }
+  VS_ST(12);
 }
 
-int vocab_topk_tiles(int V, int H) { return (V + vt_cols(H) - 1) / vt_cols(H); }
+// attribution probe: one span-kernel launch with PROBE bits (H = 256)
+void launch_vocab_span_probe(const bf16* X, const bf16* WT, const float* bias, float* logits, float* part_ms, int R, int V,
+                             int probe, hipStream_t st) {
+  const int nt = VP_WAVES * vp_groups(V);
+  const size_t lds = (size_t)min(VP_LDS / 512 / 64 * 64, (R + 63) / 64 * 64) * 512;
+#define VPP(PB)                                                                                               \
+  do {                                                                                                        \
+    auto kfn = vocab_logits_span_kernel<256, PB>;                                                             \
+    (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);      \
+    hipLaunchKernelGGL(kfn, dim3(nt / VP_WAVES), dim3(VP_THREADS), lds, st, X, WT, bias, logits, part_ms, R, V); \
+  } while (0)
+  switch (probe) {
+    case 0: VPP(0); break;
+    case 1: VPP(1); break;
+    case 3: VPP(3); break;
+    case 4: VPP(4); break;
+    case 5: VPP(5); break;
+    case 8: VPP(8); break;
+    case 16: VPP(16); break;
+    case 32: VPP(32); break;
+    default: VPP(7); break;
+  }
+#undef VPP
+}
+
+static bool vs_stamp_host = false;
+// attribution: stamps of the span-path select kernel go to buf ([R][16] u64); nullptr turns them off
+void set_vocab_select_stamps(unsigned long long* buf) {
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(vs_stamps), &buf, sizeof(buf));
+  vs_stamp_host = buf != nullptr;
+}
+
+int vocab_topk_tiles(int V, int H) { return vp_use(H) ? VP_WAVES * vp_groups(V) : (V + vt_cols(H) - 1) / vt_cols(H); }
 
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
                        int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st, const BeamTail* bt) {
-  const int nt = vocab_topk_tiles(V, H), tcols = vt_cols(H);
+  const int nt = vocab_topk_tiles(V, H);
   const BeamTail none{};
+  const bool span = vp_use(H);
+  if (span) {
+    const int subr = H >= 512 ? 32 : 64, rs = VP_LDS / (2 * H) / subr * subr;
+    const size_t lds = (size_t)min(rs, (R + subr - 1) / subr * subr) * 2 * H;
+#define VPL(HH)                                                                                             \
+  do {                                                                                                      \
+    auto kfn = vocab_logits_span_kernel<HH>;                                                                \
+    (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
+    hipLaunchKernelGGL(kfn, dim3(nt / VP_WAVES), dim3(VP_THREADS), lds, st, X, WT, bias, logits, part_ms, R, V); \
+  } while (0)
+    if (H == 128) VPL(128);
+    else if (H == 256) VPL(256);
+    else VPL(512);
+#undef VPL
+    if (vs_stamp_host)
+      hipLaunchKernelGGL(vocab_select_kernel<true>, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens,
+                         out_ids, out_lp, V, T, K, beam, nt, 16 * VP_NI, pgi, bt ? *bt : none, 1);
+    else
+      hipLaunchKernelGGL(vocab_select_kernel<false>, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens,
+                         out_ids, out_lp, V, T, K, beam, nt, 16 * VP_NI, pgi, bt ? *bt : none, 1);
+    return;
+  }
+  const int tcols = vt_cols(H);
   // default: 128-row workgroups (392 at R = 256, V = 50k: one round at 2 per CU; W^T fragments
   // fetched once per 128 rows): decode 5610 -> 5927 summaries/s at 64 articles, 6940 -> 7300 at
   // 128 (64-row workgroups, 784 at R = 256, run 1.5 rounds)
@@ -536,6 +886,6 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
     hipLaunchKernelGGL((vocab_logits_kernel<2, 1, 512, true>), dim3(8 * RB * ((nt + 7) / 8)), dim3(256), 0, st, X, WT,
                        bias, logits, part_ms, R, V, H);
   }
-  hipLaunchKernelGGL(vocab_select_kernel, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens, out_ids,
-                     out_lp, V, T, K, beam, nt, tcols, pgi, bt ? *bt : none);
+  hipLaunchKernelGGL(vocab_select_kernel<false>, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens,
+                     out_ids, out_lp, V, T, K, beam, nt, tcols, pgi, bt ? *bt : none, 0);
 }

@@ -32,3 +32,31 @@ def make_dataset(root, n_files=2, per_file=12, seed=0, corpus=None):
     vp = os.path.join(root, "vocab")
     c.vocab().save(vp)
     return d, vp, c
+
+
+def grad_mismatches(params, g_hip, g_ref, rel=5e-2, abs_frac=1e-3):
+    """Per-parameter gradient check of an engine against the fp32 oracle.  A parameter whose
+    reference gradient norm is >= 1e-6 must match at relative error < ``rel``; a smaller one
+    (a near-zero gradient at init, where relative error is noise) must match absolutely, within
+    ``abs_frac`` of the GLOBAL reference gradient norm -- never a looser relative bound.
+    Returns [(name, rel_err, ref_norm, abs_err)] of the failures."""
+    gnorm = float(g_ref.norm())
+    bad = []
+    for n in params.names:
+        o, c = params.offsets[n]
+        gr, gh = g_ref[o:o + c], g_hip[o:o + c]
+        gn, d = float(gr.norm()), float((gh - gr).norm())
+        ok = d <= abs_frac * gnorm if gn < 1e-6 else d < rel * gn
+        if not ok:
+            bad.append((n, round(d / (gn + 1e-12), 4), gn, d))
+    return bad
+
+
+def grad_rel(params, g_hip, g_ref):
+    """{name: relative gradient error} against the oracle."""
+    out = {}
+    for n in params.names:
+        o, c = params.offsets[n]
+        gr = g_ref[o:o + c]
+        out[n] = float((g_hip[o:o + c] - gr).norm() / (gr.norm() + 1e-12))
+    return out

@@ -22,6 +22,7 @@ from textsummarization_on_flink_amd.config import HParams
 from textsummarization_on_flink_amd.data.synthetic import SyntheticCorpus, make_batches
 from textsummarization_on_flink_amd.models.params import build_params
 from textsummarization_on_flink_amd.models.reference import ReferencePointerGenerator, batch_to_tensors
+from helpers import grad_mismatches, grad_rel
 
 pytestmark = pytest.mark.gpu
 
@@ -78,20 +79,23 @@ def _oracle_check(hps, B, T_, D_, seed, cov_tol=2e-2):
     assert abs(float(got["coverage_loss"]) - float(ref["coverage_loss"])) < cov_tol * abs(float(ref["coverage_loss"]))
     assert _rel(att[live], ref["attn_dists"].detach()[:, src][live]) < 2e-2
     assert _rel(pg[live], ref["p_gens"].detach()[:, src][live]) < 2e-2
-    bad = []
-    for n in params.names:
-        o, c = params.offsets[n]
-        r = _rel(g_hip[o:o + c], g_ref[o:o + c])
-        gn = float(g_ref[o:o + c].norm())
-        if not (r < 5e-2 or (gn < 1e-6 and r < 0.2)):
-            bad.append((n, round(r, 4), gn))
+    bad = grad_mismatches(params, g_hip, g_ref)
     assert not bad, bad
+    kinds["grad_rel"] = grad_rel(params, g_hip, g_ref)
     return kinds
 
 
 def test_bench_shape_matches_fp32_oracle():
     kinds = _oracle_check(_hps(256, trunc_norm_init_std=0.05), 256, T, D, seed=11)
     assert kinds["persistent_lstm"] and kinds["fused_vocab"] and kinds["row_attn_bwd"] and kinds["proj_attn"]
+    # the small parameters whose gradients are near zero at a larger init (coverage w_c, the p_gen
+    # bias, the reduce-state biases: attention_decoder.py:72-73, 164-168; model.py:111-114) are
+    # each checked on their own at this init, at the same relative bound as the large ones
+    rel = kinds["grad_rel"]
+    small = [n for n in rel if n.endswith(("coverage/w_c", "calculate_pgen/Linear/Bias", "bias_reduce_c",
+                                           "bias_reduce_h"))]
+    assert len(small) == 4, small
+    assert all(rel[n] < 5e-2 for n in small), {n: rel[n] for n in small}
 
 
 @pytest.mark.parametrize("B", [8, 128, 512, 1024])
