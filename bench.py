@@ -371,6 +371,10 @@ def bench_config5(args, info, D, torch, dev_id):
                           use_graph=not args.no_graph)
         warm(tr, batches)
     n_warm = len(batches)
+    # the footprint of the CHOSEN batch: the capacity search's peak also holds larger candidates'
+    # partial allocations and the freed trial trainer (reported apart)
+    trial_peak = torch.cuda.max_memory_allocated(dev_id) / 2 ** 30
+    torch.cuda.reset_peak_memory_stats(dev_id)
 
     def loop():
         tokens = 0
@@ -391,6 +395,7 @@ def bench_config5(args, info, D, torch, dev_id):
     rec = {"config5_tokens_per_sec": round(tok_all / el_max, 1),
            "config5_ms_per_step": round(1000.0 * el_max / args.config5_steps, 3),
            "config5_peak_mem_gb": round(peak, 1),
+           "config5_search_peak_mem_gb": round(D.all_reduce_scalar(trial_peak, info, op="max", device=dev), 1),
            "config5_config": {"model": f"pointer-generator+coverage hidden={c['hidden']} emb={args.emb} "
                                        f"enc={c['enc']} dec={args.dec} vocab={args.vocab} enc_layers={c['layers']}",
                               "per_gpu_batch": B, "global_batch": B * info.world,

@@ -354,6 +354,11 @@ void tr01(const Tensor& in, const OT& out, const OT& outb, int64_t np_, int64_t 
   TORCH_CHECK(!acc || (out.has_value() && !outb.has_value()), "tr01: acc adds into out (no bf16 twin)");
   numel_eq(in, np_ * nq * nr, "in");
   chko(out, F32, np_ * nq * nr, "out"); chko(outb, BF, np_ * nq * nr, "outb");
+  // 16-byte fp32 vector accesses, 8-byte bf16 stores: a contiguous view at an offset (a per-step
+  // slice) must still be aligned
+  TORCH_CHECK((uintptr_t)in.data_ptr() % 16 == 0, "tr01: in must be 16-byte aligned");
+  TORCH_CHECK(!PO<float>(out) || (uintptr_t)PO<float>(out) % 16 == 0, "tr01: out must be 16-byte aligned");
+  TORCH_CHECK(!PO<bf16>(outb) || (uintptr_t)PO<bf16>(outb) % 8 == 0, "tr01: outb must be 8-byte aligned");
   launch_tr01(P<float>(in), PO<float>(out), PO<bf16>(outb), (int)np_, (int)nq, (int)nr, acc, stream());
 }
 void cast_colsum(const Tensor& x, const Tensor& xb, const Tensor& colsum, int64_t N, int64_t C) {
@@ -776,7 +781,7 @@ void vocab_span_probe(const Tensor& X, const Tensor& WT, const Tensor& bias, con
   chk(X, BF, "X"); chk(WT, BF, "WT"); chk(bias, F32, "bias"); chk(logits, F32, "logits"); chk(part_ms, F32, "part_ms");
   numel_eq(X, R * 256, "X"); numel_eq(WT, V * 256, "WT"); numel_eq(bias, V, "bias");
   // (the span-major store probe writes [NW][R][32] floats)
-  TORCH_CHECK(logits.numel() >= std::max(R * V, R * 32 * (int64_t)vocab_topk_tiles((int)V, 256)), "logits too small");
+  TORCH_CHECK(logits.numel() >= std::max(R * V, R * 32 * 8 * (int64_t)vocab_topk_tiles((int)V, 256)), "logits too small");
   numel_eq(part_ms, R * vocab_topk_tiles((int)V, 256) * 2, "part_ms");
   launch_vocab_span_probe(P<bf16>(X), P<bf16>(WT), P<float>(bias), P<float>(logits), P<float>(part_ms), (int)R, (int)V,
                           (int)probe, stream());

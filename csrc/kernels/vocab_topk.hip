@@ -247,7 +247,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 #define VP_WAVES 8
 #define VP_THREADS (64 * VP_WAVES)
 #define VP_NI 2                 // 16-column tiles per wave, at most
-#define VP_LDS (144 * 1024)     // X chunk bytes
+#define VP_LDS (150 * 1024)     // X chunk + per-wave row partials (RB + 64 bytes per row)
+// rows per X chunk: a multiple of the sub-chunk rows within VP_LDS
+__host__ __device__ constexpr int vp_subr(int H) { return H >= 512 ? 32 : 64; }
+__host__ __device__ constexpr int vp_rows(int H) { return VP_LDS / (2 * H + 8 * VP_WAVES) / vp_subr(H) * vp_subr(H); }
+__host__ __device__ inline int vp_xrows(int H, int R) { return min(vp_rows(H), (R + vp_subr(H) - 1) / vp_subr(H) * vp_subr(H)); }
 #define VP_CUS 256
 
 __host__ __device__ inline int vp_groups(int V) {
@@ -289,12 +293,15 @@ __global__ __launch_bounds__(VP_THREADS, 1) void vocab_logits_span_kernel(
     float* __restrict__ logits, float* __restrict__ part_ms, int R, int V) {
   constexpr float L2E = 1.4426950408889634f;
   constexpr int KS = H / 32, RB = 2 * H;             // k-steps, LDS row bytes
-  constexpr int SUBR = H >= 512 ? 32 : 64, NJ = SUBR / 16;
-  constexpr int RS = VP_LDS / RB / SUBR * SUBR;      // rows per X chunk
+  constexpr int SUBR = vp_subr(H), NJ = SUBR / 16;
+  constexpr int RS = vp_rows(H);                     // rows per X chunk
   constexpr int PS = SUBR * RB / 1024;               // 1 KB pieces per sub-chunk (a multiple of 8)
   constexpr int PPW = PS / VP_WAVES;                 // pieces per wave per sub-chunk
   constexpr int MAXSUB = RS / SUBR;
   extern __shared__ __attribute__((aligned(16))) char Xs[];
+  // per-wave (max, sum exp) of the chunk's rows, after the X image: [VP_WAVES][xrows]
+  float2* Pw = reinterpret_cast<float2*>(Xs + (size_t)vp_xrows(H, R) * RB);
+  const int xrows = vp_xrows(H, R);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int nt16 = (V + 15) >> 4, NW = gridDim.x * VP_WAVES, q = blockIdx.x * VP_WAVES + wid;
   const int lo = vp_lo(q, nt16, NW), ni = vp_lo(q + 1, nt16, NW) - lo;
@@ -418,9 +425,7 @@ __global__ __launch_bounds__(VP_THREADS, 1) void vocab_logits_span_kernel(
       if (jr >= nj) break;
       const int row = r0 + 16 * (jg + jr) + c16;
       if (row >= R) break;
-      if (lane < 16)
-        *reinterpret_cast<float2*>(part_ms + (((size_t)blockIdx.x * R + row) * VP_WAVES + wid) * 2) =
-            make_float2(m[jr], sm[jr]);
+      if (lane < 16) Pw[wid * xrows + row - r0] = make_float2(m[jr], sm[jr]);
       if (PROBE & 1) continue;
       float* dst = logits + (size_t)row * V;
 #pragma unroll
@@ -471,6 +476,17 @@ __global__ __launch_bounds__(VP_THREADS, 1) void vocab_logits_span_kernel(
         if (s + VP_LOOK < MAXSUB && (FULL || s + VP_LOOK < nsub)) issue(r0, s + VP_LOOK, st[s % VP_LOOK]);
         if (ni > 0) compute(r0, s, nrt);
       }
+    }
+    // the workgroup's (max, sum exp) per row over its 8 waves' spans -> part_ms[row][G] (waves with
+    // an empty span wrote nothing)
+    lds_barrier();
+    const int nr = min(RS, R - r0), q0 = blockIdx.x * VP_WAVES;
+    for (int rr = threadIdx.x; rr < nr; rr += VP_THREADS) {
+      float mm = -INFINITY, ss = 0.f;
+#pragma unroll
+      for (int w = 0; w < VP_WAVES; ++w)
+        if (vp_lo(q0 + w + 1, nt16, NW) > vp_lo(q0 + w, nt16, NW)) ms_combine(mm, ss, Pw[w * xrows + rr].x, Pw[w * xrows + rr].y);
+      *reinterpret_cast<float2*>(part_ms + ((size_t)(r0 + rr) * gridDim.x + blockIdx.x) * 2) = make_float2(mm, ss);
     }
   };
   int r0 = 0;
@@ -593,14 +609,7 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
 #pragma unroll
   for (int u = 0; u < PPT; ++u) {
     const int q = tid + u * VS_THREADS;
-    if (span) {  // empty spans (V < 16 NW) hold no partial
-      const int nt16 = (V + 15) >> 4;
-      pm[u] = q < nt && vp_lo(q + 1, nt16, nt) > vp_lo(q, nt16, nt)
-                  ? *reinterpret_cast<const float2*>(part_ms + (((size_t)(q >> 3) * gridDim.x + r) * VP_WAVES + (q & 7)) * 2)
-                  : make_float2(-INFINITY, 0.f);
-    } else {
-      pm[u] = q < nt ? *reinterpret_cast<const float2*>(part_ms + ((size_t)r * nt + q) * 2) : make_float2(-INFINITY, 0.f);
-    }
+    pm[u] = q < nt ? *reinterpret_cast<const float2*>(part_ms + ((size_t)r * nt + q) * 2) : make_float2(-INFINITY, 0.f);
   }
   int ew[TPT];
   float ea[TPT];
@@ -686,10 +695,10 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
   for (int u = 0; u < EPT; ++u) {
     const int e = tid + u * VS_THREADS;
     const int tq = e < K * tcols ? pi_s[0][e / tcols] : VS_NONE;
-    if (span) {  // tile tq = columns [16 vp_lo(tq), 16 vp_lo(tq + 1)), tcols = 16 VP_NI
-      const int nt16 = (V + 15) >> 4;
-      const int c = tq < nt ? 16 * vp_lo(tq, nt16, nt) + (e % tcols) : V;
-      cs[u] = tq < nt && c < 16 * vp_lo(tq + 1, nt16, nt) ? c : V;
+    if (span) {  // tile tq = workgroup tq's columns [16 vp_lo(8 tq), 16 vp_lo(8 tq + 8)), tcols its maximum
+      const int nt16 = (V + 15) >> 4, nw = VP_WAVES * nt;
+      const int c = tq < nt ? 16 * vp_lo(VP_WAVES * tq, nt16, nw) + (e % tcols) : V;
+      cs[u] = tq < nt && c < 16 * vp_lo(VP_WAVES * tq + VP_WAVES, nt16, nw) ? c : V;
     } else {
       cs[u] = tq < nt ? tq * tcols + (e % tcols) : V;
     }
@@ -813,13 +822,13 @@ __global__ __launch_bounds__(VS_THREADS) void vocab_select_kernel(
 // attribution probe: one span-kernel launch with PROBE bits (H = 256)
 void launch_vocab_span_probe(const bf16* X, const bf16* WT, const float* bias, float* logits, float* part_ms, int R, int V,
                              int probe, hipStream_t st) {
-  const int nt = VP_WAVES * vp_groups(V);
-  const size_t lds = (size_t)min(VP_LDS / 512 / 64 * 64, (R + 63) / 64 * 64) * 512;
+  const int nt = vp_groups(V);
+  const size_t lds = (size_t)vp_xrows(256, R) * (512 + 8 * VP_WAVES);
 #define VPP(PB)                                                                                               \
   do {                                                                                                        \
     auto kfn = vocab_logits_span_kernel<256, PB>;                                                             \
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);      \
-    hipLaunchKernelGGL(kfn, dim3(nt / VP_WAVES), dim3(VP_THREADS), lds, st, X, WT, bias, logits, part_ms, R, V); \
+    hipLaunchKernelGGL(kfn, dim3(nt), dim3(VP_THREADS), lds, st, X, WT, bias, logits, part_ms, R, V); \
   } while (0)
   switch (probe) {
     case 0: VPP(0); break;
@@ -842,7 +851,7 @@ void set_vocab_select_stamps(unsigned long long* buf) {
   vs_stamp_host = buf != nullptr;
 }
 
-int vocab_topk_tiles(int V, int H) { return vp_use(H) ? VP_WAVES * vp_groups(V) : (V + vt_cols(H) - 1) / vt_cols(H); }
+int vocab_topk_tiles(int V, int H) { return vp_use(H) ? vp_groups(V) : (V + vt_cols(H) - 1) / vt_cols(H); }
 
 void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const float* pgen, const float* attn,
                        const int* ext, const int* lens, int* out_ids, float* out_lp, float* logits, float* part_ms,
@@ -851,13 +860,12 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
   const BeamTail none{};
   const bool span = vp_use(H);
   if (span) {
-    const int subr = H >= 512 ? 32 : 64, rs = VP_LDS / (2 * H) / subr * subr;
-    const size_t lds = (size_t)min(rs, (R + subr - 1) / subr * subr) * 2 * H;
+    const size_t lds = (size_t)vp_xrows(H, R) * (2 * H + 8 * VP_WAVES);
 #define VPL(HH)                                                                                             \
   do {                                                                                                      \
     auto kfn = vocab_logits_span_kernel<HH>;                                                                \
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
-    hipLaunchKernelGGL(kfn, dim3(nt / VP_WAVES), dim3(VP_THREADS), lds, st, X, WT, bias, logits, part_ms, R, V); \
+    hipLaunchKernelGGL(kfn, dim3(nt), dim3(VP_THREADS), lds, st, X, WT, bias, logits, part_ms, R, V); \
   } while (0)
     if (H == 128) VPL(128);
     else if (H == 256) VPL(256);
@@ -865,10 +873,10 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
 #undef VPL
     if (vs_stamp_host)
       hipLaunchKernelGGL(vocab_select_kernel<true>, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens,
-                         out_ids, out_lp, V, T, K, beam, nt, 16 * VP_NI, pgi, bt ? *bt : none, 1);
+                         out_ids, out_lp, V, T, K, beam, nt, 16 * VP_NI * VP_WAVES, pgi, bt ? *bt : none, 1);
     else
       hipLaunchKernelGGL(vocab_select_kernel<false>, dim3(R), dim3(VS_THREADS), 0, st, logits, part_ms, pgen, attn, ext, lens,
-                         out_ids, out_lp, V, T, K, beam, nt, 16 * VP_NI, pgi, bt ? *bt : none, 1);
+                         out_ids, out_lp, V, T, K, beam, nt, 16 * VP_NI * VP_WAVES, pgi, bt ? *bt : none, 1);
     return;
   }
   const int tcols = vt_cols(H);

@@ -312,6 +312,83 @@ def test_synced_batcher_stops_every_rank_at_the_same_step(lengths, window):
         assert coll <= n // window + 1, (r, coll)
 
 
+def _synced_nccl_layout_worker(rank, world, port, q, lengths, window):
+    """The production GPU layout: the default group is the gradient backend (RCCL there; gloo
+    stands in for it here) and the window agreement runs on the dedicated gloo group cpu_group()
+    creates when the default backend is "nccl" -- with a gradient-sized collective on the default
+    group after every batch, interleaved with the agreement collectives."""
+    import dataclasses
+    info = _init(rank, world, port)
+    from textsummarization_on_flink_amd.parallel import dist as D
+    nccl_info = dataclasses.replace(info, backend="nccl")
+    grp = D.cpu_group(nccl_info)
+    assert grp is not None and grp is not torch.distributed.group.WORLD
+    sb = D.SyncedBatcher(_ListBatcher(lengths[rank]), nccl_info, window=window)
+    assert sb._group is grp
+    got, grads = [], []
+    while True:
+        b = sb.next_batch()
+        if b is None:
+            break
+        got.append(b)
+        g = torch.full((4096,), float(rank + 1))
+        torch.distributed.all_reduce(g)  # the step's gradient all-reduce on the default group
+        grads.append(float(g[0]))
+    sb.close()
+    after = torch.ones(1)
+    torch.distributed.all_reduce(after)  # every rank reaches the next collective after the stop
+    q.put((rank, got, sb.collectives, grads, float(after[0])))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("lengths,window", [((23, 17), 5), ((3, 40), 4)])
+def test_synced_batcher_on_dedicated_gloo_group_beside_gradient_collectives(lengths, window):
+    """SyncedBatcher under the NCCL default backend agrees on a dedicated gloo subgroup
+    (dist.new_group(backend="gloo")): every rank stops after the shortest stream's batch count,
+    each step's default-group all-reduce pairs up across ranks (sum = 1 + 2), and every rank
+    reaches a later collective."""
+    res = _spawn(_synced_nccl_layout_worker, 2, lengths, window)
+    n = min(lengths)
+    for r in range(2):
+        got, coll, grads, after = res[r]
+        assert got == list(range(n)), (r, got)
+        assert coll <= n // window + 1
+        assert grads == [3.0] * n and after == 2.0
+
+
+class _BlockingBatcher:
+    """A stream that blocks in next_batch until stopped (a training run ended before its stream)."""
+    def __init__(self):
+        import threading
+        self.n = 0
+        self.stopped = threading.Event()
+
+    def next_batch(self):
+        if self.n < 3:
+            self.n += 1
+            return self.n
+        self.stopped.wait(30)
+        return None
+
+    def interrupt(self):
+        self.stopped.set()
+
+
+def test_synced_batcher_close_stops_a_blocked_source_promptly():
+    """close() before the stream ends must interrupt the inner source before joining
+    the prefetch thread, not wait out the join timeout with the thread blocked in
+    next_batch() (flink_entry then releases the rings under it)."""
+    import time
+    from textsummarization_on_flink_amd.parallel.dist import DistInfo, SyncedBatcher
+    inner = _BlockingBatcher()
+    sb = SyncedBatcher(inner, DistInfo(rank=0, world=2, backend="gloo"), window=2, group=object())
+    time.sleep(0.3)  # the prefetch thread took the 3 batches and blocks in next_batch
+    t0 = time.monotonic()
+    sb.close()
+    assert time.monotonic() - t0 < 1.0 and inner.stopped.is_set()
+    assert not sb._thread.is_alive()
+
+
 def _agree_worker(rank, world, port, q, fits_on_rank1):
     info = _init(rank, world, port)
     import sys as _sys

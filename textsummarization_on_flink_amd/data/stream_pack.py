@@ -96,6 +96,7 @@ class _Pool:
 
     def __init__(self, target, n: int, extra_rings: int, ring_bytes: int, args: tuple):
         from ..runtime.ring import RecordRing
+        self.interrupted = False
         from ..utils.forking import fork_safe
         if n < 1:
             raise ValueError("packers must be >= 1")
@@ -121,6 +122,8 @@ class _Pool:
         packer died or reported an error."""
         t0 = time.time()
         while True:
+            if self.interrupted:  # interrupt(): the consumer stopped before the stream ended
+                return None
             try:
                 rec = self.rings[p][ring].pop(timeout_ms=100)
             except TimeoutError:
@@ -258,6 +261,11 @@ class StreamTrainPacker:
         meta, payload = got
         self.k += 1
         return PackedBatch(payload, meta["shape"], meta["tokens"], meta["padded"], meta["valid"])
+
+    def interrupt(self):
+        """Make a pending / later ``next_batch`` return None within one 100 ms pop slice, without
+        releasing anything (a prefetch thread may still be inside the pop; ``stop`` after it)."""
+        self.pool.interrupted = True
 
     def stop(self):
         self.pool.stop()

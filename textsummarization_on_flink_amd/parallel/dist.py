@@ -291,6 +291,14 @@ class SyncedBatcher:
         return self._buf.popleft()
 
     def close(self):
+        """Stop the prefetch thread.  A run that ends before its stream leaves the thread blocked
+        inside ``inner.next_batch()`` (a stream packer's pool pop waits while the packers live):
+        the inner source is interrupted first (``interrupt()``: its pop returns None within one
+        poll slice, nothing released), so the join returns at once and the caller's
+        ``packer.stop()`` afterwards releases rings no thread is reading."""
         self._stop.set()
-        if self._thread is not None:
+        if self._thread is not None and self._thread.is_alive():
+            fn = getattr(self.inner, "interrupt", None)
+            if callable(fn):
+                fn()
             self._thread.join(timeout=5)

@@ -21,7 +21,7 @@ def main():
     WT = (torch.randn(V, H, generator=g) * 0.1).to("cuda", torch.bfloat16)
     bias = (torch.randn(V, generator=g) * 0.1).cuda()
     nt = int(k.vocab_topk_parts(V, H))
-    lg = torch.empty(max(R * V, nt * R * 32), device="cuda")  # the span-major probe writes [nt][R][32]
+    lg = torch.empty(max(R * V, 8 * nt * R * 32), device="cuda")  # the span-major probe writes [8 nt waves][R][32]
     pms = torch.empty(R, nt, 2, device="cuda")
     if os.environ.get("PMC"):  # counter pass: a few production launches only
         for _ in range(5):
