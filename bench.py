@@ -208,6 +208,8 @@ def main(argv=None):
     if _pg.BLT:  # library GEMMs through blt_mm: GEMM shapes seen / given a timed candidate search
         st = tr.engine.k.blt_stats()
         eng_flags["blt_mm"] = {"keys": int(st[0]), "tuned": int(st[1])}
+    # which activation GEMMs ran on the hand-written kernel (fixed table, not per-run timing)
+    eng_flags["gemm_dispatch"] = _pg.gemm_bt_stats()
     c5 = None
     if args.config5_steps > 0 and args.hidden != 512:
         del tr, batches

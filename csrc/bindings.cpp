@@ -512,6 +512,37 @@ void ptr_loss(const Tensor& logits, const OT& bias, const Tensor& target, const 
 
 // weight gradient out[M][N] += a[K][M]^T . b[K][N] (wgrad.hip): 2-D row-major views with unit
 // column stride (row strides free), out fp32 and already zero (split-K atomics)
+// out[Ma][Nb] (= or +=) a[K][Ma]^T . b[K][Nb] by wgrad_tt (256 x 256 / 128 tiles, split-K into the
+// fp32 workspace ws, summed in split order: deterministic).  The operand roles are swapped when
+// only Nb is a multiple of 256 (the slab is then summed transposed).  Returns false (nothing
+// launched) for shapes it does not take.
+int64_t wgrad_tt_ws(int64_t M, int64_t N, int64_t K) {  // workspace floats for out [M][N]
+  if (wgrad_tt_ok((int)M, (int)N, (int)K)) return (int64_t)wgrad_tt_splits((int)M, (int)N, (int)K) * M * N;
+  if (wgrad_tt_ok((int)N, (int)M, (int)K)) return (int64_t)wgrad_tt_splits((int)N, (int)M, (int)K) * M * N;
+  return 0;
+}
+bool wgrad_tt(const Tensor& a, const Tensor& b, const Tensor& out, const Tensor& ws, bool acc) {
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "wgrad_tt: 2-D views");
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda() && ws.is_cuda(), "wgrad_tt: GPU tensors");
+  TORCH_CHECK(a.scalar_type() == BF && b.scalar_type() == BF && out.scalar_type() == F32 && ws.scalar_type() == F32,
+              "wgrad_tt: bf16, bf16 -> fp32");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.stride(1) == 1 && ws.is_contiguous(), "wgrad_tt: unit column stride");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "wgrad_tt: shapes");
+  if (!(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 4 == 0 && (uintptr_t)a.data_ptr() % 16 == 0 &&
+        (uintptr_t)b.data_ptr() % 16 == 0 && (uintptr_t)out.data_ptr() % 16 == 0))
+    return false;  // 16-byte aligned rows only (the caller takes its other path)
+  const bool direct = wgrad_tt_ok((int)M, (int)N, (int)K), swapped = !direct && wgrad_tt_ok((int)N, (int)M, (int)K);
+  if (!direct && !swapped) return false;
+  TORCH_CHECK(ws.numel() >= wgrad_tt_ws(M, N, K), "wgrad_tt: workspace too small");
+  if (direct)
+    launch_wgrad_tt(P<bf16>(a), (int)a.stride(0), P<bf16>(b), (int)b.stride(0), P<float>(ws), P<float>(out),
+                    (int)out.stride(0), (int)M, (int)N, (int)K, false, acc, stream());
+  else  // GEMM over (b, a): slab [S][N][M], summed into out [M][N] transposed
+    launch_wgrad_tt(P<bf16>(b), (int)b.stride(0), P<bf16>(a), (int)a.stride(0), P<float>(ws), P<float>(out),
+                    (int)out.stride(0), (int)N, (int)M, (int)K, true, acc, stream());
+  return true;
+}
 void wgrad_tn(const Tensor& a, const Tensor& b, const Tensor& out) {
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "wgrad_tn: 2-D views");
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "wgrad_tn: GPU tensors");
@@ -1056,6 +1087,8 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("dec_bwd_dz", &dec_bwd_dz);
   m.def("ptr_loss", &ptr_loss);
   m.def("wgrad_tn", &wgrad_tn);
+  m.def("wgrad_tt", &wgrad_tt);
+  m.def("wgrad_tt_ws", &wgrad_tt_ws);
   m.def("pgen_dirs", &pgen_dirs);
   m.def("pack_cast", &pack_cast);
   m.def("pack_max_jobs", &pack_max_jobs_op);

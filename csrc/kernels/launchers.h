@@ -184,6 +184,10 @@ void tsamd_debug_clear();
 
 // weight-gradient GEMM out[M][N] += a[K][M]^T b[K][N] (wgrad.hip; out pre-zeroed, M, N % 128 == 0)
 int wgrad_tn_splits(int M, int N, int K);
+int wgrad_tt_splits(int M, int N, int K);
+bool wgrad_tt_ok(int M, int N, int K);
+void launch_wgrad_tt(const bf16* a, int lda, const bf16* b, int ldb, float* slab, float* out, int ldo, int M, int N,
+                     int K, bool trans, bool acc, hipStream_t st);
 void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out, int ldo, int M, int N, int K,
                      hipStream_t st);
 

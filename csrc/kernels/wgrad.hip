@@ -150,3 +150,226 @@ void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out,
   const dim3 grid(gm * ((ny + 7) / 8 * 8));
   hipLaunchKernelGGL(wgrad_tn_kernel<WBK>, grid, dim3(256), 0, st, a, lda, b, ldb, out, ldo, N, K, kchunk, gm, gn, ny);
 }
+
+// ---------------------------------------------------------------------------------------------
+// wgrad_tt: the long-K weight-gradient GEMM as 256 x BN tiles with a deterministic split-K
+// (round-6 review item 2; reference model.py:290-297 -- tf.gradients over the encoder LSTM input
+// / recurrent kernels, model.py:89-93):
+//
+//   slab[s][m][n] = sum_{k in chunk s} a[k][m] b[k][n]      (this kernel, fp32, no atomics)
+//   out[m][n]     = sum_s slab[s][m][n]  in s order         (wgrad_sum_kernel)
+//
+// so the result does not depend on scheduling (the torch split-K path's bmm + torch.sum and the
+// fp32-atomic wgrad_tn above are replaced for the encoder weight gradients).
+//
+// Geometry: 512 threads = 8 waves as 2 (m) x 4 (n), a wave 128 (m) x BN/4 (n) of
+// v_mfma_f32_16x16x32_bf16 accumulators; K steps of 64.  Both operands are K-major ([k][m] /
+// [k][n] rows of 512 bytes); each K tile is staged by global_load_lds_dwordx4 (1 KB per wave
+// instruction: 4 rows of a 128-column half image) into two LDS stages; the MFMA operands are read
+// transposed by ds_read_b64_tr_b16 (two per fragment).  Half images of 128 columns use
+// 256-byte rows with the 16-byte chunk ch of row r at ch ^ (((r & 3) << 2) | ((r >> 2) & 3))
+// (cdna_hip_programming.md T10 (b)): the two 4-row blocks a 32-lane half reads, 8 rows apart in
+// the same columns, hit distinct banks.  The XOR is applied to the per-lane GLOBAL source
+// address, so the LDS-DMA image stays lane-linear.
+//
+// Workgroup order: lin (the bijective XCD remap) -> split s = lin / tiles, tile = lin % tiles, so
+// the tiles of one K chunk are consecutive in lin, i.e. on one XCD: that XCD's L2 serves the
+// chunk's a / b panels to all of its tiles (HBM reads each operand once).
+namespace {
+typedef __attribute__((address_space(3))) void* tt_lds_t;
+typedef const __attribute__((address_space(1))) void* tt_gbl_t;
+
+__device__ __forceinline__ int tt_sw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+// global_load_lds_dwordx4 hidden from hipcc's wait bookkeeping (cdna_hip_programming.md s5.7):
+// with the builtin, hipcc cannot tell the in-flight DMA of the NEXT stage from the one being read
+// and waits vmcnt(0) before the first ds_read of every K step -- the staging then never overlaps
+// the MFMAs.  The kernel counts these loads itself (vmcnt(0) + barrier at the end of the step).
+__device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+// one operand fragment (16 columns c0.. of a half image, k rows kb + 8 (l >> 4) .. + 7) by two
+// transposed reads: lane 4q + p of each 16-lane group addresses row (.. + 4 half + q), columns
+// c0 + 4 p .. + 3
+__device__ __forceinline__ bf16x8 tt_frag(const char* img, int kb, int c0, int lane) {
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const int q = (lane >> 2) & 3, p = lane & 3, g = lane >> 4;
+  v4i16 h[2];
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const int r = kb + 8 * g + 4 * hf + q, ch = (c0 >> 3) + (p >> 1);
+    const char* a = img + r * 256 + 16 * (ch ^ tt_sw(r)) + 8 * (p & 1);
+    h[hf] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(const_cast<char*>(a)));
+  }
+  return __builtin_bit_cast(bf16x8, v8i16{h[0][0], h[0][1], h[0][2], h[0][3], h[1][0], h[1][1], h[1][2], h[1][3]});
+}
+}  // namespace
+
+template <int BN>
+__global__ __launch_bounds__(512, 1) void wgrad_tt_kernel(const bf16* __restrict__ a, int lda, const bf16* __restrict__ b,
+                                                          int ldb, float* __restrict__ slab, int M, int N, int kchunk,
+                                                          int K) {
+  constexpr int BM = 256, BK = 64, HI = 64 * 256;           // half-image bytes (64 rows x 256 B)
+  constexpr int NHA = BM / 128, NHB = BN / 128;             // half images per operand
+  constexpr int STAGE = (NHA + NHB) * HI;
+  constexpr int WN = BN / 4, NJ = WN / 16;                  // wave columns, 16-col subtiles
+  constexpr int PPW = (NHA + NHB) * 16 / 8;                 // glds pieces per wave per stage
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int tm = M / BM, tn = N / BN, tiles = tm * tn;
+  const int nwg = gridDim.x, id = blockIdx.x, xcd = id & 7, qq = nwg >> 3, r8 = nwg & 7;
+  const int lin = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + (id >> 3);
+  const int s = lin / tiles, tile = lin - s * tiles;
+  const int m0 = (tile / tn) * BM, n0 = (tile % tn) * BN;
+  const int k0 = s * kchunk, nk = (min(K, k0 + kchunk) - k0) / BK;
+  // glds piece pc (0 .. 16 (NHA + NHB) - 1) of a stage: half image h = pc / 16, rows 4 (pc % 16) ..
+  // + 3; lane l: row 4 (pc % 16) + (l >> 4), physical chunk l & 15 <- logical chunk (l & 15) ^ sw(row)
+  const bf16* src[PPW];
+  size_t kstep[PPW];  // elements per K step of the piece's operand
+  int ldst[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int pc = wid * PPW + j, h = pc >> 4, row = 4 * (pc & 15) + (lane >> 4);
+    const int ch = (lane & 15) ^ tt_sw(row);
+    src[j] = h < NHA ? a + (size_t)(k0 + row) * lda + m0 + 128 * h + 8 * ch
+                     : b + (size_t)(k0 + row) * ldb + n0 + 128 * (h - NHA) + 8 * ch;
+    kstep[j] = (size_t)BK * (h < NHA ? lda : ldb);
+    ldst[j] = h * HI + (pc & 15) * 1024;
+  }
+  const unsigned sbase = (unsigned)(uintptr_t)(tt_lds_t)smem;
+  auto stage = [&](int buf, int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j)
+      glds16_asm(src[j] + kt * kstep[j], __builtin_amdgcn_readfirstlane(sbase + buf * STAGE + ldst[j]));
+  };
+  const int wr = wid >> 2, wc = wid & 3;
+  // the wave's images: a half image wr (its 128 m), b half image (wc * WN) / 128 at column offset
+  const int bimg = NHA + (wc * WN) / 128, bcol = (wc * WN) % 128;
+  f32x4 acc[8][NJ];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+  // (A ping-pong schedule -- the two wave groups one barrier apart, reads of one beside the
+  // MFMAs of the other -- needed 256 VGPRs + 36 bytes of scratch here and ran 1.6x slower.)
+  if (nk > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) stage(buf ^ 1, kt + 1);
+    const char* Ai = smem + buf * STAGE + wr * HI;
+    const char* Bi = smem + buf * STAGE + bimg * HI;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 fb[NJ], fa[8];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = tt_frag(Bi, 32 * kk, bcol + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = tt_frag(Ai, 32 * kk, 16 * i, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // accumulator (i, j, r): m = m0 + 128 wr + 16 i + 4 (l >> 4) + r, n = n0 + wc WN + 16 j + (l & 15)
+  float* sl = slab + (size_t)s * M * N;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float* row = sl + (size_t)(m0 + 128 * wr + 16 * i + 4 * (lane >> 4) + r) * N + n0 + wc * WN + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) row[16 * j] = acc[i][j][r];
+    }
+}
+
+// out[m][n] (= or +=) sum_{s < S} slab[s][m][n], s ascending; trans: slab is [S][N][M] (the roles
+// of the operands were swapped) and out[m][n] = sum_s slab[s][n][m] through a 64 x 64 LDS tile
+template <bool TRANS>
+__global__ __launch_bounds__(256) void wgrad_sum_kernel(const float* __restrict__ slab, float* __restrict__ out, int ldo,
+                                                        int M, int N, int S, bool acc) {
+  if constexpr (!TRANS) {
+    const size_t i4 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4, MN = (size_t)M * N;
+    if (i4 >= MN) return;
+    float4 t = *reinterpret_cast<const float4*>(slab + i4);
+    for (int s = 1; s < S; ++s) {
+      const float4 u = *reinterpret_cast<const float4*>(slab + (size_t)s * MN + i4);
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    const int m = (int)(i4 / N), n = (int)(i4 % N);
+    float4* o = reinterpret_cast<float4*>(out + (size_t)m * ldo + n);
+    if (acc) {
+      const float4 u = *o;
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    *o = t;
+  } else {
+    // slab [S][N][M] -> out [M][N]; block = 64 (n) x 64 (m) of the slab
+    __shared__ float tile[64][65];
+    const int nb = blockIdx.x % (N / 64), mb = blockIdx.x / (N / 64);
+    const size_t MN = (size_t)M * N;
+    const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+    float t[16];  // slab rows n = nb 64 + r0 + 4 e, column m = mb 64 + c: 16 independent loads per split
+    const float* base = slab + (size_t)(nb * 64 + r0) * M + mb * 64 + c;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) t[e] = base[(size_t)4 * e * M];
+    for (int s = 1; s < S; ++s) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) t[e] += base[s * MN + (size_t)4 * e * M];
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) tile[r0 + 4 * e][c] = t[e];
+    __syncthreads();
+    for (int rr = r0; rr < 64; rr += 4) {  // out row m = mb 64 + rr, column n = nb 64 + c
+      float* o = out + (size_t)(mb * 64 + rr) * ldo + nb * 64 + c;
+      *o = acc ? *o + tile[c][rr] : tile[c][rr];
+    }
+  }
+}
+
+// the split of K: ~1 workgroup per CU (tiles x S >= 256), chunks of whole 64-row steps
+int wgrad_tt_splits(int M, int N, int K) {
+  const int BN = N % 256 == 0 ? 256 : 128;
+  const int tiles = (M / 256) * (N / BN), steps = K / 64;
+  int s = (256 + tiles - 1) / tiles;
+  s = s < 1 ? 1 : (s > steps ? steps : s);
+  const int kc = (steps + s - 1) / s;
+  return (steps + kc - 1) / kc;
+}
+bool wgrad_tt_ok(int M, int N, int K) { return M % 256 == 0 && N % 128 == 0 && K % 64 == 0 && K >= 64; }
+
+void launch_wgrad_tt(const bf16* a, int lda, const bf16* b, int ldb, float* slab, float* out, int ldo, int M, int N,
+                     int K, bool trans, bool acc, hipStream_t st) {
+  const int BN = N % 256 == 0 ? 256 : 128;
+  const int S = wgrad_tt_splits(M, N, K), steps = K / 64, kc = (steps + S - 1) / S;
+  const int grid = (M / 256) * (N / BN) * S;
+  const size_t lds = (size_t)(2 + BN / 128) * 64 * 256 * 2;
+  if (BN == 256) {
+    (void)hipFuncSetAttribute((const void*)wgrad_tt_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(wgrad_tt_kernel<256>, dim3(grid), dim3(512), lds, st, a, lda, b, ldb, slab, M, N, kc * 64, K);
+  } else {
+    (void)hipFuncSetAttribute((const void*)wgrad_tt_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(wgrad_tt_kernel<128>, dim3(grid), dim3(512), lds, st, a, lda, b, ldb, slab, M, N, kc * 64, K);
+  }
+  if (!trans) {
+    const size_t n4 = (size_t)M * N / 4;
+    hipLaunchKernelGGL(wgrad_sum_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, slab, out, ldo, M, N,
+                       S, acc);
+  } else {  // out is [N][M] (ldo), the slab [S][M][N]: out[n][m] = sum slab[s][m][n]
+    hipLaunchKernelGGL(wgrad_sum_kernel<true>, dim3((M / 64) * (N / 64)), dim3(256), 0, st, slab, out, ldo, N, M, S, acc);
+  }
+}

@@ -104,3 +104,38 @@ def test_gemm_bt_merge_matches_two_direction_sum(mode):
         ref = ref.transpose(0, 1)  # step frame: m = t * B + b
     _close(out.view(ref.shape), ref)
     assert bool((full[T * B:] == 12345.0).all())
+
+
+@pytest.mark.parametrize("K,M,N,acc", [(4096, 256, 256, False), (6400, 512, 384, False), (8192, 128, 512, False),
+                                       (3200, 256, 1024, True), (64, 256, 128, False)])
+def test_wgrad_tt_matches_fp32_and_is_deterministic(K, M, N, acc):
+    """wgrad_tt (wgrad.hip): out (+)= a[K][M]^T . b[K][N] by 256 x BN MFMA tiles with the K range
+    split over workgroups into fp32 slabs summed in split order -- against an fp32 matmul of the
+    same bf16 operands; bit-identical on a repeat (no atomics); M = 128 runs with the operand
+    roles swapped (transposed slab sum); the rows after the output keep their sentinel."""
+    k = _k()
+    g = torch.Generator(device="cuda").manual_seed(K + M + N)
+    a = (torch.randn(K, M, device="cuda", generator=g) * 0.1).bfloat16()
+    b = (torch.randn(K, N, device="cuda", generator=g) * 0.1).bfloat16()
+    c0 = torch.randn(M, N, device="cuda", generator=g)
+    full = torch.full((M + 64, N), 12345.0, device="cuda")
+    out = full[:M]
+    out.copy_(c0) if acc else out.fill_(float("nan"))
+    ws = torch.empty(int(k.wgrad_tt_ws(M, N, K)), device="cuda")
+    assert k.wgrad_tt(a, b, out, ws, acc)
+    torch.cuda.synchronize()
+    ref = a.float().t() @ b.float() + (c0 if acc else 0)
+    _close(out, ref, 1e-4)
+    assert bool((full[M:] == 12345.0).all())
+    if not acc:
+        again = torch.empty_like(out)
+        k.wgrad_tt(a, b, again, ws, False)
+        assert torch.equal(again, out)
+
+
+def test_wgrad_tt_declines_unsupported_shapes():
+    k = _k()
+    a = torch.zeros(100, 96, device="cuda", dtype=torch.bfloat16)
+    b = torch.zeros(100, 64, device="cuda", dtype=torch.bfloat16)
+    assert int(k.wgrad_tt_ws(96, 64, 100)) == 0
+    assert not k.wgrad_tt(a, b, torch.empty(96, 64, device="cuda"), torch.empty(1, device="cuda"), False)

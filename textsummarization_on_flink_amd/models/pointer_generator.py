@@ -68,11 +68,12 @@ BLT_VDW = BLT and os.environ.get("TSAMD_BLT_VOCAB_DW", "0") == "1"
 
 
 # TSAMD_GEMM_BT: the hand-written MFMA GEMM (csrc/kernels/gemm_mfma.hip) for the activation GEMMs
-# whose weight operand has a [N][K] twin: "auto" (default) times it against blt_mm once per shape
-# on the first eager call (a row subset, scratch output) and keeps the faster -- hipBLASLt stays only
-# where the hand-written kernel measures slower; "1" always where eligible (deterministic mode
-# too: no timing-dependent choice); "0" never
-GEMM_BT = os.environ.get("TSAMD_GEMM_BT", "auto")
+# whose weight operand has a [N][K] twin.  "table" (default): a fixed per-shape rule from the
+# recorded head-to-head timings (``_bt_rule``; profiles/r5/gemm_micro_v3.jsonl,
+# profiles/r6/gemm_dispatch.md) -- the same pick on every run, box and rank; "auto" times it
+# against blt_mm once per shape on the first eager call and keeps the faster (the round-5 default:
+# picks could differ between runs); "1" always where eligible (deterministic mode too); "0" never
+GEMM_BT = os.environ.get("TSAMD_GEMM_BT", "table")
 _BT_PICK: Dict[tuple, bool] = {}
 _BT_TIMES: Dict[tuple, tuple] = {}
 # TSAMD_DX_MERGE=0: the input gradients of an upper encoder layer as two per-direction GEMMs +
@@ -135,6 +136,17 @@ def _bt_timed(out, sa, Bt, beta, bias, sb, tb):
     return _BT_TIMES[key]
 
 
+def _bt_rule(K: int, out_bf16: bool, slack: float) -> bool:
+    """The fixed dispatch (TSAMD_GEMM_BT=table), from the head-to-head records
+    (profiles/r5/gemm_micro_v3.jsonl and the round-6 timed picks, profiles/r6/gemm_dispatch.md):
+    the hand-written GEMM wins every K <= 256 shape (b256_gx 104 vs 112 us, c5_gx_l0 1340 vs 1443,
+    25600 x 128 x 128 8.1 vs 16.2), the bf16-out shapes up to K = 1024 (25600 x 512 x 512 22.2 vs
+    29.1, c5_F 1694 vs 1707; b256_F measured both ways across runs) and loses the fp32-out
+    K >= 512 shapes (25600 x 256 x 512 28.1 vs 20.4, 102400 x 512 x 512 154 vs 117, c5_dx_l1 3380
+    vs 3010) -- within FRAME_SLACK where it also saves the step-frame layout pass."""
+    return slack > 1.0 or K <= 256 or (out_bf16 and K <= 1024)
+
+
 def _use_bt(out, sa, ta, Bt, beta, bias, sb, tb, slack: float = 1.0) -> bool:
     if not _bt_ok(out, sa, ta, Bt, beta, bias):
         return False
@@ -142,16 +154,23 @@ def _use_bt(out, sa, ta, Bt, beta, bias, sb, tb, slack: float = 1.0) -> bool:
         return True
     key = (tuple(out.shape), out.dtype, sa.shape[1], beta != 0.0, bias is not None, sa.stride(0), Bt.stride(0), slack)
     if key not in _BT_PICK:
-        if torch.cuda.is_current_stream_capturing():
+        if GEMM_BT != "auto":
+            _BT_PICK[key] = _bt_rule(sa.shape[1], out.dtype == BF, slack)
+        elif torch.cuda.is_current_stream_capturing():
             return False  # first seen inside a capture: no timing possible, keep the library GEMM
-        t_bt, t_blt = _bt_timed(out, sa, Bt, beta, bias, sb, tb)
-        _BT_PICK[key] = t_bt <= slack * t_blt
+        else:
+            t_bt, t_blt = _bt_timed(out, sa, Bt, beta, bias, sb, tb)
+            _BT_PICK[key] = t_bt <= slack * t_blt
     return _BT_PICK[key]
 
 
 def gemm_bt_stats() -> Dict[str, object]:
-    """Shapes seen by the hand-written-GEMM dispatch and the ones it took, with their timings."""
-    return {"shapes": len(_BT_PICK), "gemm_bt": int(sum(_BT_PICK.values())),
+    """The hand-written-GEMM dispatch: mode, every shape seen (M x N x K, out dtype, frame
+    gather) with the kernel it got, and (mode "auto") the timings behind the picks."""
+    picks = {f"{k[0][0]}x{k[0][1]}x{k[2]}{'_bf16' if k[1] == BF else ''}{'_frame' if k[7] > 1.0 else ''}":
+             ("gemm_bt" if v else "hipblaslt") for k, v in _BT_PICK.items()}
+    return {"mode": "deterministic" if _deterministic() else GEMM_BT, "shapes": len(_BT_PICK),
+            "gemm_bt": int(sum(_BT_PICK.values())), "picks": picks,
             "timed_us": {f"{k[0][0]}x{k[0][1]}x{k[2]}": [round(v[0], 1), round(v[1], 1)] for k, v in _BT_TIMES.items()}}
 
 
@@ -217,6 +236,39 @@ def wgrad_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
                                   out_dtype=F32)
                 return torch.sum(parts, 0, out=out)
     return out.copy_(mmf(a.t(), b))
+
+
+WGRAD_TT = os.environ.get("TSAMD_WGRAD_TT", "1") != "0"
+WGRAD_TT_MIN = float(os.environ.get("TSAMD_WGRAD_TT_MIN", 1e11))
+_WG_WS: Dict[object, torch.Tensor] = {}
+_WG_WS_OLD: List[torch.Tensor] = []
+
+
+def wgrad_enc_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
+    """The encoder weight gradients x^T.dz / h^T.dz (K = T.B tokens: 102k at the headline, 1.6M at
+    config #5): the hand-written deterministic split-K GEMM (wgrad.hip ``wgrad_tt``: fp32 slabs
+    summed in split order, no atomics, no torch.sum pass) where the shape fits it, else
+    ``wgrad_into``.  Its slab workspace is one buffer per device, grown outside graph capture
+    (the trainer's eager warm-up) and reused by the captured graphs: these calls run one after
+    another on the encoder-backward stream (model.py:290-297 / 89-93 gradients)."""
+    # large shapes only (config #5: K.M.N >= 3e11); at the headline's K = 102k the split-K bmm is
+    # as fast or faster (profiles/r6/wgrad_tt.md)
+    if (WGRAD_TT and a.is_cuda and a.dtype == BF and b.dtype == BF and out.dtype == F32
+            and a.shape[0] * a.shape[1] * b.shape[1] >= WGRAD_TT_MIN):
+        k = _ops()
+        n = int(k.wgrad_tt_ws(a.shape[1], b.shape[1], a.shape[0]))
+        if n > 0:
+            key = out.device
+            ws = _WG_WS.get(key)
+            if ws is None or ws.numel() < n:
+                if torch.cuda.is_current_stream_capturing():
+                    return wgrad_into(out, a, b)  # first seen inside a capture: no allocation there
+                if ws is not None:  # graphs captured earlier may hold the old buffer: never freed
+                    _WG_WS_OLD.append(ws)
+                ws = _WG_WS[key] = torch.empty(n, device=out.device, dtype=F32)
+            if k.wgrad_tt(a, b, out, ws, False):
+                return out
+    return wgrad_into(out, a, b)
 
 
 def mmf(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -1383,8 +1435,8 @@ class HipPointerGenerator:
             for di, d in enumerate(("fw", "bw")):
                 dzd = st["dz"][di].view(T * B, 4 * H)
                 gkd = g(enc_k(layer, d))
-                wgrad_into(gkd[:din], st["x_sf"][di].view(T * B, din), dzd)
-                wgrad_into(gkd[din:], st["hs"][di, :T].reshape(T * B, H), dzd)
+                wgrad_enc_into(gkd[:din], st["x_sf"][di].view(T * B, din), dzd)
+                wgrad_enc_into(gkd[din:], st["hs"][di, :T].reshape(T * B, H), dzd)
                 if self.persistent_lstm and not self.det:
                     g(enc_b(layer, d)).copy_(w["lstm_db"][di])
                 else:
