@@ -256,8 +256,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_tt_kernel(const bf16* __restrict
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-  // (A ping-pong schedule -- the two wave groups one barrier apart, reads of one beside the
-  // MFMAs of the other -- needed 256 VGPRs + 36 bytes of scratch here and ran 1.6x slower.)
+  // Measured and not kept (profiles/r6/wgrad_tt.md): a ping-pong schedule (the two wave groups
+  // one barrier apart, reads of one beside the MFMAs of the other: 256 VGPRs + 36 bytes of
+  // scratch, 1.6x slower) and a 4-wave 128 x 128-per-wave kernel with register-double-buffered
+  // fragments (452 registers, 7-13 % slower at the config #5 shapes).
   if (nk > 0) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
