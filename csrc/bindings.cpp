@@ -178,6 +178,19 @@ void attn_fwd_row(const Tensor& F, const Tensor& E, const Tensor& s, const Tenso
                       PO<float>(cov), P<int>(lens), P<float>(a_out), PO<float>(cov_out), PO<float>(covloss), P<float>(ctx),
                       PO<bf16>(ctx_bf), B, T, A, (int)rep, stream());
 }
+// attribution probe of the beam-decode attention forward (A = 512; tools/attn_decode_probe.py)
+void attn_fwd_row_probe(const Tensor& F, const Tensor& E, const Tensor& s, const Tensor& v, const Tensor& wc,
+                        const Tensor& cov, const Tensor& lens, const Tensor& a_out, const Tensor& ctx, int64_t B, int64_t T,
+                        int64_t rep, int64_t probe) {
+  chk(F, BF, "F"); chk(E, BF, "E"); chk(s, F32, "s"); chk(v, F32, "v"); chk(wc, F32, "wc"); chk(cov, F32, "cov");
+  chk(lens, I32, "lens"); chk(a_out, F32, "a_out"); chk(ctx, F32, "ctx");
+  TORCH_CHECK(rep >= 1 && B % rep == 0 && T <= 2048, "attn_fwd_row_probe: rep | B, T <= 2048");
+  numel_eq(F, B / rep * T * 512, "F"); numel_eq(E, B / rep * T * 512, "E"); numel_eq(s, B * 512, "s");
+  numel_eq(v, 512, "v"); numel_eq(wc, 512, "wc"); numel_eq(cov, B * T, "cov"); numel_eq(lens, B / rep, "lens");
+  numel_eq(a_out, B * T, "a_out"); numel_eq(ctx, B * 512, "ctx");
+  launch_attn_fwd_row_probe(P<bf16>(F), P<bf16>(E), P<float>(s), P<float>(v), P<float>(wc), P<float>(cov), P<int>(lens),
+                            P<float>(a_out), P<float>(ctx), (int)B, (int)T, (int)rep, (int)probe, stream());
+}
 void attn_bwd_row(const Tensor& E, const Tensor& F, const Tensor& s, const Tensor& v, const OT& wc, const OT& cov,
                   const Tensor& a, const Tensor& dctx, const Tensor& ctx, const OT& Ga, const OT& dcov_next,
                   const OT& gcl, const Tensor& lens, const Tensor& de_out, const Tensor& ds, const OT& dcov_out,
@@ -1130,6 +1143,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("vocab_topk", &vocab_topk);
   m.def("vocab_topk_parts", &vocab_topk_parts);
   m.def("vocab_span_probe", &vocab_span_probe);
+  m.def("attn_fwd_row_probe", &attn_fwd_row_probe);
   m.def("vocab_select_stamps", &vocab_select_stamps);
   m.def("vocab_topk_beam", &vocab_topk_beam);
   m.def("dec_cell_fwd_beam", &dec_cell_fwd_beam);

@@ -58,7 +58,9 @@ __device__ __forceinline__ void load_rows(Rows<NK>& r, const bf16* base, int p0,
 }  // namespace
 
 // ------------------------------------------------------------------------------ forward
-template <int NK, int NW>
+// PROBE (attribution builds only, attn_fwd_row_probe): bit 0 no score arithmetic, bit 1 no context
+// accumulation, bit 2 no E loads, bit 3 no F / E loads at all (results wrong by design)
+template <int NK, int NW, int PROBE = 0>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     const bf16* __restrict__ F, const bf16* __restrict__ E, const float* __restrict__ s,
     const float* __restrict__ v, const float* __restrict__ wc, const float* __restrict__ cov,
@@ -88,10 +90,19 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
   const int qm = lane >> 4;  // the position (within a group) whose total this lane's 16-lane group holds
   const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1;
   Rows<NK> fA, eA, fB, eB;
+  if constexpr (PROBE & 12) {
+#pragma unroll
+    for (int kb = 0; kb < NK; ++kb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        fA.x[kb][q] = fB.x[kb][q] = u32x4{(unsigned)lane, 1u, 2u, 3u};
+        eA.x[kb][q] = eB.x[kb][q] = u32x4{(unsigned)lane, 3u, 2u, 1u};
+      }
+  }
   float cA = 0.f, cB = 0.f;
   auto load = [&](int grp, Rows<NK>& f, Rows<NK>& e, float& c) {
-    load_rows<NK>(f, Fb, 4 * grp, len, lane);
-    load_rows<NK>(e, Eb, 4 * grp, len, lane);
+    if constexpr (!(PROBE & 8)) load_rows<NK>(f, Fb, 4 * grp, len, lane);
+    if constexpr (!(PROBE & 12)) load_rows<NK>(e, Eb, 4 * grp, len, lane);
     const int p = min(4 * grp + qm, len - 1);
     c = cov ? cov[cb + p] + (cg ? asrc[cb + p] : 0.f) : 0.f;
   };
@@ -123,13 +134,17 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     for (int q = 0; q < 4; ++q) {
       const float c = rdlane(c_l, 16 * q);
       f32x2 d2 = f32x2{0.f, 0.f};
+      if constexpr (PROBE & 1) {
+        d2.x = __uint_as_float(f.x[0][q][0] & 0x3fffffffu) + c;
+      } else {
 #pragma unroll
-      for (int kb = 0; kb < NK; ++kb)
+        for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
-        for (int jp = 0; jp < 4; ++jp) {
-          const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]), dsel);
-          d2 = fma2(v2[kb][jp], rsig2(y), d2);
-        }
+          for (int jp = 0; jp < 4; ++jp) {
+            const f32x2 y = fadd_bf2(f.x[kb][q][jp], fma2(w2[kb][jp], splat2(c), s2[kb][jp]), dsel);
+            d2 = fma2(v2[kb][jp], rsig2(y), d2);
+          }
+      }
       pd[q] = vsum - 2.0f * (d2.x + d2.y);
     }
     float eq = bfly4(pd, b5, b4);
@@ -141,6 +156,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_row_kernel(
     const float sc = m_w == -INFINITY ? 0.f : fexp(m_w - mn);
     const float p0 = fexp(e0 - mn), p1 = fexp(e1 - mn), p2 = fexp(e2 - mn), p3 = fexp(e3 - mn);
     l_w = l_w * sc + ((p0 + p1) + (p2 + p3));
+    if constexpr (PROBE & 2) {
+      acc[0][0].x += __uint_as_float(e.x[0][0][0] & 0x3fffffffu) * p0;
+    } else
 #pragma unroll
     for (int kb = 0; kb < NK; ++kb)
 #pragma unroll
@@ -766,6 +784,26 @@ void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const flo
   else if (A == 512) LF(1);
   else LF(2);
 #undef LF
+}
+
+// attribution probe: the beam-decode forward (A = 512, 12 waves) with PROBE bits
+void launch_attn_fwd_row_probe(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
+                               const float* cov, const int* lens, float* a_out, float* ctx, int B, int T, int rep,
+                               int probe, hipStream_t st) {
+  const int xper = (rep > 1 && B % 8 == 0 && (B / 8) % rep == 0) ? B / 8 : 0;
+#define LP(PB)                                                                                                  \
+  hipLaunchKernelGGL((attn_fwd_row_kernel<1, 12, PB>), dim3(B), dim3(12 * 64), 0, st, F, E, s, v, wc, cov, lens, a_out, \
+                     nullptr, nullptr, ctx, nullptr, T, rep, xper, nullptr, nullptr, nullptr)
+  switch (probe) {
+    case 0: LP(0); break;
+    case 1: LP(1); break;
+    case 2: LP(2); break;
+    case 3: LP(3); break;
+    case 4: LP(4); break;
+    case 8: LP(8); break;
+    default: LP(11); break;
+  }
+#undef LP
 }
 
 void launch_attn_bwd_row(const bf16* E, const bf16* F, const float* s, const float* v, const float* wc,

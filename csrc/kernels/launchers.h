@@ -24,6 +24,9 @@ void launch_attn_bwd_feat(const bf16* F, const float* S_all, const float* v, con
                           int A, int nslot, hipStream_t st, const int* dlen = nullptr);
 
 bool attn_row_supported(int A, int T);
+void launch_attn_fwd_row_probe(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
+                               const float* cov, const int* lens, float* a_out, float* ctx, int B, int T, int rep,
+                               int probe, hipStream_t st);
 void launch_attn_fwd_row(const bf16* F, const bf16* E, const float* s, const float* v, const float* wc,
                          const float* cov, const int* lens, float* a_out, float* cov_out, float* covloss, float* ctx,
                          bf16* ctx_bf, int B, int T, int A, int rep, hipStream_t st, const int* cg = nullptr,
