@@ -66,3 +66,28 @@ def test_vocab_live_blocks():
     assert h["vlive"][np.nonzero(w.reshape(-1))[0] // 32].all()
     layout, total = input_layout(B, hps.max_enc_steps, D)
     assert pack_host_inputs(h, layout).nbytes == total
+
+
+def test_gemm_dispatch_table_is_fixed_by_shape():
+    """The activation-GEMM dispatch (TSAMD_GEMM_BT=table, the default) depends only on the shape:
+    the hand-written GEMM for step-frame gathers, K <= 256 and bf16-out K <= 1024; hipBLASLt for
+    the fp32-out K >= 512 shapes -- the same pick on every run and rank (profiles/r6/gemm_dispatch.md)."""
+    from textsummarization_on_flink_amd.models import pointer_generator as pg
+    assert pg.GEMM_BT in ("table", "auto", "0", "1")
+    rule = pg._bt_rule
+    assert rule(128, False, 1.0) and rule(256, False, 1.0)
+    assert not rule(512, False, 1.0) and not rule(1024, False, 1.0)
+    assert rule(512, True, 1.0) and rule(1024, True, 1.0) and not rule(2048, True, 1.0)
+    assert rule(2048, False, pg.FRAME_SLACK)  # the gather GEMMs save the layout pass
+    assert all(rule(k, b, 1.0) == rule(k, b, 1.0) for k in (128, 512, 4096) for b in (False, True))
+
+
+def test_encoder_wgrad_cpu_path_matches_matmul():
+    """wgrad_enc_into on CPU tensors (the oracle backend) falls back to the plain matmul path."""
+    import torch
+    from textsummarization_on_flink_amd.models.pointer_generator import wgrad_enc_into
+    g = torch.Generator().manual_seed(0)
+    a, b = torch.randn(64, 16, generator=g), torch.randn(64, 24, generator=g)
+    out = torch.empty(16, 24)
+    wgrad_enc_into(out, a, b)
+    assert torch.allclose(out, a.t() @ b, atol=1e-5)

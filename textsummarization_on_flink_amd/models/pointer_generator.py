@@ -275,6 +275,8 @@ def mmf(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """bf16 x bf16 -> fp32 GEMM (fp32 accumulate), hipBLASLt."""
     if BLT and a.is_cuda:
         return gemm(torch.empty(a.shape[0], b.shape[1], device=a.device, dtype=F32), a, b)
+    if not a.is_cuda:  # (the out_dtype matmul is GPU-only)
+        return a.float() @ b.float()
     return torch.mm(a, b, out_dtype=F32)
 
 
