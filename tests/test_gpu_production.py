@@ -85,6 +85,17 @@ def _oracle_check(hps, B, T_, D_, seed, cov_tol=2e-2):
     return kinds
 
 
+def test_bench_shape_with_every_weight_gradient_on_wgrad_tt(monkeypatch):
+    """The bench shape against the fp32 oracle with every eligible long-K weight gradient on the
+    deterministic split-K wgrad_tt (threshold 0; deterministic mode runs the decoder-side ones
+    inline, where they take it too): encoder x^T.dz / h^T.dz (K = T.B = 102400, layer 0's M = 128
+    with the operand roles swapped), decoder cell / output-projection / attention / W_h (K = D.B)."""
+    from textsummarization_on_flink_amd.models import pointer_generator as pgm
+    monkeypatch.setattr(pgm, "WGRAD_TT_MIN", 0)
+    monkeypatch.setenv("TSAMD_DETERMINISTIC", "1")
+    _oracle_check(_hps(256, trunc_norm_init_std=0.05), 256, T, D, seed=13)
+
+
 def test_bench_shape_matches_fp32_oracle():
     kinds = _oracle_check(_hps(256, trunc_norm_init_std=0.05), 256, T, D, seed=11)
     assert kinds["persistent_lstm"] and kinds["fused_vocab"] and kinds["row_attn_bwd"] and kinds["proj_attn"]

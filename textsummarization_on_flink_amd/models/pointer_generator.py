@@ -245,12 +245,13 @@ _WG_WS_OLD: List[torch.Tensor] = []
 
 
 def wgrad_enc_into(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
-    """The encoder weight gradients x^T.dz / h^T.dz (K = T.B tokens: 102k at the headline, 1.6M at
-    config #5): the hand-written deterministic split-K GEMM (wgrad.hip ``wgrad_tt``: fp32 slabs
-    summed in split order, no atomics, no torch.sum pass) where the shape fits it, else
+    """Long-K weight gradients out = a^T . b: the encoder's x^T.dz / h^T.dz (K = T.B tokens:
+    102k at the headline, 1.6M at config #5) and the inline decoder-side ones (K = D.B): the
+    hand-written deterministic split-K GEMM (wgrad.hip ``wgrad_tt``: fp32 slabs summed in split
+    order, no atomics, no torch.sum pass) where the shape fits it and is large, else
     ``wgrad_into``.  Its slab workspace is one buffer per device, grown outside graph capture
     (the trainer's eager warm-up) and reused by the captured graphs: these calls run one after
-    another on the encoder-backward stream (model.py:290-297 / 89-93 gradients)."""
+    another on the backward stream (model.py:290-297 / 89-93 gradients)."""
     # large shapes only (config #5: K.M.N >= 3e11); at the headline's K = 102k the split-K bmm is
     # as fast or faster (profiles/r6/wgrad_tt.md)
     if (WGRAD_TT and a.is_cuda and a.dtype == BF and b.dtype == BF and out.dtype == F32
@@ -1206,7 +1207,8 @@ class HipPointerGenerator:
         run = late.append if self.defer_wgrad else (lambda f: f())
         # the deferred ones go through wgrad_tn (wgrad.hip: no inter-workgroup waits) into the
         # zeroed gradient slices; inline, the library split-K path
-        wg = (lambda out, a, b: k.wgrad_tn(a, b, out)) if self.defer_wgrad else wgrad_into
+        # inline (config #5's batch 2048, deterministic mode): the large shapes on wgrad_tt
+        wg = (lambda out, a, b: k.wgrad_tn(a, b, out)) if self.defer_wgrad else wgrad_enc_into
 
         def out_proj_wgrad():
             wg(g(OUT_M)[:H], Hn, doutb)
