@@ -542,9 +542,9 @@ bool wgrad_tt(const Tensor& a, const Tensor& b, const Tensor& out, const Tensor&
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.stride(1) == 1 && ws.is_contiguous(), "wgrad_tt: unit column stride");
   const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
   TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "wgrad_tt: shapes");
-  if (!(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 4 == 0 && (uintptr_t)a.data_ptr() % 16 == 0 &&
-        (uintptr_t)b.data_ptr() % 16 == 0 && (uintptr_t)out.data_ptr() % 16 == 0))
-    return false;  // 16-byte aligned rows only (the caller takes its other path)
+  if (!(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && (uintptr_t)a.data_ptr() % 16 == 0 &&
+        (uintptr_t)b.data_ptr() % 16 == 0))
+    return false;  // 16-byte aligned operand rows only (the caller takes its other path); out: any
   const bool direct = wgrad_tt_ok((int)M, (int)N, (int)K), swapped = !direct && wgrad_tt_ok((int)N, (int)M, (int)K);
   if (!direct && !swapped) return false;
   TORCH_CHECK(ws.numel() >= wgrad_tt_ws(M, N, K), "wgrad_tt: workspace too small");

@@ -313,12 +313,20 @@ __global__ __launch_bounds__(256) void wgrad_sum_kernel(const float* __restrict_
       t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
     }
     const int m = (int)(i4 / N), n = (int)(i4 % N);
-    float4* o = reinterpret_cast<float4*>(out + (size_t)m * ldo + n);
-    if (acc) {
-      const float4 u = *o;
-      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    float* op = out + (size_t)m * ldo + n;
+    if (((uintptr_t)op & 15) == 0) {
+      float4* o = reinterpret_cast<float4*>(op);
+      if (acc) {
+        const float4 u = *o;
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      }
+      *o = t;
+    } else {  // an output slice of the flat gradient buffer need not be 16-byte aligned
+      if (acc) {
+        t.x += op[0]; t.y += op[1]; t.z += op[2]; t.w += op[3];
+      }
+      op[0] = t.x; op[1] = t.y; op[2] = t.z; op[3] = t.w;
     }
-    *o = t;
   } else {
     // slab [S][N][M] -> out [M][N]; block = 64 (n) x 64 (m) of the slab
     __shared__ float tile[64][65];

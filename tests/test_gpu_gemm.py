@@ -139,3 +139,21 @@ def test_wgrad_tt_declines_unsupported_shapes():
     b = torch.zeros(100, 64, device="cuda", dtype=torch.bfloat16)
     assert int(k.wgrad_tt_ws(96, 64, 100)) == 0
     assert not k.wgrad_tt(a, b, torch.empty(96, 64, device="cuda"), torch.empty(1, device="cuda"), False)
+
+
+@pytest.mark.parametrize("M,N", [(256, 256), (128, 512)])
+def test_wgrad_tt_writes_an_unaligned_gradient_slice(M, N):
+    """The output may be a slice of the flat gradient buffer at any 4-byte offset (the parameter
+    offsets are not 16-byte aligned): the slab sum falls back to scalar stores there."""
+    k = _k()
+    K = 2048
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    a = (torch.randn(K, M, device="cuda", generator=g) * 0.1).bfloat16()
+    b = (torch.randn(K, N, device="cuda", generator=g) * 0.1).bfloat16()
+    flat = torch.full((M * N + 8,), 7.0, device="cuda")
+    out = flat[1:1 + M * N].view(M, N)
+    ws = torch.empty(int(k.wgrad_tt_ws(M, N, K)), device="cuda")
+    assert k.wgrad_tt(a, b, out, ws, False)
+    torch.cuda.synchronize()
+    _close(out, a.float().t() @ b.float(), 1e-4)
+    assert float(flat[0]) == 7.0 and bool((flat[1 + M * N:] == 7.0).all())
