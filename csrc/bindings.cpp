@@ -529,8 +529,12 @@ void ptr_loss(const Tensor& logits, const OT& bias, const Tensor& target, const 
 // fp32 workspace ws, summed in split order: deterministic).  The operand roles are swapped when
 // only Nb is a multiple of 256 (the slab is then summed transposed).  Returns false (nothing
 // launched) for shapes it does not take.
-int64_t wgrad_tt_ws(int64_t M, int64_t N, int64_t K) {  // workspace floats for out [M][N]
-  if (wgrad_tt_ok((int)M, (int)N, (int)K)) return (int64_t)wgrad_tt_splits((int)M, (int)N, (int)K) * M * N;
+// workspace floats for out [M][N] (acc = false; 0: shape not supported; 1: one split, the kernel
+// stores straight into out)
+int64_t wgrad_tt_ws(int64_t M, int64_t N, int64_t K) {
+  if (wgrad_tt_ok((int)M, (int)N, (int)K))
+    return wgrad_tt_direct((int)M, (int)N, (int)K, false, false) ? 1
+                                                                 : (int64_t)wgrad_tt_splits((int)M, (int)N, (int)K) * M * N;
   if (wgrad_tt_ok((int)N, (int)M, (int)K)) return (int64_t)wgrad_tt_splits((int)N, (int)M, (int)K) * M * N;
   return 0;
 }
@@ -540,20 +544,28 @@ bool wgrad_tt(const Tensor& a, const Tensor& b, const Tensor& out, const Tensor&
   TORCH_CHECK(a.scalar_type() == BF && b.scalar_type() == BF && out.scalar_type() == F32 && ws.scalar_type() == F32,
               "wgrad_tt: bf16, bf16 -> fp32");
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.stride(1) == 1 && ws.is_contiguous(), "wgrad_tt: unit column stride");
-  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
-  TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "wgrad_tt: shapes");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1), nv = out.size(1);
+  // out may be narrower than b (nv < N: b's columns past nv are K-padding of a 128-aligned
+  // operand, e.g. the vocab dlogits rows; those output columns are dropped)
+  TORCH_CHECK(b.size(0) == K && out.size(0) == M && nv <= N, "wgrad_tt: shapes");
   if (!(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && (uintptr_t)a.data_ptr() % 16 == 0 &&
         (uintptr_t)b.data_ptr() % 16 == 0))
     return false;  // 16-byte aligned operand rows only (the caller takes its other path); out: any
-  const bool direct = wgrad_tt_ok((int)M, (int)N, (int)K), swapped = !direct && wgrad_tt_ok((int)N, (int)M, (int)K);
-  if (!direct && !swapped) return false;
-  TORCH_CHECK(ws.numel() >= wgrad_tt_ws(M, N, K), "wgrad_tt: workspace too small");
-  if (direct)
+  const bool plain = wgrad_tt_ok((int)M, (int)N, (int)K), swapped = !plain && wgrad_tt_ok((int)N, (int)M, (int)K);
+  if (!plain && !(swapped && nv == N)) return false;
+  if (nv != N && (nv % 4 != 0)) return false;
+  const bool direct = plain && wgrad_tt_direct((int)M, (int)N, (int)K, false, acc);
+  const int64_t need = direct ? 0 : (int64_t)wgrad_tt_splits((int)(plain ? M : N), (int)(plain ? N : M), (int)K) * M * N;
+  if (ws.numel() < need) {
+    TORCH_CHECK(acc, "wgrad_tt: workspace too small");
+    return false;  // acc on a one-split shape needs the slab wgrad_tt_ws did not count
+  }
+  if (plain)
     launch_wgrad_tt(P<bf16>(a), (int)a.stride(0), P<bf16>(b), (int)b.stride(0), P<float>(ws), P<float>(out),
-                    (int)out.stride(0), (int)M, (int)N, (int)K, false, acc, stream());
+                    (int)out.stride(0), (int)M, (int)N, (int)K, false, acc, (int)nv, stream());
   else  // GEMM over (b, a): slab [S][N][M], summed into out [M][N] transposed
     launch_wgrad_tt(P<bf16>(b), (int)b.stride(0), P<bf16>(a), (int)a.stride(0), P<float>(ws), P<float>(out),
-                    (int)out.stride(0), (int)N, (int)M, (int)K, true, acc, stream());
+                    (int)out.stride(0), (int)N, (int)M, (int)K, true, acc, (int)M, stream());
   return true;
 }
 void wgrad_tn(const Tensor& a, const Tensor& b, const Tensor& out) {
@@ -598,6 +610,31 @@ void debug_clear() { tsamd_debug_clear(); }
 // through the encoder step frame (rev [B][T] int64, direction dir; ids [B][T] int64 optional: A is
 // then the embedding table) -- every operand row-contiguous with its own leading dimension
 bool gemm_bt_ok(int64_t M, int64_t N, int64_t K) { return gemm_bt_supported((int)M, (int)N, (int)K, N % 256 == 0 ? 256 : 128); }
+// split-K gemm_bt: out (= or +=) A . Bt^T over S K-splits into the fp32 slab ws ([S][M][N]),
+// summed in split order (deterministic).  Workspace floats, 0 when the shape does not split.
+int64_t gemm_bt_splitk_ws(int64_t M, int64_t N, int64_t K) {
+  if (!gemm_bt_ok(M, N, K)) return 0;
+  const int S = gemm_bt_splits((int)M, (int)N, (int)K);
+  return S > 1 ? (int64_t)S * M * N : 0;
+}
+bool gemm_bt_splitk(const Tensor& A, const Tensor& Bt, const Tensor& out, const Tensor& ws, bool acc) {
+  TORCH_CHECK(A.is_cuda() && A.dim() == 2 && A.scalar_type() == BF && A.stride(1) == 1, "gemm_bt_splitk: A [rows, K] bf16");
+  TORCH_CHECK(Bt.is_cuda() && Bt.dim() == 2 && Bt.scalar_type() == BF && Bt.stride(1) == 1, "gemm_bt_splitk: Bt [N, K] bf16");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.stride(1) == 1 && out.scalar_type() == F32, "gemm_bt_splitk: out fp32");
+  TORCH_CHECK(ws.is_cuda() && ws.is_contiguous() && ws.scalar_type() == F32, "gemm_bt_splitk: fp32 workspace");
+  const int64_t M = out.size(0), N = out.size(1), K = Bt.size(1);
+  TORCH_CHECK(Bt.size(0) == N && A.size(1) == K && A.size(0) >= M, "gemm_bt_splitk: shape mismatch A ", A.sizes(), " Bt ",
+              Bt.sizes(), " out ", out.sizes());
+  const int64_t need = gemm_bt_splitk_ws(M, N, K);
+  if (need == 0 || ws.numel() < need) return false;
+  if (!(A.stride(0) % 8 == 0 && Bt.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 &&
+        reinterpret_cast<uintptr_t>(Bt.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 &&
+        out.stride(0) % 4 == 0))
+    return false;
+  launch_gemm_bt_splitk(P<bf16>(A), A.stride(0), P<bf16>(Bt), Bt.stride(0), P<float>(ws), P<float>(out), out.stride(0),
+                        (int)M, (int)N, (int)K, acc, stream());
+  return true;
+}
 void gemm_bt(const Tensor& A, const Tensor& Bt, const Tensor& out, double beta, const OT& bias, const OT& ids,
              const OT& rev, int64_t B, int64_t T, int64_t dir, const OT& xsf) {
   TORCH_CHECK(A.is_cuda() && A.dim() == 2 && A.scalar_type() == BF && A.stride(1) == 1, "gemm_bt: A [rows, K] bf16");
@@ -704,7 +741,13 @@ void vocab_train_bwd(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
   TORCH_CHECK(H == 128 || H == 256 || H == 512, "fused training vocab head: hidden size 128, 256 or 512");
   TORCH_CHECK(N >= 1 && V >= 1 && ldx >= H && ldx % 8 == 0, "bad N/V/ldx");
   numel_eq(X, N * ldx, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias"); numel_eq(target, N, "target");
-  numel_eq(lse, N, "lse"); numel_eq(alpha, N, "alpha"); numel_eq(dl, N * V, "dl"); chko(dbias, F32, V, "dbias");
+  numel_eq(lse, N, "lse"); numel_eq(alpha, N, "alpha"); chko(dbias, F32, V, "dbias");
+  // dlogits rows of ldd >= V elements (numel N * ldd): the columns past V are written 0, so the
+  // gradient GEMMs can run over a 128-aligned K / N (every column up to ldd lies in a vocab tile)
+  TORCH_CHECK(dl.numel() % N == 0, "dl: numel must be N * ldd");
+  const int64_t ldd = dl.numel() / N;
+  TORCH_CHECK(ldd >= V && (ldd == V || (ldd % 8 == 0 && ldd <= (int64_t)vocab_train_cols((int)V, (int)H))),
+              "dl: row length ", ldd, " must be V or a multiple of 8 covered by the vocab tiles");
   const int64_t RB = (N + 31) / 32;
   const bool has = vblk.has_value();
   // vblk + vblk_n alone: compacted dlogits (live block j -> rows 32 j ..); with vlive + vstate: in place
@@ -713,7 +756,7 @@ void vocab_train_bwd(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
   chko(vblk, I32, RB, "vblk"); chko(vblk_n, I32, 1, "vblk_n"); chko(vlive, I32, RB, "vlive");
   chko(vstate, I32, RB, "vstate");
   launch_vocab_train_bwd(P<bf16>(X), (int)ldx, P<bf16>(WT), P<float>(bias), P<int>(target), P<float>(lse), P<float>(alpha),
-                         P<bf16>(dl), PO<float>(dbias), N, V, H, PO<int>(vblk), PO<int>(vblk_n), PO<int>(vlive),
+                         P<bf16>(dl), (int)ldd, PO<float>(dbias), N, V, H, PO<int>(vblk), PO<int>(vblk_n), PO<int>(vlive),
                          PO<int>(vstate), stream());
 }
 
@@ -1111,6 +1154,8 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("debug_clear", &debug_clear);
   m.def("gemm_bt_ok", &gemm_bt_ok);
   m.def("gemm_bt", &gemm_bt);
+  m.def("gemm_bt_splitk_ws", &gemm_bt_splitk_ws);
+  m.def("gemm_bt_splitk", &gemm_bt_splitk);
   m.def("gemm_bt_merge", &gemm_bt_merge);
   m.def("cu_hold_max_lds", &cu_hold_max_lds_op);
   m.def("cu_hold", &cu_hold);

@@ -47,6 +47,8 @@ struct GemmP {
   bf16* xsf;           // AMODE 1, nullable: the gathered A rows [M][K]
   long lda, ldb, ldc, nsrc;
   int M, N, K, B, T, dir;
+  int kchunk;    // split-K (AMODE 0, fp32 out): K columns per split (multiple of 64; K when unsplit)
+  long sstride;  // split s writes its partial tile to C + s * sstride (a slab summed afterwards)
 };
 
 __device__ __forceinline__ const bf16* a_row(const GemmP& p, int m, int AMODE) {
@@ -155,14 +157,18 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
   // workgroup -> (m tile, n tile): groups of 8 consecutive ids = one id per XCD; within an XCD the
   // ids walk the N tiles of one M tile before the next M tile
   const int ntn = p.N / BN, ntm = (p.M + BM - 1) / BM;
-  const int nwg = ntn * ntm;
+  const int nwg = gridDim.x;  // ntn x ntm tiles x the K splits
   const int id = blockIdx.x;
   const int xcd = id & 7, per = (nwg + 7) >> 3, q = nwg >> 3, r8 = nwg & 7;
   // bijective remap (cdna_hip_programming.md s5, XCD swizzle)
-  const int lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (id >> 3);
+  const int lin0 = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (id >> 3);
   (void)per;
+  // split-K: split sk = lin0 / tiles (the tiles of one split are consecutive, so one XCD's L2
+  // serves a K chunk's B panel to the M tiles it runs)
+  const int sk = lin0 / (ntn * ntm), lin = lin0 - sk * (ntn * ntm);
   const int tm = lin / ntn, tn = lin - tm * ntn;
   const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = sk * p.kchunk;
 
   // per-lane source pointers of the glds pieces: piece i of this wave covers 8 rows; lane l
   // loads row (piece row0 + l / 8), k-chunk (l % 8) ^ (row & 7) of the current K tile
@@ -176,7 +182,7 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
       asrc[i] = a_row2(p, m0 + row, 0) + ((lc ^ (row & 7)) * 8);
       asrc1[i] = a_row2(p, m0 + row, 1) + ((lc ^ (row & 7)) * 8);
     } else {
-      asrc[i] = a_row(p, m0 + row, AMODE) + ((lc ^ (row & 7)) * 8);
+      asrc[i] = a_row(p, m0 + row, AMODE) + kbeg + ((lc ^ (row & 7)) * 8);
     }
   }
   const int nkh = p.K / (2 * BK);  // AMODE 2: k tiles per half
@@ -184,7 +190,7 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
 #pragma unroll
   for (int i = 0; i < B_PER_WAVE; ++i) {
     const int row = (wid * B_PER_WAVE + i) * 8 + lr;
-    bsrc[i] = p.Bt + (size_t)(n0 + row) * p.ldb + ((lc ^ (row & 7)) * 8);
+    bsrc[i] = p.Bt + (size_t)(n0 + row) * p.ldb + kbeg + ((lc ^ (row & 7)) * 8);
   }
   auto stage_load = [&](int s, int kt) {
     char* base = smem + s * STAGE;
@@ -206,7 +212,7 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.K / BK;
+  const int nk = (min(p.K, kbeg + p.kchunk) - kbeg) / BK;
   // fragment read offsets: lane reads row (l & 15) of a subtile, k-chunk kb * 4 + (l >> 4)
   const int fr = lane & 15, fq = lane >> 4;
   stage_load(0, 0);
@@ -253,7 +259,9 @@ __global__ __launch_bounds__(GM_THREADS, 1) void gemm_bt_kernel(GemmP p) {
     __syncthreads();
   }
 
-  gemm_epilogue<BN, OUT, BETA>(p, acc, smem, m0, n0, wr, wc, wid, lane);
+  GemmP ps = p;  // split sk's partial tile: its slab
+  ps.C = reinterpret_cast<char*>(p.C) + (size_t)sk * p.sstride * (OUT == 1 ? 2 : 4);
+  gemm_epilogue<BN, OUT, BETA>(ps, acc, smem, m0, n0, wr, wc, wid, lane);
 }
 
 bool gemm_bt_supported(int M, int N, int K, int BN) {
@@ -265,7 +273,7 @@ size_t gemm_bt_lds(int BN) { return 2 * (size_t)(GM_BM * GM_BK * 2 + BN * GM_BK 
 void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, long ldc, bool out_bf16, bool beta,
                     const float* bias, int M, int N, int K, int amode, const int64_t* ids, const int64_t* rev,
                     bf16* xsf, long nsrc, int B, int T, int dir, hipStream_t st) {
-  GemmP p{A, Bt, C, bias, ids, rev, xsf, lda, ldb, ldc, nsrc, M, N, K, B, T, dir};
+  GemmP p{A, Bt, C, bias, ids, rev, xsf, lda, ldb, ldc, nsrc, M, N, K, B, T, dir, K, 0};
   const int BN = N % 256 == 0 ? 256 : 128;
   const int grid = ((M + GM_BM - 1) / GM_BM) * (N / BN);
   const size_t lds = gemm_bt_lds(BN);
@@ -291,4 +299,37 @@ void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, 
   }
 #undef GL_OUT
 #undef GL
+}
+
+// Split-K (long K, few output tiles: the vocab input gradient dX = dlogits . W, K = V): S
+// splits of the K range as S x the tiles, each storing its fp32 partial tile to slab[s]
+// ([S][M][N]), then the slab sum (wgrad.hip) adds the splits in order into out -- deterministic,
+// no atomics.  S fills about one round of the 256 CUs (one 512-thread workgroup per CU).
+int gemm_bt_splits(int M, int N, int K) {
+  const int BN = N % 256 == 0 ? 256 : 128, tiles = ((M + GM_BM - 1) / GM_BM) * (N / BN), steps = K / GM_BK;
+  int s = 256 / tiles;
+  if (s > steps / 16) s = steps / 16;  // >= 16 K steps per split
+  if (s < 2) return 1;
+  const int kc = (steps + s - 1) / s;
+  return (steps + kc - 1) / kc;
+}
+
+void launch_gemm_bt_splitk(const bf16* A, long lda, const bf16* Bt, long ldb, float* slab, float* out, long ldo, int M,
+                           int N, int K, bool acc, hipStream_t st) {
+  const int S = gemm_bt_splits(M, N, K), steps = K / GM_BK, kc = (steps + S - 1) / S;
+  GemmP p{A, Bt, slab, nullptr, nullptr, nullptr, nullptr, lda, ldb, (long)N, 0, M, N, K, 0, 0, 0, kc * GM_BK,
+          (long)M * N};
+  const int BN = N % 256 == 0 ? 256 : 128;
+  const int grid = ((M + GM_BM - 1) / GM_BM) * (N / BN) * S;
+  const size_t lds = gemm_bt_lds(BN);
+  if (BN == 256) {
+    (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<0, 256, 0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    hipLaunchKernelGGL((gemm_bt_kernel<0, 256, 0, false>), dim3(grid), dim3(GM_THREADS), lds, st, p);
+  } else {
+    (void)hipFuncSetAttribute((const void*)gemm_bt_kernel<0, 128, 0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    hipLaunchKernelGGL((gemm_bt_kernel<0, 128, 0, false>), dim3(grid), dim3(GM_THREADS), lds, st, p);
+  }
+  launch_slab_sum(slab, out, (int)ldo, M, N, S, acc, st);
 }

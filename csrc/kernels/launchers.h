@@ -141,11 +141,12 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
                        int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st,
                        const BeamTail* bt = nullptr);
 int vocab_train_tiles(int V, int H);
+int vocab_train_cols(int V, int H);  // columns the vocab tiles cover (>= V)
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
                             float* zg, float* lse, float* pv, int N, int V, int H, const int* vblk, const int* vblk_n,
                             hipStream_t st);
 void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
-                            const float* lse, const float* alpha, bf16* dl, float* dbias, int N, int V, int H,
+                            const float* lse, const float* alpha, bf16* dl, int ldd, float* dbias, int N, int V, int H,
                             const int* vblk, const int* vblk_n, const int* vlive, int* vstate, hipStream_t st);
 void launch_ptr_rowfin(const float* pv, const int* target, const float* rowg, const float* pgen, const float* attn,
                        const int* ext, const int* lens, float* loss_row, float* alpha, float* dpre, float* dA, int N,
@@ -190,7 +191,8 @@ int wgrad_tn_splits(int M, int N, int K);
 int wgrad_tt_splits(int M, int N, int K);
 bool wgrad_tt_ok(int M, int N, int K);
 void launch_wgrad_tt(const bf16* a, int lda, const bf16* b, int ldb, float* slab, float* out, int ldo, int M, int N,
-                     int K, bool trans, bool acc, hipStream_t st);
+                     int K, bool trans, bool acc, int nv, hipStream_t st);
+bool wgrad_tt_direct(int M, int N, int K, bool trans, bool acc);
 void launch_wgrad_tn(const bf16* a, int lda, const bf16* b, int ldb, float* out, int ldo, int M, int N, int K,
                      hipStream_t st);
 
@@ -211,6 +213,10 @@ void launch_tanh_tput(const float* in, float* out, int threads, int iters, int m
 
 // gemm_mfma.hip: C (+)= A[arow(m)] . Bt^T (+ bias); amode 0 plain rows, 1 step-frame gather
 bool gemm_bt_supported(int M, int N, int K, int BN);
+int gemm_bt_splits(int M, int N, int K);
+void launch_gemm_bt_splitk(const bf16* A, long lda, const bf16* Bt, long ldb, float* slab, float* out, long ldo, int M,
+                           int N, int K, bool acc, hipStream_t st);
+void launch_slab_sum(const float* slab, float* out, int ldo, int M, int N, int S, bool acc, hipStream_t st);
 void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, long ldc, bool out_bf16, bool beta,
                     const float* bias, int M, int N, int K, int amode, const int64_t* ids, const int64_t* rev,
                     bf16* xsf, long nsrc, int B, int T, int dir, hipStream_t st);

@@ -112,9 +112,9 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     float* __restrict__ zg,           // [N]      pass 1: gold logit (rows with w < V)
     const float* __restrict__ lse,    // [N]      pass 2
     const float* __restrict__ alpha,  // [N]      pass 2
-    bf16* __restrict__ dl,            // [N][V]   pass 2: dlogits
+    bf16* __restrict__ dl,            // [N][ldd] pass 2: dlogits (columns V .. ldd - 1 written 0)
     float* __restrict__ dbias,        // [V]      pass 2 (nullable): += column sums of dlogits
-    int N, int V, int ldx,
+    int N, int V, int ldx, int ldd,
     const int* __restrict__ vblk,     // nullable: the live 32-row blocks (EngineConfig.skip_pad_steps),
     const int* __restrict__ vblk_n,   // *vblk_n of them; the units enumerate only those
     int compact) {                    // pass 2: live block j's dlogits go to rows 32 j .. (compacted)
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
             cs[i][0] += d[i][0];
             cs[i][1] += d[i][1];
           }
-          bf16* dst = dl + (size_t)(compact ? (u % RB) * VR_ROWS + rr : row) * V + cw + q4;
+          bf16* dst = dl + (size_t)(compact ? (u % RB) * VR_ROWS + rr : row) * ldd + cw + q4;
           if (full) {
             // (plain stores: the 4 stores of a row's 128-byte line are merged in L2; non-temporal
             // stores went to HBM as 32-byte pieces, 1.31 -> 1.75 ms)
@@ -329,6 +329,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 if (col + r < V) dst[16 * i + r] = f2bf(dv[r]);
+                else if (col + r < ldd) dst[16 * i + r] = f2bf(0.f);  // the GEMMs' zero K padding
             }
           }
         }
@@ -359,13 +360,13 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
 // becomes this batch's liveness.  Consecutive batches have similar length profiles (rows sorted
 // by live steps), so few blocks change.
 __global__ __launch_bounds__(256) void vocab_zero_dead_kernel(bf16* __restrict__ dl, const int* __restrict__ vlive,
-                                                              int* __restrict__ state, int N, int V) {
+                                                              int* __restrict__ state, int N, int ldd) {
   const int b = blockIdx.x;
   const int live = vlive[b];
   if (!live && state[b]) {
     const size_t r0 = (size_t)b * VR_ROWS, r1 = min((size_t)N, r0 + VR_ROWS);
-    bf16* p = dl + r0 * V;
-    const size_t n = (r1 - r0) * (size_t)V;
+    bf16* p = dl + r0 * ldd;
+    const size_t n = (r1 - r0) * (size_t)ldd;
     const size_t head = (16 - ((uintptr_t)p & 15)) & 15;  // bytes to 16-byte alignment
     const size_t h = min(n, head / 2);
     for (size_t i = threadIdx.x; i < h; i += 256) p[i] = f2bf(0.f);
@@ -441,6 +442,7 @@ __global__ __launch_bounds__(256) void ptr_rowfin_kernel(
 }
 
 int vocab_train_tiles(int V, int H) { return (V + vr_cols(H) - 1) / vr_cols(H); }
+int vocab_train_cols(int V, int H) { return vocab_train_tiles(V, H) * vr_cols(H); }
 
 // 2 workgroups per CU (<= 256 VGPRs, ~36 KB LDS each at H = 256, ~67 KB at H = 512): 512
 // persistent workgroups
@@ -454,7 +456,7 @@ void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float*
                             hipStream_t st) {
   const int grid = vocab_train_grid(N, V, H);
 #define VF(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, false>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
-                                  part, zg, nullptr, nullptr, nullptr, nullptr, N, V, ldx, vblk, vblk_n, 0)
+                                  part, zg, nullptr, nullptr, nullptr, nullptr, N, V, ldx, V, vblk, vblk_n, 0)
   if (H == 512) VF(512);
   else if (H == 256) VF(256);
   else VF(128);
@@ -464,7 +466,7 @@ void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float*
 }
 
 void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target,
-                            const float* lse, const float* alpha, bf16* dl, float* dbias, int N, int V, int H,
+                            const float* lse, const float* alpha, bf16* dl, int ldd, float* dbias, int N, int V, int H,
                             const int* vblk, const int* vblk_n, const int* vlive, int* vstate, hipStream_t st) {
   const int grid = vocab_train_grid(N, V, H);
   // with the live-block list: either the dead blocks an earlier pass wrote are zeroed (vlive /
@@ -472,9 +474,9 @@ void launch_vocab_train_bwd(const bf16* X, int ldx, const bf16* WT, const float*
   const int compact = vblk && !vlive;
   if (vblk && vlive)
     hipLaunchKernelGGL(vocab_zero_dead_kernel, dim3((N + VR_ROWS - 1) / VR_ROWS), dim3(256), 0, st, dl, vlive, vstate,
-                       N, V);
+                       N, ldd);
 #define VB(HH) hipLaunchKernelGGL((vocab_train_kernel<HH, true>), dim3(grid), dim3(256), 0, st, X, WT, bias, target, \
-                                  nullptr, nullptr, lse, alpha, dl, dbias, N, V, ldx, vblk, vblk_n, compact)
+                                  nullptr, nullptr, lse, alpha, dl, dbias, N, V, ldx, ldd, vblk, vblk_n, compact)
   if (H == 512) VB(512);
   else if (H == 256) VB(256);
   else VB(128);

@@ -213,8 +213,8 @@ __device__ __forceinline__ bf16x8 tt_frag(const char* img, int kb, int c0, int l
 
 template <int BN>
 __global__ __launch_bounds__(512, 1) void wgrad_tt_kernel(const bf16* __restrict__ a, int lda, const bf16* __restrict__ b,
-                                                          int ldb, float* __restrict__ slab, int M, int N, int kchunk,
-                                                          int K) {
+                                                          int ldb, float* __restrict__ dst, long sstride, int ldd,
+                                                          int nv, int M, int N, int kchunk, int K) {
   constexpr int BM = 256, BK = 64, HI = 64 * 256;           // half-image bytes (64 rows x 256 B)
   constexpr int NHA = BM / 128, NHB = BN / 128;             // half images per operand
   constexpr int STAGE = (NHA + NHB) * HI;
@@ -287,15 +287,19 @@ __global__ __launch_bounds__(512, 1) void wgrad_tt_kernel(const bf16* __restrict
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  // accumulator (i, j, r): m = m0 + 128 wr + 16 i + 4 (l >> 4) + r, n = n0 + wc WN + 16 j + (l & 15)
-  float* sl = slab + (size_t)s * M * N;
+  // accumulator (i, j, r): m = m0 + 128 wr + 16 i + 4 (l >> 4) + r, n = n0 + wc WN + 16 j + (l & 15);
+  // to split s's slab (sstride apart, rows of ldd = N) or, unsplit, straight to the output rows
+  // (ldd = ldo), columns n < nv
+  float* sl = dst + (size_t)s * sstride;
+  const int nl = n0 + wc * WN + (lane & 15);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float* row = sl + (size_t)(m0 + 128 * wr + 16 * i + 4 * (lane >> 4) + r) * N + n0 + wc * WN + (lane & 15);
+      float* row = sl + (size_t)(m0 + 128 * wr + 16 * i + 4 * (lane >> 4) + r) * ldd + nl;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) row[16 * j] = acc[i][j][r];
+      for (int j = 0; j < NJ; ++j)
+        if (nl + 16 * j < nv) row[16 * j] = acc[i][j][r];
     }
 }
 
@@ -303,10 +307,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_tt_kernel(const bf16* __restrict
 // of the operands were swapped) and out[m][n] = sum_s slab[s][n][m] through a 64 x 64 LDS tile
 template <bool TRANS>
 __global__ __launch_bounds__(256) void wgrad_sum_kernel(const float* __restrict__ slab, float* __restrict__ out, int ldo,
-                                                        int M, int N, int S, bool acc) {
-  if constexpr (!TRANS) {
+                                                        int M, int N, int S, bool acc, int nv) {
+  if constexpr (!TRANS) {  // out columns n < nv (nv % 4 == 0)
     const size_t i4 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4, MN = (size_t)M * N;
-    if (i4 >= MN) return;
+    if (i4 >= MN || (int)(i4 % N) >= nv) return;
     float4 t = *reinterpret_cast<const float4*>(slab + i4);
     for (int s = 1; s < S; ++s) {
       const float4 u = *reinterpret_cast<const float4*>(slab + (size_t)s * MN + i4);
@@ -351,6 +355,13 @@ __global__ __launch_bounds__(256) void wgrad_sum_kernel(const float* __restrict_
   }
 }
 
+// out[m][n] (= or +=) sum_s slab[s][m][n] in split order ([S][M][N] fp32; the split-K gemm_bt)
+void launch_slab_sum(const float* slab, float* out, int ldo, int M, int N, int S, bool acc, hipStream_t st) {
+  const size_t n4 = (size_t)M * N / 4;
+  hipLaunchKernelGGL(wgrad_sum_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, slab, out, ldo, M, N,
+                     S, acc, N);
+}
+
 // the split of K: ~1 workgroup per CU (tiles x S >= 256), chunks of whole 64-row steps
 int wgrad_tt_splits(int M, int N, int K) {
   const int BN = N % 256 == 0 ? 256 : 128;
@@ -361,25 +372,35 @@ int wgrad_tt_splits(int M, int N, int K) {
   return (steps + kc - 1) / kc;
 }
 bool wgrad_tt_ok(int M, int N, int K) { return M % 256 == 0 && N % 128 == 0 && K % 64 == 0 && K >= 64; }
+bool wgrad_tt_direct(int M, int N, int K, bool trans, bool acc) { return !trans && !acc && wgrad_tt_splits(M, N, K) == 1; }
 
 void launch_wgrad_tt(const bf16* a, int lda, const bf16* b, int ldb, float* slab, float* out, int ldo, int M, int N,
-                     int K, bool trans, bool acc, hipStream_t st) {
+                     int K, bool trans, bool acc, int nv, hipStream_t st) {
   const int BN = N % 256 == 0 ? 256 : 128;
   const int S = wgrad_tt_splits(M, N, K), steps = K / 64, kc = (steps + S - 1) / S;
   const int grid = (M / 256) * (N / BN) * S;
   const size_t lds = (size_t)(2 + BN / 128) * 64 * 256 * 2;
+  // one split and a plain store: the tiles go straight to out (no slab pass)
+  const bool direct = wgrad_tt_direct(M, N, K, trans, acc);
+  float* dst = direct ? out : slab;
+  const long sstride = direct ? 0 : (long)M * N;
+  const int ldd = direct ? ldo : N, nvk = direct ? nv : N;
   if (BN == 256) {
     (void)hipFuncSetAttribute((const void*)wgrad_tt_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(wgrad_tt_kernel<256>, dim3(grid), dim3(512), lds, st, a, lda, b, ldb, slab, M, N, kc * 64, K);
+    hipLaunchKernelGGL(wgrad_tt_kernel<256>, dim3(grid), dim3(512), lds, st, a, lda, b, ldb, dst, sstride, ldd, nvk, M, N,
+                       kc * 64, K);
   } else {
     (void)hipFuncSetAttribute((const void*)wgrad_tt_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(wgrad_tt_kernel<128>, dim3(grid), dim3(512), lds, st, a, lda, b, ldb, slab, M, N, kc * 64, K);
+    hipLaunchKernelGGL(wgrad_tt_kernel<128>, dim3(grid), dim3(512), lds, st, a, lda, b, ldb, dst, sstride, ldd, nvk, M, N,
+                       kc * 64, K);
   }
+  if (direct) return;
   if (!trans) {
     const size_t n4 = (size_t)M * N / 4;
     hipLaunchKernelGGL(wgrad_sum_kernel<false>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, slab, out, ldo, M, N,
-                       S, acc);
+                       S, acc, nv);
   } else {  // out is [N][M] (ldo), the slab [S][M][N]: out[n][m] = sum slab[s][m][n]
-    hipLaunchKernelGGL(wgrad_sum_kernel<true>, dim3((M / 64) * (N / 64)), dim3(256), 0, st, slab, out, ldo, N, M, S, acc);
+    hipLaunchKernelGGL(wgrad_sum_kernel<true>, dim3((M / 64) * (N / 64)), dim3(256), 0, st, slab, out, ldo, N, M, S, acc,
+                       M);
   }
 }

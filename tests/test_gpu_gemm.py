@@ -157,3 +157,50 @@ def test_wgrad_tt_writes_an_unaligned_gradient_slice(M, N):
     torch.cuda.synchronize()
     _close(out, a.float().t() @ b.float(), 1e-4)
     assert float(flat[0]) == 7.0 and bool((flat[1 + M * N:] == 7.0).all())
+
+
+@pytest.mark.parametrize("M,N,K,acc", [(16000, 256, 50048, False), (1000, 512, 8192, True), (300, 128, 4096, False)])
+def test_gemm_bt_splitk_matches_fp32_and_is_deterministic(M, N, K, acc):
+    """Split-K gemm_bt (the vocab input gradient dX = dlogits . W^T, K = the padded vocabulary):
+    S K-splits into fp32 slabs summed in split order -- against an fp32 matmul of the same bf16
+    operands, bit-identical on a repeat, rows past M untouched; partial last row tile."""
+    k = _k()
+    n = int(k.gemm_bt_splitk_ws(M, N, K))
+    assert n > 0, "the shape should split"
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.05).bfloat16()
+    Bt = (torch.randn(N, K, device="cuda", generator=g) * 0.05).bfloat16()
+    c0 = torch.randn(M, N, device="cuda", generator=g)
+    full = torch.full((M + 16, N), 12345.0, device="cuda")
+    out = full[:M]
+    out.copy_(c0) if acc else out.fill_(float("nan"))
+    ws = torch.empty(n, device="cuda")
+    assert k.gemm_bt_splitk(A, Bt, out, ws, acc)
+    torch.cuda.synchronize()
+    ref = A.float() @ Bt.float().t() + (c0 if acc else 0)
+    _close(out, ref, 1e-4)
+    assert bool((full[M:] == 12345.0).all())
+    if not acc:
+        again = torch.empty_like(out)
+        k.gemm_bt_splitk(A, Bt, again, ws, False)
+        assert torch.equal(again, out)
+    assert int(k.gemm_bt_splitk_ws(131072, 512, 4096)) == 0  # many tiles: no split, the caller's other path
+
+
+@pytest.mark.parametrize("N,nv", [(1152, 1000), (32896, 32800)])
+def test_wgrad_tt_narrow_output_drops_padding_columns(N, nv):
+    """b wider than out (the padded dlogits rows, Vp = 128-aligned): out gets b's first nv columns
+    only, through the slab sum (N = 1152: 9 tiles, split K) or stored straight into out (N =
+    32896: 257 tiles, one split, no slab); the columns after it keep their sentinel."""
+    k = _k()
+    K, M = 2048, 256
+    g = torch.Generator(device="cuda").manual_seed(3)
+    a = (torch.randn(K, M, device="cuda", generator=g) * 0.1).bfloat16()
+    b = (torch.randn(K, N, device="cuda", generator=g) * 0.1).bfloat16()
+    full = torch.full((M, nv + 24), 7.0, device="cuda")
+    out = full[:, :nv]
+    ws = torch.empty(max(1, int(k.wgrad_tt_ws(M, N, K))), device="cuda")
+    assert k.wgrad_tt(a, b, out, ws, False)
+    torch.cuda.synchronize()
+    _close(out, (a.float().t() @ b.float())[:, :nv], 1e-4)
+    assert bool((full[:, nv:] == 7.0).all())

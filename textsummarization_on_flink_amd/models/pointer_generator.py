@@ -65,6 +65,16 @@ BLT = os.environ.get("TSAMD_BLT", "1") != "0"
 # the long-K weight gradients (encoder, vocab dW) through blt_mm too (default: split-K batched GEMM)
 BLT_WGRAD = BLT and os.environ.get("TSAMD_BLT_WGRAD", "0") == "1"
 BLT_VDW = BLT and os.environ.get("TSAMD_BLT_VOCAB_DW", "0") == "1"
+# TSAMD_VOCAB_PAD (default 1, fused vocab head): dlogits rows and the bf16 output-projection weight
+# padded to Vp = 128-aligned columns (the pad columns are zero: the vocab head writes them), so
+# the two vocab-gradient GEMMs run at an aligned K / N -- dX = dlogits . W^T on the split-K
+# hand-written GEMM (headline: 566 -> 426 us) or the library (config #5: 7.88 -> 6.76 ms),
+# dW = X^T . dlogits on the library into a [H][Vp] scratch (653 -> 502 us with the copy)
+# (tools/vocab_grad_micro.py, profiles/r6/vocab_grad.md)
+VOCAB_PAD = os.environ.get("TSAMD_VOCAB_PAD", "1") != "0"
+# K.M.N above which the vocab dW keeps the 4-way split-K batched GEMM (config #5: 8.2 ms against
+# 9.5 ms for the library at the padded N)
+VOCAB_DW_SPLIT_MIN = 1e12
 
 
 # TSAMD_GEMM_BT: the hand-written MFMA GEMM (csrc/kernels/gemm_mfma.hip) for the activation GEMMs
@@ -622,7 +632,11 @@ class HipPointerGenerator:
                 w[n] = z(N)
             w["dbias"] = z(V)  # output_projection/v gradient, column sums taken inside pass 2
             w["vstate"] = z((N + 31) // 32, dt=torch.int32)  # dlogits blocks written by the last pass 2
-        w["logits"] = z(D * B, V, dt=BF)
+        # the fused head's dlogits rows: Vp columns (TSAMD_VOCAB_PAD; zero past V)
+        self.Vp = -(-V // 128) * 128 if (self.fused_vocab and VOCAB_PAD) else V
+        w["logits"] = z(D * B, self.Vp, dt=BF)
+        if self.Vp != V and self.det:
+            w["dbias_p"] = z(self.Vp)  # deterministic column sums over the padded rows
         # backward
         w["dlogits"] = w["logits"]
         # compacted vocab head (skip_pad with the fused head, not deterministic mode): pass 2 writes the
@@ -798,6 +812,10 @@ class HipPointerGenerator:
         put("WsT", p[ATT_M].t())
         put("OUTm", p[OUT_M])
         put("OUTmT", p[OUT_M].t())  # [H][H+A] for the per-step linear2 kernel (decode)
+        if getattr(self, "Vp", self.V) != self.V and "owP" not in pk:
+            # [H][Vp], zero past V: the K operand of the padded dX GEMM; "ow" is its [:, :V] view
+            pk["owP"] = torch.zeros(H, self.Vp, dtype=BF, device=p[OW].device)
+            pk["ow"] = pk["owP"][:, :self.V]
         put("ow", p[OW])
         put("ovb", p[OV])  # bias of the bf16 logits GEMM epilogue
         if getattr(self, "fused_vocab", False):
@@ -1044,7 +1062,11 @@ class HipPointerGenerator:
                                   w["dlogits"], None if self.det else w["dbias"], N, V, H, ldx, vb, vn,
                                   w["vlive"] if inplace else None, w["vstate"] if inplace else None)
                 if self.det:  # column sums of the bf16 dlogits in a fixed order
-                    k.colsum(w["dlogits"], w["dbias"], N, V, False)
+                    if self.Vp != V:
+                        k.colsum(w["dlogits"], w["dbias_p"], N, self.Vp, False)
+                        w["dbias"].copy_(w["dbias_p"][:V])
+                    else:
+                        k.colsum(w["dlogits"], w["dbias"], N, V, False)
             return
         gemm(w["logits"], w["outb"], self.pk["ow"], 0.0, self.pk["ovb"])
         self.k.ptr_loss(w["logits"], None, w["target_t"], w["rowg"], pg, w["ATT"] if hps.pointer_gen else None,
@@ -1128,6 +1150,10 @@ class HipPointerGenerator:
         N = self.D * self.B
         if self.compact_vocab:
             return self._backward_head_compact(g, dl, H, V, N)
+        if self.Vp != V:  # padded dlogits rows (fused head, m == H)
+            self._vocab_dw(dst, w["outb_ext"][:, :H], dl)
+            self._dout = self._vocab_dx(dl)
+            return
 
         def dw():
             Sw = 4
@@ -1166,6 +1192,17 @@ class HipPointerGenerator:
         dlc = dl[:M]
         g(OV).copy_(w["dbias"])
         dst = g(OW)
+        if self.Vp != V:
+            self._vocab_dw(dst, xc[:, :H], dlc)
+            dxc = self._vocab_dx(dlc)
+        else:
+            dxc = self._vocab_grads_unpadded(dst, xc, dlc, H, V, M)
+        de = self._dout_ext
+        de.zero_()
+        de.index_copy_(0, idx, dxc.view(nbk, 32, H))  # padding entries land in the dummy block nb
+        self._dout = de[:nb].view(nb * 32, H)[:N]
+
+    def _vocab_grads_unpadded(self, dst, xc, dlc, H, V, M):
         Sw = 4 if not BLT_VDW and M % 4 == 0 and (M // 4) * V < 2 ** 31 else 1
         if Sw > 1:  # split K = M in 4 (one batched GEMM + a sum), as the full head
             parts = torch.bmm(xc.view(Sw, M // Sw, H + 8)[:, :, :H].transpose(1, 2), dlc.view(Sw, M // Sw, V),
@@ -1173,11 +1210,47 @@ class HipPointerGenerator:
             torch.sum(parts, 0, out=dst)
         else:
             gemm(dst, xc[:, :H].t(), dlc)
-        dxc = mmf(dlc, self.pk["ow"].t())  # [M, H]
-        de = self._dout_ext
-        de.zero_()
-        de.index_copy_(0, idx, dxc.view(nbk, 32, H))  # padding entries land in the dummy block nb
-        self._dout = de[:nb].view(nb * 32, H)[:N]
+        return mmf(dlc, self.pk["ow"].t())  # [M, H]
+
+    def _vocab_dw(self, dst, x, dl):
+        """dst[H][V] = x^T . dl[:, :V] (output-projection weight gradient, model.py:290-297 over
+        model.py:229-236) from the padded dlogits rows dl [K][Vp]: the library GEMM at the aligned
+        N into a [H][Vp] scratch, then the first V columns; above VOCAB_DW_SPLIT_MIN the 4-way
+        split-K batched GEMM (+ ordered torch.sum) as before."""
+        K, H, V, Vp = dl.shape[0], self.H, self.V, self.Vp
+        if not BLT_VDW and K * H * V >= VOCAB_DW_SPLIT_MIN and K % 4 == 0 and (K // 4) * Vp < 2 ** 31:
+            parts = torch.bmm(x.unflatten(0, (4, K // 4)).transpose(1, 2), dl.view(4, K // 4, Vp), out_dtype=F32)
+            torch.sum(parts[:, :, :V], 0, out=dst)
+            return
+        if getattr(self, "_dWp", None) is None:
+            self._dWp = torch.empty(H, Vp, dtype=F32, device=self.dev)
+        gemm(self._dWp, x.t(), dl)
+        dst.copy_(self._dWp[:, :V])
+
+    def _vocab_dx(self, dl):
+        """dlogits . W^T [K][H] fp32 (the output-projection input gradient) from the padded dlogits
+        rows and the padded bf16 W [H][Vp]: the hand-written split-K GEMM (gemm_bt + ordered slab
+        sum: deterministic) where the output is a few tiles, else the library GEMM."""
+        K, H, Vp = dl.shape[0], self.H, self.Vp
+        out = torch.empty(K, H, dtype=F32, device=self.dev)
+        ow = self.pk["owP"]
+        if dl.is_cuda and GEMM_BT != "0":
+            k = self.k
+            n = int(k.gemm_bt_splitk_ws(K, H, Vp))
+            if n > 0:
+                ws = getattr(self, "_vdx_ws", None)
+                if ws is None or ws.numel() < n:
+                    if torch.cuda.is_current_stream_capturing():
+                        ws = None  # first seen inside a capture: no allocation there
+                    else:
+                        old = getattr(self, "_vdx_ws_old", [])
+                        if ws is not None:
+                            old.append(ws)  # graphs captured earlier may hold it
+                        self._vdx_ws_old = old
+                        ws = self._vdx_ws = torch.empty(n, dtype=F32, device=self.dev)
+                if ws is not None and k.gemm_bt_splitk(dl, ow, out, ws, False):
+                    return out
+        return gemm(out, dl, ow.t())
 
     def _cast_colsum(self, x, bias_grad):
         """bf16 copy of x [N, C] plus bias_grad += its column sums in one read of x (the

@@ -2,7 +2,10 @@
 H = 256): HIP-event time of the fused pass 1 (logits -> per-tile LSE partials + row stats)
 and pass 2 (recomputed logits -> bf16 dlogits + bias gradient).  Synthetic inputs.
 
-  python tools/vocab_train_micro.py [--rows 25600] [--reps 2]
+  python tools/vocab_train_micro.py [--rows 25600] [--reps 2] [--ldd 50000,50048,...]
+
+--ldd: pass 2 with dlogits rows of these lengths (>= V, the pad columns written 0): the row
+stride's effect on the dlogits stores (profiles/r6/vocab_grad.md).
 """
 import argparse
 import json
@@ -35,6 +38,7 @@ def main():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--ldd", type=str, default="")
     a = ap.parse_args()
     k = ops()
     N, V, H = a.rows, a.vocab, a.hidden
@@ -68,6 +72,14 @@ def main():
             r["dl_maxdiff"] = (cur[1] - ref[1]).abs().max().item()
             r["db_rel"] = ((cur[2] - ref[2]).abs().max() / ref[2].abs().max()).item()
         print(json.dumps(r), flush=True)
+    for ld in [int(v) for v in a.ldd.split(",") if v]:
+        dlp = torch.empty(N, ld, dtype=torch.bfloat16, device=dev)
+        bwd = lambda: k.vocab_train_bwd(X, WT, bias, target, lse, alpha, dlp, db, N, V, H, ldx, None, None, None, None)
+        r = {"ldd": ld, "row_bytes": 2 * ld, "bwd_us": timed(bwd, a.iters)}
+        r["pad_zero"] = bool((dlp[:, V:] == 0).all().item()) if ld > V else None
+        r["same_dl"] = bool(torch.equal(dlp[:64, :V], dl[:64]))
+        print(json.dumps(r), flush=True)
+        del dlp
 
 
 if __name__ == "__main__":
