@@ -742,12 +742,11 @@ void vocab_train_bwd(const Tensor& X, const Tensor& WT, const Tensor& bias, cons
   TORCH_CHECK(N >= 1 && V >= 1 && ldx >= H && ldx % 8 == 0, "bad N/V/ldx");
   numel_eq(X, N * ldx, "X"); numel_eq(WT, V * H, "WT"); numel_eq(bias, V, "bias"); numel_eq(target, N, "target");
   numel_eq(lse, N, "lse"); numel_eq(alpha, N, "alpha"); chko(dbias, F32, V, "dbias");
-  // dlogits rows of ldd >= V elements (numel N * ldd): the columns past V are written 0, so the
-  // gradient GEMMs can run over a 128-aligned K / N (every column up to ldd lies in a vocab tile)
+  // dlogits rows of ldd >= V elements (numel N * ldd): the columns past V are never written (the
+  // caller keeps them zero: the K / N padding of the 128-aligned gradient GEMMs)
   TORCH_CHECK(dl.numel() % N == 0, "dl: numel must be N * ldd");
   const int64_t ldd = dl.numel() / N;
-  TORCH_CHECK(ldd >= V && (ldd == V || (ldd % 8 == 0 && ldd <= (int64_t)vocab_train_cols((int)V, (int)H))),
-              "dl: row length ", ldd, " must be V or a multiple of 8 covered by the vocab tiles");
+  TORCH_CHECK(ldd >= V && (ldd == V || ldd % 8 == 0), "dl: row length ", ldd, " must be V or a multiple of 8");
   const int64_t RB = (N + 31) / 32;
   const bool has = vblk.has_value();
   // vblk + vblk_n alone: compacted dlogits (live block j -> rows 32 j ..); with vlive + vstate: in place

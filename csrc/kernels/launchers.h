@@ -141,7 +141,6 @@ void launch_vocab_topk(const bf16* X, const bf16* WT, const float* bias, const f
                        int R, int V, int H, int T, int K, int beam, PgIn pgi, hipStream_t st,
                        const BeamTail* bt = nullptr);
 int vocab_train_tiles(int V, int H);
-int vocab_train_cols(int V, int H);  // columns the vocab tiles cover (>= V)
 void launch_vocab_train_fwd(const bf16* X, int ldx, const bf16* WT, const float* bias, const int* target, float* part,
                             float* zg, float* lse, float* pv, int N, int V, int H, const int* vblk, const int* vblk_n,
                             hipStream_t st);

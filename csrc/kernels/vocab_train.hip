@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     float* __restrict__ zg,           // [N]      pass 1: gold logit (rows with w < V)
     const float* __restrict__ lse,    // [N]      pass 2
     const float* __restrict__ alpha,  // [N]      pass 2
-    bf16* __restrict__ dl,            // [N][ldd] pass 2: dlogits (columns V .. ldd - 1 written 0)
+    bf16* __restrict__ dl,            // [N][ldd] pass 2: dlogits (columns V .. ldd - 1 never written)
     float* __restrict__ dbias,        // [V]      pass 2 (nullable): += column sums of dlogits
     int N, int V, int ldx, int ldd,
     const int* __restrict__ vblk,     // nullable: the live 32-row blocks (EngineConfig.skip_pad_steps),
@@ -329,7 +329,6 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 if (col + r < V) dst[16 * i + r] = f2bf(dv[r]);
-                else if (col + r < ldd) dst[16 * i + r] = f2bf(0.f);  // the GEMMs' zero K padding
             }
           }
         }
@@ -442,7 +441,6 @@ __global__ __launch_bounds__(256) void ptr_rowfin_kernel(
 }
 
 int vocab_train_tiles(int V, int H) { return (V + vr_cols(H) - 1) / vr_cols(H); }
-int vocab_train_cols(int V, int H) { return vocab_train_tiles(V, H) * vr_cols(H); }
 
 // 2 workgroups per CU (<= 256 VGPRs, ~36 KB LDS each at H = 256, ~67 KB at H = 512): 512
 // persistent workgroups

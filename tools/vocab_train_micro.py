@@ -4,7 +4,7 @@ and pass 2 (recomputed logits -> bf16 dlogits + bias gradient).  Synthetic input
 
   python tools/vocab_train_micro.py [--rows 25600] [--reps 2] [--ldd 50000,50048,...]
 
---ldd: pass 2 with dlogits rows of these lengths (>= V, the pad columns written 0): the row
+--ldd: pass 2 with dlogits rows of these lengths (>= V; the pad columns are never written and stay zero): the row
 stride's effect on the dlogits stores (profiles/r6/vocab_grad.md).
 """
 import argparse
@@ -73,7 +73,7 @@ def main():
             r["db_rel"] = ((cur[2] - ref[2]).abs().max() / ref[2].abs().max()).item()
         print(json.dumps(r), flush=True)
     for ld in [int(v) for v in a.ldd.split(",") if v]:
-        dlp = torch.empty(N, ld, dtype=torch.bfloat16, device=dev)
+        dlp = torch.zeros(N, ld, dtype=torch.bfloat16, device=dev)  # pad columns: zero, never written
         bwd = lambda: k.vocab_train_bwd(X, WT, bias, target, lse, alpha, dlp, db, N, V, H, ldx, None, None, None, None)
         r = {"ldd": ld, "row_bytes": 2 * ld, "bwd_us": timed(bwd, a.iters)}
         r["pad_zero"] = bool((dlp[:, V:] == 0).all().item()) if ld > V else None
