@@ -568,6 +568,31 @@ bool wgrad_tt(const Tensor& a, const Tensor& b, const Tensor& out, const Tensor&
                     (int)out.stride(0), (int)N, (int)M, (int)K, true, acc, (int)M, stream());
   return true;
 }
+// batched attention-context GEMMs (ctx_bmm.hip): att / dctx step-major [D][B][T] / [D][B][A] bf16,
+// enc [B][T][A] bf16; outputs fp32 (ctx_fwd also the bf16 twin)
+bool ctx_bmm_ok_op(int64_t B, int64_t T, int64_t D, int64_t A) { return ctx_bmm_ok((int)B, (int)T, (int)D, (int)A); }
+static void ctx_chk(const Tensor& t, at::ScalarType dt, int64_t n, const char* name) {
+  chk(t, dt, name);
+  numel_eq(t, n, name);
+  TORCH_CHECK((uintptr_t)t.data_ptr() % 16 == 0, name, ": 16-byte aligned base");
+}
+void ctx_fwd(const Tensor& att, const Tensor& enc, const Tensor& ctx, const Tensor& ctxb, int64_t B, int64_t T, int64_t D,
+             int64_t A) {
+  TORCH_CHECK(ctx_bmm_ok((int)B, (int)T, (int)D, (int)A), "ctx_fwd: D <= 128, T % 8 == 0, A % 128 == 0");
+  ctx_chk(att, BF, D * B * T, "att"); ctx_chk(enc, BF, B * T * A, "enc");
+  ctx_chk(ctx, F32, D * B * A, "ctx"); ctx_chk(ctxb, BF, D * B * A, "ctxb");
+  launch_ctx_fwd(P<bf16>(att), P<bf16>(enc), P<float>(ctx), P<bf16>(ctxb), (int)B, (int)T, (int)D, (int)A, stream());
+}
+void ctx_da(const Tensor& dctx, const Tensor& enc, const Tensor& da, int64_t B, int64_t T, int64_t D, int64_t A, bool acc) {
+  TORCH_CHECK(ctx_bmm_ok((int)B, (int)T, (int)D, (int)A), "ctx_da: D <= 128, T % 8 == 0, A % 128 == 0");
+  ctx_chk(dctx, BF, D * B * A, "dctx"); ctx_chk(enc, BF, B * T * A, "enc"); ctx_chk(da, F32, D * B * T, "da");
+  launch_ctx_da(P<bf16>(dctx), P<bf16>(enc), P<float>(da), (int)B, (int)T, (int)D, (int)A, acc, stream());
+}
+void ctx_de(const Tensor& att, const Tensor& dctx, const Tensor& de, int64_t B, int64_t T, int64_t D, int64_t A) {
+  TORCH_CHECK(ctx_bmm_ok((int)B, (int)T, (int)D, (int)A), "ctx_de: D <= 128, T % 8 == 0, A % 128 == 0");
+  ctx_chk(att, BF, D * B * T, "att"); ctx_chk(dctx, BF, D * B * A, "dctx"); ctx_chk(de, F32, B * T * A, "de");
+  launch_ctx_de(P<bf16>(att), P<bf16>(dctx), P<float>(de), (int)B, (int)T, (int)D, (int)A, stream());
+}
 void wgrad_tn(const Tensor& a, const Tensor& b, const Tensor& out) {
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "wgrad_tn: 2-D views");
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && out.is_cuda(), "wgrad_tn: GPU tensors");
@@ -1143,6 +1168,10 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("ptr_loss", &ptr_loss);
   m.def("wgrad_tn", &wgrad_tn);
   m.def("wgrad_tt", &wgrad_tt);
+  m.def("ctx_bmm_ok", &ctx_bmm_ok_op);
+  m.def("ctx_fwd", &ctx_fwd);
+  m.def("ctx_da", &ctx_da);
+  m.def("ctx_de", &ctx_de);
   m.def("wgrad_tt_ws", &wgrad_tt_ws);
   m.def("pgen_dirs", &pgen_dirs);
   m.def("pack_cast", &pack_cast);

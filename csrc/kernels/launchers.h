@@ -219,3 +219,9 @@ void launch_slab_sum(const float* slab, float* out, int ldo, int M, int N, int S
 void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, long ldc, bool out_bf16, bool beta,
                     const float* bias, int M, int N, int K, int amode, const int64_t* ids, const int64_t* rev,
                     bf16* xsf, long nsrc, int B, int T, int dir, hipStream_t st);
+
+// batched attention-context GEMMs (ctx_bmm.hip)
+bool ctx_bmm_ok(int B, int T, int D, int A);
+void launch_ctx_fwd(const bf16* att, const bf16* enc, float* ctx, bf16* ctxb, int B, int T, int D, int A, hipStream_t st);
+void launch_ctx_da(const bf16* dctx, const bf16* enc, float* da, int B, int T, int D, int A, bool acc, hipStream_t st);
+void launch_ctx_de(const bf16* att, const bf16* dctx, float* de, int B, int T, int D, int A, hipStream_t st);

@@ -72,6 +72,10 @@ BLT_VDW = BLT and os.environ.get("TSAMD_BLT_VOCAB_DW", "0") == "1"
 # dW = X^T . dlogits on the library into a [H][Vp] scratch (653 -> 502 us with the copy)
 # (tools/vocab_grad_micro.py, profiles/r6/vocab_grad.md)
 VOCAB_PAD = os.environ.get("TSAMD_VOCAB_PAD", "1") != "0"
+# TSAMD_CTX_NATIVE (default 1): the three batched attention-context GEMMs (ctx = a . enc_out, its
+# gradients dA = dctx . enc_out^T and dE = a^T . dctx) on the hand-written ctx_bmm.hip kernels
+# (step-major outputs, no tr01 pass) instead of torch.bmm + tr01
+CTX_NATIVE = os.environ.get("TSAMD_CTX_NATIVE", "1") != "0"
 # K.M.N above which the vocab dW keeps the 4-way split-K batched GEMM (config #5: 8.2 ms against
 # 9.5 ms for the library at the padded N)
 VOCAB_DW_SPLIT_MIN = 1e12
@@ -634,6 +638,7 @@ class HipPointerGenerator:
             w["vstate"] = z((N + 31) // 32, dt=torch.int32)  # dlogits blocks written by the last pass 2
         # the fused head's dlogits rows: Vp columns (TSAMD_VOCAB_PAD; zero past V)
         self.Vp = -(-V // 128) * 128 if (self.fused_vocab and VOCAB_PAD) else V
+        self.ctx_native = CTX_NATIVE and self.dev.type == "cuda" and bool(self.k.ctx_bmm_ok(B, T, D, A))
         w["logits"] = z(D * B, self.Vp, dt=BF)
         if self.Vp != V and self.det:
             w["dbias_p"] = z(self.Vp)  # deterministic column sums over the padded rows
@@ -1024,6 +1029,9 @@ class HipPointerGenerator:
         # ctx_t = a_t . enc_out for every step: [B][D, T] x [B][T, A] (bf16 a -- written by the
         # attention kernel next to the fp32 a -- fp32 accumulate), then [B][D][A] -> CTX [D][B][A]
         # and its bf16 twin in one pass (tr01)
+        if self.ctx_native:
+            self.k.ctx_fwd(w["ATTb"], enc_out, w["CTX"], w["CTXb"], B, T, D, A)
+            return
         ctx = w["bd_tmp"][:B * D * A].view(B, D, A)
         torch.bmm(w["ATTb"].permute(1, 0, 2), enc_out, out_dtype=F32, out=ctx)
         self.k.tr01(ctx, w["CTX"], w["CTXb"], B, D, A, False)
@@ -1359,15 +1367,18 @@ class HipPointerGenerator:
         enc_out, lens, F, G = self.enc[-1]["out"], w["enc_lens"], w["F"], w["Genc"]
         v, wc = self.f32["v"], self.f32["wc"]
         w["DCTXb"].copy_(dCTX_dir)
-        da = w["bd_tmp"][:B * D * T].view(B, D, T)
-        torch.bmm(w["DCTXb"].permute(1, 0, 2), enc_out.transpose(1, 2), out_dtype=F32, out=da)
-        Ga = w["dA"]  # [D][B][T] (+)= da^T, one vectorised pass (tr01; T % 4 == 0)
-        if T % 4 == 0:
-            k.tr01(da, Ga, None, B, D, T, bool(hps.pointer_gen))
-        elif hps.pointer_gen:
-            Ga.add_(da.transpose(0, 1))
+        Ga = w["dA"]  # [D][B][T] (+)= da^T
+        if self.ctx_native:  # step-major straight from the kernel (accumulated with pointer_gen)
+            k.ctx_da(w["DCTXb"], enc_out, Ga, B, T, D, A, bool(hps.pointer_gen))
         else:
-            Ga.copy_(da.transpose(0, 1))
+            da = w["bd_tmp"][:B * D * T].view(B, D, T)
+            torch.bmm(w["DCTXb"].permute(1, 0, 2), enc_out.transpose(1, 2), out_dtype=F32, out=da)
+            if T % 4 == 0:  # one vectorised pass (tr01; T % 4 == 0)
+                k.tr01(da, Ga, None, B, D, T, bool(hps.pointer_gen))
+            elif hps.pointer_gen:
+                Ga.add_(da.transpose(0, 1))
+            else:
+                Ga.copy_(da.transpose(0, 1))
         w["dh_rec"].zero_()
         w["dc_carry"].zero_()
         dcov = w["dcov"]
@@ -1451,7 +1462,10 @@ class HipPointerGenerator:
         if not self.proj_attn:  # (the projected-context forward made ATTb already)
             w["ATTb"].copy_(w["ATT"])
         w["DCTXb"].copy_(w["DCTX"])
-        torch.bmm(w["ATTb"].permute(1, 2, 0), w["DCTXb"].permute(1, 0, 2), out_dtype=F32, out=dE)
+        if self.ctx_native:
+            k.ctx_de(w["ATTb"], w["DCTXb"], dE, B, T, D, A)
+        else:
+            torch.bmm(w["ATTb"].permute(1, 2, 0), w["DCTXb"].permute(1, 0, 2), out_dtype=F32, out=dE)
         dE2 = dE.view(B * T, A)
         gemm(dE2, dFb, self.pk["Wh"].t(), 1.0)
         self._dE = dE

@@ -68,9 +68,15 @@ def main():
         CTX = torch.empty(D, B, A, device=dev, dtype=F32)
         CTXb = torch.empty(D, B, A, device=dev, dtype=BF)
         dA = torch.zeros(D, B, T, device=dev, dtype=F32)
+        tr = torch.empty(B * D * max(A, T), device=dev)
+        r["ctx_bmm_tr01"] = timed(lambda: (torch.bmm(att.permute(1, 0, 2), enc, out_dtype=F32, out=ctx),
+                                           k.tr01(ctx, CTX, CTXb, B, D, A, False)))
+        r["da_bmm_tr01"] = timed(lambda: (torch.bmm(dctx.permute(1, 0, 2), enc.transpose(1, 2), out_dtype=F32, out=da),
+                                          k.tr01(da, dA, None, B, D, T, True)))
         r["ctx_native"] = timed(lambda: k.ctx_fwd(att, enc, CTX, CTXb, B, T, D, A))
         r["da_native"] = timed(lambda: k.ctx_da(dctx, enc, dA, B, T, D, A, True))
         r["dE_native"] = timed(lambda: k.ctx_de(att, dctx, dE, B, T, D, A))
+        del tr
     print(json.dumps(r), flush=True)
 
 
