@@ -210,67 +210,92 @@ __global__ __launch_bounds__(256) void ctx_da_kernel(const bf16* __restrict__ dc
     }
 }
 
-// one workgroup per (b, 128 t rows t0.., 128 columns n0..), K = D <= 128 in one stage: att rows
-// [d][t0 ..] and dctx rows [d][n0 ..] as half images (rows past D zeroed), read transposed;
-// waves 2 x 2, each 64 t x 64 n
+// one workgroup per (b, 128 t rows t0..), looping over the 128-column blocks n0 = 0, 128, .. of A:
+// K = D <= 128 in one stage.  The att rows [d][t0 ..] stay in LDS as one half image for the whole
+// loop; the dctx rows [d][n0 ..] of the next block are staged into the (single) dctx image while
+// the current block's tile is stored -- the fp32 dE output is the traffic that matters; 64 KB of
+// LDS keeps 2 workgroups per CU.  Measured (profiles/r6/ctx_bmm.md): one tile per workgroup
+// 56.3 / 2128 us (headline / config #5), this loop 58.6 / 1726, the loop with a second dctx buffer
+// (96 KB, 1 workgroup per CU) 71.6 / 2024.  Rows past D of the att image are zero, both operands
+// are read transposed; waves 2 x 2, each 64 t x 64 n.
 __global__ __launch_bounds__(256) void ctx_de_kernel(const bf16* __restrict__ att, const bf16* __restrict__ dctx,
                                                      float* __restrict__ de, int B, int T, int D, int A) {
   constexpr int IMG = 128 * 256;
-  __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG];  // att image, dctx image
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int ntt = (T + 127) / 128, ntn = A / 128, per_b = ntt * ntn;
-  const int lin = xcd_lin(), b = lin / per_b, rem = lin - b * per_b, t0 = (rem / ntn) * 128, n0 = (rem % ntn) * 128;
+  const int ntt = (T + 127) / 128, ntn = A / 128;
+  const int lin = xcd_lin(), b = lin / ntt, t0 = (lin - b * ntt) * 128;
   const unsigned sbase = lds_addr(smem);
-  // 32 pieces (4 rows x 256 B) per image, 8 of each per wave; rows past D: zeros by ds_write
+  const int np = (D + 3) / 4;  // 4-row pieces holding rows < D
+  // 32 pieces (4 rows x 256 B) per image, 8 per wave
+  auto stage_dctx = [&](int n0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int p = 8 * wid + j, row = 4 * p + (lane >> 4), ch = (lane & 15) ^ tt_sw(row);
+      if (p < np)
+        glds16_asm(dctx + ((size_t)min(row, D - 1) * B + b) * A + n0 + 8 * ch,
+                   __builtin_amdgcn_readfirstlane(sbase + IMG + p * 1024));
+    }
+  };
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int p = 8 * wid + j, row = 4 * p + (lane >> 4), ch = (lane & 15) ^ tt_sw(row);
-    if (4 * p < D) {
-      const int dr = min(row, D - 1);
-      glds16_asm(att + ((size_t)dr * B + b) * T + min(t0 + 8 * ch, T - 8),
+    if (p < np)
+      glds16_asm(att + ((size_t)min(row, D - 1) * B + b) * T + min(t0 + 8 * ch, T - 8),
                  __builtin_amdgcn_readfirstlane(sbase + p * 1024));
-      glds16_asm(dctx + ((size_t)dr * B + b) * A + n0 + 8 * ch, __builtin_amdgcn_readfirstlane(sbase + IMG + p * 1024));
-    }
   }
-  // rows D .. 127 (and a partial piece's rows past D) -> 0: plain LDS stores, after the DMA of
-  // the piece they overwrite has landed
+  stage_dctx(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int e = tid; e < 2 * 128 * 16; e += 256) {
-    const int img = e >> 11, row = (e >> 4) & 127;
-    if (row >= D) *reinterpret_cast<bf16x8*>(smem + img * IMG + row * 256 + 16 * (e & 15)) = zero8();
+  // rows D .. 127 of both images -> 0 (plain LDS stores, once).  Only the att image's must stay
+  // zero: a partial last piece (D % 4) re-lands clamped copies of row D - 1 in the dctx image,
+  // finite, so their products with the zero att rows are exact zeros.
+  if (D < 128) {
+    for (int e = tid; e < 2 * 128 * 16; e += 256) {
+      const int img = e >> 11, row = (e >> 4) & 127;
+      if (row >= D) *reinterpret_cast<bf16x8*>(smem + img * IMG + row * 256 + 16 * (e & 15)) = zero8();
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  const int wr = wid >> 1, wc = wid & 1;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-  const int nkk = (D + 31) / 32;
-  for (int kk = 0; kk < nkk; ++kk) {
-    bf16x8 fa[4], fb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = tt_frag(smem, 32 * kk, 64 * wr + 16 * i, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = tt_frag(smem + IMG, 32 * kk, 64 * wc + 16 * j, lane);
+  const int wr = wid >> 1, wc = wid & 1, nkk = (D + 31) / 32;
+  for (int nb = 0; nb < ntn; ++nb) {
+    f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
-  }
-  const int nl = n0 + 64 * wc + (lane & 15);
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+    for (int kk = 0; kk < nkk; ++kk) {
+      bf16x8 fa[4], fb[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) fa[i] = tt_frag(smem, 32 * kk, 64 * wr + 16 * i, lane);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = t0 + 64 * wr + 16 * i + 4 * (lane >> 4) + r;
-      if (t < T) {
-        float* o = de + ((size_t)b * T + t) * A + nl;
+      for (int j = 0; j < 4; ++j) fb[j] = tt_frag(smem + IMG, 32 * kk, 64 * wc + 16 * j, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[16 * j] = acc[i][j][r];
-      }
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
     }
+    if (nb + 1 < ntn) {  // every wave's reads of this dctx image done -> stage the next block
+      __syncthreads();
+      stage_dctx((nb + 1) * 128);
+    }
+    const int nl = nb * 128 + 64 * wc + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = t0 + 64 * wr + 16 * i + 4 * (lane >> 4) + r;
+        if (t < T) {
+          float* o = de + ((size_t)b * T + t) * A + nl;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[16 * j] = acc[i][j][r];
+        }
+      }
+    if (nb + 1 < ntn) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next block's dctx has landed
+      __syncthreads();
+    }
+  }
 }
 
 bool ctx_bmm_ok(int B, int T, int D, int A) {
@@ -287,5 +312,5 @@ void launch_ctx_da(const bf16* dctx, const bf16* enc, float* da, int B, int T, i
 }
 
 void launch_ctx_de(const bf16* att, const bf16* dctx, float* de, int B, int T, int D, int A, hipStream_t st) {
-  hipLaunchKernelGGL(ctx_de_kernel, dim3(B * ((T + 127) / 128) * (A / 128)), dim3(256), 0, st, att, dctx, de, B, T, D, A);
+  hipLaunchKernelGGL(ctx_de_kernel, dim3(B * ((T + 127) / 128)), dim3(256), 0, st, att, dctx, de, B, T, D, A);
 }
