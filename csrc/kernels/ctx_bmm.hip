@@ -25,6 +25,7 @@
 #include "common.h"
 #include "launchers.h"
 #include "lds_frag.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -137,34 +138,43 @@ __global__ __launch_bounds__(256) void ctx_fwd_kernel(const bf16* __restrict__ a
     }
 }
 
-// one workgroup per (b, 128 t columns t0..): the dctx rows of b and the enc rows t0.. as K-major
-// images, K = A in steps of 64 (A % 64 == 0); wave w owns t columns t0 + 32 w .. + 31
-__global__ __launch_bounds__(256) void ctx_da_kernel(const bf16* __restrict__ dctx, const bf16* __restrict__ enc,
-                                                     float* __restrict__ da, int B, int T, int D, int A, int acc_out) {
-  constexpr int IMG = 128 * 128, STAGE = 2 * IMG;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+// one workgroup of NW waves per (b, 32 NW t columns t0..): the dctx rows of b and the enc rows t0..
+// as K-major images, K = A in steps of 64 (A % 64 == 0); wave w owns t columns t0 + 32 w .. + 31.
+// NW = 8 halves the L2 re-reads of the dctx rows (one image per 256 t instead of per 128).
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void ctx_da_kernel(const bf16* __restrict__ dctx, const bf16* __restrict__ enc,
+                                                         float* __restrict__ da, int B, int T, int D, int A,
+                                                         int acc_out) {
+  constexpr int DI = 128 * 128, EI = 32 * NW * 128, STAGE = DI + EI, DPW = 16 / NW;  // dctx pieces per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int ntn = (T + 127) / 128, lin = xcd_lin(), b = lin / ntn, t0 = (lin - b * ntn) * 128;
+  const int TT = 32 * NW, ntn = (T + TT - 1) / TT, lin = xcd_lin(), b = lin / ntn, t0 = (lin - b * ntn) * TT;
   const int mt = (D + 15) >> 4, nk = A / 64;
-  const bf16* dsrc[4];
+  const bf16* dsrc[DPW];
   const bf16* esrc[4];
-  bool don[4], eon[4];
+  bool don[DPW], eon[4];
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) {
+    const int p = DPW * wid + j, row = 8 * p + (lane >> 3), c = (lane & 7) ^ km_sw(row);
+    don[j] = 8 * p < D;
+    dsrc[j] = dctx + ((size_t)min(row, D - 1) * B + b) * A + 8 * c;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int p = 4 * wid + j, row = 8 * p + (lane >> 3), c = (lane & 7) ^ km_sw(row);
-    don[j] = 8 * p < D;
     eon[j] = t0 + 8 * p < T;
-    dsrc[j] = dctx + ((size_t)min(row, D - 1) * B + b) * A + 8 * c;
     esrc[j] = enc + ((size_t)b * T + min(t0 + row, T - 1)) * A + 8 * c;
   }
   const unsigned sbase = lds_addr(smem);
   auto stage = [&](int buf, int kt) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int p = 4 * wid + j;
-      if (don[j]) glds16_asm(dsrc[j] + kt * 64, __builtin_amdgcn_readfirstlane(sbase + buf * STAGE + p * 1024));
-      if (eon[j]) glds16_asm(esrc[j] + kt * 64, __builtin_amdgcn_readfirstlane(sbase + buf * STAGE + IMG + p * 1024));
-    }
+    for (int j = 0; j < DPW; ++j)
+      if (don[j])
+        glds16_asm(dsrc[j] + kt * 64, __builtin_amdgcn_readfirstlane(sbase + buf * STAGE + (DPW * wid + j) * 1024));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (eon[j])
+        glds16_asm(esrc[j] + kt * 64, __builtin_amdgcn_readfirstlane(sbase + buf * STAGE + DI + (4 * wid + j) * 1024));
   };
   const bool live = t0 + 32 * wid < T;  // (uniform) this wave has columns before T
   f32x4 acc[CB_MT][2];
@@ -177,7 +187,7 @@ __global__ __launch_bounds__(256) void ctx_da_kernel(const bf16* __restrict__ dc
     const int buf = kt & 1;
     if (kt + 1 < nk) stage(buf ^ 1, kt + 1);
     const char* Di = smem + buf * STAGE;
-    const char* Ei = Di + IMG;
+    const char* Ei = Di + DI;
     if (live) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -308,7 +318,20 @@ void launch_ctx_fwd(const bf16* att, const bf16* enc, float* ctx, bf16* ctxb, in
 }
 
 void launch_ctx_da(const bf16* dctx, const bf16* enc, float* da, int B, int T, int D, int A, bool acc, hipStream_t st) {
-  hipLaunchKernelGGL(ctx_da_kernel, dim3(B * ((T + 127) / 128)), dim3(256), 0, st, dctx, enc, da, B, T, D, A, (int)acc);
+  static const int nw_env = [] {
+    const char* e = getenv("TSAMD_CTX_DA_NW");
+    return e ? atoi(e) : 0;
+  }();
+  const int nw = nw_env == 4 || nw_env == 8 ? nw_env : 8;
+  const int lds = 2 * (128 * 128 + 32 * nw * 128);
+  if (nw == 8) {
+    (void)hipFuncSetAttribute((const void*)ctx_da_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(ctx_da_kernel<8>, dim3(B * ((T + 255) / 256)), dim3(512), lds, st, dctx, enc, da, B, T, D, A,
+                       (int)acc);
+  } else {
+    hipLaunchKernelGGL(ctx_da_kernel<4>, dim3(B * ((T + 127) / 128)), dim3(256), lds, st, dctx, enc, da, B, T, D, A,
+                       (int)acc);
+  }
 }
 
 void launch_ctx_de(const bf16* att, const bf16* dctx, float* de, int B, int T, int D, int A, hipStream_t st) {
