@@ -16,7 +16,10 @@
 //   1 contiguous src and dst: 2048 elements per block, 8 per thread (two 16-byte loads, one
 //     16-byte bf16 store);
 //   2 transpose: dst [d1][d2] contiguous, src its transpose view of a contiguous [d2][d1]
-//     matrix (strides (1, d1)): 64 x 64 tiles through LDS, both sides coalesced.
+//     matrix (strides (1, d1)): 64 x 64 tiles through LDS, both sides coalesced;
+//   3 row-strided 2-D copy (unit column strides, d2 % 8 == 0, 16-byte aligned rows): kind 1's
+//     8 per thread with a row stride on either side -- the vocab W into its 128-aligned [H][Vp]
+//     image (as kind 0 it took the repack from 50 to 85 us).
 // Round 3's single element-per-thread kernel spent 194 us per step on the 32M-element repack
 // (the 12.8M-element vocab W^T transpose and two plain 6.4M / 12.8M copies dominate).
 __global__ __launch_bounds__(256) void pack_cast_kernel(const long* __restrict__ jobs, int nj, long total) {
@@ -81,6 +84,28 @@ __global__ __launch_bounds__(256) void pack_cast_kernel(const long* __restrict__
         if (f32o) reinterpret_cast<float*>(J[1])[i * C + c] = v;
         else reinterpret_cast<bf16*>(J[1])[i * C + c] = f2bf(v);
       }
+    }
+    return;
+  }
+  if (kind == 3) {  // 2-D [R][C] with row strides J[6] (src) / J[9] (dst), C % 8 == 0: 8 per thread
+    const long e0 = jb * 2048 + (long)threadIdx.x * 8;
+    if (e0 >= n) return;
+    const long C = J[4], r = e0 / C, c = e0 - r * C;
+    const float* sp = src + r * J[6] + c;
+    float4 a = *reinterpret_cast<const float4*>(sp);
+    float4 b = *reinterpret_cast<const float4*>(sp + 4);
+    a.x *= sc; a.y *= sc; a.z *= sc; a.w *= sc;
+    b.x *= sc; b.y *= sc; b.z *= sc; b.w *= sc;
+    const long o = r * J[9] + c;
+    if (f32o) {
+      float* d = reinterpret_cast<float*>(J[1]) + o;
+      *reinterpret_cast<float4*>(d) = a;
+      *reinterpret_cast<float4*>(d + 4) = b;
+    } else {
+      bf16x8 v;
+      v[0] = f2bf(a.x); v[1] = f2bf(a.y); v[2] = f2bf(a.z); v[3] = f2bf(a.w);
+      v[4] = f2bf(b.x); v[5] = f2bf(b.y); v[6] = f2bf(b.z); v[7] = f2bf(b.w);
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(J[1]) + o) = v;
     }
     return;
   }

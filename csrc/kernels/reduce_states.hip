@@ -82,6 +82,11 @@ __global__ __launch_bounds__(256) void rs_fwd_kernel(
 
 // grid (ceil(B/16), 2): one workgroup per (16-row tile, problem); wave w computes column
 // tiles w, w + 4, ... of d_old = dp . W^T (K = H), dp built on the fly from g and pre.
+// grid (row tiles of 16, 2 problems, H / 32 column groups): each workgroup recomputes its 16 dp
+// rows (16 x H, cheap) and its 4 waves each own one 16-column tile of d_old (2H / 16 tiles over
+// the H / 32 groups), the W rows' fragments loaded up front -- 256 workgroups at B = 256 instead
+// of 32 with 8 dependent tiles per wave (85 -> see profiles/r6/rs_bwd.md).  Group 0 alone writes
+// the bf16 dp rows and the bias-gradient atomics.
 __global__ __launch_bounds__(256) void rs_bwd_kernel(
     const float* __restrict__ gc, const float* __restrict__ gh,        // dL/dc0, dL/dh0 [B][H]
     const float* __restrict__ pre_c, const float* __restrict__ pre_h,  // [B][H]
@@ -91,7 +96,7 @@ __global__ __launch_bounds__(256) void rs_bwd_kernel(
     float* __restrict__ dold_c, float* __restrict__ dold_h, size_t dstride,  // fw rows [B][H]; bw at +dstride
     int B, int H) {
   __shared__ __attribute__((aligned(16))) bf16 Ds[16][512 + 8];  // dp rows of the tile (H <= 512)
-  const int prob = blockIdx.y;
+  const int prob = blockIdx.y, grp = blockIdx.z;
   const float* g = prob ? gh : gc;
   const float* pre = prob ? pre_h : pre_c;
   const bf16* R = prob ? RH : RC;
@@ -100,7 +105,14 @@ __global__ __launch_bounds__(256) void rs_bwd_kernel(
   float* dold = prob ? dold_h : dold_c;
   const int r0 = blockIdx.x * 16;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // dp tile -> LDS (and the bf16 dp rows), bias-gradient column partials
+  // this wave's d_old column tile and its W rows' fragments, loaded before the dp pass
+  const int kof = 8 * (lane >> 4), j0 = (4 * grp + wid) * 16;
+  const bf16* brow = R + (size_t)(j0 + (lane & 15)) * H + kof;
+  bf16x8 bw[16];
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk)
+    if (32 * kk < H) bw[kk] = ld8(brow + 32 * kk);
+  // dp tile -> LDS (and, group 0, the bf16 dp rows and the bias-gradient column partials)
   for (int col = threadIdx.x; col < H; col += 256) {
     float cs = 0.f;
     for (int rr = 0; rr < 16; ++rr) {
@@ -109,28 +121,24 @@ __global__ __launch_bounds__(256) void rs_bwd_kernel(
       if (r < B) {
         const size_t ix = (size_t)r * H + col;
         v = pre[ix] > 0.f ? g[ix] : 0.f;
-        dpo[ix] = f2bf(v);
+        if (grp == 0) dpo[ix] = f2bf(v);
       }
       cs += v;
       Ds[rr][col] = f2bf(v);
     }
-    if (gb) atomicAdd(gb + col, cs);
+    if (gb && grp == 0) atomicAdd(gb + col, cs);
   }
   __syncthreads();
   // d_old[r][j] = sum_u dp[r][u] R[j][u], j < 2H: MFMA A = dp rows (LDS), B = R rows
-  const int kof = 8 * (lane >> 4);
-  for (int jt = wid; jt < 2 * H / 16; jt += 4) {
-    const int j0 = jt * 16;
-    const bf16* brow = R + (size_t)(j0 + (lane & 15)) * H + kof;
-    f32x4 acc = f32x4{0, 0, 0, 0};
-    for (int k = 0; k < H; k += 32)
-      acc = mfma16(*reinterpret_cast<const bf16x8*>(&Ds[lane & 15][k + kof]), ld8(brow + k), acc);
-    const int j = j0 + (lane & 15), d = j >= H;
+  f32x4 acc = f32x4{0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = r0 + (lane >> 4) * 4 + i;
-      if (r < B) dold[d * dstride + (size_t)r * H + (j - d * H)] = acc[i];
-    }
+  for (int kk = 0; kk < 16; ++kk)
+    if (32 * kk < H) acc = mfma16(*reinterpret_cast<const bf16x8*>(&Ds[lane & 15][32 * kk + kof]), bw[kk], acc);
+  const int j = j0 + (lane & 15), d = j >= H;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + (lane >> 4) * 4 + i;
+    if (r < B) dold[d * dstride + (size_t)r * H + (j - d * H)] = acc[i];
   }
 }
 
@@ -144,6 +152,6 @@ void launch_rs_fwd(const float* c_fw, const bf16* h_fw, size_t dstride, const bf
 void launch_rs_bwd(const float* gc, const float* gh, const float* pre_c, const float* pre_h, const bf16* RC,
                    const bf16* RH, bf16* dpc, bf16* dph, float* gbc, float* gbh, float* dold_c, float* dold_h,
                    size_t dstride, int B, int H, hipStream_t st) {
-  hipLaunchKernelGGL(rs_bwd_kernel, dim3((B + 15) / 16, 2), dim3(256), 0, st, gc, gh, pre_c, pre_h, RC, RH, dpc, dph,
-                     gbc, gbh, dold_c, dold_h, dstride, B, H);
+  hipLaunchKernelGGL(rs_bwd_kernel, dim3((B + 15) / 16, 2, H / 32), dim3(256), 0, st, gc, gh, pre_c, pre_h, RC, RH, dpc,
+                     dph, gbc, gbh, dold_c, dold_h, dstride, B, H);
 }

@@ -221,7 +221,7 @@ def test_skip_pad_steps_same_loss_and_gradients(monkeypatch, coverage, pointer_g
 @pytest.mark.parametrize("layers,H,V", [(1, 256, 2000), (2, 128, 2000), (1, 256, 50000)])
 def test_fast_pack_matches_torch_pack(layers, H, V):
     """pack() after the first call = one pack_cast launch over the job table (pack.hip: contiguous
-    copies, 64 x 64 transposes, generic strided jobs): every bf16 / fp32 layout bit-identical to
+    copies, 64 x 64 transposes, row-strided copies, generic strided jobs): every bf16 / fp32 layout bit-identical to
     the torch cast / transpose / cat path (V = 50k: the bench's 12.8M-element vocab transpose)."""
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
     hps = HParams(batch_size=16, max_enc_steps=32, max_dec_steps=6, vocab_size=V, emb_dim=128, hidden_dim=H,
@@ -231,6 +231,9 @@ def test_fast_pack_matches_torch_pack(layers, H, V):
     assert eng._pack_jobs is not None
     kinds = eng._pack_jobs[:, 12].tolist()
     assert 1 in kinds and 2 in kinds and 0 in kinds, kinds
+    if eng.Vp != V:  # the vocab W into its 128-aligned [H][Vp] image: the row-strided kind
+        assert 3 in kinds, kinds
+        assert float(eng.pk["owP"][:, V:].abs().max()) == 0.0
     params.flat.add_(torch.randn_like(params.flat) * 0.01)  # new master weights
     eng.pack()  # fast path
     torch.cuda.synchronize()

@@ -756,6 +756,10 @@ class HipPointerGenerator:
             elif (dst.dim() == 2 and dst.is_contiguous() and src.stride() == (1, src.shape[0])):
                 R, C = dst.shape  # src = the transpose view of a contiguous [C][R] matrix
                 kind, nblk = 2, -(-R // 64) * -(-C // 64)
+            elif (dst.dim() == 2 and dst.stride(1) == 1 and src.stride(1) == 1 and dst.shape[1] % 8 == 0
+                  and dst.stride(0) % 8 == 0 and src.stride(0) % 4 == 0 and src.data_ptr() % 16 == 0
+                  and dst.data_ptr() % 16 == 0):
+                kind, nblk = 3, -(-n // 2048)  # row-strided rows (e.g. the [H][Vp] padded W): 8 per thread
             else:
                 kind, nblk = 0, -(-n // 256)
             sc = int(np.array(scale[0], dtype=np.float32).view(np.int32)) if scale else 0  # fp32 bits, 0 = 1.0
