@@ -1119,8 +1119,12 @@ void pgen_bwd(const Tensor& ctx, const Tensor& c, const Tensor& h, const Tensor&
   chk(gw, F32, "gw");
   numel_eq(ctx, N * A, "ctx"); numel_eq(c, N * H, "c"); numel_eq(h, N * H, "h"); numel_eq(x, N * E, "x");
   numel_eq(dpre, N, "dpre"); numel_eq(gw, A + 2 * H + E, "gw");
-  launch_pgen_bwd(P<float>(ctx), P<float>(c), P<bf16>(h), P<float>(x), P<float>(dpre), P<float>(gw), N, A, H, E,
-                  det, stream());
+  (void)det;  // (the split sums are added in a fixed order in every mode)
+  const int64_t Kt = A + 2 * H + E, S = pgen_bwd_splits((int)N, (int)A, (int)H, (int)E);
+  auto part = at::empty({S, Kt}, gw.options());
+  auto cpart = at::empty({(int64_t)colsum_det_chunks((int)S, (int)Kt), Kt}, gw.options());
+  launch_pgen_bwd(P<float>(ctx), P<float>(c), P<bf16>(h), P<float>(x), P<float>(dpre), P<float>(gw), P<float>(part),
+                  P<float>(cpart), N, A, H, E, stream());
 }
 
 // gb (+)= sum(dpre) with atomics: pass the zeroed p_gen bias-gradient slot (or None: the caller sums)

@@ -16,6 +16,7 @@
 // Every kernel: one block = 4 waves on a 16x16 output tile (x 4 gates for the cell),
 // K split across the waves (kslice_mma) and summed in LDS (ksplit_reduce).
 #include "common.h"
+#include "launchers.h"
 #include <stdlib.h>
 
 // XCD-aware tile order for the (column tile, row tile) grids below.  Blocks are dealt to
@@ -219,28 +220,33 @@ __global__ __launch_bounds__(256) void pgen_kernel(const float* __restrict__ ctx
 // grid (ceil(Ktot/256), nsplit): each thread owns one column (coalesced row reads),
 // loops its row chunk, then one atomicAdd.  Replaces four fp32 GEMVs (transposed
 // large-N GEMV is a slow path in the BLAS library).  gw must be zeroed by the caller.
+// p_gen weight gradient, stage 1: column k's partial sum over rows [n0, n0 + rows_per) of split
+// blockIdx.y into part[split][k] (4 independent accumulators); stage 2 (colsum_det) adds the
+// splits in a fixed order.  The round-5 form added every split's partial into gw with an atomic:
+// 400 adds per column address serialised at the memory side (45 us at N = 25600); deterministic
+// now in every mode.
 __global__ __launch_bounds__(256) void pgen_bwd_kernel(const float* __restrict__ ctx, const float* __restrict__ c,
                                                        const bf16* __restrict__ h, const float* __restrict__ x,
-                                                       const float* __restrict__ dpre, float* __restrict__ gw,
+                                                       const float* __restrict__ dpre, float* __restrict__ part,
                                                        int N, int A, int H, int E, int rows_per) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   const int Kt = A + 2 * H + E;
   if (k >= Kt) return;
   const int n0 = blockIdx.y * rows_per, n1 = min(N, n0 + rows_per);
-  float acc = 0.f;
-  if (k < A) {
-    for (int n = n0; n < n1; ++n) acc += dpre[n] * ctx[(size_t)n * A + k];
-  } else if (k < A + H) {
-    const int kk = k - A;
-    for (int n = n0; n < n1; ++n) acc += dpre[n] * c[(size_t)n * H + kk];
-  } else if (k < A + 2 * H) {
-    const int kk = k - A - H;
-    for (int n = n0; n < n1; ++n) acc += dpre[n] * bf2f(h[(size_t)n * H + kk]);
-  } else {
-    const int kk = k - A - 2 * H;
-    for (int n = n0; n < n1; ++n) acc += dpre[n] * x[(size_t)n * E + kk];
-  }
-  atomicAdd(gw + k, acc);
+  float a4[4] = {0.f, 0.f, 0.f, 0.f};
+  auto sweep = [&](auto ld) {
+    int n = n0;
+    for (; n + 4 <= n1; n += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a4[u] += dpre[n + u] * ld(n + u);
+    }
+    for (; n < n1; ++n) a4[0] += dpre[n] * ld(n);
+  };
+  if (k < A) sweep([&](int n) { return ctx[(size_t)n * A + k]; });
+  else if (k < A + H) sweep([&](int n) { return c[(size_t)n * H + (k - A)]; });
+  else if (k < A + 2 * H) sweep([&](int n) { return bf2f(h[(size_t)n * H + (k - A - H)]); });
+  else sweep([&](int n) { return x[(size_t)n * E + (k - A - 2 * H)]; });
+  part[(size_t)blockIdx.y * Kt + k] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
 }
 
 // p_gen gradient into the decoder inputs, all D*B rows in one launch (the hoisted per-step
@@ -455,14 +461,20 @@ void launch_dec_sproj(const bf16* cb, const bf16* hb, const bf16* WsT, const flo
   p.step = step;
   L2_LAUNCH(linear2_kernel, H + H, grid, st, p, B);
 }
+int pgen_bwd_splits(int N, int A, int H, int E) {
+  const int cols = (A + 2 * H + E + 255) / 256;
+  return max(1, min((N + 63) / 64, 2048 / cols));
+}
+// part: [pgen_bwd_splits][Kt] fp32, cpart: [colsum_det_chunks(splits, Kt)][Kt] fp32 (workspaces)
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
-                     int N, int A, int H, int E, bool det, hipStream_t st) {
+                     float* part, float* cpart, int N, int A, int H, int E, hipStream_t st) {
   const int Kt = A + 2 * H + E;
   const int cols = (Kt + 255) / 256;
-  const int nsplit = det ? 1 : max(1, min((N + 63) / 64, 2048 / cols));
+  const int nsplit = pgen_bwd_splits(N, A, H, E);
   const int rows_per = (N + nsplit - 1) / nsplit;
-  hipLaunchKernelGGL(pgen_bwd_kernel, dim3(cols, nsplit), dim3(256), 0, st, ctx, c, h, x, dpre, gw, N, A, H, E,
+  hipLaunchKernelGGL(pgen_bwd_kernel, dim3(cols, nsplit), dim3(256), 0, st, ctx, c, h, x, dpre, part, N, A, H, E,
                      rows_per);
+  launch_colsum_det(part, false, cpart, gw, nsplit, Kt, true, st);
 }
 void launch_pgen_dirs(const float* dpre, const float* w, float* dctx, float* dc, float* dh, float* dx, float* gb,
                       int N, int A, int H, int E, hipStream_t st) {

@@ -100,8 +100,9 @@ void launch_linear2_pair(const bf16* a1, int K1, const bf16* a2, int K2, const b
                          int M, int B, hipStream_t st);
 void launch_pgen(const float* ctx, const float* c, const bf16* h, const float* x, const float* w, const float* b,
                  float* pg, int R, int A, int H, int E, hipStream_t st);
+int pgen_bwd_splits(int N, int A, int H, int E);
 void launch_pgen_bwd(const float* ctx, const float* c, const bf16* h, const float* x, const float* dpre, float* gw,
-                     int N, int A, int H, int E, bool det, hipStream_t st);
+                     float* part, float* cpart, int N, int A, int H, int E, hipStream_t st);
 int lstm_persistent_grid(int H, int B);
 int lstm_persistent_capacity(int H);
 int lstm_persistent_launches(int H, int B);
