@@ -883,6 +883,9 @@ void vocab_topk_pg(const Tensor& X, const Tensor& WT, const Tensor& bias, const 
 }
 int64_t vocab_topk_parts(int64_t V, int64_t H) { return vocab_topk_tiles((int)V, (int)H); }
 // attribution: per-phase s_memtime stamps of the decode select kernel into buf ([R][16] int64), or off
+void lstm_bwd_stamps(const OT& buf) {
+  set_lstm_bwd_stamps(buf.has_value() && buf->defined() ? (unsigned long long*)buf->data_ptr() : nullptr);
+}
 void vocab_select_stamps(const OT& buf) {
   set_vocab_select_stamps(buf.has_value() && buf->defined() ? (unsigned long long*)buf->data_ptr() : nullptr);
 }
@@ -1222,6 +1225,7 @@ TORCH_LIBRARY(tsamd, m) {
   m.def("vocab_span_probe", &vocab_span_probe);
   m.def("attn_fwd_row_probe", &attn_fwd_row_probe);
   m.def("vocab_select_stamps", &vocab_select_stamps);
+  m.def("lstm_bwd_stamps", &lstm_bwd_stamps);
   m.def("vocab_topk_beam", &vocab_topk_beam);
   m.def("dec_cell_fwd_beam", &dec_cell_fwd_beam);
   m.def("beam_sproj_xmerge", &beam_sproj_xmerge);

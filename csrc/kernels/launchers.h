@@ -226,3 +226,6 @@ bool ctx_bmm_ok(int B, int T, int D, int A);
 void launch_ctx_fwd(const bf16* att, const bf16* enc, float* ctx, bf16* ctxb, int B, int T, int D, int A, hipStream_t st);
 void launch_ctx_da(const bf16* dctx, const bf16* enc, float* da, int B, int T, int D, int A, bool acc, hipStream_t st);
 void launch_ctx_de(const bf16* att, const bf16* dctx, float* de, int B, int T, int D, int A, hipStream_t st);
+
+// attribution: per-phase s_memtime sums of the 32-row H = 512 BPTT (nullptr: off)
+void set_lstm_bwd_stamps(unsigned long long* buf);

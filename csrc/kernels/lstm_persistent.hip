@@ -656,6 +656,22 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
         cpv[i] = cs[((size_t)d * (T + 1) + s) * BH + ri];
       }
     }
+    // dz rows of step `step` -> global from the LDS copy (own-lane values), issued after this step's
+    // hand-off stores (as in the forward: the granules must not queue behind the activation
+    // traffic).  Deferring them to the next step's polls with LDS-only barriers measured slower:
+    // H = 256, B = 256: 4.57 vs 3.67 us per step (profiles/r6/lstm_bptt.md)
+    auto store_dz = [&](int step) {
+#pragma unroll
+      for (int i = 0; i < RPL; ++i)
+        if (rok[i]) {
+          bf16* dzr = dz + (((size_t)d * T + step) * B + rc[i]) * G4;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if constexpr (NT) st_b(dzr + g * H + u, Ash[swz<256>(row0 + i, g * 64 + ul)], true);
+            else dzr[g * H + u] = Ash[swz<256>(row0 + i, g * 64 + ul)];
+          }
+        }
+    };
     // ---- recurrent dh for this lane's rows: own partial (LDS) + the peers' (granules)
     float rec[RPL];
 #pragma unroll
@@ -734,22 +750,8 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) Ash[swz<256>(row, g * 64 + ul)] = f2bf(dzv[g]);
     }
-    // dz rows -> global from the LDS copy, issued after this step's hand-off stores (as in the
-    // forward: the granules must not queue behind the activation traffic)
-    auto store_dz = [&]() {
-#pragma unroll
-      for (int i = 0; i < RPL; ++i)
-        if (rok[i]) {
-          bf16* dzr = dz + (((size_t)d * T + s) * B + rc[i]) * G4;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            if constexpr (NT) st_b(dzr + g * H + u, Ash[swz<256>(row0 + i, g * 64 + ul)], true);
-            else dzr[g * H + u] = Ash[swz<256>(row0 + i, g * 64 + ul)];
-          }
-        }
-    };
     if (s == 0) {
-      store_dz();  // own-lane LDS values: no barrier needed
+      store_dz(0);  // own-lane LDS values: no barrier needed
       break;
     }
     __syncthreads();  // dz slice complete in LDS (and every lane has read Pown)
@@ -780,7 +782,7 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
                         __float_as_uint(acc[t][r]));
     }
     }
-    store_dz();
+    store_dz(s);
     __syncthreads();  // Pown visible before the next step reads it; Ash free for rewriting
   }
 #pragma unroll
@@ -816,8 +818,22 @@ __device__ __forceinline__ const gu64* gboff(const gu64* p, unsigned bytes) {
   return reinterpret_cast<const gu64*>(reinterpret_cast<const __attribute__((address_space(1))) char*>(p) + bytes);
 }
 
-// PC: peers polled per chunk (4: 8 registers spill); SL: s_sleep between poll passes
-template <bool NT, int PC = 2, int SL = 96, bool DBF = false>
+// attribution builds (tools/lstm_bptt_stamps.py): thread 0 of every workgroup sums s_memtime
+// deltas per step phase over the recurrence and stores the 8 sums at lb_stamps[(team NC + c) 8]
+// (a buffer only the tool reads; STAMP = false compiles none of it)
+__device__ unsigned long long* lb_stamps = nullptr;
+static bool lb_stamps_on = false;
+void set_lstm_bwd_stamps(unsigned long long* buf) {
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(lb_stamps), &buf, sizeof(buf));
+  lb_stamps_on = buf != nullptr;
+}
+
+// PC: peers polled per chunk (4: 8 registers spill); SL: s_sleep between poll passes.
+// Measured and not kept (profiles/r6/lstm_bptt.md): the step's dz stores issued after the NEXT
+// step's hand-off poll with LDS-only barriers -- the stamps moved 1.7k of the 7.4k "dz stores +
+// barrier 2" cycles, the BPTT micro -2.5 % at batch 2048, config #5 per step unchanged
+// (356.3 / 356.9 vs 357.0 / 356.2 ms).
+template <bool NT, int PC = 2, int SL = 96, bool DBF = false, bool STAMP = false>
 __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
@@ -862,7 +878,21 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
   gu64* xb = xbuf + (size_t)team * TEAMX;  // [parity][dest][src][32][64]
   bool dead = false;
   float bacc[4] = {0.f, 0.f, 0.f, 0.f};
+  // STAMP: phase sums (0 loads issued, 1 hand-off wait, 2 cell backward, 3 barrier 1, 4 MFMA,
+  // 5 publish, 6 dz stores + barrier 2, 7 steps)
+  unsigned long long st_last = 0;
+  unsigned st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  auto stamp = [&](int ph) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) st_sum[ph] += (unsigned)(t - st_last);
+      st_last = t;
+    }
+  };
   for (int s = T - 1; s >= 0; --s) {
+    stamp(-1);
+    if constexpr (STAMP) st_sum[7] += 1;
     int row0v = row0;
     asm volatile("" : "+v"(row0v));
     // uniform step bases + 32-bit per-lane byte offsets (saddr addressing: no 64-bit address
@@ -892,9 +922,21 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
       a4[i][0] = q[0]; a4[i][1] = q[1]; a4[i][2] = q[2]; a4[i][3] = q[3];
       cpv[i] = ld_f(boff(cs_s, ri * 4u), NT);
     }
+    auto store_dz = [&](int step) {
+#pragma unroll
+      for (int i = 0; i < RPL; ++i)
+        if (rok[i]) {
+          bf16* dz_s = dz + ((size_t)d * T + step) * B * G4;
+          const int sb = swz<256>(row0 + i, ul);
+          const unsigned o = (rio[i] + (unsigned)(rc[i] * 3 * H)) * 2u;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) st_b(boff(dz_s, o + g * H * 2u), Ash[sb + g * 64], NT);
+        }
+    };
     float rec[RPL];
 #pragma unroll
     for (int i = 0; i < RPL; ++i) rec[i] = 0.f;
+    stamp(0);
     if (s + 1 < T) {
 #pragma unroll
       for (int i = 0; i < RPL; ++i) rec[i] = Pown[(row0 + i) * 64 + ul];
@@ -937,6 +979,7 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
             if (p0 + q != c) rec[i] += ((ready >> (q * RPL + i)) & 1) ? __uint_as_float((unsigned)x[q][i]) : 0.f;
       }
     }
+    stamp(1);
     // ---- cell backward -> dz (4 gates) for (the lane's rows, unit u)
 #pragma unroll
     for (int i = 0; i < RPL; ++i) {
@@ -962,22 +1005,14 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) Ash[sb + g * 64] = f2bf(dzv[g]);
     }
-    auto store_dz = [&]() {
-#pragma unroll
-      for (int i = 0; i < RPL; ++i)
-        if (rok[i]) {
-          bf16* dz_s = dz + ((size_t)d * T + s) * B * G4;
-          const int sb = swz<256>(row0 + i, ul);
-          const unsigned o = (rio[i] + (unsigned)(rc[i] * 3 * H)) * 2u;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) st_b(boff(dz_s, o + g * H * 2u), Ash[sb + g * 64], NT);
-        }
-    };
+    if constexpr (STAMP) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (stamp after the LDS writes)
+    stamp(2);
     if (s == 0) {
-      store_dz();
+      store_dz(0);
       break;
     }
     __syncthreads();  // dz slice complete in LDS (and every lane has read Pown)
+    stamp(3);
     // ---- partial dh over this slice's gate columns, output units 32 wid .. +31, all 32 rows
     f32x4 acc[2][2];
 #pragma unroll
@@ -994,6 +1029,11 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
         acc[rt][1] = mfma16(a, w1, acc[rt][1]);
       }
     }
+    if constexpr (STAMP) {  // (stamp once the accumulators are final)
+      float sink = acc[0][0][0] + acc[1][1][3];
+      asm volatile("" : "+v"(sink));
+    }
+    stamp(4);
     // ---- publish: units 32 wid .. +31 are units (wid & 1) * 32 .. +31 of slice wid / 2
     const int dw = wid >> 1, ub = (wid & 1) * 32 + (lane & 15);
     if (dw == c) {
@@ -1016,8 +1056,16 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
             store_granule(gboff(dst, lo + (unsigned)((rt * 16 + r) * 64 + 16 * t) * 8u), (unsigned)(T - s),
                           __float_as_uint(acc[rt][t][r]));
     }
-    store_dz();
+    stamp(5);
+    store_dz(s);
     __syncthreads();  // Pown visible before the next step reads it; Ash free for rewriting
+    stamp(6);
+  }
+  if constexpr (STAMP) {
+    if (threadIdx.x == 0 && lb_stamps) {
+#pragma unroll
+      for (int ph = 0; ph < 8; ++ph) lb_stamps[((size_t)team * NC + c) * 8 + ph] = st_sum[ph];
+    }
   }
 #pragma unroll
   for (int i = 0; i < RPL; ++i)
@@ -1191,25 +1239,28 @@ void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, con
   for (int t0 = 0; t0 < ntile; t0 += nl) {
     const int n = min(nl, ntile - t0), grid = 8 * NC * ((2 * n + 7) / 8);
     if (R == 32) {
-#define LB32(PC, SL, DB) hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false, PC, SL, DB>), dim3(grid), dim3(1024), 0, st, \
-                                            dz, Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+#define LB32(PC, SL, DB, STP) hipLaunchKernelGGL((lstm_bwd_persistent32_kernel<false, PC, SL, DB, STP>), dim3(grid), \
+                                                 dim3(1024), 0, st, dz, Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, \
+                                                 dbias, T, B, ntile, t0, n)
       // poll 2 peers per pass, s_sleep(96): profiles/r4/ab/bptt32.md
-      if (dout_bf) LB32(2, 96, true);
-      else LB32(2, 96, false);
+      if (lb_stamps_on) {
+        if (dout_bf) LB32(2, 96, true, true);
+        else LB32(2, 96, false, true);
+      } else if (dout_bf) LB32(2, 96, true, false);
+      else LB32(2, 96, false, false);
 #undef LB32
       continue;
     }
-#define LAUNCH_B(HH, NTV)                                                                                                 \
-  if (dout_bf)                                                                                                        \
-    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV, true>), dim3(grid), dim3(512), 0, st, dz, Wn, dout,  \
-                       dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n);                          \
-  else                                                                                                                \
-    hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV>), dim3(grid), dim3(512), 0, st, dz, Wn, dout, dh_fin, \
-                       dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+#define LB16(HH, NTV, DB) hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV, DB>), dim3(grid), dim3(512), 0, st, \
+                                           dz, Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
+#define LAUNCH_B(HH, NTV)           \
+  if (dout_bf) LB16(HH, NTV, true); \
+  else LB16(HH, NTV, false)
     if (H == 64) LAUNCH_B(64, false);
     else if (H == 128) LAUNCH_B(128, false);
     else if (H == 256) LAUNCH_B(256, false);
     else LAUNCH_B(512, false);
 #undef LAUNCH_B
+#undef LB16
   }
 }
