@@ -115,7 +115,10 @@ void lstm_bwd_persistent(const Tensor& dz, const Tensor& Wn, const Tensor& dout,
                          const Tensor& dc_carry, const Tensor& acts, const Tensor& cs, const Tensor& lens,
                          const Tensor& xbuf, const Tensor& err, const OT& dbias, int64_t T, int64_t B, int64_t H,
                          bool dout_batch_frame) {
-  chk(dz, BF, "dz"); chk(Wn, BF, "Wn"); chk(dout, F32, "dout"); chk(dh_fin, F32, "dh_fin");
+  // dout: fp32, or bf16 in the batch frame (the top layer reading the bf16 encoder-output gradient)
+  const bool dout16 = dout.scalar_type() == BF;
+  TORCH_CHECK(!dout16 || dout_batch_frame, "lstm_bwd_persistent: a bf16 dout is read in the batch frame only");
+  chk(dz, BF, "dz"); chk(Wn, BF, "Wn"); chk(dout, dout16 ? BF : F32, "dout"); chk(dh_fin, F32, "dh_fin");
   chko(dbias, F32, 2 * 4 * H, "dbias");
   chk(dc_carry, F32, "dc_carry"); chk(acts, F32, "acts"); chk(cs, F32, "cs"); chk(lens, I32, "lens");
   chk(xbuf, at::kLong, "xbuf"); chk(err, I32, "err");
@@ -126,9 +129,10 @@ void lstm_bwd_persistent(const Tensor& dz, const Tensor& Wn, const Tensor& dout,
   numel_eq(acts, 2 * T * B * 4 * H, "acts"); numel_eq(cs, 2 * (T + 1) * B * H, "cs"); numel_eq(lens, B, "lens");
   TORCH_CHECK(xbuf.numel() >= (int64_t)lstm_persistent_xbuf_elems((int)H, (int)B, true), "xbuf too small");
   numel_eq(err, 1, "err");
-  launch_lstm_bwd_persistent(P<bf16>(dz), P<bf16>(Wn), P<float>(dout), P<float>(dh_fin), P<float>(dc_carry),
-                             P<float>(acts), P<float>(cs), P<int>(lens), (unsigned long long*)xbuf.data_ptr(),
-                             (unsigned*)err.data_ptr(), PO<float>(dbias), T, B, H, dout_batch_frame, stream());
+  launch_lstm_bwd_persistent(P<bf16>(dz), P<bf16>(Wn), (const float*)dout.data_ptr(), P<float>(dh_fin),
+                             P<float>(dc_carry), P<float>(acts), P<float>(cs), P<int>(lens),
+                             (unsigned long long*)xbuf.data_ptr(), (unsigned*)err.data_ptr(), PO<float>(dbias), T, B, H,
+                             dout_batch_frame, stream(), dout16);
 }
 
 // ---------------------------------------------------------------- attention
@@ -588,10 +592,13 @@ void ctx_da(const Tensor& dctx, const Tensor& enc, const Tensor& da, int64_t B, 
   ctx_chk(dctx, BF, D * B * A, "dctx"); ctx_chk(enc, BF, B * T * A, "enc"); ctx_chk(da, F32, D * B * T, "da");
   launch_ctx_da(P<bf16>(dctx), P<bf16>(enc), P<float>(da), (int)B, (int)T, (int)D, (int)A, acc, stream());
 }
+// dE = a^T . dctx into an fp32 or a bf16 de
 void ctx_de(const Tensor& att, const Tensor& dctx, const Tensor& de, int64_t B, int64_t T, int64_t D, int64_t A) {
   TORCH_CHECK(ctx_bmm_ok((int)B, (int)T, (int)D, (int)A), "ctx_de: D <= 128, T % 8 == 0, A % 128 == 0");
-  ctx_chk(att, BF, D * B * T, "att"); ctx_chk(dctx, BF, D * B * A, "dctx"); ctx_chk(de, F32, B * T * A, "de");
-  launch_ctx_de(P<bf16>(att), P<bf16>(dctx), P<float>(de), (int)B, (int)T, (int)D, (int)A, stream());
+  const bool b16 = de.scalar_type() == BF;
+  ctx_chk(att, BF, D * B * T, "att"); ctx_chk(dctx, BF, D * B * A, "dctx"); ctx_chk(de, b16 ? BF : F32, B * T * A, "de");
+  launch_ctx_de(P<bf16>(att), P<bf16>(dctx), b16 ? nullptr : P<float>(de), b16 ? P<bf16>(de) : nullptr, (int)B, (int)T,
+                (int)D, (int)A, stream());
 }
 void wgrad_tn(const Tensor& a, const Tensor& b, const Tensor& out) {
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "wgrad_tn: 2-D views");

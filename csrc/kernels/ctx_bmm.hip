@@ -228,8 +228,12 @@ __global__ __launch_bounds__(NW * 64) void ctx_da_kernel(const bf16* __restrict_
 // 56.3 / 2128 us (headline / config #5), this loop 58.6 / 1726, the loop with a second dctx buffer
 // (96 KB, 1 workgroup per CU) 71.6 / 2024.  Rows past D of the att image are zero, both operands
 // are read transposed; waves 2 x 2, each 64 t x 64 n.
+// deb (bf16 mode): the product stored in bf16 (the engine's bf16 encoder-output gradient, to which
+// the W_h GEMM then adds dF . W_h^T with beta = 1).  An in-place bf16 accumulate here measured
+// 3023 vs 1729 us at config #5 (64 two-byte reads per lane in the epilogue).
 __global__ __launch_bounds__(256) void ctx_de_kernel(const bf16* __restrict__ att, const bf16* __restrict__ dctx,
-                                                     float* __restrict__ de, int B, int T, int D, int A) {
+                                                     float* __restrict__ de, bf16* __restrict__ deb, int B, int T,
+                                                     int D, int A) {
   constexpr int IMG = 128 * 256;
   __shared__ __attribute__((aligned(16))) char smem[2 * IMG];  // att image, dctx image
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -296,9 +300,14 @@ __global__ __launch_bounds__(256) void ctx_de_kernel(const bf16* __restrict__ at
       for (int r = 0; r < 4; ++r) {
         const int t = t0 + 64 * wr + 16 * i + 4 * (lane >> 4) + r;
         if (t < T) {
-          float* o = de + ((size_t)b * T + t) * A + nl;
+          const size_t o = ((size_t)b * T + t) * A + nl;
+          if (deb) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[16 * j] = acc[i][j][r];
+            for (int j = 0; j < 4; ++j) deb[o + 16 * j] = f2bf(acc[i][j][r]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) de[o + 16 * j] = acc[i][j][r];
+          }
         }
       }
     if (nb + 1 < ntn) {
@@ -334,6 +343,6 @@ void launch_ctx_da(const bf16* dctx, const bf16* enc, float* da, int B, int T, i
   }
 }
 
-void launch_ctx_de(const bf16* att, const bf16* dctx, float* de, int B, int T, int D, int A, hipStream_t st) {
-  hipLaunchKernelGGL(ctx_de_kernel, dim3(B * ((T + 127) / 128)), dim3(256), 0, st, att, dctx, de, B, T, D, A);
+void launch_ctx_de(const bf16* att, const bf16* dctx, float* de, bf16* deb, int B, int T, int D, int A, hipStream_t st) {
+  hipLaunchKernelGGL(ctx_de_kernel, dim3(B * ((T + 127) / 128)), dim3(256), 0, st, att, dctx, de, deb, B, T, D, A);
 }

@@ -114,7 +114,8 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
 bool lstm_persistent_fx_ok(int H, int B, int E);
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
-                                unsigned* err, float* dbias, int T, int B, int H, bool dout_bf, hipStream_t st);
+                                unsigned* err, float* dbias, int T, int B, int H, bool dout_bf, hipStream_t st,
+                                bool dout_bf16 = false);
 int vocab_topk_tiles(int V, int H);
 void set_vocab_select_stamps(unsigned long long* buf);
 void launch_vocab_span_probe(const bf16* X, const bf16* WT, const float* bias, float* logits, float* part_ms, int R, int V,
@@ -225,7 +226,7 @@ void launch_gemm_bt(const bf16* A, long lda, const bf16* Bt, long ldb, void* C, 
 bool ctx_bmm_ok(int B, int T, int D, int A);
 void launch_ctx_fwd(const bf16* att, const bf16* enc, float* ctx, bf16* ctxb, int B, int T, int D, int A, hipStream_t st);
 void launch_ctx_da(const bf16* dctx, const bf16* enc, float* da, int B, int T, int D, int A, bool acc, hipStream_t st);
-void launch_ctx_de(const bf16* att, const bf16* dctx, float* de, int B, int T, int D, int A, hipStream_t st);
+void launch_ctx_de(const bf16* att, const bf16* dctx, float* de, bf16* deb, int B, int T, int D, int A, hipStream_t st);
 
 // attribution: per-phase s_memtime sums of the 32-row H = 512 BPTT (nullptr: off)
 void set_lstm_bwd_stamps(unsigned long long* buf);

@@ -107,6 +107,17 @@ __device__ __forceinline__ f32x4 ld_f4(const float* p, bool nt) {
   return *reinterpret_cast<const f32x4*>(p);
 }
 __device__ __forceinline__ float ld_f(const float* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
+// the BPTT's dL/dh_out element idx: DBF 0 / 1 fp32 (step / batch frame), DBF 2 bf16 (batch frame:
+// the encoder-output gradient dE kept in bf16, profiles/r6/de_bf16.md)
+template <int DBF>
+__device__ __forceinline__ float ld_dout(const float* dout, size_t idx, bool nt) {
+  if constexpr (DBF == 2) {
+    const unsigned short* p = reinterpret_cast<const unsigned short*>(dout) + idx;
+    return __uint_as_float((unsigned)(nt ? __builtin_nontemporal_load(p) : *p) << 16);
+  } else {
+    return ld_f(dout + idx, nt);
+  }
+}
 
 // LDS tile [16 rows][RS] bf16 with the 16-byte chunk index XOR-swizzled by row (no padding:
 // the backward tile is exactly 2 x 32 KB at H = 256).
@@ -579,7 +590,7 @@ __global__ __launch_bounds__(512, 1) void lstm_fwd_persistent8_kernel(
 // (its own partial stays in LDS): per step a lane reads 4 x (NC-1) granules instead of 32.
 // NW = 4 or 8 waves: the cell update covers the tile's 16 rows x 64 units with RPL = 16 / NW
 // rows per lane (4 or 2); waves < NC run the partial GEMM (at H = 512, NC = 8: all 8 waves).
-template <int H, int NW, bool NT, bool DBF = false>
+template <int H, int NW, bool NT, int DBF = 0>
 __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
@@ -645,12 +656,12 @@ __global__ __launch_bounds__(64 * NW, 1) void lstm_bwd_persistent_kernel(
     for (int i = 0; i < RPL; ++i) {
       const size_t ri = (size_t)rc[i] * H + u;
       if constexpr (NT) {
-        dho[i] = ld_f(dout + (DBF ? dout_bf_idx(d, s, rc[i], ln[i], u, T, H) : ((size_t)d * T + s) * BH + ri), true);
+        dho[i] = ld_dout<DBF>(dout, DBF ? dout_bf_idx(d, s, rc[i], ln[i], u, T, H) : ((size_t)d * T + s) * BH + ri, true);
         const f32x4 q = ld_f4(acts + ((((size_t)d * T + s) * B + rc[i]) * H + u) * 4, true);
         a4[i][0] = q[0]; a4[i][1] = q[1]; a4[i][2] = q[2]; a4[i][3] = q[3];
         cpv[i] = ld_f(cs + ((size_t)d * (T + 1) + s) * BH + ri, true);
       } else {
-        dho[i] = dout[DBF ? dout_bf_idx(d, s, rc[i], ln[i], u, T, H) : ((size_t)d * T + s) * BH + ri];
+        dho[i] = ld_dout<DBF>(dout, DBF ? dout_bf_idx(d, s, rc[i], ln[i], u, T, H) : ((size_t)d * T + s) * BH + ri, false);
         const float4 q = *reinterpret_cast<const float4*>(acts + ((((size_t)d * T + s) * B + rc[i]) * H + u) * 4);
         a4[i][0] = q.x; a4[i][1] = q.y; a4[i][2] = q.z; a4[i][3] = q.w;
         cpv[i] = cs[((size_t)d * (T + 1) + s) * BH + ri];
@@ -833,7 +844,7 @@ void set_lstm_bwd_stamps(unsigned long long* buf) {
 // step's hand-off poll with LDS-only barriers -- the stamps moved 1.7k of the 7.4k "dz stores +
 // barrier 2" cycles, the BPTT micro -2.5 % at batch 2048, config #5 per step unchanged
 // (356.3 / 356.9 vs 357.0 / 356.2 ms).
-template <bool NT, int PC = 2, int SL = 96, bool DBF = false, bool STAMP = false>
+template <bool NT, int PC = 2, int SL = 96, int DBF = 0, bool STAMP = false>
 __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
     bf16* __restrict__ dz, const bf16* __restrict__ Wn, const float* __restrict__ dout,
     const float* __restrict__ dh_fin, float* __restrict__ dc_carry, const float* __restrict__ acts,
@@ -898,7 +909,8 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
     // uniform step bases + 32-bit per-lane byte offsets (saddr addressing: no 64-bit address
     // pairs per row held across the step)
     // (DBF: the batch-frame gradient's direction half; rows and positions per lane below)
-    const float* dout_s = DBF ? dout + d * H : dout + ((size_t)d * T + s) * BH;
+    const float* dout_s = DBF == 1 ? dout + d * H : dout + ((size_t)d * T + s) * BH;
+    const bf16* doutb_s = reinterpret_cast<const bf16*>(dout) + d * H;  // (DBF 2)
     const float* acts_s = acts + ((size_t)d * T + s) * BH * 4;
     const float* cs_s = cs + ((size_t)d * (T + 1) + s) * BH;
     float dho[RPL], a4[RPL][4], cpv[RPL];
@@ -914,7 +926,10 @@ __global__ __launch_bounds__(1024, 1) void lstm_bwd_persistent32_kernel(
       if constexpr (DBF) {  // batch-frame row (rc * T + position), opaque: no hoisted 64-bit offsets
         // (the row from the opaque rio = rc * H + u: no extra live register per row)
         const unsigned rt = (ri / H) * (unsigned)T + (unsigned)((d == 0 || s >= ln[i]) ? s : ln[i] - 1 - s);
-        dho[i] = ld_f(boff(dout_s, (unsigned)u * 4u) + (size_t)rt * (2 * H), NT);
+        if constexpr (DBF == 2)
+          dho[i] = ld_dout<2>(reinterpret_cast<const float*>(boff(doutb_s, (unsigned)u * 2u)), (size_t)rt * (2 * H), NT);
+        else
+          dho[i] = ld_f(boff(dout_s, (unsigned)u * 4u) + (size_t)rt * (2 * H), NT);
       } else {
         dho[i] = ld_f(boff(dout_s, ri * 4u), NT);
       }
@@ -1231,7 +1246,8 @@ void launch_lstm_fwd_persistent(const float* gx, const float* bias, const bf16* 
 
 void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, const float* dh_fin, float* dc_carry,
                                 const float* acts, const float* cs, const int* lens, unsigned long long* xbuf,
-                                unsigned* err, float* dbias, int T, int B, int H, bool dout_bf, hipStream_t st) {
+                                unsigned* err, float* dbias, int T, int B, int H, bool dout_bf, hipStream_t st,
+                                bool dout_bf16) {
   const int R = lstm_rows(H, B, true), ntile = (B + R - 1) / R, nl = lstm_tiles_per_launch(H, ntile), NC = H / 64;
   if (nl <= 0) return;
   gu64* xb = (gu64*)xbuf;
@@ -1243,19 +1259,23 @@ void launch_lstm_bwd_persistent(bf16* dz, const bf16* Wn, const float* dout, con
                                                  dim3(1024), 0, st, dz, Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, \
                                                  dbias, T, B, ntile, t0, n)
       // poll 2 peers per pass, s_sleep(96): profiles/r4/ab/bptt32.md
+      const int dbf = dout_bf ? (dout_bf16 ? 2 : 1) : 0;
       if (lb_stamps_on) {
-        if (dout_bf) LB32(2, 96, true, true);
-        else LB32(2, 96, false, true);
-      } else if (dout_bf) LB32(2, 96, true, false);
-      else LB32(2, 96, false, false);
+        if (dbf == 2) LB32(2, 96, 2, true);
+        else if (dbf == 1) LB32(2, 96, 1, true);
+        else LB32(2, 96, 0, true);
+      } else if (dbf == 2) LB32(2, 96, 2, false);
+      else if (dbf == 1) LB32(2, 96, 1, false);
+      else LB32(2, 96, 0, false);
 #undef LB32
       continue;
     }
 #define LB16(HH, NTV, DB) hipLaunchKernelGGL((lstm_bwd_persistent_kernel<HH, 8, NTV, DB>), dim3(grid), dim3(512), 0, st, \
                                            dz, Wn, dout, dh_fin, dc_carry, acts, cs, lens, xb, e, dbias, T, B, ntile, t0, n)
-#define LAUNCH_B(HH, NTV)           \
-  if (dout_bf) LB16(HH, NTV, true); \
-  else LB16(HH, NTV, false)
+#define LAUNCH_B(HH, NTV)                          \
+  if (dout_bf && dout_bf16) LB16(HH, NTV, 2);      \
+  else if (dout_bf) LB16(HH, NTV, 1);              \
+  else LB16(HH, NTV, 0)
     if (H == 64) LAUNCH_B(64, false);
     else if (H == 128) LAUNCH_B(128, false);
     else if (H == 256) LAUNCH_B(256, false);

@@ -74,6 +74,22 @@ def test_ctx_de_matches_fp32(B, T, D, A):
     assert bool((full[B * T * A:] == 12345.0).all())
 
 
+@pytest.mark.parametrize("B,T,D,A", SHAPES[:3])
+def test_ctx_de_into_bf16(B, T, D, A):
+    """bf16 dE mode: a^T . dctx stored in bf16 (the engine's bf16 encoder-output gradient, to which the
+    W_h GEMM adds dF . W_h^T): the fp32 result rounded once."""
+    k = _k()
+    att, _, dctx = _ops(B, T, D, A, 5 * B + T + D + A)
+    de = torch.full((B, T, A), float("nan"), device="cuda", dtype=torch.bfloat16)
+    k.ctx_de(att, dctx, de, B, T, D, A)
+    de32 = torch.empty(B, T, A, device="cuda")
+    k.ctx_de(att, dctx, de32, B, T, D, A)
+    torch.cuda.synchronize()
+    assert torch.equal(de, de32.bfloat16())
+    ref = torch.einsum("dbt,dba->bta", att.float(), dctx.float())
+    _close(de, ref, 1e-2)
+
+
 def test_ctx_bmm_declines_unsupported_shapes():
     k = _k()
     assert not k.ctx_bmm_ok(4, 100, 129, 512)  # D > 128

@@ -65,6 +65,7 @@ def test_persistent_matches_step_kernels(H, B, T):
             xb = torch.zeros(int(k.lstm_persistent_xbuf(H, B, True)), device="cuda", dtype=torch.long)
             db = torch.full((2, 4 * H), 0.25, device="cuda")  # accumulates onto what is there
             dcc0 = dcc.clone()
+            dcc_init = dcc.clone()
             k.lstm_bwd_persistent(dz, Wn, dout, dh_fin, dcc, acts, cs, lens, xb, err, db, T, B, H, False)
             # the same gradient in the BATCH frame ([B][T][2H], bw half at the reversed position), read
             # by the kernel directly (what the top layer's to_step_frame pass used to rebuild): same bits
@@ -78,6 +79,17 @@ def test_persistent_matches_step_kernels(H, B, T):
             k.lstm_bwd_persistent(dz2, Wn, dE, dh_fin, dcc0, acts, cs, lens, xb, err, None, T, B, H, True)
             torch.cuda.synchronize()
             assert torch.equal(dz2, dz) and torch.equal(dcc0, dcc)
+            # the batch-frame gradient in bf16 (the engine's bf16 dE): the same bits as the fp32 read
+            # of the same rounded values
+            dEb = dE.bfloat16()
+            outs = []
+            for src in (dEb, dEb.float()):
+                dzx, dcx = torch.zeros_like(dz), dcc_init.clone()
+                xb.zero_()
+                k.lstm_bwd_persistent(dzx, Wn, src, dh_fin, dcx, acts, cs, lens, xb, err, None, T, B, H, True)
+                outs.append((dzx, dcx))
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
         torch.cuda.synchronize()
         assert int(err.item()) == 0
         if mode != "step":

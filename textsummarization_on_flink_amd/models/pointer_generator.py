@@ -76,6 +76,11 @@ VOCAB_PAD = os.environ.get("TSAMD_VOCAB_PAD", "1") != "0"
 # gradients dA = dctx . enc_out^T and dE = a^T . dctx) on the hand-written ctx_bmm.hip kernels
 # (step-major outputs, no tr01 pass) instead of torch.bmm + tr01
 CTX_NATIVE = os.environ.get("TSAMD_CTX_NATIVE", "1") != "0"
+# TSAMD_DE_BF16 (default 1; with the native context kernels and the persistent BPTT): the encoder-
+# output gradient dE = a^T . dctx + dF . W_h^T kept in bf16 -- ctx_de writes a^T . dctx in bf16, the
+# W_h GEMM adds into it (beta = 1, bf16 in and out), the top layer's BPTT reads it -- instead of an
+# fp32 [B][T][A] buffer written, re-read and rewritten, and read again (profiles/r6/de_bf16.md)
+DE_BF16 = os.environ.get("TSAMD_DE_BF16", "1") != "0"
 # K.M.N above which the vocab dW keeps the 4-way split-K batched GEMM (config #5: 8.2 ms against
 # 9.5 ms for the library at the padded N)
 VOCAB_DW_SPLIT_MIN = 1e12
@@ -667,7 +672,8 @@ class HipPointerGenerator:
         w["dF"] = z(B, T, A, dt=BF)  # written whole (zeros past len) by attn_bwd_feat, in bf16
         w["ATTb"] = z(D, B, T, dt=BF)
         w["DCTXb"] = z(D, B, A, dt=BF)
-        self._dE = z(B, T, A)
+        self.de_bf16 = DE_BF16 and self.ctx_native and self.persistent_lstm
+        self._dE = z(B, T, A, dt=BF if self.de_bf16 else F32)
         # attn_bwd_feat partial rows (spread the atomics), summed after; deterministic mode: one
         # row per workgroup (a single writer per slot)
         nfeat = ((T + 15) // 16) * B
@@ -1466,13 +1472,16 @@ class HipPointerGenerator:
         if not self.proj_attn:  # (the projected-context forward made ATTb already)
             w["ATTb"].copy_(w["ATT"])
         w["DCTXb"].copy_(w["DCTX"])
+        if self.de_bf16:  # bf16 dE: a^T . dctx stored bf16, then += dF . W_h^T (library GEMM, beta = 1)
+            k.ctx_de(w["ATTb"], w["DCTXb"], dE, B, T, D, A)
+            _ops().blt_mm(dFb, self.pk["Wh"], dE.view(B * T, A), False, True, 1.0, None)
+            return
         if self.ctx_native:
             k.ctx_de(w["ATTb"], w["DCTXb"], dE, B, T, D, A)
         else:
             torch.bmm(w["ATTb"].permute(1, 2, 0), w["DCTXb"].permute(1, 0, 2), out_dtype=F32, out=dE)
         dE2 = dE.view(B * T, A)
         gemm(dE2, dFb, self.pk["Wh"].t(), 1.0)
-        self._dE = dE
 
     def backward_tail_enc(self):
         """reduce_states, encoder BPTT and weight gradients; joins the deferred decoder weight

@@ -76,6 +76,15 @@ def main():
         r["ctx_native"] = timed(lambda: k.ctx_fwd(att, enc, CTX, CTXb, B, T, D, A))
         r["da_native"] = timed(lambda: k.ctx_da(dctx, enc, dA, B, T, D, A, True))
         r["dE_native"] = timed(lambda: k.ctx_de(att, dctx, dE, B, T, D, A))
+        dEb = torch.zeros(B, T, A, device=dev, dtype=BF)
+        r["dE_native_bf16"] = timed(lambda: k.ctx_de(att, dctx, dEb, B, T, D, A))
+        # the rest of dE: dF . W_h^T over B * T rows (fp32 beta = 1 after the fp32 dE, or bf16 out first)
+        dF = (torch.randn(B * T, A, device=dev) * 0.01).to(BF)
+        Wh = (torch.randn(A, A, device=dev) * 0.05).to(BF)
+        r["dFWh_blt_f32_beta1"] = timed(lambda: k.blt_mm(dF, Wh, dE.view(B * T, A), False, True, 1.0, None))
+        r["dFWh_blt_bf16"] = timed(lambda: k.blt_mm(dF, Wh, dEb.view(B * T, A), False, True, 0.0, None))
+        r["dFWh_gemm_bt_bf16"] = timed(lambda: k.gemm_bt(dF, Wh, dEb.view(B * T, A), 0.0, None, None, None, 0, 0, 0, None))
+        r["dFWh_blt_bf16_beta1"] = timed(lambda: k.blt_mm(dF, Wh, dEb.view(B * T, A), False, True, 1.0, None))
         del tr
     print(json.dumps(r), flush=True)
 
