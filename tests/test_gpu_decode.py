@@ -165,11 +165,13 @@ def test_device_beam_graph_equals_eager_and_tracks_oracle(coverage, pointer_gen)
         assert len(hg[0].attn_dists) == len(hg[0].tokens) - 1
 
 
-@pytest.mark.parametrize("overlap,flush", [(False, False), (True, False), (True, True)])
-def test_pipelined_decode_batches_equal_batch_by_batch(overlap, flush):
+@pytest.mark.parametrize("overlap,flush,pair", [(False, False, False), (False, False, True), (False, True, True),
+                                                (True, False, False), (True, True, False)])
+def test_pipelined_decode_batches_equal_batch_by_batch(overlap, flush, pair):
     """decode_batches (results snapshotted to pinned memory, backtracked while the next batch
-    runs; overlap: the next batch's encoder on a side stream beside the decode steps) ==
-    decode() batch by batch: same summaries in the same order."""
+    runs; overlap: the next batch's encoder on a side stream beside the decode steps; pair: two
+    queued batches encoded as one 2 n_articles-row pass, the third alone) == decode() batch by
+    batch: same summaries in the same order."""
     from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
     hps, vocab, batch, params = _peaked_setup(True, pointer_gen=True)
     corpus = SyntheticCorpus(vocab_size=hps.vocab_size, raw_vocab=3 * hps.vocab_size, seed=9, art_mean=40, art_sd=10,
@@ -179,6 +181,7 @@ def test_pipelined_decode_batches_equal_batch_by_batch(overlap, flush):
     d = DeviceBeamDecoder(hps, vocab, params, n_articles=hps.batch_size, T=hps.max_enc_steps, use_graph=True)
     seq = [[h.tokens for h in d.decode(b)] for b in batches]
     d.overlap_encoder = overlap
+    d.pair_encoder = pair
     # flush: a streaming source with nothing queued between batches (FLUSH from the encoder
     # look-ahead, then a batch from the last-chunk poll, which was not pre-encoded)
     src = [x for b in batches for x in (b, d.FLUSH)] if flush else batches

@@ -22,6 +22,7 @@ unchanged: cov'_t = cov'_{t-1}[parent] + a_{t-1}[parent].
 from __future__ import annotations
 
 
+import os
 from typing import List
 from dataclasses import replace
 
@@ -71,6 +72,15 @@ class DeviceBeamDecoder:
         # (bench, 64 articles: hidden 512 / 2 layers / T = 800 2263 -> 2550 summaries/s; hidden
         # 256 / 1 layer / T = 400, a 1.1 ms encoder: 6016 -> 5817, so off)
         self.overlap_encoder = self.eng.L > 1 or self.eng.H >= 512
+        # decode_batches without that overlap: two queued plain batches are encoded as ONE
+        # 2 * n_articles-row encoder pass (the persistent LSTM's step time does not grow with the
+        # rows, so the pair costs about one batch's encoder); the second batch's outputs wait in
+        # that engine's buffers for its turn (TSAMD_DEC_PAIR_ENC; profiles/r6/decode_pair_encoder.md)
+        self.pair_encoder = (not self.overlap_encoder and os.environ.get("TSAMD_DEC_PAIR_ENC", "1") != "0"
+                             and self.dev.type == "cuda")
+        self.eng2 = None
+        if self.pair_encoder:
+            self._pair_engine()  # built up front: its construction must not land in a decode
         self._alloc()
         self.refresh_weights()
         self.graph = None
@@ -127,6 +137,8 @@ class DeviceBeamDecoder:
         """Per-token tables for the current weights (call after loading a checkpoint):
         Xtab = emb . W_in[:E] + b_in  and  XGtab = Xtab . W_cell[:E] + b_cell."""
         self.eng.pack()
+        if getattr(self, "eng2", None) is not None:
+            self.eng2.pack()
         p, E = self.p, self.eng.E
         emb = p[EMB]
         self.Xtab = (emb @ p[LIN_M][:E] + p[LIN_B]).contiguous()
@@ -157,22 +169,51 @@ class DeviceBeamDecoder:
         self._enc_ev = torch.cuda.Event()
         self._enc_ev.record(s)
 
-    def _encode_copy(self):
-        """Encoder outputs (engine buffers) -> the decoder's feature and initial-state buffers."""
-        eng, b, beam = self.eng, self.b, self.beam
+    def _encode_copy(self, src=None):
+        """Encoder outputs (engine buffers) -> the decoder's feature and initial-state buffers.
+        ``src`` = (engine, first row): rows first .. first + n_articles of another engine's
+        encoder outputs (the paired encoder), else this decoder's own engine."""
+        eng, lo = src if src is not None else (self.eng, 0)
+        hi = lo + self.Na
+        b, beam = self.b, self.beam
         w = eng.w
         # encoder features stay one row per article: the attention kernels read them once for
         # all ``beam`` hypotheses of the article (rep = beam)
         r = beam // self.rep
-        b["E"].copy_(eng.enc[-1]["out"].repeat_interleave(r, 0) if r > 1 else eng.enc[-1]["out"])
+        rep = (lambda x: x.repeat_interleave(r, 0)) if r > 1 else (lambda x: x)
+        b["E"].copy_(rep(eng.enc[-1]["out"][lo:hi]))
         fk = "F" if self.row_attn else "Ft"
-        b[fk].copy_(w[fk].repeat_interleave(r, 0) if r > 1 else w[fk])
-        b["lens_att"].copy_(w["enc_lens"].repeat_interleave(r, 0) if r > 1 else w["enc_lens"])
-        b["lens"].copy_(w["enc_lens"])
-        b["ext"].copy_(w["ext"])
+        b[fk].copy_(rep(w[fk][lo:hi]))
+        b["lens_att"].copy_(rep(w["enc_lens"][lo:hi]))
+        b["lens"].copy_(w["enc_lens"][lo:hi])
+        b["ext"].copy_(w["ext"][lo:hi])
         X = self.st[0]
-        X["C"].copy_(w["Cst"][0].repeat_interleave(beam, 0))
-        X["H"].copy_(w["Hb"][0].repeat_interleave(beam, 0))
+        X["C"].copy_(w["Cst"][0][lo:hi].repeat_interleave(beam, 0))
+        X["H"].copy_(w["Hb"][0][lo:hi].repeat_interleave(beam, 0))
+
+    def _pair_engine(self):
+        if self.eng2 is None:
+            self.eng2 = HipPointerGenerator(self.hps.replace(batch_size=2 * self.Na), self.V, self.p, B=2 * self.Na,
+                                            T=self.T, D=1, cfg=replace(EngineConfig.from_env(), proj_attn=False))
+            self.eng2.keep_ft = self.eng.keep_ft
+        return self.eng2
+
+    @staticmethod
+    def _pairable(a, b) -> bool:
+        return (b is not None and b is not DeviceBeamDecoder.FLUSH and getattr(a, "host_pack", None) is None
+                and getattr(b, "host_pack", None) is None and a.enc_batch.shape == b.enc_batch.shape)
+
+    def _encode_pair(self, a, b):
+        """One encoder pass over batches a and b (2 n_articles rows): a's outputs are rows
+        0 .. n_articles - 1, b's the rest, of the pair engine's buffers."""
+        import numpy as np
+        from types import SimpleNamespace
+        e2 = self._pair_engine()
+        cat = lambda n: np.concatenate([getattr(a, n), getattr(b, n)], 0)  # noqa: E731
+        merged = SimpleNamespace(**{n: cat(n) for n in ("enc_batch", "enc_lens", "enc_batch_extend_vocab", "dec_batch",
+                                                         "dec_padding_mask", "target_batch", "valid")})
+        e2.set_batch(merged)
+        e2._encoder_forward(need_grad=False)
 
     def _prologue(self):
         """Step-0 initial-state attention into state set 0, beam state reset."""
@@ -310,18 +351,24 @@ class DeviceBeamDecoder:
         for _ in self.run_chunks(batch):
             pass
 
-    def run_chunks(self, batch, pre_encoded: bool = False, next_batch=None):
+    def run_chunks(self, batch, pre_encoded: bool = False, next_batch=None, enc_src=None):
         """Generator form of ``run``: each iteration queues one early-exit chunk of decode steps
         on the current stream and yields (``decode_batches`` does host work in between).
         ``pre_encoded``: ``batch``'s encoder was queued by ``_encode_launch``; ``next_batch``:
-        queue its encoder (side stream) once this batch's encoder outputs are copied out."""
+        queue its encoder (side stream) once this batch's encoder outputs are copied out;
+        ``enc_src``: (engine, first row) holding ``batch``'s encoder outputs (the paired encoder)."""
         if pre_encoded:
             torch.cuda.current_stream().wait_event(self._enc_ev)
         if self.use_graph and self.graph is None:
-            self._encode(batch)
+            if enc_src is not None:
+                self._encode_copy(enc_src)
+            else:
+                self._encode(batch)
             self._prologue()
             self._capture()
-        if pre_encoded and not self._captured_now:
+        if enc_src is not None:
+            self._encode_copy(enc_src)  # (the source engine's buffers are intact after a capture too)
+        elif pre_encoded and not self._captured_now:
             self._encode_copy()
         else:
             self._encode(batch)
@@ -431,7 +478,12 @@ class DeviceBeamDecoder:
         pending, slot = None, 0
         it = iter(batches)
         ov = self.overlap_encoder
-        batch, pre = None, False
+        pair = self.pair_encoder and not ov
+        batch, pre, src = None, False, None
+        # pair_encoder: the batch read ahead to pair with the current one (``held``, with its
+        # encoder rows ``held_src`` when the pair was encoded together); consumed where the loop
+        # would otherwise read the next batch during the current batch's last chunk
+        held, have_held, held_src = None, False, None
         done_src = False  # the source ended while prefetching
         while True:
             if batch is None:
@@ -445,10 +497,18 @@ class DeviceBeamDecoder:
                 if batch is None:
                     break
                 self._rows_ok(batch)
-                pre = False
+                pre, src = False, None
                 if ov:
                     self._encode_launch(batch)
                     pre = True
+            if pair and src is None and not have_held:
+                held, have_held = next(it, None), True
+                if self._pairable(batch, held):
+                    self._rows_ok(held)
+                    self._encode_pair(batch, held)
+                    src, held_src = (self.eng2, 0), (self.eng2, self.Na)
+                else:
+                    held_src = None
             # overlap_encoder: batch n + 1's encoder runs on a side stream beside batch n's decode steps
             nxt = next(it, None) if ov else None
             flushed = nxt is self.FLUSH
@@ -457,8 +517,9 @@ class DeviceBeamDecoder:
             elif nxt is not None:
                 self._rows_ok(nxt)
             nxt_pre = nxt is not None  # run_chunks launches its encoder beside this batch's steps
+            nxt_src = None
             first, fetched = True, ov and not flushed
-            for _ in self.run_chunks(batch, pre_encoded=pre, next_batch=nxt):
+            for _ in self.run_chunks(batch, pre_encoded=pre, next_batch=nxt, enc_src=src):
                 if first and pending is not None:  # the GPU has this batch's work queued
                     yield self._finish(pending)
                     pending = None
@@ -468,17 +529,28 @@ class DeviceBeamDecoder:
                     # batch now, so forming and packing it overlaps the GPU instead of following it
                     # (a streaming source forms it from the requests that arrived meanwhile)
                     fetched = True
-                    nxt, nxt_pre = next(it, None), False
+                    if have_held:
+                        nxt, nxt_src, have_held, held = held, held_src, False, None
+                    else:
+                        nxt = next(it, None)
+                    nxt_pre = False
                     if nxt is self.FLUSH:
-                        nxt = None  # nothing ready: polled again once this batch is done
+                        nxt, nxt_src = None, None  # nothing ready: polled again once this batch is done
                     elif nxt is not None:
                         self._rows_ok(nxt)
                     else:
                         done_src = True
+            if have_held:  # an early exit before the last chunk: the read-ahead batch is next
+                nxt, nxt_src, have_held, held = held, held_src, False, None
+                nxt_pre = False
+                if nxt is self.FLUSH:
+                    nxt, nxt_src = None, None
+                elif nxt is None:
+                    done_src = True
             arrays, ev = self._snapshot(slot)
             slot ^= 1
             pending = (arrays, ev, self._n_valid(batch), self.steps_run)
-            batch, pre = nxt, (nxt is not None and nxt_pre)
+            batch, pre, src = nxt, (nxt is not None and nxt_pre), nxt_src
             if batch is None and done_src:
                 break
         if pending is not None:
