@@ -165,13 +165,14 @@ def test_device_beam_graph_equals_eager_and_tracks_oracle(coverage, pointer_gen)
         assert len(hg[0].attn_dists) == len(hg[0].tokens) - 1
 
 
-@pytest.mark.parametrize("overlap,flush,pair", [(False, False, False), (False, False, True), (False, True, True),
-                                                (True, False, False), (True, True, False)])
-def test_pipelined_decode_batches_equal_batch_by_batch(overlap, flush, pair):
+@pytest.mark.parametrize("overlap,flush,group", [(False, False, 1), (False, False, 2), (False, False, 4),
+                                                 (False, True, 4), (True, False, 1), (True, True, 1)])
+def test_pipelined_decode_batches_equal_batch_by_batch(overlap, flush, group):
     """decode_batches (results snapshotted to pinned memory, backtracked while the next batch
-    runs; overlap: the next batch's encoder on a side stream beside the decode steps; pair: two
-    queued batches encoded as one 2 n_articles-row pass, the third alone) == decode() batch by
-    batch: same summaries in the same order."""
+    runs; overlap: the next batch's encoder on a side stream beside the decode steps; group: up to
+    that many queued batches encoded as one pass -- 2: a pair then the third alone, 4: all three in
+    one 4-batch pass with a repeated batch filling the rows) == decode() batch by batch: same
+    summaries in the same order."""
     from textsummarization_on_flink_amd.decode.device_beam import DeviceBeamDecoder
     hps, vocab, batch, params = _peaked_setup(True, pointer_gen=True)
     corpus = SyntheticCorpus(vocab_size=hps.vocab_size, raw_vocab=3 * hps.vocab_size, seed=9, art_mean=40, art_sd=10,
@@ -181,7 +182,7 @@ def test_pipelined_decode_batches_equal_batch_by_batch(overlap, flush, pair):
     d = DeviceBeamDecoder(hps, vocab, params, n_articles=hps.batch_size, T=hps.max_enc_steps, use_graph=True)
     seq = [[h.tokens for h in d.decode(b)] for b in batches]
     d.overlap_encoder = overlap
-    d.pair_encoder = pair
+    d.group_enc = group
     # flush: a streaming source with nothing queued between batches (FLUSH from the encoder
     # look-ahead, then a batch from the last-chunk poll, which was not pre-encoded)
     src = [x for b in batches for x in (b, d.FLUSH)] if flush else batches

@@ -72,15 +72,16 @@ class DeviceBeamDecoder:
         # (bench, 64 articles: hidden 512 / 2 layers / T = 800 2263 -> 2550 summaries/s; hidden
         # 256 / 1 layer / T = 400, a 1.1 ms encoder: 6016 -> 5817, so off)
         self.overlap_encoder = self.eng.L > 1 or self.eng.H >= 512
-        # decode_batches without that overlap: two queued plain batches are encoded as ONE
-        # 2 * n_articles-row encoder pass (the persistent LSTM's step time does not grow with the
-        # rows, so the pair costs about one batch's encoder); the second batch's outputs wait in
-        # that engine's buffers for its turn (TSAMD_DEC_PAIR_ENC; profiles/r6/decode_pair_encoder.md)
-        self.pair_encoder = (not self.overlap_encoder and os.environ.get("TSAMD_DEC_PAIR_ENC", "1") != "0"
-                             and self.dev.type == "cuda")
+        # decode_batches without that overlap: up to ``group_enc`` queued plain batches are encoded
+        # as ONE group_enc * n_articles-row encoder pass (the persistent LSTM's step time does not
+        # grow with the rows, so the group costs about one batch's encoder); the later batches'
+        # outputs wait in that engine's buffers for their turn (TSAMD_DEC_GROUP_ENC, 1 = off;
+        # profiles/r6/decode_pair_encoder.md)
+        g = int(os.environ.get("TSAMD_DEC_GROUP_ENC", "8"))
+        self.group_enc = g if (g > 1 and not self.overlap_encoder and self.dev.type == "cuda") else 1
         self.eng2 = None
-        if self.pair_encoder:
-            self._pair_engine()  # built up front: its construction must not land in a decode
+        if self.group_enc > 1:
+            self._group_engine()  # built up front: its construction must not land in a decode
         self._alloc()
         self.refresh_weights()
         self.graph = None
@@ -191,25 +192,27 @@ class DeviceBeamDecoder:
         X["C"].copy_(w["Cst"][0][lo:hi].repeat_interleave(beam, 0))
         X["H"].copy_(w["Hb"][0][lo:hi].repeat_interleave(beam, 0))
 
-    def _pair_engine(self):
+    def _group_engine(self):
         if self.eng2 is None:
-            self.eng2 = HipPointerGenerator(self.hps.replace(batch_size=2 * self.Na), self.V, self.p, B=2 * self.Na,
-                                            T=self.T, D=1, cfg=replace(EngineConfig.from_env(), proj_attn=False))
+            n = self.group_enc * self.Na
+            self.eng2 = HipPointerGenerator(self.hps.replace(batch_size=n), self.V, self.p, B=n, T=self.T, D=1,
+                                            cfg=replace(EngineConfig.from_env(), proj_attn=False))
             self.eng2.keep_ft = self.eng.keep_ft
         return self.eng2
 
     @staticmethod
-    def _pairable(a, b) -> bool:
+    def _groupable(a, b) -> bool:
         return (b is not None and b is not DeviceBeamDecoder.FLUSH and getattr(a, "host_pack", None) is None
                 and getattr(b, "host_pack", None) is None and a.enc_batch.shape == b.enc_batch.shape)
 
-    def _encode_pair(self, a, b):
-        """One encoder pass over batches a and b (2 n_articles rows): a's outputs are rows
-        0 .. n_articles - 1, b's the rest, of the pair engine's buffers."""
-        import numpy as np
+    def _encode_group(self, grp):
+        """One encoder pass over the batches of ``grp`` (at most the engine's rows / n_articles; the
+        rest of its rows repeat the last batch): batch j's outputs are rows j n_articles .. of the
+        group engine's buffers."""
         from types import SimpleNamespace
-        e2 = self._pair_engine()
-        cat = lambda n: np.concatenate([getattr(a, n), getattr(b, n)], 0)  # noqa: E731
+        e2 = self._group_engine()
+        full = list(grp) + [grp[-1]] * (e2.B // self.Na - len(grp))
+        cat = lambda n: np.concatenate([getattr(b, n) for b in full], 0)  # noqa: E731
         merged = SimpleNamespace(**{n: cat(n) for n in ("enc_batch", "enc_lens", "enc_batch_extend_vocab", "dec_batch",
                                                          "dec_padding_mask", "target_batch", "valid")})
         e2.set_batch(merged)
@@ -475,19 +478,25 @@ class DeviceBeamDecoder:
         ``batches`` may yield ``FLUSH`` (a streaming source with nothing queued): the pending
         batch is finished and yielded at once instead of waiting for the next batch (a result
         must not lag behind the next request, Issue-6)."""
+        from collections import deque
         pending, slot = None, 0
         it = iter(batches)
         ov = self.overlap_encoder
-        pair = self.pair_encoder and not ov
+        group = self.group_enc > 1 and not ov
         batch, pre, src = None, False, None
-        # pair_encoder: the batch read ahead to pair with the current one (``held``, with its
-        # encoder rows ``held_src`` when the pair was encoded together); consumed where the loop
-        # would otherwise read the next batch during the current batch's last chunk
-        held, have_held, held_src = None, False, None
+        # group_enc: the batches read ahead with the current one, each with its encoder rows
+        # (engine, first row), then the item that ended the read-ahead (a FLUSH, the end None, or a
+        # batch that cannot join), in source order; taken where the loop would otherwise read the
+        # next item during the current batch's last chunk
+        ahead = deque()
         done_src = False  # the source ended while prefetching
+
+        def take():  # the next item: read ahead first, else the source
+            return ahead.popleft() if ahead else (next(it, None), None)
+
         while True:
             if batch is None:
-                batch = next(it, None)
+                batch, src = take()
                 if batch is self.FLUSH:
                     batch = None
                     if pending is not None:
@@ -497,18 +506,24 @@ class DeviceBeamDecoder:
                 if batch is None:
                     break
                 self._rows_ok(batch)
-                pre, src = False, None
+                pre = False
                 if ov:
                     self._encode_launch(batch)
                     pre = True
-            if pair and src is None and not have_held:
-                held, have_held = next(it, None), True
-                if self._pairable(batch, held):
-                    self._rows_ok(held)
-                    self._encode_pair(batch, held)
-                    src, held_src = (self.eng2, 0), (self.eng2, self.Na)
-                else:
-                    held_src = None
+            if group and src is None and not ahead:
+                grp = [batch]
+                while len(grp) < self.group_enc:
+                    nb = next(it, None)
+                    if not self._groupable(batch, nb):
+                        ahead.append((nb, None))
+                        break
+                    self._rows_ok(nb)
+                    grp.append(nb)
+                if len(grp) > 1:
+                    self._encode_group(grp)
+                    src = (self.eng2, 0)
+                    for j, nb in enumerate(grp[1:], 1):
+                        ahead.insert(j - 1, (nb, (self.eng2, j * self.Na)))
             # overlap_encoder: batch n + 1's encoder runs on a side stream beside batch n's decode steps
             nxt = next(it, None) if ov else None
             flushed = nxt is self.FLUSH
@@ -529,10 +544,7 @@ class DeviceBeamDecoder:
                     # batch now, so forming and packing it overlaps the GPU instead of following it
                     # (a streaming source forms it from the requests that arrived meanwhile)
                     fetched = True
-                    if have_held:
-                        nxt, nxt_src, have_held, held = held, held_src, False, None
-                    else:
-                        nxt = next(it, None)
+                    nxt, nxt_src = take()
                     nxt_pre = False
                     if nxt is self.FLUSH:
                         nxt, nxt_src = None, None  # nothing ready: polled again once this batch is done
@@ -540,8 +552,8 @@ class DeviceBeamDecoder:
                         self._rows_ok(nxt)
                     else:
                         done_src = True
-            if have_held:  # an early exit before the last chunk: the read-ahead batch is next
-                nxt, nxt_src, have_held, held = held, held_src, False, None
+            if not fetched and ahead:  # an early exit before the last chunk: the read-ahead is next
+                nxt, nxt_src = ahead.popleft()
                 nxt_pre = False
                 if nxt is self.FLUSH:
                     nxt, nxt_src = None, None
