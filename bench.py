@@ -35,7 +35,7 @@ hidden 512, 2-layer encoder, enc 800, per-GPU batch sized for the GPU's HBM (the
 2048 / 1024 / 512 whose captured step fits EVERY rank, agreed before any gradient collective;
 ``config5_peak_mem_gb`` reports the footprint), ``--config5-steps`` timed steps after two warm-up
 steps (graph capture + one replay of the other batch), the same timed region as the headline;
-then 4 beam-4 decode batches at that size.  ``--config5-steps 0`` skips it.
+then 8 beam-4 decode batches at that size.  ``--config5-steps 0`` skips it.
 """
 import argparse
 import json
@@ -404,8 +404,10 @@ def bench_config5(args, info, D, torch, dev_id):
                               "batch_sizing": f"largest of {list(CONFIG5_BATCHES)} whose step fits every rank",
                               "steps": args.config5_steps, "warmup": n_warm}}
     if args.decode_batches > 0:
+        # 8 batches (4 before round 6): the decoder encodes up to 8 queued batches in one pass
+        # (decode/device_beam.py group_enc), so a 4-batch run padded half of that pass
         a5 = _ap.Namespace(**{**vars(args), "hidden": c["hidden"], "layers": c["layers"], "enc": c["enc"],
-                              "decode_batches": 4})
+                              "decode_batches": 8})
         d5 = bench_decode(a5, info, D, torch, dev_id)
         rec["config5_beam4_summaries_per_sec"] = d5["beam4_summaries_per_sec"]
         rec["config5_beam4_ms_per_batch"] = d5["beam4_ms_per_batch"]

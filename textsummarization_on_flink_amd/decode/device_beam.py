@@ -67,20 +67,24 @@ class DeviceBeamDecoder:
         self.row_attn = self.eng.cfg.decode_row_attn and bool(self.k.attn_row_ok(self.eng.A, T))
         self.eng.keep_ft = not self.row_attn  # the multi-block score kernel reads transposed features
         self.dev = self.eng.dev
-        # decode_batches: run batch n + 1's encoder on a side stream beside batch n's decode
+        # decode_batches: up to ``group_enc`` queued plain batches are encoded as ONE
+        # group_enc * n_articles-row encoder pass (the persistent LSTM's step time does not grow
+        # with the rows, so the group costs about one batch's encoder); the later batches' outputs
+        # wait in that engine's buffers for their turn (TSAMD_DEC_GROUP_ENC, 1 = off): headline
+        # decode 6273 -> 6792-6877, config #5 decode 2838-2855 (the side-stream overlap below)
+        # -> 3154-3167 summaries/s (profiles/r6/decode_pair_encoder.md)
+        g = int(os.environ.get("TSAMD_DEC_GROUP_ENC", "8"))
+        self.group_enc = g if (g > 1 and self.dev.type == "cuda") else 1
+        # without grouping: run batch n + 1's encoder on a side stream beside batch n's decode
         # steps when the encoder is long enough to pay for the CUs its persistent LSTM holds
         # (bench, 64 articles: hidden 512 / 2 layers / T = 800 2263 -> 2550 summaries/s; hidden
-        # 256 / 1 layer / T = 400, a 1.1 ms encoder: 6016 -> 5817, so off)
-        self.overlap_encoder = self.eng.L > 1 or self.eng.H >= 512
-        # decode_batches without that overlap: up to ``group_enc`` queued plain batches are encoded
-        # as ONE group_enc * n_articles-row encoder pass (the persistent LSTM's step time does not
-        # grow with the rows, so the group costs about one batch's encoder); the later batches'
-        # outputs wait in that engine's buffers for their turn (TSAMD_DEC_GROUP_ENC, 1 = off;
-        # profiles/r6/decode_pair_encoder.md)
-        g = int(os.environ.get("TSAMD_DEC_GROUP_ENC", "8"))
-        self.group_enc = g if (g > 1 and not self.overlap_encoder and self.dev.type == "cuda") else 1
+        # 256 / 1 layer / T = 400, a 1.1 ms encoder: 6016 -> 5817, so off); TSAMD_DEC_OVERLAP_ENC
+        # 0 / 1 forces it
+        ov = os.environ.get("TSAMD_DEC_OVERLAP_ENC", "auto")
+        self.overlap_encoder = ((self.eng.L > 1 or self.eng.H >= 512) and self.group_enc == 1) if ov == "auto" \
+            else ov != "0"
         self.eng2 = None
-        if self.group_enc > 1:
+        if self.group_enc > 1 and not self.overlap_encoder:
             self._group_engine()  # built up front: its construction must not land in a decode
         self._alloc()
         self.refresh_weights()
@@ -671,6 +675,11 @@ class DeviceBeamDecoder:
         """Decode a Batch of up to n_articles examples; best hypothesis per valid row."""
         if batch.enc_batch.shape[0] != self.Na:
             raise ValueError(f"batch has {batch.enc_batch.shape[0]} rows, engine expects {self.Na}")
+        if self.eng2 is not None and not getattr(self, "_group_warm", False) and self._groupable(batch, batch):
+            # the first call (a warm-up) also runs the group encoder once: its first-shape library
+            # picks and kernel loads then happen here, not inside a timed decode_batches
+            self._encode_group([batch])
+            self._group_warm = True
         self.run(batch)
         hyps = self.results(self._n_valid(batch))  # synchronises
         self.eng.check_lstm_err()  # the encoder ran the persistent LSTM: never emit garbage summaries
