@@ -66,7 +66,7 @@ BLT = os.environ.get("TSAMD_BLT", "1") != "0"
 BLT_WGRAD = BLT and os.environ.get("TSAMD_BLT_WGRAD", "0") == "1"
 BLT_VDW = BLT and os.environ.get("TSAMD_BLT_VOCAB_DW", "0") == "1"
 # TSAMD_VOCAB_PAD (default 1, fused vocab head): dlogits rows and the bf16 output-projection weight
-# padded to Vp = 128-aligned columns (the pad columns are zero: the vocab head writes them), so
+# padded to Vp = 128-aligned columns (the pad columns stay zero: allocated zeroed, never written), so
 # the two vocab-gradient GEMMs run at an aligned K / N -- dX = dlogits . W^T on the split-K
 # hand-written GEMM (headline: 566 -> 426 us) or the library (config #5: 7.88 -> 6.76 ms),
 # dW = X^T . dlogits on the library into a [H][Vp] scratch (653 -> 502 us with the copy)
@@ -641,7 +641,7 @@ class HipPointerGenerator:
                 w[n] = z(N)
             w["dbias"] = z(V)  # output_projection/v gradient, column sums taken inside pass 2
             w["vstate"] = z((N + 31) // 32, dt=torch.int32)  # dlogits blocks written by the last pass 2
-        # the fused head's dlogits rows: Vp columns (TSAMD_VOCAB_PAD; zero past V)
+        # the fused head's dlogits rows: Vp columns (TSAMD_VOCAB_PAD; the columns past V stay zero)
         self.Vp = -(-V // 128) * 128 if (self.fused_vocab and VOCAB_PAD) else V
         self.ctx_native = CTX_NATIVE and self.dev.type == "cuda" and bool(self.k.ctx_bmm_ok(B, T, D, A))
         w["logits"] = z(D * B, self.Vp, dt=BF)
@@ -1037,8 +1037,8 @@ class HipPointerGenerator:
             torch.add(w["xe"][1:], w["GV"][:D - 1], out=w["X"][1:])
         w["Xb"].copy_(w["X"])
         # ctx_t = a_t . enc_out for every step: [B][D, T] x [B][T, A] (bf16 a -- written by the
-        # attention kernel next to the fp32 a -- fp32 accumulate), then [B][D][A] -> CTX [D][B][A]
-        # and its bf16 twin in one pass (tr01)
+        # attention kernel next to the fp32 a -- fp32 accumulate) into the step-major CTX [D][B][A]
+        # and its bf16 twin: one ctx_bmm.hip launch, or torch.bmm + the tr01 layout pass
         if self.ctx_native:
             self.k.ctx_fwd(w["ATTb"], enc_out, w["CTX"], w["CTXb"], B, T, D, A)
             return
