@@ -222,13 +222,14 @@ def test_lstm_error_on_one_rank_skips_the_step_on_all_ranks():
         assert not finite and g0 == 2.0 and healthy_finite
 
 
-@pytest.mark.parametrize("defer", [True, False])
-def test_bucket_issue_order_leaves_only_the_embedding(defer):
+@pytest.mark.parametrize("defer,dw_side", [(True, False), (False, False), (True, True), (False, True)])
+def test_bucket_issue_order_leaves_only_the_embedding(defer, dw_side):
     """GraphTrainer's replay order (train/trainer.py replay_phases / issue_plan) with a recording
     reducer over the real flat-gradient layout of the bench model: every bucket except the
     embedding's is issued before the last phase graph is queued, so at most the 25.6 MB embedding
     gradient is all-reduced with nothing left to overlap; with the decoder weight gradients
-    deferred beside the encoder BPTT their bucket goes out right after that phase."""
+    deferred beside the encoder BPTT their bucket goes out right after that phase; with the vocab dW
+    beside the decoder loop (dw_side) phase 1 issues bucket 0 itself (GraphTrainer._Phase1)."""
     from textsummarization_on_flink_amd.config import HParams
     from textsummarization_on_flink_amd.models.params import FlatParams, param_specs
     from textsummarization_on_flink_amd.models.pointer_generator import HipPointerGenerator
@@ -255,6 +256,8 @@ def test_bucket_issue_order_leaves_only_the_embedding(defer):
 
         def replay(self):
             events.append(("graph", self.i))
+            if dw_side and self.i == 1:
+                events.append(("bucket", 0))  # _Phase1: from the side stream, before the decoder graph ends
 
     class Rec:
         def bucket_ready(self, b):
@@ -263,15 +266,16 @@ def test_bucket_issue_order_leaves_only_the_embedding(defer):
         def wait_issued(self):
             events.append(("wait",))
 
-    replay_phases([G(i) for i in range(4)], Rec(), issue_plan(defer), BPTT_PHASE, lstm_exclusive=True)
+    replay_phases([G(i) for i in range(4)], Rec(), issue_plan(defer, dw_side), BPTT_PHASE, lstm_exclusive=True)
     issued_before_last = {e[1] for e in events[:events.index(("graph", 3))] if e[0] == "bucket"}
     assert issued_before_last == {0, 1, 2}
-    assert events.index(("bucket", 0)) == events.index(("graph", 0)) + 1
+    assert [e for e in events if e[0] == "bucket"].count(("bucket", 0)) == 1
+    assert events.index(("bucket", 0)) == events.index(("graph", 1 if dw_side else 0)) + 1
     assert events.index(("wait",)) == events.index(("graph", BPTT_PHASE)) - 1  # no RCCL beside the full-grid BPTT
     if defer:
         assert events.index(("bucket", 1)) == events.index(("graph", 2)) + 1
     else:
-        assert events.index(("bucket", 1)) == events.index(("graph", 1)) + 1
+        assert events.index(("bucket", 1)) == events.index(("graph", 1)) + 1 + dw_side
     left = sum(red.buckets[b].numel() * 4 for b in range(4) if b not in issued_before_last)
     assert left == 50000 * 128 * 4 <= 26 * 2 ** 20  # the embedding only
 

@@ -369,6 +369,35 @@ def test_deterministic_mode_bit_identical(monkeypatch, B, split):
     assert _rel(res["det1"][0].view(torch.float32), res["atomic"][0].view(torch.float32)) < 1e-3
 
 
+@pytest.mark.parametrize("det", ["1", "0"])
+def test_vocab_dw_beside_decoder_loop_matches_inline(monkeypatch, det):
+    """TSAMD_VOCAB_DW_SIDE: the vocab dW graph replayed on a side stream beside the decoder backward
+    graph (GraphTrainer._Phase1) trains like the dW inside the vocab-backward graph -- bit-identical
+    in deterministic mode (same GEMM, only its timing moves), close with the atomic path (compact
+    vocab buckets: one dW graph per bucket, batches of different live-row counts)."""
+    from textsummarization_on_flink_amd.train import trainer as trm
+    B = 256
+    hps = _hps(B)
+    vocab, batches = _batches(hps, 3, seed=23)
+    monkeypatch.setenv("TSAMD_DETERMINISTIC", det)
+    res = []
+    for side in (False, True):
+        monkeypatch.setattr(trm, "VOCAB_DW_SIDE", side)
+        tr = trm.GraphTrainer(hps, vocab.size(), B=B, T=T, device="cuda:0")
+        assert tr.dw_side == side
+        for i in range(4):
+            tr.check_finite(tr.step(batches[i % len(batches)]))
+        assert bool(tr.g_dw) == side and (len(tr.g_dw) == len(tr.engine.vocab_buckets) or det == "1" or not side)
+        res.append((tr.params.flat.clone(), tr.params.accum.clone()))
+        del tr
+        torch.cuda.empty_cache()
+    if det == "1":
+        assert torch.equal(res[0][0].view(torch.int32), res[1][0].view(torch.int32))
+        assert torch.equal(res[0][1].view(torch.int32), res[1][1].view(torch.int32))
+    else:
+        assert _rel(res[1][0], res[0][0]) < 1e-4 and _rel(res[1][1], res[0][1]) < 1e-4
+
+
 def test_bptt_phase_beside_cus_held_like_rccl(monkeypatch):
     """The data-parallel co-residency guard (train/trainer.py): RCCL collective kernels hold at most
     RCCL_MAX_CHANNELS CUs (one workgroup per channel, capped in every rank's environment), and a

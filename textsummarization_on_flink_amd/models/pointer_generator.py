@@ -84,6 +84,12 @@ DE_BF16 = os.environ.get("TSAMD_DE_BF16", "1") != "0"
 # K.M.N above which the vocab dW keeps the 4-way split-K batched GEMM (config #5: 8.2 ms against
 # 9.5 ms for the library at the padded N)
 VOCAB_DW_SPLIT_MIN = 1e12
+# TSAMD_VOCAB_DW_SIDE=1 (graph trainer; default 0): the vocab weight gradient dW = X^T . dlogits
+# leaves the vocab-backward graph for a graph of its own, replayed on a side stream beside the
+# decoder backward loop (train/trainer.py _Phase1).  Measured at the headline: phase 0 -0.4 ms,
+# phase 1 +0.4 ms -- the loop's step kernels wait behind the GEMM's workgroups and share its HBM
+# stream; CU-masked and low-priority side streams were slower still (profiles/r6/vocab_dw_side.md)
+VOCAB_DW_SIDE = os.environ.get("TSAMD_VOCAB_DW_SIDE", "0") == "1"
 
 
 # TSAMD_GEMM_BT: the hand-written MFMA GEMM (csrc/kernels/gemm_mfma.hip) for the activation GEMMs
@@ -674,6 +680,8 @@ class HipPointerGenerator:
         w["DCTXb"] = z(D, B, A, dt=BF)
         self.de_bf16 = DE_BF16 and self.ctx_native and self.persistent_lstm
         self._dE = z(B, T, A, dt=BF if self.de_bf16 else F32)
+        self.split_vocab_dw = False  # see _dw_job (the graph trainer sets it with TSAMD_VOCAB_DW_SIDE)
+        self._pending_dw = None
         # attn_bwd_feat partial rows (spread the atomics), summed after; deterministic mode: one
         # row per workgroup (a single writer per slot)
         nfeat = ((T + 15) // 16) * B
@@ -1139,6 +1147,7 @@ class HipPointerGenerator:
 
     def backward(self):
         self.backward_head()
+        self.backward_head_dw()
         self.backward_mid()
         self.backward_tail()
 
@@ -1169,7 +1178,7 @@ class HipPointerGenerator:
         if self.compact_vocab:
             return self._backward_head_compact(g, dl, H, V, N)
         if self.Vp != V:  # padded dlogits rows (fused head, m == H)
-            self._vocab_dw(dst, w["outb_ext"][:, :H], dl)
+            self._dw_job(lambda: self._vocab_dw(dst, w["outb_ext"][:, :H], dl))
             self._dout = self._vocab_dx(dl)
             return
 
@@ -1211,7 +1220,7 @@ class HipPointerGenerator:
         g(OV).copy_(w["dbias"])
         dst = g(OW)
         if self.Vp != V:
-            self._vocab_dw(dst, xc[:, :H], dlc)
+            self._dw_job(lambda: self._vocab_dw(dst, xc[:, :H], dlc))
             dxc = self._vocab_dx(dlc)
         else:
             dxc = self._vocab_grads_unpadded(dst, xc, dlc, H, V, M)
@@ -1229,6 +1238,20 @@ class HipPointerGenerator:
         else:
             gemm(dst, xc[:, :H].t(), dlc)
         return mmf(dlc, self.pk["ow"].t())  # [M, H]
+
+    def _dw_job(self, f):
+        """Run the vocab dW now, or -- split_vocab_dw, set by the graph trainer -- keep it for
+        backward_head_dw (its own graph, replayed beside the decoder backward loop)."""
+        if self.split_vocab_dw:
+            self._pending_dw = f
+        else:
+            f()
+
+    def backward_head_dw(self):
+        """The vocab dW left pending by the last backward_head (split_vocab_dw); else nothing."""
+        f, self._pending_dw = self._pending_dw, None
+        if f is not None:
+            f()
 
     def _vocab_dw(self, dst, x, dl):
         """dst[H][V] = x^T . dl[:, :V] (output-projection weight gradient, model.py:290-297 over

@@ -32,7 +32,7 @@ from typing import Callable, Dict, Optional
 import torch
 
 from ..models.params import FlatParams, build_params
-from ..models.pointer_generator import HipPointerGenerator, LstmHandoffError  # noqa: F401
+from ..models.pointer_generator import VOCAB_DW_SIDE, HipPointerGenerator, LstmHandoffError  # noqa: F401
 from ..parallel.dist import DistInfo, GradAllReducer, broadcast_params, rccl_cu_reserve
 from ..utils.graphs import capture_guard
 
@@ -59,11 +59,13 @@ def check_lstm_err(engine) -> None:
 BPTT_PHASE = 2
 
 
-def issue_plan(defer_wgrad: bool):
+def issue_plan(defer_wgrad: bool, dw_side: bool = False):
     """Buckets whose all-reduce is issued after each phase graph (the last bucket, the embedding,
     is issued by the reducer call after the last graph).  With the decoder weight gradients
-    deferred beside the encoder BPTT, bucket 1 completes with phase 2."""
-    return [[0], [] if defer_wgrad else [1], [1, 2] if defer_wgrad else [2], []]
+    deferred beside the encoder BPTT, bucket 1 completes with phase 2.  With the vocab dW beside
+    the decoder backward loop (dw_side), phase 1 issues bucket 0 itself, from the side stream
+    (GraphTrainer._Phase1)."""
+    return [[] if dw_side else [0], [] if defer_wgrad else [1], [1, 2] if defer_wgrad else [2], []]
 
 
 def replay_phases(graphs, reducer, plan, bptt_phase: int, lstm_exclusive: bool, ev=None):
@@ -121,6 +123,11 @@ class GraphTrainer:
         self.poison_next = False  # fault injection: NaN gradient on the next step (exercises the NaN guard)
         self.timing = False       # per-phase HIP-event timing (phase_ms)
         self._ev = None
+        # the vocab dW on a side stream beside the decoder backward loop (VOCAB_DW_SIDE): graph mode,
+        # padded fused vocab head only (the other heads compute dW and dX in one call)
+        self.dw_side = bool(use_graph and VOCAB_DW_SIDE and eng.fused_vocab and eng.Vp != eng.V)
+        eng.split_vocab_dw = self.dw_side
+        self.g_dw = {}
 
     # ------------------------------------------------------------------ capture
     def _fb(self):
@@ -132,6 +139,7 @@ class GraphTrainer:
     def _fwd_head(self):
         out = self.engine.forward(need_grad=True)
         self.engine.backward_head()
+        self.engine.backward_head_dw()
         return out
 
     class _Phase0:
@@ -144,6 +152,29 @@ class GraphTrainer:
         def replay(self):
             self.t.g_fwd.replay()
             self.t.g_head[self.t.engine.nbk].replay()
+
+    class _Phase1:
+        """Phase graph 1 = the decoder backward graph; with dw_side, the batch bucket's vocab-dW graph
+        replayed on a side stream beside it (forked after phase 0, joined at the end), and bucket 0's
+        all-reduce issued from that stream as soon as the dW is queued (it overlaps the decoder loop
+        as before)."""
+
+        def __init__(self, trainer):
+            self.t = weakref.proxy(trainer)
+
+        def replay(self):
+            t = self.t
+            if not t.g_dw:
+                t.g_mid.replay()
+                return
+            cur = torch.cuda.current_stream()
+            side = t._dw_stream
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                t.g_dw[t.engine.nbk].replay()
+                t.reducer.bucket_ready(0)
+            t.g_mid.replay()
+            cur.wait_stream(side)
 
     def _opt(self):
         self.engine.optimizer_step()
@@ -163,6 +194,7 @@ class GraphTrainer:
             for b in buckets:  # every head variant once before its capture
                 eng.nbk = b
                 eng.backward_head()
+                eng.backward_head_dw()
             eng.nbk = nbk
         torch.cuda.current_stream().wait_stream(s)
         # undo the warm-up updates so capture does not change the model
@@ -174,19 +206,30 @@ class GraphTrainer:
             pool = torch.cuda.graph_pool_handle()
             # four graphs (forward + vocab backward | decoder backward | encoder backward |
             # embedding gradient) so each gradient bucket's all-reduce overlaps the next phase
-            self.g_fb = [self._Phase0(self)] + [torch.cuda.CUDAGraph() for _ in range(3)]
+            self.g_fb = [self._Phase0(self), self._Phase1(self)] + [torch.cuda.CUDAGraph() for _ in range(2)]
             self.g_fwd = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_fwd, pool=pool):
                 self.out = self.engine.forward(need_grad=True)
             nbk = eng.nbk
             self.g_head = {}
+            self.g_dw = {}
+            # the dW graphs replay beside g_mid: a pool of their own, so none of their private
+            # allocations can alias one of g_mid's
+            dw_pool = torch.cuda.graph_pool_handle() if self.dw_side else None
             for b in buckets:
                 eng.nbk = b
                 self.g_head[b] = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.g_head[b], pool=pool):
                     eng.backward_head()
+                if self.dw_side:
+                    self.g_dw[b] = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self.g_dw[b], pool=dw_pool):
+                        eng.backward_head_dw()
             eng.nbk = nbk
-            with torch.cuda.graph(self.g_fb[1], pool=pool):
+            if self.dw_side:
+                self._dw_stream = torch.cuda.Stream(self.device)
+            self.g_mid = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_mid, pool=pool):
                 self.engine.backward_mid()
             with torch.cuda.graph(self.g_fb[2], pool=pool):
                 eng.backward_tail_enc()
@@ -207,7 +250,7 @@ class GraphTrainer:
             if ev:
                 ev[0].record()
             ng = len(self.g_fb)
-            replay_phases(self.g_fb, self.reducer, issue_plan(self.engine.defer_wgrad), BPTT_PHASE,
+            replay_phases(self.g_fb, self.reducer, issue_plan(self.engine.defer_wgrad, bool(self.g_dw)), BPTT_PHASE,
                           self.lstm_exclusive, ev)
             self._maybe_poison()
             self.reducer()
