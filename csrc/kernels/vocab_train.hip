@@ -120,7 +120,12 @@ __global__ __launch_bounds__(256, 2) void vocab_train_kernel(
     int compact) {                    // pass 2: live block j's dlogits go to rows 32 j .. (compacted)
   constexpr int KS = H / 32;          // k-steps of 32
   constexpr int NI = vr_ni(H), VR_COLS = vr_cols(H);
-  constexpr int XS = H + 8;           // padded LDS row (bank spread)
+  // LDS X row stride = 2 16-byte slots past a multiple of 256 bytes: the 16-lane groups of a
+  // ds_read_b128 fragment read (lanes {0-3,12-15,20-27}, ...: rows 16 j + (lane & 15), chunk
+  // 4 h + (lane >> 4)) put their 8 rows of one chunk on the even slots and the other 8 on the odd
+  // ones -- the 64 banks once.  (An H + 8 pad, 1 slot, left every group 2-way conflicted: PMC
+  // SQ_LDS_BANK_CONFLICT 36 % of the LDS cycles, profiles/r6/vocab_train_pmc.md)
+  constexpr int XS = H + 16;
   constexpr int RJ = VR_ROWS / 16;    // 16-row MFMA tiles per unit
   constexpr int CH = VR_ROWS * H / 8 / 256;  // 16-byte X chunks per thread per unit
   static_assert(CH >= 1 && VR_ROWS * H / 8 % 256 == 0, "X staging");
