@@ -16,7 +16,8 @@ import torch
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DEBUG = os.environ.get("TSAMD_KERNEL_DEBUG", "0") == "1"
-_LIB = os.path.join(_PKG, "_C_debug.so" if DEBUG else "_C.so")
+# TSAMD_C_LIB: another in-tree build of the library (same-box A/B of a kernel change)
+_LIB = os.path.join(_PKG, os.environ.get("TSAMD_C_LIB") or ("_C_debug.so" if DEBUG else "_C.so"))
 # check ids of csrc/kernels/dcheck.h
 DEBUG_CHECKS = {1: "to_step_frame row id", 2: "step-frame reversal index", 3: "embedding-gradient token id",
                 4: "attention encoder length", 5: "pointer-loss / copy-mass encoder length",
